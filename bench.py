@@ -1,0 +1,201 @@
+#!/usr/bin/env python3
+"""Benchmark: ranked samples/sec (fwd+bwd) of the OneTrans training step at B=4096 seq=128
+(BASELINE.json configs[1] = "C2": 4 layers, d=128, H=4, f=512, 12 NS + 128 S tokens, Criteo-shape
+inputs with replicated embedding tables), one process per GPU (weak scaling: 4096 samples per GPU).
+
+A step = forward + backward + optimizer (clip + RMSprop dense, Adagrad sparse) + the DP gradient
+exchange when N > 1.  Inputs are synthetic Criteo-shape batches generated on the host and made
+resident in HBM before the timed region (a ring of distinct batches is cycled).
+
+Launch: python bench.py --gpus 1 --steps 20 --warmup 5
+        python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Prints ONE JSON line (rank 0) with the roofline of the dominant kernel (the mixed-parameterisation
+GEMM family, fp32 MFMA) measured with HIP events around its launches inside the timed region, and
+the CPU baseline (oracle/ restatement, torch CPU fp32) timed on this node's host cores.
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--config', default='C2')
+    ap.add_argument('--batch', type=int, default=0, help='per-GPU batch (default: the config\'s)')
+    ap.add_argument('--nbatches', type=int, default=4, help='distinct resident batches cycled')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-seconds', type=float, default=15.0)
+    ap.add_argument('--no-probe', action='store_true', help='skip per-kernel HIP-event timing')
+    return ap.parse_args()
+
+
+def init_dist(args):
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def device_batches(cfg, B, n, rank, dev):
+    from recommend_amd.data import make_batch
+    from recommend_amd.trainer import stack_labels
+    out = []
+    for i in range(n):
+        ns, seq, lab = make_batch(B, cfg, seed=100000 * (rank + 1) + i)
+        out.append(({k: torch.from_numpy(v).to(dev) for k, v in ns.items()},
+                    {k: torch.from_numpy(v).to(dev) for k, v in seq.items()},
+                    stack_labels(lab, cfg.tasks, dev)))
+    return out
+
+
+def cpu_baseline(cfg_name, seconds):
+    """Oracle (torch CPU fp32, vectorized restatement) fwd+bwd+optimizer steps on the host cores."""
+    from recommend_amd.config import workload_config
+    from recommend_amd.data import make_batch
+    from recommend_amd.params import init_params, keras_variables
+    from oracle import onetrans_ref as R
+    cores = len(os.sched_getaffinity(0))
+    cores = min(cores, 64)
+    torch.set_num_threads(cores)
+    cfg = workload_config(cfg_name)
+    # the oracle's table gradient is dense: cap table cardinalities (transformer work is unchanged)
+    cfg.sparse_features = {k: min(v, 20000) for k, v in cfg.sparse_features.items()}
+    cfg.seq_item_vocab = min(cfg.seq_item_vocab, 50000)
+    B = 64
+    P = init_params(cfg, cfg.ns_input_width(), seed=0)
+    Pt = R.to_torch(P, dtype=torch.float32)
+    st = R.init_state(Pt, cfg)
+    kv = keras_variables(cfg, {k: v.shape for k, v in P.items() if not k.startswith('emb.')})
+    batches = [make_batch(B, cfg, seed=7000 + i) for i in range(2)]
+    tb = [tuple(R.to_torch(x, dtype=torch.float32) for x in b) for b in batches]
+    Pt, st, _, _ = R.train_step(Pt, st, cfg, kv, *tb[0], seed=1)          # warm-up
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        Pt, st, _, _ = R.train_step(Pt, st, cfg, kv, *tb[n % 2], seed=2 + n)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or n >= 200:
+            break
+    return {'value': round(B * n / el, 2), 'unit': 'samples/s', 'cores': torch.get_num_threads(),
+            'kind': 'port',
+            'sample': f'{n} train steps x B={B} of {cfg_name} (full model shape, fp32, vectorized oracle '
+                      f'restatement of model.py/train.py; tables capped at 2e4/5e4 rows), {el:.1f}s'}
+
+
+def main():
+    args = parse()
+    world, rank, local = init_dist(args)
+    from recommend_amd import kernels as K
+    from recommend_amd.config import algorithmic_flops_per_sample, workload_config
+    from recommend_amd.model import OneTransModel, keras_bce_loss
+    from recommend_amd.trainer import OneTransOptimizer, OneTransTrainer
+
+    dev = torch.device('cuda', local if world > 1 else 0)
+    cfg = workload_config(args.config)
+    B = args.batch or cfg._batch
+    model = OneTransModel(cfg, device=dev, seed=0)
+    trainer = OneTransTrainer(cfg, model=model)
+    batches = device_batches(cfg, B, args.nbatches, rank, dev)
+    torch.cuda.synchronize()
+
+    def step(i):
+        ns, seq, y = batches[i % len(batches)]
+        return trainer.train_step((ns, seq, y))
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+
+    probe = None if args.no_probe else K.Probe()
+    K.set_probe(probe)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for i in range(args.steps):
+        out = step(args.warmup + i)
+    ev1.record()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    barrier(world)
+    torch.cuda.synchronize()
+    K.set_probe(None)
+    gpu_s = ev0.elapsed_time(ev1) / 1e3
+    t = max(wall, gpu_s)
+    if world > 1:
+        import torch.distributed as dist
+        tt = torch.tensor([t], device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt.item())
+    loss = float(out['total_loss'].item())
+
+    if rank != 0:
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
+
+    seq_lens = cfg._seq_lens
+    fl = algorithmic_flops_per_sample(cfg, seq_lens, cfg.ns_input_width())
+    samples = B * args.steps * world
+    value = samples / t
+    res = {
+        'metric': 'ranked samples/sec (fwd+bwd) at B=4096 seq=128; AUC parity vs ref',
+        'value': round(value, 1), 'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': round(1e3 * t / args.steps, 3), 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
+        'config': {'workload': f'{args.config}: OneTrans 4L d{cfg.hidden_dim} H{cfg.num_heads} f{cfg.ffn_dim} '
+                               f'L_NS{cfg.num_ns_tokens} L_S{sum(seq_lens) + 2} (seq 3x{seq_lens[0]}), '
+                               f'Criteo-shape 13 dense + 26 ids, replicated tables, fwd+bwd+optimizer',
+                   'global_batch': B * world, 'per_gpu_batch': B, 'seq_len': sum(seq_lens) + 2,
+                   'parallelism': f'dp{world}'},
+        'model_tflops': round(fl['fwd_bwd'] * value / 1e12, 2),
+        'final_loss': round(loss, 5),
+    }
+    if probe is not None:
+        rep = probe.report(args.steps)
+        dom = rep['families']['mixed_gemm']
+        res['roofline'] = {'bound': 'mfma', 'kernel': 'mixed_gemm_kernel + wgrad_kernel (fp32 MFMA)',
+                           'achieved': round(dom['tflops'], 2), 'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+                           'frac': round(dom['tflops'] / FP32_MFMA_PEAK_TFLOPS, 4), 'traffic': None,
+                           'avg_launch_us': round(dom['avg_us'], 2), 'launches_per_step': dom['launches_per_step'],
+                           'gflop_per_launch': round(dom['gflop_per_launch'], 3)}
+        res['kernel_time_ms_per_step'] = {k: round(v['ms_per_step'], 3) for k, v in rep['families'].items()}
+    if not args.no_cpu_baseline:
+        res['cpu_baseline'] = cpu_baseline(args.config, args.cpu_seconds)
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == '__main__':
+    main()

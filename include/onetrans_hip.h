@@ -1,0 +1,183 @@
+/* onetrans_hip.h — C ABI of libonetrans_hip.so, the gfx950 (MI355X) kernels of the OneTrans
+ * ranking training step (fwd + bwd + optimizer).
+ *
+ * The reference (ScottHCL/recommend, rank/scaling_up/oneTrans/practice) is TensorFlow/Keras with
+ * no native code; every entry point below replaces a TF op call site of that model (cited per
+ * function as file:line relative to rank/scaling_up/oneTrans/practice/).  The host-side mirror
+ * of the reference interface (recommend_amd.OneTransModel / OneTransTrainer) binds this library
+ * with ctypes.
+ *
+ * Conventions
+ *  - All tensors are caller-allocated device memory (fp32 activations/weights, int32 row maps,
+ *    int64 ids).  The library never allocates, never synchronises the device and keeps no global
+ *    mutable state: every call is stream-ordered on `stream` (a hipStream_t passed as void*),
+ *    so calls are graph-capturable and thread-safe on distinct streams.
+ *  - Scratch memory is passed as (workspace, ws_bytes); size it with the matching
+ *    *_workspace_size() function.
+ *  - Return 0 (OT_OK) on success, else an OT_ERR_* code; ot_get_last_error_string() describes
+ *    the last failure of the calling host thread.
+ *  - Row-major 2-D operands are (pointer, leading dimension in elements).  Row maps (int32)
+ *    list, per tile row, the source / destination row; -1 marks padding.
+ *  - Dropout masks are counter-based: element (token t, column n) of site s is kept iff
+ *    fmix32((t*width + n) * 0x9E3779B1 + seed ^ s * 0x85EBCA77) >= rate * 2^32, kept values are
+ *    scaled by 1/(1-rate).  A compacted tail row r (the last K of I tokens per sample) maps to
+ *    token t = (r / K) * I + (I - K) + r % K.
+ */
+#ifndef ONETRANS_HIP_H
+#define ONETRANS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OT_OK 0
+#define OT_ERR_INVALID_ARG 1
+#define OT_ERR_UNSUPPORTED 2
+#define OT_ERR_HIP 3
+
+/* GEMM modes */
+#define OT_GEMM_NN 0 /* C = A @ W[g],   W[g] stored [K][N] (Keras Dense kernel layout) */
+#define OT_GEMM_NT 1 /* C = A @ W[g]^T, W[g] stored [N][K] (dgrad through a Keras kernel) */
+
+/* A-load prologues */
+#define OT_AX_NONE 0
+#define OT_AX_RMSNORM 1 /* a * rstd[in_row] * gamma[k]  (RMSNorm fused into the consumer GEMM) */
+#define OT_AX_GELU 2    /* gelu_erf(a)                   (FFN hidden recomputed from its pre-activation) */
+
+/* GEMM epilogue flags (applied in this order) */
+#define OT_EPI_BIAS 1        /* + bias[g][n] */
+#define OT_EPI_GELU_BWD 2    /* * gelu'(aux[out_row][n]) */
+#define OT_EPI_GELU 4        /* gelu_erf(.) */
+#define OT_EPI_DROPOUT 8     /* counter-based mask, index (token, n) */
+#define OT_EPI_RESIDUAL 16   /* + res[res_tok ? token : out_row][n] */
+#define OT_EPI_ACCUMULATE 32 /* C += result */
+
+int ot_version(void);
+const char* ot_get_last_error_string(void);
+
+/* ---- mixed-parameterisation grouped GEMM (gemm.hip) --------------------------------------
+ * Replaces: per-token Q/K/V Dense loop model.py:84-92 (+ weights 38-54, group rule 67-74),
+ * Wo model.py:117, per-token FFN loop model.py:154-161 (weights 136-147), tokenizer Dense layers
+ * model.py:211-219/254/265, task-head Dense(d/2) model.py:325-330/391, and their gradients
+ * (tape.gradient, train.py:131).  Tiles are 128 rows (ot_gemm_tile_rows()); tile i multiplies the
+ * rows in_rows[128 i .. 128 i + 127] by W + tile_group[i] * w_gstride. */
+int ot_gemm_tile_rows(void);
+int ot_mixed_gemm(int mode, const float* A, int64_t lda, int K, const int32_t* in_rows,
+                  int a_xform, const float* a_rstd, const float* a_gamma,
+                  const float* W, int64_t w_gstride, int64_t ldw, int N,
+                  const int32_t* tile_group, int ntiles,
+                  const float* bias, int64_t bias_gstride,
+                  float* C, int64_t ldc, const int32_t* out_rows, int epi,
+                  const float* res, int64_t ldres, int res_tok,
+                  const float* aux, int64_t ldaux,
+                  uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
+                  void* stream);
+/* dW[g] (+)= sum pro(A[a_rows])^T D[d_rows], db[g] (+)= sum D[d_rows] over the rows of every
+ * chunk of group g.  chunks: [nchunks][3] {group, row_begin, row_count} indexing the row maps;
+ * gchunk: [ngroups][2] {first chunk, chunk count} (a group's chunks are contiguous).
+ * Deterministic: per-chunk partial slabs summed in chunk order. */
+size_t ot_wgrad_workspace_size(int nchunks, int K, int N);
+int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a_rows, int a_xform,
+                        const float* a_rstd, const float* a_gamma,
+                        const float* D, int64_t ldd, const int32_t* d_rows, int K, int N,
+                        const int32_t* chunks, int nchunks, const int32_t* gchunk, int ngroups,
+                        float* dW, int64_t dw_gstride, float* db, int64_t db_gstride,
+                        int accumulate, void* workspace, size_t ws_bytes, void* stream);
+
+/* ---- causal attention with a query tail (attention.hip) ----------------------------------
+ * Replaces model.py:100-114 (einsum QK^T/sqrt(hd), band_part mask with -1e9, softmax, einsum PV)
+ * and the pyramid gather of queries model.py:356/371 (only the last K of I queries computed).
+ * qkv: [B*I, ld] (q | k | v, head h at +h*head_dim); out: [B*K, H*head_dim]; lse: [B, H, K]. */
+int ot_attn_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, int head_dim,
+                float* out, float* lse, void* stream);
+/* dqkv: like qkv (dq written on the K tail rows only; dk, dv on all rows); delta_ws: B*H*K floats */
+int ot_attn_bwd(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
+                int B, int H, int I, int K, int head_dim, float* dqkv, float* delta_ws, void* stream);
+
+/* ---- row-wise kernels (rowwise.hip) -------------------------------------------------------
+ * RMSNorm model.py:19-23 (forward writes rstd, and y only when asked: the output norm
+ * model.py:384); dropout model.py:184/193/198. */
+int ot_rmsnorm_fwd(const float* x, int64_t ldx, const float* gamma, float* y, int64_t ldy, float* rstd,
+                   int64_t rows, int d, float eps, void* stream);
+size_t ot_rmsnorm_bwd_workspace_size(int64_t rows, int d);
+/* dres (residual-branch gradient added to dx): when dres_tail_K > 0 it holds only the compact tail
+ * rows (last dres_tail_K of every dres_tail_I rows of x); the other rows get no residual term. */
+int ot_rmsnorm_bwd(const float* dy, int64_t lddy, const float* x, int64_t ldx, const float* gamma,
+                   const float* rstd, const float* dres, int64_t lddres, int dres_tail_K, int dres_tail_I,
+                   float* dx, int64_t lddx,
+                   float* dx_masked, int64_t lddxm, uint32_t seed, uint32_t site, float drop_rate,
+                   int tail_K, int tail_I, float* dgamma, int accumulate_dgamma, int64_t rows, int d,
+                   void* workspace, size_t ws_bytes, void* stream);
+int ot_dropout_apply(const float* src, int64_t lds, float* dst, int64_t ldd, int64_t rows, int d,
+                     uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I, void* stream);
+size_t ot_rows_colsum_workspace_size(int64_t nrows, int ncols);
+int ot_rows_colsum(const float* src, int64_t ld, const int32_t* rows, int64_t nrows, int ncols,
+                   float* out, int accumulate, void* workspace, size_t ws_bytes, void* stream);
+
+/* ---- tokenizer + heads + loss (model_io.hip) ---------------------------------------------- */
+typedef struct {
+  const float* dense;   /* [B] float feature (stride dense_stride) or NULL */
+  const int64_t* ids;   /* [B] ids (stride ids_stride) for an embedding feature, or NULL */
+  int64_t row_offset;   /* row of id 0 in the (concatenated) table */
+  int64_t stride;       /* element stride between samples of `dense` / `ids` */
+  int col;              /* first destination column */
+  int width;            /* 1 for dense, embedding width for ids */
+} ot_ns_field;
+/* NS feature concat model.py:243-253 (+ embedding gather for id features):
+ * out[b][col .. col+width) = table[row_offset + ids[b]] or dense[b]; columns >= F are untouched. */
+int ot_ns_assemble(const ot_ns_field* fields_dev, int nfields, const float* table, int B, float* out,
+                   int64_t ld_out, void* stream);
+/* Pack the NS embedding-feature gradients of ot_ns_assemble: keys[f*B + b] = row_offset+ids[b],
+ * grads[f*B + b][:] = dmat[b][col .. col+width) for the nsparse id fields (equal width). */
+int ot_ns_grad_pack(const ot_ns_field* fields_dev, int nsparse, int width, const float* dmat, int64_t ld,
+                    int B, int64_t* keys, float* grads, void* stream);
+/* [SEP] placement model.py:270-272: dst[rows[i]][:] = vec[:] */
+int ot_fill_rows(float* dst, int64_t ld, const int32_t* rows, int64_t nrows, const float* vec, int d,
+                 void* stream);
+/* Row maps of the per-sequence projection GEMM model.py:262-265: in_rows[m] = ids (item id) of
+ * sequence element m; sequences concatenated, tiles padded to ot_gemm_tile_rows(). */
+int ot_seq_rows(const int64_t* ids, int64_t ids_stride_b, int B, int L, int64_t vocab, int32_t* in_rows,
+                void* stream);
+/* Task heads model.py:388-391: logits[t][b] = gelu(pre1[t*B+b]) . w2[t] + b2[t], probs = sigmoid */
+int ot_head_fwd(const float* pre1, const float* w2, const float* b2, int T, int B, int dh,
+                float* logits, float* probs, void* stream);
+size_t ot_head_bwd_workspace_size(int T, int B, int dh);
+int ot_head_bwd(const float* pre1, const float* w2, const float* probs, const float* dprobs, int T, int B,
+                int dh, float* dpre1, float* dw2, float* db2, int64_t task_stride_w2, int64_t task_stride_b2,
+                int accumulate, void* workspace, size_t ws_bytes, void* stream);
+/* tf.keras.losses.BinaryCrossentropy(from_logits=False) summed over tasks, train.py:78-93/124-128:
+ * loss = sum_t mean_b -(y log(clip(p)+eps) + (1-y) log(1-clip(p)+eps)). */
+size_t ot_bce_workspace_size(int T, int B);
+int ot_bce_fwd(const float* probs, const float* labels, int T, int B, float* loss, void* workspace,
+               size_t ws_bytes, void* stream);
+/* dprobs = gscale[0] * d loss / d probs (zero where p was clipped) */
+int ot_bce_bwd(const float* probs, const float* labels, const float* gscale, int T, int B, float* dprobs,
+               void* stream);
+
+/* ---- sparse embedding update (embedding.hip) ----------------------------------------------
+ * Build extension (no reference site; paper: sparse Adagrad, clip 120, complete_translation.md:190).
+ * Keras-2.12 Adagrad on a de-duplicated gradient: rows sorted (rocPRIM radix sort, stable) and
+ * summed per unique key in a fixed order (deterministic), clip_by_norm(clip) over the unique-row
+ * gradient, then acc[r] += g^2; w[r] -= lr g / sqrt(acc[r] + eps). */
+size_t ot_sparse_adagrad_workspace_size(int64_t n, int E);
+int ot_sparse_adagrad(float* table, float* accum, int E, int64_t num_rows, const int64_t* keys,
+                      const float* grads, int64_t n, float lr, float eps, float clip,
+                      void* workspace, size_t ws_bytes, void* stream);
+
+/* ---- dense optimizer (optim.hip) ----------------------------------------------------------
+ * Per-variable tf.clip_by_norm (train.py:134-135) over 2-D strided segments of one flat
+ * gradient buffer, then Keras-2.12 RMSprop(momentum) (train.py:64-70, 138):
+ *   v = rho v + (1-rho) g^2; inc = lr g rsqrt(v + eps); m = mom m + inc; w -= m.
+ * segs: [nseg][4] int64 {offset, rows, cols, row_stride}. */
+size_t ot_clip_rmsprop_workspace_size(int nseg, int64_t max_seg_elems);
+int ot_clip_rmsprop(float* w, float* g, float* v, float* m, const int64_t* segs_dev, int nseg,
+                    int64_t max_seg_elems, float lr, float rho, float eps, float momentum, float clip,
+                    void* workspace, size_t ws_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ONETRANS_HIP_H */

@@ -1,0 +1,110 @@
+"""ctypes binding of ``libonetrans_hip.so`` (C ABI: ``include/onetrans_hip.h``).
+
+There is no fallback: if the library is missing, fails to load, or a call is made
+without a ROCm device, the call raises.  ``load()`` works without a GPU (it only
+dlopens the library), which the CPU test-suite uses to check the exported symbols.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import c_float, c_int, c_int64, c_size_t, c_uint32, c_void_p, c_char_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libonetrans_hip.so')
+HEADER = os.path.join(os.path.dirname(_HERE), 'include', 'onetrans_hip.h')
+
+OT_GEMM_NN, OT_GEMM_NT = 0, 1
+OT_AX_NONE, OT_AX_RMSNORM, OT_AX_GELU = 0, 1, 2
+OT_EPI_BIAS, OT_EPI_GELU_BWD, OT_EPI_GELU = 1, 2, 4
+OT_EPI_DROPOUT, OT_EPI_RESIDUAL, OT_EPI_ACCUMULATE = 8, 16, 32
+
+P = c_void_p
+I64 = c_int64
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    'ot_version': (c_int, []),
+    'ot_get_last_error_string': (c_char_p, []),
+    'ot_gemm_tile_rows': (c_int, []),
+    'ot_mixed_gemm': (c_int, [c_int, P, I64, c_int, P, c_int, P, P, P, I64, I64, c_int, P, c_int, P, I64,
+                              P, I64, P, c_int, P, I64, c_int, P, I64, c_uint32, c_uint32, c_float, c_int,
+                              c_int, P]),
+    'ot_wgrad_workspace_size': (c_size_t, [c_int, c_int, c_int]),
+    'ot_mixed_gemm_wgrad': (c_int, [P, I64, P, c_int, P, P, P, I64, P, c_int, c_int, P, c_int, P, c_int, P,
+                                    I64, P, I64, c_int, P, c_size_t, P]),
+    'ot_attn_fwd': (c_int, [P, I64, c_int, c_int, c_int, c_int, c_int, P, P, P]),
+    'ot_attn_bwd': (c_int, [P, I64, P, P, P, c_int, c_int, c_int, c_int, c_int, P, P, P]),
+    'ot_rmsnorm_fwd': (c_int, [P, I64, P, P, I64, P, I64, c_int, c_float, P]),
+    'ot_rmsnorm_bwd_workspace_size': (c_size_t, [I64, c_int]),
+    'ot_rmsnorm_bwd': (c_int, [P, I64, P, I64, P, P, P, I64, c_int, c_int, P, I64, P, I64, c_uint32,
+                               c_uint32, c_float, c_int, c_int, P, c_int, I64, c_int, P, c_size_t, P]),
+    'ot_dropout_apply': (c_int, [P, I64, P, I64, I64, c_int, c_uint32, c_uint32, c_float, c_int, c_int, P]),
+    'ot_rows_colsum_workspace_size': (c_size_t, [I64, c_int]),
+    'ot_rows_colsum': (c_int, [P, I64, P, I64, c_int, P, c_int, P, c_size_t, P]),
+    'ot_ns_assemble': (c_int, [P, c_int, P, c_int, P, I64, P]),
+    'ot_ns_grad_pack': (c_int, [P, c_int, c_int, P, I64, c_int, P, P, P]),
+    'ot_fill_rows': (c_int, [P, I64, P, I64, P, c_int, P]),
+    'ot_seq_rows': (c_int, [P, I64, c_int, c_int, I64, P, P]),
+    'ot_head_fwd': (c_int, [P, P, P, c_int, c_int, c_int, P, P, P]),
+    'ot_head_bwd_workspace_size': (c_size_t, [c_int, c_int, c_int]),
+    'ot_head_bwd': (c_int, [P, P, P, P, c_int, c_int, c_int, P, P, P, I64, I64, c_int, P, c_size_t, P]),
+    'ot_bce_workspace_size': (c_size_t, [c_int, c_int]),
+    'ot_bce_fwd': (c_int, [P, P, c_int, c_int, P, P, c_size_t, P]),
+    'ot_bce_bwd': (c_int, [P, P, P, c_int, c_int, P, P]),
+    'ot_sparse_adagrad_workspace_size': (c_size_t, [I64, c_int]),
+    'ot_sparse_adagrad': (c_int, [P, P, c_int, I64, P, P, I64, c_float, c_float, c_float, P, c_size_t, P]),
+    'ot_clip_rmsprop_workspace_size': (c_size_t, [c_int, I64]),
+    'ot_clip_rmsprop': (c_int, [P, P, P, P, P, c_int, I64, c_float, c_float, c_float, c_float, c_float, P,
+                                c_size_t, P]),
+}
+
+# ABI notes (mirrors include/onetrans_hip.h): the modes/flags above; the only struct is
+# ot_ns_field {const float* dense; const int64_t* ids; int64 row_offset; int64 stride; int col;
+# int width} = 40 bytes.
+NS_FIELD_BYTES = 40
+
+_lib = None
+
+
+class OneTransHipError(RuntimeError):
+    pass
+
+
+def load():
+    """dlopen the library and bind every C-ABI symbol (raises if missing)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise OneTransHipError(
+            f'{LIB_PATH} not found: build it with `python -c "import __graft_entry__ as g; g.build()"` '
+            '(there is no CPU fallback)')
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def call(name: str, *args) -> None:
+    """Invoke a status-returning entry point; raise OneTransHipError on a non-zero status."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.ot_get_last_error_string()
+        raise OneTransHipError(f'{name} failed ({rc}): {msg.decode() if msg else ""}')
+
+
+def size(name: str, *args) -> int:
+    return int(getattr(load(), name)(*args))
+
+
+def header_symbols() -> list:
+    """Entry points declared in include/onetrans_hip.h (for the ABI test)."""
+    import re
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r'\b(ot_[a-z0-9_]+)\s*\(', txt)))

@@ -1,0 +1,339 @@
+// Causal attention with a query tail offset on gfx950 fp32 MFMA (v_mfma_f32_32x32x2_f32).
+//
+// Replaces model.py:100-114 (einsum QK^T / sqrt(hd), band_part causal mask filled with -1e9,
+// softmax, einsum PV).  The -1e9 fill equals -inf here because the diagonal is never masked.
+// Only the last K queries of a layer with I tokens are computed (pyramid keep / last-layer DCE,
+// exact), keys/values cover all I tokens.
+//
+// Layout: qkv [B*I, ld] token-major (q at col 0, k at col d, v at col 2d, head h at +h*hd);
+// o / dO compact [B*K, d]; lse [B, H, K]; dqkv like qkv (dq only on the K tail rows).
+// One wave per (sample, head); a block of 4 waves = 4 consecutive (b, h) pairs.
+//
+// Orientation: S^T = K Q^T puts the query on the MFMA column (lane) and keys in registers, so
+// P^T (registers) is directly the B operand of O^T = V^T P^T (the accumulator-as-operand idiom,
+// cdna_hip_programming.md §3) with the k index of step r = the key held in register r.
+#include "common.h"
+
+namespace ot {
+
+struct AttnArgs {
+  const float* qkv; int64_t ld; int d;
+  const float* o; const float* dout; float* out; float* lse; float* dqkv; float* delta;
+  int B, H, I, K;
+  float scale;
+};
+
+__device__ __forceinline__ int acc_row(int r, int hh) { return (r & 3) + 8 * (r >> 2) + 4 * hh; }
+
+// Fragment of a [32 rows x HD] operand for a product over HD: lane (li, hh) holds row li,
+// dims (HD/2)*hh + s, s < HD/2 (the k permutation).  Rows >= nrows give zeros.
+template <int HD>
+__device__ __forceinline__ void load_frag(float (&f)[HD / 2], const float* base, int64_t ld, int row,
+                                          int nrows, int hh) {
+  if (row < nrows) {
+    const float* p = base + (int64_t)row * ld + (HD / 2) * hh;
+    if constexpr (HD >= 8) {
+#pragma unroll
+      for (int q = 0; q < HD / 8; ++q) {
+        f32x4 v = *reinterpret_cast<const f32x4*>(p + 4 * q);
+        f[4 * q] = v.x; f[4 * q + 1] = v.y; f[4 * q + 2] = v.z; f[4 * q + 3] = v.w;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < HD / 2; ++s) f[s] = 0.f;
+  }
+}
+
+template <int HD>
+__device__ __forceinline__ f32x16 mm_frag(const float (&a)[HD / 2], const float (&b)[HD / 2]) {
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+  for (int s = 0; s < HD / 2; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
+  return acc;
+}
+
+constexpr int NB(int hd) { return (hd + 31) / 32; }
+
+// O^T[d][col] += sum_r X[row(r)][d0 + li] * P[r]   (X rows are the k index of register r)
+template <int HD>
+__device__ __forceinline__ void acc_xT_p(f32x16 (&acc)[NB(HD)], const float* xbase, int64_t ld, int row0,
+                                         int nrows, const f32x16& p, int li, int hh) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = row0 + acc_row(r, hh);
+#pragma unroll
+    for (int c = 0; c < NB(HD); ++c) {
+      const int dd = 32 * c + li;
+      float a = 0.f;
+      if (row < nrows && dd < HD) a = xbase[(int64_t)row * ld + dd];
+      acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, p[r], acc[c], 0, 0, 0);
+    }
+  }
+}
+
+template <int HD>
+__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs p) {
+  const int lane = threadIdx.x & 63, li = lane & 31, hh = lane >> 5;
+  const int pair = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (pair >= p.B * p.H) return;
+  const int b = pair / p.H, h = pair % p.H;
+  const int I = p.I, K = p.K, q_off = I - K;
+  const float* Q = p.qkv + (int64_t)b * I * p.ld + h * HD;
+  const float* Kp = Q + p.d;
+  const float* V = Q + 2 * p.d;
+  const float* Qt = Q + (int64_t)q_off * p.ld;      // tail rows
+  const int nqb = (K + 31) / 32;
+  for (int qb = 0; qb < nqb; ++qb) {
+    const int j = 32 * qb + li;                     // this lane's query (tail index)
+    const int qpos = q_off + (j < K ? j : K - 1);
+    float qf[HD / 2];
+    load_frag<HD>(qf, Qt, p.ld, j, K, hh);
+    f32x16 oacc[NB(HD)];
+#pragma unroll
+    for (int c = 0; c < NB(HD); ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) oacc[c][r] = 0.f;
+    float m = -INFINITY, l = 0.f;
+    const int last_q = q_off + min(32 * qb + 31, K - 1);
+    const int nkb = last_q / 32 + 1;
+    for (int kb = 0; kb < nkb; ++kb) {
+      const int key0 = 32 * kb;
+      float kf[HD / 2];
+      load_frag<HD>(kf, Kp, p.ld, key0 + li, I, hh);
+      f32x16 s = mm_frag<HD>(kf, qf);               // S^T: row = key, col = query
+      float mloc = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int kpos = key0 + acc_row(r, hh);
+        float v = s[r] * p.scale;
+        v = (kpos <= qpos) ? v : -INFINITY;         // kpos <= qpos < I
+        s[r] = v;
+        mloc = fmaxf(mloc, v);
+      }
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+      const float mnew = fmaxf(m, mloc);            // finite: key 0 is always visible
+      const float corr = __expf(m - mnew);
+      float lsum = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float e = __expf(s[r] - mnew);
+        s[r] = e;
+        lsum += e;
+      }
+      lsum += __shfl_xor(lsum, 32, 64);
+      l = l * corr + lsum;
+      m = mnew;
+#pragma unroll
+      for (int c = 0; c < NB(HD); ++c) oacc[c] *= corr;
+      acc_xT_p<HD>(oacc, V, p.ld, key0, I, s, li, hh);
+    }
+    if (j < K) {
+      const float inv = 1.f / l;
+      float* orow = p.out + ((int64_t)b * K + j) * p.d + h * HD;
+#pragma unroll
+      for (int c = 0; c < NB(HD); ++c)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int dd = 32 * c + 8 * g + 4 * hh;
+          if (dd < HD) {
+            f32x4 v = {oacc[c][4 * g] * inv, oacc[c][4 * g + 1] * inv, oacc[c][4 * g + 2] * inv,
+                       oacc[c][4 * g + 3] * inv};
+            *reinterpret_cast<f32x4*>(orow + dd) = v;
+          }
+        }
+      if (hh == 0) p.lse[((int64_t)b * p.H + h) * K + j] = m + __logf(l);
+    }
+  }
+}
+
+// delta[b,h,j] = sum_d dO[b*K+j][h*hd+d] * O[b*K+j][h*hd+d]   (one thread per (row, head))
+__global__ void attn_bwd_prep_kernel(const float* __restrict__ o, const float* __restrict__ dout, float* delta,
+                                     int B, int H, int K, int hd) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // (b*K + j)*H + h
+  if (i >= (int64_t)B * K * H) return;
+  const int h = (int)(i % H);
+  const int64_t row = i / H;
+  const int64_t b = row / K, j = row % K;
+  const float* a = o + row * H * hd + h * hd;
+  const float* c = dout + row * H * hd + h * hd;
+  float s = 0.f;
+  for (int q = 0; q < hd; q += 4) {
+    f32x4 x = *reinterpret_cast<const f32x4*>(a + q);
+    f32x4 y = *reinterpret_cast<const f32x4*>(c + q);
+    s += x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
+  }
+  delta[(b * H + h) * K + j] = s;
+}
+
+// ------------------------------------------------------------------------------------------
+// Backward.  Pass A (per key block): S, dP with the key on the lane -> dV^T, dK^T.
+//            Pass B (per query block): S^T, dP^T with the query on the lane -> dQ^T.
+// Both are plain two-pass recomputation (no atomics, no cross-wave traffic): deterministic.
+template <int HD>
+__global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs p) {
+  const int lane = threadIdx.x & 63, li = lane & 31, hh = lane >> 5;
+  const int pair = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (pair >= p.B * p.H) return;
+  const int b = pair / p.H, h = pair % p.H;
+  const int I = p.I, K = p.K, q_off = I - K;
+  const int64_t tok0 = (int64_t)b * I;
+  const float* Q = p.qkv + tok0 * p.ld + h * HD;
+  const float* Kp = Q + p.d;
+  const float* V = Q + 2 * p.d;
+  const float* Qt = Q + (int64_t)q_off * p.ld;
+  const float* O = p.o + (int64_t)b * K * p.d + h * HD;
+  const float* dO = p.dout + (int64_t)b * K * p.d + h * HD;
+  const float* lse = p.lse + ((int64_t)b * p.H + h) * K;
+  float* dQt = p.dqkv + (tok0 + q_off) * p.ld + h * HD;
+  float* dK = p.dqkv + tok0 * p.ld + p.d + h * HD;
+  float* dV = dK + p.d;
+  const int nqb = (K + 31) / 32;
+
+  const float* delta = p.delta + ((int64_t)b * p.H + h) * K;   // rowsum(dO * O), attn_bwd_prep_kernel
+
+  // ---------------- pass A: dK, dV for every key block
+  const int nkb = (I + 31) / 32;
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int key0 = 32 * kb;
+    const int kpos = key0 + li;                        // this lane's key
+    float kf[HD / 2], vf[HD / 2];
+    load_frag<HD>(kf, Kp, p.ld, kpos, I, hh);
+    load_frag<HD>(vf, V, p.ld, kpos, I, hh);
+    f32x16 dk[NB(HD)], dv[NB(HD)];
+#pragma unroll
+    for (int c = 0; c < NB(HD); ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { dk[c][r] = 0.f; dv[c][r] = 0.f; }
+    // first query block whose last query can see key0
+    int qb0 = key0 - q_off; qb0 = qb0 < 0 ? 0 : qb0 / 32;
+    for (int qb = qb0; qb < nqb; ++qb) {
+      const int q0 = 32 * qb;
+      float qf[HD / 2], of[HD / 2];
+      load_frag<HD>(qf, Qt, p.ld, q0 + li, K, hh);
+      load_frag<HD>(of, dO, p.d, q0 + li, K, hh);
+      f32x16 s = mm_frag<HD>(qf, kf);                  // S: row = query, col = key
+      f32x16 dp = mm_frag<HD>(of, vf);                 // dP: row = query, col = key
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int j = q0 + acc_row(r, hh);
+        const bool ok = j < K && kpos <= q_off + j;
+        const float lj = j < K ? lse[j] : 0.f;
+        const float P = ok ? __expf(s[r] * p.scale - lj) : 0.f;
+        s[r] = P;
+        dp[r] = ok ? P * (dp[r] - delta[j]) : 0.f;
+      }
+      acc_xT_p<HD>(dv, dO, p.d, q0, K, s, li, hh);    // dV^T += dO^T P
+      acc_xT_p<HD>(dk, Qt, p.ld, q0, K, dp, li, hh);  // dK^T += Q^T dS
+    }
+    if (kpos < I) {
+#pragma unroll
+      for (int c = 0; c < NB(HD); ++c)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int dd = 32 * c + 8 * g + 4 * hh;
+          if (dd < HD) {
+            f32x4 a = {dk[c][4 * g] * p.scale, dk[c][4 * g + 1] * p.scale, dk[c][4 * g + 2] * p.scale,
+                       dk[c][4 * g + 3] * p.scale};
+            f32x4 v = {dv[c][4 * g], dv[c][4 * g + 1], dv[c][4 * g + 2], dv[c][4 * g + 3]};
+            *reinterpret_cast<f32x4*>(dK + (int64_t)kpos * p.ld + dd) = a;
+            *reinterpret_cast<f32x4*>(dV + (int64_t)kpos * p.ld + dd) = v;
+          }
+        }
+    }
+  }
+
+  // ---------------- pass B: dQ for every tail query block
+  for (int qb = 0; qb < nqb; ++qb) {
+    const int j = 32 * qb + li;
+    const int qpos = q_off + (j < K ? j : K - 1);
+    float qf[HD / 2], of[HD / 2];
+    load_frag<HD>(qf, Qt, p.ld, j, K, hh);
+    load_frag<HD>(of, dO, p.d, j, K, hh);
+    const float lj = j < K ? lse[j] : 0.f;
+    const float dj = j < K ? delta[j] : 0.f;
+    f32x16 dq[NB(HD)];
+#pragma unroll
+    for (int c = 0; c < NB(HD); ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dq[c][r] = 0.f;
+    const int last_q = q_off + min(32 * qb + 31, K - 1);
+    const int nkb2 = last_q / 32 + 1;
+    for (int kb = 0; kb < nkb2; ++kb) {
+      const int key0 = 32 * kb;
+      float kf[HD / 2], vf[HD / 2];
+      load_frag<HD>(kf, Kp, p.ld, key0 + li, I, hh);
+      load_frag<HD>(vf, V, p.ld, key0 + li, I, hh);
+      f32x16 s = mm_frag<HD>(kf, qf);                  // S^T: row = key, col = query
+      f32x16 dp = mm_frag<HD>(vf, of);                 // dP^T
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int kpos = key0 + acc_row(r, hh);
+        const bool ok = j < K && kpos <= qpos;
+        const float P = ok ? __expf(s[r] * p.scale - lj) : 0.f;
+        dp[r] = ok ? P * (dp[r] - dj) : 0.f;
+      }
+      acc_xT_p<HD>(dq, Kp, p.ld, key0, I, dp, li, hh); // dQ^T += K^T dS^T
+    }
+    if (j < K) {
+#pragma unroll
+      for (int c = 0; c < NB(HD); ++c)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int dd = 32 * c + 8 * g + 4 * hh;
+          if (dd < HD) {
+            f32x4 a = {dq[c][4 * g] * p.scale, dq[c][4 * g + 1] * p.scale, dq[c][4 * g + 2] * p.scale,
+                       dq[c][4 * g + 3] * p.scale};
+            *reinterpret_cast<f32x4*>(dQt + (int64_t)j * p.ld + dd) = a;
+          }
+        }
+    }
+  }
+}
+
+}  // namespace ot
+
+using namespace ot;
+
+#define OT_ATTN_DISPATCH(KERNEL, HD_, ...)                                                   \
+  switch (HD_) {                                                                             \
+    case 16: hipLaunchKernelGGL(KERNEL<16>, __VA_ARGS__); break;                             \
+    case 32: hipLaunchKernelGGL(KERNEL<32>, __VA_ARGS__); break;                             \
+    case 64: hipLaunchKernelGGL(KERNEL<64>, __VA_ARGS__); break;                             \
+    case 128: hipLaunchKernelGGL(KERNEL<128>, __VA_ARGS__); break;                           \
+    default: return fail(OT_ERR_UNSUPPORTED, "attention: head_dim %d unsupported", HD_);     \
+  }
+
+extern "C" int ot_attn_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, int head_dim,
+                           float* out, float* lse, void* stream) {
+  OT_REQUIRE(qkv && out && lse, "ot_attn_fwd: null operand");
+  OT_REQUIRE(B >= 0 && H > 0 && I > 0 && K > 0 && K <= I, "ot_attn_fwd: bad sizes B=%d H=%d I=%d K=%d", B, H, I, K);
+  OT_REQUIRE(ld % 4 == 0 && ld >= 3 * H * head_dim, "ot_attn_fwd: ld must be >= 3d and a multiple of 4");
+  if (B == 0) return OT_OK;
+  AttnArgs p{qkv, ld, H * head_dim, nullptr, nullptr, out, lse, nullptr, nullptr, B, H, I, K,
+             1.f / sqrtf((float)head_dim)};
+  const unsigned grid = ceil_div((int64_t)B * H, 4);
+  OT_ATTN_DISPATCH(attn_fwd_kernel, head_dim, dim3(grid), dim3(256), 0, (hipStream_t)stream, p);
+  OT_LAUNCH_CHECK("ot_attn_fwd");
+  return OT_OK;
+}
+
+extern "C" int ot_attn_bwd(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
+                           int B, int H, int I, int K, int head_dim, float* dqkv, float* delta_ws,
+                           void* stream) {
+  OT_REQUIRE(qkv && out && dout && lse && dqkv && delta_ws, "ot_attn_bwd: null operand");
+  OT_REQUIRE(B >= 0 && H > 0 && I > 0 && K > 0 && K <= I, "ot_attn_bwd: bad sizes");
+  OT_REQUIRE(ld % 4 == 0 && ld >= 3 * H * head_dim, "ot_attn_bwd: bad ld");
+  if (B == 0) return OT_OK;
+  AttnArgs p{qkv, ld, H * head_dim, out, dout, nullptr, const_cast<float*>(lse), dqkv, delta_ws, B, H, I, K,
+             1.f / sqrtf((float)head_dim)};
+  hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3(ceil_div((int64_t)B * K * H, 256)), dim3(256), 0,
+                     (hipStream_t)stream, out, dout, delta_ws, B, H, K, head_dim);
+  OT_LAUNCH_CHECK("ot_attn_bwd(prep)");
+  const unsigned grid = ceil_div((int64_t)B * H, 4);
+  OT_ATTN_DISPATCH(attn_bwd_kernel, head_dim, dim3(grid), dim3(256), 0, (hipStream_t)stream, p);
+  OT_LAUNCH_CHECK("ot_attn_bwd");
+  return OT_OK;
+}

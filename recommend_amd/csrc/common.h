@@ -1,0 +1,80 @@
+// Shared helpers for the OneTrans gfx950 kernels (C-ABI in include/onetrans_hip.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+
+#include "../../include/onetrans_hip.h"
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+namespace ot {
+
+// ---- error reporting (per host thread) ---------------------------------------------
+void set_error(const char* fmt, ...);
+int fail(int code, const char* fmt, ...);
+
+#define OT_REQUIRE(cond, ...)                                   \
+  do {                                                          \
+    if (!(cond)) return ::ot::fail(OT_ERR_INVALID_ARG, __VA_ARGS__); \
+  } while (0)
+
+#define OT_LAUNCH_CHECK(name)                                                        \
+  do {                                                                              \
+    hipError_t _e = hipGetLastError();                                              \
+    if (_e != hipSuccess)                                                           \
+      return ::ot::fail(OT_ERR_HIP, "%s: %s", name, hipGetErrorString(_e));         \
+  } while (0)
+
+// ---- dropout: counter-based mask (oracle/keras_math.py::dropout_keep) ---------------
+__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+  return h;
+}
+// keep iff hash >= thr (thr = round(rate * 2^32)); index = (b*I + p)*d + n
+__device__ __forceinline__ bool drop_keep(uint32_t seed, uint32_t site, uint32_t index, uint32_t thr) {
+  uint32_t h = index * 0x9E3779B1u + seed;
+  h ^= site * 0x85EBCA77u;
+  return fmix32(h) >= thr;
+}
+
+// token index in the layer-input space for compacted tail row r (tail of K out of I per sample)
+__device__ __forceinline__ int64_t tail_token(int64_t r, int K, int I) {
+  if (K == I) return r;
+  int64_t b = r / K;
+  return b * I + (I - K) + (r - b * K);
+}
+
+__device__ __forceinline__ float gelu_erf(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+}
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+  // d/dx 0.5 x (1 + erf(x/sqrt2)) = 0.5 (1 + erf(x/sqrt2)) + x * exp(-x^2/2) / sqrt(2 pi)
+  return 0.5f * (1.0f + erff(x * 0.70710678118654752440f)) +
+         x * 0.39894228040143267794f * __expf(-0.5f * x * x);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+inline unsigned ceil_div(int64_t a, int64_t b) { return (unsigned)((a + b - 1) / b); }
+
+}  // namespace ot
+
+namespace ot {
+inline uint32_t drop_threshold(float rate) {
+  double thr = (double)rate * 4294967296.0;
+  return thr >= 4294967295.0 ? 4294967295u : (uint32_t)llround(thr);
+}
+}  // namespace ot

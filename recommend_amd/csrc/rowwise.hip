@@ -1,0 +1,260 @@
+// Row-wise HBM-bound kernels: RMSNorm (model.py:19-23) forward/backward, the dropout mask
+// (model.py:184,193,198) applied to a gradient, and deterministic column sums.
+//
+// RMSNorm is never materialised in the forward pass of a block: ot_rmsnorm_fwd writes only
+// rstd[row] and the consuming GEMM applies x * rstd * gamma in its A-load prologue
+// (OT_AX_RMSNORM).  The backward fuses the residual pass-through and the dropout mask of the
+// residual branch that produced x:
+//   dx   = dres + rstd * (gamma * dy) - x * rstd^3 / d * sum(gamma * dy * x)
+//   dx_m = mask(dx)                                  (optional: gradient of the pre-dropout branch)
+//   dgamma_partial[block] = sum_rows dy * x * rstd   (reduced by ot_colsum_reduce)
+#include "common.h"
+
+namespace ot {
+
+// threads per row: TPR lanes cover d/4 float4 chunks (TPR = min(64, d/4) rounded down to pow2)
+__device__ __forceinline__ float group_sum(float v, int tpr) {
+  for (int o = tpr >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const float* __restrict__ x, int64_t ldx,
+                                                          const float* __restrict__ gamma, float* y, int64_t ldy,
+                                                          float* rstd, int64_t rows, int d, float eps, int tpr) {
+  const int rpb = 256 / tpr;
+  const int64_t row = (int64_t)blockIdx.x * rpb + threadIdx.x / tpr;
+  const int lt = threadIdx.x % tpr;
+  const bool live = row < rows;
+  const float* xr = x + (live ? row : 0) * ldx;
+  float ss = 0.f;
+  for (int c = lt * 4; c < d; c += tpr * 4) {
+    f32x4 v = *reinterpret_cast<const f32x4*>(xr + c);
+    ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  ss = group_sum(ss, tpr);
+  const float r = rsqrtf(ss / (float)d + eps);
+  if (!live) return;
+  if (lt == 0 && rstd) rstd[row] = r;
+  if (y) {
+    float* yr = y + row * ldy;
+    for (int c = lt * 4; c < d; c += tpr * 4) {
+      f32x4 v = *reinterpret_cast<const f32x4*>(xr + c);
+      f32x4 g = *reinterpret_cast<const f32x4*>(gamma + c);
+      *reinterpret_cast<f32x4*>(yr + c) = v * r * g;
+    }
+  }
+}
+
+struct RmsBwdArgs {
+  const float* dy; int64_t lddy;
+  const float* x; int64_t ldx;
+  const float* gamma; const float* rstd;
+  const float* dres; int64_t lddres; int dres_K, dres_I;   // dres_K > 0: dres holds only the tail rows
+  float* dx; int64_t lddx;
+  float* dxm; int64_t lddxm;            // optional masked copy
+  uint32_t seed, site, thr; float dscale; int tail_K, tail_I;
+  float* dgamma_part;                   // [gridDim.x][d] or null
+  int64_t rows; int d; int tpr;
+};
+
+__global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(RmsBwdArgs p) {
+  extern __shared__ __attribute__((aligned(16))) float red[];   // [256/tpr][d] for dgamma
+  const int tpr = p.tpr, rpb = 256 / tpr, d = p.d;
+  const int lr = threadIdx.x / tpr, lt = threadIdx.x % tpr;
+  f32x4 dg[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) dg[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int64_t row0 = (int64_t)blockIdx.x * rpb; row0 < p.rows; row0 += (int64_t)gridDim.x * rpb) {
+    const int64_t row = row0 + lr;
+    const bool live = row < p.rows;
+    const int64_t rr = live ? row : 0;
+    const float* dyr = p.dy + rr * p.lddy;
+    const float* xr = p.x + rr * p.ldx;
+    const float r = live ? p.rstd[rr] : 0.f;
+    float s = 0.f;
+    for (int c = lt * 4; c < d; c += tpr * 4) {
+      f32x4 a = *reinterpret_cast<const f32x4*>(dyr + c);
+      f32x4 g = *reinterpret_cast<const f32x4*>(p.gamma + c);
+      f32x4 v = *reinterpret_cast<const f32x4*>(xr + c);
+      s += a.x * g.x * v.x + a.y * g.y * v.y + a.z * g.z * v.z + a.w * g.w * v.w;
+    }
+    s = group_sum(s, tpr);
+    const float coef = r * r * r * s / (float)d;
+    const int64_t tok = p.dxm ? tail_token(rr, p.tail_K, p.tail_I) : 0;
+    int q = 0;
+    for (int c = lt * 4; c < d; c += tpr * 4, ++q) {
+      f32x4 a = *reinterpret_cast<const f32x4*>(dyr + c);
+      f32x4 g = *reinterpret_cast<const f32x4*>(p.gamma + c);
+      f32x4 v = *reinterpret_cast<const f32x4*>(xr + c);
+      if (!live) continue;
+      f32x4 o = a * g * r - v * coef;
+      if (p.dres) {
+        int64_t dr = rr;
+        if (p.dres_K > 0) {
+          const int64_t b = rr / p.dres_I, pos = rr - b * p.dres_I, j = pos - (p.dres_I - p.dres_K);
+          dr = j >= 0 ? b * p.dres_K + j : -1;
+        }
+        if (dr >= 0) o += *reinterpret_cast<const f32x4*>(p.dres + dr * p.lddres + c);
+      }
+      if (q < 4) dg[q] += a * v * r;
+      *reinterpret_cast<f32x4*>(p.dx + rr * p.lddx + c) = o;
+      if (p.dxm) {
+        f32x4 m;
+        uint32_t base = (uint32_t)(tok * d + c);
+        m.x = drop_keep(p.seed, p.site, base + 0, p.thr) ? o.x * p.dscale : 0.f;
+        m.y = drop_keep(p.seed, p.site, base + 1, p.thr) ? o.y * p.dscale : 0.f;
+        m.z = drop_keep(p.seed, p.site, base + 2, p.thr) ? o.z * p.dscale : 0.f;
+        m.w = drop_keep(p.seed, p.site, base + 3, p.thr) ? o.w * p.dscale : 0.f;
+        *reinterpret_cast<f32x4*>(p.dxm + rr * p.lddxm + c) = m;
+      }
+    }
+  }
+  if (p.dgamma_part) {
+    int q = 0;
+    for (int c = lt * 4; c < d; c += tpr * 4, ++q) *reinterpret_cast<f32x4*>(red + lr * d + c) = dg[q];
+    __syncthreads();
+    for (int c = threadIdx.x; c < d; c += 256) {
+      float acc = 0.f;
+      for (int k = 0; k < rpb; ++k) acc += red[k * d + c];
+      p.dgamma_part[(int64_t)blockIdx.x * d + c] = acc;
+    }
+  }
+}
+
+// out[c] (+)= sum_{b < nparts} part[b][c]   (fixed order: deterministic)
+__global__ void colsum_reduce_kernel(const float* __restrict__ part, int64_t nparts, int ncols, float* out,
+                                     int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ncols) return;
+  float s = 0.f;
+  for (int64_t b = 0; b < nparts; ++b) s += part[b * ncols + c];
+  out[c] = accumulate ? out[c] + s : s;
+}
+
+// part[blk][c] = sum of rows [blk*RPB, (blk+1)*RPB) of the listed rows, column c
+__global__ void rows_colsum_kernel(const float* __restrict__ src, int64_t ld, const int32_t* __restrict__ rows,
+                                   int64_t nrows, int ncols, int rows_per_block, float* part) {
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ncols) return;
+  float s = 0.f;
+  for (int64_t i = r0; i < r0 + rows_per_block && i < nrows; ++i) {
+    int64_t r = rows ? rows[i] : i;
+    s += src[r * ld + c];
+  }
+  part[(int64_t)blockIdx.y * ncols + c] = s;
+}
+
+__global__ void dropout_apply_kernel(const float* __restrict__ src, int64_t lds, float* dst, int64_t ldd,
+                                     int64_t rows, int d, uint32_t seed, uint32_t site, uint32_t thr, float scale,
+                                     int tail_K, int tail_I) {
+  const int64_t i4 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i4 >= rows * d) return;
+  const int64_t r = i4 / d;
+  const int c = (int)(i4 % d);
+  const int64_t tok = tail_token(r, tail_K, tail_I);
+  f32x4 v = *reinterpret_cast<const f32x4*>(src + r * lds + c);
+  uint32_t base = (uint32_t)(tok * d + c);
+  v.x = drop_keep(seed, site, base + 0, thr) ? v.x * scale : 0.f;
+  v.y = drop_keep(seed, site, base + 1, thr) ? v.y * scale : 0.f;
+  v.z = drop_keep(seed, site, base + 2, thr) ? v.z * scale : 0.f;
+  v.w = drop_keep(seed, site, base + 3, thr) ? v.w * scale : 0.f;
+  *reinterpret_cast<f32x4*>(dst + r * ldd + c) = v;
+}
+
+inline int tpr_for(int d) {
+  int t = d / 4;
+  int p = 1;
+  while (p * 2 <= t && p * 2 <= 64) p *= 2;
+  return p;
+}
+
+}  // namespace ot
+
+using namespace ot;
+
+extern "C" int ot_rmsnorm_fwd(const float* x, int64_t ldx, const float* gamma, float* y, int64_t ldy, float* rstd,
+                              int64_t rows, int d, float eps, void* stream) {
+  OT_REQUIRE(x && (rstd || y), "ot_rmsnorm_fwd: null operand");
+  OT_REQUIRE(!y || gamma, "ot_rmsnorm_fwd: y needs gamma");
+  OT_REQUIRE(d > 0 && d % 4 == 0 && ldx % 4 == 0 && (!y || ldy % 4 == 0), "ot_rmsnorm_fwd: d/ld must be multiples of 4");
+  if (rows == 0) return OT_OK;
+  const int tpr = tpr_for(d);
+  hipLaunchKernelGGL(rmsnorm_fwd_kernel, dim3(ceil_div(rows, 256 / tpr)), dim3(256), 0, (hipStream_t)stream,
+                     x, ldx, gamma, y, ldy, rstd, rows, d, eps, tpr);
+  OT_LAUNCH_CHECK("ot_rmsnorm_fwd");
+  return OT_OK;
+}
+
+inline unsigned rms_bwd_grid(int64_t rows, int d) {
+  const int tpr = ot::tpr_for(d);
+  unsigned g = ceil_div(rows, 256 / tpr);
+  return g < 1024 ? g : 1024;
+}
+
+extern "C" size_t ot_rmsnorm_bwd_workspace_size(int64_t rows, int d) {
+  return (size_t)rms_bwd_grid(rows, d) * d * sizeof(float);
+}
+
+extern "C" int ot_rmsnorm_bwd(const float* dy, int64_t lddy, const float* x, int64_t ldx, const float* gamma,
+                              const float* rstd, const float* dres, int64_t lddres, int dres_tail_K,
+                              int dres_tail_I, float* dx, int64_t lddx,
+                              float* dx_masked, int64_t lddxm, uint32_t seed, uint32_t site, float drop_rate,
+                              int tail_K, int tail_I, float* dgamma, int accumulate_dgamma, int64_t rows, int d,
+                              void* workspace, size_t ws_bytes, void* stream) {
+  OT_REQUIRE(dy && x && gamma && rstd && dx, "ot_rmsnorm_bwd: null operand");
+  OT_REQUIRE(d % 4 == 0 && lddy % 4 == 0 && ldx % 4 == 0 && lddx % 4 == 0, "ot_rmsnorm_bwd: alignment");
+  OT_REQUIRE(!dgamma || (workspace && ws_bytes >= ot_rmsnorm_bwd_workspace_size(rows, d)),
+             "ot_rmsnorm_bwd: workspace too small");
+  OT_REQUIRE(!dx_masked || (tail_K > 0 && tail_I >= tail_K), "ot_rmsnorm_bwd: bad tail map");
+  if (rows == 0) return OT_OK;
+  OT_REQUIRE(d <= 16 * tpr_for(d), "ot_rmsnorm_bwd: d=%d too large", d);
+  const int tpr = tpr_for(d);
+  const unsigned grid = rms_bwd_grid(rows, d);
+  OT_REQUIRE(dres_tail_K == 0 || (dres_tail_K > 0 && dres_tail_I >= dres_tail_K), "ot_rmsnorm_bwd: bad dres tail");
+  RmsBwdArgs p{dy, lddy, x, ldx, gamma, rstd, dres, lddres, dres_tail_K, dres_tail_I, dx, lddx, dx_masked, lddxm, seed, site,
+               drop_threshold(drop_rate), drop_rate < 1.f ? 1.f / (1.f - drop_rate) : 0.f, tail_K, tail_I,
+               dgamma ? (float*)workspace : nullptr, rows, d, tpr};
+  const size_t shmem = dgamma ? (size_t)(256 / tpr) * d * sizeof(float) : 0;
+  OT_REQUIRE(shmem <= 65536, "ot_rmsnorm_bwd: d too large for the dgamma staging");
+  hipLaunchKernelGGL(rmsnorm_bwd_kernel, dim3(grid), dim3(256), shmem, (hipStream_t)stream, p);
+  OT_LAUNCH_CHECK("ot_rmsnorm_bwd");
+  if (dgamma) {
+    hipLaunchKernelGGL(colsum_reduce_kernel, dim3(ceil_div(d, 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const float*)workspace, (int64_t)grid, d, dgamma, accumulate_dgamma);
+    OT_LAUNCH_CHECK("ot_rmsnorm_bwd(reduce)");
+  }
+  return OT_OK;
+}
+
+extern "C" int ot_dropout_apply(const float* src, int64_t lds, float* dst, int64_t ldd, int64_t rows, int d,
+                                uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I, void* stream) {
+  OT_REQUIRE(src && dst && d % 4 == 0 && lds % 4 == 0 && ldd % 4 == 0, "ot_dropout_apply: bad args");
+  OT_REQUIRE(tail_K > 0 && tail_I >= tail_K, "ot_dropout_apply: bad tail map");
+  if (rows == 0) return OT_OK;
+  hipLaunchKernelGGL(dropout_apply_kernel, dim3(ceil_div(rows * d / 4, 256)), dim3(256), 0, (hipStream_t)stream,
+                     src, lds, dst, ldd, rows, d, seed, site, drop_threshold(drop_rate),
+                     drop_rate < 1.f ? 1.f / (1.f - drop_rate) : 0.f, tail_K, tail_I);
+  OT_LAUNCH_CHECK("ot_dropout_apply");
+  return OT_OK;
+}
+
+extern "C" size_t ot_rows_colsum_workspace_size(int64_t nrows, int ncols) {
+  return (size_t)ceil_div(nrows, 256) * ncols * sizeof(float);
+}
+
+extern "C" int ot_rows_colsum(const float* src, int64_t ld, const int32_t* rows, int64_t nrows, int ncols,
+                              float* out, int accumulate, void* workspace, size_t ws_bytes, void* stream) {
+  OT_REQUIRE(src && out && ncols > 0, "ot_rows_colsum: bad args");
+  OT_REQUIRE(workspace && ws_bytes >= ot_rows_colsum_workspace_size(nrows, ncols), "ot_rows_colsum: workspace");
+  const unsigned nb = ceil_div(nrows, 256);
+  if (nb > 0) {
+    hipLaunchKernelGGL(rows_colsum_kernel, dim3(ceil_div(ncols, 256), nb), dim3(256), 0, (hipStream_t)stream,
+                       src, ld, rows, nrows, ncols, 256, (float*)workspace);
+    OT_LAUNCH_CHECK("ot_rows_colsum");
+  }
+  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(ceil_div(ncols, 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const float*)workspace, (int64_t)nb, ncols, out, accumulate);
+  OT_LAUNCH_CHECK("ot_rows_colsum(reduce)");
+  return OT_OK;
+}

@@ -1,0 +1,234 @@
+"""Thin torch-tensor wrappers over the C ABI (``_lib``).  No arithmetic happens here: every
+function forwards device pointers, sizes and the current HIP stream to libonetrans_hip.so.
+
+Pointer arguments accept a tensor, ``(tensor, element_offset)`` or None."""
+
+from __future__ import annotations
+
+from typing import Optional, Tuple, Union
+
+import torch
+
+from . import _lib
+from ._lib import call, size
+
+Ptrish = Union[None, torch.Tensor, Tuple[torch.Tensor, int]]
+
+
+class Probe:
+    """Times kernel launches with HIP events recorded on the launch stream (bench.py uses it over
+    the timed region) and accumulates the algorithmic FLOPs of each launch (valid rows only)."""
+
+    def __init__(self):
+        self.recs = []
+
+    def begin(self):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+
+    def end(self, family: str, flops: float, ev0) -> None:
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev1.record()
+        self.recs.append((family, flops, ev0, ev1))
+
+    def report(self, steps: int):
+        torch.cuda.synchronize()
+        fam = {}
+        for (f, fl, a, b) in self.recs:
+            d = fam.setdefault(f, {'ms': 0.0, 'flops': 0.0, 'n': 0})
+            d['ms'] += a.elapsed_time(b)
+            d['flops'] += fl
+            d['n'] += 1
+        out = {}
+        for f, d in fam.items():
+            out[f] = {'ms_per_step': d['ms'] / steps, 'avg_us': 1e3 * d['ms'] / d['n'],
+                      'launches_per_step': d['n'] / steps, 'gflop_per_launch': d['flops'] / d['n'] / 1e9,
+                      'tflops': d['flops'] / (d['ms'] * 1e-3) / 1e12 if d['ms'] > 0 else 0.0}
+        return {'families': out}
+
+
+_probe = None
+
+
+def set_probe(p) -> None:
+    global _probe
+    _probe = p
+
+
+def ptr(x: Ptrish):
+    if x is None:
+        return None
+    if isinstance(x, tuple):
+        t, off = x
+        return t.data_ptr() + off * t.element_size()
+    return x.data_ptr()
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def workspace(nbytes: int, device) -> torch.Tensor:
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+
+
+def gemm(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish, w_gstride: int, ldw: int, N: int,
+         tile_group: Ptrish, ntiles: int, C: Ptrish, ldc: int, out_rows: Ptrish, *, a_xform: int = 0,
+         rstd: Ptrish = None, gamma: Ptrish = None, bias: Ptrish = None, bias_gstride: int = 0, epi: int = 0,
+         res: Ptrish = None, ldres: int = 0, res_tok: int = 0, aux: Ptrish = None, ldaux: int = 0,
+         seed: int = 0, site: int = 0, drop: float = 0.0, tail: Tuple[int, int] = (1, 1),
+         m_rows: int = 0) -> None:
+    ev = _probe.begin() if _probe is not None else None
+    call('ot_mixed_gemm', mode, ptr(A), lda, K, ptr(in_rows), a_xform, ptr(rstd), ptr(gamma), ptr(W), w_gstride,
+         ldw, N, ptr(tile_group), ntiles, ptr(bias), bias_gstride, ptr(C), ldc, ptr(out_rows), epi, ptr(res),
+         ldres, res_tok, ptr(aux), ldaux, seed & 0xFFFFFFFF, site, float(drop), tail[0], tail[1], stream())
+    if ev is not None:
+        _probe.end('mixed_gemm', 2.0 * (m_rows or ntiles * 128) * K * N, ev)
+
+
+def wgrad(A: Ptrish, lda: int, a_rows: Ptrish, D: Ptrish, ldd: int, d_rows: Ptrish, K: int, N: int, rmap_dev,
+          nchunks: int, ngroups: int, dW: Ptrish, dw_gstride: int, db: Ptrish = None, db_gstride: int = 0, *,
+          a_xform: int = 0, rstd: Ptrish = None, gamma: Ptrish = None, accumulate: bool = False,
+          device=None, m_rows: int = 0) -> None:
+    nbytes = size('ot_wgrad_workspace_size', nchunks, K, N)
+    ws = workspace(nbytes, device)
+    ev = _probe.begin() if _probe is not None else None
+    call('ot_mixed_gemm_wgrad', ptr(A), lda, ptr(a_rows), a_xform, ptr(rstd), ptr(gamma), ptr(D), ldd,
+         ptr(d_rows), K, N, ptr(rmap_dev['chunks']), nchunks, ptr(rmap_dev['gchunk']), ngroups, ptr(dW),
+         dw_gstride, ptr(db), db_gstride, int(accumulate), ptr(ws), ws.numel(), stream())
+    if ev is not None:
+        _probe.end('mixed_gemm', 2.0 * m_rows * K * N, ev)
+
+
+def attn_fwd(qkv: torch.Tensor, ld: int, B: int, H: int, I: int, K: int, hd: int, out: torch.Tensor,
+             lse: torch.Tensor) -> None:
+    ev = _probe.begin() if _probe is not None else None
+    call('ot_attn_fwd', ptr(qkv), ld, B, H, I, K, hd, ptr(out), ptr(lse), stream())
+    if ev is not None:
+        _probe.end('attention', 4.0 * (K * I - K * (K - 1) / 2) * hd * H * B, ev)
+
+
+def attn_bwd(qkv, ld, out, dout, lse, B, H, I, K, hd, dqkv) -> None:
+    delta = torch.empty(max(B * H * K, 1), dtype=torch.float32, device=qkv.device)
+    ev = _probe.begin() if _probe is not None else None
+    call('ot_attn_bwd', ptr(qkv), ld, ptr(out), ptr(dout), ptr(lse), B, H, I, K, hd, ptr(dqkv), ptr(delta),
+         stream())
+    if ev is not None:
+        _probe.end('attention', 8.0 * (K * I - K * (K - 1) / 2) * hd * H * B, ev)
+
+
+def rmsnorm_fwd(x: Ptrish, ldx: int, rows: int, d: int, rstd: Ptrish, gamma: Ptrish = None, y: Ptrish = None,
+                ldy: int = 0, eps: float = 1e-6) -> None:
+    ev = _probe.begin() if _probe is not None else None
+    call('ot_rmsnorm_fwd', ptr(x), ldx, ptr(gamma), ptr(y), ldy, ptr(rstd), rows, d, eps, stream())
+    if ev is not None:
+        _probe.end('rowwise', 0.0, ev)
+
+
+def rmsnorm_bwd(dy: Ptrish, lddy: int, x: Ptrish, ldx: int, gamma: Ptrish, rstd: Ptrish, dx: Ptrish, lddx: int,
+                rows: int, d: int, *, dres: Ptrish = None, lddres: int = 0, dres_tail=(0, 0), dx_masked: Ptrish = None,
+                lddxm: int = 0, seed: int = 0, site: int = 0, drop: float = 0.0, tail=(1, 1),
+                dgamma: Ptrish = None, accumulate: bool = False, device=None) -> None:
+    nbytes = size('ot_rmsnorm_bwd_workspace_size', rows, d) if dgamma is not None else 16
+    ws = workspace(nbytes, device)
+    ev = _probe.begin() if _probe is not None else None
+    call('ot_rmsnorm_bwd', ptr(dy), lddy, ptr(x), ldx, ptr(gamma), ptr(rstd), ptr(dres), lddres, dres_tail[0],
+         dres_tail[1], ptr(dx), lddx, ptr(dx_masked), lddxm, seed & 0xFFFFFFFF, site, float(drop), tail[0], tail[1],
+         ptr(dgamma), int(accumulate), rows, d, ptr(ws), ws.numel(), stream())
+    if ev is not None:
+        _probe.end('rowwise', 0.0, ev)
+
+
+def dropout_apply(src, lds, dst, ldd, rows, d, seed, site, drop, tail) -> None:
+    ev = _probe.begin() if _probe is not None else None
+    call('ot_dropout_apply', ptr(src), lds, ptr(dst), ldd, rows, d, seed & 0xFFFFFFFF, site, float(drop), tail[0],
+         tail[1], stream())
+    if ev is not None:
+        _probe.end('rowwise', 0.0, ev)
+
+
+def rows_colsum(src, ld, rows: Ptrish, nrows: int, ncols: int, out: Ptrish, accumulate=False, device=None) -> None:
+    ws = workspace(size('ot_rows_colsum_workspace_size', nrows, ncols), device)
+    ev = _probe.begin() if _probe is not None else None
+    call('ot_rows_colsum', ptr(src), ld, ptr(rows), nrows, ncols, ptr(out), int(accumulate), ptr(ws), ws.numel(),
+         stream())
+    if ev is not None:
+        _probe.end('rowwise', 0.0, ev)
+
+
+def ns_assemble(fields_dev, nfields, table, B, out, ld_out) -> None:
+    ev = _probe.begin() if _probe is not None else None
+    call('ot_ns_assemble', ptr(fields_dev), nfields, ptr(table), B, ptr(out), ld_out, stream())
+    if ev is not None:
+        _probe.end('embedding', 0.0, ev)
+
+
+def ns_grad_pack(fields_dev, nsparse, width, dmat, ld, B, keys, grads) -> None:
+    ev = _probe.begin() if _probe is not None else None
+    call('ot_ns_grad_pack', ptr(fields_dev), nsparse, width, ptr(dmat), ld, B, ptr(keys), ptr(grads), stream())
+    if ev is not None:
+        _probe.end('embedding', 0.0, ev)
+
+
+def fill_rows(dst, ld, rows, nrows, vec, d) -> None:
+    ev = _probe.begin() if _probe is not None else None
+    call('ot_fill_rows', ptr(dst), ld, ptr(rows), nrows, ptr(vec), d, stream())
+    if ev is not None:
+        _probe.end('embedding', 0.0, ev)
+
+
+def seq_rows(ids, stride_b, B, L, vocab, in_rows) -> None:
+    ev = _probe.begin() if _probe is not None else None
+    call('ot_seq_rows', ptr(ids), stride_b, B, L, vocab, ptr(in_rows), stream())
+    if ev is not None:
+        _probe.end('embedding', 0.0, ev)
+
+
+def head_fwd(pre1, w2, b2, T, B, dh, logits, probs) -> None:
+    ev = _probe.begin() if _probe is not None else None
+    call('ot_head_fwd', ptr(pre1), ptr(w2), ptr(b2), T, B, dh, ptr(logits), ptr(probs), stream())
+    if ev is not None:
+        _probe.end('head_loss', 0.0, ev)
+
+
+def head_bwd(pre1, w2, probs, dprobs, T, B, dh, dpre1, dw2, db2, sw2, sb2, accumulate=False, device=None) -> None:
+    ws = workspace(size('ot_head_bwd_workspace_size', T, B, dh), device)
+    ev = _probe.begin() if _probe is not None else None
+    call('ot_head_bwd', ptr(pre1), ptr(w2), ptr(probs), ptr(dprobs), T, B, dh, ptr(dpre1), ptr(dw2), ptr(db2), sw2,
+         sb2, int(accumulate), ptr(ws), ws.numel(), stream())
+    if ev is not None:
+        _probe.end('head_loss', 0.0, ev)
+
+
+def bce_fwd(probs, labels, T, B, loss, device=None) -> None:
+    ws = workspace(size('ot_bce_workspace_size', T, B), device)
+    ev = _probe.begin() if _probe is not None else None
+    call('ot_bce_fwd', ptr(probs), ptr(labels), T, B, ptr(loss), ptr(ws), ws.numel(), stream())
+    if ev is not None:
+        _probe.end('head_loss', 0.0, ev)
+
+
+def bce_bwd(probs, labels, gscale, T, B, dprobs) -> None:
+    ev = _probe.begin() if _probe is not None else None
+    call('ot_bce_bwd', ptr(probs), ptr(labels), ptr(gscale), T, B, ptr(dprobs), stream())
+    if ev is not None:
+        _probe.end('head_loss', 0.0, ev)
+
+
+def sparse_adagrad(table, accum, E, num_rows, keys, grads, n, lr, eps, clip, device=None) -> None:
+    ws = workspace(size('ot_sparse_adagrad_workspace_size', n, E), device)
+    ev = _probe.begin() if _probe is not None else None
+    call('ot_sparse_adagrad', ptr(table), ptr(accum), E, num_rows, ptr(keys), ptr(grads), n, float(lr), float(eps),
+         float(clip), ptr(ws), ws.numel(), stream())
+    if ev is not None:
+        _probe.end('embedding', 0.0, ev)
+
+
+def clip_rmsprop(w, g, v, m, segs_dev, nseg, max_seg, lr, rho, eps, momentum, clip, device=None) -> None:
+    ws = workspace(size('ot_clip_rmsprop_workspace_size', nseg, max_seg), device)
+    ev = _probe.begin() if _probe is not None else None
+    call('ot_clip_rmsprop', ptr(w), ptr(g), ptr(v), ptr(m), ptr(segs_dev), nseg, max_seg, float(lr), float(rho),
+         float(eps), float(momentum), float(clip), ptr(ws), ws.numel(), stream())
+    if ev is not None:
+        _probe.end('optimizer', 0.0, ev)

@@ -1,0 +1,151 @@
+"""Device data layout: the flat dense-parameter buffer and the row maps of the grouped GEMMs.
+
+HBM layout:
+
+* every dense parameter bank of ``params.dense_param_shapes`` lives in ONE flat fp32 buffer
+  (bank offsets 64-float aligned); gradients and the RMSprop state (v, m) are flat buffers
+  of the same layout, so the optimizer is one multi-segment launch and the DP all-reduce is
+  one contiguous buffer.
+* activations are token-major ``[B * I, width]`` (row = b * I + p); a layer that keeps only
+  its last K tokens writes compact ``[B * K, width]`` rows (row = b * K + j).
+* a *row map* lists, tile by tile (128 rows per tile), which rows a grouped GEMM reads and
+  writes; every tile belongs to one weight group (mixed parameterisation, model.py:67-74).
+  Padding entries are -1.
+"""
+
+from __future__ import annotations
+
+from typing import Callable, Dict, List, Sequence, Tuple
+
+import numpy as np
+
+from .config import OneTransConfig
+from .params import dense_param_shapes, keras_variables
+
+TILE = 128
+ALIGN = 64
+
+
+def round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+class FlatLayout:
+    """Offsets of every dense bank inside the flat parameter buffer."""
+
+    def __init__(self, cfg: OneTransConfig, f_ns: int):
+        self.f_ns = f_ns
+        self.f_pad = max(4, round_up(f_ns, 4))
+        self.shapes = dense_param_shapes(cfg, self.f_pad)
+        self.offsets: Dict[str, int] = {}
+        off = 0
+        for name, shp in self.shapes.items():
+            self.offsets[name] = off
+            off += round_up(int(np.prod(shp)), ALIGN)
+        self.total = off
+        segs = []
+        for (bank, eoff, rows, cols, stride) in keras_variables(cfg, self.shapes, f_ns=f_ns):
+            segs.append((self.offsets[bank] + eoff, rows, cols, stride))
+        self.segments = np.array(segs, dtype=np.int64)
+        self.max_seg_elems = int((self.segments[:, 1] * self.segments[:, 2]).max())
+
+    def view(self, flat, name):
+        off = self.offsets[name]
+        n = int(np.prod(self.shapes[name]))
+        return flat[off:off + n].view(self.shapes[name])
+
+
+class RowMap:
+    """Tiles of a grouped GEMM: ``rows[k]`` (one int32 array per index space, length
+    ntiles*TILE, -1 padded), ``tile_group`` [ntiles], and wgrad chunks {group, begin, count}
+    with ``gchunk`` [G, 2] {first chunk, n chunks}."""
+
+    def __init__(self, rows: List[np.ndarray], tile_group: np.ndarray, chunks: np.ndarray,
+                 gchunk: np.ndarray, nrows: int):
+        self.rows = rows
+        self.tile_group = tile_group
+        self.chunks = chunks
+        self.gchunk = gchunk
+        self.ntiles = len(tile_group)
+        self.nrows = nrows              # real (unpadded) rows
+        self.dev = None
+
+    def to(self, device):
+        import torch
+        if self.dev is None:
+            self.dev = {
+                'rows': [torch.from_numpy(r).to(device) for r in self.rows],
+                'tile_group': torch.from_numpy(self.tile_group).to(device),
+                'chunks': torch.from_numpy(self.chunks).to(device),
+                'gchunk': torch.from_numpy(self.gchunk).to(device),
+            }
+        return self.dev
+
+
+def build_map(per_group: Sequence[Sequence[np.ndarray]], chunk_rows: int = 0) -> RowMap:
+    """``per_group[g]`` = list (one per index space) of equal-length int arrays of rows of group g.
+    Each group is padded to a multiple of TILE; wgrad chunks split each group into runs of
+    ``chunk_rows`` (a multiple of TILE; 0 = auto, ~256 chunks overall)."""
+    G = len(per_group)
+    nspace = len(per_group[0]) if G else 0
+    total = sum(len(pg[0]) for pg in per_group)
+    if chunk_rows <= 0:
+        chunk_rows = max(4 * TILE, round_up(max(1, total // 256), TILE))
+    rows = [[] for _ in range(nspace)]
+    tile_group, chunks, gchunk = [], [], []
+    base = 0
+    for g, pg in enumerate(per_group):
+        n = len(pg[0])
+        npad = round_up(n, TILE)
+        for s in range(nspace):
+            r = np.full(npad, -1, dtype=np.int32)
+            r[:n] = pg[s]
+            rows[s].append(r)
+        tile_group.extend([g] * (npad // TILE))
+        first = len(chunks)
+        for c0 in range(0, npad, chunk_rows):
+            chunks.append((g, base + c0, min(chunk_rows, npad - c0)))
+        gchunk.append((first, len(chunks) - first))
+        base += npad
+    cat = [np.concatenate(r) if r else np.zeros(0, np.int32) for r in rows]
+    return RowMap(cat, np.array(tile_group, dtype=np.int32),
+                  np.array(chunks, dtype=np.int32).reshape(-1, 3),
+                  np.array(gchunk, dtype=np.int32).reshape(-1, 2), total)
+
+
+def layer_maps(cfg: OneTransConfig, B: int, I: int, K: int) -> Dict[str, RowMap]:
+    """Row maps of one block whose input has I tokens and which keeps the last K.
+
+    * ``all``:  every token (b*I + p), grouped by group_of_position(p, I): K/V projections,
+      and the Q projection too when K == I.
+    * ``tail``: the kept tokens; space 0 = token rows b*I + p in the input, space 1 = compact
+      rows b*K + j (p = I - K + j): Q projection (K < I), Wo, FFN.
+    """
+    G = cfg.num_groups
+    grp = np.array([cfg.group_of_position(p, I) for p in range(I)])
+    b = np.arange(B)[:, None]
+
+    def rows_for(positions, fn):
+        if len(positions) == 0:
+            return np.zeros(0, np.int64)
+        return fn(b, np.asarray(positions)[None, :]).reshape(-1)
+
+    all_pg, tail_pg = [], []
+    for g in range(G):
+        pos = np.nonzero(grp == g)[0]
+        all_pg.append([rows_for(pos, lambda bb, pp: bb * I + pp)])
+        tpos = pos[pos >= I - K]
+        tail_pg.append([rows_for(tpos, lambda bb, pp: bb * I + pp),
+                        rows_for(tpos, lambda bb, pp: bb * K + (pp - (I - K)))])
+    return {'all': build_map(all_pg), 'tail': build_map(tail_pg)}
+
+
+def head_map(B: int, T: int) -> RowMap:
+    """Task heads: group t reads sample row b (space 0) and writes row t*B + b (space 1)."""
+    b = np.arange(B)
+    return build_map([[b, t * B + b] for t in range(T)])
+
+
+def identity_map(n: int) -> RowMap:
+    r = np.arange(n)
+    return build_map([[r, r]])

@@ -1,0 +1,623 @@
+"""OneTransModel on MI355X: the reference ``OneTransModel`` (model.py:305-416) as a torch
+``nn.Module`` whose every arithmetic step runs in libonetrans_hip.so.
+
+Drop-in surface: ``OneTransModel(config)``;
+``forward(non_seq_features, seq_features=None, training=None, use_kv_cache=False) ->
+{task: probs [B,1]}``, also accepting the callers' tuple form ``model((non_seq, seq),
+training=...)`` (train.py:118, evaluate.py:87 — defect D4); ``reset_kv_cache()``;
+``get_model_info()``; ``trainable_variables``; ``save_weights/load_weights``;
+``create_onetrans_model(model_type)``.
+
+Autograd: four ``torch.autograd.Function``s (tokenizer, block, output-norm+heads, loss).  Their
+backward passes write parameter gradients straight into the flat gradient buffer
+``model.flat.grad`` (one bank per reference variable group), so the optimizer and the DP
+all-reduce each touch one contiguous buffer.  Embedding-table gradients are handed to the
+optimizer as (row keys, gradient rows) pairs: sparse updates, never a dense table gradient.
+"""
+
+from __future__ import annotations
+
+import json
+import os
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _lib
+from . import kernels as K
+from ._lib import (OT_AX_GELU, OT_AX_RMSNORM, OT_EPI_ACCUMULATE, OT_EPI_BIAS, OT_EPI_DROPOUT, OT_EPI_GELU_BWD,
+                   OT_EPI_RESIDUAL, OT_GEMM_NN, OT_GEMM_NT, NS_FIELD_BYTES)
+from .config import OneTransConfig, get_model_config
+from .layout import TILE, FlatLayout, RowMap, build_map, head_map, identity_map, layer_maps, round_up
+from .params import init_params, ns_table_offsets
+
+RMS_EPS = 1e-6   # RMSNorm eps, model.py:14
+
+
+# =============================================================================== autograd ops
+class _Tokenize(torch.autograd.Function):
+    """Tokenizer.call (model.py:224-277): [S tokens ; NS tokens] -> x0 [B*L0, d]."""
+
+    @staticmethod
+    def forward(ctx, flat, m, plan):
+        d = m.config.hidden_dim
+        B, L0, L_S = plan['B'], plan['L0'], plan['L_S']
+        dev = flat.device
+        x0 = torch.empty(B * L0, d, device=dev)
+        # ---- NS tokens: gather/concat -> Dense(L_NS*d) straight into token rows L_S.. (model.py:253-254)
+        if plan['ns_fields'] > 0:
+            nsm = plan['nsmat']
+            K.ns_assemble(plan['ns_desc'], plan['ns_fields'], m.tables.get('emb.ns'), B, nsm, m.layout.f_pad)
+            mp = plan['ns_map'].to(dev)
+            K.gemm(OT_GEMM_NN, nsm, m.layout.f_pad, m.layout.f_pad, mp['rows'][0], m.p('tok.ns.kernel'), 0,
+                   m.cfg_Lnsd, m.cfg_Lnsd, mp['tile_group'], plan['ns_map'].ntiles, (x0, L_S * d), L0 * d,
+                   mp['rows'][0], bias=m.p('tok.ns.bias'), epi=OT_EPI_BIAS, m_rows=B)
+        else:                                                   # model.py:249-251
+            x0.view(B, L0, d)[:, L_S:].zero_()
+        # ---- S tokens: per-sequence Dense(d) on gathered item rows (model.py:262-265)
+        if plan['seq_map'] is not None:
+            sm = plan['seq_map'].to(dev)
+            A, lda = plan['seq_A'], m.config.seq_feature_dim
+            K.gemm(OT_GEMM_NN, A, lda, lda, plan['seq_in'], m.p('tok.seq.kernel'), lda * d, d, d, sm['tile_group'],
+                   plan['seq_map'].ntiles, x0, d, sm['rows'][0], bias=m.p('tok.seq.bias'), bias_gstride=d,
+                   epi=OT_EPI_BIAS, m_rows=plan['seq_M'])
+        if plan['n_sep'] > 0:                                   # model.py:270-272
+            K.fill_rows(x0, d, plan['sep_rows'], plan['n_sep'], m.p('tok.sep'), d)
+        ctx.m, ctx.plan, ctx.gen = m, plan, plan['gen']
+        return x0
+
+    @staticmethod
+    def backward(ctx, dx0):
+        m, plan = ctx.m, ctx.plan
+        if plan['gen'] != ctx.gen:
+            raise RuntimeError('OneTransModel: a second forward with the same input shapes ran before this '
+                               'backward; run backward before the next forward (inputs are staged in place)')
+        dx0 = dx0.contiguous()
+        d = m.config.hidden_dim
+        B, L0, L_S = plan['B'], plan['L0'], plan['L_S']
+        dev = dx0.device
+        acc = m.accumulate_grads
+        m._pending_sparse = []
+        if plan['ns_fields'] > 0:
+            mp = plan['ns_map'].to(dev)
+            nsm = plan['nsmat']
+            K.wgrad(nsm, m.layout.f_pad, mp['rows'][0], (dx0, L_S * d), L0 * d, mp['rows'][0], m.layout.f_pad,
+                    m.cfg_Lnsd, mp, plan['ns_map'].chunks.shape[0], 1, m.g('tok.ns.kernel'), 0, m.g('tok.ns.bias'),
+                    0, accumulate=acc, device=dev, m_rows=B)
+            if plan['n_sparse'] > 0:
+                dns = torch.empty(B, m.layout.f_pad, device=dev)
+                K.gemm(OT_GEMM_NT, (dx0, L_S * d), L0 * d, m.cfg_Lnsd, mp['rows'][0], m.p('tok.ns.kernel'), 0,
+                       m.cfg_Lnsd, m.layout.f_pad, mp['tile_group'], plan['ns_map'].ntiles, dns, m.layout.f_pad,
+                       mp['rows'][0], m_rows=B)
+                e = m.config.ns_embedding_dim
+                n = plan['n_sparse'] * B
+                keys = torch.empty(n, dtype=torch.int64, device=dev)
+                grads = torch.empty(n, e, device=dev)
+                K.ns_grad_pack(plan['ns_desc'], plan['n_sparse'], e, dns, m.layout.f_pad, B, keys, grads)
+                m._pending_sparse.append(('emb.ns', keys, grads))
+        elif not acc:
+            m.g('tok.ns.kernel').zero_()
+            m.g('tok.ns.bias').zero_()
+        E = m.config.seq_feature_dim
+        if plan['seq_map'] is not None:
+            sm = plan['seq_map'].to(dev)
+            K.wgrad(plan['seq_A'], E, plan['seq_in'], dx0, d, sm['rows'][0], E, d, sm,
+                    plan['seq_map'].chunks.shape[0], plan['nseq'], m.g('tok.seq.kernel'), E * d,
+                    m.g('tok.seq.bias'), d, accumulate=acc, device=dev, m_rows=plan['seq_M'])
+            if plan['seq_ids'] is not None:
+                M = plan['seq_M']
+                demb = torch.empty(M, E, device=dev)
+                K.gemm(OT_GEMM_NT, dx0, d, d, sm['rows'][0], m.p('tok.seq.kernel'), E * d, d, E, sm['tile_group'],
+                       plan['seq_map'].ntiles, demb, E, sm['rows'][1], m_rows=plan['seq_M'])
+                m._pending_sparse.append(('emb.seq_item', plan['seq_ids'], demb))
+        elif not acc:
+            m.g('tok.seq.kernel').zero_(); m.g('tok.seq.bias').zero_()
+        if plan['n_sep'] > 0:
+            K.rows_colsum(dx0, d, plan['sep_rows'], plan['n_sep'], d, m.g('tok.sep'), accumulate=acc, device=dev)
+        elif not acc:
+            m.g('tok.sep').zero_()
+        return None, None, None
+
+
+class _Block(torch.autograd.Function):
+    """OneTransBlock.call (model.py:186-200) for the last K of I tokens (pyramid / last-layer DCE).
+    x: [B*I, d] -> [B*K, d]."""
+
+    @staticmethod
+    def forward(ctx, flat, x, m, l, I, Kq, seed, training):
+        cfg = m.config
+        d, f, H = cfg.hidden_dim, cfg.ffn_dim, cfg.num_heads
+        hd = d // H
+        B = x.shape[0] // I
+        dev = x.device
+        maps = m.maps(B, I, Kq)
+        ma, mt = maps['all'].to(dev), maps['tail'].to(dev)
+        na, nt = maps['all'].ntiles, maps['tail'].ntiles
+        rate = cfg.dropout_rate if training else 0.0
+        dflag = OT_EPI_DROPOUT if rate > 0 else 0
+        wqkv, wo = m.p(f'blk.{l}.wqkv'), m.p(f'blk.{l}.wo')
+        w1, b1, w2, b2 = m.p(f'blk.{l}.w1'), m.p(f'blk.{l}.b1'), m.p(f'blk.{l}.w2'), m.p(f'blk.{l}.b2')
+        g1, g2 = m.p(f'blk.{l}.norm1'), m.p(f'blk.{l}.norm2')
+        # norm1 -> rstd only; the QKV GEMM applies it in its A prologue
+        rstd1 = torch.empty(B * I, device=dev)
+        K.rmsnorm_fwd(x, d, B * I, d, rstd1, eps=RMS_EPS)
+        qkv = torch.empty(B * I, 3 * d, device=dev)
+        if Kq == I:
+            K.gemm(OT_GEMM_NN, x, d, d, ma['rows'][0], wqkv, 3 * d * d, 3 * d, 3 * d, ma['tile_group'], na, qkv,
+                   3 * d, ma['rows'][0], a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=maps['all'].nrows)
+        else:
+            K.gemm(OT_GEMM_NN, x, d, d, ma['rows'][0], (wqkv, d), 3 * d * d, 3 * d, 2 * d, ma['tile_group'], na,
+                   (qkv, d), 3 * d, ma['rows'][0], a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=maps['all'].nrows)
+            K.gemm(OT_GEMM_NN, x, d, d, mt['rows'][0], wqkv, 3 * d * d, 3 * d, d, mt['tile_group'], nt, qkv,
+                   3 * d, mt['rows'][0], a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=maps['tail'].nrows)
+        o = torch.empty(B * Kq, d, device=dev)
+        lse = torch.empty(B * H * Kq, device=dev)
+        K.attn_fwd(qkv, 3 * d, B, H, I, Kq, hd, o, lse)
+        # x1 = x[tail] + drop(o @ Wo)      (model.py:117, 193)
+        x1 = torch.empty(B * Kq, d, device=dev)
+        K.gemm(OT_GEMM_NN, o, d, d, mt['rows'][1], wo, 0, d, d, mt['tile_group'], nt, x1, d, mt['rows'][1],
+               epi=OT_EPI_RESIDUAL | dflag, res=x, ldres=d, res_tok=1, seed=seed, site=2 * l, drop=rate,
+               tail=(Kq, I), m_rows=maps['tail'].nrows)
+        rstd2 = torch.empty(B * Kq, device=dev)
+        K.rmsnorm_fwd(x1, d, B * Kq, d, rstd2, eps=RMS_EPS)
+        # u = norm2(x1) @ W1[g] + b1[g]  (pre-activation; GELU applied by its consumers)
+        u = torch.empty(B * Kq, f, device=dev)
+        K.gemm(OT_GEMM_NN, x1, d, d, mt['rows'][1], w1, d * f, f, f, mt['tile_group'], nt, u, f, mt['rows'][1],
+               a_xform=OT_AX_RMSNORM, rstd=rstd2, gamma=g2, bias=b1, bias_gstride=f, epi=OT_EPI_BIAS, m_rows=maps['tail'].nrows)
+        # x2 = x1 + drop(gelu(u) @ W2[g] + b2[g])     (model.py:154-161, 198)
+        x2 = torch.empty(B * Kq, d, device=dev)
+        K.gemm(OT_GEMM_NN, u, f, f, mt['rows'][1], w2, f * d, d, d, mt['tile_group'], nt, x2, d, mt['rows'][1],
+               a_xform=OT_AX_GELU, bias=b2, bias_gstride=d, epi=OT_EPI_BIAS | OT_EPI_RESIDUAL | dflag, res=x1,
+               ldres=d, res_tok=0, seed=seed, site=2 * l + 1, drop=rate, tail=(Kq, I), m_rows=maps['tail'].nrows)
+        ctx.save_for_backward(x, rstd1, qkv, o, lse, x1, rstd2, u)
+        ctx.m, ctx.l, ctx.I, ctx.Kq, ctx.seed, ctx.rate = m, l, I, Kq, seed, rate
+        return x2
+
+    @staticmethod
+    def backward(ctx, dx2):
+        x, rstd1, qkv, o, lse, x1, rstd2, u = ctx.saved_tensors
+        m, l, I, Kq, seed, rate = ctx.m, ctx.l, ctx.I, ctx.Kq, ctx.seed, ctx.rate
+        cfg = m.config
+        d, f, H = cfg.hidden_dim, cfg.ffn_dim, cfg.num_heads
+        hd = d // H
+        B = x.shape[0] // I
+        dev = x.device
+        acc = m.accumulate_grads
+        maps = m.maps(B, I, Kq)
+        ma, mt = maps['all'].to(dev), maps['tail'].to(dev)
+        na, nt = maps['all'].ntiles, maps['tail'].ntiles
+        nca, nct = maps['all'].chunks.shape[0], maps['tail'].chunks.shape[0]
+        G = cfg.num_groups
+        dx2 = dx2.contiguous()
+        # FFN branch: dY2 = mask(dx2)
+        if rate > 0:
+            dy2 = torch.empty_like(dx2)
+            K.dropout_apply(dx2, d, dy2, d, B * Kq, d, seed, 2 * l + 1, rate, (Kq, I))
+        else:
+            dy2 = dx2
+        K.wgrad(u, f, mt['rows'][1], dy2, d, mt['rows'][1], f, d, mt, nct, G, m.g(f'blk.{l}.w2'), f * d,
+                m.g(f'blk.{l}.b2'), d, a_xform=OT_AX_GELU, accumulate=acc, device=dev, m_rows=maps['tail'].nrows)
+        du = torch.empty(B * Kq, f, device=dev)
+        K.gemm(OT_GEMM_NT, dy2, d, d, mt['rows'][1], m.p(f'blk.{l}.w2'), f * d, d, f, mt['tile_group'], nt, du, f,
+               mt['rows'][1], epi=OT_EPI_GELU_BWD, aux=u, ldaux=f, m_rows=maps['tail'].nrows)
+        K.wgrad(x1, d, mt['rows'][1], du, f, mt['rows'][1], d, f, mt, nct, G, m.g(f'blk.{l}.w1'), d * f,
+                m.g(f'blk.{l}.b1'), f, a_xform=OT_AX_RMSNORM, rstd=rstd2, gamma=m.p(f'blk.{l}.norm2'),
+                accumulate=acc, device=dev, m_rows=maps['tail'].nrows)
+        dxn2 = torch.empty(B * Kq, d, device=dev)
+        K.gemm(OT_GEMM_NT, du, f, f, mt['rows'][1], m.p(f'blk.{l}.w1'), d * f, f, d, mt['tile_group'], nt, dxn2, d,
+               mt['rows'][1], m_rows=maps['tail'].nrows)
+        # norm2 backward + residual; emit mask(dx1) for the attention branch
+        dx1 = torch.empty(B * Kq, d, device=dev)
+        dyo = torch.empty(B * Kq, d, device=dev) if rate > 0 else dx1
+        K.rmsnorm_bwd(dxn2, d, x1, d, m.p(f'blk.{l}.norm2'), rstd2, dx1, d, B * Kq, d, dres=dx2, lddres=d,
+                      dx_masked=dyo if rate > 0 else None, lddxm=d, seed=seed, site=2 * l, drop=rate, tail=(Kq, I),
+                      dgamma=m.g(f'blk.{l}.norm2'), accumulate=acc, device=dev)
+        # Wo
+        _wgrad_single(m, o, dyo, d, d, mt, m.g(f'blk.{l}.wo'), acc, dev, maps['tail'].nrows)
+        do = torch.empty(B * Kq, d, device=dev)
+        K.gemm(OT_GEMM_NT, dyo, d, d, mt['rows'][1], m.p(f'blk.{l}.wo'), 0, d, d, mt['tile_group'], nt, do, d,
+               mt['rows'][1], m_rows=maps['tail'].nrows)
+        # attention
+        dqkv = torch.empty(B * I, 3 * d, device=dev)
+        if Kq < I:
+            dqkv[:, :d].zero_()
+        K.attn_bwd(qkv, 3 * d, o, do, lse, B, H, I, Kq, hd, dqkv)
+        K.wgrad(x, d, ma['rows'][0], dqkv, 3 * d, ma['rows'][0], d, 3 * d, ma, nca, G, m.g(f'blk.{l}.wqkv'),
+                3 * d * d, None, 0, a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=m.p(f'blk.{l}.norm1'), accumulate=acc,
+                device=dev, m_rows=maps['all'].nrows)
+        dxn1 = torch.empty(B * I, d, device=dev)
+        K.gemm(OT_GEMM_NT, dqkv, 3 * d, 3 * d, ma['rows'][0], m.p(f'blk.{l}.wqkv'), 3 * d * d, 3 * d, d,
+               ma['tile_group'], na, dxn1, d, ma['rows'][0], m_rows=maps['all'].nrows)
+        dx = torch.empty(B * I, d, device=dev)
+        K.rmsnorm_bwd(dxn1, d, x, d, m.p(f'blk.{l}.norm1'), rstd1, dx, d, B * I, d, dres=dx1, lddres=d,
+                      dres_tail=(Kq, I) if Kq < I else (0, 0), dgamma=m.g(f'blk.{l}.norm1'), accumulate=acc,
+                      device=dev)
+        return None, dx, None, None, None, None, None, None
+
+
+def _wgrad_single(m, A, D, K_, N, mt, dW, acc, dev, mrows=0):
+    """Wo gradient: one weight shared by every group -> wgrad with every chunk mapped to group 0."""
+    mp = m.single_group_chunks(mt)
+    K.wgrad(A, K_, mt['rows'][1], D, N, mt['rows'][1], K_, N, mp, mp['chunks'].shape[0], 1, dW, 0, None, 0,
+            accumulate=acc, device=dev, m_rows=mrows)
+
+
+class _Head(torch.autograd.Function):
+    """output_norm + task heads on the last token (model.py:384-391): x [B, d] -> probs [T, B]."""
+
+    @staticmethod
+    def forward(ctx, flat, x, m):
+        cfg = m.config
+        d, T = cfg.hidden_dim, len(cfg.tasks)
+        dh = d // 2
+        B = x.shape[0]
+        dev = x.device
+        y = torch.empty(B, d, device=dev)
+        rstd = torch.empty(B, device=dev)
+        K.rmsnorm_fwd(x, d, B, d, rstd, gamma=m.p('out_norm'), y=y, ldy=d, eps=RMS_EPS)
+        hm = m.head_rows(B)
+        hmd = hm.to(dev)
+        pre1 = torch.empty(T * B, dh, device=dev)
+        K.gemm(OT_GEMM_NN, y, d, d, hmd['rows'][0], m.p('head.w1'), d * dh, dh, dh, hmd['tile_group'], hm.ntiles,
+               pre1, dh, hmd['rows'][1], bias=m.p('head.b1'), bias_gstride=dh, epi=OT_EPI_BIAS, m_rows=hm.nrows)
+        logits = torch.empty(T, B, device=dev)
+        probs = torch.empty(T, B, device=dev)
+        K.head_fwd(pre1, m.p('head.w2'), m.p('head.b2'), T, B, dh, logits, probs)
+        ctx.save_for_backward(x, rstd, y, pre1, probs)
+        ctx.m = m
+        m._last_logits = logits
+        return probs
+
+    @staticmethod
+    def backward(ctx, dprobs):
+        x, rstd, y, pre1, probs = ctx.saved_tensors
+        m = ctx.m
+        cfg = m.config
+        d, T = cfg.hidden_dim, len(cfg.tasks)
+        dh = d // 2
+        B = x.shape[0]
+        dev = x.device
+        acc = m.accumulate_grads
+        dprobs = dprobs.contiguous()
+        dpre1 = torch.empty(T * B, dh, device=dev)
+        K.head_bwd(pre1, m.p('head.w2'), probs, dprobs, T, B, dh, dpre1, m.g('head.w2'), m.g('head.b2'), dh, 1,
+                   accumulate=acc, device=dev)
+        hm = m.head_rows(B)
+        hmd = hm.to(dev)
+        K.wgrad(y, d, hmd['rows'][0], dpre1, dh, hmd['rows'][1], d, dh, hmd, hm.chunks.shape[0], T, m.g('head.w1'),
+                d * dh, m.g('head.b1'), dh, accumulate=acc, device=dev, m_rows=hm.nrows)
+        im = m.ident_rows(B).to(dev)
+        nti = m.ident_rows(B).ntiles
+        dy = torch.empty(B, d, device=dev)
+        for t in range(T):
+            K.gemm(OT_GEMM_NT, (dpre1, t * B * dh), dh, dh, im['rows'][0], (m.p('head.w1'), t * d * dh), 0, dh, d,
+                   im['tile_group'], nti, dy, d, im['rows'][0], epi=OT_EPI_ACCUMULATE if t > 0 else 0, m_rows=B)
+        dx = torch.empty(B, d, device=dev)
+        K.rmsnorm_bwd(dy, d, x, d, m.p('out_norm'), rstd, dx, d, B, d, dgamma=m.g('out_norm'), accumulate=acc,
+                      device=dev)
+        return None, dx, None
+
+
+class _BCE(torch.autograd.Function):
+    """Σ_task tf.keras.losses.BinaryCrossentropy (train.py:84-87, 124-128) on probs [T, B]."""
+
+    @staticmethod
+    def forward(ctx, probs, labels):
+        T, B = probs.shape
+        loss = torch.empty(1, device=probs.device)
+        K.bce_fwd(probs, labels, T, B, loss, device=probs.device)
+        ctx.save_for_backward(probs, labels)
+        return loss[0]
+
+    @staticmethod
+    def backward(ctx, gl):
+        probs, labels = ctx.saved_tensors
+        T, B = probs.shape
+        dprobs = torch.empty_like(probs)
+        gl = gl.reshape(1).contiguous().float()
+        K.bce_bwd(probs, labels, gl, T, B, dprobs)
+        return dprobs, None
+
+
+def keras_bce_loss(labels: torch.Tensor, probs: torch.Tensor) -> torch.Tensor:
+    """Sum over tasks of the Keras BCE; labels/probs [T, B] device tensors."""
+    return _BCE.apply(probs, labels)
+
+
+# =============================================================================== the module
+class OneTransModel(nn.Module):
+    """model.py:305-408 on MI355X (see module docstring)."""
+
+    def __init__(self, config: OneTransConfig, device=None, seed: int = 0, init: Optional[Dict] = None):
+        super().__init__()
+        _lib.load()
+        if not torch.cuda.is_available():
+            raise _lib.OneTransHipError('OneTransModel needs a ROCm GPU (no CPU fallback)')
+        self.config = config
+        self.device = torch.device(device) if device is not None else torch.device('cuda', torch.cuda.current_device())
+        cfg = config
+        if cfg.hidden_dim % cfg.num_heads or (cfg.hidden_dim // cfg.num_heads) not in (16, 32, 64, 128):
+            raise ValueError('head_dim must be 16, 32, 64 or 128')
+        self.f_ns = cfg.ns_input_width()
+        self.layout = FlatLayout(cfg, self.f_ns)
+        self.cfg_Lnsd = cfg.num_ns_tokens * cfg.hidden_dim
+        self.flat = nn.Parameter(torch.zeros(self.layout.total, device=self.device))
+        self.flat.grad = torch.zeros_like(self.flat)
+        self.tables: Dict[str, torch.Tensor] = {}
+        self.accumulate_grads = False
+        self.kv_cache = None                      # model.py:333 (reference attribute; never populated)
+        self._pending_sparse: List = []
+        self._plans: Dict = {}
+        self._maps: Dict = {}
+        self._aux_maps: Dict = {}
+        self._step = 0
+        self.dropout_seed = 0x5EED0000 ^ seed
+        params = init if init is not None else init_params(cfg, self.f_ns, seed=seed, with_tables=False)
+        self.load_param_dict(params)
+        if init is None or not any(k.startswith('emb.') for k in init):
+            self._init_tables_device(seed + 1)
+
+    # ---------------------------------------------------------------- parameter access
+    def p(self, name):
+        return self.layout.view(self.flat.data, name)
+
+    def g(self, name):
+        return self.layout.view(self.flat.grad, name)
+
+    def load_param_dict(self, params: Dict[str, np.ndarray]) -> None:
+        """Load host arrays (params.init_params layout; tok.ns.kernel may be unpadded)."""
+        with torch.no_grad():
+            for name, arr in params.items():
+                if name.startswith('emb.'):
+                    self.tables[name] = torch.as_tensor(np.asarray(arr), dtype=torch.float32).to(self.device).contiguous()
+                    continue
+                dst = self.p(name)
+                src = torch.as_tensor(np.asarray(arr), dtype=torch.float32)
+                if name == 'tok.ns.kernel' and src.shape[0] != dst.shape[0]:
+                    dst.zero_()
+                    dst[:src.shape[0]].copy_(src)
+                else:
+                    dst.copy_(src.reshape(dst.shape))
+
+    def param_dict(self) -> Dict[str, np.ndarray]:
+        out = {}
+        for name in self.layout.shapes:
+            v = self.p(name).detach().cpu().numpy().copy()
+            if name == 'tok.ns.kernel':
+                v = v[:self.f_ns]
+            out[name] = v
+        for k, t in self.tables.items():
+            out[k] = t.detach().cpu().numpy().copy()
+        return out
+
+    def _init_tables_device(self, seed: int) -> None:
+        cfg = self.config
+        gen = torch.Generator(device=self.device)
+        gen.manual_seed(seed)
+        if cfg.sparse_features:
+            total = ns_table_offsets(cfg)['__total__']
+            t = torch.empty(total, cfg.ns_embedding_dim, device=self.device)
+            t.uniform_(-0.05, 0.05, generator=gen)
+            self.tables['emb.ns'] = t
+        if cfg.seq_item_vocab:
+            t = torch.empty(cfg.seq_item_vocab, cfg.seq_feature_dim, device=self.device)
+            t.uniform_(-0.05, 0.05, generator=gen)
+            self.tables['emb.seq_item'] = t
+
+    @property
+    def trainable_variables(self):
+        """train.py:131 — the dense parameters (one flat buffer) plus the embedding tables."""
+        return [self.flat] + list(self.tables.values())
+
+    # ---------------------------------------------------------------- row maps (cached)
+    def maps(self, B, I, Kq):
+        key = (B, I, Kq)
+        if key not in self._maps:
+            self._maps[key] = layer_maps(self.config, B, I, Kq)
+        return self._maps[key]
+
+    def head_rows(self, B):
+        key = ('head', B)
+        if key not in self._aux_maps:
+            self._aux_maps[key] = head_map(B, len(self.config.tasks))
+        return self._aux_maps[key]
+
+    def ident_rows(self, B):
+        key = ('ident', B)
+        if key not in self._aux_maps:
+            self._aux_maps[key] = identity_map(B)
+        return self._aux_maps[key]
+
+    def single_group_chunks(self, mt_dev):
+        """Chunks of a row map re-labelled as one group (Wo is shared by every position)."""
+        key = ('single', mt_dev['chunks'].data_ptr())
+        if key not in self._aux_maps:
+            ch = mt_dev['chunks'].clone()
+            ch[:, 0] = 0
+            g = torch.tensor([[0, ch.shape[0]]], dtype=torch.int32, device=ch.device)
+            self._aux_maps[key] = {'chunks': ch, 'gchunk': g}
+        return self._aux_maps[key]
+
+    # ---------------------------------------------------------------- input plan
+    def _plan(self, ns: Dict[str, torch.Tensor], seq: Dict[str, torch.Tensor]):
+        cfg = self.config
+        d = cfg.hidden_dim
+        dev = self.device
+        B = next(iter(ns.values())).shape[0] if ns else next(iter(seq.values())).shape[0]
+        seq_names = cfg.feature_config['sequence_features']
+        present = [(i, n, int(seq[n].shape[1])) for i, n in enumerate(seq_names) if n in seq]
+        ns_present = tuple(n for n in cfg.ns_feature_names() if n in ns)
+        id_seq = bool(cfg.seq_item_vocab) and bool(present) and not torch.is_floating_point(seq[present[0][1]])
+        key = (B, tuple(present), ns_present, id_seq)
+        plan = self._plans.get(key)
+        if plan is None:
+            plan = self._build_plan(B, present, ns_present, id_seq)
+            self._plans[key] = plan
+        # ---- per-call data (copies into the plan's persistent buffers; no host sync)
+        plan['gen'] += 1
+        if plan['ns_fields'] > 0:
+            if plan['n_dense'] > 0:
+                plan['dense_buf'].copy_(torch.cat([ns[n].reshape(B, 1).to(dev, torch.float32)
+                                                   for n in plan['dense_names']], 1))
+            if plan['n_sparse'] > 0:
+                plan['ids_buf'].copy_(torch.cat([ns[n].reshape(B, 1).to(dev, torch.int64)
+                                                 for n in plan['sparse_names']], 1))
+        if plan['seq_map'] is not None:
+            if id_seq:
+                ids = [seq[n].to(dev, torch.int64).contiguous() for (_, n, _) in present]
+                for (i, n, L), t, off in zip(present, ids, plan['seq_seg_off']):
+                    K.seq_rows(t, L, B, L, cfg.seq_item_vocab, (plan['seq_in'], off))
+                plan['seq_ids'] = torch.cat([t.reshape(-1) for t in ids])
+                plan['seq_A'] = self.tables['emb.seq_item']
+            else:
+                buf = plan['seq_buf']
+                o = 0
+                for (i, n, L) in present:
+                    buf[o:o + B * L].copy_(seq[n].reshape(B * L, -1).to(dev, torch.float32))
+                    o += B * L
+                plan['seq_A'] = buf
+                plan['seq_ids'] = None
+        return plan
+
+    def _build_plan(self, B, present, ns_present, id_seq):
+        cfg = self.config
+        d = cfg.hidden_dim
+        dev = self.device
+        nseq_cfg = len(cfg.feature_config['sequence_features'])
+        plan = {'B': B, 'gen': 0}
+        # ---- sequence token positions (model.py:259-277)
+        pos = 0
+        seq_groups, sep_pos = [], []
+        for (i, n, L) in present:
+            seq_groups.append((i, pos, L))
+            pos += L
+            if i < nseq_cfg - 1:
+                sep_pos.append(pos)
+                pos += 1
+        L_S = pos
+        L0 = L_S + cfg.num_ns_tokens
+        plan.update(L_S=L_S, L0=L0, nseq=nseq_cfg)
+        b = np.arange(B)
+        if sep_pos:
+            sep_rows = (b[:, None] * L0 + np.array(sep_pos)[None, :]).reshape(-1).astype(np.int32)
+            plan['sep_rows'] = torch.from_numpy(sep_rows).to(dev)
+        else:
+            plan['sep_rows'] = None
+        plan['n_sep'] = B * len(sep_pos)
+        # ---- sequence projection GEMM maps: group = sequence index in the config
+        if present:
+            per_group = [[np.zeros(0, np.int64), np.zeros(0, np.int64), np.zeros(0, np.int64)]
+                         for _ in range(nseq_cfg)]
+            cmp_off = 0
+            flat_off = 0
+            for (i, p0, L) in seq_groups:
+                m_ = np.arange(B * L)
+                bb, pp = m_ // L, m_ % L
+                per_group[i] = [bb * L0 + p0 + pp, cmp_off + m_, flat_off + m_]
+                cmp_off += B * L
+                flat_off += B * L
+            rm = build_map(per_group)
+            # rows[0]: x0 rows; rows[1]: compact rows (embedding-gradient output); rows[2]: float input rows
+            plan['seq_map'] = rm
+            plan['seq_M'] = cmp_off
+            # segment offsets of each present sequence inside the padded map (for ot_seq_rows)
+            offs = []
+            starts = np.concatenate([[0], np.cumsum([round_up(len(pg[0]), TILE) for pg in per_group])])
+            for (i, p0, L) in seq_groups:
+                offs.append(int(starts[i]))
+            plan['seq_seg_off'] = offs
+            seq_in = torch.from_numpy(rm.rows[2].copy()).to(dev)
+            plan['seq_in'] = seq_in
+            if not id_seq:
+                plan['seq_buf'] = torch.empty(cmp_off, cfg.seq_feature_dim, device=dev)
+        else:
+            plan['seq_map'] = None
+        # ---- NS fields (model.py:243-253)
+        offs = ns_table_offsets(cfg)
+        dense_names = [n for n in ns_present if n not in cfg.sparse_features]
+        sparse_names = [n for n in ns_present if n in cfg.sparse_features]
+        plan.update(dense_names=dense_names, sparse_names=sparse_names, n_dense=len(dense_names),
+                    n_sparse=len(sparse_names), ns_fields=len(ns_present))
+        plan['nsmat'] = torch.zeros(B, self.layout.f_pad, device=dev)
+        if ns_present:
+            plan['dense_buf'] = torch.zeros(B, max(1, len(dense_names)), device=dev)
+            plan['ids_buf'] = torch.zeros(B, max(1, len(sparse_names)), dtype=torch.int64, device=dev)
+            # descriptors: sparse fields first (ot_ns_grad_pack packs the first n_sparse)
+            col = {}
+            c = 0
+            for n in ns_present:
+                col[n] = c
+                c += cfg.ns_embedding_dim if n in cfg.sparse_features else 1
+            recs = np.zeros(len(ns_present), dtype=np.dtype([('dense', '<u8'), ('ids', '<u8'), ('row_offset', '<i8'),
+                                                             ('stride', '<i8'), ('col', '<i4'), ('width', '<i4')]))
+            assert recs.dtype.itemsize == NS_FIELD_BYTES
+            k = 0
+            for j, n in enumerate(sparse_names):
+                recs[k] = (0, plan['ids_buf'].data_ptr() + 8 * j, offs[n], len(sparse_names), col[n],
+                           cfg.ns_embedding_dim)
+                k += 1
+            for j, n in enumerate(dense_names):
+                recs[k] = (plan['dense_buf'].data_ptr() + 4 * j, 0, 0, len(dense_names), col[n], 1)
+                k += 1
+            plan['ns_desc'] = torch.from_numpy(recs.view(np.uint8).copy()).to(dev)
+            plan['ns_map'] = identity_map(B)
+        return plan
+
+    # ---------------------------------------------------------------- forward
+    def forward(self, non_seq_features, seq_features=None, training: bool = False,
+                use_kv_cache: bool = False):
+        """model.py:335-393.  Returns {task: probs [B, 1]} (sigmoid outputs, like the Keras heads).
+        ``training`` defaults to False exactly like the reference signature (model.py:337), independent
+        of nn.Module.train()/eval().  ``use_kv_cache`` is accepted for signature compatibility; the
+        reference's cache path is defective (D6) and a full forward is computed."""
+        if seq_features is None and isinstance(non_seq_features, (tuple, list)) and len(non_seq_features) == 2:
+            non_seq_features, seq_features = non_seq_features           # D4: callers pass one tuple
+        seq_features = seq_features or {}
+        training = bool(training)
+        probs = self.forward_probs(non_seq_features, seq_features, training)
+        return {t: probs[i].view(-1, 1) for i, t in enumerate(self.config.tasks)}
+
+    def forward_probs(self, ns, seq, training: bool) -> torch.Tensor:
+        """All tasks as one [T, B] tensor (the trainer's fused loss consumes it)."""
+        plan = self._plan(ns, seq)
+        seed = 0
+        if training:
+            self._step += 1
+            seed = (self.dropout_seed + 0x9E3779B9 * self._step) & 0xFFFFFFFF
+        x = _Tokenize.apply(self.flat, self, plan)
+        sched = self.config.pyramid_schedule(plan['L0'])
+        nl = len(sched)
+        for l, s in enumerate(sched):
+            Kq = s['keep'] if l < nl - 1 else 1
+            x = _Block.apply(self.flat, x, self, l, s['in_len'], Kq, seed, training)
+        return _Head.apply(self.flat, x, self)
+
+    # ---------------------------------------------------------------- reference API
+    def reset_kv_cache(self):
+        """model.py:395-397."""
+        self.kv_cache = None
+
+    def get_model_info(self) -> Dict:
+        """model.py:399-408 (count of the reference's trainable weights; embedding tables of the
+        build extension reported separately)."""
+        n = int(sum(r * c for (_, r, c, _) in self.layout.segments))
+        return {'total_parameters': n, 'num_layers': self.config.num_layers,
+                'hidden_dim': self.config.hidden_dim, 'num_heads': self.config.num_heads,
+                'embedding_rows': {k: int(v.shape[0]) for k, v in self.tables.items()}}
+
+    def save_weights(self, path: str) -> None:
+        """Counterpart of model.save_weights (train.py:286): one .npz of named banks."""
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        np.savez(path, **self.param_dict())
+
+    def load_weights(self, path: str) -> None:
+        """Counterpart of model.load_weights (train.py:332)."""
+        with np.load(path, allow_pickle=False) as z:
+            self.load_param_dict({k: z[k] for k in z.files})
+
+
+def create_onetrans_model(model_type: str = 'default', device=None) -> OneTransModel:
+    """model.py:411-416."""
+    return OneTransModel(get_model_config(model_type), device=device)

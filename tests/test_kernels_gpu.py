@@ -1,0 +1,266 @@
+"""Per-kernel numerics on the GPU: each HIP kernel (through the C ABI) vs a plain torch fp64
+reference of the same op on the same inputs."""
+
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from recommend_amd import kernels as K
+from recommend_amd._lib import (OT_AX_GELU, OT_AX_NONE, OT_AX_RMSNORM, OT_EPI_ACCUMULATE, OT_EPI_BIAS,
+                                OT_EPI_DROPOUT, OT_EPI_GELU, OT_EPI_GELU_BWD, OT_EPI_RESIDUAL, OT_GEMM_NN, OT_GEMM_NT)
+from recommend_amd.layout import build_map
+from oracle import keras_math as km
+
+TOL = dict(rtol=2e-5, atol=2e-5)
+
+
+def gelu64(x):
+    return 0.5 * x * (1.0 + torch.erf(x / math.sqrt(2.0)))
+
+
+def gelu_grad64(x):
+    return 0.5 * (1.0 + torch.erf(x / math.sqrt(2.0))) + x * torch.exp(-0.5 * x * x) / math.sqrt(2 * math.pi)
+
+
+def _random_map(rng, n_in, n_out, G, counts):
+    per = []
+    src = rng.permutation(n_in)
+    dst = rng.permutation(n_out)
+    o = 0
+    for g in range(G):
+        c = counts[g]
+        per.append([src[o:o + c], dst[o:o + c]])
+        o += c
+    return build_map(per)
+
+
+@pytest.mark.parametrize('mode', [OT_GEMM_NN, OT_GEMM_NT])
+@pytest.mark.parametrize('K_,N', [(64, 192), (128, 384), (512, 128), (432, 100)])
+def test_mixed_gemm_plain(dev, mode, K_, N):
+    if mode == OT_GEMM_NN and N % 4:
+        pytest.skip('NN needs N % 4 == 0')
+    rng = np.random.default_rng(0)
+    G, M = 3, 700
+    counts = [400, 37, 263]
+    A = torch.randn(M, K_, dtype=torch.float64)
+    W = torch.randn(G, K_, N, dtype=torch.float64) if mode == OT_GEMM_NN else torch.randn(G, N, K_, dtype=torch.float64)
+    rm = _random_map(rng, M, M, G, counts)
+    d = rm.to(dev)
+    C = torch.full((M, N), float('nan'), device=dev)
+    Ad, Wd = A.float().to(dev), W.float().to(dev)
+    K.gemm(mode, Ad, K_, K_, d['rows'][0], Wd, W[0].numel(), N if mode == OT_GEMM_NN else K_, N, d['tile_group'],
+           rm.ntiles, C, N, d['rows'][1])
+    ref = torch.empty(M, N, dtype=torch.float64)
+    for t in range(rm.ntiles):
+        g = rm.tile_group[t]
+        r_in = rm.rows[0][t * 128:(t + 1) * 128]
+        r_out = rm.rows[1][t * 128:(t + 1) * 128]
+        ok = r_in >= 0
+        Wg = W[g] if mode == OT_GEMM_NN else W[g].T
+        ref[torch.from_numpy(r_out[ok]).long()] = A[torch.from_numpy(r_in[ok]).long()] @ Wg
+    torch.testing.assert_close(C.double().cpu(), ref, rtol=1e-4, atol=1e-4 * math.sqrt(K_))
+
+
+def test_mixed_gemm_prologue_epilogue(dev):
+    """rmsnorm / gelu prologues, bias + dropout + residual (token-mapped) + accumulate epilogues."""
+    rng = np.random.default_rng(1)
+    B, I, Kq, d, N = 9, 20, 7, 64, 64
+    G = 2
+    M = B * Kq
+    x = torch.randn(B * I, d, dtype=torch.float64)
+    gamma = 1 + 0.1 * torch.randn(d, dtype=torch.float64)
+    rstd = 1.0 / torch.sqrt((x * x).mean(1) + 1e-6)
+    W = torch.randn(G, d, N, dtype=torch.float64) * 0.2
+    bias = torch.randn(G, N, dtype=torch.float64)
+    res = torch.randn(B * I, N, dtype=torch.float64)
+    # rows: compact tail rows r = b*K + j read token rows b*I + (I-K) + j
+    r = np.arange(M)
+    tok = (r // Kq) * I + (I - Kq) + r % Kq
+    grp = (r % 2)
+    rm = build_map([[tok[grp == g], r[grp == g]] for g in range(G)])
+    dd = rm.to(dev)
+    C = torch.zeros(M, N, device=dev)
+    rate, seed, site = 0.25, 1234, 5
+    K.gemm(OT_GEMM_NN, x.float().to(dev), d, d, dd['rows'][0], W.float().to(dev), d * N, N, N, dd['tile_group'],
+           rm.ntiles, C, N, dd['rows'][1], a_xform=OT_AX_RMSNORM, rstd=rstd.float().to(dev),
+           gamma=gamma.float().to(dev), bias=bias.float().to(dev), bias_gstride=N,
+           epi=OT_EPI_BIAS | OT_EPI_DROPOUT | OT_EPI_RESIDUAL, res=res.float().to(dev), ldres=N, res_tok=1,
+           seed=seed, site=site, drop=rate, tail=(Kq, I))
+    xn = x * rstd[:, None] * gamma
+    ref = torch.empty(M, N, dtype=torch.float64)
+    for g in range(G):
+        sel = torch.from_numpy(np.nonzero(grp == g)[0])
+        ref[sel] = xn[torch.from_numpy(tok)[sel]] @ W[g] + bias[g]
+    idx = (tok[:, None].astype(np.uint64) * np.uint64(N) + np.arange(N, dtype=np.uint64)[None])
+    keep = torch.from_numpy(km.dropout_keep(seed, site, idx, rate).astype(np.float64))
+    ref = ref * keep / (1 - rate) + res[torch.from_numpy(tok)]
+    torch.testing.assert_close(C.double().cpu(), ref, rtol=1e-4, atol=1e-4)
+    # gelu prologue + gelu-bwd epilogue + accumulate
+    f = 64
+    u = torch.randn(M, f, dtype=torch.float64)
+    W2 = torch.randn(G, f, N, dtype=torch.float64) * 0.1
+    aux = torch.randn(M, N, dtype=torch.float64)
+    rm2 = build_map([[r[grp == g], r[grp == g]] for g in range(G)])
+    d2 = rm2.to(dev)
+    C0 = torch.randn(M, N, dtype=torch.float64)
+    C2 = C0.float().to(dev)
+    K.gemm(OT_GEMM_NN, u.float().to(dev), f, f, d2['rows'][0], W2.float().to(dev), f * N, N, N, d2['tile_group'],
+           rm2.ntiles, C2, N, d2['rows'][1], a_xform=OT_AX_GELU, epi=OT_EPI_GELU_BWD | OT_EPI_ACCUMULATE,
+           aux=aux.float().to(dev), ldaux=N)
+    ref2 = torch.empty(M, N, dtype=torch.float64)
+    for g in range(G):
+        sel = torch.from_numpy(np.nonzero(grp == g)[0])
+        ref2[sel] = gelu64(u[sel]) @ W2[g]
+    ref2 = ref2 * gelu_grad64(aux) + C0
+    torch.testing.assert_close(C2.double().cpu(), ref2, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize('xf', [OT_AX_NONE, OT_AX_RMSNORM, OT_AX_GELU])
+def test_wgrad(dev, xf):
+    rng = np.random.default_rng(2)
+    G, M, K_, N = 3, 1500, 128, 192
+    counts = [1000, 300, 200]
+    A = torch.randn(M, K_, dtype=torch.float64)
+    D = torch.randn(M, N, dtype=torch.float64)
+    gamma = 1 + 0.1 * torch.randn(K_, dtype=torch.float64)
+    rstd = 1.0 / torch.sqrt((A * A).mean(1) + 1e-6)
+    per = []
+    src = rng.permutation(M)
+    o = 0
+    for g in range(G):
+        per.append([src[o:o + counts[g]], src[o:o + counts[g]]])
+        o += counts[g]
+    rm = build_map(per, chunk_rows=256)
+    dd = rm.to(dev)
+    dW = torch.full((G, K_, N), float('nan'), device=dev)
+    db = torch.full((G, N), float('nan'), device=dev)
+    K.wgrad(A.float().to(dev), K_, dd['rows'][0], D.float().to(dev), N, dd['rows'][1], K_, N, dd,
+            rm.chunks.shape[0], G, dW, K_ * N, db, N, a_xform=xf, rstd=rstd.float().to(dev),
+            gamma=gamma.float().to(dev), device=dev)
+    Ax = A * rstd[:, None] * gamma if xf == OT_AX_RMSNORM else (gelu64(A) if xf == OT_AX_GELU else A)
+    for g in range(G):
+        rows = torch.from_numpy(per[g][0]).long()
+        torch.testing.assert_close(dW[g].double().cpu(), Ax[rows].T @ D[rows], rtol=1e-4, atol=1e-3)
+        torch.testing.assert_close(db[g].double().cpu(), D[rows].sum(0), rtol=1e-4, atol=1e-3)
+
+
+def attn_ref(qkv, B, H, I, Kq, hd):
+    d = H * hd
+    q = qkv[:, :d].reshape(B, I, H, hd)[:, I - Kq:]
+    k = qkv[:, d:2 * d].reshape(B, I, H, hd)
+    v = qkv[:, 2 * d:].reshape(B, I, H, hd)
+    s = torch.einsum('bqhd,bkhd->bhqk', q, k) / math.sqrt(hd)
+    qpos = torch.arange(I - Kq, I)[:, None]
+    kpos = torch.arange(I)[None]
+    s = torch.where(kpos <= qpos, s, torch.tensor(-1e9, dtype=s.dtype))
+    return torch.einsum('bhqk,bkhd->bqhd', torch.softmax(s, -1), v).reshape(B * Kq, d)
+
+
+@pytest.mark.parametrize('B,H,I,Kq,hd', [(3, 4, 140, 140, 32), (2, 4, 140, 1, 32), (2, 2, 70, 33, 64),
+                                         (3, 4, 40, 40, 16), (1, 2, 33, 17, 128), (2, 4, 5, 5, 32)])
+def test_attention(dev, B, H, I, Kq, hd):
+    torch.manual_seed(0)
+    d = H * hd
+    qkv = torch.randn(B * I, 3 * d, dtype=torch.float64)
+    qkv_d = qkv.float().to(dev)
+    out = torch.empty(B * Kq, d, device=dev)
+    lse = torch.empty(B * H * Kq, device=dev)
+    K.attn_fwd(qkv_d, 3 * d, B, H, I, Kq, hd, out, lse)
+    qkv_r = qkv.clone().requires_grad_(True)
+    ref = attn_ref(qkv_r, B, H, I, Kq, hd)
+    torch.testing.assert_close(out.double().cpu(), ref.detach(), rtol=1e-4, atol=1e-5)
+    dout = torch.randn(B * Kq, d, dtype=torch.float64)
+    ref.backward(dout)
+    dqkv = torch.full((B * I, 3 * d), float('nan'), device=dev)
+    if Kq < I:
+        dqkv[:, :d].zero_()
+    K.attn_bwd(qkv_d, 3 * d, out, dout.float().to(dev), lse, B, H, I, Kq, hd, dqkv)
+    torch.testing.assert_close(dqkv.double().cpu(), qkv_r.grad, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize('d', [64, 128, 256, 512])
+def test_rmsnorm(dev, d):
+    torch.manual_seed(1)
+    rows, Kq, I = 600, 5, 12
+    x = torch.randn(rows, d, dtype=torch.float64)
+    gamma = 1 + 0.1 * torch.randn(d, dtype=torch.float64)
+    rstd = torch.empty(rows, device=dev)
+    y = torch.empty(rows, d, device=dev)
+    K.rmsnorm_fwd(x.float().to(dev), d, rows, d, rstd, gamma=gamma.float().to(dev), y=y, ldy=d)
+    xr = x.clone().requires_grad_(True)
+    gr = gamma.clone().requires_grad_(True)
+    yr = xr * torch.rsqrt((xr * xr).mean(1, keepdim=True) + 1e-6) * gr
+    torch.testing.assert_close(y.double().cpu(), yr.detach(), **TOL)
+    dy = torch.randn(rows, d, dtype=torch.float64)
+    yr.backward(dy)
+    # residual grad given only for the tail rows (rows are [B=50, I=12]; tail K=5)
+    B = rows // I
+    dres_c = torch.randn(B * Kq, d, dtype=torch.float64)
+    dres_full = torch.zeros(rows, d, dtype=torch.float64)
+    for b in range(B):
+        dres_full[b * I + I - Kq:b * I + I] = dres_c[b * Kq:(b + 1) * Kq]
+    dx = torch.empty(rows, d, device=dev)
+    dxm = torch.empty(rows, d, device=dev)
+    dg = torch.empty(d, device=dev)
+    K.rmsnorm_bwd(dy.float().to(dev), d, x.float().to(dev), d, gamma.float().to(dev), rstd, dx, d, rows, d,
+                  dres=dres_c.float().to(dev), lddres=d, dres_tail=(Kq, I), dx_masked=dxm, lddxm=d, seed=7,
+                  site=3, drop=0.3, tail=(1, 1), dgamma=dg, device=dev)
+    ref_dx = xr.grad + dres_full
+    torch.testing.assert_close(dx.double().cpu(), ref_dx, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(dg.double().cpu(), gr.grad, rtol=1e-4, atol=1e-3)
+    idx = np.arange(rows * d, dtype=np.uint64).reshape(rows, d)
+    keep = torch.from_numpy(km.dropout_keep(7, 3, idx, 0.3).astype(np.float64))
+    torch.testing.assert_close(dxm.double().cpu(), ref_dx * keep / 0.7, rtol=1e-4, atol=1e-4)
+
+
+def test_sparse_adagrad(dev):
+    rng = np.random.default_rng(3)
+    rows, E, n = 1000, 16, 5000
+    table = rng.uniform(-0.05, 0.05, (rows, E))
+    acc = np.full((rows, E), 0.1)
+    keys = (rng.zipf(1.2, n) - 1) % rows
+    grads = rng.normal(size=(n, E))
+    lr, eps, clip = 0.1, 1e-7, 3.0
+    uk = np.unique(keys)
+    gsum = np.zeros((rows, E))
+    np.add.at(gsum, keys, grads)
+    g = gsum[uk]
+    g = g * clip / max(np.sqrt((g * g).sum()), clip)
+    w_ref, a_ref = km.adagrad_sparse_update(table, acc, uk, g, lr, eps)
+    t_d = torch.tensor(table, dtype=torch.float32, device=dev)
+    a_d = torch.tensor(acc, dtype=torch.float32, device=dev)
+    K.sparse_adagrad(t_d, a_d, E, rows, torch.from_numpy(keys).to(dev), torch.tensor(grads, dtype=torch.float32,
+                     device=dev), n, lr, eps, clip, device=dev)
+    np.testing.assert_allclose(t_d.cpu().numpy(), w_ref, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(a_d.cpu().numpy(), a_ref, rtol=1e-5, atol=1e-5)
+
+
+def test_clip_rmsprop(dev):
+    rng = np.random.default_rng(4)
+    total = 5000
+    w = rng.normal(size=total)
+    g = rng.normal(size=total) * 10
+    v = np.abs(rng.normal(size=total)) * 0.01
+    m = rng.normal(size=total) * 0.01
+    segs = np.array([[0, 10, 30, 60], [30, 10, 30, 60], [600, 1, 4000, 4000], [4600, 20, 20, 20]], np.int64)
+    lr, rho, eps, mom, clip = 0.005, 0.9, 1e-7, 0.99999, 50.0
+    gc = g.copy()
+    for (o, r, c, s) in segs:
+        idx = (o + np.arange(r)[:, None] * s + np.arange(c)[None]).reshape(-1)
+        gc[idx] = km.clip_by_norm(g[idx], clip)
+    covered = np.zeros(total, bool)
+    for (o, r, c, s) in segs:
+        covered[(o + np.arange(r)[:, None] * s + np.arange(c)[None]).reshape(-1)] = True
+    w2, v2, m2 = km.rmsprop_update(w, gc, v, m, lr, rho, eps, mom)
+    w2 = np.where(covered, w2, w); v2 = np.where(covered, v2, v); m2 = np.where(covered, m2, m)
+    T = lambda a: torch.tensor(a, dtype=torch.float32, device=dev)
+    wd, gd, vd, md = T(w), T(g), T(v), T(m)
+    K.clip_rmsprop(wd, gd, vd, md, torch.from_numpy(segs.reshape(-1)).to(dev), len(segs), 4000, lr, rho, eps, mom,
+                   clip, device=dev)
+    np.testing.assert_allclose(wd.cpu().numpy(), w2, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(vd.cpu().numpy(), v2, rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(md.cpu().numpy(), m2, rtol=1e-5, atol=1e-7)

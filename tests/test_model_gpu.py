@@ -1,0 +1,152 @@
+"""End-to-end parity of the HIP path vs the CPU oracle (oracle/onetrans_ref.py, float64):
+logits/probs, every parameter gradient, the optimizer update, and AUC — on identical weights and
+batches.  Tolerance (BASELINE.json north_star): logits within 1e-3; we check far tighter (2e-4)."""
+
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from recommend_amd.config import workload_config
+from recommend_amd.data import make_batch
+from recommend_amd.metrics import auc
+from recommend_amd.model import OneTransModel, keras_bce_loss
+from recommend_amd.params import init_params, keras_variables
+from recommend_amd.trainer import OneTransTrainer, stack_labels
+from oracle import onetrans_ref as R
+
+LOGIT_TOL = 2e-4
+
+
+def small_criteo(dedicated='head', pyramid=False, layers=2, d=64, H=4, f=128, Lns=4, seq_lens=(5, 9, 7)):
+    cfg = workload_config('C2')
+    cfg.hidden_dim, cfg.num_heads, cfg.ffn_dim, cfg.num_layers, cfg.num_ns_tokens = d, H, f, layers, Lns
+    cfg.sparse_features = {k: 40 + 7 * i for i, k in enumerate(cfg.sparse_features)}
+    cfg.seq_item_vocab = 300
+    cfg._seq_lens = list(seq_lens)
+    cfg.dedicated_positions = dedicated
+    cfg.pyramid_enabled = pyramid
+    cfg.pyramid_ratios = [0.5, 0.25, 0.2]
+    return cfg
+
+
+def c1(dedicated='head'):
+    cfg = workload_config('C1')
+    cfg.dedicated_positions = dedicated
+    return cfg
+
+
+CASES = {
+    'c1_head': lambda: c1('head'),
+    'c1_tail': lambda: c1('tail'),
+    'criteo_head': lambda: small_criteo('head'),
+    'criteo_tail_pyramid': lambda: small_criteo('tail', pyramid=True, layers=3),
+    'criteo_d128_hd32': lambda: small_criteo('head', d=128, H=4, f=256, Lns=12, seq_lens=(20, 20, 20)),
+}
+
+
+def setup(cfg, B, dev, seed=0):
+    P = init_params(cfg, cfg.ns_input_width(), seed=seed, perturb=True)
+    model = OneTransModel(cfg, device=dev, init=P)
+    batch = make_batch(B, cfg, seed=1000)
+    return P, model, batch
+
+
+def oracle_out(P, cfg, batch, training=False, seed=0):
+    ns, seq, lab = batch
+    return R.forward(R.to_torch(P), cfg, R.to_torch(ns), R.to_torch(seq), training=training, seed=seed)
+
+
+@pytest.mark.parametrize('case', list(CASES))
+def test_forward_parity(dev, case):
+    cfg = CASES[case]()
+    B = 37 if case.startswith('criteo') else 64
+    P, model, batch = setup(cfg, B, dev)
+    ns, seq, _ = batch
+    with torch.no_grad():
+        out = model((ns_t(ns, dev), ns_t(seq, dev)), training=False)
+    ref = oracle_out(P, cfg, batch)
+    for t in cfg.tasks:
+        lg = model._last_logits[cfg.tasks.index(t)].double().cpu().numpy()
+        np.testing.assert_allclose(lg, ref['logits'][t].numpy()[:, 0], atol=LOGIT_TOL, rtol=0)
+        np.testing.assert_allclose(out[t].double().cpu().numpy(), ref['probs'][t].numpy(), atol=LOGIT_TOL / 4, rtol=0)
+
+
+def ns_t(d, dev):
+    return {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in d.items()}
+
+
+@pytest.mark.parametrize('case', ['c1_head', 'criteo_head', 'criteo_tail_pyramid'])
+@pytest.mark.parametrize('training', [False, True])
+def test_gradient_parity(dev, case, training):
+    cfg = CASES[case]()
+    B = 37 if case.startswith('criteo') else 64
+    P, model, batch = setup(cfg, B, dev)
+    ns, seq, lab = batch
+    seed = 0
+    model.flat.grad.fill_(float('nan'))
+    probs = model.forward_probs(ns_t(ns, dev), ns_t(seq, dev), training=training)
+    if training:
+        seed = (model.dropout_seed + 0x9E3779B9 * model._step) & 0xFFFFFFFF
+    y = stack_labels(lab, cfg.tasks, dev)
+    loss = keras_bce_loss(y, probs)
+    loss.backward()
+    rl, rg, rout = R.loss_and_grads(R.to_torch(P), cfg, R.to_torch(ns), R.to_torch(seq), R.to_torch(lab),
+                                    training=training, seed=seed)
+    assert abs(loss.item() - rl.item()) < 1e-4
+    for name in model.layout.shapes:
+        g = model.g(name).double().cpu()
+        r = rg[name]
+        if name == 'tok.ns.kernel':
+            assert torch.all(g[r.shape[0]:] == 0)
+            g = g[:r.shape[0]]
+        scale = max(1e-3, r.abs().max().item())
+        err = (g.reshape(r.shape) - r).abs().max().item() / scale
+        assert err < 2e-4, f'{name}: rel err {err:.2e}'
+    # sparse table gradients (de-duplicated) vs the oracle's dense table gradient
+    for (tname, keys, grads) in model._pending_sparse:
+        dense = torch.zeros(rg[tname].shape, dtype=torch.float64)
+        dense.index_add_(0, keys.cpu(), grads.double().cpu())
+        scale = max(1e-3, rg[tname].abs().max().item())
+        assert (dense - rg[tname]).abs().max().item() / scale < 2e-4, tname
+
+
+@pytest.mark.parametrize('case', ['c1_head', 'criteo_head'])
+def test_train_steps_parity(dev, case):
+    cfg = CASES[case]()
+    cfg.optimizer_config = dict(cfg.optimizer_config, dense_lr=0.001, momentum=0.9)
+    B = 37 if case.startswith('criteo') else 64
+    P, model, _ = setup(cfg, B, dev)
+    tr = OneTransTrainer(cfg, model=model)
+    Pt = R.to_torch(P)
+    st = R.init_state(Pt, cfg)
+    kv = keras_variables(cfg, {k: v.shape for k, v in P.items() if not k.startswith('emb.')})
+    for step in range(3):
+        batch = make_batch(B, cfg, seed=2000 + step)
+        out = tr.train_step(batch)
+        seed = (model.dropout_seed + 0x9E3779B9 * model._step) & 0xFFFFFFFF
+        ns, seq, lab = batch
+        Pt, st, rl, _ = R.train_step(Pt, st, cfg, kv, R.to_torch(ns), R.to_torch(seq), R.to_torch(lab), seed=seed)
+        assert abs(out['total_loss'].item() - rl.item()) < 2e-4, step
+    got = model.param_dict()
+    for name, ref in Pt.items():
+        r = ref.detach().numpy()
+        err = np.abs(got[name] - r).max()
+        assert err < 2e-4, f'{name} after 3 steps: {err:.2e}'
+
+
+def test_auc_parity(dev):
+    """AUC of the HIP path's predictions == AUC of the oracle's on the same batch (|dAUC| < 1e-3)."""
+    cfg = small_criteo('head')
+    P, model, batch = setup(cfg, 512, dev)
+    ns, seq, lab = batch
+    with torch.no_grad():
+        out = model((ns_t(ns, dev), ns_t(seq, dev)))
+    ref = oracle_out(P, cfg, batch)
+    for t in cfg.tasks:
+        a = auc(lab[t], out[t].cpu().numpy())
+        b = auc(lab[t], ref['probs'][t].numpy())
+        assert abs(a - b) < 1e-3, (t, a, b)

@@ -149,23 +149,26 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs p) {
   }
 }
 
-// delta[b,h,j] = sum_d dO[b*K+j][h*hd+d] * O[b*K+j][h*hd+d]   (one thread per (row, head))
-__global__ void attn_bwd_prep_kernel(const float* __restrict__ o, const float* __restrict__ dout, float* delta,
-                                     int B, int H, int K, int hd) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // (b*K + j)*H + h
-  if (i >= (int64_t)B * K * H) return;
-  const int h = (int)(i % H);
-  const int64_t row = i / H;
-  const int64_t b = row / K, j = row % K;
-  const float* a = o + row * H * hd + h * hd;
-  const float* c = dout + row * H * hd + h * hd;
+// delta[b,h,j] = sum_d dO[b*K+j][h*hd+d] * O[b*K+j][h*hd+d]: one float4 per thread (coalesced rows),
+// reduced over the hd/4 lanes of a head with shuffles.
+__global__ __launch_bounds__(256) void attn_bwd_prep_kernel(const float* __restrict__ o, const float* __restrict__ dout,
+                                                            float* delta, int B, int H, int K, int hd) {
+  const int d = H * hd;
+  const int64_t i4 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;   // element index in [B*K, d]
+  const bool live = i4 < (int64_t)B * K * d;
   float s = 0.f;
-  for (int q = 0; q < hd; q += 4) {
-    f32x4 x = *reinterpret_cast<const f32x4*>(a + q);
-    f32x4 y = *reinterpret_cast<const f32x4*>(c + q);
-    s += x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
+  if (live) {
+    f32x4 x = *reinterpret_cast<const f32x4*>(o + i4);
+    f32x4 y = *reinterpret_cast<const f32x4*>(dout + i4);
+    s = x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
   }
-  delta[(b * H + h) * K + j] = s;
+  for (int off = (hd >> 3); off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  const int c = (int)(i4 % d);
+  if (live && (c % hd) == 0) {
+    const int64_t row = i4 / d;
+    const int64_t b = row / K, j = row % K;
+    delta[(b * H + c / hd) * K + j] = s;
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -329,7 +332,7 @@ extern "C" int ot_attn_bwd(const float* qkv, int64_t ld, const float* out, const
   if (B == 0) return OT_OK;
   AttnArgs p{qkv, ld, H * head_dim, out, dout, nullptr, const_cast<float*>(lse), dqkv, delta_ws, B, H, I, K,
              1.f / sqrtf((float)head_dim)};
-  hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3(ceil_div((int64_t)B * K * H, 256)), dim3(256), 0,
+  hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3(ceil_div((int64_t)B * K * H * head_dim / 4, 256)), dim3(256), 0,
                      (hipStream_t)stream, out, dout, delta_ws, B, H, K, head_dim);
   OT_LAUNCH_CHECK("ot_attn_bwd(prep)");
   const unsigned grid = ceil_div((int64_t)B * H, 4);

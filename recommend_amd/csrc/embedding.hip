@@ -43,11 +43,47 @@ __global__ void seg_start_kernel(const int32_t* __restrict__ flags, const int32_
   }
 }
 
-// TPS threads per segment, float4 each (E = 4*TPS*k)
-__global__ __launch_bounds__(256) void seg_sum_kernel(const float* __restrict__ grads, int E,
+// Hot keys (Zipf) can own tens of thousands of rows: every segment is cut into pieces of at most
+// PIECE rows; pass 1 sums each piece, pass 2 sums each key's pieces in order (both deterministic).
+constexpr int PIECE = 64;
+
+__global__ void piece_count_kernel(const int32_t* __restrict__ seg_start, const int32_t* __restrict__ nuniq,
+                                   int64_t n, int32_t* pcount) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s > n) return;
+  const int U = nuniq[0];
+  pcount[s] = s < U ? (seg_start[s + 1] - seg_start[s] + PIECE - 1) / PIECE : 0;
+}
+
+// TPS threads per piece / segment, float4 each (E = 4*TPS*k)
+__global__ __launch_bounds__(256) void piece_sum_kernel(const float* __restrict__ grads, int E,
+                                                        const int32_t* __restrict__ perm,
+                                                        const int32_t* __restrict__ seg_start,
+                                                        const int32_t* __restrict__ pstart,
+                                                        const int32_t* __restrict__ nuniq, int tps, float* psum) {
+  const int ppb = 256 / tps;
+  const int64_t pc = (int64_t)blockIdx.x * ppb + threadIdx.x / tps;
+  const int lt = threadIdx.x % tps;
+  const int U = nuniq[0];
+  if (pc >= pstart[U]) return;
+  int lo = 0, hi = U - 1;                         // largest s with pstart[s] <= pc
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (pstart[mid] <= pc) lo = mid; else hi = mid - 1;
+  }
+  const int i0 = seg_start[lo] + (int)(pc - pstart[lo]) * PIECE;
+  const int i1 = min(i0 + PIECE, seg_start[lo + 1]);
+  for (int c = lt * 4; c < E; c += tps * 4) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int i = i0; i < i1; ++i) acc += *reinterpret_cast<const f32x4*>(grads + (int64_t)perm[i] * E + c);
+    *reinterpret_cast<f32x4*>(psum + pc * E + c) = acc;
+  }
+}
+
+__global__ __launch_bounds__(256) void seg_sum_kernel(const float* __restrict__ psum, int E,
                                                       const uint32_t* __restrict__ ksorted,
-                                                      const int32_t* __restrict__ perm,
                                                       const int32_t* __restrict__ seg_start,
+                                                      const int32_t* __restrict__ pstart,
                                                       const int32_t* __restrict__ nuniq, int tps, float* gsum,
                                                       float* sq_part) {
   __shared__ float red[4];
@@ -56,10 +92,10 @@ __global__ __launch_bounds__(256) void seg_sum_kernel(const float* __restrict__ 
   const int lt = threadIdx.x % tps;
   float sq = 0.f;
   if (s < nuniq[0] && ksorted[seg_start[s]] != 0xFFFFFFFFu) {
-    const int b = seg_start[s], e = seg_start[s + 1];
+    const int b = pstart[s], e = pstart[s + 1];
     for (int c = lt * 4; c < E; c += tps * 4) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      for (int i = b; i < e; ++i) acc += *reinterpret_cast<const f32x4*>(grads + (int64_t)perm[i] * E + c);
+      for (int q = b; q < e; ++q) acc += *reinterpret_cast<const f32x4*>(psum + (int64_t)q * E + c);
       *reinterpret_cast<f32x4*>(gsum + s * E + c) = acc;
       sq += acc.x * acc.x + acc.y * acc.y + acc.z * acc.z + acc.w * acc.w;
     }
@@ -115,8 +151,8 @@ __global__ __launch_bounds__(256) void adagrad_apply_kernel(float* table, float*
 
 struct SparseWs {
   uint32_t *k_in, *k_out;
-  int32_t *v_in, *v_out, *flags, *pos, *seg_start, *nuniq;
-  float *gsum, *sq_part, *scale;
+  int32_t *v_in, *v_out, *flags, *pos, *seg_start, *nuniq, *pcount, *pstart;
+  float *gsum, *psum, *sq_part, *scale;
   void* tmp;
   size_t tmp_bytes;
   size_t total;
@@ -136,7 +172,11 @@ SparseWs carve(void* base, int64_t n, int E) {
                                   (int32_t*)nullptr, (size_t)n, 0, 32);
   (void)rocprim::inclusive_scan(nullptr, scan_bytes, (int32_t*)nullptr, (int32_t*)nullptr, (size_t)n,
                                 rocprim::plus<int32_t>());
+  size_t escan_bytes = 0;
+  (void)rocprim::exclusive_scan(nullptr, escan_bytes, (int32_t*)nullptr, (int32_t*)nullptr, 0, (size_t)n + 1,
+                                rocprim::plus<int32_t>());
   w.tmp_bytes = sort_bytes > scan_bytes ? sort_bytes : scan_bytes;
+  w.tmp_bytes = w.tmp_bytes > escan_bytes ? w.tmp_bytes : escan_bytes;
   const int spb = 256 / tps_for(E);
   const int64_t nblk = (n + spb - 1) / spb;
   char* p = (char*)base;
@@ -146,7 +186,9 @@ SparseWs carve(void* base, int64_t n, int E) {
   w.v_in = (int32_t*)take(n * 4); w.v_out = (int32_t*)take(n * 4);
   w.flags = (int32_t*)take(n * 4); w.pos = (int32_t*)take(n * 4);
   w.seg_start = (int32_t*)take((n + 1) * 4); w.nuniq = (int32_t*)take(4);
-  w.gsum = (float*)take((size_t)n * E * 4); w.sq_part = (float*)take(nblk * 4); w.scale = (float*)take(4);
+  w.pcount = (int32_t*)take((n + 1) * 4); w.pstart = (int32_t*)take((n + 1) * 4);
+  w.gsum = (float*)take((size_t)n * E * 4); w.psum = (float*)take((size_t)(n + n / PIECE + 1) * E * 4);
+  w.sq_part = (float*)take(nblk * 4); w.scale = (float*)take(4);
   w.tmp = take(w.tmp_bytes);
   w.total = off;
   return w;
@@ -189,8 +231,18 @@ extern "C" int ot_sparse_adagrad(float* table, float* accum, int E, int64_t num_
   hipLaunchKernelGGL(seg_start_kernel, dim3(g1), dim3(256), 0, s, w.flags, w.pos, n, w.seg_start, w.nuniq);
   OT_LAUNCH_CHECK("ot_sparse_adagrad(segments)");
   const int tps = tps_for(E);
+  hipLaunchKernelGGL(piece_count_kernel, dim3(ceil_div(n + 1, 256)), dim3(256), 0, s, w.seg_start, w.nuniq, n,
+                     w.pcount);
+  OT_LAUNCH_CHECK("ot_sparse_adagrad(pieces)");
+  tb = w.tmp_bytes;
+  e = rocprim::exclusive_scan(w.tmp, tb, w.pcount, w.pstart, 0, (size_t)n + 1, rocprim::plus<int32_t>(), s);
+  if (e != hipSuccess) return fail(OT_ERR_HIP, "ot_sparse_adagrad(piece scan): %s", hipGetErrorString(e));
+  const unsigned gp = ceil_div(n + n / PIECE + 1, 256 / tps);
+  hipLaunchKernelGGL(piece_sum_kernel, dim3(gp), dim3(256), 0, s, grads, E, w.v_out, w.seg_start, w.pstart, w.nuniq,
+                     tps, w.psum);
+  OT_LAUNCH_CHECK("ot_sparse_adagrad(piecesum)");
   const unsigned g2 = ceil_div(n, 256 / tps);
-  hipLaunchKernelGGL(seg_sum_kernel, dim3(g2), dim3(256), 0, s, grads, E, w.k_out, w.v_out, w.seg_start, w.nuniq,
+  hipLaunchKernelGGL(seg_sum_kernel, dim3(g2), dim3(256), 0, s, w.psum, E, w.k_out, w.seg_start, w.pstart, w.nuniq,
                      tps, w.gsum, w.sq_part);
   OT_LAUNCH_CHECK("ot_sparse_adagrad(segsum)");
   hipLaunchKernelGGL(clip_scale_kernel, dim3(1), dim3(256), 0, s, w.sq_part, (int)g2, clip, w.scale);

@@ -121,14 +121,22 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(RmsBwdArgs p) {
   }
 }
 
-// out[c] (+)= sum_{b < nparts} part[b][c]   (fixed order: deterministic)
-__global__ void colsum_reduce_kernel(const float* __restrict__ part, int64_t nparts, int ncols, float* out,
-                                     int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= ncols) return;
+// out[c] (+)= sum_{b < nparts} part[b][c]   (fixed order: deterministic).  Block = 64 columns x 4
+// row-groups; each wave reads 64 consecutive columns of a partial row (coalesced).
+__global__ __launch_bounds__(256) void colsum_reduce_kernel(const float* __restrict__ part, int64_t nparts, int ncols,
+                                                            float* out, int accumulate) {
+  __shared__ float red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rg = threadIdx.x >> 6;
   float s = 0.f;
-  for (int64_t b = 0; b < nparts; ++b) s += part[b * ncols + c];
-  out[c] = accumulate ? out[c] + s : s;
+  if (c < ncols)
+    for (int64_t b = rg; b < nparts; b += 4) s += part[b * ncols + c];
+  red[rg][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (threadIdx.x < 64 && c < ncols) {
+    const float t = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+    out[c] = accumulate ? out[c] + t : t;
+  }
 }
 
 // part[blk][c] = sum of rows [blk*RPB, (blk+1)*RPB) of the listed rows, column c
@@ -220,7 +228,7 @@ extern "C" int ot_rmsnorm_bwd(const float* dy, int64_t lddy, const float* x, int
   hipLaunchKernelGGL(rmsnorm_bwd_kernel, dim3(grid), dim3(256), shmem, (hipStream_t)stream, p);
   OT_LAUNCH_CHECK("ot_rmsnorm_bwd");
   if (dgamma) {
-    hipLaunchKernelGGL(colsum_reduce_kernel, dim3(ceil_div(d, 256)), dim3(256), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(colsum_reduce_kernel, dim3(ceil_div(d, 64)), dim3(256), 0, (hipStream_t)stream,
                        (const float*)workspace, (int64_t)grid, d, dgamma, accumulate_dgamma);
     OT_LAUNCH_CHECK("ot_rmsnorm_bwd(reduce)");
   }
@@ -253,7 +261,7 @@ extern "C" int ot_rows_colsum(const float* src, int64_t ld, const int32_t* rows,
                        src, ld, rows, nrows, ncols, 256, (float*)workspace);
     OT_LAUNCH_CHECK("ot_rows_colsum");
   }
-  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(ceil_div(ncols, 256)), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(ceil_div(ncols, 64)), dim3(256), 0, (hipStream_t)stream,
                      (const float*)workspace, (int64_t)nb, ncols, out, accumulate);
   OT_LAUNCH_CHECK("ot_rows_colsum(reduce)");
   return OT_OK;

@@ -87,6 +87,12 @@ int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a_rows, int 
                         float* dW, int64_t dw_gstride, float* db, int64_t db_gstride,
                         int accumulate, void* workspace, size_t ws_bytes, void* stream);
 
+/* Transposed weight shadow for the forward GEMMs (NT staging reads k-contiguous rows):
+ * dst[g][n][k] = src[g][k][n] per bank; banks_dev: [nbanks][6] int64 {src_off, dst_off, G, K, N,
+ * first_tile}, a bank owning G*ceil(K/32)*ceil(N/32) consecutive 32x32 tiles of the launch. */
+int ot_transpose_banks(const float* src, float* dst, const int64_t* banks_dev, int nbanks, int64_t total_tiles,
+                       void* stream);
+
 /* ---- causal attention with a query tail (attention.hip) ----------------------------------
  * Replaces model.py:100-114 (einsum QK^T/sqrt(hd), band_part mask with -1e9, softmax, einsum PV)
  * and the pyramid gather of queries model.py:356/371 (only the last K of I queries computed).

@@ -12,7 +12,7 @@ import os
 from ctypes import c_float, c_int, c_int64, c_size_t, c_uint32, c_void_p, c_char_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libonetrans_hip.so')
+LIB_PATH = os.environ.get('ONETRANS_HIP_LIB') or os.path.join(_HERE, 'libonetrans_hip.so')
 HEADER = os.path.join(os.path.dirname(_HERE), 'include', 'onetrans_hip.h')
 
 OT_GEMM_NN, OT_GEMM_NT = 0, 1
@@ -34,6 +34,7 @@ SIGNATURES = {
     'ot_wgrad_workspace_size': (c_size_t, [c_int, c_int, c_int]),
     'ot_mixed_gemm_wgrad': (c_int, [P, I64, P, c_int, P, P, P, I64, P, c_int, c_int, P, c_int, P, c_int, P,
                                     I64, P, I64, c_int, P, c_size_t, P]),
+    'ot_transpose_banks': (c_int, [P, P, P, c_int, I64, P]),
     'ot_attn_fwd': (c_int, [P, I64, c_int, c_int, c_int, c_int, c_int, P, P, P]),
     'ot_attn_bwd': (c_int, [P, I64, P, P, P, c_int, c_int, c_int, c_int, c_int, P, P, P]),
     'ot_rmsnorm_fwd': (c_int, [P, I64, P, P, I64, P, I64, c_int, c_float, P]),

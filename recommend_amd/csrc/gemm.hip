@@ -19,9 +19,15 @@
 
 namespace ot {
 
-constexpr int GT = 128;        // tile rows / cols
-constexpr int GBK = 32;        // k per LDS stage
-constexpr int GLD = GBK + 4;   // LDS row stride (floats)
+#ifndef OT_GEMM_BK
+#define OT_GEMM_BK 16
+#endif
+#ifndef OT_WGRAD_DBUF
+#define OT_WGRAD_DBUF 0
+#endif
+constexpr int GT = 128;           // tile rows / cols
+constexpr int GBK = OT_GEMM_BK;   // k per LDS stage (16 or 32)
+constexpr int GLD = GBK + 4;      // LDS row stride (floats)
 
 struct GemmArgs {
   const float* A; int64_t lda; int K;
@@ -55,11 +61,15 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
   return base + (b >> 3);
 }
 
-template <bool NT>
+// AXT / EPIT: compile-time prologue / epilogue (-1 = read p.a_xform / p.epi at run time).
+// EDGE: K % 32 != 0 or N % 128 != 0 (bounds checks in staging and epilogue).
+template <bool NT, int AXT, int EPIT, bool EDGE>
 __global__ __launch_bounds__(256, 2) void mixed_gemm_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* As = smem;                      // [2][GT][GLD]
   float* Bs = smem + 2 * GT * GLD;       // [2][GT][GLD]
+  const int ax = AXT >= 0 ? AXT : p.a_xform;
+  const int epi = EPIT >= 0 ? EPIT : p.epi;
 
   const int nwg = p.ntm * p.ntn;
   const int wg = xcd_remap(blockIdx.x, nwg);
@@ -71,48 +81,54 @@ __global__ __launch_bounds__(256, 2) void mixed_gemm_kernel(GemmArgs p) {
   const int h = lane >> 5, li = lane & 31;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
 
-  // ---- per-thread staging coordinates
-  // A / NT-B: row = (t>>3) + 32*i (i<4), float4 column c = t&7
-  const int sc = t & 7, sr = t >> 3;
-  int64_t a_off[4]; float a_rs[4]; bool a_ok[4];
+  // ---- staging coordinates: a row holds CPR float4 chunks; thread t stages chunk sc of rows
+  // sr + RPP*i (i < NPASS), for A and (NT) B
+  constexpr int CPR = GBK / 4, RPP = 256 / CPR, NPASS = GT / RPP;
+  const int sc = t % CPR, sr = t / CPR;
+  const float* arow[NPASS];
+  const float* brow[NPASS];
+  float ars[NPASS];
+  bool aok[NPASS], bok[NPASS];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    int r = sr + 32 * i;
-    int64_t gr = (int64_t)tm * GT + r;
-    int ir = p.in_rows ? p.in_rows[gr] : (int)gr;
-    a_ok[i] = ir >= 0;
-    a_off[i] = (int64_t)(ir < 0 ? 0 : ir) * p.lda;
-    a_rs[i] = (p.a_xform == OT_AX_RMSNORM && ir >= 0) ? p.a_rstd[ir] : 1.f;
+  for (int i = 0; i < NPASS; ++i) {
+    const int r = sr + RPP * i;
+    const int64_t gr = (int64_t)tm * GT + r;
+    const int ir = p.in_rows ? p.in_rows[gr] : (int)gr;
+    aok[i] = ir >= 0;
+    arow[i] = p.A + (int64_t)(ir < 0 ? 0 : ir) * p.lda + 4 * sc;
+    ars[i] = (ax == OT_AX_RMSNORM && ir >= 0) ? p.a_rstd[ir] : 1.f;
+    const int n = n0 + r;
+    bok[i] = !EDGE || n < p.N;
+    brow[i] = W + (int64_t)(bok[i] ? n : 0) * p.ldw + 4 * sc;
   }
-  // NN-B: kk = lane&31, n4 = 2*wave + (lane>>5) + 8*i (i<4)
-  f32x4 ra[4], rb[4];
+  f32x4 ra[NPASS], rb[NPASS];
+  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  // NN B staging: lane reads W[k0 + kk][n0 + 4*n4 ...], kk = lane % GBK
+  const int nn_kk = lane % GBK, nn_n4 = wave * (64 / GBK) + lane / GBK;
 
   auto load_stage = [&](int k0) {
+    const bool kin = !EDGE || (k0 + 4 * sc < p.K);
+    f32x4 gm = {1.f, 1.f, 1.f, 1.f};
+    if (ax == OT_AX_RMSNORM && kin) gm = *reinterpret_cast<const f32x4*>(p.a_gamma + k0 + 4 * sc);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int k = k0 + 4 * sc;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (a_ok[i] && k < p.K) {
-        v = *reinterpret_cast<const f32x4*>(p.A + a_off[i] + k);
-        v = apply_pro(v, p.a_xform, a_rs[i], p.a_gamma, k);
+    for (int i = 0; i < NPASS; ++i) {
+      f32x4 v = zero4;
+      if (aok[i] && kin) v = *reinterpret_cast<const f32x4*>(arow[i] + k0);
+      if (ax == OT_AX_RMSNORM) {
+        v = v * gm * ars[i];
+      } else if (ax == OT_AX_GELU) {
+        v.x = gelu_erf(v.x); v.y = gelu_erf(v.y); v.z = gelu_erf(v.z); v.w = gelu_erf(v.w);
       }
       ra[i] = v;
     }
     if (NT) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        int n = n0 + sr + 32 * i, k = k0 + 4 * sc;
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        if (n < p.N && k < p.K) v = *reinterpret_cast<const f32x4*>(W + (int64_t)n * p.ldw + k);
-        rb[i] = v;
-      }
+      for (int i = 0; i < NPASS; ++i) rb[i] = (bok[i] && kin) ? *reinterpret_cast<const f32x4*>(brow[i] + k0) : zero4;
     } else {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        int k = k0 + li, n = n0 + 4 * (2 * wave + h + 8 * i);
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        if (k < p.K && n < p.N) v = *reinterpret_cast<const f32x4*>(W + (int64_t)k * p.ldw + n);
-        rb[i] = v;
+      for (int i = 0; i < NPASS; ++i) {
+        const int k = k0 + nn_kk, n = n0 + 4 * (nn_n4 + (256 / GBK) * i);
+        rb[i] = ((!EDGE || (k < p.K && n < p.N))) ? *reinterpret_cast<const f32x4*>(W + (int64_t)k * p.ldw + n) : zero4;
       }
     }
   };
@@ -120,18 +136,18 @@ __global__ __launch_bounds__(256, 2) void mixed_gemm_kernel(GemmArgs p) {
     float* as = As + buf * GT * GLD;
     float* bs = Bs + buf * GT * GLD;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) *reinterpret_cast<f32x4*>(as + (sr + 32 * i) * GLD + 4 * sc) = ra[i];
+    for (int i = 0; i < NPASS; ++i) *reinterpret_cast<f32x4*>(as + (sr + RPP * i) * GLD + 4 * sc) = ra[i];
     if (NT) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) *reinterpret_cast<f32x4*>(bs + (sr + 32 * i) * GLD + 4 * sc) = rb[i];
+      for (int i = 0; i < NPASS; ++i) *reinterpret_cast<f32x4*>(bs + (sr + RPP * i) * GLD + 4 * sc) = rb[i];
     } else {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        int n = 4 * (2 * wave + h + 8 * i);
-        bs[(n + 0) * GLD + li] = rb[i].x;
-        bs[(n + 1) * GLD + li] = rb[i].y;
-        bs[(n + 2) * GLD + li] = rb[i].z;
-        bs[(n + 3) * GLD + li] = rb[i].w;
+      for (int i = 0; i < NPASS; ++i) {
+        const int n = 4 * (nn_n4 + (256 / GBK) * i);
+        bs[(n + 0) * GLD + nn_kk] = rb[i].x;
+        bs[(n + 1) * GLD + nn_kk] = rb[i].y;
+        bs[(n + 2) * GLD + nn_kk] = rb[i].z;
+        bs[(n + 3) * GLD + nn_kk] = rb[i].w;
       }
     }
   };
@@ -150,62 +166,96 @@ __global__ __launch_bounds__(256, 2) void mixed_gemm_kernel(GemmArgs p) {
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) load_stage((kt + 1) * GBK);
-    const float* as = As + cur * GT * GLD;
-    const float* bs = Bs + cur * GT * GLD;
+    const bool more = kt + 1 < nk;
+    if (more) load_stage((kt + 1) * GBK);
+    const float* as = As + cur * GT * GLD + (wm + li) * GLD + (GBK / 2) * h;
+    const float* bs = Bs + cur * GT * GLD + (wn + li) * GLD + (GBK / 2) * h;
 #pragma unroll
-    for (int half = 0; half < 2; ++half) {
+    for (int half = 0; half < GBK / 16; ++half) {
       f32x4 fa[2][2], fb[2][2];
 #pragma unroll
       for (int m = 0; m < 2; ++m)
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-          fa[m][q] = *reinterpret_cast<const f32x4*>(as + (wm + 32 * m + li) * GLD + 16 * h + 8 * half + 4 * q);
-          fb[m][q] = *reinterpret_cast<const f32x4*>(bs + (wn + 32 * m + li) * GLD + 16 * h + 8 * half + 4 * q);
+          fa[m][q] = *reinterpret_cast<const f32x4*>(as + 32 * m * GLD + 8 * half + 4 * q);
+          fb[m][q] = *reinterpret_cast<const f32x4*>(bs + 32 * m * GLD + 8 * half + 4 * q);
         }
 #pragma unroll
-      for (int s = 0; s < 8; ++s) {
+      for (int s = 0; s < 8; ++s)
 #pragma unroll
         for (int m = 0; m < 2; ++m)
 #pragma unroll
           for (int n = 0; n < 2; ++n)
             acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[m][s >> 2][s & 3], fb[n][s >> 2][s & 3],
                                                              acc[m][n], 0, 0, 0);
-      }
     }
-    if (kt + 1 < nk) {
-      __syncthreads();               // everyone finished reading buf cur^1 (previous iteration)
-      store_stage(cur ^ 1);
-      __syncthreads();
-    }
+    // the other buffer was last read in iteration kt-1, which every wave finished before the
+    // barrier that ended it: one barrier per k-tile
+    if (more) store_stage(cur ^ 1);
+    __syncthreads();
   }
 
-  // ---- epilogue
+  // ---- epilogue (flags compile-time unless EPIT < 0).  Per 32-row block m: resolve the 16 output
+  // rows of this lane, issue every operand load (aux / residual / accumulate source) for the block,
+  // then compute and store — no load-use chains per element.
+  float bias_v[2] = {0.f, 0.f};
+  int cols[2];
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    cols[n] = n0 + wn + 32 * n + li;
+    if ((epi & OT_EPI_BIAS) && (!EDGE || cols[n] < p.N)) bias_v[n] = p.bias[(int64_t)g * p.bias_gstride + cols[n]];
+  }
+  const bool need_tok = (epi & OT_EPI_DROPOUT) || ((epi & OT_EPI_RESIDUAL) && p.res_tok);
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
+    int orow[16];
+    int64_t tok[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int row = wm + 32 * m + (r & 3) + 8 * (r >> 2) + 4 * h;
       const int64_t gr = (int64_t)tm * GT + row;
-      const int orow = p.out_rows ? p.out_rows[gr] : (int)gr;
-      if (orow < 0) continue;
-      const int64_t tok = (p.epi & (OT_EPI_DROPOUT)) || p.res_tok ? tail_token(orow, p.tail_K, p.tail_I) : orow;
+      orow[r] = p.out_rows ? p.out_rows[gr] : (int)gr;
+      tok[r] = (need_tok && orow[r] >= 0) ? tail_token(orow[r], p.tail_K, p.tail_I) : orow[r];
+    }
+    float ld0[16][2];
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
 #pragma unroll
       for (int n = 0; n < 2; ++n) {
-        const int col = n0 + wn + 32 * n + li;
-        if (col >= p.N) continue;
+        float v = 0.f;
+        const bool ok = orow[r] >= 0 && (!EDGE || cols[n] < p.N);
+        if (ok) {
+          if (epi & OT_EPI_GELU_BWD) v = p.aux[(int64_t)orow[r] * p.ldaux + cols[n]];
+          else if (epi & OT_EPI_RESIDUAL) v = p.res[(p.res_tok ? tok[r] : (int64_t)orow[r]) * p.ldres + cols[n]];
+          else if (epi & OT_EPI_ACCUMULATE) v = p.C[(int64_t)orow[r] * p.ldc + cols[n]];
+        }
+        ld0[r][n] = v;
+      }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if (orow[r] < 0) continue;
+      float* crow = p.C + (int64_t)orow[r] * p.ldc;
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        const int col = cols[n];
+        if (EDGE && col >= p.N) continue;
         float v = acc[m][n][r];
-        if (p.epi & OT_EPI_BIAS) v += p.bias[(int64_t)g * p.bias_gstride + col];
-        if (p.epi & OT_EPI_GELU_BWD) v *= gelu_erf_grad(p.aux[(int64_t)orow * p.ldaux + col]);
-        if (p.epi & OT_EPI_GELU) v = gelu_erf(v);
-        if (p.epi & OT_EPI_DROPOUT) {
-          uint32_t idx = (uint32_t)(tok * p.drop_width + col);
+        if (epi & OT_EPI_BIAS) v += bias_v[n];
+        if (epi & OT_EPI_GELU_BWD) v *= gelu_erf_grad(ld0[r][n]);
+        if (epi & OT_EPI_GELU) v = gelu_erf(v);
+        if (epi & OT_EPI_DROPOUT) {
+          const uint32_t idx = (uint32_t)(tok[r] * p.drop_width + col);
           v = drop_keep(p.seed, p.site, idx, p.drop_thr) ? v * p.drop_scale : 0.f;
         }
-        if (p.epi & OT_EPI_RESIDUAL) v += p.res[(p.res_tok ? tok : (int64_t)orow) * p.ldres + col];
-        float* dst = p.C + (int64_t)orow * p.ldc + col;
-        if (p.epi & OT_EPI_ACCUMULATE) v += *dst;
-        *dst = v;
+        if (epi & OT_EPI_RESIDUAL) {
+          if (!(epi & OT_EPI_GELU_BWD)) v += ld0[r][n];
+          else v += p.res[(p.res_tok ? tok[r] : (int64_t)orow[r]) * p.ldres + col];
+        }
+        if (epi & OT_EPI_ACCUMULATE) {
+          if (!(epi & (OT_EPI_GELU_BWD | OT_EPI_RESIDUAL))) v += ld0[r][n];
+          else v += crow[col];
+        }
+        crow[col] = v;
       }
     }
   }
@@ -228,10 +278,11 @@ struct WgradArgs {
   int ntk, ntn;
 };
 
+template <int AXT>
 __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* As = smem;                 // [GT][WLD]  (k, r)
-  float* Ds = smem + GT * WLD;      // [GT][WLD]  (n, r)
+  // [2][GT][WLD] for A^T (k, r) then [2][GT][WLD] for D^T (n, r)
+  const int ax = AXT >= 0 ? AXT : p.a_xform;
   const int per_chunk = p.ntk * p.ntn;
   const int c = blockIdx.x / per_chunk;
   const int rem = blockIdx.x % per_chunk;
@@ -241,8 +292,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int h = lane >> 5, li = lane & 31;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
-  // staging: row r = t>>3 (0..31), float4 column sc = t&7 (+ 8*i, i<4) covering 128 columns
-  const int sr = t >> 3, sc = t & 7;
+  const int sr = t >> 3, sc = t & 7;       // staging: row sr of the stage, float4 columns sc + 8i
+  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
 
   f32x16 acc[2][2];
 #pragma unroll
@@ -254,43 +305,70 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
   float bsum = 0.f;
   const bool do_bias = p.bslab && tk == 0 && t < GT;
 
-  for (int rs = 0; rs < row_count; rs += WBR) {
-    // load A rows and D rows of this stage into registers
+  auto rows_of = [&](int rs, int& ar, int& dr) {
     const int lr = rs + sr;
-    int ar = -1, dr = -1;
+    ar = -1; dr = -1;
     if (lr < row_count) {
-      int64_t mi = (int64_t)row_begin + lr;
+      const int64_t mi = (int64_t)row_begin + lr;
       ar = p.a_rows ? p.a_rows[mi] : (int)mi;
       dr = p.d_rows ? p.d_rows[mi] : (int)mi;
     }
     if (ar < 0 || dr < 0) { ar = -1; dr = -1; }
-    float rsd = (p.a_xform == OT_AX_RMSNORM && ar >= 0) ? p.a_rstd[ar] : 1.f;
-    f32x4 va[4], vd[4];
+  };
+  f32x4 va[4], vd[4];
+  auto load_stage = [&](int ar, int dr) {
+    const float rsd = (ax == OT_AX_RMSNORM && ar >= 0) ? p.a_rstd[ar] : 1.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      int k = k0 + 4 * (sc + 8 * i), n = n0 + 4 * (sc + 8 * i);
-      f32x4 z = {0.f, 0.f, 0.f, 0.f};
-      va[i] = z; vd[i] = z;
+      const int k = k0 + 4 * (sc + 8 * i), n = n0 + 4 * (sc + 8 * i);
+      f32x4 a = zero4, dv = zero4;
       if (ar >= 0 && k < p.K) {
-        va[i] = *reinterpret_cast<const f32x4*>(p.A + (int64_t)ar * p.lda + k);
-        va[i] = apply_pro(va[i], p.a_xform, rsd, p.a_gamma, k);
+        a = *reinterpret_cast<const f32x4*>(p.A + (int64_t)ar * p.lda + k);
+        if (ax == OT_AX_RMSNORM) {
+          a = a * *reinterpret_cast<const f32x4*>(p.a_gamma + k) * rsd;
+        } else if (ax == OT_AX_GELU) {
+          a.x = gelu_erf(a.x); a.y = gelu_erf(a.y); a.z = gelu_erf(a.z); a.w = gelu_erf(a.w);
+        }
       }
-      if (dr >= 0 && n < p.N) vd[i] = *reinterpret_cast<const f32x4*>(p.D + (int64_t)dr * p.ldd + n);
+      if (dr >= 0 && n < p.N) dv = *reinterpret_cast<const f32x4*>(p.D + (int64_t)dr * p.ldd + n);
+      va[i] = a; vd[i] = dv;
     }
-    __syncthreads();   // previous stage fully consumed
+  };
+  constexpr int NBUF = OT_WGRAD_DBUF ? 2 : 1;
+  auto store_stage = [&](int buf) {
+    float* As = smem + buf * GT * WLD;
+    float* Ds = smem + (NBUF + buf) * GT * WLD;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      int kk = 4 * (sc + 8 * i);
+      const int kk = 4 * (sc + 8 * i);
       As[(kk + 0) * WLD + sr] = va[i].x; As[(kk + 1) * WLD + sr] = va[i].y;
       As[(kk + 2) * WLD + sr] = va[i].z; As[(kk + 3) * WLD + sr] = va[i].w;
       Ds[(kk + 0) * WLD + sr] = vd[i].x; Ds[(kk + 1) * WLD + sr] = vd[i].y;
       Ds[(kk + 2) * WLD + sr] = vd[i].z; Ds[(kk + 3) * WLD + sr] = vd[i].w;
     }
-    __syncthreads();
+  };
+
+  const int nst = (row_count + WBR - 1) / WBR;
+  int ar, dr, ar2 = -1, dr2 = -1;
+  rows_of(0, ar, dr);
+  if (nst > 1) rows_of(WBR, ar2, dr2);
+  load_stage(ar, dr);
+  store_stage(0);
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    const int cur = NBUF == 2 ? (st & 1) : 0;
+    const bool more = st + 1 < nst;
+    int ar3 = -1, dr3 = -1;
+    if (more) {
+      load_stage(ar2, dr2);                               // stage st+1 data
+      if (st + 2 < nst) rows_of((st + 2) * WBR, ar3, dr3);   // stage st+2 row indices
+    }
+    const float* As = smem + cur * GT * WLD;
+    const float* Ds = smem + (NBUF + cur) * GT * WLD;
     if (do_bias) {
 #pragma unroll
       for (int q = 0; q < WBR; q += 4) {
-        f32x4 v = *reinterpret_cast<const f32x4*>(Ds + t * WLD + q);
+        const f32x4 v = *reinterpret_cast<const f32x4*>(Ds + t * WLD + q);
         bsum += (v.x + v.y) + (v.z + v.w);
       }
     }
@@ -311,6 +389,15 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
         for (int n = 0; n < 2; ++n)
           acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[m][s >> 2][s & 3], fb[n][s >> 2][s & 3],
                                                            acc[m][n], 0, 0, 0);
+    if (NBUF == 2) {
+      if (more) store_stage(cur ^ 1);
+      __syncthreads();
+    } else {
+      __syncthreads();
+      if (more) store_stage(0);
+      __syncthreads();
+    }
+    ar2 = ar3; dr2 = dr3;
   }
   float* slab = p.slab + (int64_t)c * p.K * p.N;
 #pragma unroll
@@ -356,9 +443,50 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, const float*
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Transposed weight shadow: dst[g][n][k] = src[g][k][n] for each bank (32x32 LDS tiles).
+// banks: [nbanks][6] int64 {src_off, dst_off, G, K, N, first_tile}; tiles of a bank: G*ceil(K/32)*ceil(N/32)
+__global__ __launch_bounds__(256) void transpose_banks_kernel(const float* __restrict__ src, float* dst,
+                                                              const int64_t* __restrict__ banks, int nbanks) {
+  __shared__ float tile[32][33];
+  const int64_t tid = blockIdx.x;
+  int b = 0;
+  while (b + 1 < nbanks && banks[6 * (b + 1) + 5] <= tid) ++b;
+  const int64_t* bk = banks + 6 * b;
+  const int64_t G = bk[2], K = bk[3], N = bk[4];
+  const int64_t tk = (K + 31) / 32, tnn = (N + 31) / 32;
+  int64_t rem = tid - bk[5];
+  if (rem >= G * tk * tnn) return;
+  const int64_t g = rem / (tk * tnn);
+  rem %= tk * tnn;
+  const int64_t k0 = (rem / tnn) * 32, n0 = (rem % tnn) * 32;
+  const float* s = src + bk[0] + g * K * N;
+  float* d = dst + bk[1] + g * K * N;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8
+  for (int i = ty; i < 32; i += 8) {
+    const int64_t k = k0 + i, n = n0 + tx;
+    tile[i][tx] = (k < K && n < N) ? s[k * N + n] : 0.f;
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    const int64_t n = n0 + i, k = k0 + tx;
+    if (k < K && n < N) d[n * K + k] = tile[tx][i];
+  }
+}
+
 }  // namespace ot
 
 using namespace ot;
+
+extern "C" int ot_transpose_banks(const float* src, float* dst, const int64_t* banks_dev, int nbanks,
+                                  int64_t total_tiles, void* stream) {
+  OT_REQUIRE(src && dst && banks_dev && nbanks > 0, "ot_transpose_banks: bad args");
+  if (total_tiles == 0) return OT_OK;
+  hipLaunchKernelGGL(transpose_banks_kernel, dim3((unsigned)total_tiles), dim3(256), 0, (hipStream_t)stream, src, dst,
+                     banks_dev, nbanks);
+  OT_LAUNCH_CHECK("ot_transpose_banks");
+  return OT_OK;
+}
 
 extern "C" int ot_mixed_gemm(int mode, const float* A, int64_t lda, int K, const int32_t* in_rows,
                              int a_xform, const float* a_rstd, const float* a_gamma,
@@ -391,19 +519,40 @@ extern "C" int ot_mixed_gemm(int mode, const float* A, int64_t lda, int K, const
     p.drop_scale = 1.f / (1.f - drop_rate);
   }
   const size_t shmem = 4 * GT * GLD * sizeof(float);
-  static std::once_flag once;   // LDS > 64 KiB per workgroup (gfx950 has 160 KiB per CU)
-  std::call_once(once, [] {
-    constexpr int shmem = 4 * GT * GLD * sizeof(float);
-    (void)hipFuncSetAttribute((const void*)mixed_gemm_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, shmem);
-    (void)hipFuncSetAttribute((const void*)mixed_gemm_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, shmem);
-    (void)hipGetLastError();
-  });
+  const bool edge = (K % GBK) != 0 || (N % GT) != 0;
   const unsigned nwg = (unsigned)ntiles * p.ntn;
   hipStream_t s = (hipStream_t)stream;
-  if (mode == OT_GEMM_NN)
-    hipLaunchKernelGGL(mixed_gemm_kernel<false>, dim3(nwg), dim3(256), shmem, s, p);
-  else
-    hipLaunchKernelGGL(mixed_gemm_kernel<true>, dim3(nwg), dim3(256), shmem, s, p);
+  void (*kern)(GemmArgs) = nullptr;
+  const int e = epi, x = a_xform;
+#define OT_SPEC(NT_, AX_, EP_)                                                                  \
+  if (mode == (NT_ ? OT_GEMM_NT : OT_GEMM_NN) && x == AX_ && e == (EP_))                         \
+    kern = edge ? mixed_gemm_kernel<NT_, AX_, EP_, true> : mixed_gemm_kernel<NT_, AX_, EP_, false>;
+  OT_SPEC(true, OT_AX_RMSNORM, 0)
+  OT_SPEC(true, OT_AX_RMSNORM, OT_EPI_BIAS)
+  OT_SPEC(true, OT_AX_GELU, OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_DROPOUT)
+  OT_SPEC(true, OT_AX_GELU, OT_EPI_BIAS | OT_EPI_RESIDUAL)
+  OT_SPEC(true, OT_AX_NONE, OT_EPI_RESIDUAL | OT_EPI_DROPOUT)
+  OT_SPEC(true, OT_AX_NONE, OT_EPI_RESIDUAL)
+  OT_SPEC(true, OT_AX_NONE, OT_EPI_BIAS)
+  OT_SPEC(true, OT_AX_NONE, OT_EPI_GELU_BWD)
+  OT_SPEC(true, OT_AX_NONE, 0)
+  OT_SPEC(true, OT_AX_NONE, OT_EPI_ACCUMULATE)
+#undef OT_SPEC
+  if (!kern) {   // any other combination: generic instantiation (run-time prologue/epilogue)
+    if (mode == OT_GEMM_NT)
+      kern = edge ? mixed_gemm_kernel<true, -1, -1, true> : mixed_gemm_kernel<true, -1, -1, false>;
+    else
+      kern = edge ? mixed_gemm_kernel<false, -1, -1, true> : mixed_gemm_kernel<false, -1, -1, false>;
+  }
+  static std::once_flag lds_once;   // opt every instantiation in to > 64 KiB LDS (gfx950: 160 KiB per CU)
+  std::call_once(lds_once, [] {
+    const int bytes = 4 * GT * GLD * sizeof(float);
+    for (void (*k)(GemmArgs) : {mixed_gemm_kernel<true, -1, -1, true>, mixed_gemm_kernel<true, -1, -1, false>,
+                                mixed_gemm_kernel<false, -1, -1, true>, mixed_gemm_kernel<false, -1, -1, false>})
+      (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    (void)hipGetLastError();
+  });
+  hipLaunchKernelGGL(kern, dim3(nwg), dim3(256), shmem, s, p);
   OT_LAUNCH_CHECK("ot_mixed_gemm");
   return OT_OK;
 }
@@ -429,8 +578,19 @@ extern "C" int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a
   if (nchunks > 0) {
     WgradArgs p{A, lda, a_rows, a_xform, a_rstd, a_gamma, D, ldd, d_rows, K, N, chunks, nchunks, slab, bslab,
                 (int)ceil_div(K, GT), (int)ceil_div(N, GT)};
-    const size_t shmem = 2 * GT * WLD * sizeof(float);
-    hipLaunchKernelGGL(wgrad_kernel, dim3((unsigned)nchunks * p.ntk * p.ntn), dim3(256), shmem, s, p);
+    const size_t shmem = (OT_WGRAD_DBUF ? 4 : 2) * GT * WLD * sizeof(float);
+    void (*kern)(WgradArgs) = a_xform == OT_AX_NONE      ? wgrad_kernel<OT_AX_NONE>
+                              : a_xform == OT_AX_RMSNORM ? wgrad_kernel<OT_AX_RMSNORM>
+                              : a_xform == OT_AX_GELU    ? wgrad_kernel<OT_AX_GELU>
+                                                         : wgrad_kernel<-1>;
+    static std::once_flag lds_once;
+    std::call_once(lds_once, [] {
+      for (void (*k)(WgradArgs) : {wgrad_kernel<OT_AX_NONE>, wgrad_kernel<OT_AX_RMSNORM>, wgrad_kernel<OT_AX_GELU>,
+                                   wgrad_kernel<-1>})
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * GT * WLD * 4);
+      (void)hipGetLastError();
+    });
+    hipLaunchKernelGGL(kern, dim3((unsigned)nchunks * p.ntk * p.ntn), dim3(256), shmem, s, p);
     OT_LAUNCH_CHECK("ot_mixed_gemm_wgrad");
   }
   dim3 rg(ceil_div((int64_t)K * N / 4, 256), ngroups);

@@ -90,7 +90,13 @@ def gemm(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish, w_g
 def wgrad(A: Ptrish, lda: int, a_rows: Ptrish, D: Ptrish, ldd: int, d_rows: Ptrish, K: int, N: int, rmap_dev,
           nchunks: int, ngroups: int, dW: Ptrish, dw_gstride: int, db: Ptrish = None, db_gstride: int = 0, *,
           a_xform: int = 0, rstd: Ptrish = None, gamma: Ptrish = None, accumulate: bool = False,
-          device=None, m_rows: int = 0) -> None:
+          device=None, m_rows: int = 0, rowmap=None) -> None:
+    """rmap_dev: dict with 'chunks'/'gchunk' device tensors; when ``rowmap`` (a layout.RowMap) is given
+    its chunking is re-balanced for this call's output tile count (one resident round)."""
+    if rowmap is not None and rowmap.group_rows:
+        tiles = ((K + 127) // 128) * ((N + 127) // 128)
+        ch, gc, nchunks = rowmap.chunks_for(tiles, device)
+        rmap_dev = {'chunks': ch, 'gchunk': gc}
     nbytes = size('ot_wgrad_workspace_size', nchunks, K, N)
     ws = workspace(nbytes, device)
     ev = _probe.begin() if _probe is not None else None
@@ -99,6 +105,10 @@ def wgrad(A: Ptrish, lda: int, a_rows: Ptrish, D: Ptrish, ldd: int, d_rows: Ptri
          dw_gstride, ptr(db), db_gstride, int(accumulate), ptr(ws), ws.numel(), stream())
     if ev is not None:
         _probe.end('mixed_gemm', 2.0 * m_rows * K * N, ev)
+
+
+def transpose_banks(src, dst, banks_dev, nbanks, total_tiles) -> None:
+    call('ot_transpose_banks', ptr(src), ptr(dst), ptr(banks_dev), nbanks, total_tiles, stream())
 
 
 def attn_fwd(qkv: torch.Tensor, ld: int, B: int, H: int, I: int, K: int, hd: int, out: torch.Tensor,

@@ -24,6 +24,7 @@ from .params import dense_param_shapes, keras_variables
 
 TILE = 128
 ALIGN = 64
+WGRAD_SLOTS = 768          # resident wgrad workgroups (3 per CU x 256 CUs): size chunks for one round
 
 
 def round_up(x: int, m: int) -> int:
@@ -48,6 +49,30 @@ class FlatLayout:
             segs.append((self.offsets[bank] + eoff, rows, cols, stride))
         self.segments = np.array(segs, dtype=np.int64)
         self.max_seg_elems = int((self.segments[:, 1] * self.segments[:, 2]).max())
+        # GEMM weight banks (Keras [G][K][N]) kept transposed ([G][N][K]) in a shadow buffer for the
+        # forward GEMMs: name -> (G, K, N)
+        d, f, T = cfg.hidden_dim, cfg.ffn_dim, len(cfg.tasks)
+        nseq = len(cfg.feature_config['sequence_features'])
+        self.gemm_banks = {'tok.ns.kernel': (1, self.f_pad, cfg.num_ns_tokens * d),
+                           'tok.seq.kernel': (nseq, cfg.seq_feature_dim, d),
+                           'head.w1': (T, d, d // 2)}
+        for l in range(cfg.num_layers):
+            G = cfg.num_groups
+            self.gemm_banks.update({f'blk.{l}.wqkv': (G, d, 3 * d), f'blk.{l}.wo': (1, d, d),
+                                    f'blk.{l}.w1': (G, d, f), f'blk.{l}.w2': (G, f, d)})
+        recs, tiles = [], 0
+        for name, (G, K, N) in self.gemm_banks.items():
+            o = self.offsets[name]
+            recs.append((o, o, G, K, N, tiles))
+            tiles += G * ((K + 31) // 32) * ((N + 31) // 32)
+        self.transpose_desc = np.array(recs, dtype=np.int64)
+        self.transpose_tiles = tiles
+
+    def tview(self, flatT, name):
+        """Transposed bank [G][N][K] inside the shadow buffer (1-D view)."""
+        off = self.offsets[name]
+        G, K, N = self.gemm_banks[name]
+        return flatT[off:off + G * K * N]
 
     def view(self, flat, name):
         off = self.offsets[name]
@@ -61,7 +86,9 @@ class RowMap:
     with ``gchunk`` [G, 2] {first chunk, n chunks}."""
 
     def __init__(self, rows: List[np.ndarray], tile_group: np.ndarray, chunks: np.ndarray,
-                 gchunk: np.ndarray, nrows: int):
+                 gchunk: np.ndarray, nrows: int, group_rows=None):
+        self.group_rows = list(group_rows) if group_rows is not None else []
+        self._chunk_cache = {}
         self.rows = rows
         self.tile_group = tile_group
         self.chunks = chunks
@@ -80,6 +107,38 @@ class RowMap:
                 'gchunk': torch.from_numpy(self.gchunk).to(device),
             }
         return self.dev
+
+    def chunks_for(self, tiles_per_chunk: int, device):
+        """wgrad chunk table whose workgroup count (chunks x output tiles) fits one resident round
+        (WGRAD_SLOTS): the smallest chunk size (multiple of 32 rows) that does.  Returns
+        (chunks_dev, gchunk_dev, nchunks)."""
+        import torch
+        key = (tiles_per_chunk, str(device))
+        if key not in self._chunk_cache:
+            padded = [round_up(n, TILE) for n in self.group_rows]
+            budget = max(1, WGRAD_SLOTS // max(1, tiles_per_chunk))
+            lo, hi = 32, max(32, round_up(max(padded) if padded else 32, 32))
+            while lo < hi:
+                mid = round_up((lo + hi) // 2, 32)
+                if mid >= hi:
+                    mid = hi - 32 if hi - 32 >= lo else lo
+                n = sum((p + mid - 1) // mid for p in padded if p > 0)
+                if n <= budget:
+                    hi = mid
+                else:
+                    lo = mid + 32
+            cr = lo
+            chunks, gchunk, base = [], [], 0
+            for g, p in enumerate(padded):
+                first = len(chunks)
+                for c0 in range(0, p, cr):
+                    chunks.append((g, base + c0, min(cr, p - c0)))
+                gchunk.append((first, len(chunks) - first))
+                base += p
+            ch = np.array(chunks, dtype=np.int32).reshape(-1, 3)
+            gc = np.array(gchunk, dtype=np.int32).reshape(-1, 2)
+            self._chunk_cache[key] = (torch.from_numpy(ch).to(device), torch.from_numpy(gc).to(device), len(ch))
+        return self._chunk_cache[key]
 
 
 def build_map(per_group: Sequence[Sequence[np.ndarray]], chunk_rows: int = 0) -> RowMap:
@@ -110,7 +169,8 @@ def build_map(per_group: Sequence[Sequence[np.ndarray]], chunk_rows: int = 0) ->
     cat = [np.concatenate(r) if r else np.zeros(0, np.int32) for r in rows]
     return RowMap(cat, np.array(tile_group, dtype=np.int32),
                   np.array(chunks, dtype=np.int32).reshape(-1, 3),
-                  np.array(gchunk, dtype=np.int32).reshape(-1, 2), total)
+                  np.array(gchunk, dtype=np.int32).reshape(-1, 2), total,
+                  group_rows=[len(pg[0]) for pg in per_group])
 
 
 def layer_maps(cfg: OneTransConfig, B: int, I: int, K: int) -> Dict[str, RowMap]:

@@ -51,8 +51,8 @@ class _Tokenize(torch.autograd.Function):
             nsm = plan['nsmat']
             K.ns_assemble(plan['ns_desc'], plan['ns_fields'], m.tables.get('emb.ns'), B, nsm, m.layout.f_pad)
             mp = plan['ns_map'].to(dev)
-            K.gemm(OT_GEMM_NN, nsm, m.layout.f_pad, m.layout.f_pad, mp['rows'][0], m.p('tok.ns.kernel'), 0,
-                   m.cfg_Lnsd, m.cfg_Lnsd, mp['tile_group'], plan['ns_map'].ntiles, (x0, L_S * d), L0 * d,
+            K.gemm(OT_GEMM_NT, nsm, m.layout.f_pad, m.layout.f_pad, mp['rows'][0], m.pT('tok.ns.kernel'), 0,
+                   m.layout.f_pad, m.cfg_Lnsd, mp['tile_group'], plan['ns_map'].ntiles, (x0, L_S * d), L0 * d,
                    mp['rows'][0], bias=m.p('tok.ns.bias'), epi=OT_EPI_BIAS, m_rows=B)
         else:                                                   # model.py:249-251
             x0.view(B, L0, d)[:, L_S:].zero_()
@@ -60,7 +60,7 @@ class _Tokenize(torch.autograd.Function):
         if plan['seq_map'] is not None:
             sm = plan['seq_map'].to(dev)
             A, lda = plan['seq_A'], m.config.seq_feature_dim
-            K.gemm(OT_GEMM_NN, A, lda, lda, plan['seq_in'], m.p('tok.seq.kernel'), lda * d, d, d, sm['tile_group'],
+            K.gemm(OT_GEMM_NT, A, lda, lda, plan['seq_in'], m.pT('tok.seq.kernel'), lda * d, lda, d, sm['tile_group'],
                    plan['seq_map'].ntiles, x0, d, sm['rows'][0], bias=m.p('tok.seq.bias'), bias_gstride=d,
                    epi=OT_EPI_BIAS, m_rows=plan['seq_M'])
         if plan['n_sep'] > 0:                                   # model.py:270-272
@@ -137,38 +137,38 @@ class _Block(torch.autograd.Function):
         na, nt = maps['all'].ntiles, maps['tail'].ntiles
         rate = cfg.dropout_rate if training else 0.0
         dflag = OT_EPI_DROPOUT if rate > 0 else 0
-        wqkv, wo = m.p(f'blk.{l}.wqkv'), m.p(f'blk.{l}.wo')
-        w1, b1, w2, b2 = m.p(f'blk.{l}.w1'), m.p(f'blk.{l}.b1'), m.p(f'blk.{l}.w2'), m.p(f'blk.{l}.b2')
+        wqkv, wo = m.pT(f'blk.{l}.wqkv'), m.pT(f'blk.{l}.wo')          # transposed shadow: [G][N][K]
+        w1, b1, w2, b2 = m.pT(f'blk.{l}.w1'), m.p(f'blk.{l}.b1'), m.pT(f'blk.{l}.w2'), m.p(f'blk.{l}.b2')
         g1, g2 = m.p(f'blk.{l}.norm1'), m.p(f'blk.{l}.norm2')
         # norm1 -> rstd only; the QKV GEMM applies it in its A prologue
         rstd1 = torch.empty(B * I, device=dev)
         K.rmsnorm_fwd(x, d, B * I, d, rstd1, eps=RMS_EPS)
         qkv = torch.empty(B * I, 3 * d, device=dev)
         if Kq == I:
-            K.gemm(OT_GEMM_NN, x, d, d, ma['rows'][0], wqkv, 3 * d * d, 3 * d, 3 * d, ma['tile_group'], na, qkv,
+            K.gemm(OT_GEMM_NT, x, d, d, ma['rows'][0], wqkv, 3 * d * d, d, 3 * d, ma['tile_group'], na, qkv,
                    3 * d, ma['rows'][0], a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=maps['all'].nrows)
         else:
-            K.gemm(OT_GEMM_NN, x, d, d, ma['rows'][0], (wqkv, d), 3 * d * d, 3 * d, 2 * d, ma['tile_group'], na,
+            K.gemm(OT_GEMM_NT, x, d, d, ma['rows'][0], (wqkv, d * d), 3 * d * d, d, 2 * d, ma['tile_group'], na,
                    (qkv, d), 3 * d, ma['rows'][0], a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=maps['all'].nrows)
-            K.gemm(OT_GEMM_NN, x, d, d, mt['rows'][0], wqkv, 3 * d * d, 3 * d, d, mt['tile_group'], nt, qkv,
+            K.gemm(OT_GEMM_NT, x, d, d, mt['rows'][0], wqkv, 3 * d * d, d, d, mt['tile_group'], nt, qkv,
                    3 * d, mt['rows'][0], a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=maps['tail'].nrows)
         o = torch.empty(B * Kq, d, device=dev)
         lse = torch.empty(B * H * Kq, device=dev)
         K.attn_fwd(qkv, 3 * d, B, H, I, Kq, hd, o, lse)
         # x1 = x[tail] + drop(o @ Wo)      (model.py:117, 193)
         x1 = torch.empty(B * Kq, d, device=dev)
-        K.gemm(OT_GEMM_NN, o, d, d, mt['rows'][1], wo, 0, d, d, mt['tile_group'], nt, x1, d, mt['rows'][1],
+        K.gemm(OT_GEMM_NT, o, d, d, mt['rows'][1], wo, 0, d, d, mt['tile_group'], nt, x1, d, mt['rows'][1],
                epi=OT_EPI_RESIDUAL | dflag, res=x, ldres=d, res_tok=1, seed=seed, site=2 * l, drop=rate,
                tail=(Kq, I), m_rows=maps['tail'].nrows)
         rstd2 = torch.empty(B * Kq, device=dev)
         K.rmsnorm_fwd(x1, d, B * Kq, d, rstd2, eps=RMS_EPS)
         # u = norm2(x1) @ W1[g] + b1[g]  (pre-activation; GELU applied by its consumers)
         u = torch.empty(B * Kq, f, device=dev)
-        K.gemm(OT_GEMM_NN, x1, d, d, mt['rows'][1], w1, d * f, f, f, mt['tile_group'], nt, u, f, mt['rows'][1],
+        K.gemm(OT_GEMM_NT, x1, d, d, mt['rows'][1], w1, d * f, d, f, mt['tile_group'], nt, u, f, mt['rows'][1],
                a_xform=OT_AX_RMSNORM, rstd=rstd2, gamma=g2, bias=b1, bias_gstride=f, epi=OT_EPI_BIAS, m_rows=maps['tail'].nrows)
         # x2 = x1 + drop(gelu(u) @ W2[g] + b2[g])     (model.py:154-161, 198)
         x2 = torch.empty(B * Kq, d, device=dev)
-        K.gemm(OT_GEMM_NN, u, f, f, mt['rows'][1], w2, f * d, d, d, mt['tile_group'], nt, x2, d, mt['rows'][1],
+        K.gemm(OT_GEMM_NT, u, f, f, mt['rows'][1], w2, f * d, f, d, mt['tile_group'], nt, x2, d, mt['rows'][1],
                a_xform=OT_AX_GELU, bias=b2, bias_gstride=d, epi=OT_EPI_BIAS | OT_EPI_RESIDUAL | dflag, res=x1,
                ldres=d, res_tok=0, seed=seed, site=2 * l + 1, drop=rate, tail=(Kq, I), m_rows=maps['tail'].nrows)
         ctx.save_for_backward(x, rstd1, qkv, o, lse, x1, rstd2, u)
@@ -198,13 +198,14 @@ class _Block(torch.autograd.Function):
         else:
             dy2 = dx2
         K.wgrad(u, f, mt['rows'][1], dy2, d, mt['rows'][1], f, d, mt, nct, G, m.g(f'blk.{l}.w2'), f * d,
-                m.g(f'blk.{l}.b2'), d, a_xform=OT_AX_GELU, accumulate=acc, device=dev, m_rows=maps['tail'].nrows)
+                m.g(f'blk.{l}.b2'), d, a_xform=OT_AX_GELU, accumulate=acc, device=dev, m_rows=maps['tail'].nrows,
+                rowmap=maps['tail'])
         du = torch.empty(B * Kq, f, device=dev)
         K.gemm(OT_GEMM_NT, dy2, d, d, mt['rows'][1], m.p(f'blk.{l}.w2'), f * d, d, f, mt['tile_group'], nt, du, f,
                mt['rows'][1], epi=OT_EPI_GELU_BWD, aux=u, ldaux=f, m_rows=maps['tail'].nrows)
         K.wgrad(x1, d, mt['rows'][1], du, f, mt['rows'][1], d, f, mt, nct, G, m.g(f'blk.{l}.w1'), d * f,
                 m.g(f'blk.{l}.b1'), f, a_xform=OT_AX_RMSNORM, rstd=rstd2, gamma=m.p(f'blk.{l}.norm2'),
-                accumulate=acc, device=dev, m_rows=maps['tail'].nrows)
+                accumulate=acc, device=dev, m_rows=maps['tail'].nrows, rowmap=maps['tail'])
         dxn2 = torch.empty(B * Kq, d, device=dev)
         K.gemm(OT_GEMM_NT, du, f, f, mt['rows'][1], m.p(f'blk.{l}.w1'), d * f, f, d, mt['tile_group'], nt, dxn2, d,
                mt['rows'][1], m_rows=maps['tail'].nrows)
@@ -226,7 +227,7 @@ class _Block(torch.autograd.Function):
         K.attn_bwd(qkv, 3 * d, o, do, lse, B, H, I, Kq, hd, dqkv)
         K.wgrad(x, d, ma['rows'][0], dqkv, 3 * d, ma['rows'][0], d, 3 * d, ma, nca, G, m.g(f'blk.{l}.wqkv'),
                 3 * d * d, None, 0, a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=m.p(f'blk.{l}.norm1'), accumulate=acc,
-                device=dev, m_rows=maps['all'].nrows)
+                device=dev, m_rows=maps['all'].nrows, rowmap=maps['all'])
         dxn1 = torch.empty(B * I, d, device=dev)
         K.gemm(OT_GEMM_NT, dqkv, 3 * d, 3 * d, ma['rows'][0], m.p(f'blk.{l}.wqkv'), 3 * d * d, 3 * d, d,
                ma['tile_group'], na, dxn1, d, ma['rows'][0], m_rows=maps['all'].nrows)
@@ -260,7 +261,7 @@ class _Head(torch.autograd.Function):
         hm = m.head_rows(B)
         hmd = hm.to(dev)
         pre1 = torch.empty(T * B, dh, device=dev)
-        K.gemm(OT_GEMM_NN, y, d, d, hmd['rows'][0], m.p('head.w1'), d * dh, dh, dh, hmd['tile_group'], hm.ntiles,
+        K.gemm(OT_GEMM_NT, y, d, d, hmd['rows'][0], m.pT('head.w1'), d * dh, d, dh, hmd['tile_group'], hm.ntiles,
                pre1, dh, hmd['rows'][1], bias=m.p('head.b1'), bias_gstride=dh, epi=OT_EPI_BIAS, m_rows=hm.nrows)
         logits = torch.empty(T, B, device=dev)
         probs = torch.empty(T, B, device=dev)
@@ -345,6 +346,8 @@ class OneTransModel(nn.Module):
         self.cfg_Lnsd = cfg.num_ns_tokens * cfg.hidden_dim
         self.flat = nn.Parameter(torch.zeros(self.layout.total, device=self.device))
         self.flat.grad = torch.zeros_like(self.flat)
+        self.flatT = torch.zeros(self.layout.total, device=self.device)     # transposed GEMM weight shadow
+        self._tdesc = torch.from_numpy(self.layout.transpose_desc.reshape(-1)).to(self.device)
         self.tables: Dict[str, torch.Tensor] = {}
         self.accumulate_grads = False
         self.kv_cache = None                      # model.py:333 (reference attribute; never populated)
@@ -366,6 +369,14 @@ class OneTransModel(nn.Module):
     def g(self, name):
         return self.layout.view(self.flat.grad, name)
 
+    def pT(self, name):
+        return self.layout.tview(self.flatT, name)
+
+    def refresh_shadow(self) -> None:
+        """Re-derive the transposed weight banks after any change of the weights (init, load, optimizer)."""
+        K.transpose_banks(self.flat.data, self.flatT, self._tdesc, self.layout.transpose_desc.shape[0],
+                          self.layout.transpose_tiles)
+
     def load_param_dict(self, params: Dict[str, np.ndarray]) -> None:
         """Load host arrays (params.init_params layout; tok.ns.kernel may be unpadded)."""
         with torch.no_grad():
@@ -380,6 +391,7 @@ class OneTransModel(nn.Module):
                     dst[:src.shape[0]].copy_(src)
                 else:
                     dst.copy_(src.reshape(dst.shape))
+        self.refresh_shadow()
 
     def param_dict(self) -> Dict[str, np.ndarray]:
         out = {}

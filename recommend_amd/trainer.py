@@ -68,6 +68,7 @@ class OneTransOptimizer:
         otdist.allreduce_dense(m.flat.grad)
         K.clip_rmsprop(m.flat.data, m.flat.grad, self.v, self.m, self.segs, self.nseg, m.layout.max_seg_elems,
                        self.lr, self.rho, self.eps, self.momentum, self.clip, device=m.flat.device)
+        m.refresh_shadow()
         for (name, keys, grads) in m._pending_sparse:
             keys, grads = otdist.allgather_sparse(keys, grads)
             table = m.tables[name]

@@ -264,3 +264,24 @@ def test_clip_rmsprop(dev):
     np.testing.assert_allclose(wd.cpu().numpy(), w2, rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(vd.cpu().numpy(), v2, rtol=1e-5, atol=1e-7)
     np.testing.assert_allclose(md.cpu().numpy(), m2, rtol=1e-5, atol=1e-7)
+
+
+def test_transpose_banks(dev):
+    shapes = [(3, 40, 70), (1, 128, 384), (2, 33, 5)]
+    offs, recs, tiles, o = [], [], 0, 0
+    srcs = []
+    for (G, K_, N) in shapes:
+        a = torch.randn(G, K_, N)
+        srcs.append(a)
+        recs.append((o, o, G, K_, N, tiles))
+        tiles += G * ((K_ + 31) // 32) * ((N + 31) // 32)
+        o += G * K_ * N + 7
+    src = torch.zeros(o)
+    for (r, a) in zip(recs, srcs):
+        src[r[0]:r[0] + a.numel()] = a.reshape(-1)
+    dst = torch.full((o,), float('nan'), device=dev)
+    desc = torch.tensor(recs, dtype=torch.int64).reshape(-1).to(dev)
+    K.transpose_banks(src.to(dev), dst, desc, len(recs), tiles)
+    for (r, a) in zip(recs, srcs):
+        got = dst[r[1]:r[1] + a.numel()].cpu().view(a.shape[0], a.shape[2], a.shape[1])
+        assert torch.equal(got, a.transpose(1, 2))

@@ -74,9 +74,41 @@ __device__ __forceinline__ void acc_xT_p(f32x16 (&acc)[NB(HD)], const float* xba
   }
 }
 
+// Per-wave LDS tile [32][HD+4]: a block the wave holds as row fragments (lane li = row li) is
+// written once and read transposed (lane li = column) as the A operand of the accumulator-as-
+// operand products — no scalar global re-reads inside the MFMA chains.
+template <int HD>
+constexpr int TLD() { return HD + 4; }
+
+template <int HD>
+__device__ __forceinline__ void frag_to_lds(float* tile, const float (&f)[HD / 2], int li, int hh) {
+#pragma unroll
+  for (int q = 0; q < HD / 8; ++q)
+    *reinterpret_cast<f32x4*>(tile + li * TLD<HD>() + (HD / 2) * hh + 4 * q) =
+        f32x4{f[4 * q], f[4 * q + 1], f[4 * q + 2], f[4 * q + 3]};
+}
+
+// acc[c] (+)= sum_r tile[row(r)][32c + li] * p[r]
+template <int HD>
+__device__ __forceinline__ void acc_tile_p(f32x16 (&acc)[NB(HD)], const float* tile, const f32x16& p, int li,
+                                           int hh) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = acc_row(r, hh);
+#pragma unroll
+    for (int c = 0; c < NB(HD); ++c) {
+      const int dd = 32 * c + li;
+      const float a = dd < HD ? tile[row * TLD<HD>() + dd] : 0.f;
+      acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, p[r], acc[c], 0, 0, 0);
+    }
+  }
+}
+
 template <int HD>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs p) {
+  __shared__ __attribute__((aligned(16))) float lds[4][32 * TLD<HD>()];
   const int lane = threadIdx.x & 63, li = lane & 31, hh = lane >> 5;
+  float* tV = lds[threadIdx.x >> 6];
   const int pair = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (pair >= p.B * p.H) return;
   const int b = pair / p.H, h = pair % p.H;
@@ -101,8 +133,10 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs p) {
     const int nkb = last_q / 32 + 1;
     for (int kb = 0; kb < nkb; ++kb) {
       const int key0 = 32 * kb;
-      float kf[HD / 2];
+      float kf[HD / 2], vf[HD / 2];
       load_frag<HD>(kf, Kp, p.ld, key0 + li, I, hh);
+      load_frag<HD>(vf, V, p.ld, key0 + li, I, hh);
+      frag_to_lds<HD>(tV, vf, li, hh);
       f32x16 s = mm_frag<HD>(kf, qf);               // S^T: row = key, col = query
       float mloc = -INFINITY;
 #pragma unroll
@@ -128,7 +162,9 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs p) {
       m = mnew;
 #pragma unroll
       for (int c = 0; c < NB(HD); ++c) oacc[c] *= corr;
-      acc_xT_p<HD>(oacc, V, p.ld, key0, I, s, li, hh);
+      __builtin_amdgcn_wave_barrier();
+      acc_tile_p<HD>(oacc, tV, s, li, hh);             // O^T += V^T P^T
+      __builtin_amdgcn_wave_barrier();
     }
     if (j < K) {
       const float inv = 1.f / l;
@@ -172,13 +208,39 @@ __global__ __launch_bounds__(256) void attn_bwd_prep_kernel(const float* __restr
 }
 
 // ------------------------------------------------------------------------------------------
-// Backward.  Pass A (per key block): S, dP with the key on the lane -> dV^T, dK^T.
-//            Pass B (per query block): S^T, dP^T with the query on the lane -> dQ^T.
-// Both are plain two-pass recomputation (no atomics, no cross-wave traffic): deterministic.
+// Backward, one pass per (sample, head) wave: key blocks outer, the query blocks that see them
+// inner.  S and dP are computed with the key on the lane, so P and dS feed dV^T += dO^T P and
+// dK^T += Q^T dS directly (dO and Q blocks read transposed from per-wave LDS tiles).  dS is also
+// written to an LDS tile [query][key] and read back as the A operand of dQ += dS K (K block from
+// its LDS tile), accumulated in place in dqkv: the wave owns the (b, h) slice, its first key block
+// (seen by every query) stores and later ones read-modify-write the same lanes' addresses.
+// No atomics, no recompute pass, deterministic.
+
+// 4 consecutive values v[j0..j0+3] (j0 % 4 == 0) with bounds: vector load when fully in range
+__device__ __forceinline__ f32x4 load4(const float* v, int j0, int n) {
+  if (j0 + 3 < n) return *reinterpret_cast<const f32x4*>(v + j0);
+  f32x4 r = {0.f, 0.f, 0.f, 0.f};
+  if (j0 < n) r.x = v[j0];
+  if (j0 + 1 < n) r.y = v[j0 + 1];
+  if (j0 + 2 < n) r.z = v[j0 + 2];
+  return r;
+}
+
 template <int HD>
-__global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs p) {
+constexpr int BWD_WAVES() { return HD >= 128 ? 2 : 4; }
+
+template <int HD>
+__global__ __launch_bounds__(64 * BWD_WAVES<HD>(), 2) void attn_bwd_kernel(AttnArgs p) {
+  constexpr int LD = TLD<HD>();
+  constexpr int SLD = 36;                  // dS tile row stride (32 keys + pad)
+  constexpr int PER_WAVE = 3 * 32 * LD + 32 * SLD;
+  __shared__ __attribute__((aligned(16))) float lds[BWD_WAVES<HD>() * PER_WAVE];
   const int lane = threadIdx.x & 63, li = lane & 31, hh = lane >> 5;
-  const int pair = blockIdx.x * 4 + (threadIdx.x >> 6);
+  float* tO = lds + (threadIdx.x >> 6) * PER_WAVE;   // dO block   [query][dim]
+  float* tQ = tO + 32 * LD;                          // Q block    [query][dim]
+  float* tK = tQ + 32 * LD;                          // K block    [key][dim]
+  float* tS = tK + 32 * LD;                          // dS block   [query][key]
+  const int pair = blockIdx.x * BWD_WAVES<HD>() + (threadIdx.x >> 6);
   if (pair >= p.B * p.H) return;
   const int b = pair / p.H, h = pair % p.H;
   const int I = p.I, K = p.K, q_off = I - K;
@@ -187,49 +249,94 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs p) {
   const float* Kp = Q + p.d;
   const float* V = Q + 2 * p.d;
   const float* Qt = Q + (int64_t)q_off * p.ld;
-  const float* O = p.o + (int64_t)b * K * p.d + h * HD;
   const float* dO = p.dout + (int64_t)b * K * p.d + h * HD;
   const float* lse = p.lse + ((int64_t)b * p.H + h) * K;
+  const float* delta = p.delta + ((int64_t)b * p.H + h) * K;   // rowsum(dO * O), attn_bwd_prep_kernel
   float* dQt = p.dqkv + (tok0 + q_off) * p.ld + h * HD;
   float* dK = p.dqkv + tok0 * p.ld + p.d + h * HD;
   float* dV = dK + p.d;
   const int nqb = (K + 31) / 32;
-
-  const float* delta = p.delta + ((int64_t)b * p.H + h) * K;   // rowsum(dO * O), attn_bwd_prep_kernel
-
-  // ---------------- pass A: dK, dV for every key block
   const int nkb = (I + 31) / 32;
+
   for (int kb = 0; kb < nkb; ++kb) {
     const int key0 = 32 * kb;
     const int kpos = key0 + li;                        // this lane's key
     float kf[HD / 2], vf[HD / 2];
     load_frag<HD>(kf, Kp, p.ld, kpos, I, hh);
     load_frag<HD>(vf, V, p.ld, kpos, I, hh);
+    frag_to_lds<HD>(tK, kf, li, hh);
     f32x16 dk[NB(HD)], dv[NB(HD)];
 #pragma unroll
     for (int c = 0; c < NB(HD); ++c)
 #pragma unroll
       for (int r = 0; r < 16; ++r) { dk[c][r] = 0.f; dv[c][r] = 0.f; }
-    // first query block whose last query can see key0
-    int qb0 = key0 - q_off; qb0 = qb0 < 0 ? 0 : qb0 / 32;
+    int qb0 = key0 - q_off; qb0 = qb0 < 0 ? 0 : qb0 / 32;      // first query block that sees key0
+    float qf[HD / 2], of[HD / 2];
+    load_frag<HD>(qf, Qt, p.ld, 32 * qb0 + li, K, hh);
+    load_frag<HD>(of, dO, p.d, 32 * qb0 + li, K, hh);
     for (int qb = qb0; qb < nqb; ++qb) {
       const int q0 = 32 * qb;
-      float qf[HD / 2], of[HD / 2];
-      load_frag<HD>(qf, Qt, p.ld, q0 + li, K, hh);
-      load_frag<HD>(of, dO, p.d, q0 + li, K, hh);
+      __builtin_amdgcn_wave_barrier();
+      frag_to_lds<HD>(tO, of, li, hh);
+      frag_to_lds<HD>(tQ, qf, li, hh);
       f32x16 s = mm_frag<HD>(qf, kf);                  // S: row = query, col = key
       f32x16 dp = mm_frag<HD>(of, vf);                 // dP: row = query, col = key
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int j = q0 + acc_row(r, hh);
-        const bool ok = j < K && kpos <= q_off + j;
-        const float lj = j < K ? lse[j] : 0.f;
-        const float P = ok ? __expf(s[r] * p.scale - lj) : 0.f;
-        s[r] = P;
-        dp[r] = ok ? P * (dp[r] - delta[j]) : 0.f;
+      if (qb + 1 < nqb) {                              // prefetch the next query block
+        load_frag<HD>(qf, Qt, p.ld, q0 + 32 + li, K, hh);
+        load_frag<HD>(of, dO, p.d, q0 + 32 + li, K, hh);
       }
-      acc_xT_p<HD>(dv, dO, p.d, q0, K, s, li, hh);    // dV^T += dO^T P
-      acc_xT_p<HD>(dk, Qt, p.ld, q0, K, dp, li, hh);  // dK^T += Q^T dS
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int j0 = q0 + 8 * g + 4 * hh;
+        const f32x4 l4 = load4(lse, j0, K), d4 = load4(delta, j0, K);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * g + e, j = j0 + e;
+          const bool ok = j < K && kpos <= q_off + j;
+          const float P = ok ? __expf(s[r] * p.scale - l4[e]) : 0.f;
+          s[r] = P;
+          dp[r] = ok ? P * (dp[r] - d4[e]) : 0.f;
+          tS[(8 * g + 4 * hh + e) * SLD + li] = dp[r];
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      acc_tile_p<HD>(dv, tO, s, li, hh);               // dV^T += dO^T P
+      acc_tile_p<HD>(dk, tQ, dp, li, hh);              // dK^T += Q^T dS
+      // dQ[q][d] += sum_key dS[q][key] K[key][d]: A = dS (lane = query, k = key 16hh + s),
+      // B = K (k = key, lane = dim)
+      f32x16 dq[NB(HD)];
+#pragma unroll
+      for (int c = 0; c < NB(HD); ++c)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dq[c][r] = 0.f;
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {
+        const f32x4 a4 = *reinterpret_cast<const f32x4*>(tS + li * SLD + 16 * hh + 4 * q4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int key = 16 * hh + 4 * q4 + e;
+#pragma unroll
+          for (int c = 0; c < NB(HD); ++c) {
+            const int dd = 32 * c + li;
+            const float bk = dd < HD ? tK[key * LD + dd] : 0.f;
+            dq[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[e], bk, dq[c], 0, 0, 0);
+          }
+        }
+      }
+      // acc row = query (q0 + acc_row), col = dim: accumulate into dqkv (first key block stores)
+#pragma unroll
+      for (int c = 0; c < NB(HD); ++c) {
+        const int dd = 32 * c + li;
+        if (dd >= HD) continue;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int j = q0 + acc_row(r, hh);
+          if (j >= K) continue;
+          float* dst = dQt + (int64_t)j * p.ld + dd;
+          const float v = dq[c][r] * p.scale;
+          *dst = kb == 0 ? v : *dst + v;
+        }
+      }
     }
     if (kpos < I) {
 #pragma unroll
@@ -243,53 +350,6 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs p) {
             f32x4 v = {dv[c][4 * g], dv[c][4 * g + 1], dv[c][4 * g + 2], dv[c][4 * g + 3]};
             *reinterpret_cast<f32x4*>(dK + (int64_t)kpos * p.ld + dd) = a;
             *reinterpret_cast<f32x4*>(dV + (int64_t)kpos * p.ld + dd) = v;
-          }
-        }
-    }
-  }
-
-  // ---------------- pass B: dQ for every tail query block
-  for (int qb = 0; qb < nqb; ++qb) {
-    const int j = 32 * qb + li;
-    const int qpos = q_off + (j < K ? j : K - 1);
-    float qf[HD / 2], of[HD / 2];
-    load_frag<HD>(qf, Qt, p.ld, j, K, hh);
-    load_frag<HD>(of, dO, p.d, j, K, hh);
-    const float lj = j < K ? lse[j] : 0.f;
-    const float dj = j < K ? delta[j] : 0.f;
-    f32x16 dq[NB(HD)];
-#pragma unroll
-    for (int c = 0; c < NB(HD); ++c)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) dq[c][r] = 0.f;
-    const int last_q = q_off + min(32 * qb + 31, K - 1);
-    const int nkb2 = last_q / 32 + 1;
-    for (int kb = 0; kb < nkb2; ++kb) {
-      const int key0 = 32 * kb;
-      float kf[HD / 2], vf[HD / 2];
-      load_frag<HD>(kf, Kp, p.ld, key0 + li, I, hh);
-      load_frag<HD>(vf, V, p.ld, key0 + li, I, hh);
-      f32x16 s = mm_frag<HD>(kf, qf);                  // S^T: row = key, col = query
-      f32x16 dp = mm_frag<HD>(vf, of);                 // dP^T
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int kpos = key0 + acc_row(r, hh);
-        const bool ok = j < K && kpos <= qpos;
-        const float P = ok ? __expf(s[r] * p.scale - lj) : 0.f;
-        dp[r] = ok ? P * (dp[r] - dj) : 0.f;
-      }
-      acc_xT_p<HD>(dq, Kp, p.ld, key0, I, dp, li, hh); // dQ^T += K^T dS^T
-    }
-    if (j < K) {
-#pragma unroll
-      for (int c = 0; c < NB(HD); ++c)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int dd = 32 * c + 8 * g + 4 * hh;
-          if (dd < HD) {
-            f32x4 a = {dq[c][4 * g] * p.scale, dq[c][4 * g + 1] * p.scale, dq[c][4 * g + 2] * p.scale,
-                       dq[c][4 * g + 3] * p.scale};
-            *reinterpret_cast<f32x4*>(dQt + (int64_t)j * p.ld + dd) = a;
           }
         }
     }
@@ -335,8 +395,9 @@ extern "C" int ot_attn_bwd(const float* qkv, int64_t ld, const float* out, const
   hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3(ceil_div((int64_t)B * K * H * head_dim / 4, 256)), dim3(256), 0,
                      (hipStream_t)stream, out, dout, delta_ws, B, H, K, head_dim);
   OT_LAUNCH_CHECK("ot_attn_bwd(prep)");
-  const unsigned grid = ceil_div((int64_t)B * H, 4);
-  OT_ATTN_DISPATCH(attn_bwd_kernel, head_dim, dim3(grid), dim3(256), 0, (hipStream_t)stream, p);
+  const int waves = head_dim >= 128 ? 2 : 4;
+  const unsigned grid = ceil_div((int64_t)B * H, waves);
+  OT_ATTN_DISPATCH(attn_bwd_kernel, head_dim, dim3(grid), dim3(64 * waves), 0, (hipStream_t)stream, p);
   OT_LAUNCH_CHECK("ot_attn_bwd");
   return OT_OK;
 }

@@ -416,29 +416,39 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
 }
 
 // Sum the slabs of each group's chunks (chunks of one group are contiguous) into dW[g] (and db).
-__global__ void wgrad_reduce_kernel(const float* __restrict__ slab, const float* __restrict__ bslab,
-                                    const int32_t* __restrict__ chunks, const int32_t* __restrict__ gchunk,
-                                    int ngroups, int K, int N, float* dW, int64_t dw_gstride,
-                                    float* db, int64_t db_gstride, int accumulate) {
+// Block = 16 float4 columns x 16 chunk lanes; chunk lane c sums chunks c, c+16, ... and the 16
+// partials are combined in a fixed order through LDS (deterministic).
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ slab,
+                                                           const float* __restrict__ bslab,
+                                                           const int32_t* __restrict__ gchunk, int K, int N,
+                                                           float* dW, int64_t dw_gstride, float* db,
+                                                           int64_t db_gstride, int accumulate) {
+  __shared__ f32x4 red[16][16];
   const int g = blockIdx.y;
   const int cb = gchunk[2 * g], cn = gchunk[2 * g + 1];
   const int64_t KN = (int64_t)K * N;
-  const int64_t i4 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-  if (i4 < KN) {
-    // a group with no rows (e.g. dedicated groups outside a 1-token tail) has a zero gradient
-    f32x4 s = {0.f, 0.f, 0.f, 0.f};
-    for (int c = cb; c < cb + cn; ++c) s += *reinterpret_cast<const f32x4*>(slab + (int64_t)c * KN + i4);
+  const int col = threadIdx.x & 15, cl = threadIdx.x >> 4;
+  const int64_t i4 = ((int64_t)blockIdx.x * 16 + col) * 4;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (i4 < KN)
+    for (int c = cb + cl; c < cb + cn; c += 16) s += *reinterpret_cast<const f32x4*>(slab + (int64_t)c * KN + i4);
+  red[cl][col] = s;
+  __syncthreads();
+  if (cl == 0 && i4 < KN) {   // a group with no rows (e.g. dedicated groups outside a 1-token tail) -> 0
+    f32x4 t = red[0][col];
+#pragma unroll
+    for (int q = 1; q < 16; ++q) t += red[q][col];
     float* dst = dW + (int64_t)g * dw_gstride + i4;
-    if (accumulate) s += *reinterpret_cast<const f32x4*>(dst);
-    *reinterpret_cast<f32x4*>(dst) = s;
+    if (accumulate) t += *reinterpret_cast<const f32x4*>(dst);
+    *reinterpret_cast<f32x4*>(dst) = t;
   }
   if (db && blockIdx.x == 0) {
     for (int n = threadIdx.x; n < N; n += blockDim.x) {
-      float s = 0.f;
+      float t = 0.f;
       if (bslab)
-        for (int c = cb; c < cb + cn; ++c) s += bslab[(int64_t)c * N + n];
+        for (int c = cb; c < cb + cn; ++c) t += bslab[(int64_t)c * N + n];
       float* dst = db + (int64_t)g * db_gstride + n;
-      *dst = accumulate ? *dst + s : s;
+      *dst = accumulate ? *dst + t : t;
     }
   }
 }
@@ -593,9 +603,9 @@ extern "C" int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a
     hipLaunchKernelGGL(kern, dim3((unsigned)nchunks * p.ntk * p.ntn), dim3(256), shmem, s, p);
     OT_LAUNCH_CHECK("ot_mixed_gemm_wgrad");
   }
-  dim3 rg(ceil_div((int64_t)K * N / 4, 256), ngroups);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, rg, dim3(256), 0, s, slab, bslab, chunks, gchunk, ngroups, K, N,
-                     dW, dw_gstride, db, db_gstride, accumulate);
+  dim3 rg(ceil_div((int64_t)K * N / 4, 16), ngroups);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, rg, dim3(256), 0, s, slab, bslab, gchunk, K, N, dW, dw_gstride, db,
+                     db_gstride, accumulate);
   OT_LAUNCH_CHECK("ot_mixed_gemm_wgrad(reduce)");
   return OT_OK;
 }

@@ -22,6 +22,9 @@ namespace ot {
 #ifndef OT_GEMM_BK
 #define OT_GEMM_BK 16
 #endif
+#ifndef OT_GEMM_RMS_EARLY
+#define OT_GEMM_RMS_EARLY 1
+#endif
 #ifndef OT_WGRAD_DBUF
 #define OT_WGRAD_DBUF 0
 #endif
@@ -83,6 +86,8 @@ __global__ __launch_bounds__(256, 2) void mixed_gemm_kernel(GemmArgs p) {
 
   // ---- staging coordinates: a row holds CPR float4 chunks; thread t stages chunk sc of rows
   // sr + RPP*i (i < NPASS), for A and (NT) B
+  // (Consecutive lanes read consecutive 16-B chunks of a row.  Remapping the 8 lanes of each
+  // ds_write_b128 group onto 8 rows makes the stores conflict-free but costs ~8 % on the loads.)
   constexpr int CPR = GBK / 4, RPP = 256 / CPR, NPASS = GT / RPP;
   const int sc = t % CPR, sr = t / CPR;
   const float* arow[NPASS];
@@ -101,34 +106,37 @@ __global__ __launch_bounds__(256, 2) void mixed_gemm_kernel(GemmArgs p) {
     bok[i] = !EDGE || n < p.N;
     brow[i] = W + (int64_t)(bok[i] ? n : 0) * p.ldw + 4 * sc;
   }
-  f32x4 ra[NPASS], rb[NPASS];
+  // load_stage issues raw, branch-free loads (invalid rows / k read a clamped in-bounds address and
+  // are zeroed at store time); the prologue transform runs in store_stage, after the MFMA block, so
+  // the global loads of stage k+1 stay in flight across the MFMAs of stage k.
+  // (measured: the cheap RMSNorm scale is best applied right at load time, GELU at store time)
+  constexpr bool RMS_EARLY = OT_GEMM_RMS_EARLY;
+  f32x4 ra[NPASS], rb[NPASS], gm;
+  bool kin = true;
   const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
   // NN B staging: lane reads W[k0 + kk][n0 + 4*n4 ...], kk = lane % GBK
   const int nn_kk = lane % GBK, nn_n4 = wave * (64 / GBK) + lane / GBK;
+  bool nnok[NPASS];
 
   auto load_stage = [&](int k0) {
-    const bool kin = !EDGE || (k0 + 4 * sc < p.K);
-    f32x4 gm = {1.f, 1.f, 1.f, 1.f};
-    if (ax == OT_AX_RMSNORM && kin) gm = *reinterpret_cast<const f32x4*>(p.a_gamma + k0 + 4 * sc);
+    kin = !EDGE || (k0 + 4 * sc < p.K);
+    const int ko = kin ? k0 : -4 * sc;                       // clamped: column 0 of the row
+    if (ax == OT_AX_RMSNORM) gm = *reinterpret_cast<const f32x4*>(p.a_gamma + ko + 4 * sc);
 #pragma unroll
-    for (int i = 0; i < NPASS; ++i) {
-      f32x4 v = zero4;
-      if (aok[i] && kin) v = *reinterpret_cast<const f32x4*>(arow[i] + k0);
-      if (ax == OT_AX_RMSNORM) {
-        v = v * gm * ars[i];
-      } else if (ax == OT_AX_GELU) {
-        v.x = gelu_erf(v.x); v.y = gelu_erf(v.y); v.z = gelu_erf(v.z); v.w = gelu_erf(v.w);
-      }
-      ra[i] = v;
+    for (int i = 0; i < NPASS; ++i) ra[i] = *reinterpret_cast<const f32x4*>(arow[i] + ko);
+    if (RMS_EARLY && ax == OT_AX_RMSNORM) {
+#pragma unroll
+      for (int i = 0; i < NPASS; ++i) ra[i] = ra[i] * gm * ars[i];
     }
     if (NT) {
 #pragma unroll
-      for (int i = 0; i < NPASS; ++i) rb[i] = (bok[i] && kin) ? *reinterpret_cast<const f32x4*>(brow[i] + k0) : zero4;
+      for (int i = 0; i < NPASS; ++i) rb[i] = *reinterpret_cast<const f32x4*>(brow[i] + ko);
     } else {
 #pragma unroll
       for (int i = 0; i < NPASS; ++i) {
         const int k = k0 + nn_kk, n = n0 + 4 * (nn_n4 + (256 / GBK) * i);
-        rb[i] = ((!EDGE || (k < p.K && n < p.N))) ? *reinterpret_cast<const f32x4*>(W + (int64_t)k * p.ldw + n) : zero4;
+        nnok[i] = !EDGE || (k < p.K && n < p.N);
+        rb[i] = *reinterpret_cast<const f32x4*>(W + (nnok[i] ? (int64_t)k * p.ldw + n : 0));
       }
     }
   };
@@ -136,18 +144,29 @@ __global__ __launch_bounds__(256, 2) void mixed_gemm_kernel(GemmArgs p) {
     float* as = As + buf * GT * GLD;
     float* bs = Bs + buf * GT * GLD;
 #pragma unroll
-    for (int i = 0; i < NPASS; ++i) *reinterpret_cast<f32x4*>(as + (sr + RPP * i) * GLD + 4 * sc) = ra[i];
+    for (int i = 0; i < NPASS; ++i) {
+      f32x4 v = ra[i];
+      if (!RMS_EARLY && ax == OT_AX_RMSNORM) {
+        v = v * gm * ars[i];
+      } else if (ax == OT_AX_GELU) {
+        v.x = gelu_erf(v.x); v.y = gelu_erf(v.y); v.z = gelu_erf(v.z); v.w = gelu_erf(v.w);
+      }
+      if (!(aok[i] && kin)) v = zero4;
+      *reinterpret_cast<f32x4*>(as + (sr + RPP * i) * GLD + 4 * sc) = v;
+    }
     if (NT) {
 #pragma unroll
-      for (int i = 0; i < NPASS; ++i) *reinterpret_cast<f32x4*>(bs + (sr + RPP * i) * GLD + 4 * sc) = rb[i];
+      for (int i = 0; i < NPASS; ++i)
+        *reinterpret_cast<f32x4*>(bs + (sr + RPP * i) * GLD + 4 * sc) = (bok[i] && kin) ? rb[i] : zero4;
     } else {
 #pragma unroll
       for (int i = 0; i < NPASS; ++i) {
         const int n = 4 * (nn_n4 + (256 / GBK) * i);
-        bs[(n + 0) * GLD + nn_kk] = rb[i].x;
-        bs[(n + 1) * GLD + nn_kk] = rb[i].y;
-        bs[(n + 2) * GLD + nn_kk] = rb[i].z;
-        bs[(n + 3) * GLD + nn_kk] = rb[i].w;
+        const f32x4 v = nnok[i] ? rb[i] : zero4;
+        bs[(n + 0) * GLD + nn_kk] = v.x;
+        bs[(n + 1) * GLD + nn_kk] = v.y;
+        bs[(n + 2) * GLD + nn_kk] = v.z;
+        bs[(n + 3) * GLD + nn_kk] = v.w;
       }
     }
   };
@@ -264,8 +283,24 @@ __global__ __launch_bounds__(256, 2) void mixed_gemm_kernel(GemmArgs p) {
 // ------------------------------------------------------------------------------------------
 // wgrad: partial slab per (chunk, k-tile, n-tile):  slab[c][k][n] = sum_{rows of chunk} A^T D
 // LDS images: As[k][r] and Ds[n][r] (r contiguous, BR = 32 rows per stage).
+// Default: row stride 36 (the ds_read_b128 fragment reads are conflict-free, the transposed
+// ds_write_b32 staging is 4-way conflicted).  OT_WGRAD_SWZ=1 with WLD=32 stores (k, r) at
+// k * WLD + (r ^ wswz(k)), conflict-free for both (tools/lds_conflicts.py), but measured slower on
+// the RMSNorm-prologue wgrads (82 -> 71 TF/s), so it stays off.
+#ifndef OT_WGRAD_WLD
+#define OT_WGRAD_WLD 36
+#endif
+#ifndef OT_WGRAD_SWZ
+#define OT_WGRAD_SWZ 0
+#endif
+#ifndef OT_WGRAD_LDS_EXTRA
+#define OT_WGRAD_LDS_EXTRA 0
+#endif
 constexpr int WBR = 32;
-constexpr int WLD = WBR + 4;
+constexpr int WLD = OT_WGRAD_WLD;
+__device__ __forceinline__ int wswz(int k) {
+  return OT_WGRAD_SWZ ? 4 * ((((k >> 1) ^ (k >> 4)) & 1) | ((k >> 2) & 2) | (k & 4)) : 0;
+}
 
 struct WgradArgs {
   const float* A; int64_t lda; const int32_t* a_rows; int a_xform; const float* a_rstd; const float* a_gamma;
@@ -293,6 +328,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
   const int h = lane >> 5, li = lane & 31;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
   const int sr = t >> 3, sc = t & 7;       // staging: row sr of the stage, float4 columns sc + 8i
+  const int swz = wswz(li);                // wm, wn, 32m are multiples of 32: the swizzle depends on li
   const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
 
   f32x16 acc[2][2];
@@ -305,33 +341,32 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
   float bsum = 0.f;
   const bool do_bias = p.bslab && tk == 0 && t < GT;
 
+  // row indices of a stage, raw (the in-range test is applied in load_stage, one stage later, so
+  // nothing waits on these loads before the MFMA block)
   auto rows_of = [&](int rs, int& ar, int& dr) {
     const int lr = rs + sr;
-    ar = -1; dr = -1;
-    if (lr < row_count) {
-      const int64_t mi = (int64_t)row_begin + lr;
-      ar = p.a_rows ? p.a_rows[mi] : (int)mi;
-      dr = p.d_rows ? p.d_rows[mi] : (int)mi;
-    }
-    if (ar < 0 || dr < 0) { ar = -1; dr = -1; }
+    const int64_t mi = (int64_t)row_begin + (lr < row_count ? lr : 0);
+    ar = p.a_rows ? p.a_rows[mi] : (int)mi;
+    dr = p.d_rows ? p.d_rows[mi] : (int)mi;
   };
-  f32x4 va[4], vd[4];
-  auto load_stage = [&](int ar, int dr) {
-    const float rsd = (ax == OT_AX_RMSNORM && ar >= 0) ? p.a_rstd[ar] : 1.f;
+  // raw branch-free loads (clamped addresses, masked at store time); the prologue transform runs in
+  // store_stage so stage st+1's loads stay in flight across stage st's MFMAs
+  f32x4 va[4], vd[4], gv[4];
+  float rsd = 1.f;
+  bool aok = false, dok = false;
+  auto load_stage = [&](int st, int ar, int dr) {
+    const bool in = st * WBR + sr < row_count && ar >= 0 && dr >= 0;
+    aok = in; dok = in;
+    const float* pa = p.A + (int64_t)(aok ? ar : 0) * p.lda;
+    const float* pd = p.D + (int64_t)(dok ? dr : 0) * p.ldd;
+    if (ax == OT_AX_RMSNORM) rsd = p.a_rstd[aok ? ar : 0];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int k = k0 + 4 * (sc + 8 * i), n = n0 + 4 * (sc + 8 * i);
-      f32x4 a = zero4, dv = zero4;
-      if (ar >= 0 && k < p.K) {
-        a = *reinterpret_cast<const f32x4*>(p.A + (int64_t)ar * p.lda + k);
-        if (ax == OT_AX_RMSNORM) {
-          a = a * *reinterpret_cast<const f32x4*>(p.a_gamma + k) * rsd;
-        } else if (ax == OT_AX_GELU) {
-          a.x = gelu_erf(a.x); a.y = gelu_erf(a.y); a.z = gelu_erf(a.z); a.w = gelu_erf(a.w);
-        }
-      }
-      if (dr >= 0 && n < p.N) dv = *reinterpret_cast<const f32x4*>(p.D + (int64_t)dr * p.ldd + n);
-      va[i] = a; vd[i] = dv;
+      const int kc = k < p.K ? k : 0, nc = n < p.N ? n : 0;
+      va[i] = *reinterpret_cast<const f32x4*>(pa + kc);
+      vd[i] = *reinterpret_cast<const f32x4*>(pd + nc);
+      if (ax == OT_AX_RMSNORM) gv[i] = *reinterpret_cast<const f32x4*>(p.a_gamma + kc);
     }
   };
   constexpr int NBUF = OT_WGRAD_DBUF ? 2 : 1;
@@ -341,10 +376,18 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int kk = 4 * (sc + 8 * i);
-      As[(kk + 0) * WLD + sr] = va[i].x; As[(kk + 1) * WLD + sr] = va[i].y;
-      As[(kk + 2) * WLD + sr] = va[i].z; As[(kk + 3) * WLD + sr] = va[i].w;
-      Ds[(kk + 0) * WLD + sr] = vd[i].x; Ds[(kk + 1) * WLD + sr] = vd[i].y;
-      Ds[(kk + 2) * WLD + sr] = vd[i].z; Ds[(kk + 3) * WLD + sr] = vd[i].w;
+      f32x4 a = va[i], dv = vd[i];
+      if (ax == OT_AX_RMSNORM) {
+        a = a * gv[i] * rsd;
+      } else if (ax == OT_AX_GELU) {
+        a.x = gelu_erf(a.x); a.y = gelu_erf(a.y); a.z = gelu_erf(a.z); a.w = gelu_erf(a.w);
+      }
+      if (!(aok && k0 + kk < p.K)) a = zero4;
+      if (!(dok && n0 + kk < p.N)) dv = zero4;
+      const int o0 = (kk + 0) * WLD + (sr ^ wswz(kk + 0)), o1 = (kk + 1) * WLD + (sr ^ wswz(kk + 1));
+      const int o2 = (kk + 2) * WLD + (sr ^ wswz(kk + 2)), o3 = (kk + 3) * WLD + (sr ^ wswz(kk + 3));
+      As[o0] = a.x; As[o1] = a.y; As[o2] = a.z; As[o3] = a.w;
+      Ds[o0] = dv.x; Ds[o1] = dv.y; Ds[o2] = dv.z; Ds[o3] = dv.w;
     }
   };
 
@@ -352,7 +395,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
   int ar, dr, ar2 = -1, dr2 = -1;
   rows_of(0, ar, dr);
   if (nst > 1) rows_of(WBR, ar2, dr2);
-  load_stage(ar, dr);
+  load_stage(0, ar, dr);
   store_stage(0);
   __syncthreads();
   for (int st = 0; st < nst; ++st) {
@@ -360,7 +403,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
     const bool more = st + 1 < nst;
     int ar3 = -1, dr3 = -1;
     if (more) {
-      load_stage(ar2, dr2);                               // stage st+1 data
+      load_stage(st + 1, ar2, dr2);                       // stage st+1 data
       if (st + 2 < nst) rows_of((st + 2) * WBR, ar3, dr3);   // stage st+2 row indices
     }
     const float* As = smem + cur * GT * WLD;
@@ -368,7 +411,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
     if (do_bias) {
 #pragma unroll
       for (int q = 0; q < WBR; q += 4) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(Ds + t * WLD + q);
+        const f32x4 v = *reinterpret_cast<const f32x4*>(Ds + t * WLD + (q ^ wswz(t)));
         bsum += (v.x + v.y) + (v.z + v.w);
       }
     }
@@ -378,8 +421,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
     for (int m = 0; m < 2; ++m)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        fa[m][q] = *reinterpret_cast<const f32x4*>(As + (wm + 32 * m + li) * WLD + 16 * h + 4 * q);
-        fb[m][q] = *reinterpret_cast<const f32x4*>(Ds + (wn + 32 * m + li) * WLD + 16 * h + 4 * q);
+        fa[m][q] = *reinterpret_cast<const f32x4*>(As + (wm + 32 * m + li) * WLD + ((16 * h + 4 * q) ^ swz));
+        fb[m][q] = *reinterpret_cast<const f32x4*>(Ds + (wn + 32 * m + li) * WLD + ((16 * h + 4 * q) ^ swz));
       }
 #pragma unroll
     for (int s = 0; s < 16; ++s)
@@ -588,7 +631,7 @@ extern "C" int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a
   if (nchunks > 0) {
     WgradArgs p{A, lda, a_rows, a_xform, a_rstd, a_gamma, D, ldd, d_rows, K, N, chunks, nchunks, slab, bslab,
                 (int)ceil_div(K, GT), (int)ceil_div(N, GT)};
-    const size_t shmem = (OT_WGRAD_DBUF ? 4 : 2) * GT * WLD * sizeof(float);
+    const size_t shmem = (OT_WGRAD_DBUF ? 4 : 2) * GT * WLD * sizeof(float) + OT_WGRAD_LDS_EXTRA;
     void (*kern)(WgradArgs) = a_xform == OT_AX_NONE      ? wgrad_kernel<OT_AX_NONE>
                               : a_xform == OT_AX_RMSNORM ? wgrad_kernel<OT_AX_RMSNORM>
                               : a_xform == OT_AX_GELU    ? wgrad_kernel<OT_AX_GELU>
@@ -597,7 +640,7 @@ extern "C" int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a
     std::call_once(lds_once, [] {
       for (void (*k)(WgradArgs) : {wgrad_kernel<OT_AX_NONE>, wgrad_kernel<OT_AX_RMSNORM>, wgrad_kernel<OT_AX_GELU>,
                                    wgrad_kernel<-1>})
-        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * GT * WLD * 4);
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * GT * WLD * 4 + OT_WGRAD_LDS_EXTRA);
       (void)hipGetLastError();
     });
     hipLaunchKernelGGL(kern, dim3((unsigned)nchunks * p.ntk * p.ntn), dim3(256), shmem, s, p);

@@ -121,20 +121,22 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(RmsBwdArgs p) {
   }
 }
 
-// out[c] (+)= sum_{b < nparts} part[b][c]   (fixed order: deterministic).  Block = 64 columns x 4
-// row-groups; each wave reads 64 consecutive columns of a partial row (coalesced).
+// out[c] (+)= sum_{b < nparts} part[b][c]   (fixed order: deterministic).  Block = 16 columns x 16
+// part-groups (group q sums parts q, q+16, ...), combined in a fixed order through LDS.
 __global__ __launch_bounds__(256) void colsum_reduce_kernel(const float* __restrict__ part, int64_t nparts, int ncols,
                                                             float* out, int accumulate) {
-  __shared__ float red[4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int rg = threadIdx.x >> 6;
+  __shared__ float red[16][17];
+  const int cc = threadIdx.x & 15, q = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cc;
   float s = 0.f;
   if (c < ncols)
-    for (int64_t b = rg; b < nparts; b += 4) s += part[b * ncols + c];
-  red[rg][threadIdx.x & 63] = s;
+    for (int64_t b = q; b < nparts; b += 16) s += part[b * ncols + c];
+  red[q][cc] = s;
   __syncthreads();
-  if (threadIdx.x < 64 && c < ncols) {
-    const float t = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+  if (q == 0 && c < ncols) {
+    float t = red[0][cc];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) t += red[k][cc];
     out[c] = accumulate ? out[c] + t : t;
   }
 }
@@ -228,7 +230,7 @@ extern "C" int ot_rmsnorm_bwd(const float* dy, int64_t lddy, const float* x, int
   hipLaunchKernelGGL(rmsnorm_bwd_kernel, dim3(grid), dim3(256), shmem, (hipStream_t)stream, p);
   OT_LAUNCH_CHECK("ot_rmsnorm_bwd");
   if (dgamma) {
-    hipLaunchKernelGGL(colsum_reduce_kernel, dim3(ceil_div(d, 64)), dim3(256), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(colsum_reduce_kernel, dim3(ceil_div(d, 16)), dim3(256), 0, (hipStream_t)stream,
                        (const float*)workspace, (int64_t)grid, d, dgamma, accumulate_dgamma);
     OT_LAUNCH_CHECK("ot_rmsnorm_bwd(reduce)");
   }
@@ -261,7 +263,7 @@ extern "C" int ot_rows_colsum(const float* src, int64_t ld, const int32_t* rows,
                        src, ld, rows, nrows, ncols, 256, (float*)workspace);
     OT_LAUNCH_CHECK("ot_rows_colsum");
   }
-  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(ceil_div(ncols, 64)), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(ceil_div(ncols, 16)), dim3(256), 0, (hipStream_t)stream,
                      (const float*)workspace, (int64_t)nb, ncols, out, accumulate);
   OT_LAUNCH_CHECK("ot_rows_colsum(reduce)");
   return OT_OK;

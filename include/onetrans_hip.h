@@ -99,7 +99,9 @@ int ot_transpose_banks(const float* src, float* dst, const int64_t* banks_dev, i
  * qkv: [B*I, ld] (q | k | v, head h at +h*head_dim); out: [B*K, H*head_dim]; lse: [B, H, K]. */
 int ot_attn_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, int head_dim,
                 float* out, float* lse, void* stream);
-/* dqkv: like qkv (dq written on the K tail rows only; dk, dv on all rows); delta_ws: B*H*K floats */
+/* dqkv: like qkv (dq written on the K tail rows only; dk, dv on all rows);
+ * ws: ot_attn_bwd_workspace_size(B, H, K) bytes (row stats padded to 32 queries per (b, h)) */
+int64_t ot_attn_bwd_workspace_size(int B, int H, int K);
 int ot_attn_bwd(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
                 int B, int H, int I, int K, int head_dim, float* dqkv, float* delta_ws, void* stream);
 

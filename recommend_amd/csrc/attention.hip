@@ -185,11 +185,28 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs p) {
   }
 }
 
-// delta[b,h,j] = sum_d dO[b*K+j][h*hd+d] * O[b*K+j][h*hd+d]: one float4 per thread (coalesced rows),
-// reduced over the hd/4 lanes of a head with shuffles.
+// Row statistics of the backward, padded to KP = round_up(K, 32) queries per (b, h) so the main
+// kernel reads them as aligned float4 without bounds checks:
+//   ws[0 .. BH*KP)       lse  (padding +inf: P = exp(s - inf) = 0 masks the padded queries)
+//   ws[BH*KP .. 2*BH*KP) delta[b,h,j] = sum_d dO[b*K+j][h*hd+d] * O[b*K+j][h*hd+d]   (padding 0)
+// Threads of the first `main` blocks take one float4 of [B*K, d] each (coalesced rows), reduced over
+// the hd/4 lanes of a head with shuffles; the remaining blocks fill the padding.
+__host__ __device__ constexpr int attn_kpad(int K) { return (K + 31) / 32 * 32; }
+
 __global__ __launch_bounds__(256) void attn_bwd_prep_kernel(const float* __restrict__ o, const float* __restrict__ dout,
-                                                            float* delta, int B, int H, int K, int hd) {
-  const int d = H * hd;
+                                                            const float* __restrict__ lse, float* ws, int B, int H,
+                                                            int K, int hd, int main_blocks) {
+  const int d = H * hd, KP = attn_kpad(K);
+  const int64_t BHKP = (int64_t)B * H * KP;
+  if ((int)blockIdx.x >= main_blocks) {
+    const int pad = KP - K;
+    const int64_t e = ((int64_t)blockIdx.x - main_blocks) * blockDim.x + threadIdx.x;   // [B*H][pad]
+    if (pad == 0 || e >= (int64_t)B * H * pad) return;
+    const int64_t bh = e / pad, j = K + e % pad;
+    ws[bh * KP + j] = INFINITY;
+    ws[BHKP + bh * KP + j] = 0.f;
+    return;
+  }
   const int64_t i4 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;   // element index in [B*K, d]
   const bool live = i4 < (int64_t)B * K * d;
   float s = 0.f;
@@ -203,27 +220,35 @@ __global__ __launch_bounds__(256) void attn_bwd_prep_kernel(const float* __restr
   if (live && (c % hd) == 0) {
     const int64_t row = i4 / d;
     const int64_t b = row / K, j = row % K;
-    delta[(b * H + c / hd) * K + j] = s;
+    const int64_t bh = b * H + c / hd;
+    ws[bh * KP + j] = lse[bh * K + j];
+    ws[BHKP + bh * KP + j] = s;
   }
 }
 
 // ------------------------------------------------------------------------------------------
 // Backward, one pass per (sample, head) wave: key blocks outer, the query blocks that see them
 // inner.  S and dP are computed with the key on the lane, so P and dS feed dV^T += dO^T P and
-// dK^T += Q^T dS directly (dO and Q blocks read transposed from per-wave LDS tiles).  dS is also
-// written to an LDS tile [query][key] and read back as the A operand of dQ += dS K (K block from
-// its LDS tile), accumulated in place in dqkv: the wave owns the (b, h) slice, its first key block
-// (seen by every query) stores and later ones read-modify-write the same lanes' addresses.
-// No atomics, no recompute pass, deterministic.
+// dK^T += Q^T dS directly (dO and Q blocks read transposed from per-wave LDS tiles).  dS (pre-scaled
+// by 1/sqrt(hd)) is also written to an LDS tile [query][key] and read back as the B operand of
+// dQ^T += K^T dS^T (K block from its LDS tile); the dQ^T accumulator has the query on the lane, so
+// the running partial in dqkv is read / written as whole float4 row pieces.  The wave owns its
+// (b, h) slice: the first key block (seen by every query) stores, later ones read-modify-write the
+// same lanes' addresses.  No atomics, no recompute pass, deterministic.
+//
+// Padding is branch-free: rows past the end (keys >= I, queries >= K) are loaded from a clamped
+// in-bounds row; padded keys are removed by the causal select, padded queries by lse = +inf.
 
-// 4 consecutive values v[j0..j0+3] (j0 % 4 == 0) with bounds: vector load when fully in range
-__device__ __forceinline__ f32x4 load4(const float* v, int j0, int n) {
-  if (j0 + 3 < n) return *reinterpret_cast<const f32x4*>(v + j0);
-  f32x4 r = {0.f, 0.f, 0.f, 0.f};
-  if (j0 < n) r.x = v[j0];
-  if (j0 + 1 < n) r.y = v[j0 + 1];
-  if (j0 + 2 < n) r.z = v[j0 + 2];
-  return r;
+// Fragment as load_frag, but rows >= nrows read row nrows - 1 (finite data that the masks null).
+template <int HD>
+__device__ __forceinline__ void load_frag_clamped(float (&f)[HD / 2], const float* base, int64_t ld, int row,
+                                                  int nrows, int hh) {
+  const float* p = base + (int64_t)(row < nrows ? row : nrows - 1) * ld + (HD / 2) * hh;
+#pragma unroll
+  for (int q = 0; q < HD / 8; ++q) {
+    f32x4 v = *reinterpret_cast<const f32x4*>(p + 4 * q);
+    f[4 * q] = v.x; f[4 * q + 1] = v.y; f[4 * q + 2] = v.z; f[4 * q + 3] = v.w;
+  }
 }
 
 template <int HD>
@@ -234,6 +259,9 @@ __global__ __launch_bounds__(64 * BWD_WAVES<HD>(), 2) void attn_bwd_kernel(AttnA
   constexpr int LD = TLD<HD>();
   constexpr int SLD = 36;                  // dS tile row stride (32 keys + pad)
   constexpr int PER_WAVE = 3 * 32 * LD + 32 * SLD;
+  // (HD <= 32: the dQ partial is loaded at the start of a pair; larger HD reads it at the end, as
+  // the registers of a live seed would not fit next to the dK / dV accumulators)
+  constexpr bool SEED_EARLY = HD <= 32;
   __shared__ __attribute__((aligned(16))) float lds[BWD_WAVES<HD>() * PER_WAVE];
   const int lane = threadIdx.x & 63, li = lane & 31, hh = lane >> 5;
   float* tO = lds + (threadIdx.x >> 6) * PER_WAVE;   // dO block   [query][dim]
@@ -243,27 +271,27 @@ __global__ __launch_bounds__(64 * BWD_WAVES<HD>(), 2) void attn_bwd_kernel(AttnA
   const int pair = blockIdx.x * BWD_WAVES<HD>() + (threadIdx.x >> 6);
   if (pair >= p.B * p.H) return;
   const int b = pair / p.H, h = pair % p.H;
-  const int I = p.I, K = p.K, q_off = I - K;
+  const int I = p.I, K = p.K, q_off = I - K, KP = attn_kpad(K);
   const int64_t tok0 = (int64_t)b * I;
   const float* Q = p.qkv + tok0 * p.ld + h * HD;
   const float* Kp = Q + p.d;
   const float* V = Q + 2 * p.d;
   const float* Qt = Q + (int64_t)q_off * p.ld;
   const float* dO = p.dout + (int64_t)b * K * p.d + h * HD;
-  const float* lse = p.lse + ((int64_t)b * p.H + h) * K;
-  const float* delta = p.delta + ((int64_t)b * p.H + h) * K;   // rowsum(dO * O), attn_bwd_prep_kernel
+  const float* lsep = p.delta + (int64_t)pair * KP;                              // padded lse
+  const float* dltp = p.delta + ((int64_t)p.B * p.H + pair) * KP;                // padded delta
   float* dQt = p.dqkv + (tok0 + q_off) * p.ld + h * HD;
   float* dK = p.dqkv + tok0 * p.ld + p.d + h * HD;
   float* dV = dK + p.d;
-  const int nqb = (K + 31) / 32;
+  const int nqb = KP / 32;
   const int nkb = (I + 31) / 32;
 
   for (int kb = 0; kb < nkb; ++kb) {
     const int key0 = 32 * kb;
     const int kpos = key0 + li;                        // this lane's key
     float kf[HD / 2], vf[HD / 2];
-    load_frag<HD>(kf, Kp, p.ld, kpos, I, hh);
-    load_frag<HD>(vf, V, p.ld, kpos, I, hh);
+    load_frag_clamped<HD>(kf, Kp, p.ld, kpos, I, hh);
+    load_frag_clamped<HD>(vf, V, p.ld, kpos, I, hh);
     frag_to_lds<HD>(tK, kf, li, hh);
     f32x16 dk[NB(HD)], dv[NB(HD)];
 #pragma unroll
@@ -272,43 +300,58 @@ __global__ __launch_bounds__(64 * BWD_WAVES<HD>(), 2) void attn_bwd_kernel(AttnA
       for (int r = 0; r < 16; ++r) { dk[c][r] = 0.f; dv[c][r] = 0.f; }
     int qb0 = key0 - q_off; qb0 = qb0 < 0 ? 0 : qb0 / 32;      // first query block that sees key0
     float qf[HD / 2], of[HD / 2];
-    load_frag<HD>(qf, Qt, p.ld, 32 * qb0 + li, K, hh);
-    load_frag<HD>(of, dO, p.d, 32 * qb0 + li, K, hh);
+    f32x4 l4[4], d4[4];
+    auto load_qblock = [&](int q0) {
+      load_frag_clamped<HD>(qf, Qt, p.ld, q0 + li, K, hh);
+      load_frag_clamped<HD>(of, dO, p.d, q0 + li, K, hh);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        l4[g] = *reinterpret_cast<const f32x4*>(lsep + q0 + 8 * g + 4 * hh);
+        d4[g] = *reinterpret_cast<const f32x4*>(dltp + q0 + 8 * g + 4 * hh);
+      }
+    };
+    load_qblock(32 * qb0);
     for (int qb = qb0; qb < nqb; ++qb) {
       const int q0 = 32 * qb;
+      // dQ^T block: lane = query q0 + li, register r = dim 32c + acc_row(r, hh) (4 float4 per lane)
+      const int jq = q0 + li;
+      float* dqrow = dQt + (int64_t)(jq < K ? jq : K - 1) * p.ld + 4 * hh;
+      f32x16 dq[NB(HD)];
+#pragma unroll
+      for (int c = 0; c < NB(HD); ++c)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int dd = 32 * c + 8 * g;
+          f32x4 v = {0.f, 0.f, 0.f, 0.f};
+          if (SEED_EARLY && kb > 0 && dd < HD) v = *reinterpret_cast<const f32x4*>(dqrow + dd);
+          dq[c][4 * g] = v.x; dq[c][4 * g + 1] = v.y; dq[c][4 * g + 2] = v.z; dq[c][4 * g + 3] = v.w;
+        }
       __builtin_amdgcn_wave_barrier();
       frag_to_lds<HD>(tO, of, li, hh);
       frag_to_lds<HD>(tQ, qf, li, hh);
       f32x16 s = mm_frag<HD>(qf, kf);                  // S: row = query, col = key
       f32x16 dp = mm_frag<HD>(of, vf);                 // dP: row = query, col = key
-      if (qb + 1 < nqb) {                              // prefetch the next query block
-        load_frag<HD>(qf, Qt, p.ld, q0 + 32 + li, K, hh);
-        load_frag<HD>(of, dO, p.d, q0 + 32 + li, K, hh);
-      }
+      f32x4 lc[4], dc[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) { lc[g] = l4[g]; dc[g] = d4[g]; }
+      if (qb + 1 < nqb) load_qblock(q0 + 32);          // prefetch the next query block
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int j0 = q0 + 8 * g + 4 * hh;
-        const f32x4 l4 = load4(lse, j0, K), d4 = load4(delta, j0, K);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int r = 4 * g + e, j = j0 + e;
-          const bool ok = j < K && kpos <= q_off + j;
-          const float P = ok ? __expf(s[r] * p.scale - l4[e]) : 0.f;
+          const int r = 4 * g + e, j = q0 + 8 * g + 4 * hh + e;
+          const float ex = __expf(s[r] * p.scale - lc[g][e]);
+          const float P = kpos <= q_off + j ? ex : 0.f;
           s[r] = P;
-          dp[r] = ok ? P * (dp[r] - d4[e]) : 0.f;
+          dp[r] = P * (dp[r] - dc[g][e]) * p.scale;    // dS, pre-scaled by 1/sqrt(hd)
           tS[(8 * g + 4 * hh + e) * SLD + li] = dp[r];
         }
       }
       __builtin_amdgcn_wave_barrier();
       acc_tile_p<HD>(dv, tO, s, li, hh);               // dV^T += dO^T P
       acc_tile_p<HD>(dk, tQ, dp, li, hh);              // dK^T += Q^T dS
-      // dQ[q][d] += sum_key dS[q][key] K[key][d]: A = dS (lane = query, k = key 16hh + s),
-      // B = K (k = key, lane = dim)
-      f32x16 dq[NB(HD)];
-#pragma unroll
-      for (int c = 0; c < NB(HD); ++c)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) dq[c][r] = 0.f;
+      // dQ^T[d][q] += sum_key K[key][d] dS[q][key]: A = K^T (row = dim, k = key, from tK),
+      // B = dS^T (k = key 16hh + s, col = query = lane, from tS)
 #pragma unroll
       for (int q4 = 0; q4 < 4; ++q4) {
         const f32x4 a4 = *reinterpret_cast<const f32x4*>(tS + li * SLD + 16 * hh + 4 * q4);
@@ -319,23 +362,21 @@ __global__ __launch_bounds__(64 * BWD_WAVES<HD>(), 2) void attn_bwd_kernel(AttnA
           for (int c = 0; c < NB(HD); ++c) {
             const int dd = 32 * c + li;
             const float bk = dd < HD ? tK[key * LD + dd] : 0.f;
-            dq[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[e], bk, dq[c], 0, 0, 0);
+            dq[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(bk, a4[e], dq[c], 0, 0, 0);
           }
         }
       }
-      // acc row = query (q0 + acc_row), col = dim: accumulate into dqkv (first key block stores)
+      if (jq < K) {                                      // the running dQ partial
 #pragma unroll
-      for (int c = 0; c < NB(HD); ++c) {
-        const int dd = 32 * c + li;
-        if (dd >= HD) continue;
+        for (int c = 0; c < NB(HD); ++c)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int j = q0 + acc_row(r, hh);
-          if (j >= K) continue;
-          float* dst = dQt + (int64_t)j * p.ld + dd;
-          const float v = dq[c][r] * p.scale;
-          *dst = kb == 0 ? v : *dst + v;
-        }
+          for (int g = 0; g < 4; ++g) {
+            const int dd = 32 * c + 8 * g;
+            if (dd >= HD) continue;
+            f32x4 v = {dq[c][4 * g], dq[c][4 * g + 1], dq[c][4 * g + 2], dq[c][4 * g + 3]};
+            if (!SEED_EARLY && kb > 0) v = *reinterpret_cast<const f32x4*>(dqrow + dd) + v;
+            *reinterpret_cast<f32x4*>(dqrow + dd) = v;
+          }
       }
     }
     if (kpos < I) {
@@ -345,14 +386,90 @@ __global__ __launch_bounds__(64 * BWD_WAVES<HD>(), 2) void attn_bwd_kernel(AttnA
         for (int g = 0; g < 4; ++g) {
           const int dd = 32 * c + 8 * g + 4 * hh;
           if (dd < HD) {
-            f32x4 a = {dk[c][4 * g] * p.scale, dk[c][4 * g + 1] * p.scale, dk[c][4 * g + 2] * p.scale,
-                       dk[c][4 * g + 3] * p.scale};
+            f32x4 a = {dk[c][4 * g], dk[c][4 * g + 1], dk[c][4 * g + 2], dk[c][4 * g + 3]};
             f32x4 v = {dv[c][4 * g], dv[c][4 * g + 1], dv[c][4 * g + 2], dv[c][4 * g + 3]};
             *reinterpret_cast<f32x4*>(dK + (int64_t)kpos * p.ld + dd) = a;
             *reinterpret_cast<f32x4*>(dV + (int64_t)kpos * p.ld + dd) = v;
           }
         }
     }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Backward for a short query tail (K <= SMALL_K, e.g. the last layer's single query after DCE):
+// HBM-bound (read K/V rows, write dK/dV rows), so VALU instead of 32x32 MFMA tiles that would be
+// 1/32 occupied.  One wave per (sample, head); HD/4 lanes per key (one float4 of dims each), 64/(HD/4)
+// keys per pass; dot products reduced over the key's lanes with xor shuffles.  dQ partials are
+// reduced over the wave's key slots at the end.
+constexpr int SMALL_K = 4;
+
+template <int HD>
+__global__ __launch_bounds__(256) void attn_bwd_small_kernel(AttnArgs p) {
+  constexpr int LPK = HD / 4, KPW = 64 / LPK;
+  const int lane = threadIdx.x & 63, sub = lane % LPK, slot = lane / LPK;
+  const int pair = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (pair >= p.B * p.H) return;
+  const int b = pair / p.H, h = pair % p.H;
+  const int I = p.I, K = p.K, q_off = I - K;
+  const int64_t tok0 = (int64_t)b * I;
+  const float* Q = p.qkv + tok0 * p.ld + h * HD + 4 * sub;
+  const float* Kp = Q + p.d;
+  const float* V = Q + 2 * p.d;
+  float* dK = p.dqkv + tok0 * p.ld + p.d + h * HD + 4 * sub;
+  float* dV = dK + p.d;
+  f32x4 q[SMALL_K], o[SMALL_K], dq[SMALL_K];
+  float lse[SMALL_K], delta[SMALL_K];
+#pragma unroll
+  for (int j = 0; j < SMALL_K; ++j) {
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    q[j] = z; o[j] = z; dq[j] = z; lse[j] = 0.f; delta[j] = 0.f;
+    if (j < K) {
+      q[j] = *reinterpret_cast<const f32x4*>(Q + (int64_t)(q_off + j) * p.ld);
+      o[j] = *reinterpret_cast<const f32x4*>(p.dout + ((int64_t)b * K + j) * p.d + h * HD + 4 * sub);
+      lse[j] = p.delta[(int64_t)pair * attn_kpad(K) + j];
+      delta[j] = p.delta[((int64_t)p.B * p.H + pair) * attn_kpad(K) + j];
+    }
+  }
+  for (int key0 = 0; key0 < I; key0 += KPW) {
+    const int key = key0 + slot;
+    const bool live = key < I;
+    const int64_t ro = (int64_t)(live ? key : 0) * p.ld;
+    const f32x4 kv = *reinterpret_cast<const f32x4*>(Kp + ro);
+    const f32x4 vv = *reinterpret_cast<const f32x4*>(V + ro);
+    f32x4 dk = {0.f, 0.f, 0.f, 0.f}, dv = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < SMALL_K; ++j) {
+      if (j >= K) break;
+      float sdot = q[j].x * kv.x + q[j].y * kv.y + q[j].z * kv.z + q[j].w * kv.w;
+      float pdot = o[j].x * vv.x + o[j].y * vv.y + o[j].z * vv.z + o[j].w * vv.w;
+#pragma unroll
+      for (int off = 1; off < LPK; off <<= 1) {
+        sdot += __shfl_xor(sdot, off, 64);
+        pdot += __shfl_xor(pdot, off, 64);
+      }
+      const bool vis = live && key <= q_off + j;
+      const float P = vis ? __expf(sdot * p.scale - lse[j]) : 0.f;
+      const float ds = vis ? P * (pdot - delta[j]) * p.scale : 0.f;
+      dv += P * o[j];
+      dk += ds * q[j];
+      dq[j] += ds * kv;
+    }
+    if (live) {
+      *reinterpret_cast<f32x4*>(dK + ro) = dk;
+      *reinterpret_cast<f32x4*>(dV + ro) = dv;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < SMALL_K; ++j) {
+    if (j >= K) break;
+    f32x4 v = dq[j];
+#pragma unroll
+    for (int off = LPK; off < 64; off <<= 1) {
+      v.x += __shfl_xor(v.x, off, 64); v.y += __shfl_xor(v.y, off, 64);
+      v.z += __shfl_xor(v.z, off, 64); v.w += __shfl_xor(v.w, off, 64);
+    }
+    if (slot == 0) *reinterpret_cast<f32x4*>(p.dqkv + (tok0 + q_off + j) * p.ld + h * HD + 4 * sub) = v;
   }
 }
 
@@ -383,6 +500,10 @@ extern "C" int ot_attn_fwd(const float* qkv, int64_t ld, int B, int H, int I, in
   return OT_OK;
 }
 
+extern "C" int64_t ot_attn_bwd_workspace_size(int B, int H, int K) {
+  return 2 * (int64_t)B * H * attn_kpad(K) * (int64_t)sizeof(float);
+}
+
 extern "C" int ot_attn_bwd(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
                            int B, int H, int I, int K, int head_dim, float* dqkv, float* delta_ws,
                            void* stream) {
@@ -392,12 +513,19 @@ extern "C" int ot_attn_bwd(const float* qkv, int64_t ld, const float* out, const
   if (B == 0) return OT_OK;
   AttnArgs p{qkv, ld, H * head_dim, out, dout, nullptr, const_cast<float*>(lse), dqkv, delta_ws, B, H, I, K,
              1.f / sqrtf((float)head_dim)};
-  hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3(ceil_div((int64_t)B * K * H * head_dim / 4, 256)), dim3(256), 0,
-                     (hipStream_t)stream, out, dout, delta_ws, B, H, K, head_dim);
+  const int main_blocks = (int)ceil_div((int64_t)B * K * H * head_dim / 4, 256);
+  const int pad_blocks = (int)ceil_div((int64_t)B * H * (attn_kpad(K) - K), 256);
+  hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3(main_blocks + pad_blocks), dim3(256), 0, (hipStream_t)stream, out,
+                     dout, lse, delta_ws, B, H, K, head_dim, main_blocks);
   OT_LAUNCH_CHECK("ot_attn_bwd(prep)");
-  const int waves = head_dim >= 128 ? 2 : 4;
-  const unsigned grid = ceil_div((int64_t)B * H, waves);
-  OT_ATTN_DISPATCH(attn_bwd_kernel, head_dim, dim3(grid), dim3(64 * waves), 0, (hipStream_t)stream, p);
+  if (K <= SMALL_K) {
+    OT_ATTN_DISPATCH(attn_bwd_small_kernel, head_dim, dim3(ceil_div((int64_t)B * H, 4)), dim3(256), 0,
+                     (hipStream_t)stream, p);
+  } else {
+    const int waves = head_dim >= 128 ? 2 : 4;
+    const unsigned grid = ceil_div((int64_t)B * H, waves);
+    OT_ATTN_DISPATCH(attn_bwd_kernel, head_dim, dim3(grid), dim3(64 * waves), 0, (hipStream_t)stream, p);
+  }
   OT_LAUNCH_CHECK("ot_attn_bwd");
   return OT_OK;
 }

@@ -217,6 +217,80 @@ __global__ __launch_bounds__(256, 2) void mixed_gemm_kernel(GemmArgs p) {
   // ---- epilogue (flags compile-time unless EPIT < 0).  Per 32-row block m: resolve the 16 output
   // rows of this lane, issue every operand load (aux / residual / accumulate source) for the block,
   // then compute and store — no load-use chains per element.
+  if constexpr (!EDGE && EPIT >= 0) {
+    // ---- vector epilogue: the accumulator tile goes through LDS (the staging buffers are free: the
+    // last main-loop barrier ended every read) in two 64-row halves; each thread then finishes 8
+    // rows x one float4 column chunk, so every global access is a 16-B piece of a 512-B row run and
+    // each row index is loaded once per row instead of once per element.  Operand loads of a batch
+    // of rows are issued together.
+    constexpr int CLD = GT + 4;
+    float* ct = smem;                                   // [64][CLD]
+    const int c4 = t & 31, rb = t >> 5;                 // float4 column chunk, first local row
+    const int col = n0 + 4 * c4;
+    f32x4 bias4 = {0.f, 0.f, 0.f, 0.f};
+    if (epi & OT_EPI_BIAS) bias4 = *reinterpret_cast<const f32x4*>(p.bias + (int64_t)g * p.bias_gstride + col);
+    const bool need_tok = (epi & OT_EPI_DROPOUT) || ((epi & OT_EPI_RESIDUAL) && p.res_tok);
+    int orow[2][8];
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int lr = rb + 8 * i;                      // local row of the half: tile row below
+        const int64_t gr = (int64_t)tm * GT + (lr >> 5) * 64 + 32 * hf + (lr & 31);
+        orow[hf][i] = p.out_rows ? p.out_rows[gr] : (int)gr;
+      }
+    constexpr int RB = 8;                               // rows per operand-load batch
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          ct[((wave >> 1) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * CLD + wn + 32 * n + li] = acc[hf][n][r];
+      __syncthreads();
+#pragma unroll
+      for (int i0 = 0; i0 < 8; i0 += RB) {
+        int64_t tok[RB];
+        f32x4 aux4[RB], res4[RB], cp4[RB];
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+          const int orr = orow[hf][i0 + i];
+          const int64_t o = orr < 0 ? 0 : orr;
+          tok[i] = (need_tok && orr >= 0) ? tail_token(orr, p.tail_K, p.tail_I) : o;
+          if (epi & OT_EPI_GELU_BWD) aux4[i] = *reinterpret_cast<const f32x4*>(p.aux + o * p.ldaux + col);
+          if (epi & OT_EPI_RESIDUAL)
+            res4[i] = *reinterpret_cast<const f32x4*>(p.res + (p.res_tok ? tok[i] : o) * p.ldres + col);
+          if (epi & OT_EPI_ACCUMULATE) cp4[i] = *reinterpret_cast<const f32x4*>(p.C + o * p.ldc + col);
+        }
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+          const int orr = orow[hf][i0 + i];
+          f32x4 v = *reinterpret_cast<const f32x4*>(ct + (rb + 8 * (i0 + i)) * CLD + 4 * c4);
+          if (epi & OT_EPI_BIAS) v += bias4;
+          if (epi & OT_EPI_GELU_BWD) {
+            v.x *= gelu_erf_grad(aux4[i].x); v.y *= gelu_erf_grad(aux4[i].y);
+            v.z *= gelu_erf_grad(aux4[i].z); v.w *= gelu_erf_grad(aux4[i].w);
+          }
+          if (epi & OT_EPI_GELU) {
+            v.x = gelu_erf(v.x); v.y = gelu_erf(v.y); v.z = gelu_erf(v.z); v.w = gelu_erf(v.w);
+          }
+          if (epi & OT_EPI_DROPOUT) {
+            const uint32_t idx = (uint32_t)(tok[i] * p.drop_width + col);
+            v.x = drop_keep(p.seed, p.site, idx + 0, p.drop_thr) ? v.x * p.drop_scale : 0.f;
+            v.y = drop_keep(p.seed, p.site, idx + 1, p.drop_thr) ? v.y * p.drop_scale : 0.f;
+            v.z = drop_keep(p.seed, p.site, idx + 2, p.drop_thr) ? v.z * p.drop_scale : 0.f;
+            v.w = drop_keep(p.seed, p.site, idx + 3, p.drop_thr) ? v.w * p.drop_scale : 0.f;
+          }
+          if (epi & OT_EPI_RESIDUAL) v += res4[i];
+          if (epi & OT_EPI_ACCUMULATE) v += cp4[i];
+          if (orr >= 0) *reinterpret_cast<f32x4*>(p.C + (int64_t)orr * p.ldc + col) = v;
+        }
+      }
+      __syncthreads();                                  // ct is rewritten by the next half
+    }
+    return;
+  }
+  // ---- scalar epilogue (EDGE: N % 128 != 0 or unaligned operands; generic run-time flags)
   float bias_v[2] = {0.f, 0.f};
   int cols[2];
 #pragma unroll
@@ -572,7 +646,11 @@ extern "C" int ot_mixed_gemm(int mode, const float* A, int64_t lda, int K, const
     p.drop_scale = 1.f / (1.f - drop_rate);
   }
   const size_t shmem = 4 * GT * GLD * sizeof(float);
-  const bool edge = (K % GBK) != 0 || (N % GT) != 0;
+  auto a16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+  const bool vec_ok = ldc % 4 == 0 && a16(C) && (!(epi & OT_EPI_RESIDUAL) || (ldres % 4 == 0 && a16(res))) &&
+                      (!(epi & OT_EPI_GELU_BWD) || (ldaux % 4 == 0 && a16(aux))) &&
+                      (!(epi & OT_EPI_BIAS) || (bias_gstride % 4 == 0 && a16(bias)));
+  const bool edge = (K % GBK) != 0 || (N % GT) != 0 || !vec_ok;
   const unsigned nwg = (unsigned)ntiles * p.ntn;
   hipStream_t s = (hipStream_t)stream;
   void (*kern)(GemmArgs) = nullptr;

@@ -120,7 +120,7 @@ def attn_fwd(qkv: torch.Tensor, ld: int, B: int, H: int, I: int, K: int, hd: int
 
 
 def attn_bwd(qkv, ld, out, dout, lse, B, H, I, K, hd, dqkv) -> None:
-    delta = torch.empty(max(B * H * K, 1), dtype=torch.float32, device=qkv.device)
+    delta = workspace(size('ot_attn_bwd_workspace_size', B, H, K), qkv.device)
     ev = _probe.begin() if _probe is not None else None
     call('ot_attn_bwd', ptr(qkv), ld, ptr(out), ptr(dout), ptr(lse), B, H, I, K, hd, ptr(dqkv), ptr(delta),
          stream())

@@ -161,7 +161,10 @@ def attn_ref(qkv, B, H, I, Kq, hd):
 
 
 @pytest.mark.parametrize('B,H,I,Kq,hd', [(3, 4, 140, 140, 32), (2, 4, 140, 1, 32), (2, 2, 70, 33, 64),
-                                         (3, 4, 40, 40, 16), (1, 2, 33, 17, 128), (2, 4, 5, 5, 32)])
+                                         (3, 4, 40, 40, 16), (1, 2, 33, 17, 128), (2, 4, 5, 5, 32),
+                                         # short tails (VALU backward): K <= 4
+                                         (2, 4, 140, 3, 32), (2, 2, 70, 4, 64), (2, 2, 33, 2, 128),
+                                         (3, 4, 40, 1, 16), (2, 4, 5, 5 - 1, 32)])
 def test_attention(dev, B, H, I, Kq, hd):
     torch.manual_seed(0)
     d = H * hd

@@ -21,5 +21,8 @@ def run(B, H, I, Kq, hd):
             e0.record(); fn(); e1.record(); torch.cuda.synchronize(); ts.append(e0.elapsed_time(e1))
         ms = float(np.median(ts))
         print(f'B{B} H{H} I{I} K{Kq} hd{hd} {name}: {ms*1e3:8.1f} us  {f/ms/1e9:6.1f} TF/s (algorithmic)')
-for cfg in [(4096, 4, 140, 140, 32), (4096, 4, 140, 1, 32), (4096, 4, 140, 140, 64)]:
+cfgs = [(4096, 4, 140, 140, 32), (4096, 4, 140, 1, 32), (4096, 4, 140, 140, 64)]
+if len(sys.argv) > 1:                      # e.g. `attn_bench.py 4096,4,140,140,32`
+    cfgs = [tuple(int(x) for x in a.split(',')) for a in sys.argv[1:]]
+for cfg in cfgs:
     run(*cfg)

@@ -101,7 +101,7 @@ int ot_attn_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, int he
                 float* out, float* lse, void* stream);
 /* dqkv: like qkv (dq written on the K tail rows only; dk, dv on all rows);
  * ws: ot_attn_bwd_workspace_size(B, H, K) bytes (row stats padded to 32 queries per (b, h)) */
-int64_t ot_attn_bwd_workspace_size(int B, int H, int K);
+size_t ot_attn_bwd_workspace_size(int B, int H, int K);
 int ot_attn_bwd(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
                 int B, int H, int I, int K, int head_dim, float* dqkv, float* delta_ws, void* stream);
 

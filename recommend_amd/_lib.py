@@ -36,7 +36,7 @@ SIGNATURES = {
                                     I64, P, I64, c_int, P, c_size_t, P]),
     'ot_transpose_banks': (c_int, [P, P, P, c_int, I64, P]),
     'ot_attn_fwd': (c_int, [P, I64, c_int, c_int, c_int, c_int, c_int, P, P, P]),
-    'ot_attn_bwd_workspace_size': (I64, [c_int, c_int, c_int]),
+    'ot_attn_bwd_workspace_size': (c_size_t, [c_int, c_int, c_int]),
     'ot_attn_bwd': (c_int, [P, I64, P, P, P, c_int, c_int, c_int, c_int, c_int, P, P, P]),
     'ot_rmsnorm_fwd': (c_int, [P, I64, P, P, I64, P, I64, c_int, c_float, P]),
     'ot_rmsnorm_bwd_workspace_size': (c_size_t, [I64, c_int]),

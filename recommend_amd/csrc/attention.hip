@@ -500,8 +500,8 @@ extern "C" int ot_attn_fwd(const float* qkv, int64_t ld, int B, int H, int I, in
   return OT_OK;
 }
 
-extern "C" int64_t ot_attn_bwd_workspace_size(int B, int H, int K) {
-  return 2 * (int64_t)B * H * attn_kpad(K) * (int64_t)sizeof(float);
+extern "C" size_t ot_attn_bwd_workspace_size(int B, int H, int K) {
+  return 2 * (size_t)B * H * attn_kpad(K) * sizeof(float);
 }
 
 extern "C" int ot_attn_bwd(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,

@@ -54,6 +54,10 @@ extern "C" {
 #define OT_EPI_DROPOUT 8     /* counter-based mask, index (token, n) */
 #define OT_EPI_RESIDUAL 16   /* + res[res_tok ? token : out_row][n] */
 #define OT_EPI_ACCUMULATE 32 /* C += result */
+/* row-norm epilogues (ot_mixed_gemm_rms only; N == 128 so one tile holds whole output rows) */
+#define OT_EPI_ROW_RSTD 64      /* rstd_out[out_row] = 1/sqrt(mean_n(C[out_row]^2) + eps), C as above */
+#define OT_EPI_RMSNORM_BWD 128  /* the product is dL/dy of y = RMSNorm(x) * gamma: C = dL/dx (+ dres);
+                                   with OT_EPI_DROPOUT also dx_masked = mask(C) (C itself unmasked) */
 
 int ot_version(void);
 const char* ot_get_last_error_string(void);
@@ -75,6 +79,31 @@ int ot_mixed_gemm(int mode, const float* A, int64_t lda, int K, const int32_t* i
                   const float* aux, int64_t ldaux,
                   uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
                   void* stream);
+/* Row-norm epilogue operands for ot_mixed_gemm_rms.  Replaces the RMSNorm layers around the GEMMs
+ * (model.py:11-23 RMSNorm, applied at 191/196; their tape gradients): the forward GEMM producing the
+ * residual stream emits the next norm's rstd, the dgrad GEMM feeding a norm applies its backward. */
+typedef struct ot_rms_epilogue {
+  float* rstd_out; float eps;                          /* OT_EPI_ROW_RSTD */
+  const float* x; int64_t ldx;                         /* OT_EPI_RMSNORM_BWD: norm input rows (out_row) */
+  const float* gamma; const float* rstd;               /*   gamma[N], rstd[out_row] */
+  const float* dres; int64_t lddres;                   /*   + dres (row out_row, or through the tail map */
+  int dres_tail_K, dres_tail_I;                        /*     b*I+p -> b*K+(p-(I-K)) when dres_tail_K > 0) */
+  float* dx_masked; int64_t lddxm;                     /*   with OT_EPI_DROPOUT: GEMM seed/site/rate/tail */
+  float* dgamma; int accumulate_dgamma;                /*   dgamma (+)= sum_rows dy * x * rstd */
+  void* workspace; size_t ws_bytes;                    /*   ot_mixed_gemm_rms_workspace_size(ntiles, N) */
+} ot_rms_epilogue;
+size_t ot_mixed_gemm_rms_workspace_size(int ntiles, int N);
+int ot_mixed_gemm_rms(int mode, const float* A, int64_t lda, int K, const int32_t* in_rows,
+                      int a_xform, const float* a_rstd, const float* a_gamma,
+                      const float* W, int64_t w_gstride, int64_t ldw, int N,
+                      const int32_t* tile_group, int ntiles,
+                      const float* bias, int64_t bias_gstride,
+                      float* C, int64_t ldc, const int32_t* out_rows, int epi,
+                      const float* res, int64_t ldres, int res_tok,
+                      const float* aux, int64_t ldaux,
+                      uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
+                      const ot_rms_epilogue* rms, void* stream);
+
 /* dW[g] (+)= sum pro(A[a_rows])^T D[d_rows], db[g] (+)= sum D[d_rows] over the rows of every
  * chunk of group g.  chunks: [nchunks][3] {group, row_begin, row_count} indexing the row maps;
  * gchunk: [ngroups][2] {first chunk, chunk count} (a group's chunks are contiguous).

@@ -19,6 +19,17 @@ OT_GEMM_NN, OT_GEMM_NT = 0, 1
 OT_AX_NONE, OT_AX_RMSNORM, OT_AX_GELU = 0, 1, 2
 OT_EPI_BIAS, OT_EPI_GELU_BWD, OT_EPI_GELU = 1, 2, 4
 OT_EPI_DROPOUT, OT_EPI_RESIDUAL, OT_EPI_ACCUMULATE = 8, 16, 32
+OT_EPI_ROW_RSTD, OT_EPI_RMSNORM_BWD = 64, 128
+
+
+class RmsEpilogue(ctypes.Structure):
+    """``ot_rms_epilogue`` (include/onetrans_hip.h)."""
+    _fields_ = [('rstd_out', c_void_p), ('eps', c_float),
+                ('x', c_void_p), ('ldx', c_int64), ('gamma', c_void_p), ('rstd', c_void_p),
+                ('dres', c_void_p), ('lddres', c_int64), ('dres_tail_K', c_int), ('dres_tail_I', c_int),
+                ('dx_masked', c_void_p), ('lddxm', c_int64),
+                ('dgamma', c_void_p), ('accumulate_dgamma', c_int),
+                ('workspace', c_void_p), ('ws_bytes', c_size_t)]
 
 P = c_void_p
 I64 = c_int64
@@ -31,6 +42,10 @@ SIGNATURES = {
     'ot_mixed_gemm': (c_int, [c_int, P, I64, c_int, P, c_int, P, P, P, I64, I64, c_int, P, c_int, P, I64,
                               P, I64, P, c_int, P, I64, c_int, P, I64, c_uint32, c_uint32, c_float, c_int,
                               c_int, P]),
+    'ot_mixed_gemm_rms_workspace_size': (c_size_t, [c_int, c_int]),
+    'ot_mixed_gemm_rms': (c_int, [c_int, P, I64, c_int, P, c_int, P, P, P, I64, I64, c_int, P, c_int, P, I64,
+                                  P, I64, P, c_int, P, I64, c_int, P, I64, c_uint32, c_uint32, c_float, c_int,
+                                  c_int, P, P]),
     'ot_wgrad_workspace_size': (c_size_t, [c_int, c_int, c_int]),
     'ot_mixed_gemm_wgrad': (c_int, [P, I64, P, c_int, P, P, P, I64, P, c_int, c_int, P, c_int, P, c_int, P,
                                     I64, P, I64, c_int, P, c_size_t, P]),

@@ -78,3 +78,11 @@ inline uint32_t drop_threshold(float rate) {
   return thr >= 4294967295.0 ? 4294967295u : (uint32_t)llround(thr);
 }
 }  // namespace ot
+
+namespace ot {
+// out[c] (+)= sum_b part[b][c], deterministic (rowwise.hip); shared by the fused row-norm epilogue
+// (scratch: colsum_scratch_floats(nparts, ncols) floats, used when nparts > 256)
+int64_t colsum_scratch_floats(int64_t nparts, int ncols);
+void launch_colsum_reduce(const float* part, int64_t nparts, int ncols, float* out, int accumulate, hipStream_t s,
+                          float* scratch);
+}  // namespace ot

@@ -45,7 +45,20 @@ struct GemmArgs {
   const float* aux; int64_t ldaux;
   uint32_t seed, site, drop_thr; float drop_scale; int tail_K, tail_I; int drop_width;
   int ntm, ntn;
+  // row-norm epilogues (N == GT: the tile holds whole rows)
+  float* rstd_out; float eps;                                   // OT_EPI_ROW_RSTD
+  const float* nx; int64_t ldnx; const float* ngamma; const float* nrstd;   // OT_EPI_RMSNORM_BWD
+  const float* dres; int64_t lddres; int dres_K, dres_I;
+  float* dxm; int64_t lddxm; float* dgpart;
 };
+
+// sum over the 32 lanes that hold one output row in the vector epilogue (same order as the
+// row-wise kernels' group_sum with 32 threads per row)
+__device__ __forceinline__ float row32_sum(float v) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
 
 __device__ __forceinline__ f32x4 apply_pro(f32x4 v, int xf, float rs, const float* gamma, int k) {
   if (xf == OT_AX_RMSNORM) {
@@ -224,12 +237,23 @@ __global__ __launch_bounds__(256, 2) void mixed_gemm_kernel(GemmArgs p) {
     // each row index is loaded once per row instead of once per element.  Operand loads of a batch
     // of rows are issued together.
     constexpr int CLD = GT + 4;
+    static_assert(64 * CLD + 8 * GT <= 4 * GT * GLD, "epilogue LDS exceeds the staging buffers");
     float* ct = smem;                                   // [64][CLD]
     const int c4 = t & 31, rb = t >> 5;                 // float4 column chunk, first local row
     const int col = n0 + 4 * c4;
     f32x4 bias4 = {0.f, 0.f, 0.f, 0.f};
     if (epi & OT_EPI_BIAS) bias4 = *reinterpret_cast<const f32x4*>(p.bias + (int64_t)g * p.bias_gstride + col);
     const bool need_tok = (epi & OT_EPI_DROPOUT) || ((epi & OT_EPI_RESIDUAL) && p.res_tok);
+    constexpr bool RMSBWD = EPIT >= 0 && (EPIT & OT_EPI_RMSNORM_BWD);
+    constexpr bool ROWRSTD = EPIT >= 0 && (EPIT & OT_EPI_ROW_RSTD);
+    // dgamma partials live in a thread-private LDS slot behind ct (a register accumulator here
+    // costs the whole kernel ~70 VGPRs of occupancy): dgs[rb][4 c4 .. 4 c4 + 3]
+    float* dgs = ct + 64 * CLD;
+    f32x4 ngam = {0.f, 0.f, 0.f, 0.f};
+    if (RMSBWD) {
+      ngam = *reinterpret_cast<const f32x4*>(p.ngamma + col);
+      *reinterpret_cast<f32x4*>(dgs + rb * GT + 4 * c4) = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
     int orow[2][8];
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf)
@@ -239,7 +263,7 @@ __global__ __launch_bounds__(256, 2) void mixed_gemm_kernel(GemmArgs p) {
         const int64_t gr = (int64_t)tm * GT + (lr >> 5) * 64 + 32 * hf + (lr & 31);
         orow[hf][i] = p.out_rows ? p.out_rows[gr] : (int)gr;
       }
-    constexpr int RB = 8;                               // rows per operand-load batch
+    constexpr int RB = RMSBWD ? 4 : 8;                  // rows per operand-load batch (register budget)
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
 #pragma unroll
@@ -251,12 +275,26 @@ __global__ __launch_bounds__(256, 2) void mixed_gemm_kernel(GemmArgs p) {
 #pragma unroll
       for (int i0 = 0; i0 < 8; i0 += RB) {
         int64_t tok[RB];
-        f32x4 aux4[RB], res4[RB], cp4[RB];
+        f32x4 aux4[RB], res4[RB], cp4[RB], x4[RB], dr4[RB];
+        float nr[RB];
 #pragma unroll
         for (int i = 0; i < RB; ++i) {
           const int orr = orow[hf][i0 + i];
           const int64_t o = orr < 0 ? 0 : orr;
           tok[i] = (need_tok && orr >= 0) ? tail_token(orr, p.tail_K, p.tail_I) : o;
+          if (RMSBWD) {
+            x4[i] = *reinterpret_cast<const f32x4*>(p.nx + o * p.ldnx + col);
+            nr[i] = p.nrstd[o];
+            dr4[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (p.dres) {
+              int dr = (int)o;
+              if (p.dres_K > 0) {
+                const int bb = (int)o / p.dres_I, j = (int)o - bb * p.dres_I - (p.dres_I - p.dres_K);
+                dr = j >= 0 ? bb * p.dres_K + j : -1;
+              }
+              if (dr >= 0) dr4[i] = *reinterpret_cast<const f32x4*>(p.dres + (int64_t)dr * p.lddres + col);
+            }
+          }
           if (epi & OT_EPI_GELU_BWD) aux4[i] = *reinterpret_cast<const f32x4*>(p.aux + o * p.ldaux + col);
           if (epi & OT_EPI_RESIDUAL)
             res4[i] = *reinterpret_cast<const f32x4*>(p.res + (p.res_tok ? tok[i] : o) * p.ldres + col);
@@ -274,6 +312,30 @@ __global__ __launch_bounds__(256, 2) void mixed_gemm_kernel(GemmArgs p) {
           if (epi & OT_EPI_GELU) {
             v.x = gelu_erf(v.x); v.y = gelu_erf(v.y); v.z = gelu_erf(v.z); v.w = gelu_erf(v.w);
           }
+          if (RMSBWD) {
+            // v = dL/dy of y = x * rstd * gamma:  dx = rstd * (g - x * rstd^2 * <g, x> / N) + dres
+            const f32x4 gv = v * ngam;
+            const float r = nr[i];
+            float sdot = gv.x * x4[i].x + gv.y * x4[i].y + gv.z * x4[i].z + gv.w * x4[i].w;
+            sdot = row32_sum(sdot);
+            const float coef = r * r * r * sdot / (float)p.N;
+            if (orr >= 0) {
+              f32x4* q = reinterpret_cast<f32x4*>(dgs + rb * GT + 4 * c4);
+              *q = *q + v * x4[i] * r;
+            }
+            v = gv * r - x4[i] * coef + dr4[i];
+            if (orr >= 0) *reinterpret_cast<f32x4*>(p.C + (int64_t)orr * p.ldc + col) = v;
+            if ((epi & OT_EPI_DROPOUT) && orr >= 0) {          // mask(dx) for the dropout site upstream
+              const uint32_t idx = (uint32_t)(tok[i] * p.drop_width + col);
+              f32x4 mv;
+              mv.x = drop_keep(p.seed, p.site, idx + 0, p.drop_thr) ? v.x * p.drop_scale : 0.f;
+              mv.y = drop_keep(p.seed, p.site, idx + 1, p.drop_thr) ? v.y * p.drop_scale : 0.f;
+              mv.z = drop_keep(p.seed, p.site, idx + 2, p.drop_thr) ? v.z * p.drop_scale : 0.f;
+              mv.w = drop_keep(p.seed, p.site, idx + 3, p.drop_thr) ? v.w * p.drop_scale : 0.f;
+              *reinterpret_cast<f32x4*>(p.dxm + (int64_t)orr * p.lddxm + col) = mv;
+            }
+            continue;
+          }
           if (epi & OT_EPI_DROPOUT) {
             const uint32_t idx = (uint32_t)(tok[i] * p.drop_width + col);
             v.x = drop_keep(p.seed, p.site, idx + 0, p.drop_thr) ? v.x * p.drop_scale : 0.f;
@@ -283,10 +345,20 @@ __global__ __launch_bounds__(256, 2) void mixed_gemm_kernel(GemmArgs p) {
           }
           if (epi & OT_EPI_RESIDUAL) v += res4[i];
           if (epi & OT_EPI_ACCUMULATE) v += cp4[i];
+          if (ROWRSTD) {                                       // rstd of the finished row (next RMSNorm)
+            const float ss = row32_sum(v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w);
+            if (orr >= 0 && c4 == 0) p.rstd_out[orr] = rsqrtf(ss / (float)p.N + p.eps);
+          }
           if (orr >= 0) *reinterpret_cast<f32x4*>(p.C + (int64_t)orr * p.ldc + col) = v;
         }
       }
       __syncthreads();                                  // ct is rewritten by the next half
+    }
+    if (RMSBWD && t < GT) {                             // dgamma partial of this tile (fixed order)
+      float a = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) a += dgs[k * GT + t];
+      p.dgpart[(int64_t)tm * GT + t] = a;
     }
     return;
   }
@@ -615,17 +687,19 @@ extern "C" int ot_transpose_banks(const float* src, float* dst, const int64_t* b
   return OT_OK;
 }
 
-extern "C" int ot_mixed_gemm(int mode, const float* A, int64_t lda, int K, const int32_t* in_rows,
-                             int a_xform, const float* a_rstd, const float* a_gamma,
-                             const float* W, int64_t w_gstride, int64_t ldw, int N,
-                             const int32_t* tile_group, int ntiles,
-                             const float* bias, int64_t bias_gstride,
-                             float* C, int64_t ldc, const int32_t* out_rows, int epi,
-                             const float* res, int64_t ldres, int res_tok,
-                             const float* aux, int64_t ldaux,
-                             uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
-                             void* stream) {
+static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const int32_t* in_rows,
+                           int a_xform, const float* a_rstd, const float* a_gamma,
+                           const float* W, int64_t w_gstride, int64_t ldw, int N,
+                           const int32_t* tile_group, int ntiles,
+                           const float* bias, int64_t bias_gstride,
+                           float* C, int64_t ldc, const int32_t* out_rows, int epi,
+                           const float* res, int64_t ldres, int res_tok,
+                           const float* aux, int64_t ldaux,
+                           uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
+                           const ot_rms_epilogue* rms, void* stream) {
   OT_REQUIRE(A && W && C, "ot_mixed_gemm: null operand");
+  const int rms_flags = epi & (OT_EPI_ROW_RSTD | OT_EPI_RMSNORM_BWD);
+  OT_REQUIRE(!rms_flags || rms, "ot_mixed_gemm: row-norm epilogue flags need ot_mixed_gemm_rms");
   OT_REQUIRE(K > 0 && N > 0 && ntiles >= 0, "ot_mixed_gemm: bad sizes K=%d N=%d ntiles=%d", K, N, ntiles);
   OT_REQUIRE(K % 4 == 0 && lda % 4 == 0, "ot_mixed_gemm: K and lda must be multiples of 4");
   OT_REQUIRE(ldw % 4 == 0 && w_gstride % 4 == 0, "ot_mixed_gemm: ldw/w_gstride must be multiples of 4");
@@ -636,10 +710,36 @@ extern "C" int ot_mixed_gemm(int mode, const float* A, int64_t lda, int K, const
   OT_REQUIRE(!(epi & OT_EPI_GELU_BWD) || aux, "ot_mixed_gemm: aux missing");
   OT_REQUIRE(a_xform != OT_AX_RMSNORM || (a_rstd && a_gamma), "ot_mixed_gemm: rmsnorm prologue needs rstd/gamma");
   OT_REQUIRE(!((epi & OT_EPI_DROPOUT) || res_tok) || (tail_K > 0 && tail_I >= tail_K), "ot_mixed_gemm: bad tail map");
+  if (rms_flags) {
+    OT_REQUIRE(mode == OT_GEMM_NT && N == GT, "ot_mixed_gemm_rms: row-norm epilogues need NT mode and N == %d", GT);
+    OT_REQUIRE(!(epi & OT_EPI_ROW_RSTD) || rms->rstd_out, "ot_mixed_gemm_rms: rstd_out missing");
+    OT_REQUIRE(!(epi & OT_EPI_RMSNORM_BWD) || (rms->x && rms->gamma && rms->rstd && rms->ldx % 4 == 0),
+               "ot_mixed_gemm_rms: RMSNorm backward needs x / gamma / rstd");
+    OT_REQUIRE(!(epi & OT_EPI_RMSNORM_BWD) || !(epi & ~(OT_EPI_RMSNORM_BWD | OT_EPI_DROPOUT)),
+               "ot_mixed_gemm_rms: RMSNorm backward combines with OT_EPI_DROPOUT only");
+    OT_REQUIRE(!((epi & OT_EPI_RMSNORM_BWD) && (epi & OT_EPI_DROPOUT)) || rms->dx_masked,
+               "ot_mixed_gemm_rms: dx_masked missing");
+    OT_REQUIRE(!rms->dgamma || (rms->workspace && rms->ws_bytes >= ot_mixed_gemm_rms_workspace_size(ntiles, N)),
+               "ot_mixed_gemm_rms: workspace too small");
+    OT_REQUIRE(!rms->dres || rms->lddres % 4 == 0, "ot_mixed_gemm_rms: lddres must be a multiple of 4");
+  }
   if (ntiles == 0) return OT_OK;
   GemmArgs p{A, lda, K, in_rows, a_xform, a_rstd, a_gamma, W, w_gstride, ldw, N, tile_group,
              bias, bias_gstride, C, ldc, out_rows, epi, res, ldres, res_tok, aux, ldaux,
              seed, site, 0u, 1.f, tail_K, tail_I, N, ntiles, (int)ceil_div(N, GT)};
+  float* dgpart = nullptr;
+  if (rms_flags) {
+    p.rstd_out = rms->rstd_out; p.eps = rms->eps;
+    p.nx = rms->x; p.ldnx = rms->ldx; p.ngamma = rms->gamma; p.nrstd = rms->rstd;
+    p.dres = rms->dres; p.lddres = rms->lddres; p.dres_K = rms->dres_tail_K; p.dres_I = rms->dres_tail_I;
+    p.dxm = rms->dx_masked; p.lddxm = rms->lddxm;
+    if (epi & OT_EPI_RMSNORM_BWD) {
+      // without dgamma the partials still need a home: the caller's workspace or nothing
+      dgpart = rms->dgamma ? (float*)rms->workspace : nullptr;
+      OT_REQUIRE(dgpart, "ot_mixed_gemm_rms: RMSNorm backward needs dgamma and its workspace");
+      p.dgpart = dgpart;
+    }
+  }
   if (epi & OT_EPI_DROPOUT) {
     OT_REQUIRE(drop_rate >= 0.f && drop_rate < 1.f, "ot_mixed_gemm: drop_rate out of range");
     p.drop_thr = drop_threshold(drop_rate);
@@ -651,6 +751,7 @@ extern "C" int ot_mixed_gemm(int mode, const float* A, int64_t lda, int K, const
                       (!(epi & OT_EPI_GELU_BWD) || (ldaux % 4 == 0 && a16(aux))) &&
                       (!(epi & OT_EPI_BIAS) || (bias_gstride % 4 == 0 && a16(bias)));
   const bool edge = (K % GBK) != 0 || (N % GT) != 0 || !vec_ok;
+  OT_REQUIRE(!rms_flags || !edge, "ot_mixed_gemm_rms: needs K %% %d == 0 and 16-B aligned operands", GBK);
   const unsigned nwg = (unsigned)ntiles * p.ntn;
   hipStream_t s = (hipStream_t)stream;
   void (*kern)(GemmArgs) = nullptr;
@@ -668,7 +769,14 @@ extern "C" int ot_mixed_gemm(int mode, const float* A, int64_t lda, int K, const
   OT_SPEC(true, OT_AX_NONE, OT_EPI_GELU_BWD)
   OT_SPEC(true, OT_AX_NONE, 0)
   OT_SPEC(true, OT_AX_NONE, OT_EPI_ACCUMULATE)
+  OT_SPEC(true, OT_AX_NONE, OT_EPI_RESIDUAL | OT_EPI_DROPOUT | OT_EPI_ROW_RSTD)
+  OT_SPEC(true, OT_AX_NONE, OT_EPI_RESIDUAL | OT_EPI_ROW_RSTD)
+  OT_SPEC(true, OT_AX_GELU, OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_DROPOUT | OT_EPI_ROW_RSTD)
+  OT_SPEC(true, OT_AX_GELU, OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_ROW_RSTD)
+  OT_SPEC(true, OT_AX_NONE, OT_EPI_RMSNORM_BWD)
+  OT_SPEC(true, OT_AX_NONE, OT_EPI_RMSNORM_BWD | OT_EPI_DROPOUT)
 #undef OT_SPEC
+  OT_REQUIRE(kern || !rms_flags, "ot_mixed_gemm_rms: no specialised kernel for epilogue flags %d", epi);
   if (!kern) {   // any other combination: generic instantiation (run-time prologue/epilogue)
     if (mode == OT_GEMM_NT)
       kern = edge ? mixed_gemm_kernel<true, -1, -1, true> : mixed_gemm_kernel<true, -1, -1, false>;
@@ -685,7 +793,47 @@ extern "C" int ot_mixed_gemm(int mode, const float* A, int64_t lda, int K, const
   });
   hipLaunchKernelGGL(kern, dim3(nwg), dim3(256), shmem, s, p);
   OT_LAUNCH_CHECK("ot_mixed_gemm");
+  if (dgpart) {
+    launch_colsum_reduce(dgpart, ntiles, N, rms->dgamma, rms->accumulate_dgamma, s, dgpart + (int64_t)ntiles * N);
+    OT_LAUNCH_CHECK("ot_mixed_gemm_rms(dgamma)");
+  }
   return OT_OK;
+}
+
+extern "C" int ot_mixed_gemm(int mode, const float* A, int64_t lda, int K, const int32_t* in_rows,
+                             int a_xform, const float* a_rstd, const float* a_gamma,
+                             const float* W, int64_t w_gstride, int64_t ldw, int N,
+                             const int32_t* tile_group, int ntiles,
+                             const float* bias, int64_t bias_gstride,
+                             float* C, int64_t ldc, const int32_t* out_rows, int epi,
+                             const float* res, int64_t ldres, int res_tok,
+                             const float* aux, int64_t ldaux,
+                             uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
+                             void* stream) {
+  return mixed_gemm_impl(mode, A, lda, K, in_rows, a_xform, a_rstd, a_gamma, W, w_gstride, ldw, N, tile_group,
+                         ntiles, bias, bias_gstride, C, ldc, out_rows, epi, res, ldres, res_tok, aux, ldaux, seed,
+                         site, drop_rate, tail_K, tail_I, nullptr, stream);
+}
+
+extern "C" size_t ot_mixed_gemm_rms_workspace_size(int ntiles, int N) {
+  const int64_t parts = ntiles > 0 ? ntiles : 1;
+  return (size_t)(parts * N + colsum_scratch_floats(parts, N)) * sizeof(float);
+}
+
+extern "C" int ot_mixed_gemm_rms(int mode, const float* A, int64_t lda, int K, const int32_t* in_rows,
+                                 int a_xform, const float* a_rstd, const float* a_gamma,
+                                 const float* W, int64_t w_gstride, int64_t ldw, int N,
+                                 const int32_t* tile_group, int ntiles,
+                                 const float* bias, int64_t bias_gstride,
+                                 float* C, int64_t ldc, const int32_t* out_rows, int epi,
+                                 const float* res, int64_t ldres, int res_tok,
+                                 const float* aux, int64_t ldaux,
+                                 uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
+                                 const ot_rms_epilogue* rms, void* stream) {
+  OT_REQUIRE(rms, "ot_mixed_gemm_rms: null epilogue operands");
+  return mixed_gemm_impl(mode, A, lda, K, in_rows, a_xform, a_rstd, a_gamma, W, w_gstride, ldw, N, tile_group,
+                         ntiles, bias, bias_gstride, C, ldc, out_rows, epi, res, ldres, res_tok, aux, ldaux, seed,
+                         site, drop_rate, tail_K, tail_I, rms, stream);
 }
 
 extern "C" size_t ot_wgrad_workspace_size(int nchunks, int K, int N) {

@@ -141,6 +141,25 @@ __global__ __launch_bounds__(256) void colsum_reduce_kernel(const float* __restr
   }
 }
 
+// First level for tall partial stacks: chunk[k][c] = sum of parts [64k, 64k + 64) of column c.
+// Block = 64 columns x 4 groups of 16 consecutive parts (coalesced 256-B rows), fixed-order combine.
+__global__ __launch_bounds__(256) void colsum_chunk_kernel(const float* __restrict__ part, int64_t nparts, int ncols,
+                                                           float* chunk) {
+  __shared__ float red[4][64];
+  const int cc = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cc;
+  const int64_t b0 = (int64_t)blockIdx.y * 64 + 16 * g;
+  float s = 0.f;
+  if (c < ncols) {
+#pragma unroll 4
+    for (int i = 0; i < 16; ++i)
+      if (b0 + i < nparts) s += part[(b0 + i) * ncols + c];
+  }
+  red[g][cc] = s;
+  __syncthreads();
+  if (g == 0 && c < ncols) chunk[(int64_t)blockIdx.y * ncols + c] = ((red[0][cc] + red[1][cc]) + red[2][cc]) + red[3][cc];
+}
+
 // part[blk][c] = sum of rows [blk*RPB, (blk+1)*RPB) of the listed rows, column c
 __global__ void rows_colsum_kernel(const float* __restrict__ src, int64_t ld, const int32_t* __restrict__ rows,
                                    int64_t nrows, int ncols, int rows_per_block, float* part) {
@@ -203,7 +222,8 @@ inline unsigned rms_bwd_grid(int64_t rows, int d) {
 }
 
 extern "C" size_t ot_rmsnorm_bwd_workspace_size(int64_t rows, int d) {
-  return (size_t)rms_bwd_grid(rows, d) * d * sizeof(float);
+  const int64_t parts = rms_bwd_grid(rows, d);
+  return (size_t)(parts * d + colsum_scratch_floats(parts, d)) * sizeof(float);
 }
 
 extern "C" int ot_rmsnorm_bwd(const float* dy, int64_t lddy, const float* x, int64_t ldx, const float* gamma,
@@ -230,12 +250,29 @@ extern "C" int ot_rmsnorm_bwd(const float* dy, int64_t lddy, const float* x, int
   hipLaunchKernelGGL(rmsnorm_bwd_kernel, dim3(grid), dim3(256), shmem, (hipStream_t)stream, p);
   OT_LAUNCH_CHECK("ot_rmsnorm_bwd");
   if (dgamma) {
-    hipLaunchKernelGGL(colsum_reduce_kernel, dim3(ceil_div(d, 16)), dim3(256), 0, (hipStream_t)stream,
-                       (const float*)workspace, (int64_t)grid, d, dgamma, accumulate_dgamma);
+    launch_colsum_reduce((const float*)workspace, (int64_t)grid, d, dgamma, accumulate_dgamma, (hipStream_t)stream,
+                         (float*)workspace + (int64_t)grid * d);
     OT_LAUNCH_CHECK("ot_rmsnorm_bwd(reduce)");
   }
   return OT_OK;
 }
+
+namespace ot {
+int64_t colsum_scratch_floats(int64_t nparts, int ncols) { return (int64_t)ceil_div(nparts, 64) * ncols; }
+
+void launch_colsum_reduce(const float* part, int64_t nparts, int ncols, float* out, int accumulate, hipStream_t s,
+                          float* scratch) {
+  if (nparts > 256 && scratch) {          // two levels: 64-part chunks, then the chunk sums
+    const unsigned nch = ceil_div(nparts, 64);
+    hipLaunchKernelGGL(colsum_chunk_kernel, dim3(ceil_div(ncols, 64), nch), dim3(256), 0, s, part, nparts, ncols,
+                       scratch);
+    part = scratch;
+    nparts = nch;
+  }
+  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(ceil_div(ncols, 16)), dim3(256), 0, s, part, nparts, ncols, out,
+                     accumulate);
+}
+}  // namespace ot
 
 extern "C" int ot_dropout_apply(const float* src, int64_t lds, float* dst, int64_t ldd, int64_t rows, int d,
                                 uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I, void* stream) {
@@ -250,7 +287,8 @@ extern "C" int ot_dropout_apply(const float* src, int64_t lds, float* dst, int64
 }
 
 extern "C" size_t ot_rows_colsum_workspace_size(int64_t nrows, int ncols) {
-  return (size_t)ceil_div(nrows, 256) * ncols * sizeof(float);
+  const int64_t parts = ceil_div(nrows, 256);
+  return (size_t)(parts * ncols + colsum_scratch_floats(parts, ncols)) * sizeof(float);
 }
 
 extern "C" int ot_rows_colsum(const float* src, int64_t ld, const int32_t* rows, int64_t nrows, int ncols,
@@ -263,8 +301,8 @@ extern "C" int ot_rows_colsum(const float* src, int64_t ld, const int32_t* rows,
                        src, ld, rows, nrows, ncols, 256, (float*)workspace);
     OT_LAUNCH_CHECK("ot_rows_colsum");
   }
-  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(ceil_div(ncols, 16)), dim3(256), 0, (hipStream_t)stream,
-                     (const float*)workspace, (int64_t)nb, ncols, out, accumulate);
+  launch_colsum_reduce((const float*)workspace, (int64_t)nb, ncols, out, accumulate, (hipStream_t)stream,
+                       (float*)workspace + (int64_t)nb * ncols);
   OT_LAUNCH_CHECK("ot_rows_colsum(reduce)");
   return OT_OK;
 }

@@ -5,6 +5,7 @@ Pointer arguments accept a tensor, ``(tensor, element_offset)`` or None."""
 
 from __future__ import annotations
 
+import ctypes
 from typing import Optional, Tuple, Union
 
 import torch
@@ -83,6 +84,31 @@ def gemm(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish, w_g
     call('ot_mixed_gemm', mode, ptr(A), lda, K, ptr(in_rows), a_xform, ptr(rstd), ptr(gamma), ptr(W), w_gstride,
          ldw, N, ptr(tile_group), ntiles, ptr(bias), bias_gstride, ptr(C), ldc, ptr(out_rows), epi, ptr(res),
          ldres, res_tok, ptr(aux), ldaux, seed & 0xFFFFFFFF, site, float(drop), tail[0], tail[1], stream())
+    if ev is not None:
+        _probe.end('mixed_gemm', 2.0 * (m_rows or ntiles * 128) * K * N, ev)
+
+
+def gemm_rms(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish, w_gstride: int, ldw: int,
+             N: int, tile_group: Ptrish, ntiles: int, C: Ptrish, ldc: int, out_rows: Ptrish, *, epi: int,
+             a_xform: int = 0, rstd: Ptrish = None, gamma: Ptrish = None, bias: Ptrish = None,
+             bias_gstride: int = 0, res: Ptrish = None, ldres: int = 0, res_tok: int = 0, seed: int = 0,
+             site: int = 0, drop: float = 0.0, tail: Tuple[int, int] = (1, 1), m_rows: int = 0,
+             rstd_out: Ptrish = None, eps: float = 1e-6, nx: Ptrish = None, ldnx: int = 0,
+             ngamma: Ptrish = None, nrstd: Ptrish = None, dres: Ptrish = None, lddres: int = 0,
+             dres_tail: Tuple[int, int] = (0, 0), dx_masked: Ptrish = None, lddxm: int = 0,
+             dgamma: Ptrish = None, accumulate_dgamma: bool = False, device=None) -> None:
+    """ot_mixed_gemm_rms: the GEMM with a row-norm epilogue (OT_EPI_ROW_RSTD: emit the next RMSNorm's
+    rstd; OT_EPI_RMSNORM_BWD: apply the RMSNorm backward to the product, + dres, dgamma)."""
+    ws = workspace(size('ot_mixed_gemm_rms_workspace_size', ntiles, N) if dgamma is not None else 16,
+                   device if device is not None else (C[0] if isinstance(C, tuple) else C).device)
+    e = _lib.RmsEpilogue(ptr(rstd_out), float(eps), ptr(nx), ldnx, ptr(ngamma), ptr(nrstd), ptr(dres), lddres,
+                         dres_tail[0], dres_tail[1], ptr(dx_masked), lddxm, ptr(dgamma), int(accumulate_dgamma),
+                         ptr(ws), ws.numel())
+    ev = _probe.begin() if _probe is not None else None
+    call('ot_mixed_gemm_rms', mode, ptr(A), lda, K, ptr(in_rows), a_xform, ptr(rstd), ptr(gamma), ptr(W),
+         w_gstride, ldw, N, ptr(tile_group), ntiles, ptr(bias), bias_gstride, ptr(C), ldc, ptr(out_rows), epi,
+         ptr(res), ldres, res_tok, None, 0, seed & 0xFFFFFFFF, site, float(drop), tail[0], tail[1],
+         ctypes.byref(e), stream())
     if ev is not None:
         _probe.end('mixed_gemm', 2.0 * (m_rows or ntiles * 128) * K * N, ev)
 

@@ -28,7 +28,7 @@ import torch.nn as nn
 from . import _lib
 from . import kernels as K
 from ._lib import (OT_AX_GELU, OT_AX_RMSNORM, OT_EPI_ACCUMULATE, OT_EPI_BIAS, OT_EPI_DROPOUT, OT_EPI_GELU_BWD,
-                   OT_EPI_RESIDUAL, OT_GEMM_NN, OT_GEMM_NT, NS_FIELD_BYTES)
+                   OT_EPI_RESIDUAL, OT_EPI_RMSNORM_BWD, OT_EPI_ROW_RSTD, OT_GEMM_NN, OT_GEMM_NT, NS_FIELD_BYTES)
 from .config import OneTransConfig, get_model_config
 from .layout import TILE, FlatLayout, RowMap, build_map, head_map, identity_map, layer_maps, round_up
 from .params import init_params, ns_table_offsets
@@ -123,10 +123,14 @@ class _Tokenize(torch.autograd.Function):
 
 class _Block(torch.autograd.Function):
     """OneTransBlock.call (model.py:186-200) for the last K of I tokens (pyramid / last-layer DCE).
-    x: [B*I, d] -> [B*K, d]."""
+    x: [B*I, d] -> ([B*K, d], rstd of the output rows).
+
+    When d == 128 (one GEMM tile holds whole rows) the RMSNorms are fused into the GEMMs around
+    them: the Wo / FFN2 epilogues emit the rstd of the rows they finish (norm2 of this block, norm1
+    of the next: ``rstd_in``), and the FFN1 / QKV dgrad epilogues apply the norm backward."""
 
     @staticmethod
-    def forward(ctx, flat, x, m, l, I, Kq, seed, training):
+    def forward(ctx, flat, x, m, l, I, Kq, seed, training, rstd_in=None):
         cfg = m.config
         d, f, H = cfg.hidden_dim, cfg.ffn_dim, cfg.num_heads
         hd = d // H
@@ -140,9 +144,13 @@ class _Block(torch.autograd.Function):
         wqkv, wo = m.pT(f'blk.{l}.wqkv'), m.pT(f'blk.{l}.wo')          # transposed shadow: [G][N][K]
         w1, b1, w2, b2 = m.pT(f'blk.{l}.w1'), m.p(f'blk.{l}.b1'), m.pT(f'blk.{l}.w2'), m.p(f'blk.{l}.b2')
         g1, g2 = m.p(f'blk.{l}.norm1'), m.p(f'blk.{l}.norm2')
+        fuse = m.fuse_norms
         # norm1 -> rstd only; the QKV GEMM applies it in its A prologue
-        rstd1 = torch.empty(B * I, device=dev)
-        K.rmsnorm_fwd(x, d, B * I, d, rstd1, eps=RMS_EPS)
+        if rstd_in is not None and rstd_in.numel() == B * I:
+            rstd1 = rstd_in
+        else:
+            rstd1 = torch.empty(B * I, device=dev)
+            K.rmsnorm_fwd(x, d, B * I, d, rstd1, eps=RMS_EPS)
         qkv = torch.empty(B * I, 3 * d, device=dev)
         if Kq == I:
             K.gemm(OT_GEMM_NT, x, d, d, ma['rows'][0], wqkv, 3 * d * d, d, 3 * d, ma['tile_group'], na, qkv,
@@ -157,26 +165,44 @@ class _Block(torch.autograd.Function):
         K.attn_fwd(qkv, 3 * d, B, H, I, Kq, hd, o, lse)
         # x1 = x[tail] + drop(o @ Wo)      (model.py:117, 193)
         x1 = torch.empty(B * Kq, d, device=dev)
-        K.gemm(OT_GEMM_NT, o, d, d, mt['rows'][1], wo, 0, d, d, mt['tile_group'], nt, x1, d, mt['rows'][1],
-               epi=OT_EPI_RESIDUAL | dflag, res=x, ldres=d, res_tok=1, seed=seed, site=2 * l, drop=rate,
-               tail=(Kq, I), m_rows=maps['tail'].nrows)
         rstd2 = torch.empty(B * Kq, device=dev)
-        K.rmsnorm_fwd(x1, d, B * Kq, d, rstd2, eps=RMS_EPS)
+        if fuse:
+            K.gemm_rms(OT_GEMM_NT, o, d, d, mt['rows'][1], wo, 0, d, d, mt['tile_group'], nt, x1, d, mt['rows'][1],
+                       epi=OT_EPI_RESIDUAL | dflag | OT_EPI_ROW_RSTD, res=x, ldres=d, res_tok=1, seed=seed,
+                       site=2 * l, drop=rate, tail=(Kq, I), m_rows=maps['tail'].nrows, rstd_out=rstd2, eps=RMS_EPS)
+        else:
+            K.gemm(OT_GEMM_NT, o, d, d, mt['rows'][1], wo, 0, d, d, mt['tile_group'], nt, x1, d, mt['rows'][1],
+                   epi=OT_EPI_RESIDUAL | dflag, res=x, ldres=d, res_tok=1, seed=seed, site=2 * l, drop=rate,
+                   tail=(Kq, I), m_rows=maps['tail'].nrows)
+            K.rmsnorm_fwd(x1, d, B * Kq, d, rstd2, eps=RMS_EPS)
         # u = norm2(x1) @ W1[g] + b1[g]  (pre-activation; GELU applied by its consumers)
         u = torch.empty(B * Kq, f, device=dev)
         K.gemm(OT_GEMM_NT, x1, d, d, mt['rows'][1], w1, d * f, d, f, mt['tile_group'], nt, u, f, mt['rows'][1],
                a_xform=OT_AX_RMSNORM, rstd=rstd2, gamma=g2, bias=b1, bias_gstride=f, epi=OT_EPI_BIAS, m_rows=maps['tail'].nrows)
         # x2 = x1 + drop(gelu(u) @ W2[g] + b2[g])     (model.py:154-161, 198)
         x2 = torch.empty(B * Kq, d, device=dev)
-        K.gemm(OT_GEMM_NT, u, f, f, mt['rows'][1], w2, f * d, f, d, mt['tile_group'], nt, x2, d, mt['rows'][1],
-               a_xform=OT_AX_GELU, bias=b2, bias_gstride=d, epi=OT_EPI_BIAS | OT_EPI_RESIDUAL | dflag, res=x1,
-               ldres=d, res_tok=0, seed=seed, site=2 * l + 1, drop=rate, tail=(Kq, I), m_rows=maps['tail'].nrows)
+        rstd_out = None
+        if fuse:
+            rstd_out = torch.empty(B * Kq, device=dev)
+            K.gemm_rms(OT_GEMM_NT, u, f, f, mt['rows'][1], w2, f * d, f, d, mt['tile_group'], nt, x2, d,
+                       mt['rows'][1], a_xform=OT_AX_GELU, bias=b2, bias_gstride=d,
+                       epi=OT_EPI_BIAS | OT_EPI_RESIDUAL | dflag | OT_EPI_ROW_RSTD, res=x1, ldres=d, res_tok=0,
+                       seed=seed, site=2 * l + 1, drop=rate, tail=(Kq, I), m_rows=maps['tail'].nrows,
+                       rstd_out=rstd_out, eps=RMS_EPS)
+        else:
+            K.gemm(OT_GEMM_NT, u, f, f, mt['rows'][1], w2, f * d, f, d, mt['tile_group'], nt, x2, d, mt['rows'][1],
+                   a_xform=OT_AX_GELU, bias=b2, bias_gstride=d, epi=OT_EPI_BIAS | OT_EPI_RESIDUAL | dflag, res=x1,
+                   ldres=d, res_tok=0, seed=seed, site=2 * l + 1, drop=rate, tail=(Kq, I),
+                   m_rows=maps['tail'].nrows)
         ctx.save_for_backward(x, rstd1, qkv, o, lse, x1, rstd2, u)
         ctx.m, ctx.l, ctx.I, ctx.Kq, ctx.seed, ctx.rate = m, l, I, Kq, seed, rate
-        return x2
+        if rstd_out is None:
+            rstd_out = x2.new_empty(0)          # not fused: the next block computes its own rstd
+        ctx.mark_non_differentiable(rstd_out)
+        return x2, rstd_out
 
     @staticmethod
-    def backward(ctx, dx2):
+    def backward(ctx, dx2, _drstd=None):
         x, rstd1, qkv, o, lse, x1, rstd2, u = ctx.saved_tensors
         m, l, I, Kq, seed, rate = ctx.m, ctx.l, ctx.I, ctx.Kq, ctx.seed, ctx.rate
         cfg = m.config
@@ -206,15 +232,23 @@ class _Block(torch.autograd.Function):
         K.wgrad(x1, d, mt['rows'][1], du, f, mt['rows'][1], d, f, mt, nct, G, m.g(f'blk.{l}.w1'), d * f,
                 m.g(f'blk.{l}.b1'), f, a_xform=OT_AX_RMSNORM, rstd=rstd2, gamma=m.p(f'blk.{l}.norm2'),
                 accumulate=acc, device=dev, m_rows=maps['tail'].nrows, rowmap=maps['tail'])
-        dxn2 = torch.empty(B * Kq, d, device=dev)
-        K.gemm(OT_GEMM_NT, du, f, f, mt['rows'][1], m.p(f'blk.{l}.w1'), d * f, f, d, mt['tile_group'], nt, dxn2, d,
-               mt['rows'][1], m_rows=maps['tail'].nrows)
-        # norm2 backward + residual; emit mask(dx1) for the attention branch
+        # FFN1 dgrad -> norm2 backward + residual; emit mask(dx1) for the attention branch
         dx1 = torch.empty(B * Kq, d, device=dev)
         dyo = torch.empty(B * Kq, d, device=dev) if rate > 0 else dx1
-        K.rmsnorm_bwd(dxn2, d, x1, d, m.p(f'blk.{l}.norm2'), rstd2, dx1, d, B * Kq, d, dres=dx2, lddres=d,
-                      dx_masked=dyo if rate > 0 else None, lddxm=d, seed=seed, site=2 * l, drop=rate, tail=(Kq, I),
-                      dgamma=m.g(f'blk.{l}.norm2'), accumulate=acc, device=dev)
+        if m.fuse_norms:
+            K.gemm_rms(OT_GEMM_NT, du, f, f, mt['rows'][1], m.p(f'blk.{l}.w1'), d * f, f, d, mt['tile_group'], nt,
+                       dx1, d, mt['rows'][1], epi=OT_EPI_RMSNORM_BWD | (OT_EPI_DROPOUT if rate > 0 else 0),
+                       seed=seed, site=2 * l, drop=rate, tail=(Kq, I), m_rows=maps['tail'].nrows, nx=x1, ldnx=d,
+                       ngamma=m.p(f'blk.{l}.norm2'), nrstd=rstd2, dres=dx2, lddres=d,
+                       dx_masked=dyo if rate > 0 else None, lddxm=d, dgamma=m.g(f'blk.{l}.norm2'),
+                       accumulate_dgamma=acc, device=dev)
+        else:
+            dxn2 = torch.empty(B * Kq, d, device=dev)
+            K.gemm(OT_GEMM_NT, du, f, f, mt['rows'][1], m.p(f'blk.{l}.w1'), d * f, f, d, mt['tile_group'], nt, dxn2,
+                   d, mt['rows'][1], m_rows=maps['tail'].nrows)
+            K.rmsnorm_bwd(dxn2, d, x1, d, m.p(f'blk.{l}.norm2'), rstd2, dx1, d, B * Kq, d, dres=dx2, lddres=d,
+                          dx_masked=dyo if rate > 0 else None, lddxm=d, seed=seed, site=2 * l, drop=rate,
+                          tail=(Kq, I), dgamma=m.g(f'blk.{l}.norm2'), accumulate=acc, device=dev)
         # Wo
         _wgrad_single(m, o, dyo, d, d, mt, m.g(f'blk.{l}.wo'), acc, dev, maps['tail'].nrows)
         do = torch.empty(B * Kq, d, device=dev)
@@ -228,14 +262,21 @@ class _Block(torch.autograd.Function):
         K.wgrad(x, d, ma['rows'][0], dqkv, 3 * d, ma['rows'][0], d, 3 * d, ma, nca, G, m.g(f'blk.{l}.wqkv'),
                 3 * d * d, None, 0, a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=m.p(f'blk.{l}.norm1'), accumulate=acc,
                 device=dev, m_rows=maps['all'].nrows, rowmap=maps['all'])
-        dxn1 = torch.empty(B * I, d, device=dev)
-        K.gemm(OT_GEMM_NT, dqkv, 3 * d, 3 * d, ma['rows'][0], m.p(f'blk.{l}.wqkv'), 3 * d * d, 3 * d, d,
-               ma['tile_group'], na, dxn1, d, ma['rows'][0], m_rows=maps['all'].nrows)
         dx = torch.empty(B * I, d, device=dev)
-        K.rmsnorm_bwd(dxn1, d, x, d, m.p(f'blk.{l}.norm1'), rstd1, dx, d, B * I, d, dres=dx1, lddres=d,
-                      dres_tail=(Kq, I) if Kq < I else (0, 0), dgamma=m.g(f'blk.{l}.norm1'), accumulate=acc,
-                      device=dev)
-        return None, dx, None, None, None, None, None, None
+        if m.fuse_norms:       # QKV dgrad -> norm1 backward + residual (dx1 on the kept tail rows)
+            K.gemm_rms(OT_GEMM_NT, dqkv, 3 * d, 3 * d, ma['rows'][0], m.p(f'blk.{l}.wqkv'), 3 * d * d, 3 * d, d,
+                       ma['tile_group'], na, dx, d, ma['rows'][0], epi=OT_EPI_RMSNORM_BWD,
+                       m_rows=maps['all'].nrows, nx=x, ldnx=d, ngamma=m.p(f'blk.{l}.norm1'), nrstd=rstd1,
+                       dres=dx1, lddres=d, dres_tail=(Kq, I) if Kq < I else (0, 0),
+                       dgamma=m.g(f'blk.{l}.norm1'), accumulate_dgamma=acc, device=dev)
+        else:
+            dxn1 = torch.empty(B * I, d, device=dev)
+            K.gemm(OT_GEMM_NT, dqkv, 3 * d, 3 * d, ma['rows'][0], m.p(f'blk.{l}.wqkv'), 3 * d * d, 3 * d, d,
+                   ma['tile_group'], na, dxn1, d, ma['rows'][0], m_rows=maps['all'].nrows)
+            K.rmsnorm_bwd(dxn1, d, x, d, m.p(f'blk.{l}.norm1'), rstd1, dx, d, B * I, d, dres=dx1, lddres=d,
+                          dres_tail=(Kq, I) if Kq < I else (0, 0), dgamma=m.g(f'blk.{l}.norm1'), accumulate=acc,
+                          device=dev)
+        return None, dx, None, None, None, None, None, None, None
 
 
 def _wgrad_single(m, A, D, K_, N, mt, dW, acc, dev, mrows=0):
@@ -350,6 +391,8 @@ class OneTransModel(nn.Module):
         self._tdesc = torch.from_numpy(self.layout.transpose_desc.reshape(-1)).to(self.device)
         self.tables: Dict[str, torch.Tensor] = {}
         self.accumulate_grads = False
+        # fuse the RMSNorms into the neighbouring GEMM epilogues when a tile holds whole rows
+        self.fuse_norms = (config.hidden_dim == TILE and os.environ.get('ONETRANS_FUSE_NORMS', '1') != '0')
         self.kv_cache = None                      # model.py:333 (reference attribute; never populated)
         self._pending_sparse: List = []
         self._plans: Dict = {}
@@ -601,9 +644,10 @@ class OneTransModel(nn.Module):
         x = _Tokenize.apply(self.flat, self, plan)
         sched = self.config.pyramid_schedule(plan['L0'])
         nl = len(sched)
+        rstd = None
         for l, s in enumerate(sched):
             Kq = s['keep'] if l < nl - 1 else 1
-            x = _Block.apply(self.flat, x, self, l, s['in_len'], Kq, seed, training)
+            x, rstd = _Block.apply(self.flat, x, self, l, s['in_len'], Kq, seed, training, rstd)
         return _Head.apply(self.flat, x, self)
 
     # ---------------------------------------------------------------- reference API

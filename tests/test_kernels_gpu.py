@@ -11,7 +11,8 @@ pytestmark = pytest.mark.gpu
 
 from recommend_amd import kernels as K
 from recommend_amd._lib import (OT_AX_GELU, OT_AX_NONE, OT_AX_RMSNORM, OT_EPI_ACCUMULATE, OT_EPI_BIAS,
-                                OT_EPI_DROPOUT, OT_EPI_GELU, OT_EPI_GELU_BWD, OT_EPI_RESIDUAL, OT_GEMM_NN, OT_GEMM_NT)
+                                OT_EPI_DROPOUT, OT_EPI_GELU, OT_EPI_GELU_BWD, OT_EPI_RESIDUAL, OT_EPI_RMSNORM_BWD,
+                                OT_EPI_ROW_RSTD, OT_GEMM_NN, OT_GEMM_NT)
 from recommend_amd.layout import build_map
 from oracle import keras_math as km
 
@@ -218,6 +219,62 @@ def test_rmsnorm(dev, d):
     idx = np.arange(rows * d, dtype=np.uint64).reshape(rows, d)
     keep = torch.from_numpy(km.dropout_keep(7, 3, idx, 0.3).astype(np.float64))
     torch.testing.assert_close(dxm.double().cpu(), ref_dx * keep / 0.7, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize('K_', [128, 512])
+def test_gemm_rms_epilogues(dev, K_):
+    """ot_mixed_gemm_rms: (1) residual GEMM emitting the next RMSNorm's rstd, (2) dgrad GEMM with the
+    RMSNorm backward (tail-mapped residual gradient, masked copy, dgamma) — vs torch fp64."""
+    rng = np.random.default_rng(5)
+    G, N, Kq, I = 3, 128, 5, 12
+    B = 61
+    M = B * I
+    counts = [300, 79, M - 379]
+    A = torch.randn(M, K_, dtype=torch.float64)
+    W = torch.randn(G, N, K_, dtype=torch.float64) / math.sqrt(K_)
+    rm = _random_map(rng, M, M, G, counts)
+    d = rm.to(dev)
+    prod = torch.empty(M, N, dtype=torch.float64)
+    for t in range(rm.ntiles):
+        r_in, r_out = rm.rows[0][t * 128:(t + 1) * 128], rm.rows[1][t * 128:(t + 1) * 128]
+        ok = r_in >= 0
+        prod[torch.from_numpy(r_out[ok]).long()] = A[torch.from_numpy(r_in[ok]).long()] @ W[rm.tile_group[t]].T
+    Ad, Wd = A.float().to(dev), W.float().to(dev)
+    # (1) C = res + prod, rstd of C's rows
+    res = torch.randn(M, N, dtype=torch.float64)
+    C = torch.empty(M, N, device=dev)
+    rs = torch.empty(M, device=dev)
+    K.gemm_rms(OT_GEMM_NT, Ad, K_, K_, d['rows'][0], Wd, N * K_, K_, N, d['tile_group'], rm.ntiles, C, N,
+               d['rows'][1], epi=OT_EPI_RESIDUAL | OT_EPI_ROW_RSTD, res=res.float().to(dev), ldres=N, rstd_out=rs,
+               eps=1e-6)
+    ref = res + prod
+    torch.testing.assert_close(C.double().cpu(), ref, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(rs.double().cpu(), torch.rsqrt((ref * ref).mean(1) + 1e-6), rtol=1e-5, atol=1e-6)
+    # (2) the product is dL/dy of y = rmsnorm(x) * gamma
+    x = torch.randn(M, N, dtype=torch.float64)
+    gamma = 1 + 0.1 * torch.randn(N, dtype=torch.float64)
+    rstd = torch.rsqrt((x * x).mean(1) + 1e-6)
+    xr, gr = x.clone().requires_grad_(True), gamma.clone().requires_grad_(True)
+    yr = xr * torch.rsqrt((xr * xr).mean(1, keepdim=True) + 1e-6) * gr
+    yr.backward(prod)
+    dres_c = torch.randn(B * Kq, N, dtype=torch.float64)
+    dres_full = torch.zeros(M, N, dtype=torch.float64)
+    for b in range(B):
+        dres_full[b * I + I - Kq:b * I + I] = dres_c[b * Kq:(b + 1) * Kq]
+    dx = torch.empty(M, N, device=dev)
+    dxm = torch.empty(M, N, device=dev)
+    dg = torch.full((N,), 0.5, device=dev)
+    K.gemm_rms(OT_GEMM_NT, Ad, K_, K_, d['rows'][0], Wd, N * K_, K_, N, d['tile_group'], rm.ntiles, dx, N,
+               d['rows'][1], epi=OT_EPI_RMSNORM_BWD | OT_EPI_DROPOUT, seed=11, site=4, drop=0.25, tail=(1, 1),
+               nx=x.float().to(dev), ldnx=N, ngamma=gamma.float().to(dev), nrstd=rstd.float().to(dev),
+               dres=dres_c.float().to(dev), lddres=N, dres_tail=(Kq, I), dx_masked=dxm, lddxm=N, dgamma=dg,
+               accumulate_dgamma=True)
+    ref_dx = xr.grad + dres_full
+    torch.testing.assert_close(dx.double().cpu(), ref_dx, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(dg.double().cpu(), gr.grad + 0.5, rtol=1e-4, atol=1e-3)
+    idx = np.arange(M * N, dtype=np.uint64).reshape(M, N)
+    keep = torch.from_numpy(km.dropout_keep(11, 4, idx, 0.25).astype(np.float64))
+    torch.testing.assert_close(dxm.double().cpu(), ref_dx * keep / 0.75, rtol=1e-4, atol=1e-4)
 
 
 def test_sparse_adagrad(dev):

@@ -45,6 +45,9 @@ CASES = {
     'criteo_head': lambda: small_criteo('head'),
     'criteo_tail_pyramid': lambda: small_criteo('tail', pyramid=True, layers=3),
     'criteo_d128_hd32': lambda: small_criteo('head', d=128, H=4, f=256, Lns=12, seq_lens=(20, 20, 20)),
+    # d == 128: RMSNorms fused into the GEMM epilogues (row rstd / norm backward), pyramid tail maps
+    'criteo_d128_pyramid': lambda: small_criteo('tail', pyramid=True, layers=3, d=128, H=4, f=256, Lns=12,
+                                                seq_lens=(20, 20, 20)),
 }
 
 
@@ -79,7 +82,8 @@ def ns_t(d, dev):
     return {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in d.items()}
 
 
-@pytest.mark.parametrize('case', ['c1_head', 'criteo_head', 'criteo_tail_pyramid'])
+@pytest.mark.parametrize('case', ['c1_head', 'criteo_head', 'criteo_tail_pyramid', 'criteo_d128_hd32',
+                                  'criteo_d128_pyramid'])
 @pytest.mark.parametrize('training', [False, True])
 def test_gradient_parity(dev, case, training):
     cfg = CASES[case]()
@@ -114,7 +118,7 @@ def test_gradient_parity(dev, case, training):
         assert (dense - rg[tname]).abs().max().item() / scale < 2e-4, tname
 
 
-@pytest.mark.parametrize('case', ['c1_head', 'criteo_head'])
+@pytest.mark.parametrize('case', ['c1_head', 'criteo_head', 'criteo_d128_pyramid'])
 def test_train_steps_parity(dev, case):
     cfg = CASES[case]()
     cfg.optimizer_config = dict(cfg.optimizer_config, dense_lr=0.001, momentum=0.9)
@@ -150,3 +154,22 @@ def test_auc_parity(dev):
         a = auc(lab[t], out[t].cpu().numpy())
         b = auc(lab[t], ref['probs'][t].numpy())
         assert abs(a - b) < 1e-3, (t, a, b)
+
+
+def test_fused_norms_match_unfused(dev):
+    """d == 128: the GEMM-epilogue RMSNorms give the same loss and gradients as the row-wise kernels."""
+    cfg = CASES['criteo_d128_pyramid']()
+    P, model, batch = setup(cfg, 41, dev)
+    ns, seq, lab = batch
+    y = stack_labels(lab, cfg.tasks, dev)
+    res = []
+    for fuse in (True, False):
+        model.fuse_norms = fuse
+        model.flat.grad.zero_()
+        model._step = 0
+        loss = keras_bce_loss(y, model.forward_probs(ns_t(ns, dev), ns_t(seq, dev), training=True))
+        loss.backward()
+        res.append((loss.item(), model.flat.grad.clone()))
+    assert abs(res[0][0] - res[1][0]) < 1e-5
+    scale = res[1][1].abs().max().item()
+    assert (res[0][1] - res[1][1]).abs().max().item() / scale < 1e-5

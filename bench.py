@@ -111,6 +111,21 @@ def cpu_baseline(cfg_name, seconds):
                       f'restatement of model.py/train.py; tables capped at 2e4/5e4 rows), {el:.1f}s'}
 
 
+def hbm_traffic(config):
+    """HBM bytes per launch of the GEMM family from the newest committed PMC summary
+    (tools/hbm_traffic.py: separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes over this bench,
+    calibrated on a known 1 GiB copy).  (None, None) when no summary for this config exists."""
+    import glob
+    for fn in sorted(glob.glob(os.path.join(ROOT, 'profiles', '*', 'hbm_traffic.json')), reverse=True):
+        try:
+            d = json.load(open(fn))
+        except (OSError, ValueError):
+            continue
+        if d.get('config') == config and 'gemm' in d.get('families', {}):
+            return round(d['families']['gemm']['hbm_bytes_per_launch']), os.path.relpath(fn, ROOT)
+    return None, None
+
+
 def main():
     args = parse()
     world, rank, local = init_dist(args)
@@ -184,11 +199,14 @@ def main():
         'final_loss': round(loss, 5),
     }
     if probe is not None:
+        traffic, tsrc = hbm_traffic(args.config)
         rep = probe.report(args.steps)
         dom = rep['families']['mixed_gemm']
         res['roofline'] = {'bound': 'mfma', 'kernel': 'mixed_gemm_kernel + wgrad_kernel (fp32 MFMA)',
                            'achieved': round(dom['tflops'], 2), 'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-                           'frac': round(dom['tflops'] / FP32_MFMA_PEAK_TFLOPS, 4), 'traffic': None,
+                           'frac': round(dom['tflops'] / FP32_MFMA_PEAK_TFLOPS, 4), 'traffic': traffic,
+                           'traffic_unit': 'HBM bytes per launch (PMC FETCH_SIZE + WRITE_SIZE, calibrated)',
+                           'traffic_source': tsrc,
                            'avg_launch_us': round(dom['avg_us'], 2), 'launches_per_step': dom['launches_per_step'],
                            'gflop_per_launch': round(dom['gflop_per_launch'], 3)}
         res['kernel_time_ms_per_step'] = {k: round(v['ms_per_step'], 3) for k, v in rep['families'].items()}

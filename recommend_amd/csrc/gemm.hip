@@ -428,25 +428,13 @@ __global__ __launch_bounds__(256, 2) void mixed_gemm_kernel(GemmArgs p) {
 
 // ------------------------------------------------------------------------------------------
 // wgrad: partial slab per (chunk, k-tile, n-tile):  slab[c][k][n] = sum_{rows of chunk} A^T D
-// LDS images: As[k][r] and Ds[n][r] (r contiguous, BR = 32 rows per stage).
-// Default: row stride 36 (the ds_read_b128 fragment reads are conflict-free, the transposed
-// ds_write_b32 staging is 4-way conflicted).  OT_WGRAD_SWZ=1 with WLD=32 stores (k, r) at
-// k * WLD + (r ^ wswz(k)), conflict-free for both (tools/lds_conflicts.py), but measured slower on
-// the RMSNorm-prologue wgrads (82 -> 71 TF/s), so it stays off.
-#ifndef OT_WGRAD_WLD
-#define OT_WGRAD_WLD 36
-#endif
-#ifndef OT_WGRAD_SWZ
-#define OT_WGRAD_SWZ 0
-#endif
-#ifndef OT_WGRAD_LDS_EXTRA
-#define OT_WGRAD_LDS_EXTRA 0
-#endif
+// LDS images are row-major, as loaded: As[r][k], Ds[r][n] (BR = 32 rows per stage, row stride 128,
+// no padding): the staging stores are whole 16-B pieces of 512-B rows (conflict-free), and the
+// MFMA operands need no transpose — the reduction row is the MFMA k index, so lane (li, h) of step
+// s reads As[2s + h][k0 + li] (32 consecutive floats per half-wave: conflict-free ds_read_b32, two
+// steps per ds_read2st64_b32).
 constexpr int WBR = 32;
-constexpr int WLD = OT_WGRAD_WLD;
-__device__ __forceinline__ int wswz(int k) {
-  return OT_WGRAD_SWZ ? 4 * ((((k >> 1) ^ (k >> 4)) & 1) | ((k >> 2) & 2) | (k & 4)) : 0;
-}
+constexpr int WLD = GT;
 
 struct WgradArgs {
   const float* A; int64_t lda; const int32_t* a_rows; int a_xform; const float* a_rstd; const float* a_gamma;
@@ -462,7 +450,7 @@ struct WgradArgs {
 template <int AXT>
 __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  // [2][GT][WLD] for A^T (k, r) then [2][GT][WLD] for D^T (n, r)
+  // [NBUF][WBR][WLD] for A (r, k) then [NBUF][WBR][WLD] for D (r, n)
   const int ax = AXT >= 0 ? AXT : p.a_xform;
   const int per_chunk = p.ntk * p.ntn;
   const int c = blockIdx.x / per_chunk;
@@ -474,7 +462,6 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
   const int h = lane >> 5, li = lane & 31;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
   const int sr = t >> 3, sc = t & 7;       // staging: row sr of the stage, float4 columns sc + 8i
-  const int swz = wswz(li);                // wm, wn, 32m are multiples of 32: the swizzle depends on li
   const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
 
   f32x16 acc[2][2];
@@ -517,8 +504,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
   };
   constexpr int NBUF = OT_WGRAD_DBUF ? 2 : 1;
   auto store_stage = [&](int buf) {
-    float* As = smem + buf * GT * WLD;
-    float* Ds = smem + (NBUF + buf) * GT * WLD;
+    float* As = smem + buf * WBR * WLD;
+    float* Ds = smem + (NBUF + buf) * WBR * WLD;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int kk = 4 * (sc + 8 * i);
@@ -530,10 +517,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
       }
       if (!(aok && k0 + kk < p.K)) a = zero4;
       if (!(dok && n0 + kk < p.N)) dv = zero4;
-      const int o0 = (kk + 0) * WLD + (sr ^ wswz(kk + 0)), o1 = (kk + 1) * WLD + (sr ^ wswz(kk + 1));
-      const int o2 = (kk + 2) * WLD + (sr ^ wswz(kk + 2)), o3 = (kk + 3) * WLD + (sr ^ wswz(kk + 3));
-      As[o0] = a.x; As[o1] = a.y; As[o2] = a.z; As[o3] = a.w;
-      Ds[o0] = dv.x; Ds[o1] = dv.y; Ds[o2] = dv.z; Ds[o3] = dv.w;
+      *reinterpret_cast<f32x4*>(As + sr * WLD + kk) = a;
+      *reinterpret_cast<f32x4*>(Ds + sr * WLD + kk) = dv;
     }
   };
 
@@ -552,32 +537,29 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
       load_stage(st + 1, ar2, dr2);                       // stage st+1 data
       if (st + 2 < nst) rows_of((st + 2) * WBR, ar3, dr3);   // stage st+2 row indices
     }
-    const float* As = smem + cur * GT * WLD;
-    const float* Ds = smem + (NBUF + cur) * GT * WLD;
+    const float* As = smem + cur * WBR * WLD;
+    const float* Ds = smem + (NBUF + cur) * WBR * WLD;
     if (do_bias) {
 #pragma unroll
-      for (int q = 0; q < WBR; q += 4) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(Ds + t * WLD + (q ^ wswz(t)));
-        bsum += (v.x + v.y) + (v.z + v.w);
-      }
+      for (int r = 0; r < WBR; r += 4)
+        bsum += (Ds[r * WLD + t] + Ds[(r + 1) * WLD + t]) + (Ds[(r + 2) * WLD + t] + Ds[(r + 3) * WLD + t]);
     }
-    // 16 MFMA k-steps over the 32 rows: lane half h supplies row 16h + s
-    f32x4 fa[2][4], fb[2][4];
+    // 16 MFMA k-steps over the 32 rows: step s takes rows 2s (lane half 0) and 2s + 1 (half 1)
+    float fa[16][2], fb[16][2];
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
+    for (int s2 = 0; s2 < 16; ++s2)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        fa[m][q] = *reinterpret_cast<const f32x4*>(As + (wm + 32 * m + li) * WLD + ((16 * h + 4 * q) ^ swz));
-        fb[m][q] = *reinterpret_cast<const f32x4*>(Ds + (wn + 32 * m + li) * WLD + ((16 * h + 4 * q) ^ swz));
+      for (int m = 0; m < 2; ++m) {
+        fa[s2][m] = As[(2 * s2 + h) * WLD + wm + 32 * m + li];
+        fb[s2][m] = Ds[(2 * s2 + h) * WLD + wn + 32 * m + li];
       }
 #pragma unroll
-    for (int s = 0; s < 16; ++s)
+    for (int s2 = 0; s2 < 16; ++s2)
 #pragma unroll
       for (int m = 0; m < 2; ++m)
 #pragma unroll
         for (int n = 0; n < 2; ++n)
-          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[m][s >> 2][s & 3], fb[n][s >> 2][s & 3],
-                                                           acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[s2][m], fb[s2][n], acc[m][n], 0, 0, 0);
     if (NBUF == 2) {
       if (more) store_stage(cur ^ 1);
       __syncthreads();
@@ -857,7 +839,7 @@ extern "C" int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a
   if (nchunks > 0) {
     WgradArgs p{A, lda, a_rows, a_xform, a_rstd, a_gamma, D, ldd, d_rows, K, N, chunks, nchunks, slab, bslab,
                 (int)ceil_div(K, GT), (int)ceil_div(N, GT)};
-    const size_t shmem = (OT_WGRAD_DBUF ? 4 : 2) * GT * WLD * sizeof(float) + OT_WGRAD_LDS_EXTRA;
+    const size_t shmem = (OT_WGRAD_DBUF ? 4 : 2) * WBR * WLD * sizeof(float);
     void (*kern)(WgradArgs) = a_xform == OT_AX_NONE      ? wgrad_kernel<OT_AX_NONE>
                               : a_xform == OT_AX_RMSNORM ? wgrad_kernel<OT_AX_RMSNORM>
                               : a_xform == OT_AX_GELU    ? wgrad_kernel<OT_AX_GELU>
@@ -866,7 +848,7 @@ extern "C" int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a
     std::call_once(lds_once, [] {
       for (void (*k)(WgradArgs) : {wgrad_kernel<OT_AX_NONE>, wgrad_kernel<OT_AX_RMSNORM>, wgrad_kernel<OT_AX_GELU>,
                                    wgrad_kernel<-1>})
-        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * GT * WLD * 4 + OT_WGRAD_LDS_EXTRA);
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * WBR * WLD * 4);
       (void)hipGetLastError();
     });
     hipLaunchKernelGGL(kern, dim3((unsigned)nchunks * p.ntk * p.ntn), dim3(256), shmem, s, p);

@@ -34,8 +34,8 @@ HBM_PEAK_GBS = 8000.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=20)
-    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--steps', type=int, default=50)
+    ap.add_argument('--warmup', type=int, default=10)
     ap.add_argument('--config', default='C2')
     ap.add_argument('--batch', type=int, default=0, help='per-GPU batch (default: the config\'s)')
     ap.add_argument('--nbatches', type=int, default=4, help='distinct resident batches cycled')
@@ -51,8 +51,16 @@ def init_dist(args):
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if world > 1:
         import torch.distributed as dist
+        # OT_BENCH_BACKEND=gloo OT_BENCH_SAME_DEVICE=1 rehearses the N>1 path on a one-GPU box (every
+        # rank on cuda:0, collectives over gloo); the real multi-GPU run uses RCCL ("nccl"), one GPU/rank
+        if os.environ.get('OT_BENCH_SAME_DEVICE') == '1':
+            local = 0
         torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        backend = os.environ.get('OT_BENCH_BACKEND', 'nccl')
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     return world, rank, local
@@ -210,7 +218,7 @@ def main():
                            'avg_launch_us': round(dom['avg_us'], 2), 'launches_per_step': dom['launches_per_step'],
                            'gflop_per_launch': round(dom['gflop_per_launch'], 3)}
         res['kernel_time_ms_per_step'] = {k: round(v['ms_per_step'], 3) for k, v in rep['families'].items()}
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and world == 1:          # rank 0 at N=1 only
         res['cpu_baseline'] = cpu_baseline(args.config, args.cpu_seconds)
     print(json.dumps(res), flush=True)
 

@@ -22,6 +22,12 @@ namespace ot {
 #ifndef OT_GEMM_BK
 #define OT_GEMM_BK 16
 #endif
+#ifndef OT_GEMM_MINWG
+#define OT_GEMM_MINWG 3
+#endif
+#ifndef OT_GEMM_PRIO
+#define OT_GEMM_PRIO 0
+#endif
 #ifndef OT_GEMM_RMS_EARLY
 #define OT_GEMM_RMS_EARLY 1
 #endif
@@ -80,7 +86,7 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 // AXT / EPIT: compile-time prologue / epilogue (-1 = read p.a_xform / p.epi at run time).
 // EDGE: K % 32 != 0 or N % 128 != 0 (bounds checks in staging and epilogue).
 template <bool NT, int AXT, int EPIT, bool EDGE>
-__global__ __launch_bounds__(256, 2) void mixed_gemm_kernel(GemmArgs p) {
+__global__ __launch_bounds__(256, OT_GEMM_MINWG) void mixed_gemm_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* As = smem;                      // [2][GT][GLD]
   float* Bs = smem + 2 * GT * GLD;       // [2][GT][GLD]
@@ -212,6 +218,7 @@ __global__ __launch_bounds__(256, 2) void mixed_gemm_kernel(GemmArgs p) {
           fa[m][q] = *reinterpret_cast<const f32x4*>(as + 32 * m * GLD + 8 * half + 4 * q);
           fb[m][q] = *reinterpret_cast<const f32x4*>(bs + 32 * m * GLD + 8 * half + 4 * q);
         }
+      if (OT_GEMM_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int s = 0; s < 8; ++s)
 #pragma unroll
@@ -220,6 +227,7 @@ __global__ __launch_bounds__(256, 2) void mixed_gemm_kernel(GemmArgs p) {
           for (int n = 0; n < 2; ++n)
             acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[m][s >> 2][s & 3], fb[n][s >> 2][s & 3],
                                                              acc[m][n], 0, 0, 0);
+      if (OT_GEMM_PRIO) __builtin_amdgcn_s_setprio(0);
     }
     // the other buffer was last read in iteration kt-1, which every wave finished before the
     // barrier that ended it: one barrier per k-tile

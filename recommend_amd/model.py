@@ -118,6 +118,7 @@ class _Tokenize(torch.autograd.Function):
             K.rows_colsum(dx0, d, plan['sep_rows'], plan['n_sep'], d, m.g('tok.sep'), accumulate=acc, device=dev)
         elif not acc:
             m.g('tok.sep').zero_()
+        m.join_side_stream()          # last backward of the graph: every block's weight gradients are in
         return None, None, None
 
 
@@ -223,15 +224,18 @@ class _Block(torch.autograd.Function):
             K.dropout_apply(dx2, d, dy2, d, B * Kq, d, seed, 2 * l + 1, rate, (Kq, I))
         else:
             dy2 = dx2
-        K.wgrad(u, f, mt['rows'][1], dy2, d, mt['rows'][1], f, d, mt, nct, G, m.g(f'blk.{l}.w2'), f * d,
-                m.g(f'blk.{l}.b2'), d, a_xform=OT_AX_GELU, accumulate=acc, device=dev, m_rows=maps['tail'].nrows,
-                rowmap=maps['tail'])
+        side = m.side(u, dy2)          # weight gradients overlap the dgrad chain on a second stream
+        with side:
+            K.wgrad(u, f, mt['rows'][1], dy2, d, mt['rows'][1], f, d, mt, nct, G, m.g(f'blk.{l}.w2'), f * d,
+                    m.g(f'blk.{l}.b2'), d, a_xform=OT_AX_GELU, accumulate=acc, device=dev,
+                    m_rows=maps['tail'].nrows, rowmap=maps['tail'])
         du = torch.empty(B * Kq, f, device=dev)
         K.gemm(OT_GEMM_NT, dy2, d, d, mt['rows'][1], m.p(f'blk.{l}.w2'), f * d, d, f, mt['tile_group'], nt, du, f,
                mt['rows'][1], epi=OT_EPI_GELU_BWD, aux=u, ldaux=f, m_rows=maps['tail'].nrows)
-        K.wgrad(x1, d, mt['rows'][1], du, f, mt['rows'][1], d, f, mt, nct, G, m.g(f'blk.{l}.w1'), d * f,
-                m.g(f'blk.{l}.b1'), f, a_xform=OT_AX_RMSNORM, rstd=rstd2, gamma=m.p(f'blk.{l}.norm2'),
-                accumulate=acc, device=dev, m_rows=maps['tail'].nrows, rowmap=maps['tail'])
+        with m.side(x1, du, rstd2):
+            K.wgrad(x1, d, mt['rows'][1], du, f, mt['rows'][1], d, f, mt, nct, G, m.g(f'blk.{l}.w1'), d * f,
+                    m.g(f'blk.{l}.b1'), f, a_xform=OT_AX_RMSNORM, rstd=rstd2, gamma=m.p(f'blk.{l}.norm2'),
+                    accumulate=acc, device=dev, m_rows=maps['tail'].nrows, rowmap=maps['tail'])
         # FFN1 dgrad -> norm2 backward + residual; emit mask(dx1) for the attention branch
         dx1 = torch.empty(B * Kq, d, device=dev)
         dyo = torch.empty(B * Kq, d, device=dev) if rate > 0 else dx1
@@ -250,7 +254,8 @@ class _Block(torch.autograd.Function):
                           dx_masked=dyo if rate > 0 else None, lddxm=d, seed=seed, site=2 * l, drop=rate,
                           tail=(Kq, I), dgamma=m.g(f'blk.{l}.norm2'), accumulate=acc, device=dev)
         # Wo
-        _wgrad_single(m, o, dyo, d, d, mt, m.g(f'blk.{l}.wo'), acc, dev, maps['tail'].nrows)
+        with m.side(o, dyo):
+            _wgrad_single(m, o, dyo, d, d, mt, m.g(f'blk.{l}.wo'), acc, dev, maps['tail'].nrows)
         do = torch.empty(B * Kq, d, device=dev)
         K.gemm(OT_GEMM_NT, dyo, d, d, mt['rows'][1], m.p(f'blk.{l}.wo'), 0, d, d, mt['tile_group'], nt, do, d,
                mt['rows'][1], m_rows=maps['tail'].nrows)
@@ -259,9 +264,10 @@ class _Block(torch.autograd.Function):
         if Kq < I:
             dqkv[:, :d].zero_()
         K.attn_bwd(qkv, 3 * d, o, do, lse, B, H, I, Kq, hd, dqkv)
-        K.wgrad(x, d, ma['rows'][0], dqkv, 3 * d, ma['rows'][0], d, 3 * d, ma, nca, G, m.g(f'blk.{l}.wqkv'),
-                3 * d * d, None, 0, a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=m.p(f'blk.{l}.norm1'), accumulate=acc,
-                device=dev, m_rows=maps['all'].nrows, rowmap=maps['all'])
+        with m.side(x, dqkv, rstd1):
+            K.wgrad(x, d, ma['rows'][0], dqkv, 3 * d, ma['rows'][0], d, 3 * d, ma, nca, G, m.g(f'blk.{l}.wqkv'),
+                    3 * d * d, None, 0, a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=m.p(f'blk.{l}.norm1'),
+                    accumulate=acc, device=dev, m_rows=maps['all'].nrows, rowmap=maps['all'])
         dx = torch.empty(B * I, d, device=dev)
         if m.fuse_norms:       # QKV dgrad -> norm1 backward + residual (dx1 on the kept tail rows)
             K.gemm_rms(OT_GEMM_NT, dqkv, 3 * d, 3 * d, ma['rows'][0], m.p(f'blk.{l}.wqkv'), 3 * d * d, 3 * d, d,
@@ -393,6 +399,11 @@ class OneTransModel(nn.Module):
         self.accumulate_grads = False
         # fuse the RMSNorms into the neighbouring GEMM epilogues when a tile holds whole rows
         self.fuse_norms = (config.hidden_dim == TILE and os.environ.get('ONETRANS_FUSE_NORMS', '1') != '0')
+        # block weight gradients run on a second stream, overlapping the dgrad chain
+        self.overlap_wgrad = os.environ.get('ONETRANS_OVERLAP_WGRAD', '1') != '0'
+        self._side = None
+        self._side_used = False
+        self._side_keep: List[torch.Tensor] = []
         self.kv_cache = None                      # model.py:333 (reference attribute; never populated)
         self._pending_sparse: List = []
         self._plans: Dict = {}
@@ -649,6 +660,32 @@ class OneTransModel(nn.Module):
             Kq = s['keep'] if l < nl - 1 else 1
             x, rstd = _Block.apply(self.flat, x, self, l, s['in_len'], Kq, seed, training, rstd)
         return _Head.apply(self.flat, x, self)
+
+    # ---------------------------------------------------------------- side stream (wgrad overlap)
+    def side(self, *tensors):
+        """Context running the enclosed launches on the weight-gradient side stream, after the main
+        stream's pending work.  ``tensors`` (inputs produced on the main stream) are kept referenced
+        until ``join_side_stream`` has made the main stream wait for the side stream, so the caching
+        allocator cannot hand their memory to a main-stream allocation while a side kernel still reads
+        it.  (``record_stream`` would do the same but defers frees behind events, which makes the
+        allocator grow with fresh device allocations step after step.)"""
+        import contextlib
+        if not self.overlap_wgrad:
+            return contextlib.nullcontext()
+        main = torch.cuda.current_stream(self.device)
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        self._side.wait_stream(main)
+        self._side_keep.extend(tensors)
+        self._side_used = True
+        return torch.cuda.stream(self._side)
+
+    def join_side_stream(self):
+        """The main stream waits for every weight gradient launched on the side stream."""
+        if self._side is not None and self._side_used:
+            torch.cuda.current_stream(self.device).wait_stream(self._side)
+            self._side_used = False
+        self._side_keep = []
 
     # ---------------------------------------------------------------- reference API
     def reset_kv_cache(self):

@@ -14,6 +14,21 @@
 // cdna_hip_programming.md §3) with the k index of step r = the key held in register r.
 #include "common.h"
 
+#ifndef OT_ATTN_FWD_BRANCHLOAD
+#define OT_ATTN_FWD_BRANCHLOAD 1
+#endif
+#ifndef OT_ATTN_BWD_BRANCHLOAD
+#define OT_ATTN_BWD_BRANCHLOAD 1
+#endif
+#if OT_ATTN_BWD_BRANCHLOAD
+#define BWD_LOAD load_frag
+#else
+#define BWD_LOAD load_frag_clamped
+#endif
+#ifndef OT_ATTN_FWD_MASKALL
+#define OT_ATTN_FWD_MASKALL 0
+#endif
+
 namespace ot {
 
 struct AttnArgs {
@@ -104,6 +119,22 @@ __device__ __forceinline__ void acc_tile_p(f32x16 (&acc)[NB(HD)], const float* t
   }
 }
 
+// Fragment as load_frag, but rows >= nrows read row nrows - 1 (finite data that the masks null).
+template <int HD>
+__device__ __forceinline__ void load_frag_clamped(float (&f)[HD / 2], const float* base, int64_t ld, int row,
+                                                  int nrows, int hh) {
+  const float* p = base + (int64_t)(row < nrows ? row : nrows - 1) * ld + (HD / 2) * hh;
+#pragma unroll
+  for (int q = 0; q < HD / 8; ++q) {
+    f32x4 v = *reinterpret_cast<const f32x4*>(p + 4 * q);
+    f[4 * q] = v.x; f[4 * q + 1] = v.y; f[4 * q + 2] = v.z; f[4 * q + 3] = v.w;
+  }
+}
+
+// Forward.  Scores are kept in the log2 domain (q pre-scaled by log2(e)/sqrt(hd), one multiply per
+// q element) so the online softmax uses v_exp_f32 directly; the causal mask is applied on the
+// diagonal key block only (earlier blocks are fully visible); K/V rows past the end are loaded from
+// a clamped row (finite) and removed by the mask, so the loads carry no branches.
 template <int HD>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs p) {
   __shared__ __attribute__((aligned(16))) float lds[4][32 * TLD<HD>()];
@@ -118,11 +149,14 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs p) {
   const float* V = Q + 2 * p.d;
   const float* Qt = Q + (int64_t)q_off * p.ld;      // tail rows
   const int nqb = (K + 31) / 32;
+  const float qscale = p.scale * 1.4426950408889634f;   // log2(e) / sqrt(hd)
   for (int qb = 0; qb < nqb; ++qb) {
     const int j = 32 * qb + li;                     // this lane's query (tail index)
     const int qpos = q_off + (j < K ? j : K - 1);
     float qf[HD / 2];
-    load_frag<HD>(qf, Qt, p.ld, j, K, hh);
+    load_frag_clamped<HD>(qf, Qt, p.ld, j, K, hh);
+#pragma unroll
+    for (int s = 0; s < HD / 2; ++s) qf[s] *= qscale;
     f32x16 oacc[NB(HD)];
 #pragma unroll
     for (int c = 0; c < NB(HD); ++c)
@@ -131,29 +165,34 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs p) {
     float m = -INFINITY, l = 0.f;
     const int last_q = q_off + min(32 * qb + 31, K - 1);
     const int nkb = last_q / 32 + 1;
+    const int first_masked = (q_off + 32 * qb) / 32;     // key blocks >= this one may be masked
     for (int kb = 0; kb < nkb; ++kb) {
       const int key0 = 32 * kb;
       float kf[HD / 2], vf[HD / 2];
+#if OT_ATTN_FWD_BRANCHLOAD
       load_frag<HD>(kf, Kp, p.ld, key0 + li, I, hh);
       load_frag<HD>(vf, V, p.ld, key0 + li, I, hh);
+#else
+      load_frag_clamped<HD>(kf, Kp, p.ld, key0 + li, I, hh);
+      load_frag_clamped<HD>(vf, V, p.ld, key0 + li, I, hh);
+#endif
       frag_to_lds<HD>(tV, vf, li, hh);
-      f32x16 s = mm_frag<HD>(kf, qf);               // S^T: row = key, col = query
-      float mloc = -INFINITY;
+      f32x16 s = mm_frag<HD>(kf, qf);               // S^T (log2 units): row = key, col = query
+      if (OT_ATTN_FWD_MASKALL || kb >= first_masked) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int kpos = key0 + acc_row(r, hh);
-        float v = s[r] * p.scale;
-        v = (kpos <= qpos) ? v : -INFINITY;         // kpos <= qpos < I
-        s[r] = v;
-        mloc = fmaxf(mloc, v);
+        for (int r = 0; r < 16; ++r)
+          s[r] = (key0 + acc_row(r, hh) <= qpos) ? s[r] : -INFINITY;   // kpos <= qpos < I
       }
+      float mloc = s[0];
+#pragma unroll
+      for (int r = 1; r < 16; ++r) mloc = fmaxf(mloc, s[r]);
       mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
       const float mnew = fmaxf(m, mloc);            // finite: key 0 is always visible
-      const float corr = __expf(m - mnew);
+      const float corr = __builtin_amdgcn_exp2f(m - mnew);
       float lsum = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float e = __expf(s[r] - mnew);
+        const float e = __builtin_amdgcn_exp2f(s[r] - mnew);
         s[r] = e;
         lsum += e;
       }
@@ -180,7 +219,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs p) {
             *reinterpret_cast<f32x4*>(orow + dd) = v;
           }
         }
-      if (hh == 0) p.lse[((int64_t)b * p.H + h) * K + j] = m + __logf(l);
+      // natural-log lse for the backward: m (log2 units) * ln 2 + ln l
+      if (hh == 0) p.lse[((int64_t)b * p.H + h) * K + j] = m * 0.6931471805599453f + __logf(l);
     }
   }
 }
@@ -239,18 +279,6 @@ __global__ __launch_bounds__(256) void attn_bwd_prep_kernel(const float* __restr
 // Padding is branch-free: rows past the end (keys >= I, queries >= K) are loaded from a clamped
 // in-bounds row; padded keys are removed by the causal select, padded queries by lse = +inf.
 
-// Fragment as load_frag, but rows >= nrows read row nrows - 1 (finite data that the masks null).
-template <int HD>
-__device__ __forceinline__ void load_frag_clamped(float (&f)[HD / 2], const float* base, int64_t ld, int row,
-                                                  int nrows, int hh) {
-  const float* p = base + (int64_t)(row < nrows ? row : nrows - 1) * ld + (HD / 2) * hh;
-#pragma unroll
-  for (int q = 0; q < HD / 8; ++q) {
-    f32x4 v = *reinterpret_cast<const f32x4*>(p + 4 * q);
-    f[4 * q] = v.x; f[4 * q + 1] = v.y; f[4 * q + 2] = v.z; f[4 * q + 3] = v.w;
-  }
-}
-
 template <int HD>
 constexpr int BWD_WAVES() { return HD >= 128 ? 2 : 4; }
 
@@ -290,8 +318,8 @@ __global__ __launch_bounds__(64 * BWD_WAVES<HD>(), 2) void attn_bwd_kernel(AttnA
     const int key0 = 32 * kb;
     const int kpos = key0 + li;                        // this lane's key
     float kf[HD / 2], vf[HD / 2];
-    load_frag_clamped<HD>(kf, Kp, p.ld, kpos, I, hh);
-    load_frag_clamped<HD>(vf, V, p.ld, kpos, I, hh);
+    BWD_LOAD<HD>(kf, Kp, p.ld, kpos, I, hh);
+    BWD_LOAD<HD>(vf, V, p.ld, kpos, I, hh);
     frag_to_lds<HD>(tK, kf, li, hh);
     f32x16 dk[NB(HD)], dv[NB(HD)];
 #pragma unroll
@@ -302,8 +330,8 @@ __global__ __launch_bounds__(64 * BWD_WAVES<HD>(), 2) void attn_bwd_kernel(AttnA
     float qf[HD / 2], of[HD / 2];
     f32x4 l4[4], d4[4];
     auto load_qblock = [&](int q0) {
-      load_frag_clamped<HD>(qf, Qt, p.ld, q0 + li, K, hh);
-      load_frag_clamped<HD>(of, dO, p.d, q0 + li, K, hh);
+      BWD_LOAD<HD>(qf, Qt, p.ld, q0 + li, K, hh);
+      BWD_LOAD<HD>(of, dO, p.d, q0 + li, K, hh);
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         l4[g] = *reinterpret_cast<const f32x4*>(lsep + q0 + 8 * g + 4 * hh);

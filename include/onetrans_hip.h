@@ -203,6 +203,16 @@ size_t ot_sparse_adagrad_workspace_size(int64_t n, int E);
 int ot_sparse_adagrad(float* table, float* accum, int E, int64_t num_rows, const int64_t* keys,
                       const float* grads, int64_t n, float lr, float eps, float clip,
                       void* workspace, size_t ws_bytes, void* stream);
+/* Data-parallel form for replicated tables small enough to exchange densely (all-reduce instead of
+ * an all-gather of every rank's rows): dense[key] = sum of the rows of key (dense zeroed by the
+ * caller; same de-duplication as ot_sparse_adagrad, workspace ot_sparse_adagrad_workspace_size),
+ * then clip_by_norm + Keras Adagrad over all rows (zero-gradient rows stay bitwise unchanged, i.e.
+ * the same update as the sparse path). */
+int ot_sparse_grad_dense(int E, int64_t num_rows, const int64_t* keys, const float* grads, int64_t n,
+                         float* dense, void* workspace, size_t ws_bytes, void* stream);
+size_t ot_dense_adagrad_workspace_size(void);
+int ot_dense_adagrad(float* table, float* accum, const float* grad, int64_t num_rows, int E, float lr,
+                     float eps, float clip, void* workspace, size_t ws_bytes, void* stream);
 
 /* ---- dense optimizer (optim.hip) ----------------------------------------------------------
  * Per-variable tf.clip_by_norm (train.py:134-135) over 2-D strided segments of one flat

@@ -72,6 +72,9 @@ SIGNATURES = {
     'ot_bce_bwd': (c_int, [P, P, P, c_int, c_int, P, P]),
     'ot_sparse_adagrad_workspace_size': (c_size_t, [I64, c_int]),
     'ot_sparse_adagrad': (c_int, [P, P, c_int, I64, P, P, I64, c_float, c_float, c_float, P, c_size_t, P]),
+    'ot_sparse_grad_dense': (c_int, [c_int, I64, P, P, I64, P, P, c_size_t, P]),
+    'ot_dense_adagrad_workspace_size': (c_size_t, []),
+    'ot_dense_adagrad': (c_int, [P, P, P, I64, c_int, c_float, c_float, c_float, P, c_size_t, P]),
     'ot_clip_rmsprop_workspace_size': (c_size_t, [c_int, I64]),
     'ot_clip_rmsprop': (c_int, [P, P, P, P, P, c_int, I64, c_float, c_float, c_float, c_float, c_float, P,
                                 c_size_t, P]),

@@ -149,6 +149,57 @@ __global__ __launch_bounds__(256) void adagrad_apply_kernel(float* table, float*
   }
 }
 
+// Dense form of a replicated table's gradient (data-parallel exchange by all-reduce): the unique
+// rows' sums scattered into a zeroed [num_rows, E] buffer (unique keys: no conflicts).
+__global__ __launch_bounds__(256) void scatter_rows_kernel(float* dense, int E, const uint32_t* __restrict__ ksorted,
+                                                           const int32_t* __restrict__ seg_start,
+                                                           const int32_t* __restrict__ nuniq,
+                                                           const float* __restrict__ gsum, int tps) {
+  const int spb = 256 / tps;
+  const int64_t s = (int64_t)blockIdx.x * spb + threadIdx.x / tps;
+  const int lt = threadIdx.x % tps;
+  if (s >= nuniq[0]) return;
+  const uint32_t key = ksorted[seg_start[s]];
+  if (key == 0xFFFFFFFFu) return;
+  for (int c = lt * 4; c < E; c += tps * 4)
+    *reinterpret_cast<f32x4*>(dense + (int64_t)key * E + c) = *reinterpret_cast<const f32x4*>(gsum + s * E + c);
+}
+
+// sum of squares of a dense gradient: per-block partials (fixed grid-stride order: deterministic)
+__global__ __launch_bounds__(256) void dense_sumsq_kernel(const float* __restrict__ g, int64_t n4, float* part) {
+  __shared__ float red[4];
+  float sq = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(g + 4 * i);
+    sq += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  sq = wave_sum(sq);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// Keras Adagrad over every row; rows with a zero gradient are left bitwise unchanged (acc + 0,
+// w - 0), i.e. exactly the sparse update of the touched rows.
+__global__ __launch_bounds__(256) void dense_adagrad_kernel(float* table, float* accum, const float* __restrict__ g,
+                                                            int64_t n4, const float* __restrict__ scale, float lr,
+                                                            float eps) {
+  const float sc = scale[0];
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const f32x4 gv = *reinterpret_cast<const f32x4*>(g + 4 * i) * sc;
+    if (gv.x == 0.f && gv.y == 0.f && gv.z == 0.f && gv.w == 0.f) continue;
+    f32x4 av = *reinterpret_cast<const f32x4*>(accum + 4 * i) + gv * gv;
+    f32x4 wv = *reinterpret_cast<const f32x4*>(table + 4 * i);
+    wv.x -= lr * gv.x / sqrtf(av.x + eps);
+    wv.y -= lr * gv.y / sqrtf(av.y + eps);
+    wv.z -= lr * gv.z / sqrtf(av.z + eps);
+    wv.w -= lr * gv.w / sqrtf(av.w + eps);
+    *reinterpret_cast<f32x4*>(accum + 4 * i) = av;
+    *reinterpret_cast<f32x4*>(table + 4 * i) = wv;
+  }
+}
+constexpr int DENSE_GRID = 2048;
+
 struct SparseWs {
   uint32_t *k_in, *k_out;
   int32_t *v_in, *v_out, *flags, *pos, *seg_start, *nuniq, *pcount, *pstart;
@@ -203,17 +254,10 @@ extern "C" size_t ot_sparse_adagrad_workspace_size(int64_t n, int E) {
   return carve(nullptr, n, E).total;
 }
 
-extern "C" int ot_sparse_adagrad(float* table, float* accum, int E, int64_t num_rows, const int64_t* keys,
-                                 const float* grads, int64_t n, float lr, float eps, float clip, void* workspace,
-                                 size_t ws_bytes, void* stream) {
-  OT_REQUIRE(table && accum && keys && grads, "ot_sparse_adagrad: null operand");
-  OT_REQUIRE(E > 0 && E % 4 == 0 && E <= 1024, "ot_sparse_adagrad: E=%d must be a multiple of 4 <= 1024", E);
-  OT_REQUIRE(num_rows > 0 && num_rows < 0xFFFFFFFFLL, "ot_sparse_adagrad: num_rows out of range");
-  OT_REQUIRE(n >= 0 && n < 2147483647LL, "ot_sparse_adagrad: n out of range");
-  if (n == 0) return OT_OK;
-  SparseWs w = carve(workspace, n, E);
-  OT_REQUIRE(ws_bytes >= w.total, "ot_sparse_adagrad: workspace too small (%zu < %zu)", ws_bytes, w.total);
-  hipStream_t s = (hipStream_t)stream;
+// steps 1-3 (+ the per-block squared-norm partials of the unique-row sums): fills w.k_out,
+// w.seg_start, w.nuniq, w.gsum, w.sq_part
+static int segment_rows(const SparseWs& w, int E, int64_t num_rows, const int64_t* keys, const float* grads,
+                        int64_t n, hipStream_t s) {
   const unsigned g1 = ceil_div(n, 256);
   hipLaunchKernelGGL(keys_prep_kernel, dim3(g1), dim3(256), 0, s, keys, n, num_rows, w.k_in, w.v_in);
   OT_LAUNCH_CHECK("ot_sparse_adagrad(prep)");
@@ -245,10 +289,68 @@ extern "C" int ot_sparse_adagrad(float* table, float* accum, int E, int64_t num_
   hipLaunchKernelGGL(seg_sum_kernel, dim3(g2), dim3(256), 0, s, w.psum, E, w.k_out, w.seg_start, w.pstart, w.nuniq,
                      tps, w.gsum, w.sq_part);
   OT_LAUNCH_CHECK("ot_sparse_adagrad(segsum)");
+  return OT_OK;
+}
+
+extern "C" int ot_sparse_adagrad(float* table, float* accum, int E, int64_t num_rows, const int64_t* keys,
+                                 const float* grads, int64_t n, float lr, float eps, float clip, void* workspace,
+                                 size_t ws_bytes, void* stream) {
+  OT_REQUIRE(table && accum && keys && grads, "ot_sparse_adagrad: null operand");
+  OT_REQUIRE(E > 0 && E % 4 == 0 && E <= 1024, "ot_sparse_adagrad: E=%d must be a multiple of 4 <= 1024", E);
+  OT_REQUIRE(num_rows > 0 && num_rows < 0xFFFFFFFFLL, "ot_sparse_adagrad: num_rows out of range");
+  OT_REQUIRE(n >= 0 && n < 2147483647LL, "ot_sparse_adagrad: n out of range");
+  if (n == 0) return OT_OK;
+  SparseWs w = carve(workspace, n, E);
+  OT_REQUIRE(ws_bytes >= w.total, "ot_sparse_adagrad: workspace too small (%zu < %zu)", ws_bytes, w.total);
+  hipStream_t s = (hipStream_t)stream;
+  const int rc = segment_rows(w, E, num_rows, keys, grads, n, s);
+  if (rc != OT_OK) return rc;
+  const int tps = tps_for(E);
+  const unsigned g2 = ceil_div(n, 256 / tps);
   hipLaunchKernelGGL(clip_scale_kernel, dim3(1), dim3(256), 0, s, w.sq_part, (int)g2, clip, w.scale);
   OT_LAUNCH_CHECK("ot_sparse_adagrad(clip)");
   hipLaunchKernelGGL(adagrad_apply_kernel, dim3(g2), dim3(256), 0, s, table, accum, E, w.k_out, w.seg_start, w.nuniq,
                      w.gsum, w.scale, tps, lr, eps);
   OT_LAUNCH_CHECK("ot_sparse_adagrad(apply)");
+  return OT_OK;
+}
+
+extern "C" int ot_sparse_grad_dense(int E, int64_t num_rows, const int64_t* keys, const float* grads, int64_t n,
+                                    float* dense, void* workspace, size_t ws_bytes, void* stream) {
+  OT_REQUIRE(keys && grads && dense, "ot_sparse_grad_dense: null operand");
+  OT_REQUIRE(E > 0 && E % 4 == 0 && E <= 1024, "ot_sparse_grad_dense: E=%d must be a multiple of 4 <= 1024", E);
+  OT_REQUIRE(num_rows > 0 && num_rows < 0xFFFFFFFFLL, "ot_sparse_grad_dense: num_rows out of range");
+  OT_REQUIRE(n >= 0 && n < 2147483647LL, "ot_sparse_grad_dense: n out of range");
+  if (n == 0) return OT_OK;
+  SparseWs w = carve(workspace, n, E);
+  OT_REQUIRE(ws_bytes >= w.total, "ot_sparse_grad_dense: workspace too small (%zu < %zu)", ws_bytes, w.total);
+  hipStream_t s = (hipStream_t)stream;
+  const int rc = segment_rows(w, E, num_rows, keys, grads, n, s);
+  if (rc != OT_OK) return rc;
+  const int tps = tps_for(E);
+  hipLaunchKernelGGL(scatter_rows_kernel, dim3(ceil_div(n, 256 / tps)), dim3(256), 0, s, dense, E, w.k_out,
+                     w.seg_start, w.nuniq, w.gsum, tps);
+  OT_LAUNCH_CHECK("ot_sparse_grad_dense(scatter)");
+  return OT_OK;
+}
+
+extern "C" size_t ot_dense_adagrad_workspace_size(void) { return (DENSE_GRID + 64) * sizeof(float); }
+
+extern "C" int ot_dense_adagrad(float* table, float* accum, const float* grad, int64_t num_rows, int E, float lr,
+                                float eps, float clip, void* workspace, size_t ws_bytes, void* stream) {
+  OT_REQUIRE(table && accum && grad && workspace, "ot_dense_adagrad: null operand");
+  OT_REQUIRE(E > 0 && E % 4 == 0, "ot_dense_adagrad: E must be a multiple of 4");
+  OT_REQUIRE(ws_bytes >= ot_dense_adagrad_workspace_size(), "ot_dense_adagrad: workspace too small");
+  if (num_rows <= 0) return OT_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t n4 = num_rows * E / 4;
+  float* part = (float*)workspace;
+  float* scale = part + DENSE_GRID;
+  hipLaunchKernelGGL(dense_sumsq_kernel, dim3(DENSE_GRID), dim3(256), 0, s, grad, n4, part);
+  OT_LAUNCH_CHECK("ot_dense_adagrad(norm)");
+  hipLaunchKernelGGL(clip_scale_kernel, dim3(1), dim3(256), 0, s, part, DENSE_GRID, clip, scale);
+  OT_LAUNCH_CHECK("ot_dense_adagrad(clip)");
+  hipLaunchKernelGGL(dense_adagrad_kernel, dim3(DENSE_GRID), dim3(256), 0, s, table, accum, grad, n4, scale, lr, eps);
+  OT_LAUNCH_CHECK("ot_dense_adagrad(apply)");
   return OT_OK;
 }

@@ -261,6 +261,24 @@ def sparse_adagrad(table, accum, E, num_rows, keys, grads, n, lr, eps, clip, dev
         _probe.end('embedding', 0.0, ev)
 
 
+def sparse_grad_dense(E, num_rows, keys, grads, n, dense, device=None) -> None:
+    """dense[key] = sum of the gradient rows of key (dense must be zero on entry)."""
+    ws = workspace(size('ot_sparse_adagrad_workspace_size', n, E), device)
+    ev = _probe.begin() if _probe is not None else None
+    call('ot_sparse_grad_dense', E, num_rows, ptr(keys), ptr(grads), n, ptr(dense), ptr(ws), ws.numel(), stream())
+    if ev is not None:
+        _probe.end('embedding', 0.0, ev)
+
+
+def dense_adagrad(table, accum, grad, num_rows, E, lr, eps, clip, device=None) -> None:
+    ws = workspace(size('ot_dense_adagrad_workspace_size'), device)
+    ev = _probe.begin() if _probe is not None else None
+    call('ot_dense_adagrad', ptr(table), ptr(accum), ptr(grad), num_rows, E, float(lr), float(eps), float(clip),
+         ptr(ws), ws.numel(), stream())
+    if ev is not None:
+        _probe.end('embedding', 0.0, ev)
+
+
 def clip_rmsprop(w, g, v, m, segs_dev, nseg, max_seg, lr, rho, eps, momentum, clip, device=None) -> None:
     ws = workspace(size('ot_clip_rmsprop_workspace_size', nseg, max_seg), device)
     ev = _probe.begin() if _probe is not None else None

@@ -13,6 +13,7 @@ computes in fp32 like the Keras default policy.
 from __future__ import annotations
 
 import json
+import os
 import time
 from pathlib import Path
 from typing import Dict, Optional
@@ -62,6 +63,9 @@ class OneTransOptimizer:
         self.segs = torch.from_numpy(model.layout.segments.reshape(-1)).to(dev)
         self.nseg = model.layout.segments.shape[0]
         self.acc = {k: torch.full_like(t, float(config.adagrad_initial_accumulator)) for k, t in model.tables.items()}
+        # data-parallel exchange of replicated tables: dense all-reduce up to this size, else all-gather
+        self.dense_exchange_bytes = int(float(os.environ.get('ONETRANS_DENSE_EXCHANGE_MB', '512')) * 2 ** 20)
+        self._dense_grad: Dict[str, torch.Tensor] = {}
 
     def step(self) -> None:
         m = self.model
@@ -70,10 +74,24 @@ class OneTransOptimizer:
                        self.lr, self.rho, self.eps, self.momentum, self.clip, device=m.flat.device)
         m.refresh_shadow()
         for (name, keys, grads) in m._pending_sparse:
-            keys, grads = otdist.allgather_sparse(keys, grads)
             table = m.tables[name]
-            K.sparse_adagrad(table, self.acc[name], table.shape[1], table.shape[0], keys, grads, keys.numel(),
-                             self.sparse_lr, self.sparse_eps, self.sparse_clip, device=table.device)
+            rows, E = table.shape
+            if otdist.world() > 1 and table.numel() * 4 <= self.dense_exchange_bytes:
+                # replicated table small enough to exchange densely: one all-reduce of the
+                # de-duplicated dense gradient instead of all-gathering every rank's rows
+                g = self._dense_grad.get(name)
+                if g is None:
+                    g = self._dense_grad[name] = torch.zeros_like(table)
+                else:
+                    g.zero_()
+                K.sparse_grad_dense(E, rows, keys, grads, keys.numel(), g, device=table.device)
+                otdist.allreduce_dense(g)
+                K.dense_adagrad(table, self.acc[name], g, rows, E, self.sparse_lr, self.sparse_eps,
+                                self.sparse_clip, device=table.device)
+            else:
+                keys, grads = otdist.allgather_sparse(keys, grads)
+                K.sparse_adagrad(table, self.acc[name], E, rows, keys, grads, keys.numel(),
+                                 self.sparse_lr, self.sparse_eps, self.sparse_clip, device=table.device)
         m._pending_sparse = []
 
 

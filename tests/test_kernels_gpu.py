@@ -299,6 +299,27 @@ def test_sparse_adagrad(dev):
     np.testing.assert_allclose(a_d.cpu().numpy(), a_ref, rtol=1e-5, atol=1e-5)
 
 
+def test_dense_exchange_matches_sparse(dev):
+    """Data-parallel dense form of the table update (ot_sparse_grad_dense + ot_dense_adagrad) equals
+    the sparse update (ot_sparse_adagrad) on the same (key, row) gradient, including invalid keys."""
+    rng = np.random.default_rng(9)
+    rows, E, n = 3000, 64, 20000
+    table = torch.tensor(rng.uniform(-0.05, 0.05, (rows, E)), dtype=torch.float32, device=dev)
+    acc = torch.full((rows, E), 0.1, device=dev)
+    keys = torch.from_numpy((rng.zipf(1.3, n) - 1) % (rows + 50) - 10).to(dev)      # some invalid keys
+    grads = torch.tensor(rng.normal(size=(n, E)), dtype=torch.float32, device=dev)
+    t1, a1 = table.clone(), acc.clone()
+    K.sparse_adagrad(t1, a1, E, rows, keys, grads, n, 0.1, 1e-7, 40.0, device=dev)
+    dense = torch.zeros(rows, E, device=dev)
+    K.sparse_grad_dense(E, rows, keys, grads, n, dense, device=dev)
+    t2, a2 = table.clone(), acc.clone()
+    K.dense_adagrad(t2, a2, dense, rows, E, 0.1, 1e-7, 40.0, device=dev)
+    torch.testing.assert_close(t2, t1, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(a2, a1, rtol=1e-5, atol=1e-6)
+    untouched = dense.abs().sum(1) == 0
+    assert bool((t2[untouched] == table[untouched]).all()) and bool((a2[untouched] == acc[untouched]).all())
+
+
 def test_clip_rmsprop(dev):
     rng = np.random.default_rng(4)
     total = 5000

@@ -328,19 +328,22 @@ __global__ __launch_bounds__(64 * BWD_WAVES<HD>(), 2) void attn_bwd_kernel(AttnA
       for (int r = 0; r < 16; ++r) { dk[c][r] = 0.f; dv[c][r] = 0.f; }
     int qb0 = key0 - q_off; qb0 = qb0 < 0 ? 0 : qb0 / 32;      // first query block that sees key0
     float qf[HD / 2], of[HD / 2];
-    f32x4 l4[4], d4[4];
     auto load_qblock = [&](int q0) {
       BWD_LOAD<HD>(qf, Qt, p.ld, q0 + li, K, hh);
       BWD_LOAD<HD>(of, dO, p.d, q0 + li, K, hh);
+    };
+    load_qblock(32 * qb0);
+    // Per pair, in issue order (vmcnt stays counted, nothing waits early): this block's row stats and
+    // dQ seed loads; S / dP chains on the prefetched q block; the next q block's prefetch; softmax
+    // gradient; dV / dK chains; dQ chain; dQ store.
+    for (int qb = qb0; qb < nqb; ++qb) {
+      const int q0 = 32 * qb;
+      f32x4 l4[4], d4[4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         l4[g] = *reinterpret_cast<const f32x4*>(lsep + q0 + 8 * g + 4 * hh);
         d4[g] = *reinterpret_cast<const f32x4*>(dltp + q0 + 8 * g + 4 * hh);
       }
-    };
-    load_qblock(32 * qb0);
-    for (int qb = qb0; qb < nqb; ++qb) {
-      const int q0 = 32 * qb;
       // dQ^T block: lane = query q0 + li, register r = dim 32c + acc_row(r, hh) (4 float4 per lane)
       const int jq = q0 + li;
       float* dqrow = dQt + (int64_t)(jq < K ? jq : K - 1) * p.ld + 4 * hh;
@@ -359,38 +362,62 @@ __global__ __launch_bounds__(64 * BWD_WAVES<HD>(), 2) void attn_bwd_kernel(AttnA
       frag_to_lds<HD>(tQ, qf, li, hh);
       f32x16 s = mm_frag<HD>(qf, kf);                  // S: row = query, col = key
       f32x16 dp = mm_frag<HD>(of, vf);                 // dP: row = query, col = key
-      f32x4 lc[4], dc[4];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) { lc[g] = l4[g]; dc[g] = d4[g]; }
       if (qb + 1 < nqb) load_qblock(q0 + 32);          // prefetch the next query block
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int r = 4 * g + e, j = q0 + 8 * g + 4 * hh + e;
-          const float ex = __expf(s[r] * p.scale - lc[g][e]);
+          const float ex = __expf(s[r] * p.scale - l4[g][e]);
           const float P = kpos <= q_off + j ? ex : 0.f;
           s[r] = P;
-          dp[r] = P * (dp[r] - dc[g][e]) * p.scale;    // dS, pre-scaled by 1/sqrt(hd)
+          dp[r] = P * (dp[r] - d4[g][e]) * p.scale;    // dS, pre-scaled by 1/sqrt(hd)
           tS[(8 * g + 4 * hh + e) * SLD + li] = dp[r];
         }
       }
       __builtin_amdgcn_wave_barrier();
-      acc_tile_p<HD>(dv, tO, s, li, hh);               // dV^T += dO^T P
-      acc_tile_p<HD>(dk, tQ, dp, li, hh);              // dK^T += Q^T dS
-      // dQ^T[d][q] += sum_key K[key][d] dS[q][key]: A = K^T (row = dim, k = key, from tK),
-      // B = dS^T (k = key 16hh + s, col = query = lane, from tS)
+      if constexpr (HD <= 32) {
+        // dV^T += dO^T P and dK^T += Q^T dS: all 32 LDS operands read first, then the two chains
+        // interleaved (independent accumulators) — no LDS round trip between consecutive MFMAs
+        float ao[16], aq[16];
 #pragma unroll
-      for (int q4 = 0; q4 < 4; ++q4) {
-        const f32x4 a4 = *reinterpret_cast<const f32x4*>(tS + li * SLD + 16 * hh + 4 * q4);
+        for (int r = 0; r < 16; ++r) {
+          const int row = acc_row(r, hh);
+          ao[r] = li < HD ? tO[row * LD + li] : 0.f;
+          aq[r] = li < HD ? tQ[row * LD + li] : 0.f;
+        }
+        __builtin_amdgcn_sched_barrier(0);             // keep the reads above: the scheduler sinks them
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int key = 16 * hh + 4 * q4 + e;
+        for (int r = 0; r < 16; ++r) {
+          dv[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(ao[r], s[r], dv[0], 0, 0, 0);
+          dk[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(aq[r], dp[r], dk[0], 0, 0, 0);
+        }
+        float bk[16];
+        f32x4 a4[4];
 #pragma unroll
-          for (int c = 0; c < NB(HD); ++c) {
-            const int dd = 32 * c + li;
-            const float bk = dd < HD ? tK[key * LD + dd] : 0.f;
-            dq[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(bk, a4[e], dq[c], 0, 0, 0);
+        for (int q4 = 0; q4 < 4; ++q4) a4[q4] = *reinterpret_cast<const f32x4*>(tS + li * SLD + 16 * hh + 4 * q4);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) bk[e] = li < HD ? tK[(16 * hh + e) * LD + li] : 0.f;
+        __builtin_amdgcn_sched_barrier(0);
+        // dQ^T[d][q] += sum_key K[key][d] dS[q][key]: A = K^T (row = dim, k = key, from tK),
+        // B = dS^T (k = key 16hh + s, col = query = lane, from tS)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) dq[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(bk[e], a4[e >> 2][e & 3], dq[0], 0, 0, 0);
+      } else {
+        acc_tile_p<HD>(dv, tO, s, li, hh);             // dV^T += dO^T P
+        acc_tile_p<HD>(dk, tQ, dp, li, hh);            // dK^T += Q^T dS
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+          const f32x4 a4 = *reinterpret_cast<const f32x4*>(tS + li * SLD + 16 * hh + 4 * q4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int key = 16 * hh + 4 * q4 + e;
+#pragma unroll
+            for (int c = 0; c < NB(HD); ++c) {
+              const int dd = 32 * c + li;
+              const float bkv = dd < HD ? tK[key * LD + dd] : 0.f;
+              dq[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(bkv, a4[e], dq[c], 0, 0, 0);
+            }
           }
         }
       }

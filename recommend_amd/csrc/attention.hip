@@ -12,6 +12,8 @@
 // Orientation: S^T = K Q^T puts the query on the MFMA column (lane) and keys in registers, so
 // P^T (registers) is directly the B operand of O^T = V^T P^T (the accumulator-as-operand idiom,
 // cdna_hip_programming.md §3) with the k index of step r = the key held in register r.
+#include <mutex>
+
 #include "common.h"
 
 #ifndef OT_ATTN_FWD_BRANCHLOAD
@@ -24,6 +26,9 @@
 #define BWD_LOAD load_frag
 #else
 #define BWD_LOAD load_frag_clamped
+#endif
+#ifndef OT_ATTN_KV_LDS_MAX
+#define OT_ATTN_KV_LDS_MAX (80 * 1024)
 #endif
 #ifndef OT_ATTN_FWD_MASKALL
 #define OT_ATTN_FWD_MASKALL 0
@@ -220,6 +225,111 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs p) {
           }
         }
       // natural-log lse for the backward: m (log2 units) * ln 2 + ln l
+      if (hh == 0) p.lse[((int64_t)b * p.H + h) * K + j] = m * 0.6931471805599453f + __logf(l);
+    }
+  }
+}
+
+// Forward, one workgroup per (sample, head) for short sequences: the (b, h) slice's K and V rows
+// are staged in LDS once ([KP][HD+4], zero rows past I) and shared by the 4 waves, each of which
+// takes whole query blocks (snake order from the heaviest causal block: balanced).  Every K/V byte
+// is read from HBM once (the one-wave-per-head kernel re-reads them for every query block).
+template <int HD>
+__global__ __launch_bounds__(256) void attn_fwd_kv_kernel(AttnArgs p) {
+  extern __shared__ __attribute__((aligned(16))) float kv[];   // Ks [KP][LD] then Vs [KP][LD]
+  constexpr int LD = TLD<HD>();
+  const int lane = threadIdx.x & 63, li = lane & 31, hh = lane >> 5, wave = threadIdx.x >> 6;
+  const int pair = blockIdx.x;
+  const int b = pair / p.H, h = pair % p.H;
+  const int I = p.I, K = p.K, q_off = I - K;
+  const int KP = (I + 31) / 32 * 32;
+  float* Ks = kv;
+  float* Vs = kv + KP * LD;
+  const float* Q = p.qkv + (int64_t)b * I * p.ld + h * HD;
+  // stage K and V: thread t copies float4 chunks (row, c4) of both, rows >= I zero
+  constexpr int C4 = HD / 4;
+  for (int i = threadIdx.x; i < KP * C4; i += 256) {
+    const int row = i / C4, c = 4 * (i % C4);
+    f32x4 kvv = {0.f, 0.f, 0.f, 0.f}, vvv = {0.f, 0.f, 0.f, 0.f};
+    if (row < I) {
+      const float* src = Q + (int64_t)row * p.ld + c;
+      kvv = *reinterpret_cast<const f32x4*>(src + p.d);
+      vvv = *reinterpret_cast<const f32x4*>(src + 2 * p.d);
+    }
+    *reinterpret_cast<f32x4*>(Ks + row * LD + c) = kvv;
+    *reinterpret_cast<f32x4*>(Vs + row * LD + c) = vvv;
+  }
+  __syncthreads();
+  const float* Qt = Q + (int64_t)q_off * p.ld;
+  const int nqb = (K + 31) / 32;
+  const float qscale = p.scale * 1.4426950408889634f;   // log2(e) / sqrt(hd)
+  for (int i = 0; i < nqb; ++i) {
+    const int slot = (i >> 2) & 1 ? 3 - (i & 3) : (i & 3);   // snake assignment
+    if (slot != wave) continue;
+    const int qb = nqb - 1 - i;
+    const int j = 32 * qb + li;
+    const int qpos = q_off + (j < K ? j : K - 1);
+    float qf[HD / 2];
+    load_frag<HD>(qf, Qt, p.ld, j, K, hh);
+#pragma unroll
+    for (int s2 = 0; s2 < HD / 2; ++s2) qf[s2] *= qscale;
+    f32x16 oacc[NB(HD)];
+#pragma unroll
+    for (int c = 0; c < NB(HD); ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) oacc[c][r] = 0.f;
+    float m = -INFINITY, l = 0.f;
+    const int last_q = q_off + min(32 * qb + 31, K - 1);
+    const int nkb = last_q / 32 + 1;
+    const int first_masked = (q_off + 32 * qb) / 32;
+    for (int kb = 0; kb < nkb; ++kb) {
+      const int key0 = 32 * kb;
+      float kf[HD / 2];
+#pragma unroll
+      for (int q4 = 0; q4 < HD / 8; ++q4) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(Ks + (key0 + li) * LD + (HD / 2) * hh + 4 * q4);
+        kf[4 * q4] = v.x; kf[4 * q4 + 1] = v.y; kf[4 * q4 + 2] = v.z; kf[4 * q4 + 3] = v.w;
+      }
+      f32x16 s = mm_frag<HD>(kf, qf);               // S^T (log2 units): row = key, col = query
+      if (kb >= first_masked) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          s[r] = (key0 + acc_row(r, hh) <= qpos) ? s[r] : -INFINITY;
+      }
+      float mloc = s[0];
+#pragma unroll
+      for (int r = 1; r < 16; ++r) mloc = fmaxf(mloc, s[r]);
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+      const float mnew = fmaxf(m, mloc);
+      const float corr = __builtin_amdgcn_exp2f(m - mnew);
+      float lsum = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float e = __builtin_amdgcn_exp2f(s[r] - mnew);
+        s[r] = e;
+        lsum += e;
+      }
+      lsum += __shfl_xor(lsum, 32, 64);
+      l = l * corr + lsum;
+      m = mnew;
+#pragma unroll
+      for (int c = 0; c < NB(HD); ++c) oacc[c] *= corr;
+      acc_tile_p<HD>(oacc, Vs + key0 * LD, s, li, hh);     // O^T += V^T P^T
+    }
+    if (j < K) {
+      const float inv = 1.f / l;
+      float* orow = p.out + ((int64_t)b * K + j) * p.d + h * HD;
+#pragma unroll
+      for (int c = 0; c < NB(HD); ++c)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int dd = 32 * c + 8 * g + 4 * hh;
+          if (dd < HD) {
+            f32x4 v = {oacc[c][4 * g] * inv, oacc[c][4 * g + 1] * inv, oacc[c][4 * g + 2] * inv,
+                       oacc[c][4 * g + 3] * inv};
+            *reinterpret_cast<f32x4*>(orow + dd) = v;
+          }
+        }
       if (hh == 0) p.lse[((int64_t)b * p.H + h) * K + j] = m * 0.6931471805599453f + __logf(l);
     }
   }
@@ -549,8 +659,25 @@ extern "C" int ot_attn_fwd(const float* qkv, int64_t ld, int B, int H, int I, in
   if (B == 0) return OT_OK;
   AttnArgs p{qkv, ld, H * head_dim, nullptr, nullptr, out, lse, nullptr, nullptr, B, H, I, K,
              1.f / sqrtf((float)head_dim)};
-  const unsigned grid = ceil_div((int64_t)B * H, 4);
-  OT_ATTN_DISPATCH(attn_fwd_kernel, head_dim, dim3(grid), dim3(256), 0, (hipStream_t)stream, p);
+  const size_t kv_bytes = 2 * (size_t)((I + 31) / 32 * 32) * (head_dim + 4) * sizeof(float);
+  if (head_dim <= 64 && kv_bytes <= OT_ATTN_KV_LDS_MAX && (K + 31) / 32 >= 3) {
+    // short sequence: K/V of a head staged once in LDS, shared by 4 waves
+    static std::once_flag once;
+    std::call_once(once, [] {
+      for (const void* k : {(const void*)attn_fwd_kv_kernel<16>, (const void*)attn_fwd_kv_kernel<32>,
+                            (const void*)attn_fwd_kv_kernel<64>})
+        (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, OT_ATTN_KV_LDS_MAX);
+      (void)hipGetLastError();
+    });
+    switch (head_dim) {
+      case 16: hipLaunchKernelGGL(attn_fwd_kv_kernel<16>, dim3(B * H), dim3(256), kv_bytes, (hipStream_t)stream, p); break;
+      case 32: hipLaunchKernelGGL(attn_fwd_kv_kernel<32>, dim3(B * H), dim3(256), kv_bytes, (hipStream_t)stream, p); break;
+      default: hipLaunchKernelGGL(attn_fwd_kv_kernel<64>, dim3(B * H), dim3(256), kv_bytes, (hipStream_t)stream, p); break;
+    }
+  } else {
+    const unsigned grid = ceil_div((int64_t)B * H, 4);
+    OT_ATTN_DISPATCH(attn_fwd_kernel, head_dim, dim3(grid), dim3(256), 0, (hipStream_t)stream, p);
+  }
   OT_LAUNCH_CHECK("ot_attn_fwd");
   return OT_OK;
 }

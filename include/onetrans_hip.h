@@ -213,6 +213,31 @@ int ot_sparse_grad_dense(int E, int64_t num_rows, const int64_t* keys, const flo
 size_t ot_dense_adagrad_workspace_size(void);
 int ot_dense_adagrad(float* table, float* accum, const float* grad, int64_t num_rows, int E, float lr,
                      float eps, float clip, void* workspace, size_t ws_bytes, void* stream);
+/* Two-phase sparse update for row-sharded tables (the clip norm spans all owners): prepare
+ * de-duplicates and writes this rank's squared norm to sumsq_out (device float); the caller
+ * all-reduces it; finish applies clip_by_norm(clip) with the global norm + Keras Adagrad.  Same
+ * workspace (ot_sparse_adagrad_workspace_size) for both calls. */
+int ot_sparse_prepare(int E, int64_t num_rows, const int64_t* keys, const float* grads, int64_t n, float* sumsq_out,
+                      void* workspace, size_t ws_bytes, void* stream);
+int ot_sparse_finish(float* table, float* accum, int E, int64_t n, float lr, float eps, float clip,
+                     const float* sumsq_total, void* workspace, size_t ws_bytes, void* stream);
+
+/* ---- row-sharded embedding tables (shard.hip) ------------------------------
+ * Row id lives on rank id % world at local row id / world.  ot_shard_route buckets n ids by owner
+ * (stable): perm[j] = position of the j-th routed id, send_local[j] = its local row at the owner
+ * (-1 for ids outside [0, num_rows)), counts[r] = ids routed to rank r.  The all-to-all exchanges
+ * are the caller's (RCCL); ot_gather_rows / ot_permute_rows move the rows on each side. */
+size_t ot_shard_route_workspace_size(int64_t n);
+int ot_shard_route(const int64_t* ids, int64_t n, int64_t num_rows, int world, int32_t* perm, int64_t* send_local,
+                   int32_t* counts, void* workspace, size_t ws_bytes, void* stream);
+/* out[i] = table[idx[i]] (zeros for idx < 0) */
+int ot_gather_rows(const float* table, int E, const int64_t* idx, int64_t n, float* out, void* stream);
+/* inverse = 0: dst[j] = src[perm[j]]; inverse = 1: dst[perm[j]] = src[j] */
+int ot_permute_rows(const float* src, const int32_t* perm, int64_t n, int E, int inverse, float* dst, void* stream);
+/* shard init U(lo, hi) from a counter-based hash of (global row, column): the same logical table
+ * for every world size */
+int ot_hash_uniform_rows(float* out, int64_t local_rows, int E, int rank, int world, uint32_t seed, float lo,
+                         float hi, void* stream);
 
 /* ---- dense optimizer (optim.hip) ----------------------------------------------------------
  * Per-variable tf.clip_by_norm (train.py:134-135) over 2-D strided segments of one flat

@@ -75,6 +75,13 @@ SIGNATURES = {
     'ot_sparse_grad_dense': (c_int, [c_int, I64, P, P, I64, P, P, c_size_t, P]),
     'ot_dense_adagrad_workspace_size': (c_size_t, []),
     'ot_dense_adagrad': (c_int, [P, P, P, I64, c_int, c_float, c_float, c_float, P, c_size_t, P]),
+    'ot_sparse_prepare': (c_int, [c_int, I64, P, P, I64, P, P, c_size_t, P]),
+    'ot_sparse_finish': (c_int, [P, P, c_int, I64, c_float, c_float, c_float, P, P, c_size_t, P]),
+    'ot_shard_route_workspace_size': (c_size_t, [I64]),
+    'ot_shard_route': (c_int, [P, I64, I64, c_int, P, P, P, P, c_size_t, P]),
+    'ot_gather_rows': (c_int, [P, c_int, P, I64, P, P]),
+    'ot_permute_rows': (c_int, [P, P, I64, c_int, c_int, P, P]),
+    'ot_hash_uniform_rows': (c_int, [P, I64, c_int, c_int, c_int, c_uint32, c_float, c_float, P]),
     'ot_clip_rmsprop_workspace_size': (c_size_t, [c_int, I64]),
     'ot_clip_rmsprop': (c_int, [P, P, P, P, P, c_int, I64, c_float, c_float, c_float, c_float, c_float, P,
                                 c_size_t, P]),

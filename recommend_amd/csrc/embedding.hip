@@ -200,6 +200,25 @@ __global__ __launch_bounds__(256) void dense_adagrad_kernel(float* table, float*
 }
 constexpr int DENSE_GRID = 2048;
 
+// fixed-order sum of the per-block squared-norm partials (one block)
+__global__ __launch_bounds__(256) void sum_parts_kernel(const float* __restrict__ part, int n, float* out) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s += part[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// clip scale from an externally reduced squared norm (row-sharded tables: sum over owners)
+__global__ void clip_from_sumsq_kernel(const float* __restrict__ sumsq, float clip, float* scale) {
+  if (threadIdx.x == 0) {
+    const float l2 = sqrtf(sumsq[0]);
+    scale[0] = clip > 0.f ? clip / fmaxf(l2, clip) : 1.f;
+  }
+}
+
 struct SparseWs {
   uint32_t *k_in, *k_out;
   int32_t *v_in, *v_out, *flags, *pos, *seg_start, *nuniq, *pcount, *pstart;
@@ -352,5 +371,47 @@ extern "C" int ot_dense_adagrad(float* table, float* accum, const float* grad, i
   OT_LAUNCH_CHECK("ot_dense_adagrad(clip)");
   hipLaunchKernelGGL(dense_adagrad_kernel, dim3(DENSE_GRID), dim3(256), 0, s, table, accum, grad, n4, scale, lr, eps);
   OT_LAUNCH_CHECK("ot_dense_adagrad(apply)");
+  return OT_OK;
+}
+
+// Two-phase form for row-sharded tables, whose clip_by_norm spans every owner's rows: prepare
+// de-duplicates this rank's received (key, row) pairs and writes the local squared norm; the caller
+// all-reduces it; finish applies clip + Adagrad with the global norm.  The workspace (size
+// ot_sparse_adagrad_workspace_size(n, E)) carries the segmentation from prepare to finish.
+extern "C" int ot_sparse_prepare(int E, int64_t num_rows, const int64_t* keys, const float* grads, int64_t n,
+                                 float* sumsq_out, void* workspace, size_t ws_bytes, void* stream) {
+  OT_REQUIRE(keys && grads && sumsq_out && workspace, "ot_sparse_prepare: null operand");
+  OT_REQUIRE(E > 0 && E % 4 == 0 && E <= 1024, "ot_sparse_prepare: E=%d must be a multiple of 4 <= 1024", E);
+  OT_REQUIRE(num_rows > 0 && num_rows < 0xFFFFFFFFLL, "ot_sparse_prepare: num_rows out of range");
+  OT_REQUIRE(n >= 0 && n < 2147483647LL, "ot_sparse_prepare: n out of range");
+  hipStream_t s = (hipStream_t)stream;
+  if (n == 0) {
+    (void)hipMemsetAsync(sumsq_out, 0, sizeof(float), s);
+    return OT_OK;
+  }
+  SparseWs w = carve(workspace, n, E);
+  OT_REQUIRE(ws_bytes >= w.total, "ot_sparse_prepare: workspace too small (%zu < %zu)", ws_bytes, w.total);
+  const int rc = segment_rows(w, E, num_rows, keys, grads, n, s);
+  if (rc != OT_OK) return rc;
+  const unsigned g2 = ceil_div(n, 256 / tps_for(E));
+  hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(256), 0, s, w.sq_part, (int)g2, sumsq_out);
+  OT_LAUNCH_CHECK("ot_sparse_prepare(sumsq)");
+  return OT_OK;
+}
+
+extern "C" int ot_sparse_finish(float* table, float* accum, int E, int64_t n, float lr, float eps, float clip,
+                                const float* sumsq_total, void* workspace, size_t ws_bytes, void* stream) {
+  OT_REQUIRE(table && accum && sumsq_total && workspace, "ot_sparse_finish: null operand");
+  if (n <= 0) return OT_OK;
+  SparseWs w = carve(workspace, n, E);
+  OT_REQUIRE(ws_bytes >= w.total, "ot_sparse_finish: workspace too small (%zu < %zu)", ws_bytes, w.total);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(clip_from_sumsq_kernel, dim3(1), dim3(64), 0, s, sumsq_total, clip, w.scale);
+  OT_LAUNCH_CHECK("ot_sparse_finish(clip)");
+  const int tps = tps_for(E);
+  const unsigned g2 = ceil_div(n, 256 / tps);
+  hipLaunchKernelGGL(adagrad_apply_kernel, dim3(g2), dim3(256), 0, s, table, accum, E, w.k_out, w.seg_start, w.nuniq,
+                     w.gsum, w.scale, tps, lr, eps);
+  OT_LAUNCH_CHECK("ot_sparse_finish(apply)");
   return OT_OK;
 }

@@ -279,6 +279,38 @@ def dense_adagrad(table, accum, grad, num_rows, E, lr, eps, clip, device=None) -
         _probe.end('embedding', 0.0, ev)
 
 
+def sparse_prepare(E, num_rows, keys, grads, n, sumsq_out, ws) -> None:
+    call('ot_sparse_prepare', E, num_rows, ptr(keys), ptr(grads), n, ptr(sumsq_out), ptr(ws), ws.numel(), stream())
+
+
+def sparse_finish(table, accum, E, n, lr, eps, clip, sumsq_total, ws) -> None:
+    call('ot_sparse_finish', ptr(table), ptr(accum), E, n, float(lr), float(eps), float(clip), ptr(sumsq_total),
+         ptr(ws), ws.numel(), stream())
+
+
+def sparse_workspace(n, E, device):
+    return workspace(size('ot_sparse_adagrad_workspace_size', n, E), device)
+
+
+def shard_route(ids, n, num_rows, world, perm, send_local, counts) -> None:
+    ws = workspace(size('ot_shard_route_workspace_size', n), ids.device)
+    call('ot_shard_route', ptr(ids), n, num_rows, world, ptr(perm), ptr(send_local), ptr(counts), ptr(ws), ws.numel(),
+         stream())
+
+
+def gather_rows(table, E, idx, n, out) -> None:
+    call('ot_gather_rows', ptr(table), E, ptr(idx), n, ptr(out), stream())
+
+
+def permute_rows(src, perm, n, E, inverse, dst) -> None:
+    call('ot_permute_rows', ptr(src), ptr(perm), n, E, int(inverse), ptr(dst), stream())
+
+
+def hash_uniform_rows(out, local_rows, E, rank, world, seed, lo, hi) -> None:
+    call('ot_hash_uniform_rows', ptr(out), local_rows, E, rank, world, seed & 0xFFFFFFFF, float(lo), float(hi),
+         stream())
+
+
 def clip_rmsprop(w, g, v, m, segs_dev, nseg, max_seg, lr, rho, eps, momentum, clip, device=None) -> None:
     ws = workspace(size('ot_clip_rmsprop_workspace_size', nseg, max_seg), device)
     ev = _probe.begin() if _probe is not None else None

@@ -111,7 +111,9 @@ class _Tokenize(torch.autograd.Function):
                 demb = torch.empty(M, E, device=dev)
                 K.gemm(OT_GEMM_NT, dx0, d, d, sm['rows'][0], m.p('tok.seq.kernel'), E * d, d, E, sm['tile_group'],
                        plan['seq_map'].ntiles, demb, E, sm['rows'][1], m_rows=plan['seq_M'])
-                m._pending_sparse.append(('emb.seq_item', plan['seq_ids'], demb))
+                # a sharded table takes its gradient rows along the lookup's all-to-all route
+                keys = plan['seq_route'] if 'emb.seq_item' in m.sharded else plan['seq_ids']
+                m._pending_sparse.append(('emb.seq_item', keys, demb))
         elif not acc:
             m.g('tok.seq.kernel').zero_(); m.g('tok.seq.bias').zero_()
         if plan['n_sep'] > 0:
@@ -411,7 +413,19 @@ class OneTransModel(nn.Module):
         self._aux_maps: Dict = {}
         self._step = 0
         self.dropout_seed = 0x5EED0000 ^ seed
+        # row-sharded tables (data-parallel runs): 'emb.seq_item' lives partitioned over the ranks
+        self.sharded: Dict[str, 'ShardedTable'] = {}
+        shard_seq = self._shard_seq_table()
         params = init if init is not None else init_params(cfg, self.f_ns, seed=seed, with_tables=False)
+        if shard_seq:
+            from .sharded import ShardedTable
+            import torch.distributed as dist
+            full = params.get('emb.seq_item') if init is not None else None
+            params = {k: v for k, v in params.items() if k != 'emb.seq_item'}
+            st = ShardedTable('emb.seq_item', cfg.seq_item_vocab, cfg.seq_feature_dim, dist.get_world_size(),
+                              dist.get_rank(), self.device, seed=seed + 2, full_init=full)
+            self.sharded['emb.seq_item'] = st
+            self.tables['emb.seq_item'] = st.table
         self.load_param_dict(params)
         if init is None or not any(k.startswith('emb.') for k in init):
             self._init_tables_device(seed + 1)
@@ -455,8 +469,24 @@ class OneTransModel(nn.Module):
                 v = v[:self.f_ns]
             out[name] = v
         for k, t in self.tables.items():
-            out[k] = t.detach().cpu().numpy().copy()
+            src = self.sharded[k].full_table() if k in self.sharded else t
+            out[k] = src.detach().cpu().numpy().copy()
         return out
+
+    def _shard_seq_table(self) -> bool:
+        """Row-shard the sequence-item table?  ``config.table_sharding`` (env ONETRANS_TABLE_SHARDING
+        overrides): 'row' under torch.distributed with world > 1; 'auto' (default) when the table
+        exceeds 1 GiB (C4's 100M rows; C2's 1M-row table is replicated and exchanged densely)."""
+        import torch.distributed as dist
+        cfg = self.config
+        mode = os.environ.get('ONETRANS_TABLE_SHARDING', getattr(cfg, 'table_sharding', 'auto'))
+        if not cfg.seq_item_vocab or mode == 'none':
+            return False
+        if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+            return False
+        if mode == 'row':
+            return True
+        return cfg.seq_item_vocab * cfg.seq_feature_dim * 4 > 2 ** 30
 
     def _init_tables_device(self, seed: int) -> None:
         cfg = self.config
@@ -467,7 +497,7 @@ class OneTransModel(nn.Module):
             t = torch.empty(total, cfg.ns_embedding_dim, device=self.device)
             t.uniform_(-0.05, 0.05, generator=gen)
             self.tables['emb.ns'] = t
-        if cfg.seq_item_vocab:
+        if cfg.seq_item_vocab and 'emb.seq_item' not in self.sharded:
             t = torch.empty(cfg.seq_item_vocab, cfg.seq_feature_dim, device=self.device)
             t.uniform_(-0.05, 0.05, generator=gen)
             self.tables['emb.seq_item'] = t
@@ -531,7 +561,14 @@ class OneTransModel(nn.Module):
                 plan['ids_buf'].copy_(torch.cat([ns[n].reshape(B, 1).to(dev, torch.int64)
                                                  for n in plan['sparse_names']], 1))
         if plan['seq_map'] is not None:
-            if id_seq:
+            if id_seq and 'emb.seq_item' in self.sharded:
+                # row-sharded table: the rows arrive through the all-to-all lookup in token order, and
+                # the projection reads them through the static (identity) row map
+                ids = [seq[n].to(dev, torch.int64).contiguous() for (_, n, _) in present]
+                plan['seq_ids'] = torch.cat([t.reshape(-1) for t in ids])
+                plan['seq_A'] = self.sharded['emb.seq_item'].lookup(plan['seq_ids'])
+                plan['seq_route'] = self.sharded['emb.seq_item'].last_route
+            elif id_seq:
                 ids = [seq[n].to(dev, torch.int64).contiguous() for (_, n, _) in present]
                 for (i, n, L), t, off in zip(present, ids, plan['seq_seg_off']):
                     K.seq_rows(t, L, B, L, cfg.seq_item_vocab, (plan['seq_in'], off))

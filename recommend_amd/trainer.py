@@ -76,7 +76,11 @@ class OneTransOptimizer:
         for (name, keys, grads) in m._pending_sparse:
             table = m.tables[name]
             rows, E = table.shape
-            if otdist.world() > 1 and table.numel() * 4 <= self.dense_exchange_bytes:
+            if name in m.sharded:
+                # row-sharded: gradient rows go to their owners (all-to-all), global-norm clip, Adagrad
+                m.sharded[name].apply_gradient(keys, grads, self.acc[name], self.sparse_lr, self.sparse_eps,
+                                               self.sparse_clip)
+            elif otdist.world() > 1 and table.numel() * 4 <= self.dense_exchange_bytes:
                 # replicated table small enough to exchange densely: one all-reduce of the
                 # de-duplicated dense gradient instead of all-gathering every rank's rows
                 g = self._dense_grad.get(name)

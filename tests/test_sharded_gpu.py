@@ -1,0 +1,134 @@
+"""Row-sharded embedding table (recommend_amd/sharded.py) on the data-parallel path, world_size 2.
+
+Both ranks share the one GPU of the box and talk over gloo (RCCL refuses two ranks on one device;
+the exchange code is the same, gloo stages the all-to-alls through host memory).  Checks:
+* lookup through route -> all-to-all -> gather -> all-to-all -> unpermute == full_table[ids]
+  (zeros for out-of-range ids), and apply_gradient == the oracle's de-duplicated, globally clipped
+  Keras Adagrad (oracle/onetrans_ref.py train_step, sparse part) on the full table;
+* three training steps of OneTransModel with 'emb.seq_item' row-sharded over 2 ranks (each rank on
+  half the batch) == the oracle's full-batch train_step, every parameter and the logical table."""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _lookup_update(rank, world, dev):
+    from recommend_amd.sharded import ShardedTable
+    num_rows, E = 301, 32
+    rng = np.random.default_rng(7)
+    full = rng.uniform(-0.05, 0.05, (num_rows, E)).astype(np.float32)
+    st = ShardedTable('t', num_rows, E, world, rank, dev, full_init=full)
+    # ids of each rank: Zipf-ish with repeats, plus out-of-range ids
+    ids_all = [np.concatenate([rng.integers(0, num_rows, 200), rng.integers(0, 5, 50), [-1, num_rows, 3]])
+               for _ in range(world)]
+    grads_all = [rng.standard_normal((len(i), E)).astype(np.float32) * 0.1 for i in ids_all]
+    ids = torch.from_numpy(ids_all[rank]).to(dev)
+    got = st.lookup(ids).cpu().numpy()
+    exp = np.where(((ids_all[rank] >= 0) & (ids_all[rank] < num_rows))[:, None],
+                   full[np.clip(ids_all[rank], 0, num_rows - 1)], 0.0)
+    err_lookup = float(np.abs(got - exp).max())
+    acc = torch.full((st.table.shape[0], E), 0.1, device=dev)
+    lr, eps, clip = 0.05, 1e-7, 0.5
+    st.apply_gradient(st.last_route, torch.from_numpy(grads_all[rank]).to(dev), acc, lr, eps, clip)
+    new = st.full_table().cpu().numpy()
+    # expected: dense gradient of mean-over-ranks, invalid ids dropped, clip by global norm, Adagrad
+    g = np.zeros((num_rows, E), np.float64)
+    for i, gr in zip(ids_all, grads_all):
+        ok = (i >= 0) & (i < num_rows)
+        np.add.at(g, i[ok], gr[ok].astype(np.float64) / world)
+    l2 = np.sqrt((g * g).sum())
+    g = g * clip / max(l2, clip)
+    a = 0.1 + g * g
+    ref = full - lr * g / np.sqrt(a + eps)
+    return err_lookup, float(np.abs(new - ref).max())
+
+
+def _worker(rank, world, port, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    os.environ['ONETRANS_TABLE_SHARDING'] = 'row'
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        dev = torch.device('cuda:0')
+        res = {}
+        res['lookup'], res['adagrad'] = _lookup_update(rank, world, dev)
+
+        from recommend_amd.data import make_batch
+        from recommend_amd.model import OneTransModel
+        from recommend_amd.params import init_params, keras_variables
+        from recommend_amd.trainer import OneTransTrainer
+        from oracle import onetrans_ref as R
+        from test_model_gpu import small_criteo
+        cfg = small_criteo('head', d=64, H=4, f=128, Lns=4, seq_lens=(5, 9, 7))
+        cfg.dropout_rate = 0.0
+        cfg.optimizer_config = dict(cfg.optimizer_config, dense_lr=0.001, momentum=0.9)
+        P = init_params(cfg, cfg.ns_input_width(), seed=0, perturb=True)
+        model = OneTransModel(cfg, device=dev, init=P)
+        assert 'emb.seq_item' in model.sharded
+        assert model.sharded['emb.seq_item'].local_rows == (cfg.seq_item_vocab - rank + 1) // 2
+        tr = OneTransTrainer(cfg, model=model)
+        B = 40
+        Pt = R.to_torch(P)
+        st = R.init_state(Pt, cfg)
+        kv = keras_variables(cfg, {k: v.shape for k, v in P.items() if not k.startswith('emb.')})
+        losses = []
+        for step in range(3):
+            ns, seq, lab = make_batch(B, cfg, seed=3000 + step)
+            sl = slice(rank * B // world, (rank + 1) * B // world)
+            part = lambda d: {k: v[sl] for k, v in d.items()}
+            out = tr.train_step((part(ns), part(seq), part(lab)))
+            loss = out['total_loss'].detach().reshape(1).cpu()
+            dist.all_reduce(loss)
+            losses.append(float(loss) / world)
+            Pt, st, rl, _ = R.train_step(Pt, st, cfg, kv, R.to_torch(ns), R.to_torch(seq), R.to_torch(lab), seed=0)
+            res[f'loss{step}'] = abs(losses[-1] - float(rl))
+        got = model.param_dict()
+        res['params'] = {k: float(np.abs(got[k] - v.detach().numpy()).max()) for k, v in Pt.items()}
+        if rank == 0:
+            q.put(res)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_row_sharded_table_two_ranks():
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    env_pp = os.environ.get('PYTHONPATH', '')
+    here = os.path.dirname(os.path.abspath(__file__))
+    os.environ['PYTHONPATH'] = os.pathsep.join([here, os.path.dirname(here)] + ([env_pp] if env_pp else []))
+    try:
+        procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(300)
+    finally:
+        os.environ['PYTHONPATH'] = env_pp
+    for p in procs:
+        if p.exitcode is None:
+            p.kill()
+        assert p.exitcode == 0, p.exitcode
+    res = q.get(timeout=10)
+    assert res['lookup'] == 0.0
+    assert res['adagrad'] < 1e-6, res['adagrad']
+    for step in range(3):
+        assert res[f'loss{step}'] < 2e-4, (step, res[f'loss{step}'])
+    bad = {k: v for k, v in res['params'].items() if v >= 2e-4}
+    assert not bad, bad

@@ -212,7 +212,7 @@ def main():
         'value': round(value, 1), 'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': round(1e3 * t / args.steps, 3), 'higher_is_better': True,
         'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
-        'config': {'workload': f'{args.config}: OneTrans 4L d{cfg.hidden_dim} H{cfg.num_heads} f{cfg.ffn_dim} '
+        'config': {'workload': f'{args.config}: OneTrans {cfg.num_layers}L d{cfg.hidden_dim} H{cfg.num_heads} f{cfg.ffn_dim} '
                                f'L_NS{cfg.num_ns_tokens} L_S{sum(seq_lens) + 2} (seq 3x{seq_lens[0]}), '
                                f'Criteo-shape 13 dense + 26 ids, replicated tables, fwd+bwd+optimizer',
                    'global_batch': B * world, 'per_gpu_batch': B, 'seq_len': sum(seq_lens) + 2,
@@ -233,6 +233,24 @@ def main():
                            'measured': f'HIP events per launch, {args.probe_steps}-step pass after the timed region, '
                                        'wgrad side stream off (standalone kernel durations)'}
         res['kernel_time_ms_per_step'] = {k: round(v['ms_per_step'], 3) for k, v in rep['families'].items()}
+        # north_star "MFMA utilisation on OneTrans attention" (standalone attention at
+        # L~140 is memory-heavy, so the block's matrix work is reported beside the core): achieved
+        # fp32-MFMA fraction of (i) the attention core kernels, (ii) the transformer block = every
+        # MFMA kernel (GEMMs + attention) over all of the block's kernel time (+ row-wise kernels)
+        fams = rep['families']
+        att = fams.get('attention')
+        if att is not None:
+            ms = lambda f: fams[f]['ms_per_step'] if f in fams else 0.0
+            fl = lambda f: fams[f]['tflops'] * fams[f]['ms_per_step'] * 1e9 if f in fams else 0.0
+            blk_fl = fl('mixed_gemm') + fl('attention')
+            blk_ms = ms('mixed_gemm') + ms('attention') + ms('rowwise')
+            res['attention_mfma'] = {
+                'core_tflops': round(att['tflops'], 2),
+                'core_frac': round(att['tflops'] / FP32_MFMA_PEAK_TFLOPS, 4),
+                'block_tflops': round(blk_fl / (blk_ms * 1e-3) / 1e12, 2),
+                'block_frac': round(blk_fl / (blk_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
+                'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+                'note': 'algorithmic flops (tail-only queries, causal pairs) / HIP-event kernel time'}
     if not args.no_cpu_baseline and world == 1:          # rank 0 at N=1 only
         res['cpu_baseline'] = cpu_baseline(args.config, args.cpu_seconds)
     print(json.dumps(res), flush=True)

@@ -48,13 +48,33 @@ __device__ __forceinline__ int64_t tail_token(int64_t r, int K, int I) {
   return b * I + (I - K) + (r - b * K);
 }
 
+// erf for the GELU: branch-free rational minimax on [-4, 4] (|error| < 5e-7; erf(±4) rounds to ±1 in
+// fp32).  This is the float erf TensorFlow's CPU kernels evaluate (Eigen's generic fast erf), so it
+// is also the reference's own arithmetic; ~15 VALU ops instead of the two-regime libm erff.
+__device__ __forceinline__ float fast_erf(float a) {
+  const float x = fminf(fmaxf(a, -4.f), 4.f);
+  const float x2 = x * x;
+  float p = -2.72614225801306e-10f;
+  p = fmaf(p, x2, 2.77068142495902e-08f);
+  p = fmaf(p, x2, -2.10102402082508e-06f);
+  p = fmaf(p, x2, -5.69250639462346e-05f);
+  p = fmaf(p, x2, -7.34990630326855e-04f);
+  p = fmaf(p, x2, -2.95459980854025e-03f);
+  p = fmaf(p, x2, -1.60960333262415e-02f);
+  float q = -1.45660718464996e-05f;
+  q = fmaf(q, x2, -2.13374055278905e-04f);
+  q = fmaf(q, x2, -1.68282697438203e-03f);
+  q = fmaf(q, x2, -7.37332916720468e-03f);
+  q = fmaf(q, x2, -1.42647390514189e-02f);
+  return x * p * __builtin_amdgcn_rcpf(q);
+}
 __device__ __forceinline__ float gelu_erf(float x) {
-  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+  return 0.5f * x * (1.0f + fast_erf(x * 0.70710678118654752440f));
 }
 __device__ __forceinline__ float gelu_erf_grad(float x) {
   // d/dx 0.5 x (1 + erf(x/sqrt2)) = 0.5 (1 + erf(x/sqrt2)) + x * exp(-x^2/2) / sqrt(2 pi)
-  return 0.5f * (1.0f + erff(x * 0.70710678118654752440f)) +
-         x * 0.39894228040143267794f * __expf(-0.5f * x * x);
+  return 0.5f * (1.0f + fast_erf(x * 0.70710678118654752440f)) +
+         x * 0.39894228040143267794f * __builtin_amdgcn_exp2f(-0.72134752044448170368f * x * x);
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

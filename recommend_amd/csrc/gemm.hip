@@ -461,8 +461,11 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
   // [NBUF][WBR][WLD] for A (r, k) then [NBUF][WBR][WLD] for D (r, n)
   const int ax = AXT >= 0 ? AXT : p.a_xform;
   const int per_chunk = p.ntk * p.ntn;
-  const int c = blockIdx.x / per_chunk;
-  const int rem = blockIdx.x % per_chunk;
+  // XCD-aware: the output tiles of one chunk (which share its A or D rows) get consecutive logical
+  // ids, and xcd_remap places consecutive ids on one XCD, so the shared rows come from that L2
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int c = wg / per_chunk;
+  const int rem = wg % per_chunk;
   const int tk = rem / p.ntn, tn = rem % p.ntn;
   const int k0 = tk * GT, n0 = tn * GT;
   const int row_begin = p.chunks[3 * c + 1], row_count = p.chunks[3 * c + 2];

@@ -28,15 +28,27 @@ class Probe:
         ev.record()
         return ev
 
-    def end(self, family: str, flops: float, ev0) -> None:
+    def end(self, family: str, flops: float, ev0, label: str = '') -> None:
         ev1 = torch.cuda.Event(enable_timing=True)
         ev1.record()
-        self.recs.append((family, flops, ev0, ev1))
+        self.recs.append((family, flops, ev0, ev1, label))
+
+    def by_label(self, steps: int):
+        """Per-launch-shape breakdown: {label: (launches/step, avg us, TF/s)} (tools/gemm_shapes.py)."""
+        torch.cuda.synchronize()
+        agg = {}
+        for (f, fl, a, b, lab) in self.recs:
+            d = agg.setdefault(f'{f} {lab}', [0, 0.0, 0.0])
+            d[0] += 1
+            d[1] += a.elapsed_time(b)
+            d[2] += fl
+        return {k: (n / steps, 1e3 * ms / n, fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0)
+                for k, (n, ms, fl) in agg.items()}
 
     def report(self, steps: int):
         torch.cuda.synchronize()
         fam = {}
-        for (f, fl, a, b) in self.recs:
+        for (f, fl, a, b, _) in self.recs:
             d = fam.setdefault(f, {'ms': 0.0, 'flops': 0.0, 'n': 0})
             d['ms'] += a.elapsed_time(b)
             d['flops'] += fl
@@ -85,7 +97,8 @@ def gemm(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish, w_g
          ldw, N, ptr(tile_group), ntiles, ptr(bias), bias_gstride, ptr(C), ldc, ptr(out_rows), epi, ptr(res),
          ldres, res_tok, ptr(aux), ldaux, seed & 0xFFFFFFFF, site, float(drop), tail[0], tail[1], stream())
     if ev is not None:
-        _probe.end('mixed_gemm', 2.0 * (m_rows or ntiles * 128) * K * N, ev)
+        _probe.end('mixed_gemm', 2.0 * (m_rows or ntiles * 128) * K * N, ev,
+                   f'gemm mode{mode} ax{a_xform} epi{epi} M{m_rows or ntiles * 128} K{K} N{N}')
 
 
 def gemm_rms(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish, w_gstride: int, ldw: int,
@@ -110,7 +123,8 @@ def gemm_rms(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish,
          ptr(res), ldres, res_tok, None, 0, seed & 0xFFFFFFFF, site, float(drop), tail[0], tail[1],
          ctypes.byref(e), stream())
     if ev is not None:
-        _probe.end('mixed_gemm', 2.0 * (m_rows or ntiles * 128) * K * N, ev)
+        _probe.end('mixed_gemm', 2.0 * (m_rows or ntiles * 128) * K * N, ev,
+                   f'gemm_rms mode{mode} ax{a_xform} epi{epi} M{m_rows or ntiles * 128} K{K} N{N}')
 
 
 def wgrad(A: Ptrish, lda: int, a_rows: Ptrish, D: Ptrish, ldd: int, d_rows: Ptrish, K: int, N: int, rmap_dev,
@@ -130,7 +144,7 @@ def wgrad(A: Ptrish, lda: int, a_rows: Ptrish, D: Ptrish, ldd: int, d_rows: Ptri
          ptr(d_rows), K, N, ptr(rmap_dev['chunks']), nchunks, ptr(rmap_dev['gchunk']), ngroups, ptr(dW),
          dw_gstride, ptr(db), db_gstride, int(accumulate), ptr(ws), ws.numel(), stream())
     if ev is not None:
-        _probe.end('mixed_gemm', 2.0 * m_rows * K * N, ev)
+        _probe.end('mixed_gemm', 2.0 * m_rows * K * N, ev, f'wgrad ax{a_xform} M{m_rows} K{K} N{N} ch{nchunks}')
 
 
 def transpose_banks(src, dst, banks_dev, nbanks, total_tiles) -> None:
@@ -142,7 +156,7 @@ def attn_fwd(qkv: torch.Tensor, ld: int, B: int, H: int, I: int, K: int, hd: int
     ev = _probe.begin() if _probe is not None else None
     call('ot_attn_fwd', ptr(qkv), ld, B, H, I, K, hd, ptr(out), ptr(lse), stream())
     if ev is not None:
-        _probe.end('attention', 4.0 * (K * I - K * (K - 1) / 2) * hd * H * B, ev)
+        _probe.end('attention', 4.0 * (K * I - K * (K - 1) / 2) * hd * H * B, ev, f'fwd I{I} K{K} hd{hd}')
 
 
 def attn_bwd(qkv, ld, out, dout, lse, B, H, I, K, hd, dqkv) -> None:
@@ -151,7 +165,7 @@ def attn_bwd(qkv, ld, out, dout, lse, B, H, I, K, hd, dqkv) -> None:
     call('ot_attn_bwd', ptr(qkv), ld, ptr(out), ptr(dout), ptr(lse), B, H, I, K, hd, ptr(dqkv), ptr(delta),
          stream())
     if ev is not None:
-        _probe.end('attention', 8.0 * (K * I - K * (K - 1) / 2) * hd * H * B, ev)
+        _probe.end('attention', 8.0 * (K * I - K * (K - 1) / 2) * hd * H * B, ev, f'bwd I{I} K{K} hd{hd}')
 
 
 def rmsnorm_fwd(x: Ptrish, ldx: int, rows: int, d: int, rstd: Ptrish, gamma: Ptrish = None, y: Ptrish = None,

@@ -85,7 +85,7 @@ class _Tokenize(torch.autograd.Function):
             nsm = plan['nsmat']
             K.wgrad(nsm, m.layout.f_pad, mp['rows'][0], (dx0, L_S * d), L0 * d, mp['rows'][0], m.layout.f_pad,
                     m.cfg_Lnsd, mp, plan['ns_map'].chunks.shape[0], 1, m.g('tok.ns.kernel'), 0, m.g('tok.ns.bias'),
-                    0, accumulate=acc, device=dev, m_rows=B)
+                    0, accumulate=acc, device=dev, m_rows=B, rowmap=plan['ns_map'])
             if plan['n_sparse'] > 0:
                 dns = torch.empty(B, m.layout.f_pad, device=dev)
                 K.gemm(OT_GEMM_NT, (dx0, L_S * d), L0 * d, m.cfg_Lnsd, mp['rows'][0], m.p('tok.ns.kernel'), 0,
@@ -105,7 +105,8 @@ class _Tokenize(torch.autograd.Function):
             sm = plan['seq_map'].to(dev)
             K.wgrad(plan['seq_A'], E, plan['seq_in'], dx0, d, sm['rows'][0], E, d, sm,
                     plan['seq_map'].chunks.shape[0], plan['nseq'], m.g('tok.seq.kernel'), E * d,
-                    m.g('tok.seq.bias'), d, accumulate=acc, device=dev, m_rows=plan['seq_M'])
+                    m.g('tok.seq.bias'), d, accumulate=acc, device=dev, m_rows=plan['seq_M'],
+                    rowmap=plan['seq_map'])
             if plan['seq_ids'] is not None:
                 M = plan['seq_M']
                 demb = torch.empty(M, E, device=dev)
@@ -257,7 +258,7 @@ class _Block(torch.autograd.Function):
                           tail=(Kq, I), dgamma=m.g(f'blk.{l}.norm2'), accumulate=acc, device=dev)
         # Wo
         with m.side(o, dyo):
-            _wgrad_single(m, o, dyo, d, d, mt, m.g(f'blk.{l}.wo'), acc, dev, maps['tail'].nrows)
+            _wgrad_single(m, o, dyo, d, d, mt, m.g(f'blk.{l}.wo'), acc, dev, maps['tail'].nrows, maps['tail'])
         do = torch.empty(B * Kq, d, device=dev)
         K.gemm(OT_GEMM_NT, dyo, d, d, mt['rows'][1], m.p(f'blk.{l}.wo'), 0, d, d, mt['tile_group'], nt, do, d,
                mt['rows'][1], m_rows=maps['tail'].nrows)
@@ -287,9 +288,14 @@ class _Block(torch.autograd.Function):
         return None, dx, None, None, None, None, None, None, None
 
 
-def _wgrad_single(m, A, D, K_, N, mt, dW, acc, dev, mrows=0):
-    """Wo gradient: one weight shared by every group -> wgrad with every chunk mapped to group 0."""
-    mp = m.single_group_chunks(mt)
+def _wgrad_single(m, A, D, K_, N, mt, dW, acc, dev, mrows=0, rowmap=None):
+    """Wo gradient: one weight shared by every group -> wgrad with every chunk mapped to group 0
+    (chunked for one resident round of its single output tile when the row map is given)."""
+    if rowmap is not None and rowmap.group_rows:
+        ch, _, _ = rowmap.chunks_for(((K_ + 127) // 128) * ((N + 127) // 128), dev)
+        mp = m.single_group_chunks({'chunks': ch})
+    else:
+        mp = m.single_group_chunks(mt)
     K.wgrad(A, K_, mt['rows'][1], D, N, mt['rows'][1], K_, N, mp, mp['chunks'].shape[0], 1, dW, 0, None, 0,
             accumulate=acc, device=dev, m_rows=mrows)
 

@@ -69,6 +69,18 @@ const char* ot_get_last_error_string(void);
  * (tape.gradient, train.py:131).  Tiles are 128 rows (ot_gemm_tile_rows()); tile i multiplies the
  * rows in_rows[128 i .. 128 i + 127] by W + tile_group[i] * w_gstride. */
 int ot_gemm_tile_rows(void);
+/* Matmul arithmetic of the GEMM family (process-wide; set before launching).
+ *   OT_MATMUL_SPLIT_BF16 (default): every f32 operand is split exactly into three bf16 parts
+ *     (x = x0 + x1 + x2, 8 significant bits each) and the product is sum_ij ai.bj over the six
+ *     largest terms on v_mfma_f32_32x32x16_bf16 (each part product exact in the f32 accumulator;
+ *     the dropped a1.b2 + a2.b1 + a2.b2 is below 2^-22 |a||b|, one f32 rounding).  Error vs an
+ *     f64 product measured no larger than native f32 (tools/split_gemm_check.py).
+ *   OT_MATMUL_F32: native v_mfma_f32_32x32x2_f32.
+ * Keras computes these Dense layers in f32 (model.py:38-57, 136-147; default float32 policy). */
+#define OT_MATMUL_F32 0
+#define OT_MATMUL_SPLIT_BF16 1
+int ot_set_matmul_mode(int mode);
+int ot_get_matmul_mode(void);
 int ot_mixed_gemm(int mode, const float* A, int64_t lda, int K, const int32_t* in_rows,
                   int a_xform, const float* a_rstd, const float* a_gamma,
                   const float* W, int64_t w_gstride, int64_t ldw, int N,

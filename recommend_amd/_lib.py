@@ -20,6 +20,8 @@ OT_AX_NONE, OT_AX_RMSNORM, OT_AX_GELU = 0, 1, 2
 OT_EPI_BIAS, OT_EPI_GELU_BWD, OT_EPI_GELU = 1, 2, 4
 OT_EPI_DROPOUT, OT_EPI_RESIDUAL, OT_EPI_ACCUMULATE = 8, 16, 32
 OT_EPI_ROW_RSTD, OT_EPI_RMSNORM_BWD = 64, 128
+OT_MATMUL_F32, OT_MATMUL_SPLIT_BF16 = 0, 1
+MATMUL_MODES = {'f32': OT_MATMUL_F32, 'split': OT_MATMUL_SPLIT_BF16}
 
 
 class RmsEpilogue(ctypes.Structure):
@@ -39,6 +41,8 @@ SIGNATURES = {
     'ot_version': (c_int, []),
     'ot_get_last_error_string': (c_char_p, []),
     'ot_gemm_tile_rows': (c_int, []),
+    'ot_set_matmul_mode': (c_int, [c_int]),
+    'ot_get_matmul_mode': (c_int, []),
     'ot_mixed_gemm': (c_int, [c_int, P, I64, c_int, P, c_int, P, P, P, I64, I64, c_int, P, c_int, P, I64,
                               P, I64, P, c_int, P, I64, c_int, P, I64, c_uint32, c_uint32, c_float, c_int,
                               c_int, P]),
@@ -114,6 +118,12 @@ def load():
         fn.restype = res
         fn.argtypes = args
     _lib = lib
+    # GEMM arithmetic (include/onetrans_hip.h ot_set_matmul_mode): ONETRANS_MATMUL=split (default,
+    # exact 3-way bf16 split, f32-accurate) or f32 (native f32 MFMA)
+    mode = os.environ.get('ONETRANS_MATMUL', 'split')
+    if mode not in MATMUL_MODES:
+        raise OneTransHipError(f'ONETRANS_MATMUL={mode!r}: expected one of {sorted(MATMUL_MODES)}')
+    call('ot_set_matmul_mode', MATMUL_MODES[mode])
     return lib
 
 

@@ -13,6 +13,7 @@
 // LDS images are [row][BK+4] (k contiguous, 144-B row stride => conflict-free ds_read_b128 for
 // 16 consecutive rows).  The k index inside an MFMA step is permuted (lane half h supplies
 // k = 16h + s at step s) so each lane reads 4 consecutive k with one ds_read_b128.
+#include <algorithm>
 #include <mutex>
 
 #include "common.h"
@@ -37,6 +38,48 @@ namespace ot {
 constexpr int GT = 128;           // tile rows / cols
 constexpr int GBK = OT_GEMM_BK;   // k per LDS stage (16 or 32)
 constexpr int GLD = GBK + 4;      // LDS row stride (floats)
+
+// Split-bf16 MFMA (OT_GEMM_SPLIT = number of product terms, 0 = native f32 MFMA).  Every f32
+// operand is split exactly into three bf16 pieces x = x0 + x1 + x2 (x0 = top 8 significant bits,
+// x1 the next 8, x2 the last 8; truncation keeps every step exact), and a.b = sum_ij ai.bj with
+// each bf16 x bf16 product exact in the f32 accumulator of v_mfma_f32_32x32x16_bf16 (32 cycles per
+// 32x32x16 against 64 cycles per 32x32x2 for the f32 form: 16x the rate).  9 terms = every
+// product (the f32 result up to accumulation order); 6 terms drop a1.b2, a2.b1, a2.b2, whose sum
+// is below 2^-22 |a||b| — the size of one f32 rounding of the product.
+#ifndef OT_GEMM_SPLIT
+#define OT_GEMM_SPLIT 6           // product terms of the split kernels (6 or 9; 3 is not f32-accurate)
+#endif
+#ifndef OT_GEMM_SPLIT_SCHED
+#define OT_GEMM_SPLIT_SCHED 0     // >0: interleave this many VALU ops after each MFMA (sched_group_barrier)
+#endif
+constexpr int SPLIT_TERMS = OT_GEMM_SPLIT;
+constexpr int SRS = 3 * 16 + 8;   // split LDS row stride (ushorts): 3 planes x 16 k + pad = 112 B
+static_assert(SPLIT_TERMS == 3 || SPLIT_TERMS == 6 || SPLIT_TERMS == 9, "OT_GEMM_SPLIT");
+static_assert(GBK == 16, "split-bf16 staging assumes 16-k stages");
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// f32x4 -> three planes of 4 bf16 (each packed into 2 dwords, element 0 in the low half)
+__device__ __forceinline__ void split3(f32x4 v, u32x2& p0, u32x2& p1, u32x2& p2) {
+  uint32_t a[4], b[4], c[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float x = v[j];
+    const uint32_t u0 = __float_as_uint(x) & 0xffff0000u;
+    const float r1 = x - __uint_as_float(u0);
+    const uint32_t u1 = __float_as_uint(r1) & 0xffff0000u;
+    const float r2 = r1 - __uint_as_float(u1);
+    a[j] = u0; b[j] = u1; c[j] = __float_as_uint(r2);
+  }
+  p0 = u32x2{__builtin_amdgcn_perm(a[1], a[0], 0x07060302u), __builtin_amdgcn_perm(a[3], a[2], 0x07060302u)};
+  p1 = u32x2{__builtin_amdgcn_perm(b[1], b[0], 0x07060302u), __builtin_amdgcn_perm(b[3], b[2], 0x07060302u)};
+  p2 = u32x2{__builtin_amdgcn_perm(c[1], c[0], 0x07060302u), __builtin_amdgcn_perm(c[3], c[2], 0x07060302u)};
+}
+__device__ __forceinline__ f32x16 mfma_bf16(u32x4 a, u32x4 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0,
+                                                  0);
+}
 
 struct GemmArgs {
   const float* A; int64_t lda; int K;
@@ -85,13 +128,16 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 
 // AXT / EPIT: compile-time prologue / epilogue (-1 = read p.a_xform / p.epi at run time).
 // EDGE: K % 32 != 0 or N % 128 != 0 (bounds checks in staging and epilogue).
-template <bool NT, int AXT, int EPIT, bool EDGE>
-__global__ __launch_bounds__(256, OT_GEMM_MINWG) void mixed_gemm_kernel(GemmArgs p) {
+// SPLT: split-bf16 MFMA (NT only; the main loop's LDS images and register sets limit it to 2
+// workgroups per CU), else native f32 MFMA.
+template <bool NT, int AXT, int EPIT, bool EDGE, bool SPLT>
+__global__ __launch_bounds__(256, (NT && SPLT) ? 2 : OT_GEMM_MINWG) void mixed_gemm_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* As = smem;                      // [2][GT][GLD]
   float* Bs = smem + 2 * GT * GLD;       // [2][GT][GLD]
   const int ax = AXT >= 0 ? AXT : p.a_xform;
   const int epi = EPIT >= 0 ? EPIT : p.epi;
+  constexpr bool SPL = NT && SPLT;
 
   const int nwg = p.ntm * p.ntn;
   const int wg = xcd_remap(blockIdx.x, nwg);
@@ -199,6 +245,119 @@ __global__ __launch_bounds__(256, OT_GEMM_MINWG) void mixed_gemm_kernel(GemmArgs
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 
   const int nk = (p.K + GBK - 1) / GBK;
+  if constexpr (SPL) {
+    // ---- split-bf16 main loop.  A 16-k stage is 4x fewer MFMA cycles than in f32, so the global
+    // loads run two stages ahead (two register sets, loop unrolled by 2): stage k+2 is issued before
+    // the MFMAs of stage k, stage k+1 (issued one iteration earlier) is split into LDS after them.
+    struct SStage { f32x4 a[NPASS], b[NPASS], g; bool kin; };
+    auto sload = [&](SStage& st, int k0) {
+      st.kin = !EDGE || (k0 + 4 * sc < p.K);
+      const int ko = st.kin ? k0 : -4 * sc;
+      if (ax == OT_AX_RMSNORM) st.g = *reinterpret_cast<const f32x4*>(p.a_gamma + ko + 4 * sc);
+#pragma unroll
+      for (int i = 0; i < NPASS; ++i) st.a[i] = *reinterpret_cast<const f32x4*>(arow[i] + ko);
+      if (RMS_EARLY && ax == OT_AX_RMSNORM) {
+#pragma unroll
+        for (int i = 0; i < NPASS; ++i) st.a[i] = st.a[i] * st.g * ars[i];
+      }
+#pragma unroll
+      for (int i = 0; i < NPASS; ++i) st.b[i] = *reinterpret_cast<const f32x4*>(brow[i] + ko);
+    };
+    // split images [row][plane][16 k] (ushorts, row stride SRS = 112 B): a lane's 8-k read of one
+    // plane is a 16-B piece, and 16 consecutive rows land in 16 distinct bank groups
+    struct SPlanes { u32x2 a[NPASS][3], b[NPASS][3]; };
+    auto ssplit = [&](const SStage& st, SPlanes& q) {
+#pragma unroll
+      for (int i = 0; i < NPASS; ++i) {
+        f32x4 v = st.a[i];
+        if (!RMS_EARLY && ax == OT_AX_RMSNORM) {
+          v = v * st.g * ars[i];
+        } else if (ax == OT_AX_GELU) {
+          v.x = gelu_erf(v.x); v.y = gelu_erf(v.y); v.z = gelu_erf(v.z); v.w = gelu_erf(v.w);
+        }
+        if (!(aok[i] && st.kin)) v = zero4;
+        split3(v, q.a[i][0], q.a[i][1], q.a[i][2]);
+        const f32x4 w = (bok[i] && st.kin) ? st.b[i] : zero4;
+        split3(w, q.b[i][0], q.b[i][1], q.b[i][2]);
+      }
+    };
+    auto swrite = [&](const SPlanes& q, int buf) {
+      uint16_t* as16 = reinterpret_cast<uint16_t*>(smem) + buf * GT * SRS;
+      uint16_t* bs16 = reinterpret_cast<uint16_t*>(smem) + (2 + buf) * GT * SRS;
+#pragma unroll
+      for (int i = 0; i < NPASS; ++i)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+          *reinterpret_cast<u32x2*>(as16 + (sr + RPP * i) * SRS + 16 * pl + 4 * sc) = q.a[i][pl];
+          *reinterpret_cast<u32x2*>(bs16 + (sr + RPP * i) * SRS + 16 * pl + 4 * sc) = q.b[i][pl];
+        }
+    };
+    auto smma = [&](int buf) {
+      const uint16_t* as16 = reinterpret_cast<const uint16_t*>(smem) + buf * GT * SRS + (wm + li) * SRS + 8 * h;
+      const uint16_t* bs16 = reinterpret_cast<const uint16_t*>(smem) + (2 + buf) * GT * SRS + (wn + li) * SRS + 8 * h;
+      u32x4 fa[2][3], fb[2][3];
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          fa[m][q] = *reinterpret_cast<const u32x4*>(as16 + 32 * m * SRS + 16 * q);
+          fb[m][q] = *reinterpret_cast<const u32x4*>(bs16 + 32 * m * SRS + 16 * q);
+        }
+      // smallest terms first; (plane of A, plane of B)
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+          if (SPLIT_TERMS >= 9) {
+            acc[m][n] = mfma_bf16(fa[m][2], fb[n][2], acc[m][n]);
+            acc[m][n] = mfma_bf16(fa[m][1], fb[n][2], acc[m][n]);
+            acc[m][n] = mfma_bf16(fa[m][2], fb[n][1], acc[m][n]);
+          }
+          if (SPLIT_TERMS >= 6) {
+            acc[m][n] = mfma_bf16(fa[m][0], fb[n][2], acc[m][n]);
+            acc[m][n] = mfma_bf16(fa[m][2], fb[n][0], acc[m][n]);
+            acc[m][n] = mfma_bf16(fa[m][1], fb[n][1], acc[m][n]);
+          }
+          acc[m][n] = mfma_bf16(fa[m][0], fb[n][1], acc[m][n]);
+          acc[m][n] = mfma_bf16(fa[m][1], fb[n][0], acc[m][n]);
+          acc[m][n] = mfma_bf16(fa[m][0], fb[n][0], acc[m][n]);
+        }
+    };
+    // one stage: issue the loads two stages ahead, MFMAs of the LDS stage interleaved with the split
+    // of the next stage (already in registers), which is then written to the other buffer.
+    // Branch-free (the loads past the end re-read the last stage; the extra image is never read)
+    // so the whole stage is one scheduling region.
+    auto stage = [&](SStage& ld, const SStage& nx, int kload, int buf) {
+      sload(ld, kload);
+      SPlanes q;
+      ssplit(nx, q);
+      smma(buf);
+      swrite(q, buf ^ 1);
+#if OT_GEMM_SPLIT_SCHED
+#pragma unroll
+      for (int i = 0; i < 4 * SPLIT_TERMS; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, OT_GEMM_SPLIT_SCHED, 0);
+      }
+#endif
+      __syncthreads();
+    };
+    SStage s0, s1;
+    sload(s0, 0);
+    sload(s1, nk > 1 ? GBK : 0);
+    {
+      SPlanes q;
+      ssplit(s0, q);
+      swrite(q, 0);
+    }
+    __syncthreads();
+    const int klast = (nk - 1) * GBK;
+    for (int kt = 0; kt < nk; kt += 2) {
+      stage(s0, s1, min((kt + 2) * GBK, klast), 0);     // stage kt in buf 0, kt+1 in s1
+      if (kt + 1 >= nk) break;
+      stage(s1, s0, min((kt + 3) * GBK, klast), 1);     // stage kt+1 in buf 1, kt+2 in s0
+    }
+  } else {
   load_stage(0);
   store_stage(0);
   __syncthreads();
@@ -233,6 +392,7 @@ __global__ __launch_bounds__(256, OT_GEMM_MINWG) void mixed_gemm_kernel(GemmArgs
     // barrier that ended it: one barrier per k-tile
     if (more) store_stage(cur ^ 1);
     __syncthreads();
+  }
   }
 
   // ---- epilogue (flags compile-time unless EPIT < 0).  Per 32-row block m: resolve the 16 output
@@ -666,9 +826,20 @@ __global__ __launch_bounds__(256) void transpose_banks_kernel(const float* __res
   }
 }
 
+// matmul arithmetic of the GEMM family (ot_set_matmul_mode); process-wide, set before launching
+static int g_matmul_mode = OT_MATMUL_SPLIT_BF16;
+
 }  // namespace ot
 
 using namespace ot;
+
+extern "C" int ot_set_matmul_mode(int mode) {
+  OT_REQUIRE(mode == OT_MATMUL_F32 || mode == OT_MATMUL_SPLIT_BF16, "ot_set_matmul_mode: unknown mode %d", mode);
+  g_matmul_mode = mode;
+  return OT_OK;
+}
+
+extern "C" int ot_get_matmul_mode(void) { return g_matmul_mode; }
 
 extern "C" int ot_transpose_banks(const float* src, float* dst, const int64_t* banks_dev, int nbanks,
                                   int64_t total_tiles, void* stream) {
@@ -738,7 +909,8 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
     p.drop_thr = drop_threshold(drop_rate);
     p.drop_scale = 1.f / (1.f - drop_rate);
   }
-  const size_t shmem = 4 * GT * GLD * sizeof(float);
+  const bool split = g_matmul_mode == OT_MATMUL_SPLIT_BF16 && mode == OT_GEMM_NT;
+  const size_t shmem = split ? 4 * GT * SRS * sizeof(uint16_t) : 4 * GT * GLD * sizeof(float);
   auto a16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
   const bool vec_ok = ldc % 4 == 0 && a16(C) && (!(epi & OT_EPI_RESIDUAL) || (ldres % 4 == 0 && a16(res))) &&
                       (!(epi & OT_EPI_GELU_BWD) || (ldaux % 4 == 0 && a16(aux))) &&
@@ -751,7 +923,8 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
   const int e = epi, x = a_xform;
 #define OT_SPEC(NT_, AX_, EP_)                                                                  \
   if (mode == (NT_ ? OT_GEMM_NT : OT_GEMM_NN) && x == AX_ && e == (EP_))                         \
-    kern = edge ? mixed_gemm_kernel<NT_, AX_, EP_, true> : mixed_gemm_kernel<NT_, AX_, EP_, false>;
+    kern = split ? (edge ? mixed_gemm_kernel<NT_, AX_, EP_, true, true> : mixed_gemm_kernel<NT_, AX_, EP_, false, true>) \
+                 : (edge ? mixed_gemm_kernel<NT_, AX_, EP_, true, false> : mixed_gemm_kernel<NT_, AX_, EP_, false, false>);
   OT_SPEC(true, OT_AX_RMSNORM, 0)
   OT_SPEC(true, OT_AX_RMSNORM, OT_EPI_BIAS)
   OT_SPEC(true, OT_AX_GELU, OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_DROPOUT)
@@ -771,16 +944,19 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
 #undef OT_SPEC
   OT_REQUIRE(kern || !rms_flags, "ot_mixed_gemm_rms: no specialised kernel for epilogue flags %d", epi);
   if (!kern) {   // any other combination: generic instantiation (run-time prologue/epilogue)
-    if (mode == OT_GEMM_NT)
-      kern = edge ? mixed_gemm_kernel<true, -1, -1, true> : mixed_gemm_kernel<true, -1, -1, false>;
+    if (mode == OT_GEMM_NT && split)
+      kern = edge ? mixed_gemm_kernel<true, -1, -1, true, true> : mixed_gemm_kernel<true, -1, -1, false, true>;
+    else if (mode == OT_GEMM_NT)
+      kern = edge ? mixed_gemm_kernel<true, -1, -1, true, false> : mixed_gemm_kernel<true, -1, -1, false, false>;
     else
-      kern = edge ? mixed_gemm_kernel<false, -1, -1, true> : mixed_gemm_kernel<false, -1, -1, false>;
+      kern = edge ? mixed_gemm_kernel<false, -1, -1, true, false> : mixed_gemm_kernel<false, -1, -1, false, false>;
   }
   static std::once_flag lds_once;   // opt every instantiation in to > 64 KiB LDS (gfx950: 160 KiB per CU)
   std::call_once(lds_once, [] {
-    const int bytes = 4 * GT * GLD * sizeof(float);
-    for (void (*k)(GemmArgs) : {mixed_gemm_kernel<true, -1, -1, true>, mixed_gemm_kernel<true, -1, -1, false>,
-                                mixed_gemm_kernel<false, -1, -1, true>, mixed_gemm_kernel<false, -1, -1, false>})
+    const int bytes = (int)std::max(4 * GT * GLD * sizeof(float), 4 * GT * SRS * sizeof(uint16_t));
+    for (void (*k)(GemmArgs) : {mixed_gemm_kernel<true, -1, -1, true, false>, mixed_gemm_kernel<true, -1, -1, false, false>,
+                                mixed_gemm_kernel<false, -1, -1, true, false>, mixed_gemm_kernel<false, -1, -1, false, false>,
+                                mixed_gemm_kernel<true, -1, -1, true, true>, mixed_gemm_kernel<true, -1, -1, false, true>})
       (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     (void)hipGetLastError();
   });

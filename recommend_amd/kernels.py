@@ -69,6 +69,20 @@ def set_probe(p) -> None:
     _probe = p
 
 
+def set_matmul_mode(mode: str) -> str:
+    """GEMM arithmetic: 'split' (exact 3-way bf16 split on bf16 MFMA, f32-accurate) or 'f32'
+    (native f32 MFMA).  Returns the previous mode."""
+    inv = {v: k for k, v in _lib.MATMUL_MODES.items()}
+    old = inv[_lib.load().ot_get_matmul_mode()]
+    call('ot_set_matmul_mode', _lib.MATMUL_MODES[mode])
+    return old
+
+
+def matmul_mode() -> str:
+    inv = {v: k for k, v in _lib.MATMUL_MODES.items()}
+    return inv[_lib.load().ot_get_matmul_mode()]
+
+
 def ptr(x: Ptrish):
     if x is None:
         return None

@@ -39,9 +39,41 @@ def _random_map(rng, n_in, n_out, G, counts):
     return build_map(per)
 
 
+@pytest.fixture(params=['split', 'f32'])
+def matmul(request, dev):
+    """Run a GEMM test under both matmul modes (ot_set_matmul_mode)."""
+    old = K.set_matmul_mode(request.param)
+    yield request.param
+    K.set_matmul_mode(old)
+
+
+@pytest.mark.parametrize('M,K_,N', [(4096, 128, 512), (4096, 512, 128), (2048, 432, 1536)])
+def test_split_gemm_accuracy(dev, M, K_, N):
+    """The split-bf16 GEMM (default) is as accurate as native f32 MFMA: errors against an f64
+    product, relative to sum_k |a_k||w_k| (the f32 error scale), stay at f32 rounding level and
+    no larger than the native f32 kernel's (x1.5 slack)."""
+    g = torch.Generator().manual_seed(1)
+    A = torch.randn(M, K_, generator=g) * torch.exp(torch.randn(M, 1, generator=g))   # varied row scales
+    W = torch.randn(N, K_, generator=g) * 0.05
+    ref = A.double() @ W.double().T
+    scale = A.double().abs() @ W.double().abs().T
+    errs = {}
+    for mode in ('f32', 'split'):
+        old = K.set_matmul_mode(mode)
+        C = torch.empty(M, N, device=dev)
+        K.gemm(OT_GEMM_NT, A.to(dev), K_, K_, None, W.to(dev), 0, K_, N, None, M // 128, C, N, None)
+        torch.cuda.synchronize()
+        K.set_matmul_mode(old)
+        e = (C.double().cpu() - ref).abs() / scale
+        errs[mode] = (float(e.max()), float(e.mean()))
+    assert errs['split'][0] < 1e-6, errs
+    assert errs['split'][1] <= 1.5 * errs['f32'][1], errs
+    assert errs['split'][0] <= 1.5 * errs['f32'][0], errs
+
+
 @pytest.mark.parametrize('mode', [OT_GEMM_NN, OT_GEMM_NT])
 @pytest.mark.parametrize('K_,N', [(64, 192), (128, 384), (512, 128), (432, 100)])
-def test_mixed_gemm_plain(dev, mode, K_, N):
+def test_mixed_gemm_plain(dev, matmul, mode, K_, N):
     if mode == OT_GEMM_NN and N % 4:
         pytest.skip('NN needs N % 4 == 0')
     rng = np.random.default_rng(0)
@@ -66,7 +98,7 @@ def test_mixed_gemm_plain(dev, mode, K_, N):
     torch.testing.assert_close(C.double().cpu(), ref, rtol=1e-4, atol=1e-4 * math.sqrt(K_))
 
 
-def test_mixed_gemm_prologue_epilogue(dev):
+def test_mixed_gemm_prologue_epilogue(dev, matmul):
     """rmsnorm / gelu prologues, bias + dropout + residual (token-mapped) + accumulate epilogues."""
     rng = np.random.default_rng(1)
     B, I, Kq, d, N = 9, 20, 7, 64, 64
@@ -224,7 +256,7 @@ def test_rmsnorm(dev, d):
 
 
 @pytest.mark.parametrize('K_', [128, 512])
-def test_gemm_rms_epilogues(dev, K_):
+def test_gemm_rms_epilogues(dev, matmul, K_):
     """ot_mixed_gemm_rms: (1) residual GEMM emitting the next RMSNorm's rstd, (2) dgrad GEMM with the
     RMSNorm backward (tail-mapped residual gradient, masked copy, dgamma) — vs torch fp64."""
     rng = np.random.default_rng(5)

@@ -28,6 +28,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
+BF16_MFMA_PEAK_TFLOPS = 16 * FP32_MFMA_PEAK_TFLOPS   # "1/16 of BF16" (same table): 2516.8 dense
+SPLIT_TERMS = 6                    # bf16 MFMA products per f32 product in OT_MATMUL_SPLIT_BF16
 HBM_PEAK_GBS = 8000.0
 
 
@@ -223,9 +225,19 @@ def main():
     if rep is not None:
         traffic, tsrc = hbm_traffic(args.config)
         dom = rep['families']['mixed_gemm']
-        res['roofline'] = {'bound': 'mfma', 'kernel': 'mixed_gemm_kernel + wgrad_kernel (fp32 MFMA)',
-                           'achieved': round(dom['tflops'], 2), 'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-                           'frac': round(dom['tflops'] / FP32_MFMA_PEAK_TFLOPS, 4), 'traffic': traffic,
+        if K.matmul_mode() == 'split':
+            # the GEMMs issue SPLIT_TERMS bf16 MFMA products per f32 product: their matrix-core
+            # ceiling in f32 flops is the bf16 dense peak / SPLIT_TERMS
+            gpeak = round(BF16_MFMA_PEAK_TFLOPS / SPLIT_TERMS, 1)
+            gkern = ('mixed_gemm_kernel + wgrad_split_kernel (f32 operands split exactly into 3 bf16 parts, '
+                     f'{SPLIT_TERMS} bf16 MFMA products per f32 product; peak = bf16 dense / {SPLIT_TERMS})')
+        else:
+            gpeak = FP32_MFMA_PEAK_TFLOPS
+            gkern = 'mixed_gemm_kernel + wgrad_kernel (native f32 MFMA)'
+        res['matmul'] = K.matmul_mode()
+        res['roofline'] = {'bound': 'mfma', 'kernel': gkern,
+                           'achieved': round(dom['tflops'], 2), 'peak': gpeak, 'unit': 'TFLOP/s',
+                           'frac': round(dom['tflops'] / gpeak, 4), 'traffic': traffic,
                            'traffic_unit': 'HBM bytes per launch (PMC FETCH_SIZE + WRITE_SIZE, calibrated)',
                            'traffic_source': tsrc,
                            'avg_launch_us': round(dom['avg_us'], 2), 'launches_per_step': dom['launches_per_step'],
@@ -244,13 +256,17 @@ def main():
             fl = lambda f: fams[f]['tflops'] * fams[f]['ms_per_step'] * 1e9 if f in fams else 0.0
             blk_fl = fl('mixed_gemm') + fl('attention')
             blk_ms = ms('mixed_gemm') + ms('attention') + ms('rowwise')
+            # matrix-core time the block's algorithmic work needs at each kernel's own peak, over the
+            # block's kernel time (GEMMs at the split ceiling, attention at the f32 MFMA peak)
+            busy_ms = fl('mixed_gemm') / (gpeak * 1e9) + fl('attention') / (FP32_MFMA_PEAK_TFLOPS * 1e9)
             res['attention_mfma'] = {
                 'core_tflops': round(att['tflops'], 2),
                 'core_frac': round(att['tflops'] / FP32_MFMA_PEAK_TFLOPS, 4),
+                'core_peak': FP32_MFMA_PEAK_TFLOPS,
                 'block_tflops': round(blk_fl / (blk_ms * 1e-3) / 1e12, 2),
-                'block_frac': round(blk_fl / (blk_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
-                'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-                'note': 'algorithmic flops (tail-only queries, causal pairs) / HIP-event kernel time'}
+                'block_frac': round(busy_ms / blk_ms, 4), 'unit': 'TFLOP/s',
+                'note': 'algorithmic flops (tail-only queries, causal pairs) / HIP-event kernel time; '
+                        'attention core on native f32 MFMA (peak 157.3)'}
     if not args.no_cpu_baseline and world == 1:          # rank 0 at N=1 only
         res['cpu_baseline'] = cpu_baseline(args.config, args.cpu_seconds)
     print(json.dumps(res), flush=True)

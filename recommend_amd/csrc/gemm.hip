@@ -757,6 +757,197 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
   if (do_bias && n0 + t < p.N) p.bslab[(int64_t)c * p.N + n0 + t] = bsum;
 }
 
+// ------------------------------------------------------------------------------------------
+// Split-bf16 wgrad (OT_MATMUL_SPLIT_BF16): same chunk/slab contract as wgrad_kernel.  The 32-row
+// stage of A and D is split into three bf16 planes stored ROW-major in LDS (the staging writes stay
+// 8-B pieces of the loaded rows), and the MFMA operands, which need 8 consecutive data rows of one
+// column per lane, come out of ds_read_b64_tr_b16 transposed reads (4 rows x 16 columns per 16-lane
+// group).  Row images are 256 B with the 16-B chunk XOR swizzle ch ^ ((r&3)<<2 | (r>>2)&3), which
+// makes both the staging writes and the transposed reads conflict-free (cdna_hip_programming T10).
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+constexpr int WSPLANE = WBR * 256;          // bytes of one plane image (32 rows x 128 bf16)
+constexpr int WSOP = 3 * WSPLANE;           // bytes of one operand (3 planes)
+
+__device__ __forceinline__ int wsw_off(int r, int ch) { return 256 * r + 16 * (ch ^ (((r & 3) << 2) | ((r >> 2) & 3))); }
+
+__device__ __forceinline__ v4i16 ds_tr16(const char* base, int off) {
+  typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + off));
+}
+
+template <int AXT>
+__global__ __launch_bounds__(256, 2) void wgrad_split_kernel(WgradArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem_c[];
+  const int ax = AXT >= 0 ? AXT : p.a_xform;
+  const int per_chunk = p.ntk * p.ntn;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int c = wg / per_chunk;
+  const int rem = wg % per_chunk;
+  const int tk = rem / p.ntn, tn = rem % p.ntn;
+  const int k0 = tk * GT, n0 = tn * GT;
+  const int row_begin = p.chunks[3 * c + 1], row_count = p.chunks[3 * c + 2];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int h = lane >> 5, li = lane & 31;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const int sr = t >> 3, sc = t & 7;       // staging: row sr of the stage, float4 columns sc + 8i
+  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  char* As = smem_c;
+  char* Ds = smem_c + WSOP;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  const bool do_bias = p.bslab && tk == 0;
+  f32x4 bsum[4] = {zero4, zero4, zero4, zero4};
+
+  auto rows_of = [&](int rs, int& ar, int& dr) {
+    const int lr = rs + sr;
+    const int64_t mi = (int64_t)row_begin + (lr < row_count ? lr : 0);
+    ar = p.a_rows ? p.a_rows[mi] : (int)mi;
+    dr = p.d_rows ? p.d_rows[mi] : (int)mi;
+  };
+  f32x4 va[4], vd[4], gv[4];
+  float rsd = 1.f;
+  bool inr = false;
+  auto load_stage = [&](int st, int ar, int dr) {
+    inr = st * WBR + sr < row_count && ar >= 0 && dr >= 0;
+    const float* pa = p.A + (int64_t)(inr ? ar : 0) * p.lda;
+    const float* pd = p.D + (int64_t)(inr ? dr : 0) * p.ldd;
+    if (ax == OT_AX_RMSNORM) rsd = p.a_rstd[inr ? ar : 0];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = k0 + 4 * (sc + 8 * i), n = n0 + 4 * (sc + 8 * i);
+      const int kc = k < p.K ? k : 0, nc = n < p.N ? n : 0;
+      va[i] = *reinterpret_cast<const f32x4*>(pa + kc);
+      vd[i] = *reinterpret_cast<const f32x4*>(pd + nc);
+      if (ax == OT_AX_RMSNORM) gv[i] = *reinterpret_cast<const f32x4*>(p.a_gamma + kc);
+    }
+  };
+  auto store_stage = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int cc = sc + 8 * i;                      // float4 column index 0..31
+      f32x4 a = va[i], dv = vd[i];
+      if (ax == OT_AX_RMSNORM) {
+        a = a * gv[i] * rsd;
+      } else if (ax == OT_AX_GELU) {
+        a.x = gelu_erf(a.x); a.y = gelu_erf(a.y); a.z = gelu_erf(a.z); a.w = gelu_erf(a.w);
+      }
+      if (!(inr && k0 + 4 * cc < p.K)) a = zero4;
+      if (!(inr && n0 + 4 * cc < p.N)) dv = zero4;
+      if (do_bias) bsum[i] += dv;
+      const int off = wsw_off(sr, cc >> 1) + 8 * (cc & 1);
+      u32x2 q0, q1, q2;
+      split3(a, q0, q1, q2);
+      *reinterpret_cast<u32x2*>(As + off) = q0;
+      *reinterpret_cast<u32x2*>(As + WSPLANE + off) = q1;
+      *reinterpret_cast<u32x2*>(As + 2 * WSPLANE + off) = q2;
+      split3(dv, q0, q1, q2);
+      *reinterpret_cast<u32x2*>(Ds + off) = q0;
+      *reinterpret_cast<u32x2*>(Ds + WSPLANE + off) = q1;
+      *reinterpret_cast<u32x2*>(Ds + 2 * WSPLANE + off) = q2;
+    }
+  };
+  // transposed-read addresses (stage-invariant): lane 4q+pp of its 16-lane group reads row
+  // r0 + q, chunk c0 + (pp >> 1), half pp & 1; r0 = 16 t2 + 8 h + 4 rd, c0 = (col0 + 16 (g & 1)) / 8
+  const int gi = lane & 15, q = gi >> 2, pp = gi & 3, g1 = (lane >> 4) & 1;
+  int aoff[2][2], doff[2][2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int rd = 0; rd < 2; ++rd) {
+      const int r = 8 * h + 4 * rd + q;
+      aoff[m][rd] = wsw_off(r, (wm + 32 * m + 16 * g1) / 8 + (pp >> 1)) + 8 * (pp & 1);
+      doff[m][rd] = wsw_off(r, (wn + 32 * m + 16 * g1) / 8 + (pp >> 1)) + 8 * (pp & 1);
+    }
+
+  const int nst = (row_count + WBR - 1) / WBR;
+  int ar, dr, ar2 = -1, dr2 = -1;
+  rows_of(0, ar, dr);
+  if (nst > 1) rows_of(WBR, ar2, dr2);
+  load_stage(0, ar, dr);
+  store_stage();
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    const bool more = st + 1 < nst;
+    int ar3 = -1, dr3 = -1;
+    if (more) {
+      load_stage(st + 1, ar2, dr2);
+      if (st + 2 < nst) rows_of((st + 2) * WBR, ar3, dr3);
+    }
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2) {                    // two 16-row MFMA k-steps per stage
+      u32x4 fa[2][3], fb[2][3];
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+          const int po = pl * WSPLANE + t2 * 16 * 256;   // row r -> r + 16 keeps the swizzle (r & 15)
+          const v4i16 a0 = ds_tr16(As + po, aoff[m][0]), a1 = ds_tr16(As + po, aoff[m][1]);
+          const v4i16 d0 = ds_tr16(Ds + po, doff[m][0]), d1 = ds_tr16(Ds + po, doff[m][1]);
+          const u32x2 a0u = __builtin_bit_cast(u32x2, a0), a1u = __builtin_bit_cast(u32x2, a1);
+          const u32x2 d0u = __builtin_bit_cast(u32x2, d0), d1u = __builtin_bit_cast(u32x2, d1);
+          fa[m][pl] = u32x4{a0u.x, a0u.y, a1u.x, a1u.y};
+          fb[m][pl] = u32x4{d0u.x, d0u.y, d1u.x, d1u.y};
+        }
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+          if (SPLIT_TERMS >= 9) {
+            acc[m][n] = mfma_bf16(fa[m][2], fb[n][2], acc[m][n]);
+            acc[m][n] = mfma_bf16(fa[m][1], fb[n][2], acc[m][n]);
+            acc[m][n] = mfma_bf16(fa[m][2], fb[n][1], acc[m][n]);
+          }
+          if (SPLIT_TERMS >= 6) {
+            acc[m][n] = mfma_bf16(fa[m][0], fb[n][2], acc[m][n]);
+            acc[m][n] = mfma_bf16(fa[m][2], fb[n][0], acc[m][n]);
+            acc[m][n] = mfma_bf16(fa[m][1], fb[n][1], acc[m][n]);
+          }
+          acc[m][n] = mfma_bf16(fa[m][0], fb[n][1], acc[m][n]);
+          acc[m][n] = mfma_bf16(fa[m][1], fb[n][0], acc[m][n]);
+          acc[m][n] = mfma_bf16(fa[m][0], fb[n][0], acc[m][n]);
+        }
+    }
+    __syncthreads();
+    if (more) store_stage();
+    __syncthreads();
+    ar2 = ar3; dr2 = dr3;
+  }
+  float* slab = p.slab + (int64_t)c * p.K * p.N;
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int k = k0 + wm + 32 * m + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (k >= p.K) continue;
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        const int col = n0 + wn + 32 * n + li;
+        if (col < p.N) slab[(int64_t)k * p.N + col] = acc[m][n][r];
+      }
+    }
+  if (do_bias) {
+    // per-thread column partials (columns 4(sc + 8i)) -> LDS [sr][32 float4] -> fixed-order sum over
+    // the 32 staging rows per column
+    f32x4* bl = reinterpret_cast<f32x4*>(smem_c);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bl[sr * 32 + sc + 8 * i] = bsum[i];
+    __syncthreads();
+    if (t < GT && n0 + t < p.N) {
+      const float* bf = reinterpret_cast<const float*>(smem_c);
+      float a = 0.f;
+      for (int r = 0; r < WBR; ++r) a += bf[r * GT + t];
+      p.bslab[(int64_t)c * p.N + n0 + t] = a;
+    }
+  }
+}
+
+
 // Sum the slabs of each group's chunks (chunks of one group are contiguous) into dW[g] (and db).
 // Block = 16 float4 columns x 16 chunk lanes; chunk lane c sums chunks c, c+16, ... and the 16
 // partials are combined in a fixed order through LDS (deterministic).
@@ -1027,10 +1218,17 @@ extern "C" int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a
     WgradArgs p{A, lda, a_rows, a_xform, a_rstd, a_gamma, D, ldd, d_rows, K, N, chunks, nchunks, slab, bslab,
                 (int)ceil_div(K, GT), (int)ceil_div(N, GT)};
     const size_t shmem = (OT_WGRAD_DBUF ? 4 : 2) * WBR * WLD * sizeof(float);
-    void (*kern)(WgradArgs) = a_xform == OT_AX_NONE      ? wgrad_kernel<OT_AX_NONE>
-                              : a_xform == OT_AX_RMSNORM ? wgrad_kernel<OT_AX_RMSNORM>
-                              : a_xform == OT_AX_GELU    ? wgrad_kernel<OT_AX_GELU>
-                                                         : wgrad_kernel<-1>;
+    const bool split = g_matmul_mode == OT_MATMUL_SPLIT_BF16;
+    void (*kern)(WgradArgs) =
+        split ? (a_xform == OT_AX_NONE      ? wgrad_split_kernel<OT_AX_NONE>
+                 : a_xform == OT_AX_RMSNORM ? wgrad_split_kernel<OT_AX_RMSNORM>
+                 : a_xform == OT_AX_GELU    ? wgrad_split_kernel<OT_AX_GELU>
+                                            : wgrad_split_kernel<-1>)
+              : (a_xform == OT_AX_NONE      ? wgrad_kernel<OT_AX_NONE>
+                 : a_xform == OT_AX_RMSNORM ? wgrad_kernel<OT_AX_RMSNORM>
+                 : a_xform == OT_AX_GELU    ? wgrad_kernel<OT_AX_GELU>
+                                            : wgrad_kernel<-1>);
+    const size_t split_shmem = 2 * WSOP;
     static std::once_flag lds_once;
     std::call_once(lds_once, [] {
       for (void (*k)(WgradArgs) : {wgrad_kernel<OT_AX_NONE>, wgrad_kernel<OT_AX_RMSNORM>, wgrad_kernel<OT_AX_GELU>,
@@ -1038,7 +1236,7 @@ extern "C" int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * WBR * WLD * 4);
       (void)hipGetLastError();
     });
-    hipLaunchKernelGGL(kern, dim3((unsigned)nchunks * p.ntk * p.ntn), dim3(256), shmem, s, p);
+    hipLaunchKernelGGL(kern, dim3((unsigned)nchunks * p.ntk * p.ntn), dim3(256), split ? split_shmem : shmem, s, p);
     OT_LAUNCH_CHECK("ot_mixed_gemm_wgrad");
   }
   dim3 rg(ceil_div((int64_t)K * N / 4, 16), ngroups);

@@ -153,7 +153,7 @@ def test_mixed_gemm_prologue_epilogue(dev, matmul):
 
 
 @pytest.mark.parametrize('xf', [OT_AX_NONE, OT_AX_RMSNORM, OT_AX_GELU])
-def test_wgrad(dev, xf):
+def test_wgrad(dev, matmul, xf):
     rng = np.random.default_rng(2)
     G, M, K_, N = 3, 1500, 128, 192
     counts = [1000, 300, 200]

@@ -20,7 +20,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-FAMILIES = {'gemm': ('mixed_gemm_kernel', 'wgrad_kernel'), 'attention': ('attn_',)}
+FAMILIES = {'gemm': ('mixed_gemm_kernel', 'wgrad_kernel', 'wgrad_split_kernel'), 'attention': ('attn_',)}
 
 
 def run_pass(counter, outdir, prog):

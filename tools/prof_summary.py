@@ -16,9 +16,9 @@ for r in rows:
 print(f'| **total** | | | {tot/1e6/steps:.3f} | 100 |')
 # the bench's roofline family (mixed_gemm_kernel + wgrad_kernel): average launch, to compare with
 # bench.py's roofline.avg_launch_us
-fam = [r for r in rows if 'mixed_gemm_kernel' in r['Name'] or 'wgrad_kernel<' in r['Name']]
+fam = [r for r in rows if 'mixed_gemm_kernel' in r['Name'] or ('wgrad_kernel<' in r['Name'] or 'wgrad_split_kernel<' in r['Name'])]
 ft, fn = sum(float(r['TotalDurationNs']) for r in fam), sum(int(r['Calls']) for r in fam)
 if fn:
-    print(f'\nGEMM family (mixed_gemm_kernel + wgrad_kernel): {fn / steps:.1f} launches/step, '
+    print(f'\nGEMM family (mixed_gemm_kernel + wgrad[_split]_kernel): {fn / steps:.1f} launches/step, '
           f'avg {ft / fn / 1e3:.1f} us/launch, {ft / 1e6 / steps:.3f} ms/step')
 

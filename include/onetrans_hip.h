@@ -21,7 +21,8 @@
  *  - Dropout masks are counter-based: element (token t, column n) of site s is kept iff
  *    fmix32((t*width + n) * 0x9E3779B1 + seed ^ s * 0x85EBCA77) >= rate * 2^32, kept values are
  *    scaled by 1/(1-rate).  A compacted tail row r (the last K of I tokens per sample) maps to
- *    token t = (r / K) * I + (I - K) + r % K.
+ *    token t = (r / K) * I + (I - K) + r % K, or, when a kept-position map `tail_pos` [B*K]
+ *    from ot_pyramid_select is passed, t = (r / K) * I + tail_pos[r].
  */
 #ifndef ONETRANS_HIP_H
 #define ONETRANS_HIP_H
@@ -90,7 +91,7 @@ int ot_mixed_gemm(int mode, const float* A, int64_t lda, int K, const int32_t* i
                   const float* res, int64_t ldres, int res_tok,
                   const float* aux, int64_t ldaux,
                   uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
-                  void* stream);
+                  const int32_t* tail_pos, void* stream);
 /* Row-norm epilogue operands for ot_mixed_gemm_rms.  Replaces the RMSNorm layers around the GEMMs
  * (model.py:11-23 RMSNorm, applied at 191/196; their tape gradients): the forward GEMM producing the
  * residual stream emits the next norm's rstd, the dgrad GEMM feeding a norm applies its backward. */
@@ -100,6 +101,7 @@ typedef struct ot_rms_epilogue {
   const float* gamma; const float* rstd;               /*   gamma[N], rstd[out_row] */
   const float* dres; int64_t lddres;                   /*   + dres (row out_row, or through the tail map */
   int dres_tail_K, dres_tail_I;                        /*     b*I+p -> b*K+(p-(I-K)) when dres_tail_K > 0) */
+  const int32_t* dres_tail_inv;                        /*     or b*I+p -> inv[b*I+p] (ot_pyramid_select) */
   float* dx_masked; int64_t lddxm;                     /*   with OT_EPI_DROPOUT: GEMM seed/site/rate/tail */
   float* dgamma; int accumulate_dgamma;                /*   dgamma (+)= sum_rows dy * x * rstd */
   void* workspace; size_t ws_bytes;                    /*   ot_mixed_gemm_rms_workspace_size(ntiles, N) */
@@ -114,7 +116,7 @@ int ot_mixed_gemm_rms(int mode, const float* A, int64_t lda, int K, const int32_
                       const float* res, int64_t ldres, int res_tok,
                       const float* aux, int64_t ldaux,
                       uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
-                      const ot_rms_epilogue* rms, void* stream);
+                      const int32_t* tail_pos, const ot_rms_epilogue* rms, void* stream);
 
 /* dW[g] (+)= sum pro(A[a_rows])^T D[d_rows], db[g] (+)= sum D[d_rows] over the rows of every
  * chunk of group g.  chunks: [nchunks][3] {group, row_begin, row_count} indexing the row maps;
@@ -137,14 +139,29 @@ int ot_transpose_banks(const float* src, float* dst, const int64_t* banks_dev, i
 /* ---- causal attention with a query tail (attention.hip) ----------------------------------
  * Replaces model.py:100-114 (einsum QK^T/sqrt(hd), band_part mask with -1e9, softmax, einsum PV)
  * and the pyramid gather of queries model.py:356/371 (only the last K of I queries computed).
- * qkv: [B*I, ld] (q | k | v, head h at +h*head_dim); out: [B*K, H*head_dim]; lse: [B, H, K]. */
-int ot_attn_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, int head_dim,
-                float* out, float* lse, void* stream);
-/* dqkv: like qkv (dq written on the K tail rows only; dk, dv on all rows);
+ * qkv: [B*I, ld] (q | k | v, head h at +h*head_dim); out: [B*K, H*head_dim]; lse: [B, H, K].
+ * qpos: NULL (query j of a sample sits at position I - K + j) or the ascending kept positions
+ * [B*K] of ot_pyramid_select (query j at qpos[b*K + j], causal limit key <= qpos). */
+int ot_attn_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos,
+                int head_dim, float* out, float* lse, void* stream);
+/* dqkv: like qkv (dq written on the K kept query rows only; dk, dv on all rows);
  * ws: ot_attn_bwd_workspace_size(B, H, K) bytes (row stats padded to 32 queries per (b, h)) */
 size_t ot_attn_bwd_workspace_size(int B, int H, int K);
 int ot_attn_bwd(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
-                int B, int H, int I, int K, int head_dim, float* dqkv, float* delta_ws, void* stream);
+                int B, int H, int I, int K, const int32_t* qpos, int head_dim, float* dqkv, float* delta_ws,
+                void* stream);
+
+/* ---- pyramid query selection (pyramid.hip) -----------------------------------------------
+ * Replaces PyramidScheduler.get_layer_config + tf.gather (model.py:287-302, 356, 371): per sample,
+ * keep the K of I tokens with the largest key (score[b*I+p] * score_sign, ties to the later
+ * position), the last `nforce` (<= K) positions always kept, positions emitted ascending.  score NULL =
+ * every score equal = the reference's tail slice (range(I-K, I), D2-fixed).  One wavefront per
+ * sample: bitwise radix select of the K-th key by ballot/popcount, ordered compaction by mbcnt.
+ * pos [B*K]: kept positions; inv [B*I] (optional): compact row b*K+j of token row b*I+p, or -1;
+ * map_rows (optional): map_rows[b*map_per_sample + j] = b*I + pos[b*K+j] for j < map_per_sample
+ * (rewrites the shared-group part of a tail row map, layout.layer_maps).  I <= 4096. */
+int ot_pyramid_select(const float* score, float score_sign, int B, int I, int K, int nforce,
+                      int32_t* pos, int32_t* inv, int32_t* map_rows, int map_per_sample, void* stream);
 
 /* ---- row-wise kernels (rowwise.hip) -------------------------------------------------------
  * RMSNorm model.py:19-23 (forward writes rstd, and y only when asked: the output norm
@@ -156,12 +173,13 @@ size_t ot_rmsnorm_bwd_workspace_size(int64_t rows, int d);
  * rows (last dres_tail_K of every dres_tail_I rows of x); the other rows get no residual term. */
 int ot_rmsnorm_bwd(const float* dy, int64_t lddy, const float* x, int64_t ldx, const float* gamma,
                    const float* rstd, const float* dres, int64_t lddres, int dres_tail_K, int dres_tail_I,
-                   float* dx, int64_t lddx,
+                   const int32_t* dres_tail_inv, float* dx, int64_t lddx,
                    float* dx_masked, int64_t lddxm, uint32_t seed, uint32_t site, float drop_rate,
-                   int tail_K, int tail_I, float* dgamma, int accumulate_dgamma, int64_t rows, int d,
+                   int tail_K, int tail_I, const int32_t* tail_pos, float* dgamma, int accumulate_dgamma, int64_t rows, int d,
                    void* workspace, size_t ws_bytes, void* stream);
 int ot_dropout_apply(const float* src, int64_t lds, float* dst, int64_t ldd, int64_t rows, int d,
-                     uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I, void* stream);
+                     uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
+                     const int32_t* tail_pos, void* stream);
 size_t ot_rows_colsum_workspace_size(int64_t nrows, int ncols);
 int ot_rows_colsum(const float* src, int64_t ld, const int32_t* rows, int64_t nrows, int ncols,
                    float* out, int accumulate, void* workspace, size_t ws_bytes, void* stream);

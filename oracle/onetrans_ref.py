@@ -49,7 +49,9 @@ def dropout_scale(seed: int, site: int, B: int, I: int, d: int, positions: np.nd
                   rate: float, dtype) -> Tensor:
     """Scale factors (0 or 1/(1-rate)) for rows (b, p in positions) of site ``site``."""
     b = np.arange(B, dtype=np.uint64)[:, None, None]
-    p = positions.astype(np.uint64)[None, :, None]
+    positions = np.asarray(positions)
+    p = (positions.astype(np.uint64)[None, :, None] if positions.ndim == 1      # same for every sample
+         else positions.astype(np.uint64)[:, :, None])                          # [B, K] per sample
     n = np.arange(d, dtype=np.uint64)[None, None, :]
     idx = (b * np.uint64(I) + p) * np.uint64(d) + n
     keep = km.dropout_keep(seed, site, idx, rate)
@@ -138,10 +140,32 @@ def block_literal(P, cfg, l: int, x: Tensor, training: bool, seed: int) -> Tenso
     return x + apply_dropout(f, training, rate, seed, 2 * l + 1, I, allpos)
 
 
-def block_vectorized(P, cfg, l: int, x: Tensor, keep: int, training: bool, seed: int) -> Tensor:
+def select_positions(cfg, x: Tensor, keep: int) -> Optional[np.ndarray]:
+    """Kept positions of a pyramid layer, [B, keep] ascending, or None for the reference's tail
+    (model.py:296, 371).  ``pyramid_select='norm'`` (build extension, ot_pyramid_select): the last
+    min(L_NS, keep) positions (the NS tokens) plus the other positions of largest mean(x^2), ties to
+    the later position."""
+    if getattr(cfg, 'pyramid_select', 'tail') == 'tail':
+        return None
+    B, I, _ = x.shape
+    nf = min(cfg.num_ns_tokens, keep)
+    ms = torch.mean(x.detach().double() ** 2, dim=-1).numpy()
+    out = np.empty((B, keep), dtype=np.int64)
+    pos = np.arange(I - nf)
+    for b in range(B):
+        order = np.lexsort((pos, ms[b, :I - nf]))          # ascending by (score, position)
+        pick = order[len(order) - (keep - nf):] if keep > nf else order[:0]
+        out[b] = np.sort(np.concatenate([pick, np.arange(I - nf, I)]))
+    return out
+
+
+def block_vectorized(P, cfg, l: int, x: Tensor, keep: int, training: bool, seed: int,
+                     sel: Optional[np.ndarray] = None) -> Tensor:
     """Same math, grouped einsums, only the last ``keep`` queries (their outputs are
     identical to the literal block's tail because attention is causal and FFN/residual
-    are per token)."""
+    are per token).  ``sel`` [B, keep]: per-sample kept positions instead of the tail."""
+    if sel is not None:
+        return _block_selected(P, cfg, l, x, sel, training, seed)
     B, I, d = x.shape
     H = cfg.num_heads
     hd = d // H
@@ -168,6 +192,36 @@ def block_vectorized(P, cfg, l: int, x: Tensor, keep: int, training: bool, seed:
     return xt + apply_dropout(f, training, rate, seed, 2 * l + 1, I, tail)
 
 
+def _block_selected(P, cfg, l: int, x: Tensor, sel: np.ndarray, training: bool, seed: int) -> Tensor:
+    """block_vectorized for per-sample kept positions sel [B, K] (ascending): queries, residuals,
+    weight groups and dropout rows follow each kept token's position in the layer input."""
+    B, I, d = x.shape
+    K = sel.shape[1]
+    H = cfg.num_heads
+    hd = d // H
+    rate = cfg.dropout_rate
+    groups = torch.tensor([cfg.group_of_position(i, I) for i in range(I)])
+    st = torch.from_numpy(sel)
+    gt = groups[st]                                          # [B, K]
+    bidx = torch.arange(B)[:, None]
+    xn = rmsnorm(x, P[f'blk.{l}.norm1'])
+    W = P[f'blk.{l}.wqkv']
+    kv = torch.einsum('bid,ide->bie', xn, W[groups][:, :, d:])
+    q = torch.einsum('bjd,bjde->bje', xn[bidx, st], W[gt][..., :d])
+    k, v = kv[..., :d], kv[..., d:]
+    qh = q.reshape(B, K, H, hd); kh = k.reshape(B, I, H, hd); vh = v.reshape(B, I, H, hd)
+    s = torch.einsum('bqhd,bkhd->bhqk', qh, kh) / math.sqrt(hd)
+    mask = torch.arange(I)[None, None, None, :] <= st[:, None, :, None]
+    s = torch.where(mask, s, torch.tensor(-1e9, dtype=s.dtype))
+    o = torch.einsum('bhqk,bkhd->bqhd', torch.softmax(s, -1), vh).reshape(B, K, d)
+    a = o @ P[f'blk.{l}.wo']
+    xt = x[bidx, st] + apply_dropout(a, training, rate, seed, 2 * l, I, sel)
+    xn2 = rmsnorm(xt, P[f'blk.{l}.norm2'])
+    h = gelu(torch.einsum('bjd,bjdf->bjf', xn2, P[f'blk.{l}.w1'][gt]) + P[f'blk.{l}.b1'][gt])
+    f = torch.einsum('bjf,bjfd->bjd', h, P[f'blk.{l}.w2'][gt]) + P[f'blk.{l}.b2'][gt]
+    return xt + apply_dropout(f, training, rate, seed, 2 * l + 1, I, sel)
+
+
 # ----------------------------------------------------------------------------- model
 def forward(P, cfg, ns, seq, training: bool = False, seed: int = 0,
             variant: str = 'vectorized') -> Dict[str, Dict[str, Tensor]]:
@@ -180,11 +234,15 @@ def forward(P, cfg, ns, seq, training: bool = False, seed: int = 0,
     for l, s in enumerate(sched):
         I, keep = s['in_len'], s['keep']
         assert x.shape[1] == I
+        sel = select_positions(cfg, x, keep) if (l < nl - 1 and keep < I) else None
         if variant == 'literal':
             y = block_literal(P, cfg, l, x, training, seed)
-            x = y[:, I - keep:]                             # model.py:371 (D2-fixed indices)
+            if sel is None:
+                x = y[:, I - keep:]                         # model.py:371 (D2-fixed indices)
+            else:
+                x = y[torch.arange(x.shape[0])[:, None], torch.from_numpy(sel)]
         else:
-            x = block_vectorized(P, cfg, l, x, keep if l < nl - 1 else 1, training, seed)
+            x = block_vectorized(P, cfg, l, x, keep if l < nl - 1 else 1, training, seed, sel=sel)
     out = rmsnorm(x, P['out_norm'])                         # model.py:384
     last = out[:, -1, :]                                    # model.py:390
     probs, logits = {}, {}

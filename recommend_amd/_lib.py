@@ -29,6 +29,7 @@ class RmsEpilogue(ctypes.Structure):
     _fields_ = [('rstd_out', c_void_p), ('eps', c_float),
                 ('x', c_void_p), ('ldx', c_int64), ('gamma', c_void_p), ('rstd', c_void_p),
                 ('dres', c_void_p), ('lddres', c_int64), ('dres_tail_K', c_int), ('dres_tail_I', c_int),
+                ('dres_tail_inv', c_void_p),
                 ('dx_masked', c_void_p), ('lddxm', c_int64),
                 ('dgamma', c_void_p), ('accumulate_dgamma', c_int),
                 ('workspace', c_void_p), ('ws_bytes', c_size_t)]
@@ -45,23 +46,24 @@ SIGNATURES = {
     'ot_get_matmul_mode': (c_int, []),
     'ot_mixed_gemm': (c_int, [c_int, P, I64, c_int, P, c_int, P, P, P, I64, I64, c_int, P, c_int, P, I64,
                               P, I64, P, c_int, P, I64, c_int, P, I64, c_uint32, c_uint32, c_float, c_int,
-                              c_int, P]),
+                              c_int, P, P]),
     'ot_mixed_gemm_rms_workspace_size': (c_size_t, [c_int, c_int]),
     'ot_mixed_gemm_rms': (c_int, [c_int, P, I64, c_int, P, c_int, P, P, P, I64, I64, c_int, P, c_int, P, I64,
                                   P, I64, P, c_int, P, I64, c_int, P, I64, c_uint32, c_uint32, c_float, c_int,
-                                  c_int, P, P]),
+                                  c_int, P, P, P]),
     'ot_wgrad_workspace_size': (c_size_t, [c_int, c_int, c_int]),
     'ot_mixed_gemm_wgrad': (c_int, [P, I64, P, c_int, P, P, P, I64, P, c_int, c_int, P, c_int, P, c_int, P,
                                     I64, P, I64, c_int, P, c_size_t, P]),
     'ot_transpose_banks': (c_int, [P, P, P, c_int, I64, P]),
-    'ot_attn_fwd': (c_int, [P, I64, c_int, c_int, c_int, c_int, c_int, P, P, P]),
+    'ot_attn_fwd': (c_int, [P, I64, c_int, c_int, c_int, c_int, P, c_int, P, P, P]),
     'ot_attn_bwd_workspace_size': (c_size_t, [c_int, c_int, c_int]),
-    'ot_attn_bwd': (c_int, [P, I64, P, P, P, c_int, c_int, c_int, c_int, c_int, P, P, P]),
+    'ot_attn_bwd': (c_int, [P, I64, P, P, P, c_int, c_int, c_int, c_int, P, c_int, P, P, P]),
+    'ot_pyramid_select': (c_int, [P, c_float, c_int, c_int, c_int, c_int, P, P, P, c_int, P]),
     'ot_rmsnorm_fwd': (c_int, [P, I64, P, P, I64, P, I64, c_int, c_float, P]),
     'ot_rmsnorm_bwd_workspace_size': (c_size_t, [I64, c_int]),
-    'ot_rmsnorm_bwd': (c_int, [P, I64, P, I64, P, P, P, I64, c_int, c_int, P, I64, P, I64, c_uint32,
-                               c_uint32, c_float, c_int, c_int, P, c_int, I64, c_int, P, c_size_t, P]),
-    'ot_dropout_apply': (c_int, [P, I64, P, I64, I64, c_int, c_uint32, c_uint32, c_float, c_int, c_int, P]),
+    'ot_rmsnorm_bwd': (c_int, [P, I64, P, I64, P, P, P, I64, c_int, c_int, P, P, I64, P, I64, c_uint32,
+                               c_uint32, c_float, c_int, c_int, P, P, c_int, I64, c_int, P, c_size_t, P]),
+    'ot_dropout_apply': (c_int, [P, I64, P, I64, I64, c_int, c_uint32, c_uint32, c_float, c_int, c_int, P, P]),
     'ot_rows_colsum_workspace_size': (c_size_t, [I64, c_int]),
     'ot_rows_colsum': (c_int, [P, I64, P, I64, c_int, P, c_int, P, c_size_t, P]),
     'ot_ns_assemble': (c_int, [P, c_int, P, c_int, P, I64, P]),

@@ -15,6 +15,12 @@ literal semantics and the fixes recorded in DESIGN.md §Semantics:
   layer 1 on; the fix indexes against the current length ``I_l`` and caps
   ``keep_l`` at ``I_l``.  With the fix off, an out-of-range schedule raises
   ``IndexError`` (TF's CPU behaviour for the same gather).
+* ``pyramid_select`` — which queries a pyramid layer keeps.  ``'tail'`` is the
+  reference's static tail slice (``model.py:296, 371``); ``'norm'`` (build
+  extension) keeps the NS tokens plus the S tokens of largest RMS (top-K per
+  sample, ``ot_pyramid_select``), which needs ``dedicated_positions='tail'`` so
+  the dedicated (NS) rows stay at fixed places.  Both run the same wavefront
+  top-K kernel; 'tail' passes no score, so the position tie-break picks the tail.
 * ``sparse_features`` / ``seq_item_vocab`` — the Criteo-shape embedding-gather
   extension (north_star): NS features named here carry int64 ids looked up in a
   per-field table of width ``ns_embedding_dim``; sequence features carry int64
@@ -84,6 +90,7 @@ class OneTransConfig:
         # ---- build knobs (not in the reference) ----
         self.dedicated_positions = 'head'    # build: 'head' (ref model.py:69) | 'tail' (paper eq.12)
         self.pyramid_fix = True              # build: index pyramid against the current length
+        self.pyramid_select = 'tail'         # build: 'tail' (ref model.py:296) | 'norm' (top-K by token RMS)
         self.seq_feature_dim = 64            # build: width of one sequence event (data_loader.py:146,322)
         self.ns_embedding_dim = 16           # build: per-field NS embedding width (Criteo shape)
         self.sparse_features: Dict[str, int] = {}   # build: NS id features -> cardinality
@@ -226,6 +233,16 @@ def _criteo_features(cfg: OneTransConfig, seq_lens: List[int], item_vocab: int) 
     cfg.sparse_features = {name: card for name, card in zip(sparse, CRITEO_CARDINALITIES)}
     cfg.seq_item_vocab = item_vocab
     cfg._seq_lens = list(seq_lens)
+
+
+def check_pyramid_select(cfg: OneTransConfig) -> None:
+    """``pyramid_select`` is 'tail' (reference) or 'norm' (needs the NS tokens at the dedicated tail)."""
+    sel = getattr(cfg, 'pyramid_select', 'tail')
+    if sel not in ('tail', 'norm'):
+        raise ValueError(f'unknown pyramid_select {sel!r}')
+    if sel == 'norm' and cfg.dedicated_positions != 'tail':
+        raise ValueError("pyramid_select='norm' needs dedicated_positions='tail' (the kept NS rows keep their "
+                         "dedicated weights)")
 
 
 def workload_config(name: str) -> OneTransConfig:

@@ -41,7 +41,11 @@ struct AttnArgs {
   const float* o; const float* dout; float* out; float* lse; float* dqkv; float* delta;
   int B, H, I, K;
   float scale;
+  const int32_t* qpos;      // kept query positions [B*K] (ot_pyramid_select) or null: I - K + j
 };
+
+// position of kept query j (< K) of the sample whose qpos slice is qp (null: the tail rule)
+__device__ __forceinline__ int query_pos(const int32_t* qp, int q_off, int j) { return qp ? qp[j] : q_off + j; }
 
 __device__ __forceinline__ int acc_row(int r, int hh) { return (r & 3) + 8 * (r >> 2) + 4 * hh; }
 
@@ -152,14 +156,14 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs p) {
   const float* Q = p.qkv + (int64_t)b * I * p.ld + h * HD;
   const float* Kp = Q + p.d;
   const float* V = Q + 2 * p.d;
-  const float* Qt = Q + (int64_t)q_off * p.ld;      // tail rows
+  const int32_t* qp = p.qpos ? p.qpos + (int64_t)b * K : nullptr;
   const int nqb = (K + 31) / 32;
   const float qscale = p.scale * 1.4426950408889634f;   // log2(e) / sqrt(hd)
   for (int qb = 0; qb < nqb; ++qb) {
-    const int j = 32 * qb + li;                     // this lane's query (tail index)
-    const int qpos = q_off + (j < K ? j : K - 1);
+    const int j = 32 * qb + li;                     // this lane's query (kept index)
+    const int qpos = query_pos(qp, q_off, j < K ? j : K - 1);
     float qf[HD / 2];
-    load_frag_clamped<HD>(qf, Qt, p.ld, j, K, hh);
+    load_frag_clamped<HD>(qf, Q, p.ld, qpos, I, hh);
 #pragma unroll
     for (int s = 0; s < HD / 2; ++s) qf[s] *= qscale;
     f32x16 oacc[NB(HD)];
@@ -168,9 +172,9 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) oacc[c][r] = 0.f;
     float m = -INFINITY, l = 0.f;
-    const int last_q = q_off + min(32 * qb + 31, K - 1);
+    const int last_q = query_pos(qp, q_off, min(32 * qb + 31, K - 1));   // positions ascend
     const int nkb = last_q / 32 + 1;
-    const int first_masked = (q_off + 32 * qb) / 32;     // key blocks >= this one may be masked
+    const int first_masked = query_pos(qp, q_off, 32 * qb) / 32;       // key blocks >= this may be masked
     for (int kb = 0; kb < nkb; ++kb) {
       const int key0 = 32 * kb;
       float kf[HD / 2], vf[HD / 2];
@@ -260,7 +264,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kv_kernel(AttnArgs p) {
     *reinterpret_cast<f32x4*>(Vs + row * LD + c) = vvv;
   }
   __syncthreads();
-  const float* Qt = Q + (int64_t)q_off * p.ld;
+  const int32_t* qp = p.qpos ? p.qpos + (int64_t)b * K : nullptr;
   const int nqb = (K + 31) / 32;
   const float qscale = p.scale * 1.4426950408889634f;   // log2(e) / sqrt(hd)
   for (int i = 0; i < nqb; ++i) {
@@ -268,9 +272,9 @@ __global__ __launch_bounds__(256) void attn_fwd_kv_kernel(AttnArgs p) {
     if (slot != wave) continue;
     const int qb = nqb - 1 - i;
     const int j = 32 * qb + li;
-    const int qpos = q_off + (j < K ? j : K - 1);
+    const int qpos = query_pos(qp, q_off, j < K ? j : K - 1);
     float qf[HD / 2];
-    load_frag<HD>(qf, Qt, p.ld, j, K, hh);
+    load_frag<HD>(qf, Q, p.ld, j < K ? qpos : I, I, hh);           // rows >= I: zeros
 #pragma unroll
     for (int s2 = 0; s2 < HD / 2; ++s2) qf[s2] *= qscale;
     f32x16 oacc[NB(HD)];
@@ -279,9 +283,9 @@ __global__ __launch_bounds__(256) void attn_fwd_kv_kernel(AttnArgs p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) oacc[c][r] = 0.f;
     float m = -INFINITY, l = 0.f;
-    const int last_q = q_off + min(32 * qb + 31, K - 1);
+    const int last_q = query_pos(qp, q_off, min(32 * qb + 31, K - 1));
     const int nkb = last_q / 32 + 1;
-    const int first_masked = (q_off + 32 * qb) / 32;
+    const int first_masked = query_pos(qp, q_off, 32 * qb) / 32;
     for (int kb = 0; kb < nkb; ++kb) {
       const int key0 = 32 * kb;
       float kf[HD / 2];
@@ -339,15 +343,26 @@ __global__ __launch_bounds__(256) void attn_fwd_kv_kernel(AttnArgs p) {
 // kernel reads them as aligned float4 without bounds checks:
 //   ws[0 .. BH*KP)       lse  (padding +inf: P = exp(s - inf) = 0 masks the padded queries)
 //   ws[BH*KP .. 2*BH*KP) delta[b,h,j] = sum_d dO[b*K+j][h*hd+d] * O[b*K+j][h*hd+d]   (padding 0)
+//   (int) ws[2*BH*KP .. +B*KP) kept query positions qpos[b][j] padded with qpos[b][K-1] (only
+//   when a selection map is given: the selected-query backward reads them as aligned int4)
 // Threads of the first `main` blocks take one float4 of [B*K, d] each (coalesced rows), reduced over
 // the hd/4 lanes of a head with shuffles; the remaining blocks fill the padding.
 __host__ __device__ constexpr int attn_kpad(int K) { return (K + 31) / 32 * 32; }
 
 __global__ __launch_bounds__(256) void attn_bwd_prep_kernel(const float* __restrict__ o, const float* __restrict__ dout,
                                                             const float* __restrict__ lse, float* ws, int B, int H,
-                                                            int K, int hd, int main_blocks) {
+                                                            int K, int hd, int main_blocks, int pad_blocks,
+                                                            const int32_t* __restrict__ qpos) {
   const int d = H * hd, KP = attn_kpad(K);
   const int64_t BHKP = (int64_t)B * H * KP;
+  if ((int)blockIdx.x >= main_blocks + pad_blocks) {
+    const int64_t e = ((int64_t)blockIdx.x - main_blocks - pad_blocks) * blockDim.x + threadIdx.x;   // [B][KP]
+    if (!qpos || e >= (int64_t)B * KP) return;
+    const int64_t b = e / KP;
+    const int j = (int)(e % KP);
+    reinterpret_cast<int32_t*>(ws + 2 * BHKP)[e] = qpos[b * K + (j < K ? j : K - 1)];
+    return;
+  }
   if ((int)blockIdx.x >= main_blocks) {
     const int pad = KP - K;
     const int64_t e = ((int64_t)blockIdx.x - main_blocks) * blockDim.x + threadIdx.x;   // [B*H][pad]
@@ -392,7 +407,8 @@ __global__ __launch_bounds__(256) void attn_bwd_prep_kernel(const float* __restr
 template <int HD>
 constexpr int BWD_WAVES() { return HD >= 128 ? 2 : 4; }
 
-template <int HD>
+// SEL: queries at selected positions (p.qpos, padded copy in the workspace) instead of the tail.
+template <int HD, bool SEL>
 __global__ __launch_bounds__(64 * BWD_WAVES<HD>(), 2) void attn_bwd_kernel(AttnArgs p) {
   constexpr int LD = TLD<HD>();
   constexpr int SLD = 36;                  // dS tile row stride (32 keys + pad)
@@ -416,6 +432,7 @@ __global__ __launch_bounds__(64 * BWD_WAVES<HD>(), 2) void attn_bwd_kernel(AttnA
   const float* V = Q + 2 * p.d;
   const float* Qt = Q + (int64_t)q_off * p.ld;
   const float* dO = p.dout + (int64_t)b * K * p.d + h * HD;
+  const int32_t* qpp = reinterpret_cast<const int32_t*>(p.delta + 2 * (int64_t)p.B * p.H * KP) + (int64_t)b * KP;
   const float* lsep = p.delta + (int64_t)pair * KP;                              // padded lse
   const float* dltp = p.delta + ((int64_t)p.B * p.H + pair) * KP;                // padded delta
   float* dQt = p.dqkv + (tok0 + q_off) * p.ld + h * HD;
@@ -436,10 +453,17 @@ __global__ __launch_bounds__(64 * BWD_WAVES<HD>(), 2) void attn_bwd_kernel(AttnA
     for (int c = 0; c < NB(HD); ++c)
 #pragma unroll
       for (int r = 0; r < 16; ++r) { dk[c][r] = 0.f; dv[c][r] = 0.f; }
-    int qb0 = key0 - q_off; qb0 = qb0 < 0 ? 0 : qb0 / 32;      // first query block that sees key0
+    int qb0;                                           // first query block that sees key0
+    if constexpr (SEL) {
+      qb0 = 0;
+      while (qb0 < nqb - 1 && qpp[32 * qb0 + 31] < key0) ++qb0;   // ascending positions, padded
+    } else {
+      qb0 = key0 - q_off; qb0 = qb0 < 0 ? 0 : qb0 / 32;
+    }
     float qf[HD / 2], of[HD / 2];
     auto load_qblock = [&](int q0) {
-      BWD_LOAD<HD>(qf, Qt, p.ld, q0 + li, K, hh);
+      if constexpr (SEL) BWD_LOAD<HD>(qf, Q, p.ld, q0 + li < K ? qpp[q0 + li] : I, I, hh);
+      else BWD_LOAD<HD>(qf, Qt, p.ld, q0 + li, K, hh);
       BWD_LOAD<HD>(of, dO, p.d, q0 + li, K, hh);
     };
     load_qblock(32 * qb0);
@@ -449,14 +473,17 @@ __global__ __launch_bounds__(64 * BWD_WAVES<HD>(), 2) void attn_bwd_kernel(AttnA
     for (int qb = qb0; qb < nqb; ++qb) {
       const int q0 = 32 * qb;
       f32x4 l4[4], d4[4];
+      i32x4 qv4[SEL ? 4 : 1];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         l4[g] = *reinterpret_cast<const f32x4*>(lsep + q0 + 8 * g + 4 * hh);
         d4[g] = *reinterpret_cast<const f32x4*>(dltp + q0 + 8 * g + 4 * hh);
+        if constexpr (SEL) qv4[g] = *reinterpret_cast<const i32x4*>(qpp + q0 + 8 * g + 4 * hh);
       }
       // dQ^T block: lane = query q0 + li, register r = dim 32c + acc_row(r, hh) (4 float4 per lane)
       const int jq = q0 + li;
-      float* dqrow = dQt + (int64_t)(jq < K ? jq : K - 1) * p.ld + 4 * hh;
+      float* dqrow = SEL ? p.dqkv + (tok0 + qpp[jq]) * p.ld + h * HD + 4 * hh
+                         : dQt + (int64_t)(jq < K ? jq : K - 1) * p.ld + 4 * hh;
       f32x16 dq[NB(HD)];
 #pragma unroll
       for (int c = 0; c < NB(HD); ++c)
@@ -479,7 +506,8 @@ __global__ __launch_bounds__(64 * BWD_WAVES<HD>(), 2) void attn_bwd_kernel(AttnA
         for (int e = 0; e < 4; ++e) {
           const int r = 4 * g + e, j = q0 + 8 * g + 4 * hh + e;
           const float ex = __expf(s[r] * p.scale - l4[g][e]);
-          const float P = kpos <= q_off + j ? ex : 0.f;
+          const int qposj = SEL ? qv4[SEL ? g : 0][e] : q_off + j;
+          const float P = kpos <= qposj ? ex : 0.f;
           s[r] = P;
           dp[r] = P * (dp[r] - d4[g][e]) * p.scale;    // dS, pre-scaled by 1/sqrt(hd)
           tS[(8 * g + 4 * hh + e) * SLD + li] = dp[r];
@@ -583,14 +611,17 @@ __global__ __launch_bounds__(256) void attn_bwd_small_kernel(AttnArgs p) {
   const float* V = Q + 2 * p.d;
   float* dK = p.dqkv + tok0 * p.ld + p.d + h * HD + 4 * sub;
   float* dV = dK + p.d;
+  const int32_t* qp = p.qpos ? p.qpos + (int64_t)b * K : nullptr;
   f32x4 q[SMALL_K], o[SMALL_K], dq[SMALL_K];
   float lse[SMALL_K], delta[SMALL_K];
+  int qpos[SMALL_K];
 #pragma unroll
   for (int j = 0; j < SMALL_K; ++j) {
     const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-    q[j] = z; o[j] = z; dq[j] = z; lse[j] = 0.f; delta[j] = 0.f;
+    q[j] = z; o[j] = z; dq[j] = z; lse[j] = 0.f; delta[j] = 0.f; qpos[j] = -1;
     if (j < K) {
-      q[j] = *reinterpret_cast<const f32x4*>(Q + (int64_t)(q_off + j) * p.ld);
+      qpos[j] = query_pos(qp, q_off, j);
+      q[j] = *reinterpret_cast<const f32x4*>(Q + (int64_t)qpos[j] * p.ld);
       o[j] = *reinterpret_cast<const f32x4*>(p.dout + ((int64_t)b * K + j) * p.d + h * HD + 4 * sub);
       lse[j] = p.delta[(int64_t)pair * attn_kpad(K) + j];
       delta[j] = p.delta[((int64_t)p.B * p.H + pair) * attn_kpad(K) + j];
@@ -613,7 +644,7 @@ __global__ __launch_bounds__(256) void attn_bwd_small_kernel(AttnArgs p) {
         sdot += __shfl_xor(sdot, off, 64);
         pdot += __shfl_xor(pdot, off, 64);
       }
-      const bool vis = live && key <= q_off + j;
+      const bool vis = live && key <= qpos[j];
       const float P = vis ? __expf(sdot * p.scale - lse[j]) : 0.f;
       const float ds = vis ? P * (pdot - delta[j]) * p.scale : 0.f;
       dv += P * o[j];
@@ -634,7 +665,7 @@ __global__ __launch_bounds__(256) void attn_bwd_small_kernel(AttnArgs p) {
       v.x += __shfl_xor(v.x, off, 64); v.y += __shfl_xor(v.y, off, 64);
       v.z += __shfl_xor(v.z, off, 64); v.w += __shfl_xor(v.w, off, 64);
     }
-    if (slot == 0) *reinterpret_cast<f32x4*>(p.dqkv + (tok0 + q_off + j) * p.ld + h * HD + 4 * sub) = v;
+    if (slot == 0) *reinterpret_cast<f32x4*>(p.dqkv + (tok0 + qpos[j]) * p.ld + h * HD + 4 * sub) = v;
   }
 }
 
@@ -651,14 +682,14 @@ using namespace ot;
     default: return fail(OT_ERR_UNSUPPORTED, "attention: head_dim %d unsupported", HD_);     \
   }
 
-extern "C" int ot_attn_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, int head_dim,
-                           float* out, float* lse, void* stream) {
+extern "C" int ot_attn_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos,
+                           int head_dim, float* out, float* lse, void* stream) {
   OT_REQUIRE(qkv && out && lse, "ot_attn_fwd: null operand");
   OT_REQUIRE(B >= 0 && H > 0 && I > 0 && K > 0 && K <= I, "ot_attn_fwd: bad sizes B=%d H=%d I=%d K=%d", B, H, I, K);
   OT_REQUIRE(ld % 4 == 0 && ld >= 3 * H * head_dim, "ot_attn_fwd: ld must be >= 3d and a multiple of 4");
   if (B == 0) return OT_OK;
   AttnArgs p{qkv, ld, H * head_dim, nullptr, nullptr, out, lse, nullptr, nullptr, B, H, I, K,
-             1.f / sqrtf((float)head_dim)};
+             1.f / sqrtf((float)head_dim), qpos};
   const size_t kv_bytes = 2 * (size_t)((I + 31) / 32 * 32) * (head_dim + 4) * sizeof(float);
   if (head_dim <= 64 && kv_bytes <= OT_ATTN_KV_LDS_MAX && (K + 31) / 32 >= 3) {
     // short sequence: K/V of a head staged once in LDS, shared by 4 waves
@@ -683,22 +714,23 @@ extern "C" int ot_attn_fwd(const float* qkv, int64_t ld, int B, int H, int I, in
 }
 
 extern "C" size_t ot_attn_bwd_workspace_size(int B, int H, int K) {
-  return 2 * (size_t)B * H * attn_kpad(K) * sizeof(float);
+  return (2 * (size_t)B * H + B) * attn_kpad(K) * sizeof(float);     // lse, delta (+ padded qpos)
 }
 
 extern "C" int ot_attn_bwd(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
-                           int B, int H, int I, int K, int head_dim, float* dqkv, float* delta_ws,
-                           void* stream) {
+                           int B, int H, int I, int K, const int32_t* qpos, int head_dim, float* dqkv,
+                           float* delta_ws, void* stream) {
   OT_REQUIRE(qkv && out && dout && lse && dqkv && delta_ws, "ot_attn_bwd: null operand");
   OT_REQUIRE(B >= 0 && H > 0 && I > 0 && K > 0 && K <= I, "ot_attn_bwd: bad sizes");
   OT_REQUIRE(ld % 4 == 0 && ld >= 3 * H * head_dim, "ot_attn_bwd: bad ld");
   if (B == 0) return OT_OK;
   AttnArgs p{qkv, ld, H * head_dim, out, dout, nullptr, const_cast<float*>(lse), dqkv, delta_ws, B, H, I, K,
-             1.f / sqrtf((float)head_dim)};
+             1.f / sqrtf((float)head_dim), qpos};
   const int main_blocks = (int)ceil_div((int64_t)B * K * H * head_dim / 4, 256);
   const int pad_blocks = (int)ceil_div((int64_t)B * H * (attn_kpad(K) - K), 256);
-  hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3(main_blocks + pad_blocks), dim3(256), 0, (hipStream_t)stream, out,
-                     dout, lse, delta_ws, B, H, K, head_dim, main_blocks);
+  const int qpos_blocks = qpos ? (int)ceil_div((int64_t)B * attn_kpad(K), 256) : 0;
+  hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3(main_blocks + pad_blocks + qpos_blocks), dim3(256), 0,
+                     (hipStream_t)stream, out, dout, lse, delta_ws, B, H, K, head_dim, main_blocks, pad_blocks, qpos);
   OT_LAUNCH_CHECK("ot_attn_bwd(prep)");
   if (K <= SMALL_K) {
     OT_ATTN_DISPATCH(attn_bwd_small_kernel, head_dim, dim3(ceil_div((int64_t)B * H, 4)), dim3(256), 0,
@@ -706,7 +738,16 @@ extern "C" int ot_attn_bwd(const float* qkv, int64_t ld, const float* out, const
   } else {
     const int waves = head_dim >= 128 ? 2 : 4;
     const unsigned grid = ceil_div((int64_t)B * H, waves);
-    OT_ATTN_DISPATCH(attn_bwd_kernel, head_dim, dim3(grid), dim3(64 * waves), 0, (hipStream_t)stream, p);
+    void (*kern)(AttnArgs) = nullptr;
+    const bool sel = qpos != nullptr;
+    switch (head_dim) {
+      case 16: kern = sel ? attn_bwd_kernel<16, true> : attn_bwd_kernel<16, false>; break;
+      case 32: kern = sel ? attn_bwd_kernel<32, true> : attn_bwd_kernel<32, false>; break;
+      case 64: kern = sel ? attn_bwd_kernel<64, true> : attn_bwd_kernel<64, false>; break;
+      case 128: kern = sel ? attn_bwd_kernel<128, true> : attn_bwd_kernel<128, false>; break;
+      default: return fail(OT_ERR_UNSUPPORTED, "attention: head_dim %d unsupported", head_dim);
+    }
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * waves), 0, (hipStream_t)stream, p);
   }
   OT_LAUNCH_CHECK("ot_attn_bwd");
   return OT_OK;

@@ -10,6 +10,7 @@
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 namespace ot {
 
@@ -41,11 +42,21 @@ __device__ __forceinline__ bool drop_keep(uint32_t seed, uint32_t site, uint32_t
   return fmix32(h) >= thr;
 }
 
-// token index in the layer-input space for compacted tail row r (tail of K out of I per sample)
-__device__ __forceinline__ int64_t tail_token(int64_t r, int K, int I) {
+// token index in the layer-input space for compacted row r of a layer keeping K of I tokens per
+// sample: the tail (p = I - K + j) or, when `pos` is given (ot_pyramid_select), p = pos[r]
+__device__ __forceinline__ int64_t tail_token(int64_t r, int K, int I, const int32_t* pos = nullptr) {
+  if (pos) return (r / K) * I + pos[r];
   if (K == I) return r;
   int64_t b = r / K;
   return b * I + (I - K) + (r - b * K);
+}
+
+// inverse: compact row of input row o (b*I + p), or -1 when p is not kept (`inv` from
+// ot_pyramid_select, else the tail rule)
+__device__ __forceinline__ int64_t kept_row(int64_t o, int K, int I, const int32_t* inv = nullptr) {
+  if (inv) return inv[o];
+  const int64_t b = o / I, j = o - b * I - (I - K);
+  return j >= 0 ? b * K + j : -1;
 }
 
 // erf for the GELU: branch-free rational minimax on [-4, 4] (|error| < 5e-7; erf(±4) rounds to ±1 in

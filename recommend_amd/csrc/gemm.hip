@@ -97,8 +97,9 @@ struct GemmArgs {
   // row-norm epilogues (N == GT: the tile holds whole rows)
   float* rstd_out; float eps;                                   // OT_EPI_ROW_RSTD
   const float* nx; int64_t ldnx; const float* ngamma; const float* nrstd;   // OT_EPI_RMSNORM_BWD
-  const float* dres; int64_t lddres; int dres_K, dres_I;
+  const float* dres; int64_t lddres; int dres_K, dres_I; const int32_t* dres_inv;
   float* dxm; int64_t lddxm; float* dgpart;
+  const int32_t* tail_pos;                      // kept positions (ot_pyramid_select) or null (tail)
 };
 
 // sum over the 32 lanes that hold one output row in the vector epilogue (same order as the
@@ -449,17 +450,13 @@ __global__ __launch_bounds__(256, (NT && SPLT) ? 2 : OT_GEMM_MINWG) void mixed_g
         for (int i = 0; i < RB; ++i) {
           const int orr = orow[hf][i0 + i];
           const int64_t o = orr < 0 ? 0 : orr;
-          tok[i] = (need_tok && orr >= 0) ? tail_token(orr, p.tail_K, p.tail_I) : o;
+          tok[i] = (need_tok && orr >= 0) ? tail_token(orr, p.tail_K, p.tail_I, p.tail_pos) : o;
           if (RMSBWD) {
             x4[i] = *reinterpret_cast<const f32x4*>(p.nx + o * p.ldnx + col);
             nr[i] = p.nrstd[o];
             dr4[i] = f32x4{0.f, 0.f, 0.f, 0.f};
             if (p.dres) {
-              int dr = (int)o;
-              if (p.dres_K > 0) {
-                const int bb = (int)o / p.dres_I, j = (int)o - bb * p.dres_I - (p.dres_I - p.dres_K);
-                dr = j >= 0 ? bb * p.dres_K + j : -1;
-              }
+              const int64_t dr = p.dres_K > 0 ? kept_row(o, p.dres_K, p.dres_I, p.dres_inv) : o;
               if (dr >= 0) dr4[i] = *reinterpret_cast<const f32x4*>(p.dres + (int64_t)dr * p.lddres + col);
             }
           }
@@ -548,7 +545,7 @@ __global__ __launch_bounds__(256, (NT && SPLT) ? 2 : OT_GEMM_MINWG) void mixed_g
       const int row = wm + 32 * m + (r & 3) + 8 * (r >> 2) + 4 * h;
       const int64_t gr = (int64_t)tm * GT + row;
       orow[r] = p.out_rows ? p.out_rows[gr] : (int)gr;
-      tok[r] = (need_tok && orow[r] >= 0) ? tail_token(orow[r], p.tail_K, p.tail_I) : orow[r];
+      tok[r] = (need_tok && orow[r] >= 0) ? tail_token(orow[r], p.tail_K, p.tail_I, p.tail_pos) : orow[r];
     }
     float ld0[16][2];
 #pragma unroll
@@ -1051,6 +1048,7 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
                            const float* res, int64_t ldres, int res_tok,
                            const float* aux, int64_t ldaux,
                            uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
+                           const int32_t* tail_pos,
                            const ot_rms_epilogue* rms, void* stream) {
   OT_REQUIRE(A && W && C, "ot_mixed_gemm: null operand");
   const int rms_flags = epi & (OT_EPI_ROW_RSTD | OT_EPI_RMSNORM_BWD);
@@ -1082,11 +1080,13 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
   GemmArgs p{A, lda, K, in_rows, a_xform, a_rstd, a_gamma, W, w_gstride, ldw, N, tile_group,
              bias, bias_gstride, C, ldc, out_rows, epi, res, ldres, res_tok, aux, ldaux,
              seed, site, 0u, 1.f, tail_K, tail_I, N, ntiles, (int)ceil_div(N, GT)};
+  p.tail_pos = tail_pos;
   float* dgpart = nullptr;
   if (rms_flags) {
     p.rstd_out = rms->rstd_out; p.eps = rms->eps;
     p.nx = rms->x; p.ldnx = rms->ldx; p.ngamma = rms->gamma; p.nrstd = rms->rstd;
     p.dres = rms->dres; p.lddres = rms->lddres; p.dres_K = rms->dres_tail_K; p.dres_I = rms->dres_tail_I;
+    p.dres_inv = rms->dres_tail_inv;
     p.dxm = rms->dx_masked; p.lddxm = rms->lddxm;
     if (epi & OT_EPI_RMSNORM_BWD) {
       // without dgamma the partials still need a home: the caller's workspace or nothing
@@ -1169,10 +1169,10 @@ extern "C" int ot_mixed_gemm(int mode, const float* A, int64_t lda, int K, const
                              const float* res, int64_t ldres, int res_tok,
                              const float* aux, int64_t ldaux,
                              uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
-                             void* stream) {
+                             const int32_t* tail_pos, void* stream) {
   return mixed_gemm_impl(mode, A, lda, K, in_rows, a_xform, a_rstd, a_gamma, W, w_gstride, ldw, N, tile_group,
                          ntiles, bias, bias_gstride, C, ldc, out_rows, epi, res, ldres, res_tok, aux, ldaux, seed,
-                         site, drop_rate, tail_K, tail_I, nullptr, stream);
+                         site, drop_rate, tail_K, tail_I, tail_pos, nullptr, stream);
 }
 
 extern "C" size_t ot_mixed_gemm_rms_workspace_size(int ntiles, int N) {
@@ -1189,11 +1189,11 @@ extern "C" int ot_mixed_gemm_rms(int mode, const float* A, int64_t lda, int K, c
                                  const float* res, int64_t ldres, int res_tok,
                                  const float* aux, int64_t ldaux,
                                  uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
-                                 const ot_rms_epilogue* rms, void* stream) {
+                                 const int32_t* tail_pos, const ot_rms_epilogue* rms, void* stream) {
   OT_REQUIRE(rms, "ot_mixed_gemm_rms: null epilogue operands");
   return mixed_gemm_impl(mode, A, lda, K, in_rows, a_xform, a_rstd, a_gamma, W, w_gstride, ldw, N, tile_group,
                          ntiles, bias, bias_gstride, C, ldc, out_rows, epi, res, ldres, res_tok, aux, ldaux, seed,
-                         site, drop_rate, tail_K, tail_I, rms, stream);
+                         site, drop_rate, tail_K, tail_I, tail_pos, rms, stream);
 }
 
 extern "C" size_t ot_wgrad_workspace_size(int nchunks, int K, int N) {

@@ -55,6 +55,7 @@ struct RmsBwdArgs {
   uint32_t seed, site, thr; float dscale; int tail_K, tail_I;
   float* dgamma_part;                   // [gridDim.x][d] or null
   int64_t rows; int d; int tpr;
+  const int32_t* tail_pos; const int32_t* dres_inv;   // ot_pyramid_select maps or null (tail rule)
 };
 
 __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(RmsBwdArgs p) {
@@ -80,7 +81,7 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(RmsBwdArgs p) {
     }
     s = group_sum(s, tpr);
     const float coef = r * r * r * s / (float)d;
-    const int64_t tok = p.dxm ? tail_token(rr, p.tail_K, p.tail_I) : 0;
+    const int64_t tok = p.dxm ? tail_token(rr, p.tail_K, p.tail_I, p.tail_pos) : 0;
     int q = 0;
     for (int c = lt * 4; c < d; c += tpr * 4, ++q) {
       f32x4 a = *reinterpret_cast<const f32x4*>(dyr + c);
@@ -89,11 +90,7 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(RmsBwdArgs p) {
       if (!live) continue;
       f32x4 o = a * g * r - v * coef;
       if (p.dres) {
-        int64_t dr = rr;
-        if (p.dres_K > 0) {
-          const int64_t b = rr / p.dres_I, pos = rr - b * p.dres_I, j = pos - (p.dres_I - p.dres_K);
-          dr = j >= 0 ? b * p.dres_K + j : -1;
-        }
+        const int64_t dr = p.dres_K > 0 ? kept_row(rr, p.dres_K, p.dres_I, p.dres_inv) : rr;
         if (dr >= 0) o += *reinterpret_cast<const f32x4*>(p.dres + dr * p.lddres + c);
       }
       if (q < 4) dg[q] += a * v * r;
@@ -176,12 +173,12 @@ __global__ void rows_colsum_kernel(const float* __restrict__ src, int64_t ld, co
 
 __global__ void dropout_apply_kernel(const float* __restrict__ src, int64_t lds, float* dst, int64_t ldd,
                                      int64_t rows, int d, uint32_t seed, uint32_t site, uint32_t thr, float scale,
-                                     int tail_K, int tail_I) {
+                                     int tail_K, int tail_I, const int32_t* tail_pos) {
   const int64_t i4 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (i4 >= rows * d) return;
   const int64_t r = i4 / d;
   const int c = (int)(i4 % d);
-  const int64_t tok = tail_token(r, tail_K, tail_I);
+  const int64_t tok = tail_token(r, tail_K, tail_I, tail_pos);
   f32x4 v = *reinterpret_cast<const f32x4*>(src + r * lds + c);
   uint32_t base = (uint32_t)(tok * d + c);
   v.x = drop_keep(seed, site, base + 0, thr) ? v.x * scale : 0.f;
@@ -228,9 +225,9 @@ extern "C" size_t ot_rmsnorm_bwd_workspace_size(int64_t rows, int d) {
 
 extern "C" int ot_rmsnorm_bwd(const float* dy, int64_t lddy, const float* x, int64_t ldx, const float* gamma,
                               const float* rstd, const float* dres, int64_t lddres, int dres_tail_K,
-                              int dres_tail_I, float* dx, int64_t lddx,
+                              int dres_tail_I, const int32_t* dres_tail_inv, float* dx, int64_t lddx,
                               float* dx_masked, int64_t lddxm, uint32_t seed, uint32_t site, float drop_rate,
-                              int tail_K, int tail_I, float* dgamma, int accumulate_dgamma, int64_t rows, int d,
+                              int tail_K, int tail_I, const int32_t* tail_pos, float* dgamma, int accumulate_dgamma, int64_t rows, int d,
                               void* workspace, size_t ws_bytes, void* stream) {
   OT_REQUIRE(dy && x && gamma && rstd && dx, "ot_rmsnorm_bwd: null operand");
   OT_REQUIRE(d % 4 == 0 && lddy % 4 == 0 && ldx % 4 == 0 && lddx % 4 == 0, "ot_rmsnorm_bwd: alignment");
@@ -244,7 +241,7 @@ extern "C" int ot_rmsnorm_bwd(const float* dy, int64_t lddy, const float* x, int
   OT_REQUIRE(dres_tail_K == 0 || (dres_tail_K > 0 && dres_tail_I >= dres_tail_K), "ot_rmsnorm_bwd: bad dres tail");
   RmsBwdArgs p{dy, lddy, x, ldx, gamma, rstd, dres, lddres, dres_tail_K, dres_tail_I, dx, lddx, dx_masked, lddxm, seed, site,
                drop_threshold(drop_rate), drop_rate < 1.f ? 1.f / (1.f - drop_rate) : 0.f, tail_K, tail_I,
-               dgamma ? (float*)workspace : nullptr, rows, d, tpr};
+               dgamma ? (float*)workspace : nullptr, rows, d, tpr, tail_pos, dres_tail_inv};
   const size_t shmem = dgamma ? (size_t)(256 / tpr) * d * sizeof(float) : 0;
   OT_REQUIRE(shmem <= 65536, "ot_rmsnorm_bwd: d too large for the dgamma staging");
   hipLaunchKernelGGL(rmsnorm_bwd_kernel, dim3(grid), dim3(256), shmem, (hipStream_t)stream, p);
@@ -275,13 +272,14 @@ void launch_colsum_reduce(const float* part, int64_t nparts, int ncols, float* o
 }  // namespace ot
 
 extern "C" int ot_dropout_apply(const float* src, int64_t lds, float* dst, int64_t ldd, int64_t rows, int d,
-                                uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I, void* stream) {
+                                uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
+                                const int32_t* tail_pos, void* stream) {
   OT_REQUIRE(src && dst && d % 4 == 0 && lds % 4 == 0 && ldd % 4 == 0, "ot_dropout_apply: bad args");
   OT_REQUIRE(tail_K > 0 && tail_I >= tail_K, "ot_dropout_apply: bad tail map");
   if (rows == 0) return OT_OK;
   hipLaunchKernelGGL(dropout_apply_kernel, dim3(ceil_div(rows * d / 4, 256)), dim3(256), 0, (hipStream_t)stream,
                      src, lds, dst, ldd, rows, d, seed, site, drop_threshold(drop_rate),
-                     drop_rate < 1.f ? 1.f / (1.f - drop_rate) : 0.f, tail_K, tail_I);
+                     drop_rate < 1.f ? 1.f / (1.f - drop_rate) : 0.f, tail_K, tail_I, tail_pos);
   OT_LAUNCH_CHECK("ot_dropout_apply");
   return OT_OK;
 }

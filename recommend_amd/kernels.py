@@ -92,6 +92,24 @@ def ptr(x: Ptrish):
     return x.data_ptr()
 
 
+def _sel(tail):
+    """Kept-token map of a (K, I[, map]) tail spec: the third element (a device int32 tensor from
+    ``pyramid_select``: positions for ``tail``, inverse rows for ``dres_tail``) or None (the tail rule)."""
+    return ptr(tail[2]) if len(tail) > 2 and tail[2] is not None else None
+
+
+def pyramid_select(B: int, I: int, K: int, pos: torch.Tensor, inv: Optional[torch.Tensor] = None,
+                   score: Optional[torch.Tensor] = None, sign: float = 1.0, nforce: int = 0,
+                   map_rows: Optional[torch.Tensor] = None, map_per_sample: int = 0) -> None:
+    """ot_pyramid_select: per-sample top-K positions (ascending) by score*sign, the last ``nforce`` kept;
+    no score = the tail (model.py:287-302, 371)."""
+    ev = _probe.begin() if _probe is not None else None
+    call('ot_pyramid_select', ptr(score), float(sign), B, I, K, nforce, ptr(pos), ptr(inv), ptr(map_rows),
+         map_per_sample, stream())
+    if ev is not None:
+        _probe.end('pyramid', 0.0, ev)
+
+
 def stream() -> int:
     return torch.cuda.current_stream().cuda_stream
 
@@ -109,7 +127,8 @@ def gemm(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish, w_g
     ev = _probe.begin() if _probe is not None else None
     call('ot_mixed_gemm', mode, ptr(A), lda, K, ptr(in_rows), a_xform, ptr(rstd), ptr(gamma), ptr(W), w_gstride,
          ldw, N, ptr(tile_group), ntiles, ptr(bias), bias_gstride, ptr(C), ldc, ptr(out_rows), epi, ptr(res),
-         ldres, res_tok, ptr(aux), ldaux, seed & 0xFFFFFFFF, site, float(drop), tail[0], tail[1], stream())
+         ldres, res_tok, ptr(aux), ldaux, seed & 0xFFFFFFFF, site, float(drop), tail[0], tail[1], _sel(tail),
+         stream())
     if ev is not None:
         _probe.end('mixed_gemm', 2.0 * (m_rows or ntiles * 128) * K * N, ev,
                    f'gemm mode{mode} ax{a_xform} epi{epi} M{m_rows or ntiles * 128} K{K} N{N}')
@@ -129,12 +148,12 @@ def gemm_rms(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish,
     ws = workspace(size('ot_mixed_gemm_rms_workspace_size', ntiles, N) if dgamma is not None else 16,
                    device if device is not None else (C[0] if isinstance(C, tuple) else C).device)
     e = _lib.RmsEpilogue(ptr(rstd_out), float(eps), ptr(nx), ldnx, ptr(ngamma), ptr(nrstd), ptr(dres), lddres,
-                         dres_tail[0], dres_tail[1], ptr(dx_masked), lddxm, ptr(dgamma), int(accumulate_dgamma),
-                         ptr(ws), ws.numel())
+                         dres_tail[0], dres_tail[1], _sel(dres_tail), ptr(dx_masked), lddxm, ptr(dgamma),
+                         int(accumulate_dgamma), ptr(ws), ws.numel())
     ev = _probe.begin() if _probe is not None else None
     call('ot_mixed_gemm_rms', mode, ptr(A), lda, K, ptr(in_rows), a_xform, ptr(rstd), ptr(gamma), ptr(W),
          w_gstride, ldw, N, ptr(tile_group), ntiles, ptr(bias), bias_gstride, ptr(C), ldc, ptr(out_rows), epi,
-         ptr(res), ldres, res_tok, None, 0, seed & 0xFFFFFFFF, site, float(drop), tail[0], tail[1],
+         ptr(res), ldres, res_tok, None, 0, seed & 0xFFFFFFFF, site, float(drop), tail[0], tail[1], _sel(tail),
          ctypes.byref(e), stream())
     if ev is not None:
         _probe.end('mixed_gemm', 2.0 * (m_rows or ntiles * 128) * K * N, ev,
@@ -166,18 +185,18 @@ def transpose_banks(src, dst, banks_dev, nbanks, total_tiles) -> None:
 
 
 def attn_fwd(qkv: torch.Tensor, ld: int, B: int, H: int, I: int, K: int, hd: int, out: torch.Tensor,
-             lse: torch.Tensor) -> None:
+             lse: torch.Tensor, qpos: Optional[torch.Tensor] = None) -> None:
     ev = _probe.begin() if _probe is not None else None
-    call('ot_attn_fwd', ptr(qkv), ld, B, H, I, K, hd, ptr(out), ptr(lse), stream())
+    call('ot_attn_fwd', ptr(qkv), ld, B, H, I, K, ptr(qpos), hd, ptr(out), ptr(lse), stream())
     if ev is not None:
         _probe.end('attention', 4.0 * (K * I - K * (K - 1) / 2) * hd * H * B, ev, f'fwd I{I} K{K} hd{hd}')
 
 
-def attn_bwd(qkv, ld, out, dout, lse, B, H, I, K, hd, dqkv) -> None:
+def attn_bwd(qkv, ld, out, dout, lse, B, H, I, K, hd, dqkv, qpos=None) -> None:
     delta = workspace(size('ot_attn_bwd_workspace_size', B, H, K), qkv.device)
     ev = _probe.begin() if _probe is not None else None
-    call('ot_attn_bwd', ptr(qkv), ld, ptr(out), ptr(dout), ptr(lse), B, H, I, K, hd, ptr(dqkv), ptr(delta),
-         stream())
+    call('ot_attn_bwd', ptr(qkv), ld, ptr(out), ptr(dout), ptr(lse), B, H, I, K, ptr(qpos), hd, ptr(dqkv),
+         ptr(delta), stream())
     if ev is not None:
         _probe.end('attention', 8.0 * (K * I - K * (K - 1) / 2) * hd * H * B, ev, f'bwd I{I} K{K} hd{hd}')
 
@@ -198,8 +217,8 @@ def rmsnorm_bwd(dy: Ptrish, lddy: int, x: Ptrish, ldx: int, gamma: Ptrish, rstd:
     ws = workspace(nbytes, device)
     ev = _probe.begin() if _probe is not None else None
     call('ot_rmsnorm_bwd', ptr(dy), lddy, ptr(x), ldx, ptr(gamma), ptr(rstd), ptr(dres), lddres, dres_tail[0],
-         dres_tail[1], ptr(dx), lddx, ptr(dx_masked), lddxm, seed & 0xFFFFFFFF, site, float(drop), tail[0], tail[1],
-         ptr(dgamma), int(accumulate), rows, d, ptr(ws), ws.numel(), stream())
+         dres_tail[1], _sel(dres_tail), ptr(dx), lddx, ptr(dx_masked), lddxm, seed & 0xFFFFFFFF, site, float(drop),
+         tail[0], tail[1], _sel(tail), ptr(dgamma), int(accumulate), rows, d, ptr(ws), ws.numel(), stream())
     if ev is not None:
         _probe.end('rowwise', 0.0, ev)
 
@@ -207,7 +226,7 @@ def rmsnorm_bwd(dy: Ptrish, lddy: int, x: Ptrish, ldx: int, gamma: Ptrish, rstd:
 def dropout_apply(src, lds, dst, ldd, rows, d, seed, site, drop, tail) -> None:
     ev = _probe.begin() if _probe is not None else None
     call('ot_dropout_apply', ptr(src), lds, ptr(dst), ldd, rows, d, seed & 0xFFFFFFFF, site, float(drop), tail[0],
-         tail[1], stream())
+         tail[1], _sel(tail), stream())
     if ev is not None:
         _probe.end('rowwise', 0.0, ev)
 

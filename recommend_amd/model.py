@@ -29,7 +29,7 @@ from . import _lib
 from . import kernels as K
 from ._lib import (OT_AX_GELU, OT_AX_RMSNORM, OT_EPI_ACCUMULATE, OT_EPI_BIAS, OT_EPI_DROPOUT, OT_EPI_GELU_BWD,
                    OT_EPI_RESIDUAL, OT_EPI_RMSNORM_BWD, OT_EPI_ROW_RSTD, OT_GEMM_NN, OT_GEMM_NT, NS_FIELD_BYTES)
-from .config import OneTransConfig, get_model_config
+from .config import OneTransConfig, check_pyramid_select, get_model_config
 from .layout import TILE, FlatLayout, RowMap, build_map, head_map, identity_map, layer_maps, round_up
 from .params import init_params, ns_table_offsets
 
@@ -134,7 +134,7 @@ class _Block(torch.autograd.Function):
     of the next: ``rstd_in``), and the FFN1 / QKV dgrad epilogues apply the norm backward."""
 
     @staticmethod
-    def forward(ctx, flat, x, m, l, I, Kq, seed, training, rstd_in=None):
+    def forward(ctx, flat, x, m, l, I, Kq, seed, training, rstd_in=None, select=False):
         cfg = m.config
         d, f, H = cfg.hidden_dim, cfg.ffn_dim, cfg.num_heads
         hd = d // H
@@ -155,6 +155,22 @@ class _Block(torch.autograd.Function):
         else:
             rstd1 = torch.empty(B * I, device=dev)
             K.rmsnorm_fwd(x, d, B * I, d, rstd1, eps=RMS_EPS)
+        # pyramid keep (model.py:287-302, 371): the kept query positions come from the wavefront
+        # top-K select (ot_pyramid_select); with no score (reference semantics) they are the tail
+        qrows, pos, inv = mt['rows'][0], None, None
+        if select:
+            pos = torch.empty(B * Kq, dtype=torch.int32, device=dev)
+            inv = torch.empty(B * I, dtype=torch.int32, device=dev)
+            if cfg.pyramid_select == 'norm':
+                # score = token RMS (1/rstd1): keep the largest; the NS tail is always kept and only the
+                # shared-group rows of the tail map change (dedicated_positions='tail', checked in config)
+                nf = min(cfg.num_ns_tokens, Kq)
+                qrows = qrows.clone()
+                K.pyramid_select(B, I, Kq, pos, inv, score=rstd1, sign=-1.0, nforce=nf, map_rows=qrows,
+                                 map_per_sample=Kq - nf)
+            else:
+                K.pyramid_select(B, I, Kq, pos, inv)
+        tail = (Kq, I, pos)
         qkv = torch.empty(B * I, 3 * d, device=dev)
         if Kq == I:
             K.gemm(OT_GEMM_NT, x, d, d, ma['rows'][0], wqkv, 3 * d * d, d, 3 * d, ma['tile_group'], na, qkv,
@@ -162,22 +178,22 @@ class _Block(torch.autograd.Function):
         else:
             K.gemm(OT_GEMM_NT, x, d, d, ma['rows'][0], (wqkv, d * d), 3 * d * d, d, 2 * d, ma['tile_group'], na,
                    (qkv, d), 3 * d, ma['rows'][0], a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=maps['all'].nrows)
-            K.gemm(OT_GEMM_NT, x, d, d, mt['rows'][0], wqkv, 3 * d * d, d, d, mt['tile_group'], nt, qkv,
-                   3 * d, mt['rows'][0], a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=maps['tail'].nrows)
+            K.gemm(OT_GEMM_NT, x, d, d, qrows, wqkv, 3 * d * d, d, d, mt['tile_group'], nt, qkv,
+                   3 * d, qrows, a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=maps['tail'].nrows)
         o = torch.empty(B * Kq, d, device=dev)
         lse = torch.empty(B * H * Kq, device=dev)
-        K.attn_fwd(qkv, 3 * d, B, H, I, Kq, hd, o, lse)
+        K.attn_fwd(qkv, 3 * d, B, H, I, Kq, hd, o, lse, qpos=pos)
         # x1 = x[tail] + drop(o @ Wo)      (model.py:117, 193)
         x1 = torch.empty(B * Kq, d, device=dev)
         rstd2 = torch.empty(B * Kq, device=dev)
         if fuse:
             K.gemm_rms(OT_GEMM_NT, o, d, d, mt['rows'][1], wo, 0, d, d, mt['tile_group'], nt, x1, d, mt['rows'][1],
                        epi=OT_EPI_RESIDUAL | dflag | OT_EPI_ROW_RSTD, res=x, ldres=d, res_tok=1, seed=seed,
-                       site=2 * l, drop=rate, tail=(Kq, I), m_rows=maps['tail'].nrows, rstd_out=rstd2, eps=RMS_EPS)
+                       site=2 * l, drop=rate, tail=tail, m_rows=maps['tail'].nrows, rstd_out=rstd2, eps=RMS_EPS)
         else:
             K.gemm(OT_GEMM_NT, o, d, d, mt['rows'][1], wo, 0, d, d, mt['tile_group'], nt, x1, d, mt['rows'][1],
                    epi=OT_EPI_RESIDUAL | dflag, res=x, ldres=d, res_tok=1, seed=seed, site=2 * l, drop=rate,
-                   tail=(Kq, I), m_rows=maps['tail'].nrows)
+                   tail=tail, m_rows=maps['tail'].nrows)
             K.rmsnorm_fwd(x1, d, B * Kq, d, rstd2, eps=RMS_EPS)
         # u = norm2(x1) @ W1[g] + b1[g]  (pre-activation; GELU applied by its consumers)
         u = torch.empty(B * Kq, f, device=dev)
@@ -191,15 +207,16 @@ class _Block(torch.autograd.Function):
             K.gemm_rms(OT_GEMM_NT, u, f, f, mt['rows'][1], w2, f * d, f, d, mt['tile_group'], nt, x2, d,
                        mt['rows'][1], a_xform=OT_AX_GELU, bias=b2, bias_gstride=d,
                        epi=OT_EPI_BIAS | OT_EPI_RESIDUAL | dflag | OT_EPI_ROW_RSTD, res=x1, ldres=d, res_tok=0,
-                       seed=seed, site=2 * l + 1, drop=rate, tail=(Kq, I), m_rows=maps['tail'].nrows,
+                       seed=seed, site=2 * l + 1, drop=rate, tail=tail, m_rows=maps['tail'].nrows,
                        rstd_out=rstd_out, eps=RMS_EPS)
         else:
             K.gemm(OT_GEMM_NT, u, f, f, mt['rows'][1], w2, f * d, f, d, mt['tile_group'], nt, x2, d, mt['rows'][1],
                    a_xform=OT_AX_GELU, bias=b2, bias_gstride=d, epi=OT_EPI_BIAS | OT_EPI_RESIDUAL | dflag, res=x1,
-                   ldres=d, res_tok=0, seed=seed, site=2 * l + 1, drop=rate, tail=(Kq, I),
+                   ldres=d, res_tok=0, seed=seed, site=2 * l + 1, drop=rate, tail=tail,
                    m_rows=maps['tail'].nrows)
         ctx.save_for_backward(x, rstd1, qkv, o, lse, x1, rstd2, u)
         ctx.m, ctx.l, ctx.I, ctx.Kq, ctx.seed, ctx.rate = m, l, I, Kq, seed, rate
+        ctx.pos, ctx.inv = pos, inv
         if rstd_out is None:
             rstd_out = x2.new_empty(0)          # not fused: the next block computes its own rstd
         ctx.mark_non_differentiable(rstd_out)
@@ -209,6 +226,8 @@ class _Block(torch.autograd.Function):
     def backward(ctx, dx2, _drstd=None):
         x, rstd1, qkv, o, lse, x1, rstd2, u = ctx.saved_tensors
         m, l, I, Kq, seed, rate = ctx.m, ctx.l, ctx.I, ctx.Kq, ctx.seed, ctx.rate
+        pos, inv = ctx.pos, ctx.inv
+        tail = (Kq, I, pos)
         cfg = m.config
         d, f, H = cfg.hidden_dim, cfg.ffn_dim, cfg.num_heads
         hd = d // H
@@ -224,7 +243,7 @@ class _Block(torch.autograd.Function):
         # FFN branch: dY2 = mask(dx2)
         if rate > 0:
             dy2 = torch.empty_like(dx2)
-            K.dropout_apply(dx2, d, dy2, d, B * Kq, d, seed, 2 * l + 1, rate, (Kq, I))
+            K.dropout_apply(dx2, d, dy2, d, B * Kq, d, seed, 2 * l + 1, rate, tail)
         else:
             dy2 = dx2
         side = m.side(u, dy2)          # weight gradients overlap the dgrad chain on a second stream
@@ -245,7 +264,7 @@ class _Block(torch.autograd.Function):
         if m.fuse_norms:
             K.gemm_rms(OT_GEMM_NT, du, f, f, mt['rows'][1], m.p(f'blk.{l}.w1'), d * f, f, d, mt['tile_group'], nt,
                        dx1, d, mt['rows'][1], epi=OT_EPI_RMSNORM_BWD | (OT_EPI_DROPOUT if rate > 0 else 0),
-                       seed=seed, site=2 * l, drop=rate, tail=(Kq, I), m_rows=maps['tail'].nrows, nx=x1, ldnx=d,
+                       seed=seed, site=2 * l, drop=rate, tail=tail, m_rows=maps['tail'].nrows, nx=x1, ldnx=d,
                        ngamma=m.p(f'blk.{l}.norm2'), nrstd=rstd2, dres=dx2, lddres=d,
                        dx_masked=dyo if rate > 0 else None, lddxm=d, dgamma=m.g(f'blk.{l}.norm2'),
                        accumulate_dgamma=acc, device=dev)
@@ -255,7 +274,7 @@ class _Block(torch.autograd.Function):
                    d, mt['rows'][1], m_rows=maps['tail'].nrows)
             K.rmsnorm_bwd(dxn2, d, x1, d, m.p(f'blk.{l}.norm2'), rstd2, dx1, d, B * Kq, d, dres=dx2, lddres=d,
                           dx_masked=dyo if rate > 0 else None, lddxm=d, seed=seed, site=2 * l, drop=rate,
-                          tail=(Kq, I), dgamma=m.g(f'blk.{l}.norm2'), accumulate=acc, device=dev)
+                          tail=tail, dgamma=m.g(f'blk.{l}.norm2'), accumulate=acc, device=dev)
         # Wo
         with m.side(o, dyo):
             _wgrad_single(m, o, dyo, d, d, mt, m.g(f'blk.{l}.wo'), acc, dev, maps['tail'].nrows, maps['tail'])
@@ -266,7 +285,7 @@ class _Block(torch.autograd.Function):
         dqkv = torch.empty(B * I, 3 * d, device=dev)
         if Kq < I:
             dqkv[:, :d].zero_()
-        K.attn_bwd(qkv, 3 * d, o, do, lse, B, H, I, Kq, hd, dqkv)
+        K.attn_bwd(qkv, 3 * d, o, do, lse, B, H, I, Kq, hd, dqkv, qpos=pos)
         with m.side(x, dqkv, rstd1):
             K.wgrad(x, d, ma['rows'][0], dqkv, 3 * d, ma['rows'][0], d, 3 * d, ma, nca, G, m.g(f'blk.{l}.wqkv'),
                     3 * d * d, None, 0, a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=m.p(f'blk.{l}.norm1'),
@@ -276,16 +295,16 @@ class _Block(torch.autograd.Function):
             K.gemm_rms(OT_GEMM_NT, dqkv, 3 * d, 3 * d, ma['rows'][0], m.p(f'blk.{l}.wqkv'), 3 * d * d, 3 * d, d,
                        ma['tile_group'], na, dx, d, ma['rows'][0], epi=OT_EPI_RMSNORM_BWD,
                        m_rows=maps['all'].nrows, nx=x, ldnx=d, ngamma=m.p(f'blk.{l}.norm1'), nrstd=rstd1,
-                       dres=dx1, lddres=d, dres_tail=(Kq, I) if Kq < I else (0, 0),
+                       dres=dx1, lddres=d, dres_tail=(Kq, I, inv) if Kq < I else (0, 0),
                        dgamma=m.g(f'blk.{l}.norm1'), accumulate_dgamma=acc, device=dev)
         else:
             dxn1 = torch.empty(B * I, d, device=dev)
             K.gemm(OT_GEMM_NT, dqkv, 3 * d, 3 * d, ma['rows'][0], m.p(f'blk.{l}.wqkv'), 3 * d * d, 3 * d, d,
                    ma['tile_group'], na, dxn1, d, ma['rows'][0], m_rows=maps['all'].nrows)
             K.rmsnorm_bwd(dxn1, d, x, d, m.p(f'blk.{l}.norm1'), rstd1, dx, d, B * I, d, dres=dx1, lddres=d,
-                          dres_tail=(Kq, I) if Kq < I else (0, 0), dgamma=m.g(f'blk.{l}.norm1'), accumulate=acc,
+                          dres_tail=(Kq, I, inv) if Kq < I else (0, 0), dgamma=m.g(f'blk.{l}.norm1'), accumulate=acc,
                           device=dev)
-        return None, dx, None, None, None, None, None, None, None
+        return None, dx, None, None, None, None, None, None, None, None
 
 
 def _wgrad_single(m, A, D, K_, N, mt, dW, acc, dev, mrows=0, rowmap=None):
@@ -396,6 +415,7 @@ class OneTransModel(nn.Module):
         cfg = config
         if cfg.hidden_dim % cfg.num_heads or (cfg.hidden_dim // cfg.num_heads) not in (16, 32, 64, 128):
             raise ValueError('head_dim must be 16, 32, 64 or 128')
+        check_pyramid_select(cfg)
         self.f_ns = cfg.ns_input_width()
         self.layout = FlatLayout(cfg, self.f_ns)
         self.cfg_Lnsd = cfg.num_ns_tokens * cfg.hidden_dim
@@ -701,7 +721,8 @@ class OneTransModel(nn.Module):
         rstd = None
         for l, s in enumerate(sched):
             Kq = s['keep'] if l < nl - 1 else 1
-            x, rstd = _Block.apply(self.flat, x, self, l, s['in_len'], Kq, seed, training, rstd)
+            select = l < nl - 1 and Kq < s['in_len']         # a pyramid keep (the last layer: DCE, tail)
+            x, rstd = _Block.apply(self.flat, x, self, l, s['in_len'], Kq, seed, training, rstd, select)
         return _Head.apply(self.flat, x, self)
 
     # ---------------------------------------------------------------- side stream (wgrad overlap)

@@ -45,10 +45,16 @@ def test_library_exports_every_symbol():
 def test_errors_are_reported_not_crashing():
     """Invalid arguments return OT_ERR_INVALID_ARG with a message (no device work)."""
     with pytest.raises(_lib.OneTransHipError, match='null operand'):
-        _lib.call('ot_attn_fwd', None, 96, 1, 1, 4, 4, 32, None, None, None)
+        _lib.call('ot_attn_fwd', None, 96, 1, 1, 4, 4, None, 32, None, None, None)
     with pytest.raises(_lib.OneTransHipError, match='multiples of 4'):
         _lib.call('ot_mixed_gemm', 0, 8, 3, 3, None, 0, None, None, 8, 0, 4, 4, None, 1, None, 0, 8, 4, None, 0,
-                  None, 0, 0, None, 0, 0, 0, 0.0, 1, 1, None)
+                  None, 0, 0, None, 0, 0, 0, 0.0, 1, 1, None, None)
+    with pytest.raises(_lib.OneTransHipError, match='bad sizes'):
+        _lib.call('ot_pyramid_select', None, 1.0, 2, 8, 9, 0, 8, None, None, 0, None)    # K > I
+    with pytest.raises(_lib.OneTransHipError, match='bad sizes'):
+        _lib.call('ot_pyramid_select', None, 1.0, 2, 5000, 9, 0, 8, None, None, 0, None)  # I > 4096
+    with pytest.raises(_lib.OneTransHipError, match='nforce'):
+        _lib.call('ot_pyramid_select', None, 1.0, 2, 40, 6, 8, 8, None, None, 0, None)    # nforce > K
 
 
 @pytest.mark.parametrize('mode', ['head', 'tail'])

@@ -220,6 +220,93 @@ def test_attention(dev, B, H, I, Kq, hd):
     torch.testing.assert_close(dqkv.double().cpu(), qkv_r.grad, rtol=1e-4, atol=1e-4)
 
 
+def attn_ref_sel(qkv, B, H, I, qpos, hd):
+    """Causal attention of the kept queries qpos [B, K] (ascending positions) over all I keys."""
+    d = H * hd
+    Kq = qpos.shape[1]
+    bi = torch.arange(B)[:, None]
+    q = qkv[:, :d].reshape(B, I, H, hd)[bi, qpos]
+    k = qkv[:, d:2 * d].reshape(B, I, H, hd)
+    v = qkv[:, 2 * d:].reshape(B, I, H, hd)
+    s = torch.einsum('bqhd,bkhd->bhqk', q, k) / math.sqrt(hd)
+    mask = torch.arange(I)[None, None, None, :] <= qpos[:, None, :, None]
+    s = torch.where(mask, s, torch.tensor(-1e9, dtype=s.dtype))
+    return torch.einsum('bhqk,bkhd->bqhd', torch.softmax(s, -1), v).reshape(B * Kq, d)
+
+
+@pytest.mark.parametrize('B,H,I,Kq,hd', [(3, 4, 140, 70, 32), (2, 2, 70, 33, 64), (3, 4, 40, 12, 16),
+                                         (1, 2, 33, 17, 128), (2, 4, 140, 3, 32), (2, 2, 70, 4, 64),
+                                         (2, 4, 150, 100, 32), (2, 2, 524, 262, 64), (2, 4, 9, 9, 32)])
+def test_attention_selected_queries(dev, B, H, I, Kq, hd):
+    """Queries at per-sample kept positions (ot_pyramid_select's output), every kernel variant:
+    one-wave and shared-K/V forwards, MFMA and short-tail (K <= 4) backwards."""
+    rng = np.random.default_rng(I * 7 + Kq)
+    qpos = np.stack([np.append(np.sort(rng.choice(I - 1, Kq - 1, replace=False)), I - 1) for _ in range(B)])
+    torch.manual_seed(2)
+    d = H * hd
+    qkv = torch.randn(B * I, 3 * d, dtype=torch.float64)
+    qkv_d = qkv.float().to(dev)
+    qp_d = torch.from_numpy(qpos.astype(np.int32).reshape(-1)).to(dev)
+    out = torch.empty(B * Kq, d, device=dev)
+    lse = torch.empty(B * H * Kq, device=dev)
+    K.attn_fwd(qkv_d, 3 * d, B, H, I, Kq, hd, out, lse, qpos=qp_d)
+    qkv_r = qkv.clone().requires_grad_(True)
+    ref = attn_ref_sel(qkv_r, B, H, I, torch.from_numpy(qpos), hd)
+    torch.testing.assert_close(out.double().cpu(), ref.detach(), rtol=1e-4, atol=1e-5)
+    dout = torch.randn(B * Kq, d, dtype=torch.float64)
+    ref.backward(dout)
+    dqkv = torch.full((B * I, 3 * d), float('nan'), device=dev)
+    dqkv[:, :d].zero_()
+    K.attn_bwd(qkv_d, 3 * d, out, dout.float().to(dev), lse, B, H, I, Kq, hd, dqkv, qpos=qp_d)
+    torch.testing.assert_close(dqkv.double().cpu(), qkv_r.grad, rtol=1e-4, atol=1e-4)
+
+
+def select_ref(score, sign, B, I, K, nforce):
+    """ot_pyramid_select semantics: per sample the K largest (fp32 score*sign, position) keys, the last
+    nforce positions forced, ascending positions."""
+    out = np.empty((B, K), dtype=np.int64)
+    for b in range(B):
+        key = (np.zeros(I, np.float32) if score is None
+               else score[b * I:(b + 1) * I].astype(np.float32) * np.float32(sign))
+        forced = np.arange(I) >= I - nforce
+        order = np.lexsort((np.arange(I), key, forced))     # ascending by (forced, key, position)
+        out[b] = np.sort(order[I - K:])
+    return out
+
+
+@pytest.mark.parametrize('B,I,Kk,nforce,scored', [(5, 140, 70, 0, False), (3, 524, 262, 0, False),
+                                                 (4, 140, 70, 12, True), (3, 524, 131, 12, True),
+                                                 (2, 65, 64, 0, True), (2, 64, 1, 0, True), (7, 5, 3, 2, True),
+                                                 (2, 1036, 518, 12, True), (2, 4096, 1000, 3, True),
+                                                 (3, 40, 8, 8, True), (3, 40, 9, 8, True), (1, 1, 1, 0, True)])
+def test_pyramid_select(dev, B, I, Kk, nforce, scored):
+    """Wavefront top-K vs a numpy restatement: exact positions, inverse map, tail-map rewrite; scores
+    drawn from a small set so ties (decided by position) are common."""
+    rng = np.random.default_rng(B * I + Kk)
+    score = rng.integers(1, 6, size=B * I).astype(np.float32) * 0.25 if scored else None
+    if scored and I > 8:
+        score[::7] = rng.standard_normal(len(score[::7])).astype(np.float32)
+    sign = -1.0 if scored and Kk % 2 else 1.0
+    want = select_ref(score, sign, B, I, Kk, nforce)
+    pos = torch.full((B * Kk,), -7, dtype=torch.int32, device=dev)
+    inv = torch.full((B * I,), -7, dtype=torch.int32, device=dev)
+    mps = max(0, Kk - nforce)
+    maprows = torch.full((B * mps + 1,), -7, dtype=torch.int32, device=dev)
+    K.pyramid_select(B, I, Kk, pos, inv, score=torch.from_numpy(score).to(dev) if scored else None, sign=sign,
+                     nforce=nforce, map_rows=maprows, map_per_sample=mps)
+    got = pos.cpu().numpy().reshape(B, Kk)
+    np.testing.assert_array_equal(got, want)
+    winv = np.full(B * I, -1)
+    for b in range(B):
+        winv[b * I + want[b]] = b * Kk + np.arange(Kk)
+    np.testing.assert_array_equal(inv.cpu().numpy(), winv)
+    wmap = (np.arange(B)[:, None] * I + want[:, :mps]).reshape(-1)
+    np.testing.assert_array_equal(maprows.cpu().numpy()[:B * mps], wmap)
+    assert maprows[B * mps].item() == -7
+    if not scored and nforce == 0:
+        np.testing.assert_array_equal(got, np.broadcast_to(np.arange(I - Kk, I), (B, Kk)))   # model.py:296
+
+
 @pytest.mark.parametrize('d', [64, 128, 256, 512])
 def test_rmsnorm(dev, d):
     torch.manual_seed(1)

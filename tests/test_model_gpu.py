@@ -48,7 +48,17 @@ CASES = {
     # d == 128: RMSNorms fused into the GEMM epilogues (row rstd / norm backward), pyramid tail maps
     'criteo_d128_pyramid': lambda: small_criteo('tail', pyramid=True, layers=3, d=128, H=4, f=256, Lns=12,
                                                 seq_lens=(20, 20, 20)),
+    # pyramid_select='norm' (build extension): NS tokens + top-RMS S tokens kept per sample (wavefront
+    # top-K); unfused norms at d=64, fused GEMM-epilogue norms at d=128
+    'criteo_norm_pyramid': lambda: norm_select(small_criteo('tail', pyramid=True, layers=3)),
+    'criteo_d128_norm_pyramid': lambda: norm_select(small_criteo('tail', pyramid=True, layers=3, d=128, H=4, f=256,
+                                                                 Lns=12, seq_lens=(20, 20, 20))),
 }
+
+
+def norm_select(cfg):
+    cfg.pyramid_select = 'norm'
+    return cfg
 
 
 def setup(cfg, B, dev, seed=0):
@@ -83,7 +93,7 @@ def ns_t(d, dev):
 
 
 @pytest.mark.parametrize('case', ['c1_head', 'criteo_head', 'criteo_tail_pyramid', 'criteo_d128_hd32',
-                                  'criteo_d128_pyramid'])
+                                  'criteo_d128_pyramid', 'criteo_norm_pyramid', 'criteo_d128_norm_pyramid'])
 @pytest.mark.parametrize('training', [False, True])
 def test_gradient_parity(dev, case, training):
     cfg = CASES[case]()

@@ -140,6 +140,50 @@ def test_restatements_agree(mode, pyramid, training):
         assert np.abs(a['logits'][t].numpy() - c['logits'][t]).max() < 1e-12
 
 
+@pytest.mark.parametrize('training', [False, True])
+def test_restatements_agree_norm_select(training):
+    """pyramid_select='norm' (build extension): literal (full block, then gather the kept rows) and
+    vectorized (kept queries only) restatements agree."""
+    cfg = _small_criteo('tail', True)
+    cfg.pyramid_select = 'norm'
+    ns, seq, _ = make_batch(5, cfg, seed=3)
+    P = init_params(cfg, cfg.ns_input_width(), seed=1, perturb=True)
+    Pt = R.to_torch(P)
+    a = R.forward(Pt, cfg, R.to_torch(ns), R.to_torch(seq), training, seed=9, variant='literal')
+    b = R.forward(Pt, cfg, R.to_torch(ns), R.to_torch(seq), training, seed=9, variant='vectorized')
+    t = R.forward(Pt, _small_criteo('tail', True), R.to_torch(ns), R.to_torch(seq), training, seed=9)
+    for task in cfg.tasks:
+        assert np.abs(a['logits'][task].numpy() - b['logits'][task].numpy()).max() < 1e-12
+    # a different kept set than the tail: the logits move
+    assert max(np.abs(a['logits'][k].numpy() - t['logits'][k].numpy()).max() for k in cfg.tasks) > 1e-6
+
+
+def test_select_positions_kat():
+    """Hand example: I=8, keep 5, 2 forced NS tokens; mean(x^2) per position picks 3 of the first 6,
+    ties to the later position; positions come out ascending."""
+    cfg = OneTransConfig()
+    cfg.num_ns_tokens, cfg.pyramid_select, cfg.dedicated_positions = 2, 'norm', 'tail'
+    ms = np.array([[4., 1., 9., 4., 0.5, 2., 0., 0.], [1., 1., 1., 1., 1., 1., 7., 7.]])
+    x = torch.from_numpy(np.sqrt(ms))[:, :, None].double()      # d = 1: mean(x^2) = ms
+    sel = R.select_positions(cfg, x, 5)
+    np.testing.assert_array_equal(sel, [[0, 2, 3, 6, 7], [3, 4, 5, 6, 7]])
+    cfg.pyramid_select = 'tail'
+    assert R.select_positions(cfg, x, 5) is None
+
+
+def test_norm_select_needs_tail_dedication():
+    from recommend_amd.config import check_pyramid_select
+    cfg = OneTransConfig()
+    cfg.pyramid_select = 'norm'
+    with pytest.raises(ValueError):
+        check_pyramid_select(cfg)                                 # dedicated_positions='head'
+    cfg.dedicated_positions = 'tail'
+    check_pyramid_select(cfg)
+    cfg.pyramid_select = 'topk'
+    with pytest.raises(ValueError):
+        check_pyramid_select(cfg)
+
+
 def test_missing_features_follow_reference():
     """model.py:249-251 (no NS feature -> zero NS tokens) and model.py:266-272 ([SEP] only after
     present sequences i < n-1, so dropping the last sequence leaves a trailing [SEP])."""

@@ -151,6 +151,14 @@ int ot_attn_bwd(const float* qkv, int64_t ld, const float* out, const float* dou
                 int B, int H, int I, int K, const int32_t* qpos, int head_dim, float* dqkv, float* delta_ws,
                 void* stream);
 
+/* Two-stage cached serving (paper §3.5.1; replaces the reference's defective cache path
+ * model.py:94-98, 359-381, D6): candidate c (request req[c]) attends with the last Kq of its n
+ * N-side rows (qkv [C*n, ld], q | k | v) over its request's Ic cached S-side rows (kv_cache
+ * [R*Ic, ldc], k at col 0, v at col d) and its own n rows, causally (query j at absolute position
+ * Ic + n - Kq + j).  out: [C*Kq, H*head_dim].  Forward only. */
+int ot_attn_fwd_cached(const float* qkv, int64_t ld, const float* kv_cache, int64_t ldc, const int32_t* req,
+                       int C, int H, int Ic, int n, int Kq, int head_dim, float* out, void* stream);
+
 /* ---- pyramid query selection (pyramid.hip) -----------------------------------------------
  * Replaces PyramidScheduler.get_layer_config + tf.gather (model.py:287-302, 356, 371): per sample,
  * keep the K of I tokens with the largest key (score[b*I+p] * score_sign, ties to the later

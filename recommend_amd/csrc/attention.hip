@@ -669,6 +669,130 @@ __global__ __launch_bounds__(256) void attn_bwd_small_kernel(AttnArgs p) {
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Serving (paper §3.5.1 two-stage KV cache; the reference's broken cache path model.py:94-98,
+// 359-381): candidate c of request req[c] attends with its last Kq N-side queries over the request's
+// cached S-side keys/values (Ic rows, computed once per request) and its own n N-side rows.
+// Absolute positions: cache rows 0..Ic-1, N rows Ic..Ic+n-1; query j sits at Ic + n - Kq + j, so
+// every cached key is visible and the causal mask only touches the N-side key blocks.  Same
+// orientation and online softmax as attn_fwd_kernel; key rows come from two sources, so each lane
+// resolves its key row's address (one pointer per lane per key block).  Forward only (no lse).
+struct AttnCachedArgs {
+  const float* qkv; int64_t ld;            // N-side rows [C*n, ld]: q | k | v
+  const float* kc; const float* vc; int64_t ldc;   // cached S-side K / V rows [R*Ic, ldc]
+  const int32_t* req;                      // [C] request of each candidate
+  float* out;                              // [C*Kq, d]
+  int C, H, Ic, n, Kq, d;
+  float scale;
+};
+
+template <int HD>
+__device__ __forceinline__ void load_row_frag(float (&f)[HD / 2], const float* row, int hh) {
+  if (row) {
+    const float* q = row + (HD / 2) * hh;
+#pragma unroll
+    for (int i = 0; i < HD / 8; ++i) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(q + 4 * i);
+      f[4 * i] = v.x; f[4 * i + 1] = v.y; f[4 * i + 2] = v.z; f[4 * i + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < HD / 2; ++s) f[s] = 0.f;
+  }
+}
+
+template <int HD>
+__global__ __launch_bounds__(256) void attn_fwd_cached_kernel(AttnCachedArgs p) {
+  __shared__ __attribute__((aligned(16))) float lds[4][32 * TLD<HD>()];
+  const int lane = threadIdx.x & 63, li = lane & 31, hh = lane >> 5;
+  float* tV = lds[threadIdx.x >> 6];
+  const int pair = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (pair >= p.C * p.H) return;
+  const int c = pair / p.H, h = pair % p.H;
+  const int Ic = p.Ic, n = p.n, Kq = p.Kq, L = Ic + n;
+  const int64_t r = p.req[c];
+  const float* Nq = p.qkv + (int64_t)c * n * p.ld + h * HD;        // this candidate's N rows
+  const float* Ck = p.kc + r * Ic * p.ldc + h * HD;
+  const float* Cv = p.vc + r * Ic * p.ldc + h * HD;
+  const int q_off = L - Kq;                                         // absolute position of query 0
+  const float qscale = p.scale * 1.4426950408889634f;
+  const int nqb = (Kq + 31) / 32;
+  for (int qb = 0; qb < nqb; ++qb) {
+    const int j = 32 * qb + li;
+    const int qpos = q_off + (j < Kq ? j : Kq - 1);
+    float qf[HD / 2];
+    load_row_frag<HD>(qf, Nq + (int64_t)(qpos - Ic) * p.ld, hh);
+#pragma unroll
+    for (int s = 0; s < HD / 2; ++s) qf[s] *= qscale;
+    f32x16 oacc[NB(HD)];
+#pragma unroll
+    for (int cc = 0; cc < NB(HD); ++cc)
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) oacc[cc][rr] = 0.f;
+    float m = -INFINITY, l = 0.f;
+    const int last_q = q_off + min(32 * qb + 31, Kq - 1);
+    const int nkb = last_q / 32 + 1;
+    const int first_masked = (q_off + 32 * qb) / 32;
+    for (int kb = 0; kb < nkb; ++kb) {
+      const int key = 32 * kb + li;                 // this lane's key row (absolute position)
+      const float* kr = nullptr;
+      const float* vr = nullptr;
+      if (key < Ic) {
+        kr = Ck + (int64_t)key * p.ldc;
+        vr = Cv + (int64_t)key * p.ldc;
+      } else if (key < L) {
+        kr = Nq + (int64_t)(key - Ic) * p.ld + p.d;
+        vr = kr + p.d;
+      }
+      float kf[HD / 2], vf[HD / 2];
+      load_row_frag<HD>(kf, kr, hh);
+      load_row_frag<HD>(vf, vr, hh);
+      frag_to_lds<HD>(tV, vf, li, hh);
+      f32x16 s = mm_frag<HD>(kf, qf);               // S^T (log2 units): row = key, col = query
+      if (kb >= first_masked) {
+#pragma unroll
+        for (int rr = 0; rr < 16; ++rr) s[rr] = (32 * kb + acc_row(rr, hh) <= qpos) ? s[rr] : -INFINITY;
+      }
+      float mloc = s[0];
+#pragma unroll
+      for (int rr = 1; rr < 16; ++rr) mloc = fmaxf(mloc, s[rr]);
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+      const float mnew = fmaxf(m, mloc);
+      const float corr = __builtin_amdgcn_exp2f(m - mnew);
+      float lsum = 0.f;
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) {
+        const float e = __builtin_amdgcn_exp2f(s[rr] - mnew);
+        s[rr] = e;
+        lsum += e;
+      }
+      lsum += __shfl_xor(lsum, 32, 64);
+      l = l * corr + lsum;
+      m = mnew;
+#pragma unroll
+      for (int cc = 0; cc < NB(HD); ++cc) oacc[cc] *= corr;
+      __builtin_amdgcn_wave_barrier();
+      acc_tile_p<HD>(oacc, tV, s, li, hh);           // O^T += V^T P^T
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (j < Kq) {
+      const float inv = 1.f / l;
+      float* orow = p.out + ((int64_t)c * Kq + j) * p.d + h * HD;
+#pragma unroll
+      for (int cc = 0; cc < NB(HD); ++cc)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int dd = 32 * cc + 8 * g + 4 * hh;
+          if (dd < HD) {
+            f32x4 v = {oacc[cc][4 * g] * inv, oacc[cc][4 * g + 1] * inv, oacc[cc][4 * g + 2] * inv,
+                       oacc[cc][4 * g + 3] * inv};
+            *reinterpret_cast<f32x4*>(orow + dd) = v;
+          }
+        }
+    }
+  }
+}
+
 }  // namespace ot
 
 using namespace ot;
@@ -681,6 +805,25 @@ using namespace ot;
     case 128: hipLaunchKernelGGL(KERNEL<128>, __VA_ARGS__); break;                           \
     default: return fail(OT_ERR_UNSUPPORTED, "attention: head_dim %d unsupported", HD_);     \
   }
+
+extern "C" int ot_attn_fwd_cached(const float* qkv, int64_t ld, const float* kv_cache, int64_t ldc,
+                                  const int32_t* req, int C, int H, int Ic, int n, int Kq, int head_dim,
+                                  float* out, void* stream) {
+  OT_REQUIRE(qkv && out && req && (Ic == 0 || kv_cache), "ot_attn_fwd_cached: null operand");
+  OT_REQUIRE(C >= 0 && H > 0 && Ic >= 0 && n > 0 && Kq > 0 && Kq <= n, "ot_attn_fwd_cached: bad sizes C=%d Ic=%d n=%d Kq=%d",
+             C, Ic, n, Kq);
+  const int d = H * head_dim;
+  OT_REQUIRE(ld % 4 == 0 && ld >= 3 * d && (Ic == 0 || (ldc % 4 == 0 && ldc >= 2 * d)),
+             "ot_attn_fwd_cached: ld/ldc must hold k|v and be multiples of 4");
+  if (C == 0) return OT_OK;
+  AttnCachedArgs p{qkv, ld, kv_cache, kv_cache ? kv_cache + d : nullptr, ldc, req, out, C, H, Ic, n, Kq, d,
+                   1.f / sqrtf((float)head_dim)};
+  const unsigned grid = ceil_div((int64_t)C * H, 4);
+  OT_ATTN_DISPATCH(attn_fwd_cached_kernel, head_dim, dim3(grid), dim3(256), 0, (hipStream_t)stream, p);
+  OT_LAUNCH_CHECK("ot_attn_fwd_cached");
+  return OT_OK;
+}
+
 
 extern "C" int ot_attn_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos,
                            int head_dim, float* out, float* lse, void* stream) {

@@ -201,6 +201,15 @@ def attn_bwd(qkv, ld, out, dout, lse, B, H, I, K, hd, dqkv, qpos=None) -> None:
         _probe.end('attention', 8.0 * (K * I - K * (K - 1) / 2) * hd * H * B, ev, f'bwd I{I} K{K} hd{hd}')
 
 
+def attn_fwd_cached(qkv, ld, kv_cache, ldc, req, C, H, Ic, n, Kq, hd, out) -> None:
+    """ot_attn_fwd_cached: N-side queries over a request's cached S-side K/V plus their own rows."""
+    ev = _probe.begin() if _probe is not None else None
+    call('ot_attn_fwd_cached', ptr(qkv), ld, ptr(kv_cache), ldc, ptr(req), C, H, Ic, n, Kq, hd, ptr(out), stream())
+    if ev is not None:
+        _probe.end('attention', 4.0 * (Kq * (Ic + n) - Kq * (Kq - 1) / 2) * hd * H * C, ev,
+                   f'fwd_cached Ic{Ic} n{n} K{Kq} hd{hd}')
+
+
 def rmsnorm_fwd(x: Ptrish, ldx: int, rows: int, d: int, rstd: Ptrish, gamma: Ptrish = None, y: Ptrish = None,
                 ldy: int = 0, eps: float = 1e-6) -> None:
     ev = _probe.begin() if _probe is not None else None

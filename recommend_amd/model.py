@@ -416,6 +416,9 @@ class OneTransModel(nn.Module):
         if cfg.hidden_dim % cfg.num_heads or (cfg.hidden_dim // cfg.num_heads) not in (16, 32, 64, 128):
             raise ValueError('head_dim must be 16, 32, 64 or 128')
         check_pyramid_select(cfg)
+        # diagnostics only: ONETRANS_PYRAMID_KERNEL=0 addresses a 'tail' keep arithmetically instead of
+        # through ot_pyramid_select's position map (same kept set; for A/B timing of the map plumbing)
+        self.pyramid_kernel = os.environ.get('ONETRANS_PYRAMID_KERNEL', '1') != '0'
         self.f_ns = cfg.ns_input_width()
         self.layout = FlatLayout(cfg, self.f_ns)
         self.cfg_Lnsd = cfg.num_ns_tokens * cfg.hidden_dim
@@ -722,6 +725,7 @@ class OneTransModel(nn.Module):
         for l, s in enumerate(sched):
             Kq = s['keep'] if l < nl - 1 else 1
             select = l < nl - 1 and Kq < s['in_len']         # a pyramid keep (the last layer: DCE, tail)
+            select = select and (self.pyramid_kernel or self.config.pyramid_select != 'tail')
             x, rstd = _Block.apply(self.flat, x, self, l, s['in_len'], Kq, seed, training, rstd, select)
         return _Head.apply(self.flat, x, self)
 

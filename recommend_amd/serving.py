@@ -1,0 +1,194 @@
+"""Two-stage cached serving of a trained OneTrans model (paper §3.5.1 "cross-request KV cache").
+
+Reference: the inference engine ``examples/inference_example.py:21-219`` (one full forward per batch
+of (user, item, context, sequence) samples) and the model's KV-cache path ``model.py:94-98, 333,
+359-381, 395-397``, which is defective (D6: block i's K/V are fed to block i+1 and the causal mask is
+not offset by the cache length), so the cache semantics are re-derived from the paper:
+
+* stage I, once per request (user): the S tokens (sequences + [SEP]) run through every layer on their
+  own.  Tokens are ordered [S; NS] (model.py:235) and the mask is causal, so no S token ever sees an
+  NS token: the S-side hidden states, keys and values do not depend on the candidate.  Each layer's
+  S-side K/V rows are cached (``RequestCache``).
+* stage II, once per candidate: the NS tokens run through every layer; their queries attend to the
+  request's cached S-side K/V plus their own (``ot_attn_fwd_cached``).  Nothing S-side is recomputed.
+
+The result equals ``OneTransModel.forward`` on the expanded batch (each candidate paired with its
+request's sequences) up to fp32 summation order — tests/test_serving_gpu.py checks it against the
+model and the CPU oracle.  Pyramid keeps (tail, model.py:296/371 with the D2 fix) and the last-layer
+dead-code elimination carry over: at layer l the kept tail of K_l tokens splits into S rows (computed
+in stage I) and N rows (stage II).  Inference only (no dropout).  Positions restart in every layer,
+so every row's weight group is the one of its position in the full layer input
+(``layout.layer_maps(p0=, I_full=)``).
+
+Not covered (documented in DESIGN.md): the incremental cross-request update (appending new behaviours
+to a cached request) — with several concatenated sequences, [SEP] tokens and position-dependent weight
+groups, an appended event shifts later positions, so only a full stage I re-encode is exact here.
+"""
+
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import torch
+
+from . import kernels as K
+from ._lib import (OT_AX_GELU, OT_AX_RMSNORM, OT_EPI_BIAS, OT_EPI_RESIDUAL, OT_GEMM_NT, OneTransHipError)
+from .layout import layer_maps
+
+RMS_EPS = 1e-6
+
+
+class RequestCache:
+    """Stage-I output for R requests: per layer the S-side qkv rows [R*Ic, 3d] (k at col d, v at 2d)
+    and Ic, the number of S tokens in that layer's input."""
+
+    def __init__(self, R: int, L_S: int, layers: List[Dict]):
+        self.R, self.L_S, self.layers = R, L_S, layers
+
+
+class OneTransServer:
+    """Cached two-stage inference on a ``OneTransModel`` (weights shared, nothing copied)."""
+
+    def __init__(self, model):
+        self.m = model
+        cfg = model.config
+        if getattr(cfg, 'pyramid_select', 'tail') != 'tail':
+            raise ValueError("OneTransServer: pyramid_select must be 'tail' (a score-based keep would depend on "
+                             "the NS tokens' positions in every layer)")
+        self._maps = {}
+
+    # ------------------------------------------------------------------ schedule
+    def schedule(self, L_S: int) -> List[Dict]:
+        """Per layer: S rows s, N rows n, kept S rows kS, kept N rows kN (kS + kN = the layer's keep)."""
+        cfg = self.m.config
+        L_NS = cfg.num_ns_tokens
+        sched = cfg.pyramid_schedule(L_S + L_NS)
+        out, s, n = [], L_S, L_NS
+        for l, e in enumerate(sched):
+            keep = e['keep'] if l < len(sched) - 1 else 1        # only the last token is read (model.py:390)
+            kN = min(keep, n)
+            kS = keep - kN
+            out.append({'I': s + n, 's': s, 'n': n, 'kS': kS, 'kN': kN})
+            s, n = kS, kN
+        return out
+
+    def _layer_maps(self, B, I, Kq, p0, I_full):
+        key = (B, I, Kq, p0, I_full)
+        if key not in self._maps:
+            self._maps[key] = layer_maps(self.m.config, B, I, Kq, p0=p0, I_full=I_full)
+        return self._maps[key]
+
+    # ------------------------------------------------------------------ one block (forward only)
+    def _block(self, l: int, x: torch.Tensor, B: int, I: int, Kq: int, p0: int, I_full: int, attn):
+        """OneTransBlock.call (model.py:186-200) on B spans of I rows (positions p0.. of a layer of I_full
+        tokens), keeping the last Kq (0: only the K/V rows are produced).  Returns (x_next, qkv)."""
+        m = self.m
+        cfg = m.config
+        d, f = cfg.hidden_dim, cfg.ffn_dim
+        dev = x.device
+        mp = self._layer_maps(B, I, max(Kq, 1), p0, I_full)
+        ma, mt = mp['all'].to(dev), mp['tail'].to(dev)
+        na, nt = mp['all'].ntiles, mp['tail'].ntiles
+        wqkv, wo = m.pT(f'blk.{l}.wqkv'), m.pT(f'blk.{l}.wo')
+        w1, b1, w2, b2 = m.pT(f'blk.{l}.w1'), m.p(f'blk.{l}.b1'), m.pT(f'blk.{l}.w2'), m.p(f'blk.{l}.b2')
+        g1, g2 = m.p(f'blk.{l}.norm1'), m.p(f'blk.{l}.norm2')
+        rstd1 = torch.empty(B * I, device=dev)
+        K.rmsnorm_fwd(x, d, B * I, d, rstd1, eps=RMS_EPS)
+        qkv = torch.empty(B * I, 3 * d, device=dev)
+        # K/V for every row (weight cols d..3d of each group's [d, 3d] bank), Q for the kept rows
+        K.gemm(OT_GEMM_NT, x, d, d, ma['rows'][0], (wqkv, d * d), 3 * d * d, d, 2 * d, ma['tile_group'], na,
+               (qkv, d), 3 * d, ma['rows'][0], a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=mp['all'].nrows)
+        if Kq == 0:
+            return None, qkv
+        K.gemm(OT_GEMM_NT, x, d, d, mt['rows'][0], wqkv, 3 * d * d, d, d, mt['tile_group'], nt, qkv, 3 * d,
+               mt['rows'][0], a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=mp['tail'].nrows)
+        o = attn(qkv)                                                   # [B*Kq, d]
+        x1 = torch.empty(B * Kq, d, device=dev)
+        K.gemm(OT_GEMM_NT, o, d, d, mt['rows'][1], wo, 0, d, d, mt['tile_group'], nt, x1, d, mt['rows'][1],
+               epi=OT_EPI_RESIDUAL, res=x, ldres=d, res_tok=1, tail=(Kq, I), m_rows=mp['tail'].nrows)
+        rstd2 = torch.empty(B * Kq, device=dev)
+        K.rmsnorm_fwd(x1, d, B * Kq, d, rstd2, eps=RMS_EPS)
+        u = torch.empty(B * Kq, f, device=dev)
+        K.gemm(OT_GEMM_NT, x1, d, d, mt['rows'][1], w1, d * f, d, f, mt['tile_group'], nt, u, f, mt['rows'][1],
+               a_xform=OT_AX_RMSNORM, rstd=rstd2, gamma=g2, bias=b1, bias_gstride=f, epi=OT_EPI_BIAS,
+               m_rows=mp['tail'].nrows)
+        x2 = torch.empty(B * Kq, d, device=dev)
+        K.gemm(OT_GEMM_NT, u, f, f, mt['rows'][1], w2, f * d, f, d, mt['tile_group'], nt, x2, d, mt['rows'][1],
+               a_xform=OT_AX_GELU, bias=b2, bias_gstride=d, epi=OT_EPI_BIAS | OT_EPI_RESIDUAL, res=x1, ldres=d,
+               res_tok=0, tail=(Kq, I), m_rows=mp['tail'].nrows)
+        return x2, qkv
+
+    # ------------------------------------------------------------------ stage I
+    @torch.no_grad()
+    def encode_requests(self, seq_features: Dict[str, torch.Tensor]) -> RequestCache:
+        """Tokenize the requests' sequences (model.py:256-277) and run the S side of every layer;
+        cache each layer's S-side K/V."""
+        from .model import _Tokenize
+        m = self.m
+        cfg = m.config
+        d, H = cfg.hidden_dim, cfg.num_heads
+        hd = d // H
+        if not seq_features:
+            raise ValueError('encode_requests: no sequence features')
+        plan = m._plan({}, seq_features)
+        R, L0, L_S = plan['B'], plan['L0'], plan['L_S']
+        x0 = _Tokenize.apply(m.flat, m, plan)                             # NS rows zero (no NS features)
+        x = x0.view(R, L0, d)[:, :L_S].reshape(R * L_S, d)
+        layers = []
+        for l, e in enumerate(self.schedule(L_S)):
+            s, kS = e['s'], e['kS']
+            if s == 0:
+                layers.append({'Ic': 0, 'kv': None})
+                continue
+
+            def attn(qkv, s=s, kS=kS):
+                o = torch.empty(R * kS, d, device=qkv.device)
+                lse = torch.empty(R * H * kS, device=qkv.device)
+                K.attn_fwd(qkv, 3 * d, R, H, s, kS, hd, o, lse)           # S queries see S keys only
+                return o
+
+            x, qkv = self._block(l, x, R, s, kS, 0, e['I'], attn)
+            layers.append({'Ic': s, 'kv': qkv})
+        return RequestCache(R, L_S, layers)
+
+    # ------------------------------------------------------------------ stage II
+    @torch.no_grad()
+    def score(self, cache: RequestCache, req: torch.Tensor, non_seq_features: Dict[str, torch.Tensor]):
+        """Candidates' NS tokens (model.py:239-254) through every layer against their request's cache;
+        returns {task: probs [C, 1]} like ``OneTransModel.forward`` (model.py:384-391)."""
+        from .model import _Head, _Tokenize
+        m = self.m
+        cfg = m.config
+        d, H = cfg.hidden_dim, cfg.num_heads
+        hd = d // H
+        dev = m.device
+        plan = m._plan(non_seq_features, {})
+        C = plan['B']
+        req = req.to(dev, torch.int32).contiguous()
+        if req.numel() != C:
+            raise ValueError(f'score: {req.numel()} request indices for {C} candidates')
+        x = _Tokenize.apply(m.flat, m, plan)                              # [C*L_NS, d]: NS tokens only
+        for l, e in enumerate(self.schedule(cache.L_S)):
+            s, n, kN = e['s'], e['n'], e['kN']
+            lay = cache.layers[l]
+            if lay['Ic'] != s:
+                raise OneTransHipError('score: request cache does not match the schedule')
+
+            def attn(qkv, lay=lay, s=s, n=n, kN=kN):
+                o = torch.empty(C * kN, d, device=dev)
+                kv = (lay['kv'], d) if s > 0 else None
+                K.attn_fwd_cached(qkv, 3 * d, kv, 3 * d, req, C, H, s, n, kN, hd, o)
+                return o
+
+            x, _ = self._block(l, x, C, n, kN, s, e['I'], attn)
+        probs = _Head.apply(m.flat, x, m)                                  # [T, C]
+        return {t: probs[i].view(-1, 1) for i, t in enumerate(cfg.tasks)}
+
+    @torch.no_grad()
+    def predict(self, non_seq_features, seq_features, req: Optional[torch.Tensor] = None):
+        """One call: ``seq_features`` hold R requests, ``non_seq_features`` C candidates, ``req`` [C] maps
+        candidates to requests (default: candidate i belongs to request i, R == C)."""
+        cache = self.encode_requests(seq_features)
+        if req is None:
+            req = torch.arange(cache.R, dtype=torch.int32)
+        return self.score(cache, req, non_seq_features)

@@ -24,7 +24,7 @@ from .params import dense_param_shapes, keras_variables
 
 TILE = 128
 ALIGN = 64
-WGRAD_SLOTS = 768          # resident wgrad workgroups (3 per CU x 256 CUs): size chunks for one round
+WGRAD_SLOTS = int(__import__("os").environ.get("ONETRANS_WGRAD_SLOTS", "768"))   # resident wgrad workgroups (3 per CU x 256 CUs): size chunks for one round
 
 
 def round_up(x: int, m: int) -> int:
@@ -116,7 +116,10 @@ class RowMap:
         key = (tiles_per_chunk, str(device))
         if key not in self._chunk_cache:
             padded = [round_up(n, TILE) for n in self.group_rows]
-            budget = max(1, WGRAD_SLOTS // max(1, tiles_per_chunk))
+            # every nonempty group needs a chunk of its own: on top of them, the budget of one round
+            # (with as many groups as budget slots -- C5's 13 groups x 64 output tiles -- a budget of
+            # one round would leave the shared group a single chunk, 64 workgroups on 256 CUs)
+            budget = max(1, WGRAD_SLOTS // max(1, tiles_per_chunk)) + sum(1 for p in padded if p > 0)
             lo, hi = 32, max(32, round_up(max(padded) if padded else 32, 32))
             while lo < hi:
                 mid = round_up((lo + hi) // 2, 32)

@@ -339,6 +339,162 @@ __global__ __launch_bounds__(256) void attn_fwd_kv_kernel(AttnArgs p) {
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Split-bf16 forward (OT_MATMUL_SPLIT_BF16; HD >= 32): the same online softmax as attn_fwd_kernel,
+// the two products on v_mfma_f32_32x32x16_bf16 with every f32 operand split exactly into three bf16
+// planes and the six largest plane products summed (mfma_split6: f32-accurate, 2.7x fewer MFMA
+// cycles than the 32x32x2 f32 form).
+//   S^T = K Q^T: K (A, lane = key) and Q (B, lane = query) fragments split in registers; lane half
+//     hh, k-step t, element j <-> dim (HD/2) hh + 8t + j on both sides.
+//   O^T += V^T P^T: P^T is the S^T accumulator (k-step s = registers 8s..8s+7, element j <-> key
+//     16s + 8(j>>2) + 4hh + (j&3)); V^T comes from the wave's row-major bf16 V plane images through
+//     ds_read_b64_tr_b16 (4 key rows of the lane's dim column per read, two reads per k-step).
+template <int HD>
+__device__ __forceinline__ u32x4 vt_frag(const char* plane, int s, int c, int lane) {
+  // lane 4q+p of each 16-lane group addresses key row r0 + q, dims c0 + 4p .. c0 + 4p + 3
+  typedef short v4i16 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+  const int hh = lane >> 5, gi = lane & 15, q = gi >> 2, pp = gi & 3;
+  const int c0 = 32 * c + 16 * ((lane >> 4) & 1) + 4 * pp;
+  const int r0 = 16 * s + 4 * hh + q;
+  const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(plane + (r0 * HD + c0) * 2));
+  const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(plane + ((r0 + 8) * HD + c0) * 2));
+  const u32x2 a = __builtin_bit_cast(u32x2, lo), b = __builtin_bit_cast(u32x2, hi);
+  return u32x4{a.x, a.y, b.x, b.y};
+}
+
+template <int HD>
+__global__ __launch_bounds__(256) void attn_fwd_split_kernel(AttnArgs p) {
+  static_assert(HD >= 32, "split forward: HD >= 32");
+  constexpr int NS = HD / 16;                         // k-steps of S^T
+  constexpr int PLANE = 32 * HD * 2;                  // bytes of one V plane image [32 keys][HD] bf16
+  __shared__ __attribute__((aligned(16))) char lds[4][3 * PLANE];
+  const int lane = threadIdx.x & 63, li = lane & 31, hh = lane >> 5;
+  char* vimg = lds[threadIdx.x >> 6];
+  const int pair = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (pair >= p.B * p.H) return;
+  const int b = pair / p.H, h = pair % p.H;
+  const int I = p.I, K = p.K, q_off = I - K;
+  const float* Q = p.qkv + (int64_t)b * I * p.ld + h * HD;
+  const float* Kp = Q + p.d;
+  const float* V = Q + 2 * p.d;
+  const int32_t* qp = p.qpos ? p.qpos + (int64_t)b * K : nullptr;
+  const int nqb = (K + 31) / 32;
+  const float qscale = p.scale * 1.4426950408889634f;   // log2(e) / sqrt(hd)
+  for (int qb = 0; qb < nqb; ++qb) {
+    const int j = 32 * qb + li;
+    const int qpos = query_pos(qp, q_off, j < K ? j : K - 1);
+    u32x4 qs[NS][3];
+    {
+      float qf[HD / 2];
+      load_frag_clamped<HD>(qf, Q, p.ld, qpos, I, hh);
+#pragma unroll
+      for (int s = 0; s < HD / 2; ++s) qf[s] *= qscale;
+#pragma unroll
+      for (int t = 0; t < NS; ++t) split8(qf + 8 * t, qs[t]);
+    }
+    f32x16 oacc[NB(HD)];
+#pragma unroll
+    for (int c = 0; c < NB(HD); ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) oacc[c][r] = 0.f;
+    float m = -INFINITY, l = 0.f;
+    const int last_q = query_pos(qp, q_off, min(32 * qb + 31, K - 1));
+    const int nkb = last_q / 32 + 1;
+    const int first_masked = query_pos(qp, q_off, 32 * qb) / 32;
+    // K/V fragments of key block kb + 1 are loaded while block kb computes (the global latency
+    // would otherwise be exposed once per block)
+    float kf[HD / 2], vf[HD / 2];
+    load_frag<HD>(kf, Kp, p.ld, li, I, hh);
+    load_frag<HD>(vf, V, p.ld, li, I, hh);
+    for (int kb = 0; kb < nkb; ++kb) {
+      const int key0 = 32 * kb;
+      float kn[HD / 2], vn[HD / 2];
+      load_frag<HD>(kn, Kp, p.ld, kb + 1 < nkb ? key0 + 32 + li : I, I, hh);    // rows >= I: no load
+      load_frag<HD>(vn, V, p.ld, kb + 1 < nkb ? key0 + 32 + li : I, I, hh);
+      f32x16 sacc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
+      {
+        // V planes -> the wave's row-major images (row = key li, dims (HD/2) hh ..)
+#pragma unroll
+        for (int t = 0; t < NS; ++t) {
+          u32x4 vp[3];
+          split8(vf + 8 * t, vp);
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl)
+            *reinterpret_cast<u32x4*>(vimg + pl * PLANE + (li * HD + (HD / 2) * hh + 8 * t) * 2) = vp[pl];
+        }
+#pragma unroll
+        for (int t = 0; t < NS; ++t) {
+          u32x4 ks[3];
+          split8(kf + 8 * t, ks);
+          sacc = mfma_split6(ks, qs[t], sacc);         // S^T (log2 units): row = key, col = query
+        }
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < HD / 2; ++s2) { kf[s2] = kn[s2]; vf[s2] = vn[s2]; }
+      f32x16 s = sacc;
+      if (kb >= first_masked) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          s[r] = (key0 + acc_row(r, hh) <= qpos) ? s[r] : -INFINITY;
+      }
+      float mloc = s[0];
+#pragma unroll
+      for (int r = 1; r < 16; ++r) mloc = fmaxf(mloc, s[r]);
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+      const float mnew = fmaxf(m, mloc);
+      const float corr = __builtin_amdgcn_exp2f(m - mnew);
+      float lsum = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float e = __builtin_amdgcn_exp2f(s[r] - mnew);
+        s[r] = e;
+        lsum += e;
+      }
+      lsum += __shfl_xor(lsum, 32, 64);
+      l = l * corr + lsum;
+      m = mnew;
+#pragma unroll
+      for (int c = 0; c < NB(HD); ++c) oacc[c] *= corr;
+      u32x4 ps[2][3];
+      {
+        float pv[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) pv[r] = s[r];
+        split8(pv, ps[0]);
+        split8(pv + 8, ps[1]);
+      }
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int c = 0; c < NB(HD); ++c)
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          u32x4 va[3];
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl) va[pl] = vt_frag<HD>(vimg + pl * PLANE, st, c, lane);
+          oacc[c] = mfma_split6(va, ps[st], oacc[c]);   // O^T += V^T P^T
+        }
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (j < K) {
+      const float inv = 1.f / l;
+      float* orow = p.out + ((int64_t)b * K + j) * p.d + h * HD;
+#pragma unroll
+      for (int c = 0; c < NB(HD); ++c)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int dd = 32 * c + 8 * g + 4 * hh;
+          f32x4 v = {oacc[c][4 * g] * inv, oacc[c][4 * g + 1] * inv, oacc[c][4 * g + 2] * inv,
+                     oacc[c][4 * g + 3] * inv};
+          *reinterpret_cast<f32x4*>(orow + dd) = v;
+        }
+      if (hh == 0) p.lse[((int64_t)b * p.H + h) * K + j] = m * 0.6931471805599453f + __logf(l);
+    }
+  }
+}
+
 // Row statistics of the backward, padded to KP = round_up(K, 32) queries per (b, h) so the main
 // kernel reads them as aligned float4 without bounds checks:
 //   ws[0 .. BH*KP)       lse  (padding +inf: P = exp(s - inf) = 0 masks the padded queries)
@@ -834,7 +990,18 @@ extern "C" int ot_attn_fwd(const float* qkv, int64_t ld, int B, int H, int I, in
   AttnArgs p{qkv, ld, H * head_dim, nullptr, nullptr, out, lse, nullptr, nullptr, B, H, I, K,
              1.f / sqrtf((float)head_dim), qpos};
   const size_t kv_bytes = 2 * (size_t)((I + 31) / 32 * 32) * (head_dim + 4) * sizeof(float);
-  if (head_dim <= 64 && kv_bytes <= OT_ATTN_KV_LDS_MAX && (K + 31) / 32 >= 3) {
+  const bool kv_fits = head_dim <= 64 && kv_bytes <= OT_ATTN_KV_LDS_MAX && (K + 31) / 32 >= 3;
+  if (ot_get_matmul_mode() == OT_MATMUL_SPLIT_BF16 && head_dim >= 32 && !kv_fits) {
+    // long sequences: split-bf16 MFMA with the next key block prefetched (short ones stay on the
+    // shared-K/V f32 kernel below, which measures faster there: profiles/r01/attention_split.md)
+    const unsigned grid = ceil_div((int64_t)B * H, 4);
+    switch (head_dim) {
+      case 32: hipLaunchKernelGGL(attn_fwd_split_kernel<32>, dim3(grid), dim3(256), 0, (hipStream_t)stream, p); break;
+      case 64: hipLaunchKernelGGL(attn_fwd_split_kernel<64>, dim3(grid), dim3(256), 0, (hipStream_t)stream, p); break;
+      case 128: hipLaunchKernelGGL(attn_fwd_split_kernel<128>, dim3(grid), dim3(256), 0, (hipStream_t)stream, p); break;
+      default: return fail(OT_ERR_UNSUPPORTED, "attention: head_dim %d unsupported", head_dim);
+    }
+  } else if (kv_fits) {
     // short sequence: K/V of a head staged once in LDS, shared by 4 waves
     static std::once_flag once;
     std::call_once(once, [] {

@@ -11,8 +11,54 @@
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 namespace ot {
+
+// ---- split-bf16 arithmetic (OT_MATMUL_SPLIT_BF16) ------------------------------------
+// f32x4 -> three planes of 4 bf16 (each packed into 2 dwords, element 0 in the low half):
+// x = x0 + x1 + x2 exactly (x0 the top 8 significant bits, x1 the next 8, x2 the rest; truncation
+// keeps every step exact)
+__device__ __forceinline__ void split3(f32x4 v, u32x2& p0, u32x2& p1, u32x2& p2) {
+  uint32_t a[4], b[4], c[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float x = v[j];
+    const uint32_t u0 = __float_as_uint(x) & 0xffff0000u;
+    const float r1 = x - __uint_as_float(u0);
+    const uint32_t u1 = __float_as_uint(r1) & 0xffff0000u;
+    const float r2 = r1 - __uint_as_float(u1);
+    a[j] = u0; b[j] = u1; c[j] = __float_as_uint(r2);
+  }
+  p0 = u32x2{__builtin_amdgcn_perm(a[1], a[0], 0x07060302u), __builtin_amdgcn_perm(a[3], a[2], 0x07060302u)};
+  p1 = u32x2{__builtin_amdgcn_perm(b[1], b[0], 0x07060302u), __builtin_amdgcn_perm(b[3], b[2], 0x07060302u)};
+  p2 = u32x2{__builtin_amdgcn_perm(c[1], c[0], 0x07060302u), __builtin_amdgcn_perm(c[3], c[2], 0x07060302u)};
+}
+// 8 floats -> three planes of one 32x32x16 operand fragment (8 bf16 = 4 dwords each)
+__device__ __forceinline__ void split8(const float* v, u32x4 (&pl)[3]) {
+  u32x2 a0, a1, a2, b0, b1, b2;
+  split3(f32x4{v[0], v[1], v[2], v[3]}, a0, a1, a2);
+  split3(f32x4{v[4], v[5], v[6], v[7]}, b0, b1, b2);
+  pl[0] = u32x4{a0.x, a0.y, b0.x, b0.y};
+  pl[1] = u32x4{a1.x, a1.y, b1.x, b1.y};
+  pl[2] = u32x4{a2.x, a2.y, b2.x, b2.y};
+}
+__device__ __forceinline__ f32x16 mfma_bf16(u32x4 a, u32x4 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0,
+                                                  0);
+}
+// a.b over the six largest plane products (smallest first): the dropped a1.b2 + a2.b1 + a2.b2 is
+// below 2^-22 |a||b|, one f32 rounding of the product
+__device__ __forceinline__ f32x16 mfma_split6(const u32x4 (&a)[3], const u32x4 (&b)[3], f32x16 c) {
+  c = mfma_bf16(a[0], b[2], c);
+  c = mfma_bf16(a[2], b[0], c);
+  c = mfma_bf16(a[1], b[1], c);
+  c = mfma_bf16(a[0], b[1], c);
+  c = mfma_bf16(a[1], b[0], c);
+  return mfma_bf16(a[0], b[0], c);
+}
 
 // ---- error reporting (per host thread) ---------------------------------------------
 void set_error(const char* fmt, ...);

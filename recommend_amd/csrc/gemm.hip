@@ -56,30 +56,6 @@ constexpr int SPLIT_TERMS = OT_GEMM_SPLIT;
 constexpr int SRS = 3 * 16 + 8;   // split LDS row stride (ushorts): 3 planes x 16 k + pad = 112 B
 static_assert(SPLIT_TERMS == 3 || SPLIT_TERMS == 6 || SPLIT_TERMS == 9, "OT_GEMM_SPLIT");
 static_assert(GBK == 16, "split-bf16 staging assumes 16-k stages");
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-
-// f32x4 -> three planes of 4 bf16 (each packed into 2 dwords, element 0 in the low half)
-__device__ __forceinline__ void split3(f32x4 v, u32x2& p0, u32x2& p1, u32x2& p2) {
-  uint32_t a[4], b[4], c[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float x = v[j];
-    const uint32_t u0 = __float_as_uint(x) & 0xffff0000u;
-    const float r1 = x - __uint_as_float(u0);
-    const uint32_t u1 = __float_as_uint(r1) & 0xffff0000u;
-    const float r2 = r1 - __uint_as_float(u1);
-    a[j] = u0; b[j] = u1; c[j] = __float_as_uint(r2);
-  }
-  p0 = u32x2{__builtin_amdgcn_perm(a[1], a[0], 0x07060302u), __builtin_amdgcn_perm(a[3], a[2], 0x07060302u)};
-  p1 = u32x2{__builtin_amdgcn_perm(b[1], b[0], 0x07060302u), __builtin_amdgcn_perm(b[3], b[2], 0x07060302u)};
-  p2 = u32x2{__builtin_amdgcn_perm(c[1], c[0], 0x07060302u), __builtin_amdgcn_perm(c[3], c[2], 0x07060302u)};
-}
-__device__ __forceinline__ f32x16 mfma_bf16(u32x4 a, u32x4 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0,
-                                                  0);
-}
 
 struct GemmArgs {
   const float* A; int64_t lda; int K;

@@ -213,7 +213,8 @@ def main():
         'metric': 'ranked samples/sec (fwd+bwd) at B=4096 seq=128; AUC parity vs ref',
         'value': round(value, 1), 'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': round(1e3 * t / args.steps, 3), 'higher_is_better': True,
-        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
+        'scaling': 'weak', 'vs_baseline': None,
+        'dtype': 'bf16' if K.matmul_mode() == 'bf16' else 'f32', 'data': 'synthetic',
         'config': {'workload': f'{args.config}: OneTrans {cfg.num_layers}L d{cfg.hidden_dim} H{cfg.num_heads} f{cfg.ffn_dim} '
                                f'L_NS{cfg.num_ns_tokens} L_S{sum(seq_lens) + 2} (seq 3x{seq_lens[0]}), '
                                f'Criteo-shape 13 dense + 26 ids, replicated tables, fwd+bwd+optimizer',
@@ -231,6 +232,9 @@ def main():
             gpeak = round(BF16_MFMA_PEAK_TFLOPS / SPLIT_TERMS, 1)
             gkern = ('mixed_gemm_kernel + wgrad_split_kernel (f32 operands split exactly into 3 bf16 parts, '
                      f'{SPLIT_TERMS} bf16 MFMA products per f32 product; peak = bf16 dense / {SPLIT_TERMS})')
+        elif K.matmul_mode() == 'bf16':
+            gpeak = BF16_MFMA_PEAK_TFLOPS
+            gkern = 'mixed_gemm_kernel + wgrad_split_kernel (operands rounded to bf16, one bf16 MFMA product)'
         else:
             gpeak = FP32_MFMA_PEAK_TFLOPS
             gkern = 'mixed_gemm_kernel + wgrad_kernel (native f32 MFMA)'

@@ -77,9 +77,13 @@ int ot_gemm_tile_rows(void);
  *     the dropped a1.b2 + a2.b1 + a2.b2 is below 2^-22 |a||b|, one f32 rounding).  Error vs an
  *     f64 product measured no larger than native f32 (tools/split_gemm_check.py).
  *   OT_MATMUL_F32: native v_mfma_f32_32x32x2_f32.
+ *   OT_MATMUL_BF16: reduced precision (BASELINE C5's bf16 configuration, not the reference's f32):
+ *     operands rounded to bf16 (nearest even), one v_mfma_f32_32x32x16_bf16 product, f32
+ *     accumulation; attention forward likewise (its backward stays f32-accurate).
  * Keras computes these Dense layers in f32 (model.py:38-57, 136-147; default float32 policy). */
 #define OT_MATMUL_F32 0
 #define OT_MATMUL_SPLIT_BF16 1
+#define OT_MATMUL_BF16 2
 int ot_set_matmul_mode(int mode);
 int ot_get_matmul_mode(void);
 int ot_mixed_gemm(int mode, const float* A, int64_t lda, int K, const int32_t* in_rows,

@@ -363,7 +363,7 @@ __device__ __forceinline__ u32x4 vt_frag(const char* plane, int s, int c, int la
   return u32x4{a.x, a.y, b.x, b.y};
 }
 
-template <int HD>
+template <int HD, int TERMS>
 __global__ __launch_bounds__(256) void attn_fwd_split_kernel(AttnArgs p) {
   static_assert(HD >= 32, "split forward: HD >= 32");
   constexpr int NS = HD / 16;                         // k-steps of S^T
@@ -391,7 +391,7 @@ __global__ __launch_bounds__(256) void attn_fwd_split_kernel(AttnArgs p) {
 #pragma unroll
       for (int s = 0; s < HD / 2; ++s) qf[s] *= qscale;
 #pragma unroll
-      for (int t = 0; t < NS; ++t) split8(qf + 8 * t, qs[t]);
+      for (int t = 0; t < NS; ++t) split8t<TERMS>(qf + 8 * t, qs[t]);
     }
     f32x16 oacc[NB(HD)];
 #pragma unroll
@@ -420,16 +420,16 @@ __global__ __launch_bounds__(256) void attn_fwd_split_kernel(AttnArgs p) {
 #pragma unroll
         for (int t = 0; t < NS; ++t) {
           u32x4 vp[3];
-          split8(vf + 8 * t, vp);
+          split8t<TERMS>(vf + 8 * t, vp);
 #pragma unroll
-          for (int pl = 0; pl < 3; ++pl)
+          for (int pl = 0; pl < (TERMS == 1 ? 1 : 3); ++pl)
             *reinterpret_cast<u32x4*>(vimg + pl * PLANE + (li * HD + (HD / 2) * hh + 8 * t) * 2) = vp[pl];
         }
 #pragma unroll
         for (int t = 0; t < NS; ++t) {
           u32x4 ks[3];
-          split8(kf + 8 * t, ks);
-          sacc = mfma_split6(ks, qs[t], sacc);         // S^T (log2 units): row = key, col = query
+          split8t<TERMS>(kf + 8 * t, ks);
+          sacc = mfma_terms<TERMS>(ks, qs[t], sacc);         // S^T (log2 units): row = key, col = query
         }
       }
 #pragma unroll
@@ -463,8 +463,8 @@ __global__ __launch_bounds__(256) void attn_fwd_split_kernel(AttnArgs p) {
         float pv[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) pv[r] = s[r];
-        split8(pv, ps[0]);
-        split8(pv + 8, ps[1]);
+        split8t<TERMS>(pv, ps[0]);
+        split8t<TERMS>(pv + 8, ps[1]);
       }
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -473,8 +473,8 @@ __global__ __launch_bounds__(256) void attn_fwd_split_kernel(AttnArgs p) {
         for (int st = 0; st < 2; ++st) {
           u32x4 va[3];
 #pragma unroll
-          for (int pl = 0; pl < 3; ++pl) va[pl] = vt_frag<HD>(vimg + pl * PLANE, st, c, lane);
-          oacc[c] = mfma_split6(va, ps[st], oacc[c]);   // O^T += V^T P^T
+          for (int pl = 0; pl < (TERMS == 1 ? 1 : 3); ++pl) va[pl] = vt_frag<HD>(vimg + pl * PLANE, st, c, lane);
+          oacc[c] = mfma_terms<TERMS>(va, ps[st], oacc[c]);   // O^T += V^T P^T
         }
       __builtin_amdgcn_wave_barrier();
     }
@@ -991,16 +991,21 @@ extern "C" int ot_attn_fwd(const float* qkv, int64_t ld, int B, int H, int I, in
              1.f / sqrtf((float)head_dim), qpos};
   const size_t kv_bytes = 2 * (size_t)((I + 31) / 32 * 32) * (head_dim + 4) * sizeof(float);
   const bool kv_fits = head_dim <= 64 && kv_bytes <= OT_ATTN_KV_LDS_MAX && (K + 31) / 32 >= 3;
-  if (ot_get_matmul_mode() == OT_MATMUL_SPLIT_BF16 && head_dim >= 32 && !kv_fits) {
-    // long sequences: split-bf16 MFMA with the next key block prefetched (short ones stay on the
-    // shared-K/V f32 kernel below, which measures faster there: profiles/r01/attention_split.md)
+  const int mm = ot_get_matmul_mode();
+  if (head_dim >= 32 && (mm == OT_MATMUL_BF16 || (mm == OT_MATMUL_SPLIT_BF16 && !kv_fits))) {
+    // split-bf16: long sequences, with the next key block prefetched (short ones stay on the
+    // shared-K/V f32 kernel below, which measures faster there: profiles/r01/attention_split.md);
+    // bf16 mode: one rounded plane, every length
     const unsigned grid = ceil_div((int64_t)B * H, 4);
+    void (*kern)(AttnArgs) = nullptr;
+    const bool one = mm == OT_MATMUL_BF16;
     switch (head_dim) {
-      case 32: hipLaunchKernelGGL(attn_fwd_split_kernel<32>, dim3(grid), dim3(256), 0, (hipStream_t)stream, p); break;
-      case 64: hipLaunchKernelGGL(attn_fwd_split_kernel<64>, dim3(grid), dim3(256), 0, (hipStream_t)stream, p); break;
-      case 128: hipLaunchKernelGGL(attn_fwd_split_kernel<128>, dim3(grid), dim3(256), 0, (hipStream_t)stream, p); break;
+      case 32: kern = one ? attn_fwd_split_kernel<32, 1> : attn_fwd_split_kernel<32, 6>; break;
+      case 64: kern = one ? attn_fwd_split_kernel<64, 1> : attn_fwd_split_kernel<64, 6>; break;
+      case 128: kern = one ? attn_fwd_split_kernel<128, 1> : attn_fwd_split_kernel<128, 6>; break;
       default: return fail(OT_ERR_UNSUPPORTED, "attention: head_dim %d unsupported", head_dim);
     }
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, (hipStream_t)stream, p);
   } else if (kv_fits) {
     // short sequence: K/V of a head staged once in LDS, shared by 4 waves
     static std::once_flag once;

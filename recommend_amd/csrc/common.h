@@ -45,6 +45,26 @@ __device__ __forceinline__ void split8(const float* v, u32x4 (&pl)[3]) {
   pl[1] = u32x4{a1.x, a1.y, b1.x, b1.y};
   pl[2] = u32x4{a2.x, a2.y, b2.x, b2.y};
 }
+// f32x4 -> 4 bf16 rounded to nearest even (OT_MATMUL_BF16: the one-plane form), packed like split3
+__device__ __forceinline__ u32x2 bf16_rne4(f32x4 v) {
+  uint32_t r[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t u = __float_as_uint(v[j]);
+    r[j] = u + 0x7fffu + ((u >> 16) & 1u);               // finite inputs (activations / weights)
+  }
+  return u32x2{__builtin_amdgcn_perm(r[1], r[0], 0x07060302u), __builtin_amdgcn_perm(r[3], r[2], 0x07060302u)};
+}
+// TERMS = 6: split8; TERMS = 1: plane 0 = the rounded bf16 (planes 1, 2 unused)
+template <int TERMS>
+__device__ __forceinline__ void split8t(const float* v, u32x4 (&pl)[3]) {
+  if constexpr (TERMS == 1) {
+    const u32x2 a = bf16_rne4(f32x4{v[0], v[1], v[2], v[3]}), b = bf16_rne4(f32x4{v[4], v[5], v[6], v[7]});
+    pl[0] = u32x4{a.x, a.y, b.x, b.y};
+  } else {
+    split8(v, pl);
+  }
+}
 __device__ __forceinline__ f32x16 mfma_bf16(u32x4 a, u32x4 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0,
                                                   0);
@@ -58,6 +78,11 @@ __device__ __forceinline__ f32x16 mfma_split6(const u32x4 (&a)[3], const u32x4 (
   c = mfma_bf16(a[0], b[1], c);
   c = mfma_bf16(a[1], b[0], c);
   return mfma_bf16(a[0], b[0], c);
+}
+template <int TERMS>
+__device__ __forceinline__ f32x16 mfma_terms(const u32x4 (&a)[3], const u32x4 (&b)[3], f32x16 c) {
+  if constexpr (TERMS == 1) return mfma_bf16(a[0], b[0], c);
+  else return mfma_split6(a, b, c);
 }
 
 // ---- error reporting (per host thread) ---------------------------------------------

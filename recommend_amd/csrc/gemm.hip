@@ -55,6 +55,8 @@ constexpr int GLD = GBK + 4;      // LDS row stride (floats)
 constexpr int SPLIT_TERMS = OT_GEMM_SPLIT;
 constexpr int SRS = 3 * 16 + 8;   // split LDS row stride (ushorts): 3 planes x 16 k + pad = 112 B
 static_assert(SPLIT_TERMS == 3 || SPLIT_TERMS == 6 || SPLIT_TERMS == 9, "OT_GEMM_SPLIT");
+// SPLT template argument of the split kernels: 0 = native f32 MFMA, SPLIT_TERMS = split-bf16,
+// 1 = OT_MATMUL_BF16 (one bf16 plane rounded to nearest: bf16 MFMA on f32 data, f32 accumulation)
 static_assert(GBK == 16, "split-bf16 staging assumes 16-k stages");
 
 struct GemmArgs {
@@ -107,14 +109,15 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 // EDGE: K % 32 != 0 or N % 128 != 0 (bounds checks in staging and epilogue).
 // SPLT: split-bf16 MFMA (NT only; the main loop's LDS images and register sets limit it to 2
 // workgroups per CU), else native f32 MFMA.
-template <bool NT, int AXT, int EPIT, bool EDGE, bool SPLT>
+template <bool NT, int AXT, int EPIT, bool EDGE, int SPLT>
 __global__ __launch_bounds__(256, (NT && SPLT) ? 2 : OT_GEMM_MINWG) void mixed_gemm_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* As = smem;                      // [2][GT][GLD]
   float* Bs = smem + 2 * GT * GLD;       // [2][GT][GLD]
   const int ax = AXT >= 0 ? AXT : p.a_xform;
   const int epi = EPIT >= 0 ? EPIT : p.epi;
-  constexpr bool SPL = NT && SPLT;
+  constexpr bool SPL = NT && SPLT != 0;
+  constexpr int TERMS = SPLT;
 
   const int nwg = p.ntm * p.ntn;
   const int wg = xcd_remap(blockIdx.x, nwg);
@@ -253,9 +256,14 @@ __global__ __launch_bounds__(256, (NT && SPLT) ? 2 : OT_GEMM_MINWG) void mixed_g
           v.x = gelu_erf(v.x); v.y = gelu_erf(v.y); v.z = gelu_erf(v.z); v.w = gelu_erf(v.w);
         }
         if (!(aok[i] && st.kin)) v = zero4;
-        split3(v, q.a[i][0], q.a[i][1], q.a[i][2]);
         const f32x4 w = (bok[i] && st.kin) ? st.b[i] : zero4;
-        split3(w, q.b[i][0], q.b[i][1], q.b[i][2]);
+        if constexpr (TERMS == 1) {
+          q.a[i][0] = bf16_rne4(v);
+          q.b[i][0] = bf16_rne4(w);
+        } else {
+          split3(v, q.a[i][0], q.a[i][1], q.a[i][2]);
+          split3(w, q.b[i][0], q.b[i][1], q.b[i][2]);
+        }
       }
     };
     auto swrite = [&](const SPlanes& q, int buf) {
@@ -264,7 +272,7 @@ __global__ __launch_bounds__(256, (NT && SPLT) ? 2 : OT_GEMM_MINWG) void mixed_g
 #pragma unroll
       for (int i = 0; i < NPASS; ++i)
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) {
+        for (int pl = 0; pl < (TERMS == 1 ? 1 : 3); ++pl) {
           *reinterpret_cast<u32x2*>(as16 + (sr + RPP * i) * SRS + 16 * pl + 4 * sc) = q.a[i][pl];
           *reinterpret_cast<u32x2*>(bs16 + (sr + RPP * i) * SRS + 16 * pl + 4 * sc) = q.b[i][pl];
         }
@@ -276,7 +284,7 @@ __global__ __launch_bounds__(256, (NT && SPLT) ? 2 : OT_GEMM_MINWG) void mixed_g
 #pragma unroll
       for (int m = 0; m < 2; ++m)
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
+        for (int q = 0; q < (TERMS == 1 ? 1 : 3); ++q) {
           fa[m][q] = *reinterpret_cast<const u32x4*>(as16 + 32 * m * SRS + 16 * q);
           fb[m][q] = *reinterpret_cast<const u32x4*>(bs16 + 32 * m * SRS + 16 * q);
         }
@@ -285,6 +293,10 @@ __global__ __launch_bounds__(256, (NT && SPLT) ? 2 : OT_GEMM_MINWG) void mixed_g
       for (int m = 0; m < 2; ++m)
 #pragma unroll
         for (int n = 0; n < 2; ++n) {
+          if constexpr (TERMS == 1) {
+            acc[m][n] = mfma_bf16(fa[m][0], fb[n][0], acc[m][n]);
+            continue;
+          }
           if (SPLIT_TERMS >= 9) {
             acc[m][n] = mfma_bf16(fa[m][2], fb[n][2], acc[m][n]);
             acc[m][n] = mfma_bf16(fa[m][1], fb[n][2], acc[m][n]);
@@ -748,7 +760,7 @@ __device__ __forceinline__ v4i16 ds_tr16(const char* base, int off) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + off));
 }
 
-template <int AXT>
+template <int AXT, int TERMS>
 __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(WgradArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem_c[];
   const int ax = AXT >= 0 ? AXT : p.a_xform;
@@ -814,6 +826,11 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(WgradArgs p) {
       if (!(inr && n0 + 4 * cc < p.N)) dv = zero4;
       if (do_bias) bsum[i] += dv;
       const int off = wsw_off(sr, cc >> 1) + 8 * (cc & 1);
+      if constexpr (TERMS == 1) {
+        *reinterpret_cast<u32x2*>(As + off) = bf16_rne4(a);
+        *reinterpret_cast<u32x2*>(Ds + off) = bf16_rne4(dv);
+        continue;
+      }
       u32x2 q0, q1, q2;
       split3(a, q0, q1, q2);
       *reinterpret_cast<u32x2*>(As + off) = q0;
@@ -858,7 +875,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(WgradArgs p) {
 #pragma unroll
       for (int m = 0; m < 2; ++m)
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) {
+        for (int pl = 0; pl < (TERMS == 1 ? 1 : 3); ++pl) {
           const int po = pl * WSPLANE + t2 * 16 * 256;   // row r -> r + 16 keeps the swizzle (r & 15)
           const v4i16 a0 = ds_tr16(As + po, aoff[m][0]), a1 = ds_tr16(As + po, aoff[m][1]);
           const v4i16 d0 = ds_tr16(Ds + po, doff[m][0]), d1 = ds_tr16(Ds + po, doff[m][1]);
@@ -871,6 +888,10 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(WgradArgs p) {
       for (int m = 0; m < 2; ++m)
 #pragma unroll
         for (int n = 0; n < 2; ++n) {
+          if constexpr (TERMS == 1) {
+            acc[m][n] = mfma_bf16(fa[m][0], fb[n][0], acc[m][n]);
+            continue;
+          }
           if (SPLIT_TERMS >= 9) {
             acc[m][n] = mfma_bf16(fa[m][2], fb[n][2], acc[m][n]);
             acc[m][n] = mfma_bf16(fa[m][1], fb[n][2], acc[m][n]);
@@ -998,7 +1019,8 @@ static int g_matmul_mode = OT_MATMUL_SPLIT_BF16;
 using namespace ot;
 
 extern "C" int ot_set_matmul_mode(int mode) {
-  OT_REQUIRE(mode == OT_MATMUL_F32 || mode == OT_MATMUL_SPLIT_BF16, "ot_set_matmul_mode: unknown mode %d", mode);
+  OT_REQUIRE(mode == OT_MATMUL_F32 || mode == OT_MATMUL_SPLIT_BF16 || mode == OT_MATMUL_BF16,
+             "ot_set_matmul_mode: unknown mode %d", mode);
   g_matmul_mode = mode;
   return OT_OK;
 }
@@ -1076,7 +1098,8 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
     p.drop_thr = drop_threshold(drop_rate);
     p.drop_scale = 1.f / (1.f - drop_rate);
   }
-  const bool split = g_matmul_mode == OT_MATMUL_SPLIT_BF16 && mode == OT_GEMM_NT;
+  const bool split = g_matmul_mode != OT_MATMUL_F32 && mode == OT_GEMM_NT;
+  const bool one = g_matmul_mode == OT_MATMUL_BF16;
   const size_t shmem = split ? 4 * GT * SRS * sizeof(uint16_t) : 4 * GT * GLD * sizeof(float);
   auto a16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
   const bool vec_ok = ldc % 4 == 0 && a16(C) && (!(epi & OT_EPI_RESIDUAL) || (ldres % 4 == 0 && a16(res))) &&
@@ -1090,8 +1113,10 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
   const int e = epi, x = a_xform;
 #define OT_SPEC(NT_, AX_, EP_)                                                                  \
   if (mode == (NT_ ? OT_GEMM_NT : OT_GEMM_NN) && x == AX_ && e == (EP_))                         \
-    kern = split ? (edge ? mixed_gemm_kernel<NT_, AX_, EP_, true, true> : mixed_gemm_kernel<NT_, AX_, EP_, false, true>) \
-                 : (edge ? mixed_gemm_kernel<NT_, AX_, EP_, true, false> : mixed_gemm_kernel<NT_, AX_, EP_, false, false>);
+    kern = split ? (one ? (edge ? mixed_gemm_kernel<NT_, AX_, EP_, true, 1> : mixed_gemm_kernel<NT_, AX_, EP_, false, 1>) \
+                        : (edge ? mixed_gemm_kernel<NT_, AX_, EP_, true, SPLIT_TERMS>                         \
+                                : mixed_gemm_kernel<NT_, AX_, EP_, false, SPLIT_TERMS>))                      \
+                 : (edge ? mixed_gemm_kernel<NT_, AX_, EP_, true, 0> : mixed_gemm_kernel<NT_, AX_, EP_, false, 0>);
   OT_SPEC(true, OT_AX_RMSNORM, 0)
   OT_SPEC(true, OT_AX_RMSNORM, OT_EPI_BIAS)
   OT_SPEC(true, OT_AX_GELU, OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_DROPOUT)
@@ -1111,19 +1136,23 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
 #undef OT_SPEC
   OT_REQUIRE(kern || !rms_flags, "ot_mixed_gemm_rms: no specialised kernel for epilogue flags %d", epi);
   if (!kern) {   // any other combination: generic instantiation (run-time prologue/epilogue)
-    if (mode == OT_GEMM_NT && split)
-      kern = edge ? mixed_gemm_kernel<true, -1, -1, true, true> : mixed_gemm_kernel<true, -1, -1, false, true>;
+    if (mode == OT_GEMM_NT && split && one)
+      kern = edge ? mixed_gemm_kernel<true, -1, -1, true, 1> : mixed_gemm_kernel<true, -1, -1, false, 1>;
+    else if (mode == OT_GEMM_NT && split)
+      kern = edge ? mixed_gemm_kernel<true, -1, -1, true, SPLIT_TERMS> : mixed_gemm_kernel<true, -1, -1, false, SPLIT_TERMS>;
     else if (mode == OT_GEMM_NT)
-      kern = edge ? mixed_gemm_kernel<true, -1, -1, true, false> : mixed_gemm_kernel<true, -1, -1, false, false>;
+      kern = edge ? mixed_gemm_kernel<true, -1, -1, true, 0> : mixed_gemm_kernel<true, -1, -1, false, 0>;
     else
-      kern = edge ? mixed_gemm_kernel<false, -1, -1, true, false> : mixed_gemm_kernel<false, -1, -1, false, false>;
+      kern = edge ? mixed_gemm_kernel<false, -1, -1, true, 0> : mixed_gemm_kernel<false, -1, -1, false, 0>;
   }
   static std::once_flag lds_once;   // opt every instantiation in to > 64 KiB LDS (gfx950: 160 KiB per CU)
   std::call_once(lds_once, [] {
     const int bytes = (int)std::max(4 * GT * GLD * sizeof(float), 4 * GT * SRS * sizeof(uint16_t));
-    for (void (*k)(GemmArgs) : {mixed_gemm_kernel<true, -1, -1, true, false>, mixed_gemm_kernel<true, -1, -1, false, false>,
-                                mixed_gemm_kernel<false, -1, -1, true, false>, mixed_gemm_kernel<false, -1, -1, false, false>,
-                                mixed_gemm_kernel<true, -1, -1, true, true>, mixed_gemm_kernel<true, -1, -1, false, true>})
+    for (void (*k)(GemmArgs) : {mixed_gemm_kernel<true, -1, -1, true, 0>, mixed_gemm_kernel<true, -1, -1, false, 0>,
+                                mixed_gemm_kernel<false, -1, -1, true, 0>, mixed_gemm_kernel<false, -1, -1, false, 0>,
+                                mixed_gemm_kernel<true, -1, -1, true, SPLIT_TERMS>,
+                                mixed_gemm_kernel<true, -1, -1, false, SPLIT_TERMS>,
+                                mixed_gemm_kernel<true, -1, -1, true, 1>, mixed_gemm_kernel<true, -1, -1, false, 1>})
       (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     (void)hipGetLastError();
   });
@@ -1194,12 +1223,17 @@ extern "C" int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a
     WgradArgs p{A, lda, a_rows, a_xform, a_rstd, a_gamma, D, ldd, d_rows, K, N, chunks, nchunks, slab, bslab,
                 (int)ceil_div(K, GT), (int)ceil_div(N, GT)};
     const size_t shmem = (OT_WGRAD_DBUF ? 4 : 2) * WBR * WLD * sizeof(float);
-    const bool split = g_matmul_mode == OT_MATMUL_SPLIT_BF16;
+    const bool split = g_matmul_mode != OT_MATMUL_F32;
     void (*kern)(WgradArgs) =
-        split ? (a_xform == OT_AX_NONE      ? wgrad_split_kernel<OT_AX_NONE>
-                 : a_xform == OT_AX_RMSNORM ? wgrad_split_kernel<OT_AX_RMSNORM>
-                 : a_xform == OT_AX_GELU    ? wgrad_split_kernel<OT_AX_GELU>
-                                            : wgrad_split_kernel<-1>)
+        g_matmul_mode == OT_MATMUL_BF16
+            ? (a_xform == OT_AX_NONE      ? wgrad_split_kernel<OT_AX_NONE, 1>
+               : a_xform == OT_AX_RMSNORM ? wgrad_split_kernel<OT_AX_RMSNORM, 1>
+               : a_xform == OT_AX_GELU    ? wgrad_split_kernel<OT_AX_GELU, 1>
+                                          : wgrad_split_kernel<-1, 1>)
+        : split ? (a_xform == OT_AX_NONE      ? wgrad_split_kernel<OT_AX_NONE, SPLIT_TERMS>
+                 : a_xform == OT_AX_RMSNORM ? wgrad_split_kernel<OT_AX_RMSNORM, SPLIT_TERMS>
+                 : a_xform == OT_AX_GELU    ? wgrad_split_kernel<OT_AX_GELU, SPLIT_TERMS>
+                                            : wgrad_split_kernel<-1, SPLIT_TERMS>)
               : (a_xform == OT_AX_NONE      ? wgrad_kernel<OT_AX_NONE>
                  : a_xform == OT_AX_RMSNORM ? wgrad_kernel<OT_AX_RMSNORM>
                  : a_xform == OT_AX_GELU    ? wgrad_kernel<OT_AX_GELU>

@@ -487,3 +487,40 @@ def test_transpose_banks(dev):
     for (r, a) in zip(recs, srcs):
         got = dst[r[1]:r[1] + a.numel()].cpu().view(a.shape[0], a.shape[2], a.shape[1])
         assert torch.equal(got, a.transpose(1, 2))
+
+
+def test_bf16_mode_bounds(dev):
+    """OT_MATMUL_BF16 (BASELINE C5's reduced-precision mode): GEMM, wgrad and attention forward
+    errors stay within the bf16 rounding bound (operands rounded to 8 significant bits: relative
+    error per product <= 2^-8, so |err| <= 2^-8 sum|a||b| + f32 accumulation)."""
+    g = torch.Generator().manual_seed(3)
+    M, K_, N = 4096, 256, 384
+    A = torch.randn(M, K_, generator=g)
+    W = torch.randn(N, K_, generator=g) * 0.05
+    old = K.set_matmul_mode('bf16')
+    try:
+        C = torch.empty(M, N, device=dev)
+        K.gemm(OT_GEMM_NT, A.to(dev), K_, K_, None, W.to(dev), 0, K_, N, None, M // 128, C, N, None)
+        ref = A.double() @ W.double().T
+        e = (C.double().cpu() - ref).abs() / (A.double().abs() @ W.double().abs().T)
+        assert e.max() < 2 ** -8 and e.mean() > 1e-6, float(e.max())      # reduced, but bounded
+        # weight gradient (identity row map)
+        from recommend_amd import layout
+        D = torch.randn(M, N, generator=g)
+        dW = torch.empty(K_, N, device=dev)
+        K.wgrad(A.to(dev), K_, None, D.to(dev), N, None, K_, N, None, 0, 1, dW, 0, device=dev, m_rows=M,
+                rowmap=layout.identity_map(M))
+        refw = A.double().T @ D.double()
+        ew = (dW.double().cpu() - refw).abs() / (A.double().abs().T @ D.double().abs())
+        assert ew.max() < 2 ** -8, float(ew.max())
+        # attention forward (bf16 MFMA, f32 softmax)
+        B, H, I, Kq, hd = 2, 2, 150, 150, 64
+        d = H * hd
+        qkv = torch.randn(B * I, 3 * d, dtype=torch.float64, generator=g)
+        out = torch.empty(B * Kq, d, device=dev)
+        lse = torch.empty(B * H * Kq, device=dev)
+        K.attn_fwd(qkv.float().to(dev), 3 * d, B, H, I, Kq, hd, out, lse)
+        ref = attn_ref(qkv, B, H, I, Kq, hd)
+        assert (out.double().cpu() - ref).abs().max() < 3e-2
+    finally:
+        K.set_matmul_mode(old)

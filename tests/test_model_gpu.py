@@ -183,3 +183,25 @@ def test_fused_norms_match_unfused(dev):
     assert abs(res[0][0] - res[1][0]) < 1e-5
     scale = res[1][1].abs().max().item()
     assert (res[0][1] - res[1][1]).abs().max().item() / scale < 1e-5
+
+
+def test_bf16_mode_forward_and_train(dev):
+    """OT_MATMUL_BF16 (C5's bf16 configuration; reduced precision, so a bf16 tolerance, not the f32
+    north_star bound): probabilities within 2e-2 of the f64 oracle, and training steps stay finite."""
+    from recommend_amd import kernels as K
+    cfg = small_criteo('tail', pyramid=True, layers=3, d=128, H=4, f=256, Lns=12, seq_lens=(20, 20, 20))
+    old = K.set_matmul_mode('bf16')
+    try:
+        P, model, batch = setup(cfg, 37, dev)
+        ns, seq, lab = batch
+        with torch.no_grad():
+            out = model((ns_t(ns, dev), ns_t(seq, dev)), training=False)
+        ref = oracle_out(P, cfg, batch)
+        for t in cfg.tasks:
+            np.testing.assert_allclose(out[t].double().cpu().numpy(), ref['probs'][t].numpy(), atol=2e-2, rtol=0)
+        tr = OneTransTrainer(cfg, model=model)
+        for _ in range(2):
+            o = tr.train_step(batch)
+        assert torch.isfinite(o['total_loss']).item()
+    finally:
+        K.set_matmul_mode(old)

@@ -992,9 +992,9 @@ extern "C" int ot_attn_fwd(const float* qkv, int64_t ld, int B, int H, int I, in
   const size_t kv_bytes = 2 * (size_t)((I + 31) / 32 * 32) * (head_dim + 4) * sizeof(float);
   const bool kv_fits = head_dim <= 64 && kv_bytes <= OT_ATTN_KV_LDS_MAX && (K + 31) / 32 >= 3;
   const int mm = ot_get_matmul_mode();
-  if (head_dim >= 32 && (mm == OT_MATMUL_BF16 || (mm == OT_MATMUL_SPLIT_BF16 && !kv_fits))) {
-    // split-bf16: long sequences, with the next key block prefetched (short ones stay on the
-    // shared-K/V f32 kernel below, which measures faster there: profiles/r01/attention_split.md);
+  if (head_dim >= 32 && (mm == OT_MATMUL_BF16 || (mm == OT_MATMUL_SPLIT_BF16 && !kv_fits && I > 256))) {
+    // split-bf16: long sequences (I > 256), with the next key block prefetched (short ones stay on
+    // the f32 kernels below, which measure faster there: profiles/r01/attention_split.md);
     // bf16 mode: one rounded plane, every length
     const unsigned grid = ceil_div((int64_t)B * H, 4);
     void (*kern)(AttnArgs) = nullptr;

@@ -199,7 +199,9 @@ def attn_ref(qkv, B, H, I, Kq, hd):
                                          (2, 4, 140, 3, 32), (2, 2, 70, 4, 64), (2, 2, 33, 2, 128),
                                          (3, 4, 40, 1, 16), (2, 4, 5, 5 - 1, 32),
                                          # shared-K/V forward (>= 3 query blocks, K/V fit in LDS)
-                                         (2, 4, 100, 96, 32), (2, 2, 150, 150, 64), (3, 4, 130, 70, 16)])
+                                         (2, 4, 100, 96, 32), (2, 2, 150, 150, 64), (3, 4, 130, 70, 16),
+                                         # split-bf16 forward (I > 256, K/V beyond the shared-K/V LDS)
+                                         (2, 4, 300, 300, 32), (1, 2, 300, 137, 64), (1, 2, 290, 100, 128)])
 def test_attention(dev, B, H, I, Kq, hd):
     torch.manual_seed(0)
     d = H * hd

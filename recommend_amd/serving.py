@@ -20,9 +20,10 @@ in stage I) and N rows (stage II).  Inference only (no dropout).  Positions rest
 so every row's weight group is the one of its position in the full layer input
 (``layout.layer_maps(p0=, I_full=)``).
 
-Not covered (documented in DESIGN.md): the incremental cross-request update (appending new behaviours
-to a cached request) — with several concatenated sequences, [SEP] tokens and position-dependent weight
-groups, an appended event shifts later positions, so only a full stage I re-encode is exact here.
+Cross-request reuse (``extend_requests``): new behaviours appended to the LAST configured sequence
+extend the S side at its end, so with no pruning before the last layer only the new tokens are computed
+(their queries over the cached K/V).  Appends anywhere else shift later positions (later sequences,
+[SEP] tokens, position-grouped weights) and need a full stage-I re-encode; that case raises.
 """
 
 from __future__ import annotations
@@ -42,8 +43,9 @@ class RequestCache:
     """Stage-I output for R requests: per layer the S-side qkv rows [R*Ic, 3d] (k at col d, v at 2d)
     and Ic, the number of S tokens in that layer's input."""
 
-    def __init__(self, R: int, L_S: int, layers: List[Dict]):
+    def __init__(self, R: int, L_S: int, layers: List[Dict], present=()):
         self.R, self.L_S, self.layers = R, L_S, layers
+        self.present = tuple(present)          # sequence names present in the requests, config order
 
 
 class OneTransServer:
@@ -149,7 +151,59 @@ class OneTransServer:
 
             x, qkv = self._block(l, x, R, s, kS, 0, e['I'], attn)
             layers.append({'Ic': s, 'kv': qkv})
-        return RequestCache(R, L_S, layers)
+        present = [n for n in cfg.feature_config['sequence_features'] if n in seq_features]
+        return RequestCache(R, L_S, layers, present)
+
+    # ------------------------------------------------------------------ cross-request append
+    @torch.no_grad()
+    def extend_requests(self, cache: RequestCache, seq_name: str, new_events: torch.Tensor) -> RequestCache:
+        """Cross-request KV cache (paper §3.5.1): the requests' newest behaviours ``new_events``
+        ([R, dL, 64] features or [R, dL] ids) are appended to sequence ``seq_name`` and only the new
+        S tokens are computed, their queries attending over the cached K/V (ot_attn_fwd_cached).
+
+        Exact (equal to encode_requests on the extended sequences) when the appended tokens land at
+        the end of the S side and shift nothing: ``seq_name`` must be the last configured sequence
+        (no [SEP] follows it, model.py:270-272) and present in the requests, and no layer before the
+        last may prune (a pyramid keep would move with the length).  Weight groups are functions of the
+        absolute position, which the old tokens keep."""
+        from .model import _Tokenize
+        m = self.m
+        cfg = m.config
+        d, H = cfg.hidden_dim, cfg.num_heads
+        hd = d // H
+        seqs = cfg.feature_config['sequence_features']
+        if seq_name != seqs[-1] or seq_name not in cache.present:
+            raise ValueError(f'extend_requests: only the last configured sequence ({seqs[-1]!r}), present in the '
+                             'cached requests, can grow without shifting earlier positions')
+        old = self.schedule(cache.L_S)
+        if any(e['kS'] + e['kN'] < e['I'] for e in old[:-1]):
+            raise ValueError('extend_requests: a pyramid keep before the last layer depends on the length; '
+                             're-encode instead')
+        R = cache.R
+        plan = m._plan({}, {seq_name: new_events})
+        if plan['B'] != R:
+            raise ValueError(f'extend_requests: {plan["B"]} rows of new events for {R} cached requests')
+        dL = plan['L_S']
+        x0 = _Tokenize.apply(m.flat, m, plan)                             # [R*(dL+L_NS), d], no [SEP]
+        x = x0.view(R, dL + cfg.num_ns_tokens, d)[:, :dL].reshape(R * dL, d)
+        new = self.schedule(cache.L_S + dL)
+        req = torch.arange(R, dtype=torch.int32, device=x.device)
+        layers = []
+        for l, (e_old, e_new) in enumerate(zip(old, new)):
+            Ic = e_old['s']
+            lay = cache.layers[l]
+            keep = e_new['kS'] - e_old['kS']                              # new S rows kept by this layer
+
+            def attn(qkv, Ic=Ic, lay=lay):
+                o = torch.empty(R * dL, d, device=qkv.device)
+                kv = (lay['kv'], d) if Ic > 0 else None
+                K.attn_fwd_cached(qkv, 3 * d, kv, 3 * d, req, R, H, Ic, dL, dL, hd, o)
+                return o
+
+            x, qkv = self._block(l, x, R, dL, dL if keep == dL else 0, Ic, e_new['I'], attn)
+            kv = qkv if Ic == 0 else torch.cat([lay['kv'].view(R, Ic, 3 * d), qkv.view(R, dL, 3 * d)], 1)
+            layers.append({'Ic': Ic + dL, 'kv': kv.reshape(R * (Ic + dL), 3 * d)})
+        return RequestCache(R, cache.L_S + dL, layers, cache.present)
 
     # ------------------------------------------------------------------ stage II
     @torch.no_grad()
@@ -192,3 +246,118 @@ class OneTransServer:
         if req is None:
             req = torch.arange(cache.R, dtype=torch.int32)
         return self.score(cache, req, non_seq_features)
+
+
+class OneTransInferenceEngine:
+    """The reference's inference engine surface (examples/inference_example.py:21-219): load a saved
+    model directory (config.json + weights, train.py:281-291), preprocess, single / batch inference,
+    latency statistics.  ``score_candidates`` adds the two-stage path: one user's sequences once,
+    many candidates against the cache."""
+
+    def __init__(self, model_path: str, device=None):
+        import json
+        import os
+        from .config import OneTransConfig
+        from .model import OneTransModel
+        cfg_path = os.path.join(model_path, 'config.json')
+        if not os.path.exists(cfg_path):                                  # inference_example.py:44-45
+            raise FileNotFoundError(f'config file not found: {cfg_path}')
+        with open(cfg_path) as f:
+            self.config = OneTransConfig.from_dict(json.load(f))
+        w = os.path.join(model_path, 'model_weights.npz')
+        if not os.path.exists(w):                                          # inference_example.py:55-56
+            raise FileNotFoundError(f'model weights not found: {w}')
+        self.model = OneTransModel(self.config, device=device)
+        self.model.load_weights(w)
+        self.server = OneTransServer(self.model)
+        self.reset_stats()
+
+    # ------------------------------------------------------------------ inference_example.py:63-92
+    def preprocess_input(self, user_features: Dict, item_features: Dict, context_features: Dict,
+                         sequence_features: Dict):
+        from .features import SequenceProcessor
+        import numpy as np
+        non_seq = {}
+        non_seq.update(user_features)
+        non_seq.update(item_features)
+        non_seq.update(context_features)
+        sp = SequenceProcessor(self.config)
+        seq = {k: sp.process_sequence(np.asarray(v)) for k, v in sequence_features.items()}
+        return non_seq, seq
+
+    def _predict(self, non_seq, seq):
+        import numpy as np
+        dev = self.model.device
+        ns = {k: torch.as_tensor(np.asarray(v)).reshape(-1, 1).to(dev) for k, v in non_seq.items()}
+        sq = {k: torch.as_tensor(np.asarray(v)).to(dev) for k, v in seq.items()}
+        with torch.no_grad():
+            out = self.model((ns, sq), training=False)
+        return {t: p.float().cpu().numpy()[:, 0] for t, p in out.items()}
+
+    def single_inference(self, user_features, item_features, context_features, sequence_features) -> Dict[str, float]:
+        """inference_example.py:94-129."""
+        import time
+        t0 = time.time()
+        try:
+            ns, seq = self.preprocess_input(user_features, item_features, context_features, sequence_features)
+            seq = {k: v[None] for k, v in seq.items()}                     # batch dimension
+            res = {t: float(v[0]) for t, v in self._predict(ns, seq).items()}
+            self._update_stats(True, (time.time() - t0) * 1e3)
+            return res
+        except Exception:
+            self._update_stats(False, 0.0)
+            raise
+
+    def batch_inference(self, batch_data) -> List[Dict[str, float]]:
+        """inference_example.py:131-179: (user, item, context, sequences) tuples, one full forward."""
+        import time
+        import numpy as np
+        t0 = time.time()
+        try:
+            pre = [self.preprocess_input(*b) for b in batch_data]
+            ns = {k: np.concatenate([np.asarray(p[0][k]).reshape(-1) for p in pre]) for k in pre[0][0]}
+            seq = {k: np.stack([p[1][k] for p in pre]) for k in pre[0][1]}
+            out = self._predict(ns, seq)
+            n = len(batch_data)
+            self._update_stats(True, (time.time() - t0) * 1e3 / n, n)
+            return [{t: float(v[i]) for t, v in out.items()} for i in range(n)]
+        except Exception:
+            self._update_stats(False, 0.0, len(batch_data))
+            raise
+
+    def score_candidates(self, user_features: Dict, sequence_features: Dict, candidates: List[Dict]):
+        """One request (user + sequences), many candidates (item / context features each): stage I once,
+        stage II for all candidates (paper §3.5.1).  Same results as ``batch_inference`` on the
+        (user, candidate, sequences) samples."""
+        import numpy as np
+        dev = self.model.device
+        _, seq = self.preprocess_input({}, {}, {}, sequence_features)
+        cache = self.server.encode_requests({k: torch.as_tensor(v[None]).to(dev) for k, v in seq.items()})
+        ns = {}
+        for k, v in user_features.items():
+            ns[k] = np.repeat(np.asarray(v).reshape(-1)[:1], len(candidates))
+        for k in candidates[0]:
+            ns[k] = np.concatenate([np.asarray(c[k]).reshape(-1) for c in candidates])
+        nsd = {k: torch.as_tensor(v).reshape(-1, 1).to(dev) for k, v in ns.items()}
+        out = self.server.score(cache, torch.zeros(len(candidates), dtype=torch.int32), nsd)
+        return [{t: float(p[i, 0]) for t, p in out.items()} for i in range(len(candidates))]
+
+    # ------------------------------------------------------------------ inference_example.py:181-219
+    def _update_stats(self, success: bool, latency: float, batch_size: int = 1):
+        st = self.inference_stats
+        st['total_requests'] += batch_size
+        if success:
+            st['successful_requests'] += batch_size
+            st['avg_latency_ms'] = 0.1 * latency + 0.9 * st['avg_latency_ms']      # EMA, alpha 0.1
+        else:
+            st['failed_requests'] += batch_size
+
+    def get_stats(self) -> Dict:
+        st = dict(self.inference_stats)
+        st['success_rate'] = (st['successful_requests'] / st['total_requests'] * 100
+                              if st['successful_requests'] > 0 else 0.0)
+        return st
+
+    def reset_stats(self):
+        self.inference_stats = {'total_requests': 0, 'avg_latency_ms': 0.0, 'successful_requests': 0,
+                                'failed_requests': 0}

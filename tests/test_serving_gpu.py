@@ -82,3 +82,74 @@ def test_norm_select_refused(dev):
     model = OneTransModel(cfg, device=dev, init=init_params(cfg, cfg.ns_input_width(), seed=0))
     with pytest.raises(ValueError):
         OneTransServer(model)
+
+
+@pytest.mark.parametrize('dedicated', ['head', 'tail'])
+def test_extend_requests_matches_reencode(dev, dedicated):
+    """Cross-request reuse: appending events to the last sequence computes only the new tokens and
+    gives the cache a full re-encode would (scores equal, and equal to the full forward)."""
+    cfg = small_criteo(dedicated)
+    P = init_params(cfg, cfg.ns_input_width(), seed=0, perturb=True)
+    model = OneTransModel(cfg, device=dev, init=P)
+    Rq, C, dL = 3, 9, 4
+    _, seq_r, _ = make_batch(Rq, cfg, seed=41)
+    ns_c, _, _ = make_batch(C, cfg, seed=42)
+    last = cfg.feature_config['sequence_features'][-1]
+    new = np.random.default_rng(5).integers(0, cfg.seq_item_vocab, (Rq, dL))
+    full = dict(seq_r)
+    full[last] = np.concatenate([seq_r[last], new], 1)
+    req = torch.tensor([0, 1, 2, 2, 1, 0, 0, 1, 2])
+    srv = OneTransServer(model)
+    ext = srv.extend_requests(srv.encode_requests(ns_t(seq_r, dev)), last, torch.from_numpy(new).to(dev))
+    ref_cache = srv.encode_requests(ns_t(full, dev))
+    assert ext.L_S == ref_cache.L_S
+    a = srv.score(ext, req, ns_t(ns_c, dev))
+    b = srv.score(ref_cache, req, ns_t(ns_c, dev))
+    with torch.no_grad():
+        f = model((ns_t(ns_c, dev), ns_t(expand(full, req.numpy()), dev)), training=False)
+    for t in cfg.tasks:
+        np.testing.assert_allclose(a[t].cpu().numpy(), b[t].cpu().numpy(), atol=2e-6, rtol=0)
+        np.testing.assert_allclose(a[t].cpu().numpy(), f[t].cpu().numpy(), atol=2e-6, rtol=0)
+    with pytest.raises(ValueError):                      # an earlier sequence would shift later positions
+        srv.extend_requests(ext, cfg.feature_config['sequence_features'][0], torch.from_numpy(new).to(dev))
+
+
+def test_extend_refused_under_pyramid(dev):
+    cfg = small_criteo('tail', pyramid=True, layers=3)
+    model = OneTransModel(cfg, device=dev, init=init_params(cfg, cfg.ns_input_width(), seed=0))
+    _, seq_r, _ = make_batch(2, cfg, seed=3)
+    srv = OneTransServer(model)
+    cache = srv.encode_requests(ns_t(seq_r, dev))
+    last = cfg.feature_config['sequence_features'][-1]
+    with pytest.raises(ValueError):
+        srv.extend_requests(cache, last, torch.zeros(2, 3, dtype=torch.int64, device=dev))
+
+
+def test_inference_engine(dev, tmp_path):
+    """The reference engine surface (examples/inference_example.py): a saved model directory, single and
+    batch inference, and the two-stage score_candidates path agreeing with them."""
+    from recommend_amd.serving import OneTransInferenceEngine
+    from recommend_amd.trainer import OneTransTrainer
+    cfg = small_criteo('head')
+    cfg.max_seq_len = 12
+    P = init_params(cfg, cfg.ns_input_width(), seed=0, perturb=True)
+    tr = OneTransTrainer(cfg, model_dir=str(tmp_path), model=OneTransModel(cfg, device=dev, init=P))
+    tr.save_model('m')
+    eng = OneTransInferenceEngine(str(tmp_path / 'm'), device=dev)
+    ns_c, seq, _ = make_batch(4, cfg, seed=9)
+    names = list(ns_c)
+    user = {k: ns_c[k][0] for k in names[:5]}
+    cands = [{k: ns_c[k][i] for k in names[5:]} for i in range(4)]
+    seq1 = {k: v[0] for k, v in seq.items()}                      # one user's sequences (unpadded)
+    batch = [(user, c, {}, seq1) for c in cands]
+    got = eng.batch_inference(batch)
+    single = eng.single_inference(user, cands[2], {}, seq1)
+    fast = eng.score_candidates(user, seq1, cands)
+    for t in cfg.tasks:
+        assert abs(single[t] - got[2][t]) < 2e-6
+        for i in range(4):
+            assert abs(fast[i][t] - got[i][t]) < 2e-6
+    st = eng.get_stats()
+    assert st['total_requests'] == 5 and st['success_rate'] == 100.0
+    with pytest.raises(FileNotFoundError):
+        OneTransInferenceEngine(str(tmp_path / 'missing'))

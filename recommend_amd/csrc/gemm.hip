@@ -945,31 +945,45 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(WgradArgs p) {
 // Sum the slabs of each group's chunks (chunks of one group are contiguous) into dW[g] (and db).
 // Block = 16 float4 columns x 16 chunk lanes; chunk lane c sums chunks c, c+16, ... and the 16
 // partials are combined in a fixed order through LDS (deterministic).
+// Blocks past the weight columns (wblocks) reduce the bias slab the same way when N % 4 == 0 (the bias
+// sums used to be one block per group looping over every chunk: the reduce's long pole).
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ slab,
                                                            const float* __restrict__ bslab,
                                                            const int32_t* __restrict__ gchunk, int K, int N,
                                                            float* dW, int64_t dw_gstride, float* db,
-                                                           int64_t db_gstride, int accumulate) {
+                                                           int64_t db_gstride, int accumulate, int wblocks) {
   __shared__ f32x4 red[16][16];
   const int g = blockIdx.y;
   const int cb = gchunk[2 * g], cn = gchunk[2 * g + 1];
-  const int64_t KN = (int64_t)K * N;
+  const bool bias_blk = (int)blockIdx.x >= wblocks;
+  const int64_t KN = bias_blk ? (int64_t)N : (int64_t)K * N;     // slab stride per chunk
+  const float* src = bias_blk ? bslab : slab;
+  float* out = bias_blk ? db + (int64_t)g * db_gstride : dW + (int64_t)g * dw_gstride;
   const int col = threadIdx.x & 15, cl = threadIdx.x >> 4;
-  const int64_t i4 = ((int64_t)blockIdx.x * 16 + col) * 4;
+  const int64_t i4 = ((int64_t)(bias_blk ? blockIdx.x - wblocks : blockIdx.x) * 16 + col) * 4;
   f32x4 s = {0.f, 0.f, 0.f, 0.f};
-  if (i4 < KN)
-    for (int c = cb + cl; c < cb + cn; c += 16) s += *reinterpret_cast<const f32x4*>(slab + (int64_t)c * KN + i4);
+  if (i4 < KN && (!bias_blk || bslab)) {
+    int c = cb + cl;
+    for (; c + 48 < cb + cn; c += 64) {        // four independent loads in flight per lane
+      const f32x4 a0 = *reinterpret_cast<const f32x4*>(src + (int64_t)c * KN + i4);
+      const f32x4 a1 = *reinterpret_cast<const f32x4*>(src + (int64_t)(c + 16) * KN + i4);
+      const f32x4 a2 = *reinterpret_cast<const f32x4*>(src + (int64_t)(c + 32) * KN + i4);
+      const f32x4 a3 = *reinterpret_cast<const f32x4*>(src + (int64_t)(c + 48) * KN + i4);
+      s += a0; s += a1; s += a2; s += a3;      // fixed order: deterministic
+    }
+    for (; c < cb + cn; c += 16) s += *reinterpret_cast<const f32x4*>(src + (int64_t)c * KN + i4);
+  }
   red[cl][col] = s;
   __syncthreads();
   if (cl == 0 && i4 < KN) {   // a group with no rows (e.g. dedicated groups outside a 1-token tail) -> 0
     f32x4 t = red[0][col];
 #pragma unroll
     for (int q = 1; q < 16; ++q) t += red[q][col];
-    float* dst = dW + (int64_t)g * dw_gstride + i4;
+    float* dst = out + i4;
     if (accumulate) t += *reinterpret_cast<const f32x4*>(dst);
     *reinterpret_cast<f32x4*>(dst) = t;
   }
-  if (db && blockIdx.x == 0) {
+  if (db && N % 4 != 0 && blockIdx.x == 0) {
     for (int n = threadIdx.x; n < N; n += blockDim.x) {
       float t = 0.f;
       if (bslab)
@@ -1249,9 +1263,11 @@ extern "C" int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a
     hipLaunchKernelGGL(kern, dim3((unsigned)nchunks * p.ntk * p.ntn), dim3(256), split ? split_shmem : shmem, s, p);
     OT_LAUNCH_CHECK("ot_mixed_gemm_wgrad");
   }
-  dim3 rg(ceil_div((int64_t)K * N / 4, 16), ngroups);
+  const int wblocks = (int)ceil_div((int64_t)K * N / 4, 16);
+  const int bblocks = (db && N % 4 == 0) ? (int)ceil_div((int64_t)N / 4, 16) : 0;
+  dim3 rg(wblocks + bblocks, ngroups);
   hipLaunchKernelGGL(wgrad_reduce_kernel, rg, dim3(256), 0, s, slab, bslab, gchunk, K, N, dW, dw_gstride, db,
-                     db_gstride, accumulate);
+                     db_gstride, accumulate, wblocks);
   OT_LAUNCH_CHECK("ot_mixed_gemm_wgrad(reduce)");
   return OT_OK;
 }

@@ -746,6 +746,224 @@ __global__ __launch_bounds__(64 * BWD_WAVES<HD>(), 2) void attn_bwd_kernel(AttnA
 }
 
 // ------------------------------------------------------------------------------------------
+// bf16 backward (TERMS = 1, OT_MATMUL_BF16; the kernel also builds with TERMS = 6 split planes, which
+// measured slower than attn_bwd_kernel and is not dispatched).
+// Same pass structure as attn_bwd_kernel (one wave per (sample, head), key blocks outer, the query
+// blocks that see them inner, dQ partial read-modify-written in dqkv), all five products on
+// v_mfma_f32_32x32x16_bf16:
+//   S = Q K^T, dP = dO V^T        A = Q / dO (lane = query), B = K / V (lane = key): register planes
+//   dV^T += dO^T P, dK^T += Q^T dS  A = dO^T / Q^T via ds_read_b64_tr_b16 from the wave's row-major
+//                                  [query][dim] plane images (k = query in the accumulator order of
+//                                  P / dS, which are the B operands straight from the registers)
+//   dQ^T += K^T dS^T              A = K^T from the [key][dim] image, B = dS^T from a [key][query]
+//                                  image the lanes write as 8-byte runs (k = key, natural order)
+// Planes: 3 (split, TERMS = 6) or 1 (bf16).  LDS per wave: (3 x 32 x HD + 32 x 32) x 2 B x planes.
+
+// two ds_read_b64_tr_b16 reads -> one 32x32x16 operand fragment: elements 0-3 from rows ra .. ra+3,
+// 4-7 from rows rb .. rb+3, the lane's column colbase + (lane & 31) (row stride rs bytes)
+__device__ __forceinline__ u32x4 tr16_frag(const char* img, int rs, int ra, int rb, int colbase, int lane) {
+  typedef short v4i16 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+  const int gi = lane & 15, q = gi >> 2, pp = gi & 3;
+  const int c = colbase + 16 * ((lane >> 4) & 1) + 4 * pp;
+  const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(img + (ra + q) * rs + c * 2));
+  const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(img + (rb + q) * rs + c * 2));
+  const u32x2 a = __builtin_bit_cast(u32x2, lo), b = __builtin_bit_cast(u32x2, hi);
+  return u32x4{a.x, a.y, b.x, b.y};
+}
+
+template <int HD, int TERMS>
+constexpr int BWDS_LDS() { return (TERMS == 1 ? 1 : 3) * (3 * 32 * HD + 32 * 32) * 2; }
+
+template <int HD, int TERMS, bool SEL, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void attn_bwd_split_kernel(AttnArgs p) {
+  static_assert(HD == 32 || HD == 64, "split backward: HD 32 or 64");
+  constexpr int NPL = TERMS == 1 ? 1 : 3;
+  constexpr int NS = HD / 16;                          // k-steps over the head dim
+  constexpr int IMG = 32 * HD * 2;                     // bytes of one [32][HD] plane image
+  constexpr int SIMG = 32 * 32 * 2;                    // bytes of one [32 keys][32 queries] plane
+  extern __shared__ __attribute__((aligned(16))) char lds_b[];
+  const int lane = threadIdx.x & 63, li = lane & 31, hh = lane >> 5;
+  char* kimg = lds_b + (threadIdx.x >> 6) * BWDS_LDS<HD, TERMS>();
+  char* qimg = kimg + NPL * IMG;
+  char* oimg = qimg + NPL * IMG;
+  char* simg = oimg + NPL * IMG;
+  const int pair = blockIdx.x * WAVES + (threadIdx.x >> 6);
+  if (pair >= p.B * p.H) return;                       // wave-uniform
+  const int b = pair / p.H, h = pair % p.H;
+  const int I = p.I, K = p.K, q_off = I - K, KP = attn_kpad(K);
+  const int64_t tok0 = (int64_t)b * I;
+  const float* Q = p.qkv + tok0 * p.ld + h * HD;
+  const float* Kp = Q + p.d;
+  const float* V = Q + 2 * p.d;
+  const float* dO = p.dout + (int64_t)b * K * p.d + h * HD;
+  const float* lsep = p.delta + (int64_t)pair * KP;
+  const float* dltp = p.delta + ((int64_t)p.B * p.H + pair) * KP;
+  const int32_t* qpp = reinterpret_cast<const int32_t*>(p.delta + 2 * (int64_t)p.B * p.H * KP) + (int64_t)b * KP;
+  float* dK = p.dqkv + tok0 * p.ld + p.d + h * HD;
+  float* dV = dK + p.d;
+  const int nqb = KP / 32;
+  const int nkb = (I + 31) / 32;
+  auto qrow = [&](int j) { return SEL ? qpp[j < KP ? j : KP - 1] : q_off + (j < K ? j : K - 1); };
+
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int key0 = 32 * kb;
+    const int kpos = key0 + li;
+    u32x4 kB[NS][3], vB[NS][3];
+    {
+      float kf[HD / 2], vf[HD / 2];
+      load_frag<HD>(kf, Kp, p.ld, kpos, I, hh);        // rows >= I: zeros (masked below)
+      load_frag<HD>(vf, V, p.ld, kpos, I, hh);
+#pragma unroll
+      for (int t = 0; t < NS; ++t) {
+        split8t<TERMS>(kf + 8 * t, kB[t]);
+        split8t<TERMS>(vf + 8 * t, vB[t]);
+#pragma unroll
+        for (int pl = 0; pl < NPL; ++pl)
+          *reinterpret_cast<u32x4*>(kimg + pl * IMG + (li * HD + (HD / 2) * hh + 8 * t) * 2) = kB[t][pl];
+      }
+    }
+    f32x16 dk[NB(HD)], dv[NB(HD)];
+#pragma unroll
+    for (int c = 0; c < NB(HD); ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { dk[c][r] = 0.f; dv[c][r] = 0.f; }
+    int qb0;
+    if constexpr (SEL) {
+      qb0 = 0;
+      while (qb0 < nqb - 1 && qpp[32 * qb0 + 31] < key0) ++qb0;
+    } else {
+      qb0 = key0 - q_off; qb0 = qb0 < 0 ? 0 : qb0 / 32;
+    }
+    for (int qb = qb0; qb < nqb; ++qb) {
+      const int q0 = 32 * qb;
+      const int jq = q0 + li;
+      // Q / dO rows of this lane's query: register planes (A of S / dP) and the plane images
+      u32x4 qA[NS][3], oA[NS][3];
+      {
+        float qf[HD / 2], of[HD / 2];
+        if constexpr (SEL) load_frag<HD>(qf, Q, p.ld, jq < K ? qpp[jq] : I, I, hh);
+        else load_frag<HD>(qf, Q, p.ld, jq < K ? q_off + jq : I, I, hh);
+        load_frag<HD>(of, dO, p.d, jq, K, hh);
+#pragma unroll
+        for (int t = 0; t < NS; ++t) {
+          split8t<TERMS>(qf + 8 * t, qA[t]);
+          split8t<TERMS>(of + 8 * t, oA[t]);
+#pragma unroll
+          for (int pl = 0; pl < NPL; ++pl) {
+            *reinterpret_cast<u32x4*>(qimg + pl * IMG + (li * HD + (HD / 2) * hh + 8 * t) * 2) = qA[t][pl];
+            *reinterpret_cast<u32x4*>(oimg + pl * IMG + (li * HD + (HD / 2) * hh + 8 * t) * 2) = oA[t][pl];
+          }
+        }
+      }
+      f32x16 s, dp;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
+#pragma unroll
+      for (int t = 0; t < NS; ++t) {
+        s = mfma_terms<TERMS>(qA[t], kB[t], s);         // S: row = query, col = key
+        dp = mfma_terms<TERMS>(oA[t], vB[t], dp);       // dP
+      }
+      // softmax gradient (rows = queries acc_row(r, hh), column = this lane's key)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 l4 = *reinterpret_cast<const f32x4*>(lsep + q0 + 8 * g + 4 * hh);
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(dltp + q0 + 8 * g + 4 * hh);
+        i32x4 qv4;
+        if constexpr (SEL) qv4 = *reinterpret_cast<const i32x4*>(qpp + q0 + 8 * g + 4 * hh);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * g + e, j = q0 + 8 * g + 4 * hh + e;
+          const int qposj = SEL ? qv4[e] : q_off + j;
+          const float ex = __expf(s[r] * p.scale - l4[e]);
+          const float P = kpos <= qposj ? ex : 0.f;
+          s[r] = P;
+          dp[r] = P * (dp[r] - d4[e]) * p.scale;         // dS, pre-scaled by 1/sqrt(hd)
+        }
+      }
+      u32x4 pB[2][3], sB[2][3];
+      {
+        float pv[16], sv[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { pv[r] = s[r]; sv[r] = dp[r]; }
+        split8t<TERMS>(pv, pB[0]); split8t<TERMS>(pv + 8, pB[1]);
+        split8t<TERMS>(sv, sB[0]); split8t<TERMS>(sv + 8, sB[1]);
+        // dS^T image [key][query]: this lane's key row, registers 4g .. 4g+3 = queries 8g + 4hh + 0..3
+#pragma unroll
+        for (int pl = 0; pl < NPL; ++pl)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const u32x4 w = sB[g >> 1][pl];
+            const u32x2 two = (g & 1) ? u32x2{w.z, w.w} : u32x2{w.x, w.y};
+            *reinterpret_cast<u32x2*>(simg + pl * SIMG + (li * 32 + 8 * g + 4 * hh) * 2) = two;
+          }
+      }
+      __builtin_amdgcn_wave_barrier();
+      // dV^T += dO^T P, dK^T += Q^T dS  (k = query, accumulator order)
+#pragma unroll
+      for (int c = 0; c < NB(HD); ++c)
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          u32x4 oT[3], qT[3];
+#pragma unroll
+          for (int pl = 0; pl < NPL; ++pl) {
+            oT[pl] = tr16_frag(oimg + pl * IMG, HD * 2, 16 * st + 4 * hh, 16 * st + 8 + 4 * hh, 32 * c, lane);
+            qT[pl] = tr16_frag(qimg + pl * IMG, HD * 2, 16 * st + 4 * hh, 16 * st + 8 + 4 * hh, 32 * c, lane);
+          }
+          dv[c] = mfma_terms<TERMS>(oT, pB[st], dv[c]);
+          dk[c] = mfma_terms<TERMS>(qT, sB[st], dk[c]);
+        }
+      // dQ^T += K^T dS^T  (k = key, natural order)
+      f32x16 dq[NB(HD)];
+#pragma unroll
+      for (int c = 0; c < NB(HD); ++c)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dq[c][r] = 0.f;
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        u32x4 sT[3];
+#pragma unroll
+        for (int pl = 0; pl < NPL; ++pl)
+          sT[pl] = tr16_frag(simg + pl * SIMG, 64, 16 * st + 8 * hh, 16 * st + 8 * hh + 4, 0, lane);
+#pragma unroll
+        for (int c = 0; c < NB(HD); ++c) {
+          u32x4 kT[3];
+#pragma unroll
+          for (int pl = 0; pl < NPL; ++pl)
+            kT[pl] = tr16_frag(kimg + pl * IMG, HD * 2, 16 * st + 8 * hh, 16 * st + 8 * hh + 4, 32 * c, lane);
+          dq[c] = mfma_terms<TERMS>(kT, sT, dq[c]);
+        }
+      }
+      __builtin_amdgcn_wave_barrier();                   // the images are rewritten by the next pair
+      if (jq < K) {                                      // the running dQ partial (single owner)
+        float* dqrow = p.dqkv + (tok0 + qrow(jq)) * p.ld + h * HD + 4 * hh;
+#pragma unroll
+        for (int c = 0; c < NB(HD); ++c)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int dd = 32 * c + 8 * g;
+            f32x4 v = {dq[c][4 * g], dq[c][4 * g + 1], dq[c][4 * g + 2], dq[c][4 * g + 3]};
+            if (kb > 0) v = *reinterpret_cast<const f32x4*>(dqrow + dd) + v;
+            *reinterpret_cast<f32x4*>(dqrow + dd) = v;
+          }
+      }
+    }
+    if (kpos < I) {
+#pragma unroll
+      for (int c = 0; c < NB(HD); ++c)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int dd = 32 * c + 8 * g + 4 * hh;
+          f32x4 a = {dk[c][4 * g], dk[c][4 * g + 1], dk[c][4 * g + 2], dk[c][4 * g + 3]};
+          f32x4 v = {dv[c][4 * g], dv[c][4 * g + 1], dv[c][4 * g + 2], dv[c][4 * g + 3]};
+          *reinterpret_cast<f32x4*>(dK + (int64_t)kpos * p.ld + dd) = a;
+          *reinterpret_cast<f32x4*>(dV + (int64_t)kpos * p.ld + dd) = v;
+        }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // Backward for a short query tail (K <= SMALL_K, e.g. the last layer's single query after DCE):
 // HBM-bound (read K/V rows, write dK/dV rows), so VALU instead of 32x32 MFMA tiles that would be
 // 1/32 occupied.  One wave per (sample, head); HD/4 lanes per key (one float4 of dims each), 64/(HD/4)
@@ -1047,9 +1265,21 @@ extern "C" int ot_attn_bwd(const float* qkv, int64_t ld, const float* out, const
   hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3(main_blocks + pad_blocks + qpos_blocks), dim3(256), 0,
                      (hipStream_t)stream, out, dout, lse, delta_ws, B, H, K, head_dim, main_blocks, pad_blocks, qpos);
   OT_LAUNCH_CHECK("ot_attn_bwd(prep)");
+  const int mm = ot_get_matmul_mode();
   if (K <= SMALL_K) {
     OT_ATTN_DISPATCH(attn_bwd_small_kernel, head_dim, dim3(ceil_div((int64_t)B * H, 4)), dim3(256), 0,
                      (hipStream_t)stream, p);
+  } else if (mm == OT_MATMUL_BF16 && (head_dim == 32 || head_dim == 64)) {
+    // bf16 mode: one-plane bf16 MFMA, 4 waves / block (C5 shape: 24 -> 18 ms).  The six-term split
+    // form of the same kernel measured slower than the f32 kernel at hd 32 (1.42 vs 1.34 ms at C2:
+    // the pass is latency-bound, not MFMA-bound), so split mode keeps the f32 backward.
+    void (*kern)(AttnArgs) = nullptr;
+    const bool sel = qpos != nullptr;
+    const int waves = 4, lds = head_dim == 32 ? BWDS_LDS<32, 1>() : BWDS_LDS<64, 1>();
+    if (head_dim == 32) kern = sel ? attn_bwd_split_kernel<32, 1, true, 4> : attn_bwd_split_kernel<32, 1, false, 4>;
+    else kern = sel ? attn_bwd_split_kernel<64, 1, true, 4> : attn_bwd_split_kernel<64, 1, false, 4>;
+    const unsigned grid = ceil_div((int64_t)B * H, waves);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * waves), (size_t)waves * lds, (hipStream_t)stream, p);
   } else {
     const int waves = head_dim >= 128 ? 2 : 4;
     const unsigned grid = ceil_div((int64_t)B * H, waves);

@@ -522,7 +522,50 @@ def test_bf16_mode_bounds(dev):
         out = torch.empty(B * Kq, d, device=dev)
         lse = torch.empty(B * H * Kq, device=dev)
         K.attn_fwd(qkv.float().to(dev), 3 * d, B, H, I, Kq, hd, out, lse)
-        ref = attn_ref(qkv, B, H, I, Kq, hd)
-        assert (out.double().cpu() - ref).abs().max() < 3e-2
+        qkv_r = qkv.clone().requires_grad_(True)
+        ref = attn_ref(qkv_r, B, H, I, Kq, hd)
+        assert (out.double().cpu() - ref.detach()).abs().max() < 3e-2
+        # attention backward (bf16 MFMA), tail and selected queries
+        dout = torch.randn(B * Kq, d, dtype=torch.float64, generator=g)
+        ref.backward(dout)
+        dqkv = torch.full((B * I, 3 * d), float('nan'), device=dev)
+        K.attn_bwd(qkv.float().to(dev), 3 * d, out, dout.float().to(dev), lse, B, H, I, Kq, hd, dqkv)
+        scale = qkv_r.grad.abs().max().item()
+        assert (dqkv.double().cpu() - qkv_r.grad).abs().max().item() < 3e-2 * scale
+    finally:
+        K.set_matmul_mode(old)
+
+
+@pytest.mark.parametrize('mode', ['split', 'bf16'])
+@pytest.mark.parametrize('B,H,I,Kq,hd,sel', [(2, 4, 140, 140, 32, False), (2, 4, 140, 70, 32, True),
+                                             (2, 2, 150, 150, 64, False), (2, 2, 300, 120, 64, True),
+                                             (3, 4, 40, 12, 32, False)])
+def test_attention_backward_modes(dev, mode, B, H, I, Kq, hd, sel):
+    """The backward in split mode (f32 kernel: f32-accurate) and in bf16 mode (one-plane bf16 kernel)
+    against the f64 reference, tail and selected queries."""
+    rng = np.random.default_rng(I + Kq)
+    qpos = (np.stack([np.append(np.sort(rng.choice(I - 1, Kq - 1, replace=False)), I - 1) for _ in range(B)])
+            if sel else np.broadcast_to(np.arange(I - Kq, I), (B, Kq)))
+    torch.manual_seed(4)
+    d = H * hd
+    qkv = torch.randn(B * I, 3 * d, dtype=torch.float64)
+    qp_d = torch.from_numpy(qpos.astype(np.int32).reshape(-1)).to(dev) if sel else None
+    old = K.set_matmul_mode(mode)
+    try:
+        out = torch.empty(B * Kq, d, device=dev)
+        lse = torch.empty(B * H * Kq, device=dev)
+        K.attn_fwd(qkv.float().to(dev), 3 * d, B, H, I, Kq, hd, out, lse, qpos=qp_d)
+        qkv_r = qkv.clone().requires_grad_(True)
+        ref = attn_ref_sel(qkv_r, B, H, I, torch.from_numpy(np.ascontiguousarray(qpos)), hd)
+        dout = torch.randn(B * Kq, d, dtype=torch.float64)
+        ref.backward(dout)
+        dqkv = torch.full((B * I, 3 * d), float('nan'), device=dev)
+        dqkv[:, :d].zero_()
+        K.attn_bwd(qkv.float().to(dev), 3 * d, out, dout.float().to(dev), lse, B, H, I, Kq, hd, dqkv, qpos=qp_d)
+        got = dqkv.double().cpu()
+        if mode == 'split':
+            torch.testing.assert_close(got, qkv_r.grad, rtol=1e-4, atol=1e-4)
+        else:
+            assert (got - qkv_r.grad).abs().max().item() < 3e-2 * qkv_r.grad.abs().max().item()
     finally:
         K.set_matmul_mode(old)

@@ -79,7 +79,7 @@ int ot_gemm_tile_rows(void);
  *   OT_MATMUL_F32: native v_mfma_f32_32x32x2_f32.
  *   OT_MATMUL_BF16: reduced precision (BASELINE C5's bf16 configuration, not the reference's f32):
  *     operands rounded to bf16 (nearest even), one v_mfma_f32_32x32x16_bf16 product, f32
- *     accumulation; attention forward likewise (its backward stays f32-accurate).
+ *     accumulation; attention forward and backward likewise.
  * Keras computes these Dense layers in f32 (model.py:38-57, 136-147; default float32 policy). */
 #define OT_MATMUL_F32 0
 #define OT_MATMUL_SPLIT_BF16 1

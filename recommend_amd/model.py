@@ -304,6 +304,8 @@ class _Block(torch.autograd.Function):
             K.rmsnorm_bwd(dxn1, d, x, d, m.p(f'blk.{l}.norm1'), rstd1, dx, d, B * I, d, dres=dx1, lddres=d,
                           dres_tail=(Kq, I, inv) if Kq < I else (0, 0), dgamma=m.g(f'blk.{l}.norm1'), accumulate=acc,
                           device=dev)
+        if m.grad_ready is not None:
+            m.grad_ready(l)                     # this block's banks are final: the DP exchange may start
         return None, dx, None, None, None, None, None, None, None, None
 
 
@@ -372,6 +374,8 @@ class _Head(torch.autograd.Function):
         dx = torch.empty(B, d, device=dev)
         K.rmsnorm_bwd(dy, d, x, d, m.p('out_norm'), rstd, dx, d, B, d, dgamma=m.g('out_norm'), accumulate=acc,
                       device=dev)
+        if m.grad_ready is not None:
+            m.grad_ready('head')                # out_norm + heads are final: the DP exchange may start
         return None, dx, None
 
 
@@ -428,6 +432,9 @@ class OneTransModel(nn.Module):
         self._tdesc = torch.from_numpy(self.layout.transpose_desc.reshape(-1)).to(self.device)
         self.tables: Dict[str, torch.Tensor] = {}
         self.accumulate_grads = False
+        # data-parallel hook (OneTransOptimizer): called with a layer index / 'head' when those gradient
+        # banks are final in backward, so their all-reduce overlaps the rest of the backward pass
+        self.grad_ready = None
         # fuse the RMSNorms into the neighbouring GEMM epilogues when a tile holds whole rows
         self.fuse_norms = (config.hidden_dim == TILE and os.environ.get('ONETRANS_FUSE_NORMS', '1') != '0')
         # block weight gradients run on a second stream, overlapping the dgrad chain

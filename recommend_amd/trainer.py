@@ -67,9 +67,53 @@ class OneTransOptimizer:
         self.dense_exchange_bytes = int(float(os.environ.get('ONETRANS_DENSE_EXCHANGE_MB', '512')) * 2 ** 20)
         self._dense_grad: Dict[str, torch.Tensor] = {}
 
+    # ---------------------------------------------------------------- DP exchange overlapped with backward
+    def bank_ranges(self):
+        """Flat-buffer ranges that become final together in backward: 'head' (out_norm + heads), each
+        block l, and the tokenizer remainder (layout order: tok.*, blk.0 .. blk.L-1, out_norm, head.*)."""
+        lay, cfg = self.model.layout, self.model.config
+        off = lay.offsets
+        starts = [off[f'blk.{l}.norm1'] for l in range(cfg.num_layers)] + [off['out_norm']]
+        r = {l: (starts[l], starts[l + 1]) for l in range(cfg.num_layers)}
+        r['head'] = (off['out_norm'], lay.total)
+        r['tok'] = (0, starts[0])
+        return r
+
+    def begin_backward(self) -> None:
+        """Arm the per-bank all-reduce hooks for the next backward (world > 1, no accumulation): each
+        block's gradient range is all-reduced on a communication stream as soon as its dgrad chain and
+        its side-stream weight gradients are issued, overlapping the earlier layers' backward."""
+        m = self.model
+        if otdist.world() == 1 or m.accumulate_grads:
+            m.grad_ready = None
+            return
+        if not hasattr(self, '_ranges'):
+            self._ranges = self.bank_ranges()
+            self._comm = torch.cuda.Stream(device=m.flat.device)
+        self._works = []
+        m.grad_ready = self._launch
+
+    def _launch(self, key) -> None:
+        m = self.model
+        lo, hi = self._ranges[key]
+        self._comm.wait_stream(torch.cuda.current_stream(m.flat.device))
+        if m._side is not None:
+            self._comm.wait_stream(m._side)              # this block's wgrads run on the side stream
+        with torch.cuda.stream(self._comm):
+            self._works.append(otdist.allreduce_sum_async(m.flat.grad[lo:hi]))
+
     def step(self) -> None:
         m = self.model
-        otdist.allreduce_dense(m.flat.grad)
+        if m.grad_ready is not None:
+            for w in self._works:                        # the current stream waits for each exchange
+                w.wait()
+            lo, hi = self._ranges['tok']
+            otdist.allreduce_dense(m.flat.grad[lo:hi], scale=False)
+            m.flat.grad.mul_(1.0 / otdist.world())
+            m.grad_ready = None
+            self._works = []
+        else:
+            otdist.allreduce_dense(m.flat.grad)
         K.clip_rmsprop(m.flat.data, m.flat.grad, self.v, self.m, self.segs, self.nseg, m.layout.max_seg_elems,
                        self.lr, self.rho, self.eps, self.momentum, self.clip, device=m.flat.device)
         m.refresh_shadow()
@@ -120,6 +164,7 @@ class OneTransTrainer:
         self.model.train()
         probs = self.model.forward_probs(_to_dev(non_seq, dev), _to_dev(seq, dev), training=True)
         loss = keras_bce_loss(y, probs)
+        self.optimizer.begin_backward()
         loss.backward()
         self.optimizer.step()
         return {'total_loss': loss.detach(), 'probs': probs.detach()}

@@ -104,6 +104,22 @@ class OneTransOptimizer:
 
     def step(self) -> None:
         m = self.model
+        # replicated tables small enough to exchange densely: scatter the de-duplicated gradient and
+        # start its all-reduce first, so the dense optimizer below runs while it is in flight
+        early = {}
+        if otdist.world() > 1:
+            for (name, keys, grads) in m._pending_sparse:
+                table = m.tables[name]
+                if name in m.sharded or table.numel() * 4 > self.dense_exchange_bytes:
+                    continue
+                rows, E = table.shape
+                g = self._dense_grad.get(name)
+                if g is None:
+                    g = self._dense_grad[name] = torch.zeros_like(table)
+                else:
+                    g.zero_()
+                K.sparse_grad_dense(E, rows, keys, grads, keys.numel(), g, device=table.device)
+                early[name] = (g, otdist.allreduce_sum_async(g))
         if m.grad_ready is not None:
             for w in self._works:                        # the current stream waits for each exchange
                 w.wait()
@@ -124,16 +140,12 @@ class OneTransOptimizer:
                 # row-sharded: gradient rows go to their owners (all-to-all), global-norm clip, Adagrad
                 m.sharded[name].apply_gradient(keys, grads, self.acc[name], self.sparse_lr, self.sparse_eps,
                                                self.sparse_clip)
-            elif otdist.world() > 1 and table.numel() * 4 <= self.dense_exchange_bytes:
-                # replicated table small enough to exchange densely: one all-reduce of the
-                # de-duplicated dense gradient instead of all-gathering every rank's rows
-                g = self._dense_grad.get(name)
-                if g is None:
-                    g = self._dense_grad[name] = torch.zeros_like(table)
-                else:
-                    g.zero_()
-                K.sparse_grad_dense(E, rows, keys, grads, keys.numel(), g, device=table.device)
-                otdist.allreduce_dense(g)
+            elif name in early:
+                # one all-reduce of the de-duplicated dense gradient (started above) instead of
+                # all-gathering every rank's rows
+                g, work = early[name]
+                work.wait()
+                g.mul_(1.0 / otdist.world())
                 K.dense_adagrad(table, self.acc[name], g, rows, E, self.sparse_lr, self.sparse_eps,
                                 self.sparse_clip, device=table.device)
             else:

@@ -59,10 +59,10 @@ def _lookup_update(rank, world, dev):
     return err_lookup, float(np.abs(new - ref).max())
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, sharding='row'):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
-    os.environ['ONETRANS_TABLE_SHARDING'] = 'row'
+    os.environ['ONETRANS_TABLE_SHARDING'] = sharding
     dist.init_process_group('gloo', rank=rank, world_size=world)
     try:
         dev = torch.device('cuda:0')
@@ -80,8 +80,11 @@ def _worker(rank, world, port, q):
         cfg.optimizer_config = dict(cfg.optimizer_config, dense_lr=0.001, momentum=0.9)
         P = init_params(cfg, cfg.ns_input_width(), seed=0, perturb=True)
         model = OneTransModel(cfg, device=dev, init=P)
-        assert 'emb.seq_item' in model.sharded
-        assert model.sharded['emb.seq_item'].local_rows == (cfg.seq_item_vocab - rank + 1) // 2
+        if sharding == 'row':
+            assert 'emb.seq_item' in model.sharded
+            assert model.sharded['emb.seq_item'].local_rows == (cfg.seq_item_vocab - rank + 1) // 2
+        else:                                            # replicated: dense-gradient all-reduce exchange
+            assert not model.sharded
         tr = OneTransTrainer(cfg, model=model)
         B = 40
         Pt = R.to_torch(P)
@@ -106,7 +109,11 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_row_sharded_table_two_ranks():
+@pytest.mark.parametrize('sharding', ['row', 'none'])
+def test_row_sharded_table_two_ranks(sharding):
+    """'row': the item table row-sharded over the ranks; 'none': replicated, exchanged as a dense
+    all-reduced gradient.  Either way three DP steps equal the oracle's full-batch steps (and the
+    dense gradients are all-reduced per block during the backward)."""
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
@@ -114,7 +121,7 @@ def test_row_sharded_table_two_ranks():
     here = os.path.dirname(os.path.abspath(__file__))
     os.environ['PYTHONPATH'] = os.pathsep.join([here, os.path.dirname(here)] + ([env_pp] if env_pp else []))
     try:
-        procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+        procs = [ctx.Process(target=_worker, args=(r, 2, port, q, sharding)) for r in range(2)]
         for p in procs:
             p.start()
         for p in procs:

@@ -15,6 +15,7 @@ HBM layout:
 
 from __future__ import annotations
 
+import os
 from typing import Callable, Dict, List, Sequence, Tuple
 
 import numpy as np
@@ -24,7 +25,9 @@ from .params import dense_param_shapes, keras_variables
 
 TILE = 128
 ALIGN = 64
-WGRAD_SLOTS = int(__import__("os").environ.get("ONETRANS_WGRAD_SLOTS", "768"))   # resident wgrad workgroups (3 per CU x 256 CUs): size chunks for one round
+# resident wgrad workgroups (3 per CU x 256 CUs): chunks are sized for one round (tuning override:
+# ONETRANS_WGRAD_SLOTS; tools/wgrad_probe.py sweeps it)
+WGRAD_SLOTS = int(os.environ.get('ONETRANS_WGRAD_SLOTS', '768'))
 
 
 def round_up(x: int, m: int) -> int:

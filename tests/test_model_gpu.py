@@ -97,7 +97,18 @@ def ns_t(d, dev):
 @pytest.mark.parametrize('training', [False, True])
 def test_gradient_parity(dev, case, training):
     cfg = CASES[case]()
-    B = 37 if case.startswith('criteo') else 64
+    check_grads(cfg, 37 if case.startswith('criteo') else 64, dev, training)
+
+
+@pytest.mark.parametrize('case', ['criteo_d128_pyramid', 'criteo_norm_pyramid'])
+@pytest.mark.parametrize('B', [1, 2, 129])
+def test_edge_batches(dev, case, B):
+    """Ragged batches: one sample (a single partial 128-row tile per group), two, and one row past a
+    whole number of tiles; forward, every gradient and the sparse rows vs the oracle (dropout on)."""
+    check_grads(CASES[case](), B, dev, training=True)
+
+
+def check_grads(cfg, B, dev, training):
     P, model, batch = setup(cfg, B, dev)
     ns, seq, lab = batch
     seed = 0

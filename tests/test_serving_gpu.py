@@ -39,8 +39,16 @@ def expand(seq, req):
 
 @pytest.mark.parametrize('case', list(CASES))
 def test_cached_serving_matches_forward(dev, case):
-    cfg = CASES[case]()
-    Rq, C = 5, 23
+    check_serving(CASES[case](), 5, 23, dev)
+
+
+@pytest.mark.parametrize('Rq,C', [(1, 1), (2, 129)])
+def test_serving_edge_sizes(dev, Rq, C):
+    """One request with one candidate; two requests sharing a ragged 129-candidate batch."""
+    check_serving(CASES['criteo_tail_pyramid'](), Rq, C, dev)
+
+
+def check_serving(cfg, Rq, C, dev):
     P = init_params(cfg, cfg.ns_input_width(), seed=0, perturb=True)
     model = OneTransModel(cfg, device=dev, init=P)
     ns_r, seq_r, _ = make_batch(Rq, cfg, seed=2000)            # request side: sequences

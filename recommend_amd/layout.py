@@ -25,9 +25,18 @@ from .params import dense_param_shapes, keras_variables
 
 TILE = 128
 ALIGN = 64
-# resident wgrad workgroups (3 per CU x 256 CUs): chunks are sized for one round (tuning override:
-# ONETRANS_WGRAD_SLOTS; tools/wgrad_probe.py sweeps it)
-WGRAD_SLOTS = int(os.environ.get('ONETRANS_WGRAD_SLOTS', '768'))
+# wgrad workgroups per launch (chunk sizing), by output tiles per chunk: weights of >= 8 tiles (d >= 256)
+# take ~3 rounds of the split kernel's 512 resident workgroups (C5 +7%, T +2% over 768); the small
+# C2 weights stay at 1.5 rounds (1536 measured 0.7% slower there: more slabs, and the wgrads share
+# the GPU with the overlapped dgrad chain).  Tuning override ONETRANS_WGRAD_SLOTS (both cases);
+# tools/wgrad_probe.py sweeps it.
+_SLOTS_ENV = os.environ.get('ONETRANS_WGRAD_SLOTS')
+WGRAD_SLOTS = int(_SLOTS_ENV) if _SLOTS_ENV else 1536
+WGRAD_SLOTS_SMALL = int(_SLOTS_ENV) if _SLOTS_ENV else 768
+
+
+def wgrad_slots(tiles_per_chunk: int) -> int:
+    return WGRAD_SLOTS if tiles_per_chunk >= 8 else WGRAD_SLOTS_SMALL
 
 
 def round_up(x: int, m: int) -> int:
@@ -112,9 +121,8 @@ class RowMap:
         return self.dev
 
     def chunks_for(self, tiles_per_chunk: int, device):
-        """wgrad chunk table whose workgroup count (chunks x output tiles) fits one resident round
-        (WGRAD_SLOTS): the smallest chunk size (multiple of 32 rows) that does.  Returns
-        (chunks_dev, gchunk_dev, nchunks)."""
+        """wgrad chunk table whose workgroup count (chunks x output tiles) stays within
+        wgrad_slots(tiles_per_chunk): the smallest chunk size (multiple of 32 rows) that does.  Returns (chunks_dev, gchunk_dev, nchunks)."""
         import torch
         key = (tiles_per_chunk, str(device))
         if key not in self._chunk_cache:
@@ -122,7 +130,7 @@ class RowMap:
             # every nonempty group needs a chunk of its own: on top of them, the budget of one round
             # (with as many groups as budget slots -- C5's 13 groups x 64 output tiles -- a budget of
             # one round would leave the shared group a single chunk, 64 workgroups on 256 CUs)
-            budget = max(1, WGRAD_SLOTS // max(1, tiles_per_chunk)) + sum(1 for p in padded if p > 0)
+            budget = max(1, wgrad_slots(tiles_per_chunk) // max(1, tiles_per_chunk)) + sum(1 for p in padded if p > 0)
             lo, hi = 32, max(32, round_up(max(padded) if padded else 32, 32))
             while lo < hi:
                 mid = round_up((lo + hi) // 2, 32)

@@ -13,7 +13,7 @@ A = torch.randn(M, Kd, device=dev)
 D = torch.randn(M, N, device=dev)
 dW = torch.empty(Kd, N, device=dev)
 for s in slots:
-    layout.WGRAD_SLOTS = s
+    layout.WGRAD_SLOTS = layout.WGRAD_SLOTS_SMALL = s
     rm = layout.identity_map(M)
     def fn():
         K.wgrad(A, Kd, None, D, N, None, Kd, N, None, 0, 1, dW, 0, accumulate=False, device=dev, m_rows=M, rowmap=rm)

@@ -112,3 +112,30 @@ def test_head_map():
     m = head_map(300, 2)
     assert m.ntiles == 2 * 3
     assert np.array_equal(m.rows[1][m.rows[1] >= 0], np.arange(600))
+
+
+@pytest.mark.parametrize('name,tiles', [('C2', 3), ('C2', 4), ('T', 12), ('C5', 64)])
+def test_wgrad_chunks_partition_and_budget(name, tiles):
+    """layout.RowMap.chunks_for: the chunks of each weight group tile its padded rows exactly once, in
+    32-row multiples, and the launch stays within the workgroup budget of layout.wgrad_slots (the
+    per-group floor aside: every nonempty group has a chunk of its own)."""
+    from recommend_amd import layout as L
+    cfg = workload_config(name)
+    I = cfg.num_ns_tokens + cfg.seq_token_count(cfg._seq_lens)       # L0: 140 / 140 / 1036
+    B = 64
+    mp = layer_maps(cfg, B, I, I)['all']
+    ch, gc, n = mp.chunks_for(tiles, 'cpu')
+    ch, gc = ch.numpy(), gc.numpy()
+    padded = [(r + TILE - 1) // TILE * TILE for r in mp.group_rows]
+    groups = sum(1 for p in padded if p > 0)
+    assert n == len(ch) and n * tiles <= L.wgrad_slots(tiles) + groups * tiles
+    base = 0
+    for g, p in enumerate(padded):
+        c0, cn = gc[g]
+        rows = ch[c0:c0 + cn]
+        assert np.all(rows[:, 0] == g)
+        assert np.all(rows[:-1, 2] % 32 == 0) if cn > 1 else True
+        assert sum(rows[:, 2]) == p and (cn == 0 or rows[0, 1] == base)
+        assert np.all(rows[1:, 1] == rows[:-1, 1] + rows[:-1, 2])
+        base += p
+    assert L.wgrad_slots(8) >= L.wgrad_slots(4)

@@ -284,8 +284,13 @@ extern "C" int ot_dropout_apply(const float* src, int64_t lds, float* dst, int64
   return OT_OK;
 }
 
+// rows per partial sum of ot_rows_colsum: short serial chains (each step an index load, then a row
+// load) and hundreds of blocks; 256 rows per block left the [SEP] gradient (8192 rows at C2) at 32
+// latency-bound blocks, 116 us
+constexpr int COLSUM_ROWS = 32;
+
 extern "C" size_t ot_rows_colsum_workspace_size(int64_t nrows, int ncols) {
-  const int64_t parts = ceil_div(nrows, 256);
+  const int64_t parts = ceil_div(nrows, COLSUM_ROWS);
   return (size_t)(parts * ncols + colsum_scratch_floats(parts, ncols)) * sizeof(float);
 }
 
@@ -293,10 +298,11 @@ extern "C" int ot_rows_colsum(const float* src, int64_t ld, const int32_t* rows,
                               float* out, int accumulate, void* workspace, size_t ws_bytes, void* stream) {
   OT_REQUIRE(src && out && ncols > 0, "ot_rows_colsum: bad args");
   OT_REQUIRE(workspace && ws_bytes >= ot_rows_colsum_workspace_size(nrows, ncols), "ot_rows_colsum: workspace");
-  const unsigned nb = ceil_div(nrows, 256);
+  const unsigned nb = ceil_div(nrows, COLSUM_ROWS);
   if (nb > 0) {
-    hipLaunchKernelGGL(rows_colsum_kernel, dim3(ceil_div(ncols, 256), nb), dim3(256), 0, (hipStream_t)stream,
-                       src, ld, rows, nrows, ncols, 256, (float*)workspace);
+    const int tpb = ncols >= 256 ? 256 : (int)ceil_div((int64_t)ncols, 64) * 64;
+    hipLaunchKernelGGL(rows_colsum_kernel, dim3(ceil_div(ncols, tpb), nb), dim3(tpb), 0, (hipStream_t)stream,
+                       src, ld, rows, nrows, ncols, COLSUM_ROWS, (float*)workspace);
     OT_LAUNCH_CHECK("ot_rows_colsum");
   }
   launch_colsum_reduce((const float*)workspace, (int64_t)nb, ncols, out, accumulate, (hipStream_t)stream,

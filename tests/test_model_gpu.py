@@ -53,6 +53,9 @@ CASES = {
     'criteo_norm_pyramid': lambda: norm_select(small_criteo('tail', pyramid=True, layers=3)),
     'criteo_d128_norm_pyramid': lambda: norm_select(small_criteo('tail', pyramid=True, layers=3, d=128, H=4, f=256,
                                                                  Lns=12, seq_lens=(20, 20, 20))),
+    # d = 256 (hd 64, as T/C3/C5): weights of >= 8 output tiles take the larger wgrad chunk budget
+    'criteo_d256_pyramid': lambda: small_criteo('tail', pyramid=True, layers=2, d=256, H=4, f=1024, Lns=4,
+                                                seq_lens=(12, 9, 7)),
 }
 
 
@@ -93,7 +96,8 @@ def ns_t(d, dev):
 
 
 @pytest.mark.parametrize('case', ['c1_head', 'criteo_head', 'criteo_tail_pyramid', 'criteo_d128_hd32',
-                                  'criteo_d128_pyramid', 'criteo_norm_pyramid', 'criteo_d128_norm_pyramid'])
+                                  'criteo_d128_pyramid', 'criteo_norm_pyramid', 'criteo_d128_norm_pyramid',
+                                  'criteo_d256_pyramid'])
 @pytest.mark.parametrize('training', [False, True])
 def test_gradient_parity(dev, case, training):
     cfg = CASES[case]()

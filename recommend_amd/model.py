@@ -311,7 +311,7 @@ class _Block(torch.autograd.Function):
 
 def _wgrad_single(m, A, D, K_, N, mt, dW, acc, dev, mrows=0, rowmap=None):
     """Wo gradient: one weight shared by every group -> wgrad with every chunk mapped to group 0
-    (chunked for one resident round of its single output tile when the row map is given)."""
+    (chunked by layout.wgrad_slots for its single output tile when the row map is given)."""
     if rowmap is not None and rowmap.group_rows:
         ch, _, _ = rowmap.chunks_for(((K_ + 127) // 128) * ((N + 127) // 128), dev)
         mp = m.single_group_chunks({'chunks': ch})

@@ -165,7 +165,7 @@ def wgrad(A: Ptrish, lda: int, a_rows: Ptrish, D: Ptrish, ldd: int, d_rows: Ptri
           a_xform: int = 0, rstd: Ptrish = None, gamma: Ptrish = None, accumulate: bool = False,
           device=None, m_rows: int = 0, rowmap=None) -> None:
     """rmap_dev: dict with 'chunks'/'gchunk' device tensors; when ``rowmap`` (a layout.RowMap) is given
-    its chunking is re-balanced for this call's output tile count (one resident round)."""
+    its chunking is re-balanced for this call's output tile count (layout.wgrad_slots)."""
     if rowmap is not None and rowmap.group_rows:
         tiles = ((K + 127) // 128) * ((N + 127) // 128)
         ch, gc, nchunks = rowmap.chunks_for(tiles, device)

@@ -25,14 +25,15 @@ from .params import dense_param_shapes, keras_variables
 
 TILE = 128
 ALIGN = 64
-# wgrad workgroups per launch (chunk sizing), by output tiles per chunk: weights of >= 8 tiles (d >= 256)
-# take ~3 rounds of the split kernel's 512 resident workgroups (C5 +7%, T +2% over 768); the small
-# C2 weights stay at 1.5 rounds (1536 measured 0.7% slower there: more slabs, and the wgrads share
-# the GPU with the overlapped dgrad chain).  Tuning override ONETRANS_WGRAD_SLOTS (both cases);
-# tools/wgrad_probe.py sweeps it.
+# wgrad workgroups per launch (chunk sizing), by output tiles per chunk.  Small weights (< 8 tiles:
+# all of C2's) are capped at one round of the split kernel's 512 resident workgroups -- a count just
+# past a multiple of 512 (e.g. 513) leaves a nearly empty extra round; capped, the C2 GEMM family
+# measured 332 -> 316 us/launch standalone.  Weights of >= 8 tiles (d >= 256) take ~3 rounds plus one
+# chunk per weight group (C5 +5-7%, T +2% over 768; a hard cap measured worse there).  Tuning override
+# ONETRANS_WGRAD_SLOTS (both cases); tools/wgrad_probe.py sweeps it.
 _SLOTS_ENV = os.environ.get('ONETRANS_WGRAD_SLOTS')
 WGRAD_SLOTS = int(_SLOTS_ENV) if _SLOTS_ENV else 1536
-WGRAD_SLOTS_SMALL = int(_SLOTS_ENV) if _SLOTS_ENV else 768
+WGRAD_SLOTS_SMALL = int(_SLOTS_ENV) if _SLOTS_ENV else 512
 
 
 def wgrad_slots(tiles_per_chunk: int) -> int:
@@ -130,7 +131,11 @@ class RowMap:
             # every nonempty group needs a chunk of its own: on top of them, the budget of one round
             # (with as many groups as budget slots -- C5's 13 groups x 64 output tiles -- a budget of
             # one round would leave the shared group a single chunk, 64 workgroups on 256 CUs)
-            budget = max(1, wgrad_slots(tiles_per_chunk) // max(1, tiles_per_chunk)) + sum(1 for p in padded if p > 0)
+            ng = sum(1 for p in padded if p > 0)
+            if tiles_per_chunk < 8:       # hard cap: chunks x tiles within the slots (groups floor aside)
+                budget = max(ng, wgrad_slots(tiles_per_chunk) // max(1, tiles_per_chunk))
+            else:
+                budget = max(1, wgrad_slots(tiles_per_chunk) // max(1, tiles_per_chunk)) + ng
             lo, hi = 32, max(32, round_up(max(padded) if padded else 32, 32))
             while lo < hi:
                 mid = round_up((lo + hi) // 2, 32)

@@ -235,6 +235,13 @@ int ot_bce_fwd(const float* probs, const float* labels, int T, int B, float* los
 /* dprobs = gscale[0] * d loss / d probs (zero where p was clipped) */
 int ot_bce_bwd(const float* probs, const float* labels, const float* gscale, int T, int B, float* dprobs,
                void* stream);
+/* Per-task loss of train.py:78-93: task t is tf.keras.losses.MeanSquaredError (SUM_OVER_BATCH_SIZE:
+ * mean_b (y - p)^2) when bit t of mse_mask is set (tasks other than 'ctr'/'cvr'), the BCE above
+ * otherwise; loss = sum over the T <= 32 tasks.  ot_bce_* == mse_mask 0.  Workspace: ot_bce_workspace_size. */
+int ot_task_loss_fwd(const float* probs, const float* labels, int T, int B, unsigned mse_mask, float* loss,
+                     void* workspace, size_t ws_bytes, void* stream);
+int ot_task_loss_bwd(const float* probs, const float* labels, const float* gscale, int T, int B,
+                     unsigned mse_mask, float* dprobs, void* stream);
 
 /* ---- sparse embedding update (embedding.hip) ----------------------------------------------
  * Build extension (no reference site; paper: sparse Adagrad, clip 120, complete_translation.md:190).

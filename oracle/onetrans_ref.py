@@ -260,6 +260,16 @@ def keras_bce(y: Tensor, p: Tensor) -> Tensor:
     return torch.mean(-(y * torch.log(pc + eps) + (1.0 - y) * torch.log(1.0 - pc + eps)))
 
 
+def keras_mse(y: Tensor, p: Tensor) -> Tensor:
+    """tf.keras.losses.MeanSquaredError(SUM_OVER_BATCH_SIZE) on [B,1] (train.py:88-91)."""
+    return torch.mean((y - p) ** 2)
+
+
+def task_loss(task: str, y: Tensor, p: Tensor) -> Tensor:
+    """train.py:82-91: BCE for 'ctr'/'cvr', MSE for every other task."""
+    return keras_bce(y, p) if task in ('ctr', 'cvr') else keras_mse(y, p)
+
+
 def to_torch(arrs: Dict[str, np.ndarray], dtype=torch.float64, requires_grad=False) -> Dict[str, Tensor]:
     out = {}
     for k, v in arrs.items():
@@ -279,7 +289,7 @@ def loss_and_grads(P: Dict[str, Tensor], cfg, ns, seq, labels, training=True, se
     out = forward(leaves, cfg, ns, seq, training=training, seed=seed, variant=variant)
     loss = 0.0
     for t in cfg.tasks:
-        loss = loss + keras_bce(labels[t].to(out['probs'][t].dtype), out['probs'][t])
+        loss = loss + task_loss(t, labels[t].to(out['probs'][t].dtype), out['probs'][t])
     loss.backward()
     grads = {k: (v.grad if v.grad is not None else torch.zeros_like(v)) for k, v in leaves.items()}
     return loss.detach(), grads, out

@@ -9,6 +9,7 @@ __version__ = '1.0.0'
 
 from .config import OneTransConfig, get_model_config, workload_config  # noqa: F401
 from .data import create_sample_batch, criteo_batch, make_batch  # noqa: F401
+from .features import DataLoader, FeatureProcessor, OneTransDataset, SequenceProcessor  # noqa: F401
 from .metrics import auc, keras_auc  # noqa: F401
 
 
@@ -23,5 +24,5 @@ def __getattr__(name):
     raise AttributeError(name)
 
 
-__all__ = ['OneTransModel', 'OneTransConfig', 'get_model_config', 'OneTransTrainer', 'train_one_trans_model',
-           'create_sample_batch', 'criteo_batch', 'make_batch', 'workload_config', 'auc', 'keras_auc']
+__all__ = ['OneTransModel', 'OneTransConfig', 'get_model_config', 'DataLoader', 'FeatureProcessor',
+           'SequenceProcessor', 'OneTransDataset', 'OneTransTrainer', 'train_one_trans_model', 'create_sample_batch', 'criteo_batch', 'make_batch', 'workload_config', 'auc', 'keras_auc']

@@ -6,6 +6,7 @@
 //                    into the GEMM's A-row load)
 //   ot_head_fwd/bwd  task heads model.py:325-330, 388-391 (second Dense(1, sigmoid) + sigmoid)
 //   ot_bce_fwd/bwd   tf.keras.losses.BinaryCrossentropy(from_logits=False) train.py:84-87,124-128
+//   ot_task_loss_*   per-task BCE ('ctr'/'cvr') or MeanSquaredError (other tasks) train.py:78-93
 #include "common.h"
 
 namespace ot {
@@ -128,13 +129,20 @@ __device__ __forceinline__ float keras_bce(float y, float p) {
   return -(y * logf(pc + eps) + (1.f - y) * logf(1.f - pc + eps));
 }
 
-// part[blk] = sum over this block's elements of bce / B (elements = T*B, task-major)
+// Keras MeanSquaredError on one [B,1] prediction (train.py:88-91): (y - p)^2
+__device__ __forceinline__ float task_loss(float y, float p, bool mse) {
+  if (mse) { const float e = p - y; return e * e; }
+  return keras_bce(y, p);
+}
+
+// part[blk] = sum over this block's elements of loss / B (elements = T*B, task-major; task t uses MSE
+// when bit t of mse_mask is set, BCE otherwise)
 __global__ __launch_bounds__(256) void bce_fwd_kernel(const float* __restrict__ probs, const float* __restrict__ labels,
-                                                      int64_t n, float invB, float* part) {
+                                                      int64_t n, int B, float invB, unsigned mse_mask, float* part) {
   __shared__ float red[4];
   float s = 0.f;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
-    s += keras_bce(labels[i], probs[i]) * invB;
+    s += task_loss(labels[i], probs[i], (mse_mask >> (int)(i / B)) & 1u) * invB;
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
@@ -150,13 +158,15 @@ __global__ void bce_reduce_kernel(const float* __restrict__ part, int nb, float*
 }
 
 __global__ void bce_bwd_kernel(const float* __restrict__ probs, const float* __restrict__ labels,
-                               const float* __restrict__ gscale, int64_t n, float invB, float* dprobs) {
+                               const float* __restrict__ gscale, int64_t n, int B, float invB, unsigned mse_mask,
+                               float* dprobs) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const float eps = 1e-7f;
   const float p = probs[i], y = labels[i];
   float g = 0.f;
-  if (p >= eps && p <= 1.f - eps) g = (-y / (p + eps) + (1.f - y) / (1.f - p + eps)) * invB;
+  if ((mse_mask >> (int)(i / B)) & 1u) g = 2.f * (p - y) * invB;
+  else if (p >= eps && p <= 1.f - eps) g = (-y / (p + eps) + (1.f - y) / (1.f - p + eps)) * invB;
   dprobs[i] = g * gscale[0];
 }
 
@@ -246,27 +256,39 @@ extern "C" int ot_head_bwd(const float* pre1, const float* w2, const float* prob
 
 extern "C" size_t ot_bce_workspace_size(int T, int B) { return (size_t)bce_blocks((int64_t)T * B) * sizeof(float); }
 
-extern "C" int ot_bce_fwd(const float* probs, const float* labels, int T, int B, float* loss, void* workspace,
-                          size_t ws_bytes, void* stream) {
-  OT_REQUIRE(probs && labels && loss && workspace, "ot_bce_fwd: null operand");
-  OT_REQUIRE(ws_bytes >= ot_bce_workspace_size(T, B), "ot_bce_fwd: workspace too small");
-  OT_REQUIRE(B > 0, "ot_bce_fwd: empty batch");
+extern "C" int ot_task_loss_fwd(const float* probs, const float* labels, int T, int B, unsigned mse_mask, float* loss,
+                                void* workspace, size_t ws_bytes, void* stream) {
+  OT_REQUIRE(probs && labels && loss && workspace, "ot_task_loss_fwd: null operand");
+  OT_REQUIRE(ws_bytes >= ot_bce_workspace_size(T, B), "ot_task_loss_fwd: workspace too small");
+  OT_REQUIRE(B > 0, "ot_task_loss_fwd: empty batch");
+  OT_REQUIRE(T > 0 && T <= 32, "ot_task_loss_fwd: 1..32 tasks");
   const int64_t n = (int64_t)T * B;
   const int nb = bce_blocks(n);
-  hipLaunchKernelGGL(bce_fwd_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, probs, labels, n, 1.f / B,
-                     (float*)workspace);
-  OT_LAUNCH_CHECK("ot_bce_fwd");
+  hipLaunchKernelGGL(bce_fwd_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, probs, labels, n, B, 1.f / B,
+                     mse_mask, (float*)workspace);
+  OT_LAUNCH_CHECK("ot_task_loss_fwd");
   hipLaunchKernelGGL(bce_reduce_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (const float*)workspace, nb, loss);
-  OT_LAUNCH_CHECK("ot_bce_fwd(reduce)");
+  OT_LAUNCH_CHECK("ot_task_loss_fwd(reduce)");
   return OT_OK;
+}
+
+extern "C" int ot_task_loss_bwd(const float* probs, const float* labels, const float* gscale, int T, int B,
+                                unsigned mse_mask, float* dprobs, void* stream) {
+  OT_REQUIRE(probs && labels && gscale && dprobs && B > 0, "ot_task_loss_bwd: bad args");
+  OT_REQUIRE(T > 0 && T <= 32, "ot_task_loss_bwd: 1..32 tasks");
+  const int64_t n = (int64_t)T * B;
+  hipLaunchKernelGGL(bce_bwd_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream, probs, labels, gscale,
+                     n, B, 1.f / B, mse_mask, dprobs);
+  OT_LAUNCH_CHECK("ot_task_loss_bwd");
+  return OT_OK;
+}
+
+extern "C" int ot_bce_fwd(const float* probs, const float* labels, int T, int B, float* loss, void* workspace,
+                          size_t ws_bytes, void* stream) {
+  return ot_task_loss_fwd(probs, labels, T, B, 0u, loss, workspace, ws_bytes, stream);
 }
 
 extern "C" int ot_bce_bwd(const float* probs, const float* labels, const float* gscale, int T, int B, float* dprobs,
                           void* stream) {
-  OT_REQUIRE(probs && labels && gscale && dprobs && B > 0, "ot_bce_bwd: bad args");
-  const int64_t n = (int64_t)T * B;
-  hipLaunchKernelGGL(bce_bwd_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream, probs, labels, gscale,
-                     n, 1.f / B, dprobs);
-  OT_LAUNCH_CHECK("ot_bce_bwd");
-  return OT_OK;
+  return ot_task_loss_bwd(probs, labels, gscale, T, B, 0u, dprobs, stream);
 }

@@ -293,17 +293,18 @@ def head_bwd(pre1, w2, probs, dprobs, T, B, dh, dpre1, dw2, db2, sw2, sb2, accum
         _probe.end('head_loss', 0.0, ev)
 
 
-def bce_fwd(probs, labels, T, B, loss, device=None) -> None:
+def bce_fwd(probs, labels, T, B, loss, device=None, mse_mask: int = 0) -> None:
+    """Σ_task loss (train.py:78-93): BCE, or MSE for the tasks whose bit is set in ``mse_mask``."""
     ws = workspace(size('ot_bce_workspace_size', T, B), device)
     ev = _probe.begin() if _probe is not None else None
-    call('ot_bce_fwd', ptr(probs), ptr(labels), T, B, ptr(loss), ptr(ws), ws.numel(), stream())
+    call('ot_task_loss_fwd', ptr(probs), ptr(labels), T, B, mse_mask, ptr(loss), ptr(ws), ws.numel(), stream())
     if ev is not None:
         _probe.end('head_loss', 0.0, ev)
 
 
-def bce_bwd(probs, labels, gscale, T, B, dprobs) -> None:
+def bce_bwd(probs, labels, gscale, T, B, dprobs, mse_mask: int = 0) -> None:
     ev = _probe.begin() if _probe is not None else None
-    call('ot_bce_bwd', ptr(probs), ptr(labels), ptr(gscale), T, B, ptr(dprobs), stream())
+    call('ot_task_loss_bwd', ptr(probs), ptr(labels), ptr(gscale), T, B, mse_mask, ptr(dprobs), stream())
     if ev is not None:
         _probe.end('head_loss', 0.0, ev)
 

@@ -380,14 +380,16 @@ class _Head(torch.autograd.Function):
 
 
 class _BCE(torch.autograd.Function):
-    """Σ_task tf.keras.losses.BinaryCrossentropy (train.py:84-87, 124-128) on probs [T, B]."""
+    """Σ_task loss (train.py:78-93, 124-128) on probs [T, B]: tf.keras BinaryCrossentropy for 'ctr' /
+    'cvr', MeanSquaredError for any other task (bit t of ``mse_mask``)."""
 
     @staticmethod
-    def forward(ctx, probs, labels):
+    def forward(ctx, probs, labels, mse_mask):
         T, B = probs.shape
         loss = torch.empty(1, device=probs.device)
-        K.bce_fwd(probs, labels, T, B, loss, device=probs.device)
+        K.bce_fwd(probs, labels, T, B, loss, device=probs.device, mse_mask=mse_mask)
         ctx.save_for_backward(probs, labels)
+        ctx.mse_mask = mse_mask
         return loss[0]
 
     @staticmethod
@@ -396,13 +398,24 @@ class _BCE(torch.autograd.Function):
         T, B = probs.shape
         dprobs = torch.empty_like(probs)
         gl = gl.reshape(1).contiguous().float()
-        K.bce_bwd(probs, labels, gl, T, B, dprobs)
-        return dprobs, None
+        K.bce_bwd(probs, labels, gl, T, B, dprobs, mse_mask=ctx.mse_mask)
+        return dprobs, None, None
 
 
-def keras_bce_loss(labels: torch.Tensor, probs: torch.Tensor) -> torch.Tensor:
-    """Sum over tasks of the Keras BCE; labels/probs [T, B] device tensors."""
-    return _BCE.apply(probs, labels)
+BINARY_TASKS = ('ctr', 'cvr')      # train.py:83: BCE for these, MSE for every other task
+
+
+def task_mse_mask(tasks) -> int:
+    """Bit t set when task t trains with MeanSquaredError (train.py:88-91)."""
+    if len(tasks) > 32:
+        raise ValueError('at most 32 tasks')
+    return sum(1 << i for i, t in enumerate(tasks) if t not in BINARY_TASKS)
+
+
+def keras_bce_loss(labels: torch.Tensor, probs: torch.Tensor, tasks=None) -> torch.Tensor:
+    """Sum over tasks of the reference's per-task loss; labels/probs [T, B] device tensors.  ``tasks``
+    (names, in row order) selects MSE for tasks other than 'ctr'/'cvr'; None = BCE for every row."""
+    return _BCE.apply(probs, labels, task_mse_mask(tasks) if tasks is not None else 0)
 
 
 # =============================================================================== the module
@@ -485,6 +498,16 @@ class OneTransModel(nn.Module):
         """Load host arrays (params.init_params layout; tok.ns.kernel may be unpadded)."""
         with torch.no_grad():
             for name, arr in params.items():
+                if name in self.sharded:
+                    # row-sharded: keep only this rank's rows (id % world == rank) in the shard the
+                    # lookups and updates use; self.tables[name] stays that shard
+                    st = self.sharded[name]
+                    arr = np.asarray(arr)
+                    if arr.shape != (st.num_rows, st.E):
+                        raise ValueError(f'{name}: loaded shape {arr.shape} != ({st.num_rows}, {st.E})')
+                    st.table[:st.local_rows].copy_(torch.as_tensor(arr[st.rank::st.world], dtype=torch.float32))
+                    self.tables[name] = st.table
+                    continue
                 if name.startswith('emb.'):
                     self.tables[name] = torch.as_tensor(np.asarray(arr), dtype=torch.float32).to(self.device).contiguous()
                     continue
@@ -498,6 +521,8 @@ class OneTransModel(nn.Module):
         self.refresh_shadow()
 
     def param_dict(self) -> Dict[str, np.ndarray]:
+        """Host copies of every parameter.  With a row-sharded table this is a COLLECTIVE (the table
+        is all-gathered): every rank must call it (``save_weights`` too), not only rank 0."""
         out = {}
         for name in self.layout.shapes:
             v = self.p(name).detach().cpu().numpy().copy()
@@ -776,9 +801,18 @@ class OneTransModel(nn.Module):
                 'embedding_rows': {k: int(v.shape[0]) for k, v in self.tables.items()}}
 
     def save_weights(self, path: str) -> None:
-        """Counterpart of model.save_weights (train.py:286): one .npz of named banks."""
+        """Counterpart of model.save_weights (train.py:286): one .npz of named banks.  Collective when a
+        table is row-sharded (every rank calls it; the gathered table is written by rank 0 only)."""
+        params = self.param_dict()
+        if self.sharded and self._rank() != 0:
+            return
         os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
-        np.savez(path, **self.param_dict())
+        np.savez(path, **params)
+
+    @staticmethod
+    def _rank() -> int:
+        import torch.distributed as dist
+        return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
 
     def load_weights(self, path: str) -> None:
         """Counterpart of model.load_weights (train.py:332)."""

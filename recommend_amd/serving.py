@@ -218,9 +218,15 @@ class OneTransServer:
         dev = m.device
         plan = m._plan(non_seq_features, {})
         C = plan['B']
-        req = req.to(dev, torch.int32).contiguous()
+        req = torch.as_tensor(req)
         if req.numel() != C:
             raise ValueError(f'score: {req.numel()} request indices for {C} candidates')
+        # the cached-attention kernel indexes the K/V cache with req unchecked: validate before launch
+        # (host indices directly; device indices with one min/max read-back)
+        lo, hi = (int(v) for v in torch.aminmax(req.reshape(-1).to(torch.int64)))
+        if lo < 0 or hi >= cache.R:
+            raise ValueError(f'score: request index out of range [0, {cache.R}) (min {lo}, max {hi})')
+        req = req.to(dev, torch.int32).contiguous()
         x = _Tokenize.apply(m.flat, m, plan)                              # [C*L_NS, d]: NS tokens only
         for l, e in enumerate(self.schedule(cache.L_S)):
             s, n, kN = e['s'], e['n'], e['kN']

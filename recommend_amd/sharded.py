@@ -43,6 +43,14 @@ class ShardedTable:
         else:
             K.hash_uniform_rows(self.table, self.local_rows, self.E, self.rank, self.world, seed, lo, hi)
         self.last_route = None
+        self.events = None        # diagnostics: a list collects HIP-event pairs around lookup / update
+
+    def _mark(self):
+        if self.events is None:
+            return None
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
 
     # -------------------------------------------------------------- all-to-all helpers
     def _a2a(self, out, inp, out_splits, in_splits):
@@ -57,6 +65,7 @@ class ShardedTable:
 
     def lookup(self, ids: torch.Tensor) -> torch.Tensor:
         """Rows of ``ids`` (int64 [n]) in order -> [n, E] fp32 (zeros for ids outside the table)."""
+        ev0 = self._mark()
         ids = ids.reshape(-1).contiguous()
         n, E, dev = ids.numel(), self.E, self.device
         perm = torch.empty(max(1, n), dtype=torch.int32, device=dev)
@@ -77,6 +86,8 @@ class ShardedTable:
         out = torch.empty(n, E, device=dev)
         K.permute_rows(back, perm, n, E, True, out)
         self.last_route = (n, perm, send_splits, recv_splits, recv_local, R)
+        if ev0 is not None:
+            self.events.append((ev0, self._mark()))
         return out
 
     def apply_gradient(self, route, grads: torch.Tensor, accum: torch.Tensor, lr: float, eps: float,
@@ -89,6 +100,7 @@ class ShardedTable:
         if grads.shape[0] != n:
             raise ValueError(f'{self.name}: {grads.shape[0]} gradient rows for a route of {n} ids')
         E, dev = self.E, self.device
+        ev0 = self._mark()
         send = torch.empty(max(1, n), E, device=dev)
         K.permute_rows(grads.contiguous(), perm, n, E, False, send)
         recv = torch.empty(max(1, R), E, device=dev)
@@ -106,6 +118,8 @@ class ShardedTable:
             else:
                 dist.all_reduce(sumsq)
         K.sparse_finish(self.table, accum, E, R, lr, eps, clip, sumsq, ws)
+        if ev0 is not None:
+            self.events.append((ev0, self._mark()))
 
     def full_table(self) -> torch.Tensor:
         """Gather the logical table on every rank (tests / checkpoints of small tables)."""

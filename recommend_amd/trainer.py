@@ -66,6 +66,25 @@ class OneTransOptimizer:
         # data-parallel exchange of replicated tables: dense all-reduce up to this size, else all-gather
         self.dense_exchange_bytes = int(float(os.environ.get('ONETRANS_DENSE_EXCHANGE_MB', '512')) * 2 ** 20)
         self._dense_grad: Dict[str, torch.Tensor] = {}
+        # diagnostics (bench.py, N > 1): when a list, every step appends HIP-event pairs bracketing the
+        # main stream's waits for the gradient exchange, i.e. the exchange time NOT hidden by backward
+        self.exchange_events = None
+
+    def _mark(self):
+        if self.exchange_events is None:
+            return None
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+
+    def exposed_exchange_ms(self) -> float:
+        """Sum over the recorded steps of the exposed exchange time (ms); clears the record."""
+        if not self.exchange_events:
+            return 0.0
+        torch.cuda.synchronize()
+        ms = sum(a.elapsed_time(b) for (a, b) in self.exchange_events)
+        self.exchange_events = []
+        return ms
 
     # ---------------------------------------------------------------- DP exchange overlapped with backward
     def bank_ranges(self):
@@ -107,6 +126,7 @@ class OneTransOptimizer:
         # replicated tables small enough to exchange densely: scatter the de-duplicated gradient and
         # start its all-reduce first, so the dense optimizer below runs while it is in flight
         early = {}
+        ev_a = self._mark() if otdist.world() > 1 else None
         if otdist.world() > 1:
             for (name, keys, grads) in m._pending_sparse:
                 table = m.tables[name]
@@ -130,6 +150,8 @@ class OneTransOptimizer:
             self._works = []
         else:
             otdist.allreduce_dense(m.flat.grad)
+        if ev_a is not None:
+            self.exchange_events.append((ev_a, self._mark()))
         K.clip_rmsprop(m.flat.data, m.flat.grad, self.v, self.m, self.segs, self.nseg, m.layout.max_seg_elems,
                        self.lr, self.rho, self.eps, self.momentum, self.clip, device=m.flat.device)
         m.refresh_shadow()
@@ -144,7 +166,10 @@ class OneTransOptimizer:
                 # one all-reduce of the de-duplicated dense gradient (started above) instead of
                 # all-gathering every rank's rows
                 g, work = early[name]
+                ev_c = self._mark()
                 work.wait()
+                if ev_c is not None:
+                    self.exchange_events.append((ev_c, self._mark()))
                 g.mul_(1.0 / otdist.world())
                 K.dense_adagrad(table, self.acc[name], g, rows, E, self.sparse_lr, self.sparse_eps,
                                 self.sparse_clip, device=table.device)
@@ -175,7 +200,7 @@ class OneTransTrainer:
         y = labels if isinstance(labels, torch.Tensor) else stack_labels(labels, self.config.tasks, dev)
         self.model.train()
         probs = self.model.forward_probs(_to_dev(non_seq, dev), _to_dev(seq, dev), training=True)
-        loss = keras_bce_loss(y, probs)
+        loss = keras_bce_loss(y, probs, self.config.tasks)
         self.optimizer.begin_backward()
         loss.backward()
         self.optimizer.step()
@@ -188,7 +213,7 @@ class OneTransTrainer:
         dev = self.device
         y = labels if isinstance(labels, torch.Tensor) else stack_labels(labels, self.config.tasks, dev)
         probs = self.model.forward_probs(_to_dev(non_seq, dev), _to_dev(seq, dev), training=False)
-        loss = keras_bce_loss(y, probs)
+        loss = keras_bce_loss(y, probs, self.config.tasks)
         return {'total_loss': loss, 'probs': probs}
 
     def evaluate(self, batches) -> Dict[str, float]:

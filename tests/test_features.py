@@ -25,13 +25,14 @@ def test_zscore_clip_matches_pandas():
     assert np.array_equal(fp.process_numerical_feature('age', np.array([7.0])), [7.0])   # unfitted: as is
 
 
-def test_categorical_ids_and_one_hot():
+def test_categorical_one_hot_default_and_ids():
     fp = FeatureProcessor(OneTransConfig()).fit({'item_id': np.array([0, 3, 4])})
-    assert fp.process_categorical_feature('item_id', np.array([4, 0])).tolist() == [4, 0]
-    oh = fp.process_categorical_feature('item_id', np.array([4, 1]), one_hot=True)    # data_loader.py:66-68
-    assert oh.shape == (2, 5) and oh[0, 4] == 1 and oh[1, 1] == 1 and oh.sum() == 2
+    oh = fp.process_categorical_feature('item_id', np.array([4, 1, 9]))              # data_loader.py:60-68
+    assert oh.shape == (3, 5) and oh[0, 4] == 1 and oh[1, 1] == 1 and oh.sum() == 2   # id 9: all-zero row
+    ids = fp.process_categorical_feature('item_id', np.array([4, 0]), one_hot=False)  # embedding-path opt-in
+    assert ids.dtype == np.int64 and ids.tolist() == [4, 0]
     with pytest.raises(ValueError):
-        fp.process_categorical_feature('item_id', np.array([5]))
+        fp.process_categorical_feature('item_id', np.array([5]), one_hot=False)
 
 
 def test_sequence_pad_truncate():
@@ -61,7 +62,7 @@ def test_dataset_batches():
     non_seq = {'user_id': rng.integers(0, 100, N), 'price': rng.uniform(0, 10, N)}
     seq = {'click_seq': [rng.standard_normal((int(rng.integers(0, 12)), 64)) for _ in range(N)]}
     labels = {'ctr': rng.integers(0, 2, N), 'cvr': rng.integers(0, 2, N)}
-    ds = OneTransDataset(cfg, non_seq, seq, labels)
+    ds = OneTransDataset(cfg, non_seq=non_seq, seq=seq, labels=labels)
     bs = list(ds.batches(16, shuffle=True, seed=3))
     assert [b[0]['user_id'].shape[0] for b in bs] == [16, 16, 16, 2]
     ns, sq, lab = bs[0]
@@ -73,3 +74,27 @@ def test_dataset_batches():
     seen = np.concatenate([b[0]['user_id'][:, 0] for b in ds.batches(16, shuffle=False)])
     assert np.array_equal(seen, non_seq['user_id'])
     assert sum(1 for _ in ds.batches(16, drop_last=True)) == 3
+
+
+def test_dataloader_surface():
+    """data_loader.py:236-297: unloaded datasets raise ValueError; load_datasets fills the reference's
+    1000-sample synthetic sets; batches feed the trainer's (non_seq, seq, labels) form."""
+    from recommend_amd import DataLoader
+    cfg = OneTransConfig()
+    cfg.max_seq_len = 6
+    dl = DataLoader(cfg)
+    for get in (dl.get_train_dataset, dl.get_val_dataset, dl.get_test_dataset):
+        with pytest.raises(ValueError):
+            get()
+    assert dl.get_data_info() == {}
+    np.random.seed(0)
+    dl.load_datasets('train', 'val', 'test')
+    assert dl.get_data_info() == {'train_samples': 1000, 'val_samples': 1000, 'test_samples': 1000}
+    bs = dl.get_val_dataset(batch_size=256)
+    assert [b[0]['user_id'].shape[0] for b in bs] == [256, 256, 256, 232]
+    ns, seq, lab = bs[0]
+    assert set(seq) == set(cfg.feature_config['sequence_features'])
+    assert seq['click_seq'].shape == (256, 6, 64) and lab['ctr'].shape == (256, 1)
+    ns1, seq1, lab1 = dl.val_dataset[0]
+    assert ns1['user_id'] == dl.val_dataset.non_seq_data['user_id'][0]      # unfitted processor: as is
+    assert seq1['click_seq'].shape == (6, 64)

@@ -121,7 +121,7 @@ def check_grads(cfg, B, dev, training):
     if training:
         seed = (model.dropout_seed + 0x9E3779B9 * model._step) & 0xFFFFFFFF
     y = stack_labels(lab, cfg.tasks, dev)
-    loss = keras_bce_loss(y, probs)
+    loss = keras_bce_loss(y, probs, cfg.tasks)
     loss.backward()
     rl, rg, rout = R.loss_and_grads(R.to_torch(P), cfg, R.to_torch(ns), R.to_torch(seq), R.to_torch(lab),
                                     training=training, seed=seed)
@@ -141,6 +141,14 @@ def check_grads(cfg, B, dev, training):
         dense.index_add_(0, keys.cpu(), grads.double().cpu())
         scale = max(1e-3, rg[tname].abs().max().item())
         assert (dense - rg[tname]).abs().max().item() / scale < 2e-4, tname
+
+
+def test_regression_task_mse(dev):
+    """A task other than 'ctr'/'cvr' trains with Keras MeanSquaredError (train.py:88-91): loss and every
+    gradient vs the oracle, with one BCE task and one MSE task."""
+    cfg = small_criteo('head')
+    cfg.tasks = ['ctr', 'watch_time']
+    check_grads(cfg, 37, dev, training=True)
 
 
 @pytest.mark.parametrize('case', ['c1_head', 'criteo_head', 'criteo_d128_pyramid'])

@@ -84,6 +84,21 @@ def test_cache_reuse_across_calls(dev):
         torch.testing.assert_close(a[t][:6], b[t], rtol=0, atol=0)
 
 
+def test_bad_request_index_refused(dev):
+    """A request index outside [0, R) is refused on the host before the cached-attention launch."""
+    cfg = small_criteo('tail', pyramid=True, layers=3)
+    model = OneTransModel(cfg, device=dev, init=init_params(cfg, cfg.ns_input_width(), seed=0))
+    _, seq_r, _ = make_batch(3, cfg, seed=5)
+    ns_c, _, _ = make_batch(4, cfg, seed=6)
+    srv = OneTransServer(model)
+    cache = srv.encode_requests(ns_t(seq_r, dev))
+    for bad in ([0, 1, 2, 3], [0, -1, 1, 2]):
+        with pytest.raises(ValueError):
+            srv.score(cache, torch.tensor(bad), ns_t(ns_c, dev))
+        with pytest.raises(ValueError):
+            srv.score(cache, torch.tensor(bad, device=dev), ns_t(ns_c, dev))
+
+
 def test_norm_select_refused(dev):
     cfg = small_criteo('tail', pyramid=True, layers=3)
     cfg.pyramid_select = 'norm'

@@ -6,7 +6,9 @@ the exchange code is the same, gloo stages the all-to-alls through host memory).
   (zeros for out-of-range ids), and apply_gradient == the oracle's de-duplicated, globally clipped
   Keras Adagrad (oracle/onetrans_ref.py train_step, sparse part) on the full table;
 * three training steps of OneTransModel with 'emb.seq_item' row-sharded over 2 ranks (each rank on
-  half the batch) == the oracle's full-batch train_step, every parameter and the logical table."""
+  half the batch) == the oracle's full-batch train_step, every parameter and the logical table;
+* a checkpoint of the row-sharded model (collective save_weights) loads into a fresh sharded model
+  bit-identically, and the loaded model's predictions are identical."""
 
 import os
 import socket
@@ -103,6 +105,28 @@ def _worker(rank, world, port, q, sharding='row'):
             res[f'loss{step}'] = abs(losses[-1] - float(rl))
         got = model.param_dict()
         res['params'] = {k: float(np.abs(got[k] - v.detach().numpy()).max()) for k, v in Pt.items()}
+        if sharding == 'row':
+            # checkpoint round trip with the table row-sharded: save_weights is collective (rank 0
+            # writes), load_weights fills each rank's shard, and the loaded model predicts the same
+            import tempfile
+            path = os.path.join(tempfile.gettempdir(), f'ot_shard_ckpt_{os.environ["MASTER_PORT"]}.npz')
+            model.save_weights(path)
+            dist.barrier()
+            fresh = OneTransModel(cfg, device=dev, seed=123)
+            fresh.load_weights(path)
+            assert fresh.tables['emb.seq_item'] is fresh.sharded['emb.seq_item'].table
+            back = fresh.param_dict()
+            res['ckpt'] = max(float(np.abs(back[k] - got[k]).max()) for k in got)
+            ns, seq, _ = make_batch(B, cfg, seed=4000)
+            sl = slice(rank * B // world, (rank + 1) * B // world)
+            tdev = lambda d: {k: torch.from_numpy(v[sl]).to(dev) for k, v in d.items()}
+            with torch.no_grad():
+                a = model.forward_probs(tdev(ns), tdev(seq), training=False)
+                b = fresh.forward_probs(tdev(ns), tdev(seq), training=False)
+            res['ckpt_fwd'] = float((a - b).abs().max())
+            dist.barrier()
+            if rank == 0:
+                os.remove(path)
         if rank == 0:
             q.put(res)
     finally:
@@ -139,3 +163,5 @@ def test_row_sharded_table_two_ranks(sharding):
         assert res[f'loss{step}'] < 2e-4, (step, res[f'loss{step}'])
     bad = {k: v for k, v in res['params'].items() if v >= 2e-4}
     assert not bad, bad
+    if sharding == 'row':
+        assert res['ckpt'] == 0.0 and res['ckpt_fwd'] == 0.0, (res['ckpt'], res['ckpt_fwd'])

@@ -46,9 +46,10 @@ def gelu(x: Tensor) -> Tensor:
 
 
 def dropout_scale(seed: int, site: int, B: int, I: int, d: int, positions: np.ndarray,
-                  rate: float, dtype) -> Tensor:
-    """Scale factors (0 or 1/(1-rate)) for rows (b, p in positions) of site ``site``."""
-    b = np.arange(B, dtype=np.uint64)[:, None, None]
+                  rate: float, dtype, b0: int = 0) -> Tensor:
+    """Scale factors (0 or 1/(1-rate)) for rows (b0 + b, p in positions) of site ``site`` (``b0``: the
+    index of this slice's first sample in the full batch, for batches evaluated in slices)."""
+    b = (np.arange(B, dtype=np.uint64) + np.uint64(b0))[:, None, None]
     positions = np.asarray(positions)
     p = (positions.astype(np.uint64)[None, :, None] if positions.ndim == 1      # same for every sample
          else positions.astype(np.uint64)[:, :, None])                          # [B, K] per sample
@@ -58,12 +59,15 @@ def dropout_scale(seed: int, site: int, B: int, I: int, d: int, positions: np.nd
     return torch.from_numpy(keep.astype(np.float64) / (1.0 - rate)).to(dtype)
 
 
+_SAMPLE_OFFSET = [0]        # first-sample index of the slice being evaluated (loss_and_grads_sliced)
+
+
 def apply_dropout(y: Tensor, training: bool, rate: float, seed: int, site: int, I: int,
                   positions: np.ndarray) -> Tensor:
     if not training or rate <= 0.0:
         return y
     B, K, d = y.shape
-    return y * dropout_scale(seed, site, B, I, d, positions, rate, y.dtype)
+    return y * dropout_scale(seed, site, B, I, d, positions, rate, y.dtype, b0=_SAMPLE_OFFSET[0])
 
 
 # ----------------------------------------------------------------------------- tokenizer
@@ -295,12 +299,46 @@ def loss_and_grads(P: Dict[str, Tensor], cfg, ns, seq, labels, training=True, se
     return loss.detach(), grads, out
 
 
+def loss_and_grads_sliced(P: Dict[str, Tensor], cfg, ns, seq, labels, training=True, seed=0, slice_size=256,
+                          variant='vectorized') -> Tuple[Tensor, Dict[str, Tensor], Dict]:
+    """loss_and_grads of the full batch evaluated in slices of ``slice_size`` samples (bounded host
+    memory at BASELINE sizes): every task loss is a mean over the batch, so the batch loss and its
+    gradients are the slice values weighted by slice/B; the dropout mask keeps each sample's global
+    index.  Returns (loss, grads, {'probs', 'logits'} concatenated over slices)."""
+    B = next(iter(labels.values())).shape[0]
+    loss, grads = None, None
+    outs = {'probs': {t: [] for t in cfg.tasks}, 'logits': {t: [] for t in cfg.tasks}}
+    try:
+        for s0 in range(0, B, slice_size):
+            sl = slice(s0, min(B, s0 + slice_size))
+            w = (sl.stop - sl.start) / B
+            _SAMPLE_OFFSET[0] = s0
+            part = lambda d: {k: v[sl] for k, v in d.items()}
+            l_, g_, o_ = loss_and_grads(P, cfg, part(ns), part(seq), part(labels), training, seed, variant)
+            loss = l_ * w if loss is None else loss + l_ * w
+            grads = ({k: g * w for k, g in g_.items()} if grads is None
+                     else {k: grads[k] + g * w for k, g in g_.items()})
+            for key in outs:
+                for t in cfg.tasks:
+                    outs[key][t].append(o_[key][t].detach())
+    finally:
+        _SAMPLE_OFFSET[0] = 0
+    return loss, grads, {key: {t: torch.cat(v) for t, v in d.items()} for key, d in outs.items()}
+
+
 def train_step(P: Dict[str, Tensor], state: Dict[str, Tensor], cfg, keras_vars, ns, seq, labels,
                seed: int = 0, variant: str = 'vectorized'):
     """One OneTransTrainer.train_step (train.py:111-138) with the D5 key mapping
     (gradient_clip_norm, dense_lr): per-variable clip_by_norm -> RMSprop(momentum);
     embedding tables: de-duplicated gradient, clip_by_norm(sparse_clip_norm), Adagrad."""
     loss, grads, out = loss_and_grads(P, cfg, ns, seq, labels, True, seed, variant)
+    newP, state = optimizer_update(P, state, cfg, keras_vars, grads)
+    return newP, state, loss, out
+
+
+def optimizer_update(P: Dict[str, Tensor], state: Dict[str, Tensor], cfg, keras_vars, grads):
+    """train.py:133-138: per-variable clip_by_norm -> RMSprop(momentum) on the dense variables;
+    tables: clip_by_norm(sparse_clip_norm) -> Keras Adagrad (rows with zero gradient unchanged)."""
     oc = cfg.optimizer_config
     lr, mom = oc['dense_lr'], oc['momentum']
     rho, eps = cfg.rmsprop_rho, cfg.rmsprop_epsilon
@@ -333,7 +371,7 @@ def train_step(P: Dict[str, Tensor], state: Dict[str, Tensor], cfg, keras_vars, 
         acc = state[f'acc.{k}'] + g * g
         newP[k] = w - slr * g / torch.sqrt(acc + seps)
         state[f'acc.{k}'] = acc
-    return newP, state, loss, out
+    return newP, state
 
 
 def init_state(P: Dict[str, Tensor], cfg) -> Dict[str, Tensor]:

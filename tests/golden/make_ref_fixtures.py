@@ -21,6 +21,7 @@ Pinned (reference file:line -> build function, checked in tests/test_reference_f
 * DataLoader errors / get_data_info                     data_loader.py:236-297 -> recommend_amd.features
 """
 
+import hashlib
 import importlib.util
 import json
 import os
@@ -142,7 +143,8 @@ def main():
         out[f'ds_ns_{k}'] = np.asarray(v)
     for t, lst in ds.seq_data.items():
         out[f'ds_seqlen_{t}'] = np.array([len(q) for q in lst])
-        out[f'ds_seqcat_{t}'] = np.concatenate(lst)
+        # the events themselves (float64 randn) only as a digest: 1000 samples x 3 sequences is ~10 MB
+        out[f'ds_seqsha_{t}'] = np.array(hashlib.sha256(np.ascontiguousarray(np.concatenate(lst))).hexdigest())
     for t, v in ds.labels.items():
         out[f'ds_lab_{t}'] = np.asarray(v)
     out['ds_len'] = np.array(len(ds))

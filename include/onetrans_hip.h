@@ -140,6 +140,44 @@ int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a_rows, int 
 int ot_transpose_banks(const float* src, float* dst, const int64_t* banks_dev, int nbanks, int64_t total_tiles,
                        void* stream);
 
+/* Pre-split B images for the plane GEMM (split-bf16 mode).  A weight bank used as the B operand
+ * B[g][n][k] = src[g*gstride + n*sn + k*sk] (* kscale[k] when kscale_off >= 0: an RMSNorm gamma folded
+ * into the weights, x*rstd*gamma @ W = rstd * (x @ (gamma W))) is written once per weight update as
+ * its three exact bf16 planes, one 12-KiB block per (g, 128-column tile, 16-k stage) in the LDS image
+ * the GEMM reads.  desc_dev: [ndesc][10] int64 {src_off, sn, sk, gstride, kscale_off, dst_off
+ * (elements of img), first_unit, G, N, K} (offsets into base; K % 16 == 0); a bank owns
+ * G*ceil(N/128)*(K/16) consecutive units of the launch; ot_split_image_elems gives its size. */
+size_t ot_split_image_elems(int G, int N, int K);
+int ot_split_images(const float* base, const int64_t* desc_dev, int ndesc, int64_t total_units, uint16_t* img,
+                    void* stream);
+/* ot_mixed_gemm / ot_mixed_gemm_rms with the B operand's pre-split image (b_image: the bank's image,
+ * image_ntn column tiles per group, the GEMM's columns starting at tile image_tn0).  In split mode,
+ * NT, whole tiles and 16-B aligned A rows the plane GEMM runs (B by global_load_lds from the image,
+ * A split once per tile at fragment time); with a_xform = OT_AX_RMSNORM the image must carry gamma
+ * (kscale) and only a_rstd is read.  Otherwise the call is ot_mixed_gemm / ot_mixed_gemm_rms. */
+int ot_mixed_gemm_img(int mode, const float* A, int64_t lda, int K, const int32_t* in_rows,
+                      int a_xform, const float* a_rstd, const float* a_gamma,
+                      const float* W, int64_t w_gstride, int64_t ldw, int N,
+                      const int32_t* tile_group, int ntiles,
+                      const float* bias, int64_t bias_gstride,
+                      float* C, int64_t ldc, const int32_t* out_rows, int epi,
+                      const float* res, int64_t ldres, int res_tok,
+                      const float* aux, int64_t ldaux,
+                      uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
+                      const int32_t* tail_pos, const uint16_t* b_image, int image_ntn, int image_tn0,
+                      void* stream);
+int ot_mixed_gemm_rms_img(int mode, const float* A, int64_t lda, int K, const int32_t* in_rows,
+                          int a_xform, const float* a_rstd, const float* a_gamma,
+                          const float* W, int64_t w_gstride, int64_t ldw, int N,
+                          const int32_t* tile_group, int ntiles,
+                          const float* bias, int64_t bias_gstride,
+                          float* C, int64_t ldc, const int32_t* out_rows, int epi,
+                          const float* res, int64_t ldres, int res_tok,
+                          const float* aux, int64_t ldaux,
+                          uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
+                          const int32_t* tail_pos, const ot_rms_epilogue* rms, const uint16_t* b_image,
+                          int image_ntn, int image_tn0, void* stream);
+
 /* ---- causal attention with a query tail (attention.hip) ----------------------------------
  * Replaces model.py:100-114 (einsum QK^T/sqrt(hd), band_part mask with -1e9, softmax, einsum PV)
  * and the pyramid gather of queries model.py:356/371 (only the last K of I queries computed).

@@ -78,6 +78,8 @@ struct GemmArgs {
   const float* dres; int64_t lddres; int dres_K, dres_I; const int32_t* dres_inv;
   float* dxm; int64_t lddxm; float* dgpart;
   const int32_t* tail_pos;                      // kept positions (ot_pyramid_select) or null (tail)
+  // plane GEMM: pre-split B image (ot_split_images), its tiles per group and the first tile used
+  const uint16_t* bimg; int bimg_ntn, bimg_tn0;
 };
 
 // sum over the 32 lanes that hold one output row in the vector epilogue (same order as the
@@ -103,6 +105,161 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
   int xcd = b & 7, q = nwg >> 3, r = nwg & 7;
   int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
   return base + (b >> 3);
+}
+
+// ---- vector epilogue shared by the GEMM kernels (compile-time flags EPIT >= 0, no edge tiles): the
+// accumulator tile goes through LDS (the staging buffers are free: the caller's last barrier ended
+// every main-loop read) in two 64-row halves; each thread then finishes 8 rows x one float4 column
+// chunk, so every global access is a 16-B piece of a 512-B row run and each row index is loaded once
+// per row instead of once per element.  Operand loads of a batch of rows are issued together.
+// LAYOUT 0: 2x2 waves, acc[2m + n] = rows 64 (wave >> 1) + 32 m, cols 64 (wave & 1) + 32 n;
+// LAYOUT 1: 4x1 waves, acc[nb] = rows 32 wave, cols 32 nb.  ROWSCALE: multiply row r by
+// a_rstd[in_rows[r]] first (the plane GEMM's RMSNorm prologue, folded into the weights).
+template <int EPIT, int LAYOUT, bool ROWSCALE>
+__device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x16 (&acc)[4], float* smem, int tm,
+                                                  int n0, int g) {
+  const int epi = EPIT;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int h = lane >> 5, li = lane & 31;
+    // ---- vector epilogue: the accumulator tile goes through LDS (the staging buffers are free: the
+    // last main-loop barrier ended every read) in two 64-row halves; each thread then finishes 8
+    // rows x one float4 column chunk, so every global access is a 16-B piece of a 512-B row run and
+    // each row index is loaded once per row instead of once per element.  Operand loads of a batch
+    // of rows are issued together.
+    constexpr int CLD = GT + 4;
+    static_assert(64 * CLD + 8 * GT <= 4 * GT * GLD, "epilogue LDS exceeds the staging buffers");
+    float* ct = smem;                                   // [64][CLD]
+    const int c4 = t & 31, rb = t >> 5;                 // float4 column chunk, first local row
+    const int col = n0 + 4 * c4;
+    f32x4 bias4 = {0.f, 0.f, 0.f, 0.f};
+    if (epi & OT_EPI_BIAS) bias4 = *reinterpret_cast<const f32x4*>(p.bias + (int64_t)g * p.bias_gstride + col);
+    const bool need_tok = (epi & OT_EPI_DROPOUT) || ((epi & OT_EPI_RESIDUAL) && p.res_tok);
+    constexpr bool RMSBWD = EPIT >= 0 && (EPIT & OT_EPI_RMSNORM_BWD);
+    constexpr bool ROWRSTD = EPIT >= 0 && (EPIT & OT_EPI_ROW_RSTD);
+    // dgamma partials live in a thread-private LDS slot behind ct (a register accumulator here
+    // costs the whole kernel ~70 VGPRs of occupancy): dgs[rb][4 c4 .. 4 c4 + 3]
+    float* dgs = ct + 64 * CLD;
+    f32x4 ngam = {0.f, 0.f, 0.f, 0.f};
+    if (RMSBWD) {
+      ngam = *reinterpret_cast<const f32x4*>(p.ngamma + col);
+      *reinterpret_cast<f32x4*>(dgs + rb * GT + 4 * c4) = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    int orow[2][8];
+    float rsc[2][8];
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int lr = rb + 8 * i;                      // local row of the half: tile row below
+        const int64_t gr = (int64_t)tm * GT + (LAYOUT == 0 ? (lr >> 5) * 64 + 32 * hf + (lr & 31) : 64 * hf + lr);
+        orow[hf][i] = p.out_rows ? p.out_rows[gr] : (int)gr;
+        if (ROWSCALE) {                                 // RMSNorm folded into B: scale by the A row's rstd
+          const int ir = p.in_rows ? p.in_rows[gr] : (int)gr;
+          rsc[hf][i] = ir >= 0 ? p.a_rstd[ir] : 0.f;
+        }
+      }
+    constexpr int RB = RMSBWD ? 4 : 8;                  // rows per operand-load batch (register budget)
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      if (LAYOUT == 0) {
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            ct[((wave >> 1) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * CLD + (wave & 1) * 64 + 32 * n + li] = acc[2 * hf + n][r];
+      } else if ((wave >> 1) == hf) {
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            ct[((wave & 1) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * CLD + 32 * nb + li] = acc[nb][r];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int i0 = 0; i0 < 8; i0 += RB) {
+        int64_t tok[RB];
+        f32x4 aux4[RB], res4[RB], cp4[RB], x4[RB], dr4[RB];
+        float nr[RB];
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+          const int orr = orow[hf][i0 + i];
+          const int64_t o = orr < 0 ? 0 : orr;
+          tok[i] = (need_tok && orr >= 0) ? tail_token(orr, p.tail_K, p.tail_I, p.tail_pos) : o;
+          if (RMSBWD) {
+            x4[i] = *reinterpret_cast<const f32x4*>(p.nx + o * p.ldnx + col);
+            nr[i] = p.nrstd[o];
+            dr4[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (p.dres) {
+              const int64_t dr = p.dres_K > 0 ? kept_row(o, p.dres_K, p.dres_I, p.dres_inv) : o;
+              if (dr >= 0) dr4[i] = *reinterpret_cast<const f32x4*>(p.dres + (int64_t)dr * p.lddres + col);
+            }
+          }
+          if (epi & OT_EPI_GELU_BWD) aux4[i] = *reinterpret_cast<const f32x4*>(p.aux + o * p.ldaux + col);
+          if (epi & OT_EPI_RESIDUAL)
+            res4[i] = *reinterpret_cast<const f32x4*>(p.res + (p.res_tok ? tok[i] : o) * p.ldres + col);
+          if (epi & OT_EPI_ACCUMULATE) cp4[i] = *reinterpret_cast<const f32x4*>(p.C + o * p.ldc + col);
+        }
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+          const int orr = orow[hf][i0 + i];
+          f32x4 v = *reinterpret_cast<const f32x4*>(ct + (rb + 8 * (i0 + i)) * CLD + 4 * c4);
+          if (ROWSCALE) v = v * rsc[hf][i0 + i];
+          if (epi & OT_EPI_BIAS) v += bias4;
+          if (epi & OT_EPI_GELU_BWD) {
+            v.x *= gelu_erf_grad(aux4[i].x); v.y *= gelu_erf_grad(aux4[i].y);
+            v.z *= gelu_erf_grad(aux4[i].z); v.w *= gelu_erf_grad(aux4[i].w);
+          }
+          if (epi & OT_EPI_GELU) {
+            v.x = gelu_erf(v.x); v.y = gelu_erf(v.y); v.z = gelu_erf(v.z); v.w = gelu_erf(v.w);
+          }
+          if (RMSBWD) {
+            // v = dL/dy of y = x * rstd * gamma:  dx = rstd * (g - x * rstd^2 * <g, x> / N) + dres
+            const f32x4 gv = v * ngam;
+            const float r = nr[i];
+            float sdot = gv.x * x4[i].x + gv.y * x4[i].y + gv.z * x4[i].z + gv.w * x4[i].w;
+            sdot = row32_sum(sdot);
+            const float coef = r * r * r * sdot / (float)p.N;
+            if (orr >= 0) {
+              f32x4* q = reinterpret_cast<f32x4*>(dgs + rb * GT + 4 * c4);
+              *q = *q + v * x4[i] * r;
+            }
+            v = gv * r - x4[i] * coef + dr4[i];
+            if (orr >= 0) *reinterpret_cast<f32x4*>(p.C + (int64_t)orr * p.ldc + col) = v;
+            if ((epi & OT_EPI_DROPOUT) && orr >= 0) {          // mask(dx) for the dropout site upstream
+              const uint32_t idx = (uint32_t)(tok[i] * p.drop_width + col);
+              f32x4 mv;
+              mv.x = drop_keep(p.seed, p.site, idx + 0, p.drop_thr) ? v.x * p.drop_scale : 0.f;
+              mv.y = drop_keep(p.seed, p.site, idx + 1, p.drop_thr) ? v.y * p.drop_scale : 0.f;
+              mv.z = drop_keep(p.seed, p.site, idx + 2, p.drop_thr) ? v.z * p.drop_scale : 0.f;
+              mv.w = drop_keep(p.seed, p.site, idx + 3, p.drop_thr) ? v.w * p.drop_scale : 0.f;
+              *reinterpret_cast<f32x4*>(p.dxm + (int64_t)orr * p.lddxm + col) = mv;
+            }
+            continue;
+          }
+          if (epi & OT_EPI_DROPOUT) {
+            const uint32_t idx = (uint32_t)(tok[i] * p.drop_width + col);
+            v.x = drop_keep(p.seed, p.site, idx + 0, p.drop_thr) ? v.x * p.drop_scale : 0.f;
+            v.y = drop_keep(p.seed, p.site, idx + 1, p.drop_thr) ? v.y * p.drop_scale : 0.f;
+            v.z = drop_keep(p.seed, p.site, idx + 2, p.drop_thr) ? v.z * p.drop_scale : 0.f;
+            v.w = drop_keep(p.seed, p.site, idx + 3, p.drop_thr) ? v.w * p.drop_scale : 0.f;
+          }
+          if (epi & OT_EPI_RESIDUAL) v += res4[i];
+          if (epi & OT_EPI_ACCUMULATE) v += cp4[i];
+          if (ROWRSTD) {                                       // rstd of the finished row (next RMSNorm)
+            const float ss = row32_sum(v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w);
+            if (orr >= 0 && c4 == 0) p.rstd_out[orr] = rsqrtf(ss / (float)p.N + p.eps);
+          }
+          if (orr >= 0) *reinterpret_cast<f32x4*>(p.C + (int64_t)orr * p.ldc + col) = v;
+        }
+      }
+      __syncthreads();                                  // ct is rewritten by the next half
+    }
+    if (RMSBWD && t < GT) {                             // dgamma partial of this tile (fixed order)
+      float a = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) a += dgs[k * GT + t];
+      p.dgpart[(int64_t)tm * GT + t] = a;
+    }
 }
 
 // AXT / EPIT: compile-time prologue / epilogue (-1 = read p.a_xform / p.epi at run time).
@@ -388,131 +545,8 @@ __global__ __launch_bounds__(256, (NT && SPLT) ? 2 : OT_GEMM_MINWG) void mixed_g
   // rows of this lane, issue every operand load (aux / residual / accumulate source) for the block,
   // then compute and store — no load-use chains per element.
   if constexpr (!EDGE && EPIT >= 0) {
-    // ---- vector epilogue: the accumulator tile goes through LDS (the staging buffers are free: the
-    // last main-loop barrier ended every read) in two 64-row halves; each thread then finishes 8
-    // rows x one float4 column chunk, so every global access is a 16-B piece of a 512-B row run and
-    // each row index is loaded once per row instead of once per element.  Operand loads of a batch
-    // of rows are issued together.
-    constexpr int CLD = GT + 4;
-    static_assert(64 * CLD + 8 * GT <= 4 * GT * GLD, "epilogue LDS exceeds the staging buffers");
-    float* ct = smem;                                   // [64][CLD]
-    const int c4 = t & 31, rb = t >> 5;                 // float4 column chunk, first local row
-    const int col = n0 + 4 * c4;
-    f32x4 bias4 = {0.f, 0.f, 0.f, 0.f};
-    if (epi & OT_EPI_BIAS) bias4 = *reinterpret_cast<const f32x4*>(p.bias + (int64_t)g * p.bias_gstride + col);
-    const bool need_tok = (epi & OT_EPI_DROPOUT) || ((epi & OT_EPI_RESIDUAL) && p.res_tok);
-    constexpr bool RMSBWD = EPIT >= 0 && (EPIT & OT_EPI_RMSNORM_BWD);
-    constexpr bool ROWRSTD = EPIT >= 0 && (EPIT & OT_EPI_ROW_RSTD);
-    // dgamma partials live in a thread-private LDS slot behind ct (a register accumulator here
-    // costs the whole kernel ~70 VGPRs of occupancy): dgs[rb][4 c4 .. 4 c4 + 3]
-    float* dgs = ct + 64 * CLD;
-    f32x4 ngam = {0.f, 0.f, 0.f, 0.f};
-    if (RMSBWD) {
-      ngam = *reinterpret_cast<const f32x4*>(p.ngamma + col);
-      *reinterpret_cast<f32x4*>(dgs + rb * GT + 4 * c4) = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    int orow[2][8];
-#pragma unroll
-    for (int hf = 0; hf < 2; ++hf)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int lr = rb + 8 * i;                      // local row of the half: tile row below
-        const int64_t gr = (int64_t)tm * GT + (lr >> 5) * 64 + 32 * hf + (lr & 31);
-        orow[hf][i] = p.out_rows ? p.out_rows[gr] : (int)gr;
-      }
-    constexpr int RB = RMSBWD ? 4 : 8;                  // rows per operand-load batch (register budget)
-#pragma unroll
-    for (int hf = 0; hf < 2; ++hf) {
-#pragma unroll
-      for (int n = 0; n < 2; ++n)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          ct[((wave >> 1) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * CLD + wn + 32 * n + li] = acc[hf][n][r];
-      __syncthreads();
-#pragma unroll
-      for (int i0 = 0; i0 < 8; i0 += RB) {
-        int64_t tok[RB];
-        f32x4 aux4[RB], res4[RB], cp4[RB], x4[RB], dr4[RB];
-        float nr[RB];
-#pragma unroll
-        for (int i = 0; i < RB; ++i) {
-          const int orr = orow[hf][i0 + i];
-          const int64_t o = orr < 0 ? 0 : orr;
-          tok[i] = (need_tok && orr >= 0) ? tail_token(orr, p.tail_K, p.tail_I, p.tail_pos) : o;
-          if (RMSBWD) {
-            x4[i] = *reinterpret_cast<const f32x4*>(p.nx + o * p.ldnx + col);
-            nr[i] = p.nrstd[o];
-            dr4[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (p.dres) {
-              const int64_t dr = p.dres_K > 0 ? kept_row(o, p.dres_K, p.dres_I, p.dres_inv) : o;
-              if (dr >= 0) dr4[i] = *reinterpret_cast<const f32x4*>(p.dres + (int64_t)dr * p.lddres + col);
-            }
-          }
-          if (epi & OT_EPI_GELU_BWD) aux4[i] = *reinterpret_cast<const f32x4*>(p.aux + o * p.ldaux + col);
-          if (epi & OT_EPI_RESIDUAL)
-            res4[i] = *reinterpret_cast<const f32x4*>(p.res + (p.res_tok ? tok[i] : o) * p.ldres + col);
-          if (epi & OT_EPI_ACCUMULATE) cp4[i] = *reinterpret_cast<const f32x4*>(p.C + o * p.ldc + col);
-        }
-#pragma unroll
-        for (int i = 0; i < RB; ++i) {
-          const int orr = orow[hf][i0 + i];
-          f32x4 v = *reinterpret_cast<const f32x4*>(ct + (rb + 8 * (i0 + i)) * CLD + 4 * c4);
-          if (epi & OT_EPI_BIAS) v += bias4;
-          if (epi & OT_EPI_GELU_BWD) {
-            v.x *= gelu_erf_grad(aux4[i].x); v.y *= gelu_erf_grad(aux4[i].y);
-            v.z *= gelu_erf_grad(aux4[i].z); v.w *= gelu_erf_grad(aux4[i].w);
-          }
-          if (epi & OT_EPI_GELU) {
-            v.x = gelu_erf(v.x); v.y = gelu_erf(v.y); v.z = gelu_erf(v.z); v.w = gelu_erf(v.w);
-          }
-          if (RMSBWD) {
-            // v = dL/dy of y = x * rstd * gamma:  dx = rstd * (g - x * rstd^2 * <g, x> / N) + dres
-            const f32x4 gv = v * ngam;
-            const float r = nr[i];
-            float sdot = gv.x * x4[i].x + gv.y * x4[i].y + gv.z * x4[i].z + gv.w * x4[i].w;
-            sdot = row32_sum(sdot);
-            const float coef = r * r * r * sdot / (float)p.N;
-            if (orr >= 0) {
-              f32x4* q = reinterpret_cast<f32x4*>(dgs + rb * GT + 4 * c4);
-              *q = *q + v * x4[i] * r;
-            }
-            v = gv * r - x4[i] * coef + dr4[i];
-            if (orr >= 0) *reinterpret_cast<f32x4*>(p.C + (int64_t)orr * p.ldc + col) = v;
-            if ((epi & OT_EPI_DROPOUT) && orr >= 0) {          // mask(dx) for the dropout site upstream
-              const uint32_t idx = (uint32_t)(tok[i] * p.drop_width + col);
-              f32x4 mv;
-              mv.x = drop_keep(p.seed, p.site, idx + 0, p.drop_thr) ? v.x * p.drop_scale : 0.f;
-              mv.y = drop_keep(p.seed, p.site, idx + 1, p.drop_thr) ? v.y * p.drop_scale : 0.f;
-              mv.z = drop_keep(p.seed, p.site, idx + 2, p.drop_thr) ? v.z * p.drop_scale : 0.f;
-              mv.w = drop_keep(p.seed, p.site, idx + 3, p.drop_thr) ? v.w * p.drop_scale : 0.f;
-              *reinterpret_cast<f32x4*>(p.dxm + (int64_t)orr * p.lddxm + col) = mv;
-            }
-            continue;
-          }
-          if (epi & OT_EPI_DROPOUT) {
-            const uint32_t idx = (uint32_t)(tok[i] * p.drop_width + col);
-            v.x = drop_keep(p.seed, p.site, idx + 0, p.drop_thr) ? v.x * p.drop_scale : 0.f;
-            v.y = drop_keep(p.seed, p.site, idx + 1, p.drop_thr) ? v.y * p.drop_scale : 0.f;
-            v.z = drop_keep(p.seed, p.site, idx + 2, p.drop_thr) ? v.z * p.drop_scale : 0.f;
-            v.w = drop_keep(p.seed, p.site, idx + 3, p.drop_thr) ? v.w * p.drop_scale : 0.f;
-          }
-          if (epi & OT_EPI_RESIDUAL) v += res4[i];
-          if (epi & OT_EPI_ACCUMULATE) v += cp4[i];
-          if (ROWRSTD) {                                       // rstd of the finished row (next RMSNorm)
-            const float ss = row32_sum(v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w);
-            if (orr >= 0 && c4 == 0) p.rstd_out[orr] = rsqrtf(ss / (float)p.N + p.eps);
-          }
-          if (orr >= 0) *reinterpret_cast<f32x4*>(p.C + (int64_t)orr * p.ldc + col) = v;
-        }
-      }
-      __syncthreads();                                  // ct is rewritten by the next half
-    }
-    if (RMSBWD && t < GT) {                             // dgamma partial of this tile (fixed order)
-      float a = 0.f;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) a += dgs[k * GT + t];
-      p.dgpart[(int64_t)tm * GT + t] = a;
-    }
+    const f32x16 acc4[4] = {acc[0][0], acc[0][1], acc[1][0], acc[1][1]};
+    gemm_vec_epilogue<EPIT, 0, false>(p, acc4, smem, tm, n0, g);
     return;
   }
   // ---- scalar epilogue (EDGE: N % 128 != 0 or unaligned operands; generic run-time flags)
@@ -577,6 +611,153 @@ __global__ __launch_bounds__(256, (NT && SPLT) ? 2 : OT_GEMM_MINWG) void mixed_g
       }
     }
   }
+}
+
+// ------------------------------------------------------------------------------------------
+// Plane GEMM (split-bf16, NT): the B operand (a weight bank) arrives pre-split — ot_split_images
+// writes, once per optimizer step, every 128-column x 16-k block of B as its three bf16 planes in
+// the exact LDS image the MFMA fragments read ([plane][128 n][2 halves of 8 k], the halves of rows
+// with bit 3 of n set swapped: conflict-free ds_read_b128) — and the A operand (activations, f32)
+// is copied global -> LDS unchanged.  Both move by global_load_lds_dwordx4 (no VGPR staging, no
+// LDS store instructions), three stages deep, one raw barrier per 16-k stage with a counted
+// vmcnt.  Waves are 4x1: wave w owns rows 32w..32w+31 x all 128 columns, so each A element is
+// read and split into its planes exactly once per tile, right before its MFMAs (the A image rows
+// are 64 B with the 16-B chunk swizzle c ^ ((r >> 2) & 3): conflict-free ds_read_b128).  An
+// RMSNorm prologue is folded into B (gamma scales B's k rows when the image is built) and its row
+// factor rstd is applied in the epilogue; a GELU prologue runs on the fragment before the split.
+constexpr int PG_NSTG = 3;                         // LDS stages
+constexpr int PG_A_BYTES = GT * 16 * 4;            // A stage image: 128 rows x 16 f32
+constexpr int PG_B_BYTES = 3 * GT * 16 * 2;        // B stage image: 3 planes x 128 n x 16 bf16
+constexpr int PG_STG_BYTES = PG_A_BYTES + PG_B_BYTES;
+constexpr int PG_SHMEM = PG_NSTG * PG_STG_BYTES;   // 60 KiB (the epilogue reuses the first 38 KiB)
+static_assert(64 * (GT + 4) * 4 + 8 * GT * 4 <= PG_SHMEM, "plane GEMM epilogue LDS");
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+template <int AXT, int EPIT>
+__global__ __launch_bounds__(256, 2) void plane_gemm_kernel(GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  char* lds = reinterpret_cast<char*>(smem);
+  const int nwg = p.ntm * p.ntn;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int tm = wg / p.ntn, tn = wg % p.ntn;
+  const int g = p.tile_group ? p.tile_group[tm] : 0;
+  const int n0 = tn * GT;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int h = lane >> 5, li = lane & 31;
+  const int nk = p.K >> 4;
+
+  // glds sources.  A: wave w's instruction i fills LDS bytes [(2w+i) KiB, +1 KiB) of the A image =
+  // rows 16(2w+i) .. +15, lane j -> row + j/4, physical chunk j%4 = logical chunk (j%4) ^ swizzle.
+  // Rows of the tile past the row map (in_rows < 0) read row 0: their outputs are never stored.
+  const float* asrc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = (2 * wave + i) * 16 + (lane >> 2);
+    const int64_t gr = (int64_t)tm * GT + r;
+    int ir = p.in_rows ? p.in_rows[gr] : (int)gr;
+    ir = ir < 0 ? 0 : ir;
+    const int lc = (lane & 3) ^ ((r >> 2) & 3);
+    asrc[i] = p.A + (int64_t)ir * p.lda + 4 * lc;
+  }
+  // B: the (g, tile) image is nk consecutive 12-KiB stage blocks; wave w copies KiB 3w .. 3w+2 (a
+  // weight shared by every group, w_gstride 0 like Wo, has one group's image)
+  const int gb = p.w_gstride ? g : 0;
+  const char* bsrc = reinterpret_cast<const char*>(p.bimg) +
+                     ((int64_t)gb * p.bimg_ntn + p.bimg_tn0 + tn) * nk * PG_B_BYTES + (3 * wave) * 1024 + 16 * lane;
+
+  auto issue = [&](int ks, int buf) {
+    char* sb = lds + buf * PG_STG_BYTES;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + 16 * ks), (lds_void_t*)(sb + (2 * wave + i) * 1024),
+                                       16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(bsrc + (int64_t)ks * PG_B_BYTES + i * 1024),
+                                       (lds_void_t*)(sb + PG_A_BYTES + (3 * wave + i) * 1024), 16, 0, 0);
+  };
+
+  f32x16 acc[4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[a][r] = 0.f;
+
+  const int ra = 32 * wave + li;                      // this lane's A row (fragment row li)
+  const int aoff0 = ra * 64 + 16 * ((2 * h) ^ ((li >> 2) & 3));
+  const int aoff1 = ra * 64 + 16 * ((2 * h + 1) ^ ((li >> 2) & 3));
+  const int boff = PG_A_BYTES + li * 32 + 16 * (h ^ ((li >> 3) & 1));
+
+  issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  for (int kt = 0; kt < nk; ++kt) {
+    // this wave's copies of stage kt are done (the 5 of stage kt+1 may still fly), every wave's
+    // after the barrier; the barrier also retires every read of stage kt-1's buffer, which the
+    // copies of stage kt+2 overwrite
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + 2 < nk) issue(kt + 2, (kt + 2) % PG_NSTG);
+    const char* sb = lds + (kt % PG_NSTG) * PG_STG_BYTES;
+    f32x4 a0 = *reinterpret_cast<const f32x4*>(sb + aoff0);
+    f32x4 a1 = *reinterpret_cast<const f32x4*>(sb + aoff1);
+    u32x4 fb[4][3];
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) fb[nb][q] = *reinterpret_cast<const u32x4*>(sb + boff + q * 4096 + nb * 1024);
+    if (AXT == OT_AX_GELU) {
+      a0.x = gelu_erf(a0.x); a0.y = gelu_erf(a0.y); a0.z = gelu_erf(a0.z); a0.w = gelu_erf(a0.w);
+      a1.x = gelu_erf(a1.x); a1.y = gelu_erf(a1.y); a1.z = gelu_erf(a1.z); a1.w = gelu_erf(a1.w);
+    }
+    const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    u32x4 fa[3];
+    split8(av, fa);
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) acc[nb] = mfma_split6(fa, fb[nb], acc[nb]);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();                                    // the epilogue reuses the stage buffers
+  gemm_vec_epilogue<EPIT, 1, AXT == OT_AX_RMSNORM>(p, acc, smem, tm, n0, g);
+}
+
+// Pre-split B images (ot_split_images).  desc [nd][10] int64: {src_off, sn, sk, gstride, kscale_off
+// (-1: none), dst_off (ushorts), first_unit, G, N, K}; B[g][n][k] = src[g*gstride + n*sn + k*sk]
+// (* kscale[k]); one unit = one (g, n tile, 16-k stage) block of 3 x 128 x 16 bf16, one thread per
+// (row n, 8-k half): split8 of the 8 values, each plane's 16 B at its swizzled half.
+__global__ __launch_bounds__(256) void split_images_kernel(const float* __restrict__ base, const int64_t* __restrict__ desc,
+                                                           int nd, uint16_t* img) {
+  const int64_t unit = blockIdx.x;
+  int b = 0;
+  while (b + 1 < nd && desc[10 * (b + 1) + 6] <= unit) ++b;
+  const int64_t* d = desc + 10 * b;
+  const int64_t G = d[7], N = d[8], K = d[9];
+  const int64_t ntn = (N + GT - 1) / GT, nks = K / 16;
+  int64_t u = unit - d[6];
+  if (u >= G * ntn * nks) return;
+  const int64_t g = u / (ntn * nks);
+  u %= ntn * nks;
+  const int64_t tn = u / nks, ks = u % nks;
+  const int n = threadIdx.x >> 1, hh = threadIdx.x & 1;
+  const int64_t gn = tn * GT + n;
+  const float* src = base + d[0] + g * d[3] + gn * d[1];
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int64_t k = ks * 16 + 8 * hh + j;
+    float x = gn < N ? src[k * d[2]] : 0.f;
+    if (d[4] >= 0) x *= base[d[4] + k];
+    v[j] = x;
+  }
+  u32x4 pl[3];
+  split8(v, pl);
+  uint16_t* dst = img + d[5] + (unit - d[6]) * (PG_B_BYTES / 2);
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+    *reinterpret_cast<u32x4*>(dst + q * GT * 16 + n * 16 + 8 * (hh ^ ((n >> 3) & 1))) = pl[q];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1061,7 +1242,8 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
                            const float* aux, int64_t ldaux,
                            uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
                            const int32_t* tail_pos,
-                           const ot_rms_epilogue* rms, void* stream) {
+                           const ot_rms_epilogue* rms, const uint16_t* bimg, int bimg_ntn, int bimg_tn0,
+                           void* stream) {
   OT_REQUIRE(A && W && C, "ot_mixed_gemm: null operand");
   const int rms_flags = epi & (OT_EPI_ROW_RSTD | OT_EPI_RMSNORM_BWD);
   OT_REQUIRE(!rms_flags || rms, "ot_mixed_gemm: row-norm epilogue flags need ot_mixed_gemm_rms");
@@ -1093,6 +1275,7 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
              bias, bias_gstride, C, ldc, out_rows, epi, res, ldres, res_tok, aux, ldaux,
              seed, site, 0u, 1.f, tail_K, tail_I, N, ntiles, (int)ceil_div(N, GT)};
   p.tail_pos = tail_pos;
+  p.bimg = bimg; p.bimg_ntn = bimg_ntn; p.bimg_tn0 = bimg_tn0;
   float* dgpart = nullptr;
   if (rms_flags) {
     p.rstd_out = rms->rstd_out; p.eps = rms->eps;
@@ -1124,6 +1307,7 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
   const unsigned nwg = (unsigned)ntiles * p.ntn;
   hipStream_t s = (hipStream_t)stream;
   void (*kern)(GemmArgs) = nullptr;
+  bool plane = false;
   const int e = epi, x = a_xform;
 #define OT_SPEC(NT_, AX_, EP_)                                                                  \
   if (mode == (NT_ ? OT_GEMM_NT : OT_GEMM_NN) && x == AX_ && e == (EP_))                         \
@@ -1148,6 +1332,33 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
   OT_SPEC(true, OT_AX_NONE, OT_EPI_RMSNORM_BWD)
   OT_SPEC(true, OT_AX_NONE, OT_EPI_RMSNORM_BWD | OT_EPI_DROPOUT)
 #undef OT_SPEC
+  // plane GEMM: split mode, pre-split B image given, whole tiles, 16-B aligned A rows
+  if (bimg && split && !one && !edge && mode == OT_GEMM_NT && lda % 4 == 0 && a16(A)) {
+    OT_REQUIRE(bimg_ntn >= bimg_tn0 + (int)p.ntn && bimg_tn0 >= 0, "ot_mixed_gemm: B image has %d tiles per group, "
+               "the GEMM needs %d from tile %d", bimg_ntn, (int)p.ntn, bimg_tn0);
+    void (*pk)(GemmArgs) = nullptr;
+#define OT_PSPEC(AX_, EP_) \
+    if (x == AX_ && e == (EP_)) pk = plane_gemm_kernel<AX_, EP_>;
+    OT_PSPEC(OT_AX_RMSNORM, 0)
+    OT_PSPEC(OT_AX_RMSNORM, OT_EPI_BIAS)
+    OT_PSPEC(OT_AX_GELU, OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_DROPOUT)
+    OT_PSPEC(OT_AX_GELU, OT_EPI_BIAS | OT_EPI_RESIDUAL)
+    OT_PSPEC(OT_AX_GELU, OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_DROPOUT | OT_EPI_ROW_RSTD)
+    OT_PSPEC(OT_AX_GELU, OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_ROW_RSTD)
+    OT_PSPEC(OT_AX_NONE, OT_EPI_RESIDUAL | OT_EPI_DROPOUT)
+    OT_PSPEC(OT_AX_NONE, OT_EPI_RESIDUAL)
+    OT_PSPEC(OT_AX_NONE, OT_EPI_BIAS)
+    OT_PSPEC(OT_AX_NONE, OT_EPI_GELU_BWD)
+    OT_PSPEC(OT_AX_NONE, 0)
+    OT_PSPEC(OT_AX_NONE, OT_EPI_ACCUMULATE)
+    OT_PSPEC(OT_AX_NONE, OT_EPI_RESIDUAL | OT_EPI_DROPOUT | OT_EPI_ROW_RSTD)
+    OT_PSPEC(OT_AX_NONE, OT_EPI_RESIDUAL | OT_EPI_ROW_RSTD)
+    OT_PSPEC(OT_AX_NONE, OT_EPI_RMSNORM_BWD)
+    OT_PSPEC(OT_AX_NONE, OT_EPI_RMSNORM_BWD | OT_EPI_DROPOUT)
+#undef OT_PSPEC
+    if (pk) { kern = pk; plane = true; }
+  }
+  const size_t launch_shmem = plane ? (size_t)PG_SHMEM : shmem;
   OT_REQUIRE(kern || !rms_flags, "ot_mixed_gemm_rms: no specialised kernel for epilogue flags %d", epi);
   if (!kern) {   // any other combination: generic instantiation (run-time prologue/epilogue)
     if (mode == OT_GEMM_NT && split && one)
@@ -1170,7 +1381,7 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
       (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     (void)hipGetLastError();
   });
-  hipLaunchKernelGGL(kern, dim3(nwg), dim3(256), shmem, s, p);
+  hipLaunchKernelGGL(kern, dim3(nwg), dim3(256), launch_shmem, s, p);
   OT_LAUNCH_CHECK("ot_mixed_gemm");
   if (dgpart) {
     launch_colsum_reduce(dgpart, ntiles, N, rms->dgamma, rms->accumulate_dgamma, s, dgpart + (int64_t)ntiles * N);
@@ -1191,7 +1402,38 @@ extern "C" int ot_mixed_gemm(int mode, const float* A, int64_t lda, int K, const
                              const int32_t* tail_pos, void* stream) {
   return mixed_gemm_impl(mode, A, lda, K, in_rows, a_xform, a_rstd, a_gamma, W, w_gstride, ldw, N, tile_group,
                          ntiles, bias, bias_gstride, C, ldc, out_rows, epi, res, ldres, res_tok, aux, ldaux, seed,
-                         site, drop_rate, tail_K, tail_I, tail_pos, nullptr, stream);
+                         site, drop_rate, tail_K, tail_I, tail_pos, nullptr, nullptr, 0, 0, stream);
+}
+
+extern "C" int ot_mixed_gemm_img(int mode, const float* A, int64_t lda, int K, const int32_t* in_rows,
+                                 int a_xform, const float* a_rstd, const float* a_gamma,
+                                 const float* W, int64_t w_gstride, int64_t ldw, int N,
+                                 const int32_t* tile_group, int ntiles,
+                                 const float* bias, int64_t bias_gstride,
+                                 float* C, int64_t ldc, const int32_t* out_rows, int epi,
+                                 const float* res, int64_t ldres, int res_tok,
+                                 const float* aux, int64_t ldaux,
+                                 uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
+                                 const int32_t* tail_pos, const uint16_t* b_image, int image_ntn, int image_tn0,
+                                 void* stream) {
+  return mixed_gemm_impl(mode, A, lda, K, in_rows, a_xform, a_rstd, a_gamma, W, w_gstride, ldw, N, tile_group,
+                         ntiles, bias, bias_gstride, C, ldc, out_rows, epi, res, ldres, res_tok, aux, ldaux, seed,
+                         site, drop_rate, tail_K, tail_I, tail_pos, nullptr, b_image, image_ntn, image_tn0, stream);
+}
+
+extern "C" size_t ot_split_image_elems(int G, int N, int K) {
+  if (G <= 0 || N <= 0 || K <= 0 || K % 16) return 0;
+  return (size_t)G * ceil_div(N, GT) * (K / 16) * (PG_B_BYTES / 2);
+}
+
+extern "C" int ot_split_images(const float* base, const int64_t* desc_dev, int ndesc, int64_t total_units,
+                               uint16_t* img, void* stream) {
+  OT_REQUIRE(base && desc_dev && img && ndesc > 0 && total_units >= 0, "ot_split_images: bad args");
+  if (total_units == 0) return OT_OK;
+  hipLaunchKernelGGL(split_images_kernel, dim3((unsigned)total_units), dim3(256), 0, (hipStream_t)stream, base,
+                     desc_dev, ndesc, img);
+  OT_LAUNCH_CHECK("ot_split_images");
+  return OT_OK;
 }
 
 extern "C" size_t ot_mixed_gemm_rms_workspace_size(int ntiles, int N) {
@@ -1212,7 +1454,24 @@ extern "C" int ot_mixed_gemm_rms(int mode, const float* A, int64_t lda, int K, c
   OT_REQUIRE(rms, "ot_mixed_gemm_rms: null epilogue operands");
   return mixed_gemm_impl(mode, A, lda, K, in_rows, a_xform, a_rstd, a_gamma, W, w_gstride, ldw, N, tile_group,
                          ntiles, bias, bias_gstride, C, ldc, out_rows, epi, res, ldres, res_tok, aux, ldaux, seed,
-                         site, drop_rate, tail_K, tail_I, tail_pos, rms, stream);
+                         site, drop_rate, tail_K, tail_I, tail_pos, rms, nullptr, 0, 0, stream);
+}
+
+extern "C" int ot_mixed_gemm_rms_img(int mode, const float* A, int64_t lda, int K, const int32_t* in_rows,
+                                     int a_xform, const float* a_rstd, const float* a_gamma,
+                                     const float* W, int64_t w_gstride, int64_t ldw, int N,
+                                     const int32_t* tile_group, int ntiles,
+                                     const float* bias, int64_t bias_gstride,
+                                     float* C, int64_t ldc, const int32_t* out_rows, int epi,
+                                     const float* res, int64_t ldres, int res_tok,
+                                     const float* aux, int64_t ldaux,
+                                     uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
+                                     const int32_t* tail_pos, const ot_rms_epilogue* rms, const uint16_t* b_image,
+                                     int image_ntn, int image_tn0, void* stream) {
+  OT_REQUIRE(rms, "ot_mixed_gemm_rms: null epilogue operands");
+  return mixed_gemm_impl(mode, A, lda, K, in_rows, a_xform, a_rstd, a_gamma, W, w_gstride, ldw, N, tile_group,
+                         ntiles, bias, bias_gstride, C, ldc, out_rows, epi, res, ldres, res_tok, aux, ldaux, seed,
+                         site, drop_rate, tail_K, tail_I, tail_pos, rms, b_image, image_ntn, image_tn0, stream);
 }
 
 extern "C" size_t ot_wgrad_workspace_size(int nchunks, int K, int N) {

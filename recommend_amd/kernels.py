@@ -123,12 +123,17 @@ def gemm(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish, w_g
          rstd: Ptrish = None, gamma: Ptrish = None, bias: Ptrish = None, bias_gstride: int = 0, epi: int = 0,
          res: Ptrish = None, ldres: int = 0, res_tok: int = 0, aux: Ptrish = None, ldaux: int = 0,
          seed: int = 0, site: int = 0, drop: float = 0.0, tail: Tuple[int, int] = (1, 1),
-         m_rows: int = 0) -> None:
+         m_rows: int = 0, bimg=None) -> None:
+    """ot_mixed_gemm; ``bimg`` = (image, tiles per group, first tile) of B's pre-split image
+    (ot_mixed_gemm_img: the plane GEMM in split mode)."""
     ev = _probe.begin() if _probe is not None else None
-    call('ot_mixed_gemm', mode, ptr(A), lda, K, ptr(in_rows), a_xform, ptr(rstd), ptr(gamma), ptr(W), w_gstride,
-         ldw, N, ptr(tile_group), ntiles, ptr(bias), bias_gstride, ptr(C), ldc, ptr(out_rows), epi, ptr(res),
-         ldres, res_tok, ptr(aux), ldaux, seed & 0xFFFFFFFF, site, float(drop), tail[0], tail[1], _sel(tail),
-         stream())
+    args = (mode, ptr(A), lda, K, ptr(in_rows), a_xform, ptr(rstd), ptr(gamma), ptr(W), w_gstride,
+            ldw, N, ptr(tile_group), ntiles, ptr(bias), bias_gstride, ptr(C), ldc, ptr(out_rows), epi, ptr(res),
+            ldres, res_tok, ptr(aux), ldaux, seed & 0xFFFFFFFF, site, float(drop), tail[0], tail[1], _sel(tail))
+    if bimg is not None:
+        call('ot_mixed_gemm_img', *args, ptr(bimg[0]), bimg[1], bimg[2], stream())
+    else:
+        call('ot_mixed_gemm', *args, stream())
     if ev is not None:
         _probe.end('mixed_gemm', 2.0 * (m_rows or ntiles * 128) * K * N, ev,
                    f'gemm mode{mode} ax{a_xform} epi{epi} M{m_rows or ntiles * 128} K{K} N{N}')
@@ -142,7 +147,7 @@ def gemm_rms(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish,
              rstd_out: Ptrish = None, eps: float = 1e-6, nx: Ptrish = None, ldnx: int = 0,
              ngamma: Ptrish = None, nrstd: Ptrish = None, dres: Ptrish = None, lddres: int = 0,
              dres_tail: Tuple[int, int] = (0, 0), dx_masked: Ptrish = None, lddxm: int = 0,
-             dgamma: Ptrish = None, accumulate_dgamma: bool = False, device=None) -> None:
+             dgamma: Ptrish = None, accumulate_dgamma: bool = False, device=None, bimg=None) -> None:
     """ot_mixed_gemm_rms: the GEMM with a row-norm epilogue (OT_EPI_ROW_RSTD: emit the next RMSNorm's
     rstd; OT_EPI_RMSNORM_BWD: apply the RMSNorm backward to the product, + dres, dgamma)."""
     ws = workspace(size('ot_mixed_gemm_rms_workspace_size', ntiles, N) if dgamma is not None else 16,
@@ -151,10 +156,14 @@ def gemm_rms(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish,
                          dres_tail[0], dres_tail[1], _sel(dres_tail), ptr(dx_masked), lddxm, ptr(dgamma),
                          int(accumulate_dgamma), ptr(ws), ws.numel())
     ev = _probe.begin() if _probe is not None else None
-    call('ot_mixed_gemm_rms', mode, ptr(A), lda, K, ptr(in_rows), a_xform, ptr(rstd), ptr(gamma), ptr(W),
-         w_gstride, ldw, N, ptr(tile_group), ntiles, ptr(bias), bias_gstride, ptr(C), ldc, ptr(out_rows), epi,
-         ptr(res), ldres, res_tok, None, 0, seed & 0xFFFFFFFF, site, float(drop), tail[0], tail[1], _sel(tail),
-         ctypes.byref(e), stream())
+    args = (mode, ptr(A), lda, K, ptr(in_rows), a_xform, ptr(rstd), ptr(gamma), ptr(W),
+            w_gstride, ldw, N, ptr(tile_group), ntiles, ptr(bias), bias_gstride, ptr(C), ldc, ptr(out_rows), epi,
+            ptr(res), ldres, res_tok, None, 0, seed & 0xFFFFFFFF, site, float(drop), tail[0], tail[1], _sel(tail),
+            ctypes.byref(e))
+    if bimg is not None:
+        call('ot_mixed_gemm_rms_img', *args, ptr(bimg[0]), bimg[1], bimg[2], stream())
+    else:
+        call('ot_mixed_gemm_rms', *args, stream())
     if ev is not None:
         _probe.end('mixed_gemm', 2.0 * (m_rows or ntiles * 128) * K * N, ev,
                    f'gemm_rms mode{mode} ax{a_xform} epi{epi} M{m_rows or ntiles * 128} K{K} N{N}')
@@ -182,6 +191,14 @@ def wgrad(A: Ptrish, lda: int, a_rows: Ptrish, D: Ptrish, ldd: int, d_rows: Ptri
 
 def transpose_banks(src, dst, banks_dev, nbanks, total_tiles) -> None:
     call('ot_transpose_banks', ptr(src), ptr(dst), ptr(banks_dev), nbanks, total_tiles, stream())
+
+
+def split_image_elems(G: int, N: int, K: int) -> int:
+    return int(_lib.load().ot_split_image_elems(G, N, K))
+
+
+def split_images(base, desc_dev, ndesc, total_units, img) -> None:
+    call('ot_split_images', ptr(base), ptr(desc_dev), ndesc, total_units, ptr(img), stream())
 
 
 def attn_fwd(qkv: torch.Tensor, ld: int, B: int, H: int, I: int, K: int, hd: int, out: torch.Tensor,

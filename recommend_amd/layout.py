@@ -25,6 +25,7 @@ from .params import dense_param_shapes, keras_variables
 
 TILE = 128
 ALIGN = 64
+IMAGE_UNIT_ELEMS = 3 * TILE * 16      # one (group, column tile, 16-k stage) block of a B image (bf16)
 # wgrad workgroups per launch (chunk sizing), by output tiles per chunk.  Small weights (< 8 tiles:
 # all of C2's) are capped at one round of the split kernel's 512 resident workgroups -- a count just
 # past a multiple of 512 (e.g. 513) leaves a nearly empty extra round; capped, the C2 GEMM family
@@ -80,6 +81,30 @@ class FlatLayout:
             tiles += G * ((K + 31) // 32) * ((N + 31) // 32)
         self.transpose_desc = np.array(recs, dtype=np.int64)
         self.transpose_tiles = tiles
+        # pre-split B images of the plane GEMM (ot_split_images), per bank and orientation:
+        # 'fwd' (B = W^T, k = the Keras input dim; the RMSNorm gamma in front of wqkv / w1 folded in)
+        # and 'dgrad' (B = W); only where the GEMM has whole 128-column tiles and 16-k stages
+        self.images: Dict[Tuple[str, str], Tuple[int, int, int, int]] = {}   # -> (offset, G, N, K)
+        irecs, units, ioff = [], 0, 0
+        for name, (G, K, N) in self.gemm_banks.items():
+            o = self.offsets[name]
+            gamma = None
+            if name.endswith('.wqkv'):
+                gamma = self.offsets[name[:-len('wqkv')] + 'norm1']
+            elif name.endswith('.w1') and name.startswith('blk.'):
+                gamma = self.offsets[name[:-len('w1')] + 'norm2']
+            for orient, (Nb, Kb, sn, sk) in (('fwd', (N, K, 1, N)), ('dgrad', (K, N, N, 1))):
+                if Nb % TILE or Kb % 16:
+                    continue
+                nu = G * (Nb // TILE) * (Kb // 16)
+                kscale = gamma if (orient == 'fwd' and gamma is not None) else -1
+                irecs.append((o, sn, sk, K * N, kscale, ioff, units, G, Nb, Kb))
+                self.images[(name, orient)] = (ioff, G, Nb, Kb)
+                units += nu
+                ioff += nu * IMAGE_UNIT_ELEMS
+        self.image_desc = np.array(irecs, dtype=np.int64).reshape(-1, 10)
+        self.image_units = units
+        self.image_elems = ioff
 
     def tview(self, flatT, name):
         """Transposed bank [G][N][K] inside the shadow buffer (1-D view)."""

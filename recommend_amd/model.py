@@ -53,7 +53,7 @@ class _Tokenize(torch.autograd.Function):
             mp = plan['ns_map'].to(dev)
             K.gemm(OT_GEMM_NT, nsm, m.layout.f_pad, m.layout.f_pad, mp['rows'][0], m.pT('tok.ns.kernel'), 0,
                    m.layout.f_pad, m.cfg_Lnsd, mp['tile_group'], plan['ns_map'].ntiles, (x0, L_S * d), L0 * d,
-                   mp['rows'][0], bias=m.p('tok.ns.bias'), epi=OT_EPI_BIAS, m_rows=B)
+                   mp['rows'][0], bias=m.p('tok.ns.bias'), epi=OT_EPI_BIAS, m_rows=B, bimg=m.bimg('tok.ns.kernel'))
         else:                                                   # model.py:249-251
             x0.view(B, L0, d)[:, L_S:].zero_()
         # ---- S tokens: per-sequence Dense(d) on gathered item rows (model.py:262-265)
@@ -62,7 +62,7 @@ class _Tokenize(torch.autograd.Function):
             A, lda = plan['seq_A'], m.config.seq_feature_dim
             K.gemm(OT_GEMM_NT, A, lda, lda, plan['seq_in'], m.pT('tok.seq.kernel'), lda * d, lda, d, sm['tile_group'],
                    plan['seq_map'].ntiles, x0, d, sm['rows'][0], bias=m.p('tok.seq.bias'), bias_gstride=d,
-                   epi=OT_EPI_BIAS, m_rows=plan['seq_M'])
+                   epi=OT_EPI_BIAS, m_rows=plan['seq_M'], bimg=m.bimg('tok.seq.kernel'))
         if plan['n_sep'] > 0:                                   # model.py:270-272
             K.fill_rows(x0, d, plan['sep_rows'], plan['n_sep'], m.p('tok.sep'), d)
         ctx.m, ctx.plan, ctx.gen = m, plan, plan['gen']
@@ -174,12 +174,15 @@ class _Block(torch.autograd.Function):
         qkv = torch.empty(B * I, 3 * d, device=dev)
         if Kq == I:
             K.gemm(OT_GEMM_NT, x, d, d, ma['rows'][0], wqkv, 3 * d * d, d, 3 * d, ma['tile_group'], na, qkv,
-                   3 * d, ma['rows'][0], a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=maps['all'].nrows)
+                   3 * d, ma['rows'][0], a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=maps['all'].nrows,
+                   bimg=m.bimg(f'blk.{l}.wqkv'))
         else:
             K.gemm(OT_GEMM_NT, x, d, d, ma['rows'][0], (wqkv, d * d), 3 * d * d, d, 2 * d, ma['tile_group'], na,
-                   (qkv, d), 3 * d, ma['rows'][0], a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=maps['all'].nrows)
+                   (qkv, d), 3 * d, ma['rows'][0], a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=maps['all'].nrows,
+                   bimg=m.bimg(f'blk.{l}.wqkv', tn0=d // TILE) if d % TILE == 0 else None)
             K.gemm(OT_GEMM_NT, x, d, d, qrows, wqkv, 3 * d * d, d, d, mt['tile_group'], nt, qkv,
-                   3 * d, qrows, a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=maps['tail'].nrows)
+                   3 * d, qrows, a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=maps['tail'].nrows,
+                   bimg=m.bimg(f'blk.{l}.wqkv'))
         o = torch.empty(B * Kq, d, device=dev)
         lse = torch.empty(B * H * Kq, device=dev)
         K.attn_fwd(qkv, 3 * d, B, H, I, Kq, hd, o, lse, qpos=pos)
@@ -189,16 +192,18 @@ class _Block(torch.autograd.Function):
         if fuse:
             K.gemm_rms(OT_GEMM_NT, o, d, d, mt['rows'][1], wo, 0, d, d, mt['tile_group'], nt, x1, d, mt['rows'][1],
                        epi=OT_EPI_RESIDUAL | dflag | OT_EPI_ROW_RSTD, res=x, ldres=d, res_tok=1, seed=seed,
-                       site=2 * l, drop=rate, tail=tail, m_rows=maps['tail'].nrows, rstd_out=rstd2, eps=RMS_EPS)
+                       site=2 * l, drop=rate, tail=tail, m_rows=maps['tail'].nrows, rstd_out=rstd2, eps=RMS_EPS,
+                       bimg=m.bimg(f'blk.{l}.wo'))
         else:
             K.gemm(OT_GEMM_NT, o, d, d, mt['rows'][1], wo, 0, d, d, mt['tile_group'], nt, x1, d, mt['rows'][1],
                    epi=OT_EPI_RESIDUAL | dflag, res=x, ldres=d, res_tok=1, seed=seed, site=2 * l, drop=rate,
-                   tail=tail, m_rows=maps['tail'].nrows)
+                   tail=tail, m_rows=maps['tail'].nrows, bimg=m.bimg(f'blk.{l}.wo'))
             K.rmsnorm_fwd(x1, d, B * Kq, d, rstd2, eps=RMS_EPS)
         # u = norm2(x1) @ W1[g] + b1[g]  (pre-activation; GELU applied by its consumers)
         u = torch.empty(B * Kq, f, device=dev)
         K.gemm(OT_GEMM_NT, x1, d, d, mt['rows'][1], w1, d * f, d, f, mt['tile_group'], nt, u, f, mt['rows'][1],
-               a_xform=OT_AX_RMSNORM, rstd=rstd2, gamma=g2, bias=b1, bias_gstride=f, epi=OT_EPI_BIAS, m_rows=maps['tail'].nrows)
+               a_xform=OT_AX_RMSNORM, rstd=rstd2, gamma=g2, bias=b1, bias_gstride=f, epi=OT_EPI_BIAS, m_rows=maps['tail'].nrows,
+               bimg=m.bimg(f'blk.{l}.w1'))
         # x2 = x1 + drop(gelu(u) @ W2[g] + b2[g])     (model.py:154-161, 198)
         x2 = torch.empty(B * Kq, d, device=dev)
         rstd_out = None
@@ -208,12 +213,12 @@ class _Block(torch.autograd.Function):
                        mt['rows'][1], a_xform=OT_AX_GELU, bias=b2, bias_gstride=d,
                        epi=OT_EPI_BIAS | OT_EPI_RESIDUAL | dflag | OT_EPI_ROW_RSTD, res=x1, ldres=d, res_tok=0,
                        seed=seed, site=2 * l + 1, drop=rate, tail=tail, m_rows=maps['tail'].nrows,
-                       rstd_out=rstd_out, eps=RMS_EPS)
+                       rstd_out=rstd_out, eps=RMS_EPS, bimg=m.bimg(f'blk.{l}.w2'))
         else:
             K.gemm(OT_GEMM_NT, u, f, f, mt['rows'][1], w2, f * d, f, d, mt['tile_group'], nt, x2, d, mt['rows'][1],
                    a_xform=OT_AX_GELU, bias=b2, bias_gstride=d, epi=OT_EPI_BIAS | OT_EPI_RESIDUAL | dflag, res=x1,
                    ldres=d, res_tok=0, seed=seed, site=2 * l + 1, drop=rate, tail=tail,
-                   m_rows=maps['tail'].nrows)
+                   m_rows=maps['tail'].nrows, bimg=m.bimg(f'blk.{l}.w2'))
         ctx.save_for_backward(x, rstd1, qkv, o, lse, x1, rstd2, u)
         ctx.m, ctx.l, ctx.I, ctx.Kq, ctx.seed, ctx.rate = m, l, I, Kq, seed, rate
         ctx.pos, ctx.inv = pos, inv
@@ -253,7 +258,8 @@ class _Block(torch.autograd.Function):
                     m_rows=maps['tail'].nrows, rowmap=maps['tail'])
         du = torch.empty(B * Kq, f, device=dev)
         K.gemm(OT_GEMM_NT, dy2, d, d, mt['rows'][1], m.p(f'blk.{l}.w2'), f * d, d, f, mt['tile_group'], nt, du, f,
-               mt['rows'][1], epi=OT_EPI_GELU_BWD, aux=u, ldaux=f, m_rows=maps['tail'].nrows)
+               mt['rows'][1], epi=OT_EPI_GELU_BWD, aux=u, ldaux=f, m_rows=maps['tail'].nrows,
+               bimg=m.bimg(f'blk.{l}.w2', 'dgrad'))
         with m.side(x1, du, rstd2):
             K.wgrad(x1, d, mt['rows'][1], du, f, mt['rows'][1], d, f, mt, nct, G, m.g(f'blk.{l}.w1'), d * f,
                     m.g(f'blk.{l}.b1'), f, a_xform=OT_AX_RMSNORM, rstd=rstd2, gamma=m.p(f'blk.{l}.norm2'),
@@ -267,11 +273,11 @@ class _Block(torch.autograd.Function):
                        seed=seed, site=2 * l, drop=rate, tail=tail, m_rows=maps['tail'].nrows, nx=x1, ldnx=d,
                        ngamma=m.p(f'blk.{l}.norm2'), nrstd=rstd2, dres=dx2, lddres=d,
                        dx_masked=dyo if rate > 0 else None, lddxm=d, dgamma=m.g(f'blk.{l}.norm2'),
-                       accumulate_dgamma=acc, device=dev)
+                       accumulate_dgamma=acc, device=dev, bimg=m.bimg(f'blk.{l}.w1', 'dgrad'))
         else:
             dxn2 = torch.empty(B * Kq, d, device=dev)
             K.gemm(OT_GEMM_NT, du, f, f, mt['rows'][1], m.p(f'blk.{l}.w1'), d * f, f, d, mt['tile_group'], nt, dxn2,
-                   d, mt['rows'][1], m_rows=maps['tail'].nrows)
+                   d, mt['rows'][1], m_rows=maps['tail'].nrows, bimg=m.bimg(f'blk.{l}.w1', 'dgrad'))
             K.rmsnorm_bwd(dxn2, d, x1, d, m.p(f'blk.{l}.norm2'), rstd2, dx1, d, B * Kq, d, dres=dx2, lddres=d,
                           dx_masked=dyo if rate > 0 else None, lddxm=d, seed=seed, site=2 * l, drop=rate,
                           tail=tail, dgamma=m.g(f'blk.{l}.norm2'), accumulate=acc, device=dev)
@@ -280,7 +286,7 @@ class _Block(torch.autograd.Function):
             _wgrad_single(m, o, dyo, d, d, mt, m.g(f'blk.{l}.wo'), acc, dev, maps['tail'].nrows, maps['tail'])
         do = torch.empty(B * Kq, d, device=dev)
         K.gemm(OT_GEMM_NT, dyo, d, d, mt['rows'][1], m.p(f'blk.{l}.wo'), 0, d, d, mt['tile_group'], nt, do, d,
-               mt['rows'][1], m_rows=maps['tail'].nrows)
+               mt['rows'][1], m_rows=maps['tail'].nrows, bimg=m.bimg(f'blk.{l}.wo', 'dgrad'))
         # attention
         dqkv = torch.empty(B * I, 3 * d, device=dev)
         if Kq < I:
@@ -296,11 +302,13 @@ class _Block(torch.autograd.Function):
                        ma['tile_group'], na, dx, d, ma['rows'][0], epi=OT_EPI_RMSNORM_BWD,
                        m_rows=maps['all'].nrows, nx=x, ldnx=d, ngamma=m.p(f'blk.{l}.norm1'), nrstd=rstd1,
                        dres=dx1, lddres=d, dres_tail=(Kq, I, inv) if Kq < I else (0, 0),
-                       dgamma=m.g(f'blk.{l}.norm1'), accumulate_dgamma=acc, device=dev)
+                       dgamma=m.g(f'blk.{l}.norm1'), accumulate_dgamma=acc, device=dev,
+                       bimg=m.bimg(f'blk.{l}.wqkv', 'dgrad'))
         else:
             dxn1 = torch.empty(B * I, d, device=dev)
             K.gemm(OT_GEMM_NT, dqkv, 3 * d, 3 * d, ma['rows'][0], m.p(f'blk.{l}.wqkv'), 3 * d * d, 3 * d, d,
-                   ma['tile_group'], na, dxn1, d, ma['rows'][0], m_rows=maps['all'].nrows)
+                   ma['tile_group'], na, dxn1, d, ma['rows'][0], m_rows=maps['all'].nrows,
+                   bimg=m.bimg(f'blk.{l}.wqkv', 'dgrad'))
             K.rmsnorm_bwd(dxn1, d, x, d, m.p(f'blk.{l}.norm1'), rstd1, dx, d, B * I, d, dres=dx1, lddres=d,
                           dres_tail=(Kq, I, inv) if Kq < I else (0, 0), dgamma=m.g(f'blk.{l}.norm1'), accumulate=acc,
                           device=dev)
@@ -443,6 +451,12 @@ class OneTransModel(nn.Module):
         self.flat.grad = torch.zeros_like(self.flat)
         self.flatT = torch.zeros(self.layout.total, device=self.device)     # transposed GEMM weight shadow
         self._tdesc = torch.from_numpy(self.layout.transpose_desc.reshape(-1)).to(self.device)
+        # pre-split bf16 plane images of the GEMM weight banks (the plane GEMM's B operand, split mode);
+        # rebuilt with the transposed shadow after every weight update.  ONETRANS_PLANE_GEMM=0: off
+        self.use_plane = os.environ.get('ONETRANS_PLANE_GEMM', '1') != '0'
+        self.img = torch.zeros(max(1, self.layout.image_elems), dtype=torch.int16, device=self.device)
+        self._idesc = (torch.from_numpy(self.layout.image_desc.reshape(-1)).to(self.device)
+                       if self.layout.image_units else None)
         self.tables: Dict[str, torch.Tensor] = {}
         self.accumulate_grads = False
         # data-parallel hook (OneTransOptimizer): called with a layer index / 'head' when those gradient
@@ -493,6 +507,21 @@ class OneTransModel(nn.Module):
         """Re-derive the transposed weight banks after any change of the weights (init, load, optimizer)."""
         K.transpose_banks(self.flat.data, self.flatT, self._tdesc, self.layout.transpose_desc.shape[0],
                           self.layout.transpose_tiles)
+        if self._idesc is not None:
+            K.split_images(self.flat.data, self._idesc, self.layout.image_desc.shape[0], self.layout.image_units,
+                           self.img)
+
+    def bimg(self, name: str, orient: str = 'fwd', tn0: int = 0):
+        """(image, column tiles per group, first tile) of a weight bank's pre-split B image for the plane
+        GEMM: orient 'fwd' = W^T (RMSNorm gamma folded in for wqkv / w1), 'dgrad' = W; None when the
+        bank has no image (partial column tiles) or the plane GEMM is off."""
+        if not self.use_plane:
+            return None
+        e = self.layout.images.get((name, orient))
+        if e is None:
+            return None
+        off, G, N, K_ = e
+        return ((self.img, off), N // TILE, tn0)
 
     def load_param_dict(self, params: Dict[str, np.ndarray]) -> None:
         """Load host arrays (params.init_params layout; tok.ns.kernel may be unpadded)."""

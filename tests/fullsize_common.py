@@ -123,4 +123,9 @@ def setup_config(name: str):
 
 
 BATCH_SEED = 424242
-DROPOUT_SEED = 0x2468ACE
+MODEL_SEED = 0
+
+
+def dropout_seed(model_seed: int = MODEL_SEED, step: int = 1) -> int:
+    """The dropout seed OneTransModel.forward_probs uses on its ``step``-th training forward."""
+    return ((0x5EED0000 ^ model_seed) + 0x9E3779B9 * step) & 0xFFFFFFFF

@@ -1,0 +1,168 @@
+"""Plane GEMM (pre-split B image + global_load_lds, gemm.hip plane_gemm_kernel) vs the register-
+staged split GEMM on the same operands: every prologue / epilogue specialisation the model uses,
+ragged row maps (partial tiles, -1 rows), several weight groups, a column-tile offset into the image
+and the RMSNorm gamma folded into the image.  The register-staged kernel is itself checked against
+torch fp64 in tests/test_kernels_gpu.py; both are f32-accurate (split-bf16, six products), so they
+agree to f32 rounding level (the folded gamma changes the rounding order only)."""
+
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from recommend_amd import kernels as K
+from recommend_amd._lib import (OT_AX_GELU, OT_AX_NONE, OT_AX_RMSNORM, OT_EPI_ACCUMULATE, OT_EPI_BIAS,
+                                OT_EPI_DROPOUT, OT_EPI_GELU_BWD, OT_EPI_RESIDUAL, OT_EPI_RMSNORM_BWD,
+                                OT_EPI_ROW_RSTD, OT_GEMM_NT)
+from recommend_amd.layout import IMAGE_UNIT_ELEMS, build_map
+
+
+@pytest.fixture(autouse=True)
+def split_mode(dev):
+    old = K.set_matmul_mode('split')
+    yield
+    K.set_matmul_mode(old)
+
+
+def make_image(W, dev, gamma=None):
+    """W [G, N, K] fp32 (B[g][n][k]) -> (image, ntn); gamma [K] folded into the k rows."""
+    G, N, K_ = W.shape
+    base = torch.cat([W.reshape(-1), gamma if gamma is not None else torch.zeros(0)]).float().to(dev)
+    desc = torch.tensor([0, K_, 1, N * K_, G * N * K_ if gamma is not None else -1, 0, 0, G, N, K_],
+                        dtype=torch.int64, device=dev)
+    units = G * (N // 128) * (K_ // 16)
+    assert K.split_image_elems(G, N, K_) == units * IMAGE_UNIT_ELEMS
+    img = torch.zeros(units * IMAGE_UNIT_ELEMS, dtype=torch.int16, device=dev)
+    K.split_images(base, desc, 1, units, img)
+    return img, N // 128
+
+
+def ragged_map(rng, M, G):
+    """Rows of M split over G groups (uneven counts, so every group has a partial tile)."""
+    cuts = np.sort(rng.choice(np.arange(1, M), G - 1, replace=False))
+    counts = np.diff(np.concatenate([[0], cuts, [M]]))
+    src, dst = rng.permutation(M), rng.permutation(M)
+    per, o = [], 0
+    for c in counts:
+        per.append([src[o:o + c], dst[o:o + c]])
+        o += c
+    return build_map(per)
+
+
+def close(a, b, K_):
+    torch.testing.assert_close(a, b, rtol=2e-5, atol=2e-5 * math.sqrt(K_))
+
+
+@pytest.mark.parametrize('K_,N,tn0,ncols', [(128, 384, 0, 384), (128, 384, 1, 256), (512, 128, 0, 128),
+                                            (384, 128, 0, 128), (64, 128, 0, 128), (432, 1536, 0, 1536)])
+@pytest.mark.parametrize('xf', [OT_AX_NONE, OT_AX_RMSNORM, OT_AX_GELU])
+def test_plane_gemm_prologues(dev, K_, N, tn0, ncols, xf):
+    rng = np.random.default_rng(K_ + N + xf)
+    G, M = 3, 777
+    rm = ragged_map(rng, M, G)
+    d = rm.to(dev)
+    A = torch.randn(M, K_, device=dev)
+    W = torch.randn(G, N, K_) / math.sqrt(K_)
+    gamma = 1 + 0.1 * torch.randn(K_)
+    rstd = torch.rand(M, device=dev) + 0.5
+    bias = torch.randn(G, ncols, device=dev)
+    img, ntn = make_image(W, dev, gamma if xf == OT_AX_RMSNORM else None)
+    Wd = W.to(dev)
+    epi = OT_EPI_BIAS if xf != OT_AX_NONE else 0
+    outs = []
+    for b in (None, (img, ntn, tn0)):
+        C = torch.full((M, ncols), float('nan'), device=dev)
+        K.gemm(OT_GEMM_NT, A, K_, K_, d['rows'][0], (Wd, tn0 * 128 * K_), N * K_, K_, ncols, d['tile_group'],
+               rm.ntiles, C, ncols, d['rows'][1], a_xform=xf, rstd=rstd, gamma=gamma.to(dev), bias=bias,
+               bias_gstride=ncols, epi=epi, bimg=b)
+        outs.append(C)
+    torch.cuda.synchronize()
+    assert not torch.isnan(outs[1]).any()
+    close(outs[1], outs[0], K_)
+
+
+@pytest.mark.parametrize('case', ['res_drop', 'res', 'res_rstd', 'res_drop_rstd', 'gelu_bias_res_drop',
+                                  'gelu_bias_res_drop_rstd', 'gelu_bwd', 'accumulate'])
+def test_plane_gemm_epilogues(dev, case):
+    rng = np.random.default_rng(7)
+    B, I, Kq = 37, 9, 4
+    G, N = 2, 128
+    M = B * Kq
+    K_ = 512 if case.startswith('gelu_bias') else 128
+    xf = OT_AX_GELU if case.startswith('gelu_bias') else OT_AX_NONE
+    epi = {'res_drop': OT_EPI_RESIDUAL | OT_EPI_DROPOUT, 'res': OT_EPI_RESIDUAL,
+           'res_rstd': OT_EPI_RESIDUAL | OT_EPI_ROW_RSTD, 'res_drop_rstd': OT_EPI_RESIDUAL | OT_EPI_DROPOUT | OT_EPI_ROW_RSTD,
+           'gelu_bias_res_drop': OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_DROPOUT,
+           'gelu_bias_res_drop_rstd': OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_DROPOUT | OT_EPI_ROW_RSTD,
+           'gelu_bwd': OT_EPI_GELU_BWD, 'accumulate': OT_EPI_ACCUMULATE}[case]
+    r = np.arange(M)
+    grp = r % G
+    rm = build_map([[r[grp == g], r[grp == g]] for g in range(G)])
+    d = rm.to(dev)
+    A = torch.randn(M, K_, device=dev)
+    # the residual cases use one weight for every group (w_gstride 0, like Wo): a one-group image
+    shared = case.startswith('res')
+    W = torch.randn(1 if shared else G, N, K_) / math.sqrt(K_)
+    wgs = 0 if shared else N * K_
+    img, ntn = make_image(W, dev)
+    Wd = W.to(dev)
+    bias = torch.randn(G, N, device=dev)
+    res = torch.randn(B * I, N, device=dev)       # token-mapped residual (res_tok) for the first cases
+    aux = torch.randn(M, N, device=dev)
+    C0 = torch.randn(M, N, device=dev)
+    res_tok = 1 if case.startswith('res') else 0
+    resv = res if res_tok else res[:M].contiguous()
+    outs = []
+    for b in (None, (img, ntn, 0)):
+        C = C0.clone()
+        rs = torch.full((M,), float('nan'), device=dev)
+        kw = dict(a_xform=xf, bias=bias, bias_gstride=N, epi=epi, res=resv, ldres=N, res_tok=res_tok, seed=99,
+                  site=3, drop=0.2, tail=(Kq, I), bimg=b)
+        if epi & OT_EPI_ROW_RSTD:
+            K.gemm_rms(OT_GEMM_NT, A, K_, K_, d['rows'][0], Wd, wgs, K_, N, d['tile_group'], rm.ntiles, C, N,
+                       d['rows'][1], rstd_out=rs, eps=1e-6, **kw)
+        else:
+            K.gemm(OT_GEMM_NT, A, K_, K_, d['rows'][0], Wd, wgs, K_, N, d['tile_group'], rm.ntiles, C, N,
+                   d['rows'][1], aux=aux, ldaux=N, **kw)
+        outs.append((C, rs))
+    torch.cuda.synchronize()
+    close(outs[1][0], outs[0][0], K_)
+    if epi & OT_EPI_ROW_RSTD:
+        torch.testing.assert_close(outs[1][1], outs[0][1], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize('K_', [128, 384, 512])
+@pytest.mark.parametrize('drop', [0.0, 0.25])
+def test_plane_gemm_rmsnorm_bwd(dev, K_, drop):
+    rng = np.random.default_rng(11)
+    G, N, Kq, I, B = 3, 128, 5, 12, 41
+    M = B * I
+    rm = ragged_map(rng, M, G)
+    d = rm.to(dev)
+    A = torch.randn(M, K_, device=dev)
+    W = torch.randn(G, N, K_) / math.sqrt(K_)
+    img, ntn = make_image(W, dev)
+    Wd = W.to(dev)
+    x = torch.randn(M, N, device=dev)
+    gamma = 1 + 0.1 * torch.randn(N, device=dev)
+    rstd = torch.rsqrt((x * x).mean(1) + 1e-6)
+    dres = torch.randn(B * Kq, N, device=dev)
+    epi = OT_EPI_RMSNORM_BWD | (OT_EPI_DROPOUT if drop > 0 else 0)
+    outs = []
+    for b in (None, (img, ntn, 0)):
+        dx = torch.full((M, N), float('nan'), device=dev)
+        dxm = torch.full((M, N), float('nan'), device=dev)
+        dg = torch.full((N,), 0.5, device=dev)
+        K.gemm_rms(OT_GEMM_NT, A, K_, K_, d['rows'][0], Wd, N * K_, K_, N, d['tile_group'], rm.ntiles, dx, N,
+                   d['rows'][1], epi=epi, seed=5, site=2, drop=drop, tail=(1, 1), nx=x, ldnx=N, ngamma=gamma,
+                   nrstd=rstd, dres=dres, lddres=N, dres_tail=(Kq, I), dx_masked=dxm if drop > 0 else None, lddxm=N,
+                   dgamma=dg, accumulate_dgamma=True, bimg=b)
+        outs.append((dx, dxm, dg))
+    torch.cuda.synchronize()
+    close(outs[1][0], outs[0][0], K_)
+    if drop > 0:
+        close(outs[1][1], outs[0][1], K_)
+    torch.testing.assert_close(outs[1][2], outs[0][2], rtol=1e-4, atol=1e-3)

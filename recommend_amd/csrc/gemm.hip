@@ -14,6 +14,7 @@
 // 16 consecutive rows).  The k index inside an MFMA step is permuted (lane half h supplies
 // k = 16h + s at step s) so each lane reads 4 consecutive k with one ds_read_b128.
 #include <algorithm>
+#include <cstdlib>
 #include <mutex>
 
 #include "common.h"
@@ -115,7 +116,7 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 // LAYOUT 0: 2x2 waves, acc[2m + n] = rows 64 (wave >> 1) + 32 m, cols 64 (wave & 1) + 32 n;
 // LAYOUT 1: 4x1 waves, acc[nb] = rows 32 wave, cols 32 nb.  ROWSCALE: multiply row r by
 // a_rstd[in_rows[r]] first (the plane GEMM's RMSNorm prologue, folded into the weights).
-template <int EPIT, int LAYOUT, bool ROWSCALE>
+template <int EPIT, int LAYOUT, bool ROWSCALE, int RBN = 8>
 __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x16 (&acc)[4], float* smem, int tm,
                                                   int n0, int g) {
   const int epi = EPIT;
@@ -144,23 +145,22 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
       ngam = *reinterpret_cast<const f32x4*>(p.ngamma + col);
       *reinterpret_cast<f32x4*>(dgs + rb * GT + 4 * c4) = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    int orow[2][8];
-    float rsc[2][8];
+    constexpr int RB = RMSBWD ? RBN / 2 : RBN;          // rows per operand-load batch (register budget)
 #pragma unroll
-    for (int hf = 0; hf < 2; ++hf)
+    for (int hf = 0; hf < 2; ++hf) {
+      // this half's output rows (the loads stay in flight across the accumulator write below)
+      int orow[8];
+      float rsc[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int lr = rb + 8 * i;                      // local row of the half: tile row below
         const int64_t gr = (int64_t)tm * GT + (LAYOUT == 0 ? (lr >> 5) * 64 + 32 * hf + (lr & 31) : 64 * hf + lr);
-        orow[hf][i] = p.out_rows ? p.out_rows[gr] : (int)gr;
+        orow[i] = p.out_rows ? p.out_rows[gr] : (int)gr;
         if (ROWSCALE) {                                 // RMSNorm folded into B: scale by the A row's rstd
           const int ir = p.in_rows ? p.in_rows[gr] : (int)gr;
-          rsc[hf][i] = ir >= 0 ? p.a_rstd[ir] : 0.f;
+          rsc[i] = ir >= 0 ? p.a_rstd[ir] : 0.f;
         }
       }
-    constexpr int RB = RMSBWD ? 4 : 8;                  // rows per operand-load batch (register budget)
-#pragma unroll
-    for (int hf = 0; hf < 2; ++hf) {
       if (LAYOUT == 0) {
 #pragma unroll
         for (int n = 0; n < 2; ++n)
@@ -182,7 +182,7 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
         float nr[RB];
 #pragma unroll
         for (int i = 0; i < RB; ++i) {
-          const int orr = orow[hf][i0 + i];
+          const int orr = orow[i0 + i];
           const int64_t o = orr < 0 ? 0 : orr;
           tok[i] = (need_tok && orr >= 0) ? tail_token(orr, p.tail_K, p.tail_I, p.tail_pos) : o;
           if (RMSBWD) {
@@ -201,9 +201,9 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
         }
 #pragma unroll
         for (int i = 0; i < RB; ++i) {
-          const int orr = orow[hf][i0 + i];
+          const int orr = orow[i0 + i];
           f32x4 v = *reinterpret_cast<const f32x4*>(ct + (rb + 8 * (i0 + i)) * CLD + 4 * c4);
-          if (ROWSCALE) v = v * rsc[hf][i0 + i];
+          if (ROWSCALE) v = v * rsc[i0 + i];
           if (epi & OT_EPI_BIAS) v += bias4;
           if (epi & OT_EPI_GELU_BWD) {
             v.x *= gelu_erf_grad(aux4[i].x); v.y *= gelu_erf_grad(aux4[i].y);
@@ -625,17 +625,16 @@ __global__ __launch_bounds__(256, (NT && SPLT) ? 2 : OT_GEMM_MINWG) void mixed_g
 // are 64 B with the 16-B chunk swizzle c ^ ((r >> 2) & 3): conflict-free ds_read_b128).  An
 // RMSNorm prologue is folded into B (gamma scales B's k rows when the image is built) and its row
 // factor rstd is applied in the epilogue; a GELU prologue runs on the fragment before the split.
-constexpr int PG_NSTG = 3;                         // LDS stages
 constexpr int PG_A_BYTES = GT * 16 * 4;            // A stage image: 128 rows x 16 f32
 constexpr int PG_B_BYTES = 3 * GT * 16 * 2;        // B stage image: 3 planes x 128 n x 16 bf16
 constexpr int PG_STG_BYTES = PG_A_BYTES + PG_B_BYTES;
-constexpr int PG_SHMEM = PG_NSTG * PG_STG_BYTES;   // 60 KiB (the epilogue reuses the first 38 KiB)
-static_assert(64 * (GT + 4) * 4 + 8 * GT * 4 <= PG_SHMEM, "plane GEMM epilogue LDS");
+static_assert(64 * (GT + 4) * 4 + 8 * GT * 4 <= 2 * PG_STG_BYTES, "plane GEMM epilogue LDS");
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-template <int AXT, int EPIT>
-__global__ __launch_bounds__(256, 2) void plane_gemm_kernel(GemmArgs p) {
+template <int AXT, int EPIT, int NSTG, int MINW>
+__global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
+  static_assert(NSTG == 2 || NSTG == 3, "plane GEMM stages");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   char* lds = reinterpret_cast<char*>(smem);
   const int nwg = p.ntm * p.ntn;
@@ -690,18 +689,18 @@ __global__ __launch_bounds__(256, 2) void plane_gemm_kernel(GemmArgs p) {
   const int boff = PG_A_BYTES + li * 32 + 16 * (h ^ ((li >> 3) & 1));
 
   issue(0, 0);
-  if (nk > 1) issue(1, 1);
+  if (NSTG == 3 && nk > 1) issue(1, 1);
   for (int kt = 0; kt < nk; ++kt) {
-    // this wave's copies of stage kt are done (the 5 of stage kt+1 may still fly), every wave's
-    // after the barrier; the barrier also retires every read of stage kt-1's buffer, which the
-    // copies of stage kt+2 overwrite
-    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    // this wave's copies of stage kt are done (with 3 stages the 5 of stage kt+1 may still fly),
+    // every wave's after the barrier; the barrier also retires every read of the buffer that the
+    // copies of stage kt+NSTG-1 then overwrite (last read in iteration kt-1)
+    if (NSTG == 3 && kt + 1 < nk) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (kt + 2 < nk) issue(kt + 2, (kt + 2) % PG_NSTG);
-    const char* sb = lds + (kt % PG_NSTG) * PG_STG_BYTES;
+    if (kt + NSTG - 1 < nk) issue(kt + NSTG - 1, (kt + NSTG - 1) % NSTG);
+    const char* sb = lds + (kt % NSTG) * PG_STG_BYTES;
     f32x4 a0 = *reinterpret_cast<const f32x4*>(sb + aoff0);
     f32x4 a1 = *reinterpret_cast<const f32x4*>(sb + aoff1);
     u32x4 fb[4][3];
@@ -721,7 +720,7 @@ __global__ __launch_bounds__(256, 2) void plane_gemm_kernel(GemmArgs p) {
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();                                    // the epilogue reuses the stage buffers
-  gemm_vec_epilogue<EPIT, 1, AXT == OT_AX_RMSNORM>(p, acc, smem, tm, n0, g);
+  gemm_vec_epilogue<EPIT, 1, AXT == OT_AX_RMSNORM, MINW >= 4 ? 4 : 8>(p, acc, smem, tm, n0, g);
 }
 
 // Pre-split B images (ot_split_images).  desc [nd][10] int64: {src_off, sn, sk, gstride, kscale_off
@@ -1208,6 +1207,12 @@ __global__ __launch_bounds__(256) void transpose_banks_kernel(const float* __res
 
 // matmul arithmetic of the GEMM family (ot_set_matmul_mode); process-wide, set before launching
 static int g_matmul_mode = OT_MATMUL_SPLIT_BF16;
+// plane GEMM pipeline: 0 = 3 LDS stages at 2 waves / SIMD, 1 = 2 stages at 4 waves / SIMD
+// (tuning switch: environment ONETRANS_PLANE_CFG, read once)
+static int g_plane_cfg = [] {
+  const char* e = getenv("ONETRANS_PLANE_CFG");
+  return e ? atoi(e) : 1;
+}();
 
 }  // namespace ot
 
@@ -1338,7 +1343,7 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
                "the GEMM needs %d from tile %d", bimg_ntn, (int)p.ntn, bimg_tn0);
     void (*pk)(GemmArgs) = nullptr;
 #define OT_PSPEC(AX_, EP_) \
-    if (x == AX_ && e == (EP_)) pk = plane_gemm_kernel<AX_, EP_>;
+    if (x == AX_ && e == (EP_)) pk = g_plane_cfg == 0 ? plane_gemm_kernel<AX_, EP_, 3, 2> : plane_gemm_kernel<AX_, EP_, 2, 4>;
     OT_PSPEC(OT_AX_RMSNORM, 0)
     OT_PSPEC(OT_AX_RMSNORM, OT_EPI_BIAS)
     OT_PSPEC(OT_AX_GELU, OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_DROPOUT)
@@ -1358,7 +1363,7 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
 #undef OT_PSPEC
     if (pk) { kern = pk; plane = true; }
   }
-  const size_t launch_shmem = plane ? (size_t)PG_SHMEM : shmem;
+  const size_t launch_shmem = plane ? (size_t)(g_plane_cfg == 0 ? 3 : 2) * PG_STG_BYTES : shmem;
   OT_REQUIRE(kern || !rms_flags, "ot_mixed_gemm_rms: no specialised kernel for epilogue flags %d", epi);
   if (!kern) {   // any other combination: generic instantiation (run-time prologue/epilogue)
     if (mode == OT_GEMM_NT && split && one)

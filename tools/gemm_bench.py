@@ -32,6 +32,21 @@ cases = {
  'ffn1_wgrad 128x512': (lambda: K.wgrad(x, d, rows, du, f, rows, d, f, ma, nch, G, dW, d*f, db, f, a_xform=OT_AX_RMSNORM, rstd=rstd, gamma=g, device=dev, rowmap=maps['all']), 2*M*f*d),
  'qkv_wgrad 128x384': (lambda: K.wgrad(x, d, rows, qkv, 3*d, rows, d, 3*d, ma, nch, G, dW, 3*d*d, None, 0, a_xform=OT_AX_RMSNORM, rstd=rstd, gamma=g, device=dev, rowmap=maps['all']), 2*M*3*d*d),
 }
+# plane GEMM variants (pre-split B images; tests/test_plane_gemm_gpu.py make_image)
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'tests'))
+from test_plane_gemm_gpu import make_image
+K.set_matmul_mode('split')
+im_qkv = make_image(wqkvT.cpu(), dev, g.cpu()); im_w1 = make_image(w1T.cpu(), dev, g.cpu()); im_w2 = make_image(w2T.cpu(), dev)
+im_w2d = make_image(w2.cpu(), dev); im_w1d = make_image(w1.cpu(), dev); im_qkvd = make_image(wqkv.cpu(), dev)
+P = lambda im, tn0=0: (im[0], im[1], tn0)
+cases.update({
+ 'P qkv_fwd 128x384': (lambda: K.gemm(OT_GEMM_NT, x, d, d, rows, wqkvT, 3*d*d, d, 3*d, tg, na, qkv, 3*d, rows, a_xform=OT_AX_RMSNORM, rstd=rstd, gamma=g, bimg=P(im_qkv)), 2*M*d*3*d),
+ 'P ffn1_fwd 128x512': (lambda: K.gemm(OT_GEMM_NT, x, d, d, rows, w1T, d*f, d, f, tg, na, u, f, rows, a_xform=OT_AX_RMSNORM, rstd=rstd, gamma=g, bias=b1, bias_gstride=f, epi=OT_EPI_BIAS, bimg=P(im_w1)), 2*M*d*f),
+ 'P ffn2_fwd 512x128': (lambda: K.gemm(OT_GEMM_NT, u, f, f, rows, w2T, f*d, f, d, tg, na, y, d, rows, a_xform=OT_AX_GELU, bias=b2, bias_gstride=d, epi=OT_EPI_BIAS|OT_EPI_RESIDUAL|OT_EPI_DROPOUT, res=x, ldres=d, seed=1, site=1, drop=0.1, tail=(I, I), bimg=P(im_w2)), 2*M*f*d),
+ 'P ffn2_dgrad NT 128->512': (lambda: K.gemm(OT_GEMM_NT, y, d, d, rows, w2, f*d, d, f, tg, na, du, f, rows, epi=OT_EPI_GELU_BWD, aux=u, ldaux=f, bimg=P(im_w2d)), 2*M*f*d),
+ 'P ffn1_dgrad NT 512->128': (lambda: K.gemm(OT_GEMM_NT, du, f, f, rows, w1, d*f, f, d, tg, na, dx, d, rows, bimg=P(im_w1d)), 2*M*f*d),
+ 'P qkv_dgrad NT 384->128': (lambda: K.gemm(OT_GEMM_NT, qkv, 3*d, 3*d, rows, wqkv, 3*d*d, 3*d, d, tg, na, dx, d, rows, bimg=P(im_qkvd)), 2*M*3*d*d),
+})
 sel = sys.argv[1:] or list(cases)
 for _ in range(2):
     for k in sel: cases[k][0]()

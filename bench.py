@@ -46,6 +46,10 @@ def parse():
     ap.add_argument('--no-probe', action='store_true', help='skip the per-kernel HIP-event (roofline) pass')
     ap.add_argument('--probe-steps', type=int, default=10, help='steps of the roofline pass (0: no roofline)')
     ap.add_argument('--repeats', type=int, default=3, help='timed regions of --steps steps; value = median')
+    ap.add_argument('--precision', default='auto', choices=['auto', 'split', 'f32', 'bf16', 'fp8attn'],
+                    help="GEMM / attention arithmetic.  auto: the config's stated precision — C5 (BASELINE "
+                         "configs[4]) 'fp8attn' (bf16 GEMMs + block-scaled fp8 attention forward), every other "
+                         "config the reference's f32 via the exact split-bf16 GEMMs (ONETRANS_MATMUL overrides)")
     return ap.parse_args()
 
 
@@ -157,6 +161,11 @@ def main():
 
     dev = torch.device('cuda', local if world > 1 else 0)
     cfg = workload_config(args.config)
+    precision = args.precision
+    if precision == 'auto':
+        precision = 'fp8attn' if args.config == 'C5' else os.environ.get('ONETRANS_MATMUL', 'split')
+    K.set_matmul_mode('bf16' if precision in ('bf16', 'fp8attn') else precision)
+    cfg.compute_dtype = {'fp8attn': 'fp8attn', 'bf16': 'bf16'}.get(precision, 'fp32')
     B = args.batch or cfg._batch
     model = OneTransModel(cfg, device=dev, seed=0)
     trainer = OneTransTrainer(cfg, model=model)
@@ -254,7 +263,7 @@ def main():
         'value': round(value, 1), 'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': round(1e3 * t / args.steps, 3), 'higher_is_better': True,
         'scaling': 'weak', 'vs_baseline': None,
-        'dtype': 'bf16' if K.matmul_mode() == 'bf16' else 'f32', 'data': 'synthetic',
+        'dtype': 'bf16' if K.matmul_mode() == 'bf16' else 'f32', 'data': 'synthetic', 'precision': precision,
         'config': {'workload': f'{args.config}: OneTrans {cfg.num_layers}L d{cfg.hidden_dim} H{cfg.num_heads} f{cfg.ffn_dim} '
                                f'L_NS{cfg.num_ns_tokens} L_S{sum(seq_lens) + 2} (seq 3x{seq_lens[0]}), '
                                f'Criteo-shape 13 dense + 26 ids, replicated tables, fwd+bwd+optimizer',
@@ -314,15 +323,19 @@ def main():
             blk_ms = ms('mixed_gemm') + ms('attention') + ms('rowwise')
             # matrix-core time the block's algorithmic work needs at each kernel's own peak, over the
             # block's kernel time (GEMMs at the split ceiling, attention at the f32 MFMA peak)
-            busy_ms = fl('mixed_gemm') / (gpeak * 1e9) + fl('attention') / (FP32_MFMA_PEAK_TFLOPS * 1e9)
+            busy_ms = fl('mixed_gemm') / (gpeak * 1e9) + fl('attention') / ((
+                BF16_MFMA_PEAK_TFLOPS if K.matmul_mode() == 'bf16' else FP32_MFMA_PEAK_TFLOPS) * 1e9)
+            apeak = BF16_MFMA_PEAK_TFLOPS if K.matmul_mode() == 'bf16' else FP32_MFMA_PEAK_TFLOPS
             res['attention_mfma'] = {
                 'core_tflops': round(att['tflops'], 2),
-                'core_frac': round(att['tflops'] / FP32_MFMA_PEAK_TFLOPS, 4),
-                'core_peak': FP32_MFMA_PEAK_TFLOPS,
+                'core_frac': round(att['tflops'] / apeak, 4),
+                'core_peak': apeak,
                 'block_tflops': round(blk_fl / (blk_ms * 1e-3) / 1e12, 2),
                 'block_frac': round(busy_ms / blk_ms, 4), 'unit': 'TFLOP/s',
                 'note': 'algorithmic flops (tail-only queries, causal pairs) / HIP-event kernel time; '
-                        'attention core on native f32 MFMA (peak 157.3)'}
+                        + ('attention core on bf16 MFMA (peak = bf16 dense 2516.8; with fp8attn the forward '
+                           'runs block-scaled fp8, whose dense peak is 2x)' if K.matmul_mode() == 'bf16'
+                           else 'attention core on native f32 MFMA (peak 157.3)')}
     if not args.no_cpu_baseline and world == 1:          # rank 0 at N=1 only
         res['cpu_baseline'] = cpu_baseline(args.config, args.cpu_seconds)
     print(json.dumps(res), flush=True)

@@ -186,6 +186,16 @@ int ot_mixed_gemm_rms_img(int mode, const float* A, int64_t lda, int K, const in
  * [B*K] of ot_pyramid_select (query j at qpos[b*K + j], causal limit key <= qpos). */
 int ot_attn_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos,
                 int head_dim, float* out, float* lse, void* stream);
+/* The same forward on block-scaled fp8 MFMA (attention_fp8.hip; BASELINE configs[4] "CDNA4 fp8 MFMA
+ * attention"): K and Q quantised to OCP e4m3 with one e8m0 scale per (row, 32 dims), V with one scale
+ * per (dim, 64 keys), P = exp(s - m) as e4m3 of P * 2^8; v_mfma_scale_f32_32x32x64_f8f6f4 for QK^T and
+ * PV, softmax statistics and O accumulation in f32.  head_dim 64 or 128.  Reduced precision (not the
+ * reference's f32): out / lse as ot_attn_fwd within the fp8 bounds of tests/test_attn_fp8_gpu.py.
+ * workspace: ot_attn_fwd_fp8_workspace_size(B, H, I, head_dim) bytes, 16-B aligned (the packed
+ * fp8 K / V^T images and their scales). */
+size_t ot_attn_fwd_fp8_workspace_size(int B, int H, int I, int head_dim);
+int ot_attn_fwd_fp8(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos,
+                    int head_dim, float* out, float* lse, void* workspace, size_t ws_bytes, void* stream);
 /* dqkv: like qkv (dq written on the K kept query rows only; dk, dv on all rows);
  * ws: ot_attn_bwd_workspace_size(B, H, K) bytes (row stats padded to 32 queries per (b, h)) */
 size_t ot_attn_bwd_workspace_size(int B, int H, int K);

@@ -1,0 +1,389 @@
+// Causal attention forward on gfx950 block-scaled fp8 MFMA (v_mfma_scale_f32_32x32x64_f8f6f4, OCP
+// e4m3 operands, one e8m0 scale per 32-element k block): BASELINE configs[4] "bf16, CDNA4 fp8 MFMA
+// attention" (C5).  Replaces the same reference op as ot_attn_fwd: model.py:100-114 (QK^T/sqrt(hd),
+// band_part mask with -1e9, softmax, PV) with the pyramid's tail / selected queries (model.py:356/371).
+//
+// Two launches:
+//  1. attn_fp8_pack_kernel — per (sample, head, 64-key block): K rows quantised to e4m3 with one
+//     scale per (key, 32 dims); V quantised with one scale per (dim, 64 keys) and written transposed
+//     ([dim][key], keys permuted inside each 64-key block into the order the P operand holds them).
+//  2. attn_fwd_fp8_kernel — one wave per (sample, head) as attn_fwd_split_kernel, 32 queries x 64 keys
+//     per step:  S^T = K Q^T  (one 32x32x64 MFMA per 32-key tile and 64 dims; Q quantised in registers
+//     once per query block with one scale per (query, 32 dims), pre-scaled by log2(e)/sqrt(hd)),
+//     online softmax in f32,
+//     O^T += V^T P^T  (P^T is the two S^T accumulators converted to e4m3 in place: lane half hh, element
+//     j = 16t + r <-> key 32t + acc_row(r, hh); the V^T image holds the same keys at byte 32hh + j).
+//     P is kept as P * 2^8 (exp2(s - m + 8): [0, 256], inside e4m3's range, small values stay normal)
+//     and the row sum l in the same units, so O = sum(P V) / l needs no extra scale.
+//
+// Operand layout of the 32x32x64 scaled MFMA, measured on the box (tools/micro/fp8_probe.hip): A lane l
+// holds row l&31, B lane l column l&31; byte j of lane half h meets byte j of the other operand's lane
+// half h (so any k assignment that agrees between A and B is a valid product); the e8m0 scale operand
+// of lane half h covers k-block h = bytes [16h, 16h+16) of BOTH half-lanes of its row / column.  So a
+// row's 64 k-elements sit as: half 0 = dims 0-15 | 32-47, half 1 = dims 16-31 | 48-63, and lane half h
+// supplies the scale of dims 32h .. 32h+31.
+#include "common.h"
+
+namespace ot {
+
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+namespace fp8 {
+
+__device__ __forceinline__ int acc_row(int r, int hh) { return (r & 3) + 8 * (r >> 2) + 4 * hh; }
+
+// scale exponent for a block with max |x| = amax: x * 2^-e lands in [-256, 256) (e4m3 max 448);
+// e8m0 byte = e + 127.  amax = 0 -> the smallest scale (the block is zeros anyway).
+__device__ __forceinline__ int block_exp(float amax) {
+  const int E = (int)((__float_as_uint(amax) >> 23) & 0xff) - 127;   // amax in [2^E, 2^(E+1))
+  int e = E - 7;
+  e = e < -120 ? -120 : (e > 120 ? 120 : e);
+  return e;
+}
+__device__ __forceinline__ float pow2f(int e) { return __uint_as_float((uint32_t)(127 + e) << 23); }
+
+// 4 floats -> 4 e4m3 bytes (element 0 in the low byte)
+__device__ __forceinline__ uint32_t pack4(float a, float b, float c, float d) {
+  int v = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  v = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, v, true);
+  return (uint32_t)v;
+}
+
+__device__ __forceinline__ f32x16 mfma_fp8(const i32x8& a, const i32x8& b, f32x16 c, int sa, int sb) {
+  return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 0, 0, 0, sa, 0, sb);
+}
+
+// 16 bytes at p (operand bytes 0-15) and 16 at p + gap (bytes 16-31)
+__device__ __forceinline__ i32x8 load32(const uint8_t* p, int gap = 16) {
+  const i32x4 lo = *reinterpret_cast<const i32x4*>(p);
+  const i32x4 hi = *reinterpret_cast<const i32x4*>(p + gap);
+  return i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+}
+
+}  // namespace fp8
+
+// Workspace of one call (all u8), Ip = I rounded up to 64 keys:
+//   k8 [BH][Ip][HD]   ks [BH][Ip][HD/32]   vt8 [BH][HD][Ip]   vs [BH][Ip/64][HD]
+struct Fp8Pack {
+  uint8_t *k8, *ks, *vt8, *vs;
+};
+
+__host__ __device__ inline int64_t fp8_ipad(int I) { return ((int64_t)I + 63) / 64 * 64; }
+
+inline Fp8Pack fp8_pack_layout(void* ws, int64_t BH, int I, int HD) {
+  const int64_t Ip = fp8_ipad(I);
+  uint8_t* p = static_cast<uint8_t*>(ws);
+  Fp8Pack f;
+  f.k8 = p;  p += BH * Ip * HD;
+  f.vt8 = p; p += BH * Ip * HD;
+  f.ks = p;  p += BH * Ip * (HD / 32);
+  f.vs = p;
+  return f;
+}
+
+inline size_t fp8_pack_bytes(int64_t BH, int I, int HD) {
+  const int64_t Ip = fp8_ipad(I);
+  return (size_t)(BH * Ip * HD * 2 + BH * Ip * (HD / 32) + BH * (Ip / 64) * HD);
+}
+
+// grid (Ip/64, B*H), 256 threads.  Keys >= I are zeros (the causal mask removes them).
+template <int HD>
+__global__ __launch_bounds__(256) void attn_fp8_pack_kernel(const float* __restrict__ qkv, int64_t ld, int H, int I,
+                                                            Fp8Pack f) {
+  constexpr int VLD = HD + 1;
+  __shared__ float vs_f[64 * VLD];
+  __shared__ __attribute__((aligned(16))) uint8_t vt_img[HD * 64];
+  const int kb = blockIdx.x, bh = blockIdx.y;
+  const int b = bh / H, h = bh % H, d = H * HD;
+  const int64_t Ip = fp8_ipad(I);
+  const int t = threadIdx.x;
+  const float* base = qkv + (int64_t)b * I * ld + h * HD;
+
+  // ---- K: thread = (key, 16 dims); a 32-dim scale block = 2 adjacent lanes
+  constexpr int TPK = HD / 16, KPP = 256 / TPK;
+#pragma unroll
+  for (int pass = 0; pass < 64 / KPP; ++pass) {
+    const int kk = pass * KPP + t / TPK, part = t % TPK;
+    const int key = 64 * kb + kk;
+    float x[16];
+    if (key < I) {
+      const float* src = base + (int64_t)key * ld + d + 16 * part;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(src + 4 * q);
+        x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) x[j] = 0.f;
+    }
+    float am = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) am = fmaxf(am, fabsf(x[j]));
+    am = fmaxf(am, __shfl_xor(am, 1, 64));
+    const int e = fp8::block_exp(am);
+    const float inv = fp8::pow2f(-e);
+    i32x4 o;
+    o.x = (int)fp8::pack4(x[0] * inv, x[1] * inv, x[2] * inv, x[3] * inv);
+    o.y = (int)fp8::pack4(x[4] * inv, x[5] * inv, x[6] * inv, x[7] * inv);
+    o.z = (int)fp8::pack4(x[8] * inv, x[9] * inv, x[10] * inv, x[11] * inv);
+    o.w = (int)fp8::pack4(x[12] * inv, x[13] * inv, x[14] * inv, x[15] * inv);
+    const int64_t row = (int64_t)bh * Ip + key;
+    *reinterpret_cast<i32x4*>(f.k8 + row * HD + 16 * part) = o;
+    if ((part & 1) == 0) f.ks[row * (HD / 32) + part / 2] = (uint8_t)(e + 127);
+  }
+
+  // ---- V: stage the [64 keys][HD] tile, then thread = (dim, KPT keys)
+  for (int i = t; i < 64 * HD / 4; i += 256) {
+    const int kk = i / (HD / 4), c4 = i % (HD / 4);
+    const int key = 64 * kb + kk;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (key < I) v = *reinterpret_cast<const f32x4*>(base + (int64_t)key * ld + 2 * d + 4 * c4);
+    float* dst = vs_f + kk * VLD + 4 * c4;
+    dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
+  }
+  __syncthreads();
+  constexpr int G = 256 / HD, KPT = 64 / G;       // threads per dim, keys per thread
+  {
+    const int c = t / G, g = t % G;
+    float am = 0.f;
+#pragma unroll
+    for (int i = 0; i < KPT; ++i) am = fmaxf(am, fabsf(vs_f[(g * KPT + i) * VLD + c]));
+#pragma unroll
+    for (int o = 1; o < G; o <<= 1) am = fmaxf(am, __shfl_xor(am, o, 64));
+    const int e = fp8::block_exp(am);
+    const float inv = fp8::pow2f(-e);
+#pragma unroll
+    for (int i = 0; i < KPT; i += 2) {
+      const int k0 = g * KPT + i;
+      const int v2 = __builtin_amdgcn_cvt_pk_fp8_f32(vs_f[k0 * VLD + c] * inv, vs_f[(k0 + 1) * VLD + c] * inv, 0, false);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int k = k0 + u, kk = k & 31;
+        // key k of the block sits at byte 32 hh + 16 t + (kk & 3) + 4 (kk >> 3) of the P order
+        const int pos = 32 * ((kk >> 2) & 1) + 16 * (k >> 5) + (kk & 3) + 4 * (kk >> 3);
+        vt_img[c * 64 + pos] = (uint8_t)((v2 >> (8 * u)) & 0xff);
+      }
+    }
+    if (g == 0) f.vs[((int64_t)bh * (Ip / 64) + kb) * HD + c] = (uint8_t)(e + 127);
+  }
+  __syncthreads();
+  for (int i = t; i < HD * 4; i += 256) {
+    const int c = i / 4, q = i % 4;
+    *reinterpret_cast<i32x4*>(f.vt8 + ((int64_t)bh * HD + c) * Ip + 64 * kb + 16 * q) =
+        *reinterpret_cast<const i32x4*>(vt_img + c * 64 + 16 * q);
+  }
+}
+
+struct Fp8AttnArgs {
+  const float* qkv; int64_t ld; int d;
+  float* out; float* lse;
+  int B, H, I, K;
+  float scale;
+  const int32_t* qpos;
+  Fp8Pack f;
+};
+
+// one wave per (b, h), 4 waves per block
+template <int HD>
+__global__ __launch_bounds__(256) void attn_fwd_fp8_kernel(Fp8AttnArgs p) {
+  static_assert(HD == 64 || HD == 128, "fp8 attention: head_dim 64 or 128");
+  constexpr int NKS = HD / 64;                   // 64-dim k steps of S^T
+  constexpr int NC = HD / 32;                    // 32-dim output chunks
+  const int lane = threadIdx.x & 63, li = lane & 31, hh = lane >> 5;
+  const int pair = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (pair >= p.B * p.H) return;
+  const int b = pair / p.H, h = pair % p.H;
+  const int I = p.I, K = p.K, q_off = I - K;
+  const int64_t Ip = fp8_ipad(I);
+  const float* Q = p.qkv + (int64_t)b * I * p.ld + h * HD;
+  const uint8_t* k8 = p.f.k8 + (int64_t)pair * Ip * HD + 16 * hh;
+  const uint8_t* ksc = p.f.ks + (int64_t)pair * Ip * (HD / 32) + hh;
+  const uint8_t* vt8 = p.f.vt8 + (int64_t)pair * HD * Ip + 32 * hh;
+  const uint8_t* vsc = p.f.vs + (int64_t)pair * (Ip / 64) * HD;
+  const int32_t* qp = p.qpos ? p.qpos + (int64_t)b * K : nullptr;
+  const int nqb = (K + 31) / 32;
+  const float qscale = p.scale * 1.4426950408889634f;   // log2(e) / sqrt(hd)
+
+  for (int qb = 0; qb < nqb; ++qb) {
+    const int j = 32 * qb + li;
+    const int jc = j < K ? j : K - 1;
+    const int qpos = qp ? qp[jc] : q_off + jc;
+    // Q fragment of k-step ks: bytes 0-15 = dims 64 ks + 16 hh .. +15 (k-block 0), bytes 16-31 =
+    // dims 64 ks + 32 + 16 hh .. +15 (k-block 1); each block's amax is completed across the two
+    // half-lanes, and lane half hh supplies block hh's scale
+    i32x8 qa[NKS];
+    int qs[NKS];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const float* src = Q + (int64_t)qpos * p.ld + 64 * ks + 16 * hh;
+      float x[32];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(src + 4 * (q & 3) + 32 * (q >> 2));
+        x[4 * q] = v.x * qscale; x[4 * q + 1] = v.y * qscale; x[4 * q + 2] = v.z * qscale; x[4 * q + 3] = v.w * qscale;
+      }
+      float am0 = 0.f, am1 = 0.f;
+#pragma unroll
+      for (int s = 0; s < 16; ++s) { am0 = fmaxf(am0, fabsf(x[s])); am1 = fmaxf(am1, fabsf(x[16 + s])); }
+      am0 = fmaxf(am0, __shfl_xor(am0, 32, 64));
+      am1 = fmaxf(am1, __shfl_xor(am1, 32, 64));
+      const int e0 = fp8::block_exp(am0), e1 = fp8::block_exp(am1);
+      const float inv0 = fp8::pow2f(-e0), inv1 = fp8::pow2f(-e1);
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        qa[ks][w] = (int)fp8::pack4(x[4 * w] * inv0, x[4 * w + 1] * inv0, x[4 * w + 2] * inv0, x[4 * w + 3] * inv0);
+        qa[ks][4 + w] = (int)fp8::pack4(x[16 + 4 * w] * inv1, x[17 + 4 * w] * inv1, x[18 + 4 * w] * inv1,
+                                        x[19 + 4 * w] * inv1);
+      }
+      qs[ks] = (hh ? e1 : e0) + 127;
+    }
+    f32x16 oacc[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) oacc[c][r] = 0.f;
+    float m = -INFINITY, l = 0.f;
+    const int last_q = qp ? qp[min(32 * qb + 31, K - 1)] : q_off + min(32 * qb + 31, K - 1);
+    const int nkb = last_q / 64 + 1;
+    const int first_masked = (qp ? qp[32 * qb] : q_off + 32 * qb) / 64;
+
+    // fragments of key block kb: K tiles t (keys 64 kb + 32 t + li), V^T chunks c (dims 32 c + li)
+    i32x8 kf[2][NKS], vf[NC];
+    int kscale[2][NKS], vscale[NC];
+    auto load_kv = [&](int kb, i32x8 (&kf_)[2][NKS], i32x8 (&vf_)[NC], int (&ksc_)[2][NKS], int (&vsc_)[NC]) {
+#pragma unroll
+      for (int t2 = 0; t2 < 2; ++t2) {
+        const int64_t key = 64 * kb + 32 * t2 + li;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+          kf_[t2][ks] = fp8::load32(k8 + key * HD + 64 * ks, 32);      // dims 16hh.. | 32+16hh..
+          ksc_[t2][ks] = ksc[key * (HD / 32) + 2 * ks];
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        vf_[c] = fp8::load32(vt8 + (int64_t)(32 * c + li) * Ip + 64 * kb);
+        vsc_[c] = vsc[(int64_t)kb * HD + 32 * c + li];
+      }
+    };
+    load_kv(0, kf, vf, kscale, vscale);
+    for (int kb = 0; kb < nkb; ++kb) {
+      i32x8 kn[2][NKS], vn[NC];
+      int kscn[2][NKS], vscn[NC];
+      load_kv(min(kb + 1, nkb - 1), kn, vn, kscn, vscn);   // unconditional: the wait before this block's
+                                                              // MFMAs can leave the prefetch in flight
+      f32x16 s[2];
+#pragma unroll
+      for (int t2 = 0; t2 < 2; ++t2) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[t2][r] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) s[t2] = fp8::mfma_fp8(kf[t2][ks], qa[ks], s[t2], kscale[t2][ks], qs[ks]);
+      }
+#ifdef OT_FP8_DEBUG
+      if (qb == 0 && kb == 0 && pair == 0) {
+        for (int t2 = 0; t2 < 2; ++t2)
+          for (int r = 0; r < 16; ++r) p.out[(32 * t2 + fp8::acc_row(r, hh)) * 32 + li] = s[t2][r];
+        if (li == 0) for (int ks = 0; ks < NKS; ++ks) p.out[4096 + hh] = (float)qs[ks];
+        p.out[4100 + lane] = (float)kscale[0][0];
+        return;
+      }
+#endif
+      if (kb >= first_masked) {
+#pragma unroll
+        for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            s[t2][r] = (64 * kb + 32 * t2 + fp8::acc_row(r, hh) <= qpos) ? s[t2][r] : -INFINITY;
+      }
+      float mloc = s[0][0];
+#pragma unroll
+      for (int r = 1; r < 16; ++r) mloc = fmaxf(mloc, s[0][r]);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mloc = fmaxf(mloc, s[1][r]);
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+      const float mnew = fmaxf(m, mloc);
+      const float corr = __builtin_amdgcn_exp2f(m - mnew);
+      const float moff = mnew - 8.f;                  // P * 2^8
+      float lsum = 0.f;
+#pragma unroll
+      for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float e = __builtin_amdgcn_exp2f(s[t2][r] - moff);
+          s[t2][r] = e;
+          lsum += e;
+        }
+      lsum += __shfl_xor(lsum, 32, 64);
+      l = l * corr + lsum;
+      m = mnew;
+      i32x8 pb;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        const int t2 = w >> 2, r = 4 * (w & 3);
+        pb[w] = (int)fp8::pack4(s[t2][r], s[t2][r + 1], s[t2][r + 2], s[t2][r + 3]);
+      }
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        oacc[c] *= corr;
+        oacc[c] = fp8::mfma_fp8(vf[c], pb, oacc[c], vscale[c], 127);   // O^T += V^T P^T
+      }
+#pragma unroll
+      for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) { kf[t2][ks] = kn[t2][ks]; kscale[t2][ks] = kscn[t2][ks]; }
+#pragma unroll
+      for (int c = 0; c < NC; ++c) { vf[c] = vn[c]; vscale[c] = vscn[c]; }
+    }
+    if (j < K) {
+      const float inv = 1.f / l;
+      float* orow = p.out + ((int64_t)b * K + j) * p.d + h * HD;
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int dd = 32 * c + 8 * g + 4 * hh;
+          f32x4 v = {oacc[c][4 * g] * inv, oacc[c][4 * g + 1] * inv, oacc[c][4 * g + 2] * inv,
+                     oacc[c][4 * g + 3] * inv};
+          *reinterpret_cast<f32x4*>(orow + dd) = v;
+        }
+      // l is in units of 2^8 (P * 2^8): lse = ln(sum exp(s)) = (m - 8) ln 2 + ln(l)
+      if (hh == 0) p.lse[((int64_t)b * p.H + h) * K + j] = (m - 8.f) * 0.6931471805599453f + __logf(l);
+    }
+  }
+}
+
+}  // namespace ot
+
+using namespace ot;
+
+extern "C" size_t ot_attn_fwd_fp8_workspace_size(int B, int H, int I, int head_dim) {
+  if (B <= 0 || H <= 0 || I <= 0 || (head_dim != 64 && head_dim != 128)) return 0;
+  return fp8_pack_bytes((int64_t)B * H, I, head_dim);
+}
+
+extern "C" int ot_attn_fwd_fp8(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos,
+                               int head_dim, float* out, float* lse, void* workspace, size_t ws_bytes, void* stream) {
+  OT_REQUIRE(qkv && out && lse, "ot_attn_fwd_fp8: null operand");
+  OT_REQUIRE(B >= 0 && H > 0 && I > 0 && K > 0 && K <= I, "ot_attn_fwd_fp8: bad sizes B=%d H=%d I=%d K=%d", B, H, I, K);
+  OT_REQUIRE(head_dim == 64 || head_dim == 128, "ot_attn_fwd_fp8: head_dim %d (64 or 128)", head_dim);
+  OT_REQUIRE(ld % 4 == 0 && ld >= 3 * H * head_dim, "ot_attn_fwd_fp8: ld must be >= 3d and a multiple of 4");
+  if (B == 0) return OT_OK;
+  OT_REQUIRE(workspace && ws_bytes >= ot_attn_fwd_fp8_workspace_size(B, H, I, head_dim) &&
+             ((uintptr_t)workspace % 16) == 0, "ot_attn_fwd_fp8: workspace");
+  const int64_t BH = (int64_t)B * H;
+  const Fp8Pack f = fp8_pack_layout(workspace, BH, I, head_dim);
+  OT_REQUIRE(BH <= 65535, "ot_attn_fwd_fp8: B*H = %lld > 65535", (long long)BH);
+  const dim3 pg((unsigned)(fp8_ipad(I) / 64), (unsigned)BH);
+  hipStream_t s = (hipStream_t)stream;
+  if (head_dim == 64) hipLaunchKernelGGL(attn_fp8_pack_kernel<64>, pg, dim3(256), 0, s, qkv, ld, H, I, f);
+  else hipLaunchKernelGGL(attn_fp8_pack_kernel<128>, pg, dim3(256), 0, s, qkv, ld, H, I, f);
+  OT_LAUNCH_CHECK("ot_attn_fwd_fp8(pack)");
+  Fp8AttnArgs p{qkv, ld, H * head_dim, out, lse, B, H, I, K, 1.f / sqrtf((float)head_dim), qpos, f};
+  const unsigned grid = ceil_div(BH, 4);
+  if (head_dim == 64) hipLaunchKernelGGL(attn_fwd_fp8_kernel<64>, dim3(grid), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(attn_fwd_fp8_kernel<128>, dim3(grid), dim3(256), 0, s, p);
+  OT_LAUNCH_CHECK("ot_attn_fwd_fp8");
+  return OT_OK;
+}

@@ -202,11 +202,20 @@ def split_images(base, desc_dev, ndesc, total_units, img) -> None:
 
 
 def attn_fwd(qkv: torch.Tensor, ld: int, B: int, H: int, I: int, K: int, hd: int, out: torch.Tensor,
-             lse: torch.Tensor, qpos: Optional[torch.Tensor] = None) -> None:
+             lse: torch.Tensor, qpos: Optional[torch.Tensor] = None, fp8: bool = False) -> None:
+    """ot_attn_fwd, or with ``fp8`` (head_dim 64/128) ot_attn_fwd_fp8: QK^T and PV on block-scaled fp8 MFMA."""
+    ws = None
+    if fp8:
+        ws = workspace(size('ot_attn_fwd_fp8_workspace_size', B, H, I, hd), qkv.device)
     ev = _probe.begin() if _probe is not None else None
-    call('ot_attn_fwd', ptr(qkv), ld, B, H, I, K, ptr(qpos), hd, ptr(out), ptr(lse), stream())
+    if fp8:
+        call('ot_attn_fwd_fp8', ptr(qkv), ld, B, H, I, K, ptr(qpos), hd, ptr(out), ptr(lse), ptr(ws), ws.numel(),
+             stream())
+    else:
+        call('ot_attn_fwd', ptr(qkv), ld, B, H, I, K, ptr(qpos), hd, ptr(out), ptr(lse), stream())
     if ev is not None:
-        _probe.end('attention', 4.0 * (K * I - K * (K - 1) / 2) * hd * H * B, ev, f'fwd I{I} K{K} hd{hd}')
+        _probe.end('attention', 4.0 * (K * I - K * (K - 1) / 2) * hd * H * B, ev,
+                   f'fwd{"_fp8" if fp8 else ""} I{I} K{K} hd{hd}')
 
 
 def attn_bwd(qkv, ld, out, dout, lse, B, H, I, K, hd, dqkv, qpos=None) -> None:

@@ -185,7 +185,7 @@ class _Block(torch.autograd.Function):
                    bimg=m.bimg(f'blk.{l}.wqkv'))
         o = torch.empty(B * Kq, d, device=dev)
         lse = torch.empty(B * H * Kq, device=dev)
-        K.attn_fwd(qkv, 3 * d, B, H, I, Kq, hd, o, lse, qpos=pos)
+        K.attn_fwd(qkv, 3 * d, B, H, I, Kq, hd, o, lse, qpos=pos, fp8=m.attn_fp8)
         # x1 = x[tail] + drop(o @ Wo)      (model.py:117, 193)
         x1 = torch.empty(B * Kq, d, device=dev)
         rstd2 = torch.empty(B * Kq, device=dev)
@@ -441,6 +441,16 @@ class OneTransModel(nn.Module):
         if cfg.hidden_dim % cfg.num_heads or (cfg.hidden_dim // cfg.num_heads) not in (16, 32, 64, 128):
             raise ValueError('head_dim must be 16, 32, 64 or 128')
         check_pyramid_select(cfg)
+        # compute_dtype (build knob): 'fp32' (the reference's arithmetic; GEMM precision is the process-wide
+        # ot_set_matmul_mode / ONETRANS_MATMUL), 'bf16', or 'fp8attn' = BASELINE configs[4]'s attention on
+        # block-scaled fp8 MFMA (forward QK^T and PV; the backward recomputes in the GEMM mode's precision).
+        # ONETRANS_ATTN=fp8 selects the fp8 forward too.
+        if getattr(cfg, 'compute_dtype', 'fp32') not in ('fp32', 'bf16', 'fp8attn'):
+            raise ValueError(f"compute_dtype {cfg.compute_dtype!r}: expected 'fp32', 'bf16' or 'fp8attn'")
+        self.attn_fp8 = (getattr(cfg, 'compute_dtype', 'fp32') == 'fp8attn'
+                         or os.environ.get('ONETRANS_ATTN', '') == 'fp8')
+        if self.attn_fp8 and cfg.hidden_dim // cfg.num_heads not in (64, 128):
+            raise ValueError('fp8 attention needs head_dim 64 or 128')
         # diagnostics only: ONETRANS_PYRAMID_KERNEL=0 addresses a 'tail' keep arithmetically instead of
         # through ot_pyramid_select's position map (same kept set; for A/B timing of the map plumbing)
         self.pyramid_kernel = os.environ.get('ONETRANS_PYRAMID_KERNEL', '1') != '0'
@@ -455,6 +465,7 @@ class OneTransModel(nn.Module):
         # rebuilt with the transposed shadow after every weight update.  ONETRANS_PLANE_GEMM=0: off
         self.use_plane = os.environ.get('ONETRANS_PLANE_GEMM', '1') != '0'
         self.img = torch.zeros(max(1, self.layout.image_elems), dtype=torch.int16, device=self.device)
+        self._img_valid = False
         self._idesc = (torch.from_numpy(self.layout.image_desc.reshape(-1)).to(self.device)
                        if self.layout.image_units else None)
         self.tables: Dict[str, torch.Tensor] = {}
@@ -507,9 +518,16 @@ class OneTransModel(nn.Module):
         """Re-derive the transposed weight banks after any change of the weights (init, load, optimizer)."""
         K.transpose_banks(self.flat.data, self.flatT, self._tdesc, self.layout.transpose_desc.shape[0],
                           self.layout.transpose_tiles)
-        if self._idesc is not None:
-            K.split_images(self.flat.data, self._idesc, self.layout.image_desc.shape[0], self.layout.image_units,
-                           self.img)
+        # the plane images only feed the split-mode GEMMs: in another matmul mode they are built lazily,
+        # if the mode is switched to split later (bimg)
+        self._img_valid = False
+        if self._idesc is not None and K.matmul_mode() == 'split':
+            self._build_images()
+
+    def _build_images(self) -> None:
+        K.split_images(self.flat.data, self._idesc, self.layout.image_desc.shape[0], self.layout.image_units,
+                       self.img)
+        self._img_valid = True
 
     def bimg(self, name: str, orient: str = 'fwd', tn0: int = 0):
         """(image, column tiles per group, first tile) of a weight bank's pre-split B image for the plane
@@ -520,6 +538,10 @@ class OneTransModel(nn.Module):
         e = self.layout.images.get((name, orient))
         if e is None:
             return None
+        if not self._img_valid:
+            if K.matmul_mode() != 'split':
+                return None
+            self._build_images()
         off, G, N, K_ = e
         return ((self.img, off), N // TILE, tn0)
 

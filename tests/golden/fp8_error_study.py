@@ -1,0 +1,64 @@
+"""Error study behind tests/test_fullsize_lowprec_gpu.py's fp8-attention bound (CPU, build container; test
+infrastructure): the float32 oracle forward of 12 C5 samples (the golden model init and batch) with the two
+attention products quantised as ot_attn_fwd_fp8 quantises them, and variants that keep one product in
+bf16.  Prints the max / mean logit change of each variant against the unquantised forward.
+
+Recorded (build container, 8 cores): fp8 0.0439 / 0.0184, K-smoothed fp8 0.0447 / 0.0169, QK^T bf16 +
+fp8 PV 0.0470 / 0.0174, fp8 QK^T + bf16 PV 0.0384 / 0.0111, bf16 attention 0.0031 / 0.0012."""
+import sys, math, time, os
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE))); sys.path.insert(0, os.path.dirname(HERE))
+import numpy as np, torch
+torch.set_num_threads(8)
+from fullsize_common import BATCH_SEED, MODEL_SEED, compact_problem, setup_config
+from oracle import onetrans_ref as R
+from recommend_amd.data import make_batch
+from recommend_amd.params import init_params
+E4 = torch.float8_e4m3fn
+def qrows(x, block):
+    sh = x.shape
+    xb = x.reshape(*sh[:-1], sh[-1] // block, block)
+    am = xb.abs().amax(-1, keepdim=True)
+    e = torch.where(am > 0, torch.floor(torch.log2(am)) - 7, torch.full_like(am, -120))
+    return ((xb * torch.exp2(-e)).to(E4).to(x.dtype) * torch.exp2(e)).reshape(sh)
+def bf(x): return x.to(torch.bfloat16).to(x.dtype)
+MODE = None
+orig = torch.einsum
+def ein(eq, *ops):
+    if MODE and eq == 'bqhd,bkhd->bhqk':
+        q, k = ops
+        if MODE in ('fp8', 'fp8_pbf16'): q, k = qrows(q, 32), qrows(k, 32)
+        elif MODE == 'smooth': k = k - k.mean(1, keepdim=True); q, k = qrows(q, 32), qrows(k, 32)
+        elif MODE in ('qkbf16', 'bf16'): q, k = bf(q), bf(k)
+        return orig(eq, q, k)
+    if MODE and eq == 'bhqk,bkhd->bqhd':
+        w, v = ops
+        if MODE in ('fp8', 'smooth', 'qkbf16'):
+            w = (w * 256).to(E4).to(w.dtype) / 256
+            B, I, H, hd = v.shape
+            Ip = (I + 63) // 64 * 64
+            vp = torch.zeros(B, Ip, H, hd, dtype=v.dtype); vp[:, :I] = v
+            v = qrows(vp.permute(0, 2, 3, 1).contiguous(), 64).permute(0, 3, 1, 2)[:, :I]
+        elif MODE in ('bf16', 'fp8_pbf16'):
+            w, v = bf(w), bf(v)
+        return orig(eq, w, v)
+    return orig(eq, *ops)
+torch.einsum = ein
+cfg = setup_config('C5')
+B = 12
+P = init_params(cfg, cfg.ns_input_width(), seed=MODEL_SEED, perturb=True, with_tables=False)
+batch = make_batch(512, cfg, seed=BATCH_SEED)
+ns, seq, lab = batch
+ns = {k: v[:B] for k, v in ns.items()}; seq = {k: v[:B] for k, v in seq.items()}
+ocfg, (ons, oseq, _), tables, _ = compact_problem(cfg, (ns, seq, lab))
+Pt = R.to_torch(dict(P, **tables), dtype=torch.float32)
+def run(mode):
+    global MODE
+    MODE = mode
+    with torch.no_grad():
+        out = R.forward(Pt, ocfg, R.to_torch(ons, dtype=torch.float32), R.to_torch(oseq, dtype=torch.float32), training=False)
+    return torch.stack([out['logits'][t].reshape(-1) for t in cfg.tasks])
+t0 = time.time(); ref = run(None); print('ref', time.time() - t0, flush=True)
+for m in ['fp8', 'smooth', 'qkbf16', 'fp8_pbf16', 'bf16']:
+    lg = run(m)
+    print(m, 'max |d logit|', float((lg - ref).abs().max()), 'mean', float((lg - ref).abs().mean()), flush=True)

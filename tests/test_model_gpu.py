@@ -208,11 +208,16 @@ def test_fused_norms_match_unfused(dev):
     assert (res[0][1] - res[1][1]).abs().max().item() / scale < 1e-5
 
 
-def test_bf16_mode_forward_and_train(dev):
+@pytest.mark.parametrize('dtype', ['bf16', 'fp8attn'])
+def test_bf16_mode_forward_and_train(dev, dtype):
     """OT_MATMUL_BF16 (C5's bf16 configuration; reduced precision, so a bf16 tolerance, not the f32
-    north_star bound): probabilities within 2e-2 of the f64 oracle, and training steps stay finite."""
+    north_star bound), alone and with the block-scaled fp8 attention forward ('fp8attn', head_dim 64):
+    probabilities within 2e-2 of the f64 oracle, and training steps (fp8 forward, bf16 backward) stay
+    finite."""
     from recommend_amd import kernels as K
-    cfg = small_criteo('tail', pyramid=True, layers=3, d=128, H=4, f=256, Lns=12, seq_lens=(20, 20, 20))
+    cfg = small_criteo('tail', pyramid=True, layers=3, d=128, H=2 if dtype == 'fp8attn' else 4, f=256, Lns=12,
+                       seq_lens=(20, 20, 20))
+    cfg.compute_dtype = dtype
     old = K.set_matmul_mode('bf16')
     try:
         P, model, batch = setup(cfg, 37, dev)

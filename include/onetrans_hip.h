@@ -55,7 +55,9 @@ extern "C" {
 #define OT_EPI_DROPOUT 8     /* counter-based mask, index (token, n) */
 #define OT_EPI_RESIDUAL 16   /* + res[res_tok ? token : out_row][n] */
 #define OT_EPI_ACCUMULATE 32 /* C += result */
-/* row-norm epilogues (ot_mixed_gemm_rms only; N == 128 so one tile holds whole output rows) */
+/* row-norm epilogues (ot_mixed_gemm_rms only): N == 128 (one tile holds whole output rows); OT_EPI_ROW_RSTD
+ * also N = 256, 384, ... on the plane GEMM (split mode, ot_mixed_gemm_rms_img; per-tile row sums of
+ * squares in the workspace, ot_mixed_gemm_rms_workspace_size(ntiles, N), then a finishing pass) */
 #define OT_EPI_ROW_RSTD 64      /* rstd_out[out_row] = 1/sqrt(mean_n(C[out_row]^2) + eps), C as above */
 #define OT_EPI_RMSNORM_BWD 128  /* the product is dL/dy of y = RMSNorm(x) * gamma: C = dL/dx (+ dres);
                                    with OT_EPI_DROPOUT also dx_masked = mask(C) (C itself unmasked) */

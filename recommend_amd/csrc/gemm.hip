@@ -73,11 +73,13 @@ struct GemmArgs {
   const float* aux; int64_t ldaux;
   uint32_t seed, site, drop_thr; float drop_scale; int tail_K, tail_I; int drop_width;
   int ntm, ntn;
-  // row-norm epilogues (N == GT: the tile holds whole rows)
+  // row-norm epilogues (N == GT: the tile holds whole rows; OT_EPI_ROW_RSTD also N > GT on the plane
+  // GEMM: per-tile row sums of squares in rowpart, finished by row_rstd_finish_kernel)
   float* rstd_out; float eps;                                   // OT_EPI_ROW_RSTD
   const float* nx; int64_t ldnx; const float* ngamma; const float* nrstd;   // OT_EPI_RMSNORM_BWD
   const float* dres; int64_t lddres; int dres_K, dres_I; const int32_t* dres_inv;
   float* dxm; int64_t lddxm; float* dgpart;
+  float* rowpart;                               // OT_EPI_ROW_RSTD with N > GT: [ntm*GT][ntn] row sums of squares
   const int32_t* tail_pos;                      // kept positions (ot_pyramid_select) or null (tail)
   // plane GEMM: pre-split B image (ot_split_images), its tiles per group and the first tile used
   const uint16_t* bimg; int bimg_ntn, bimg_tn0;
@@ -247,7 +249,15 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
           if (epi & OT_EPI_ACCUMULATE) v += cp4[i];
           if (ROWRSTD) {                                       // rstd of the finished row (next RMSNorm)
             const float ss = row32_sum(v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w);
-            if (orr >= 0 && c4 == 0) p.rstd_out[orr] = rsqrtf(ss / (float)p.N + p.eps);
+            if (p.rowpart) {                                   // N > GT: this tile's part of the row sum
+              if (c4 == 0) {
+                const int lr = rb + 8 * (i0 + i);
+                const int64_t gr = (int64_t)tm * GT + (LAYOUT == 0 ? (lr >> 5) * 64 + 32 * hf + (lr & 31) : 64 * hf + lr);
+                p.rowpart[gr * p.ntn + n0 / GT] = ss;
+              }
+            } else if (orr >= 0 && c4 == 0) {
+              p.rstd_out[orr] = rsqrtf(ss / (float)p.N + p.eps);
+            }
           }
           if (orr >= 0) *reinterpret_cast<f32x4*>(p.C + (int64_t)orr * p.ldc + col) = v;
         }
@@ -611,6 +621,20 @@ __global__ __launch_bounds__(256, (NT && SPLT) ? 2 : OT_GEMM_MINWG) void mixed_g
       }
     }
   }
+}
+
+// OT_EPI_ROW_RSTD with N > GT (plane GEMM): rstd_out[out_row] = rsqrt(sum of the row's ntn tile sums
+// of squares / N + eps), tile sums added in column order (deterministic); one thread per tile row.
+__global__ __launch_bounds__(256) void row_rstd_finish_kernel(const float* __restrict__ part, int ntn,
+                                                              const int32_t* __restrict__ out_rows, int64_t nrows,
+                                                              int N, float eps, float* rstd_out) {
+  const int64_t gr = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gr >= nrows) return;
+  const int orr = out_rows ? out_rows[gr] : (int)gr;
+  if (orr < 0) return;
+  float s = 0.f;
+  for (int j = 0; j < ntn; ++j) s += part[gr * ntn + j];
+  rstd_out[orr] = rsqrtf(s / (float)N + eps);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1263,7 +1287,10 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
   OT_REQUIRE(a_xform != OT_AX_RMSNORM || (a_rstd && a_gamma), "ot_mixed_gemm: rmsnorm prologue needs rstd/gamma");
   OT_REQUIRE(!((epi & OT_EPI_DROPOUT) || res_tok) || (tail_K > 0 && tail_I >= tail_K), "ot_mixed_gemm: bad tail map");
   if (rms_flags) {
-    OT_REQUIRE(mode == OT_GEMM_NT && N == GT, "ot_mixed_gemm_rms: row-norm epilogues need NT mode and N == %d", GT);
+    OT_REQUIRE(mode == OT_GEMM_NT && (N == GT || (!(epi & OT_EPI_RMSNORM_BWD) && N % GT == 0)),
+               "ot_mixed_gemm_rms: row-norm epilogues need NT mode and N == %d (OT_EPI_ROW_RSTD: N %% %d == 0)", GT, GT);
+    OT_REQUIRE(N == GT || (rms->workspace && rms->ws_bytes >= ot_mixed_gemm_rms_workspace_size(ntiles, N)),
+               "ot_mixed_gemm_rms: OT_EPI_ROW_RSTD with N > %d needs the workspace", GT);
     OT_REQUIRE(!(epi & OT_EPI_ROW_RSTD) || rms->rstd_out, "ot_mixed_gemm_rms: rstd_out missing");
     OT_REQUIRE(!(epi & OT_EPI_RMSNORM_BWD) || (rms->x && rms->gamma && rms->rstd && rms->ldx % 4 == 0),
                "ot_mixed_gemm_rms: RMSNorm backward needs x / gamma / rstd");
@@ -1288,6 +1315,7 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
     p.dres = rms->dres; p.lddres = rms->lddres; p.dres_K = rms->dres_tail_K; p.dres_I = rms->dres_tail_I;
     p.dres_inv = rms->dres_tail_inv;
     p.dxm = rms->dx_masked; p.lddxm = rms->lddxm;
+    if ((epi & OT_EPI_ROW_RSTD) && N > GT) p.rowpart = (float*)rms->workspace;
     if (epi & OT_EPI_RMSNORM_BWD) {
       // without dgamma the partials still need a home: the caller's workspace or nothing
       dgpart = rms->dgamma ? (float*)rms->workspace : nullptr;
@@ -1363,6 +1391,8 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
 #undef OT_PSPEC
     if (pk) { kern = pk; plane = true; }
   }
+  OT_REQUIRE(!p.rowpart || plane, "ot_mixed_gemm_rms: OT_EPI_ROW_RSTD with N = %d > %d needs the plane GEMM "
+             "(split mode, a pre-split B image, 16-B aligned A)", N, GT);
   const size_t launch_shmem = plane ? (size_t)(g_plane_cfg == 0 ? 3 : 2) * PG_STG_BYTES : shmem;
   OT_REQUIRE(kern || !rms_flags, "ot_mixed_gemm_rms: no specialised kernel for epilogue flags %d", epi);
   if (!kern) {   // any other combination: generic instantiation (run-time prologue/epilogue)
@@ -1391,6 +1421,12 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
   if (dgpart) {
     launch_colsum_reduce(dgpart, ntiles, N, rms->dgamma, rms->accumulate_dgamma, s, dgpart + (int64_t)ntiles * N);
     OT_LAUNCH_CHECK("ot_mixed_gemm_rms(dgamma)");
+  }
+  if (p.rowpart) {
+    const int64_t nr = (int64_t)ntiles * GT;
+    hipLaunchKernelGGL(row_rstd_finish_kernel, dim3(ceil_div(nr, 256)), dim3(256), 0, s, p.rowpart, p.ntn, out_rows,
+                       nr, N, rms->eps, rms->rstd_out);
+    OT_LAUNCH_CHECK("ot_mixed_gemm_rms(rstd)");
   }
   return OT_OK;
 }

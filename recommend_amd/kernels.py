@@ -150,7 +150,8 @@ def gemm_rms(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish,
              dgamma: Ptrish = None, accumulate_dgamma: bool = False, device=None, bimg=None) -> None:
     """ot_mixed_gemm_rms: the GEMM with a row-norm epilogue (OT_EPI_ROW_RSTD: emit the next RMSNorm's
     rstd; OT_EPI_RMSNORM_BWD: apply the RMSNorm backward to the product, + dres, dgamma)."""
-    ws = workspace(size('ot_mixed_gemm_rms_workspace_size', ntiles, N) if dgamma is not None else 16,
+    need_ws = dgamma is not None or (rstd_out is not None and N > 128)     # dgamma / row-sum partials
+    ws = workspace(size('ot_mixed_gemm_rms_workspace_size', ntiles, N) if need_ws else 16,
                    device if device is not None else (C[0] if isinstance(C, tuple) else C).device)
     e = _lib.RmsEpilogue(ptr(rstd_out), float(eps), ptr(nx), ldnx, ptr(ngamma), ptr(nrstd), ptr(dres), lddres,
                          dres_tail[0], dres_tail[1], _sel(dres_tail), ptr(dx_masked), lddxm, ptr(dgamma),

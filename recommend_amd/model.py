@@ -148,7 +148,7 @@ class _Block(torch.autograd.Function):
         wqkv, wo = m.pT(f'blk.{l}.wqkv'), m.pT(f'blk.{l}.wo')          # transposed shadow: [G][N][K]
         w1, b1, w2, b2 = m.pT(f'blk.{l}.w1'), m.p(f'blk.{l}.b1'), m.pT(f'blk.{l}.w2'), m.p(f'blk.{l}.b2')
         g1, g2 = m.p(f'blk.{l}.norm1'), m.p(f'blk.{l}.norm2')
-        fuse = m.fuse_norms
+        fuse = m.fuse_with((f'blk.{l}.wo', 'fwd'), (f'blk.{l}.w2', 'fwd'))
         # norm1 -> rstd only; the QKV GEMM applies it in its A prologue
         if rstd_in is not None and rstd_in.numel() == B * I:
             rstd1 = rstd_in
@@ -267,7 +267,7 @@ class _Block(torch.autograd.Function):
         # FFN1 dgrad -> norm2 backward + residual; emit mask(dx1) for the attention branch
         dx1 = torch.empty(B * Kq, d, device=dev)
         dyo = torch.empty(B * Kq, d, device=dev) if rate > 0 else dx1
-        if m.fuse_norms:
+        if m.fuse_bwd:         # FFN1 dgrad -> norm2 backward in the epilogue (d == 128: the tile holds whole rows)
             K.gemm_rms(OT_GEMM_NT, du, f, f, mt['rows'][1], m.p(f'blk.{l}.w1'), d * f, f, d, mt['tile_group'], nt,
                        dx1, d, mt['rows'][1], epi=OT_EPI_RMSNORM_BWD | (OT_EPI_DROPOUT if rate > 0 else 0),
                        seed=seed, site=2 * l, drop=rate, tail=tail, m_rows=maps['tail'].nrows, nx=x1, ldnx=d,
@@ -297,7 +297,7 @@ class _Block(torch.autograd.Function):
                     3 * d * d, None, 0, a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=m.p(f'blk.{l}.norm1'),
                     accumulate=acc, device=dev, m_rows=maps['all'].nrows, rowmap=maps['all'])
         dx = torch.empty(B * I, d, device=dev)
-        if m.fuse_norms:       # QKV dgrad -> norm1 backward + residual (dx1 on the kept tail rows)
+        if m.fuse_bwd:         # QKV dgrad -> norm1 backward + residual (dx1 on the kept tail rows)
             K.gemm_rms(OT_GEMM_NT, dqkv, 3 * d, 3 * d, ma['rows'][0], m.p(f'blk.{l}.wqkv'), 3 * d * d, 3 * d, d,
                        ma['tile_group'], na, dx, d, ma['rows'][0], epi=OT_EPI_RMSNORM_BWD,
                        m_rows=maps['all'].nrows, nx=x, ldnx=d, ngamma=m.p(f'blk.{l}.norm1'), nrstd=rstd1,
@@ -473,8 +473,14 @@ class OneTransModel(nn.Module):
         # data-parallel hook (OneTransOptimizer): called with a layer index / 'head' when those gradient
         # banks are final in backward, so their all-reduce overlaps the rest of the backward pass
         self.grad_ready = None
-        # fuse the RMSNorms into the neighbouring GEMM epilogues when a tile holds whole rows
-        self.fuse_norms = (config.hidden_dim == TILE and os.environ.get('ONETRANS_FUSE_NORMS', '1') != '0')
+        # fuse the RMSNorms into the neighbouring GEMM epilogues.  d == 128 (a tile holds whole rows, every
+        # matmul mode): the forward rstd (Wo / FFN2 epilogues) and the norm backward (FFN1 / QKV dgrad
+        # epilogues).  d = 256, 512, ...: the forward rstd only, on the split-mode plane GEMM (per-tile row
+        # sums + a finishing pass, ``fuse_with``); the norm backward stays row-wise there — a row-complete
+        # epilogue (each workgroup looping over the row's column tiles, two passes) measured slower than
+        # the row-wise kernel at T
+        self.fuse_norms = (config.hidden_dim % TILE == 0 and os.environ.get('ONETRANS_FUSE_NORMS', '1') != '0')
+        self.fuse_bwd = self.fuse_norms and config.hidden_dim == TILE
         # block weight gradients run on a second stream, overlapping the dgrad chain
         self.overlap_wgrad = os.environ.get('ONETRANS_OVERLAP_WGRAD', '1') != '0'
         self._side = None
@@ -528,6 +534,16 @@ class OneTransModel(nn.Module):
         K.split_images(self.flat.data, self._idesc, self.layout.image_desc.shape[0], self.layout.image_units,
                        self.img)
         self._img_valid = True
+
+    def fuse_with(self, *images) -> bool:
+        """Run the forward row-norm epilogue (OT_EPI_ROW_RSTD) on GEMMs whose B operands are ``images``
+        ((bank, orient) pairs)?  d == 128: always (when fusing is on); d > 128: only on the plane GEMM
+        (split mode, every image present)."""
+        if not self.fuse_norms:
+            return False
+        if self.config.hidden_dim == TILE:
+            return True
+        return all(self.bimg(n, o) is not None for (n, o) in images)
 
     def bimg(self, name: str, orient: str = 'fwd', tn0: int = 0):
         """(image, column tiles per group, first tile) of a weight bank's pre-split B image for the plane

@@ -56,6 +56,9 @@ CASES = {
     # d = 256 (hd 64, as T/C3/C5): weights of >= 8 output tiles take the larger wgrad chunk budget
     'criteo_d256_pyramid': lambda: small_criteo('tail', pyramid=True, layers=2, d=256, H=4, f=1024, Lns=4,
                                                 seq_lens=(12, 9, 7)),
+    # d = 512 (C5's width, hd 64): the row-complete plane GEMM's norm epilogues span 4 column tiles
+    'criteo_d512_pyramid': lambda: small_criteo('tail', pyramid=True, layers=2, d=512, H=8, f=1024, Lns=4,
+                                                seq_lens=(12, 9, 7)),
 }
 
 
@@ -97,7 +100,7 @@ def ns_t(d, dev):
 
 @pytest.mark.parametrize('case', ['c1_head', 'criteo_head', 'criteo_tail_pyramid', 'criteo_d128_hd32',
                                   'criteo_d128_pyramid', 'criteo_norm_pyramid', 'criteo_d128_norm_pyramid',
-                                  'criteo_d256_pyramid'])
+                                  'criteo_d256_pyramid', 'criteo_d512_pyramid'])
 @pytest.mark.parametrize('training', [False, True])
 def test_gradient_parity(dev, case, training):
     cfg = CASES[case]()
@@ -189,15 +192,22 @@ def test_auc_parity(dev):
         assert abs(a - b) < 1e-3, (t, a, b)
 
 
-def test_fused_norms_match_unfused(dev):
-    """d == 128: the GEMM-epilogue RMSNorms give the same loss and gradients as the row-wise kernels."""
-    cfg = CASES['criteo_d128_pyramid']()
-    P, model, batch = setup(cfg, 41, dev)
+@pytest.mark.parametrize('case,B', [('criteo_d128_pyramid', 41), ('criteo_d256_pyramid', 41),
+                                    ('criteo_d512_pyramid', 23), ('criteo_d256_pyramid', 129)])
+def test_fused_norms_match_unfused(dev, case, B):
+    """The GEMM-epilogue RMSNorms give the same loss and gradients as the row-wise kernels: d == 128 (one
+    tile holds whole rows: forward rstd and norm backward) and d = 256 / 512 (forward rstd from the plane
+    GEMM's per-tile row sums over 2 / 4 column tiles), dropout on, pyramid tail maps, and a batch one
+    row past whole tiles."""
+    cfg = CASES[case]()
+    P, model, batch = setup(cfg, B, dev)
+    assert model.fuse_with(('blk.0.wo', 'fwd'), ('blk.0.w2', 'fwd'))
     ns, seq, lab = batch
     y = stack_labels(lab, cfg.tasks, dev)
     res = []
     for fuse in (True, False):
         model.fuse_norms = fuse
+        model.fuse_bwd = fuse and cfg.hidden_dim == 128
         model.flat.grad.zero_()
         model._step = 0
         loss = keras_bce_loss(y, model.forward_probs(ns_t(ns, dev), ns_t(seq, dev), training=True))

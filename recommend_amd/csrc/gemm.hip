@@ -656,9 +656,17 @@ static_assert(64 * (GT + 4) * 4 + 8 * GT * 4 <= 2 * PG_STG_BYTES, "plane GEMM ep
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-template <int AXT, int EPIT, int NSTG, int MINW>
+// TERMS = 6: split mode (three planes, six products); TERMS = 1: OT_MATMUL_BF16 (plane 0 of the image
+// holds the weight rounded to nearest, A is rounded at fragment time, one product; only plane 0 is
+// copied, so a stage is 12 KiB instead of 20 KiB)
+template <int TERMS>
+constexpr int pg_stage_bytes() { return PG_A_BYTES + (TERMS == 1 ? GT * 16 * 2 : PG_B_BYTES); }
+
+template <int AXT, int EPIT, int NSTG, int MINW, int TERMS = 6>
 __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
   static_assert(NSTG == 2 || NSTG == 3, "plane GEMM stages");
+  static_assert(TERMS == 6 || TERMS == 1, "plane GEMM terms");
+  constexpr int STG = pg_stage_bytes<TERMS>();
   extern __shared__ __attribute__((aligned(16))) float smem[];
   char* lds = reinterpret_cast<char*>(smem);
   const int nwg = p.ntm * p.ntn;
@@ -686,19 +694,25 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
   // B: the (g, tile) image is nk consecutive 12-KiB stage blocks; wave w copies KiB 3w .. 3w+2 (a
   // weight shared by every group, w_gstride 0 like Wo, has one group's image)
   const int gb = p.w_gstride ? g : 0;
-  const char* bsrc = reinterpret_cast<const char*>(p.bimg) +
-                     ((int64_t)gb * p.bimg_ntn + p.bimg_tn0 + tn) * nk * PG_B_BYTES + (3 * wave) * 1024 + 16 * lane;
+  const char* bimg0 = reinterpret_cast<const char*>(p.bimg) + ((int64_t)gb * p.bimg_ntn + p.bimg_tn0 + tn) * nk * PG_B_BYTES;
+  const char* bsrc = bimg0 + (3 * wave) * 1024 + 16 * lane;
+  const char* bsrc1 = bimg0 + wave * 1024 + 16 * lane;
 
   auto issue = [&](int ks, int buf) {
-    char* sb = lds + buf * PG_STG_BYTES;
+    char* sb = lds + buf * STG;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
       __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + 16 * ks), (lds_void_t*)(sb + (2 * wave + i) * 1024),
                                        16, 0, 0);
+    if (TERMS == 1) {                                 // plane 0 only: wave w copies its KiB w
+      __builtin_amdgcn_global_load_lds((const void*)(bsrc1 + (int64_t)ks * PG_B_BYTES),
+                                       (lds_void_t*)(sb + PG_A_BYTES + wave * 1024), 16, 0, 0);
+    } else {
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(bsrc + (int64_t)ks * PG_B_BYTES + i * 1024),
-                                       (lds_void_t*)(sb + PG_A_BYTES + (3 * wave + i) * 1024), 16, 0, 0);
+      for (int i = 0; i < 3; ++i)
+        __builtin_amdgcn_global_load_lds((const void*)(bsrc + (int64_t)ks * PG_B_BYTES + i * 1024),
+                                         (lds_void_t*)(sb + PG_A_BYTES + (3 * wave + i) * 1024), 16, 0, 0);
+    }
   };
 
   f32x16 acc[4];
@@ -715,32 +729,37 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
   issue(0, 0);
   if (NSTG == 3 && nk > 1) issue(1, 1);
   for (int kt = 0; kt < nk; ++kt) {
-    // this wave's copies of stage kt are done (with 3 stages the 5 of stage kt+1 may still fly),
-    // every wave's after the barrier; the barrier also retires every read of the buffer that the
-    // copies of stage kt+NSTG-1 then overwrite (last read in iteration kt-1)
-    if (NSTG == 3 && kt + 1 < nk) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // this wave's copies of stage kt are done (with 3 stages the 5 (TERMS 1: 3) of stage kt+1 may
+    // still fly), every wave's after the barrier; the barrier also retires every read of the buffer
+    // that the copies of stage kt+NSTG-1 then overwrite (last read in iteration kt-1)
+    if (NSTG == 3 && kt + 1 < nk) {
+      if (TERMS == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (kt + NSTG - 1 < nk) issue(kt + NSTG - 1, (kt + NSTG - 1) % NSTG);
-    const char* sb = lds + (kt % NSTG) * PG_STG_BYTES;
+    const char* sb = lds + (kt % NSTG) * STG;
     f32x4 a0 = *reinterpret_cast<const f32x4*>(sb + aoff0);
     f32x4 a1 = *reinterpret_cast<const f32x4*>(sb + aoff1);
     u32x4 fb[4][3];
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb)
 #pragma unroll
-      for (int q = 0; q < 3; ++q) fb[nb][q] = *reinterpret_cast<const u32x4*>(sb + boff + q * 4096 + nb * 1024);
+      for (int q = 0; q < (TERMS == 1 ? 1 : 3); ++q)
+        fb[nb][q] = *reinterpret_cast<const u32x4*>(sb + boff + q * 4096 + nb * 1024);
     if (AXT == OT_AX_GELU) {
       a0.x = gelu_erf(a0.x); a0.y = gelu_erf(a0.y); a0.z = gelu_erf(a0.z); a0.w = gelu_erf(a0.w);
       a1.x = gelu_erf(a1.x); a1.y = gelu_erf(a1.y); a1.z = gelu_erf(a1.z); a1.w = gelu_erf(a1.w);
     }
     const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
     u32x4 fa[3];
-    split8(av, fa);
+    split8t<TERMS == 1 ? 1 : 6>(av, fa);
 #pragma unroll
-    for (int nb = 0; nb < 4; ++nb) acc[nb] = mfma_split6(fa, fb[nb], acc[nb]);
+    for (int nb = 0; nb < 4; ++nb) acc[nb] = mfma_terms<TERMS == 1 ? 1 : 6>(fa, fb[nb], acc[nb]);
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();                                    // the epilogue reuses the stage buffers
@@ -752,7 +771,7 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
 // (* kscale[k]); one unit = one (g, n tile, 16-k stage) block of 3 x 128 x 16 bf16, one thread per
 // (row n, 8-k half): split8 of the 8 values, each plane's 16 B at its swizzled half.
 __global__ __launch_bounds__(256) void split_images_kernel(const float* __restrict__ base, const int64_t* __restrict__ desc,
-                                                           int nd, uint16_t* img) {
+                                                           int nd, uint16_t* img, int one) {
   const int64_t unit = blockIdx.x;
   int b = 0;
   while (b + 1 < nd && desc[10 * (b + 1) + 6] <= unit) ++b;
@@ -776,11 +795,12 @@ __global__ __launch_bounds__(256) void split_images_kernel(const float* __restri
     v[j] = x;
   }
   u32x4 pl[3];
-  split8(v, pl);
+  if (one) split8t<1>(v, pl);                         // OT_MATMUL_BF16: plane 0 = round to nearest
+  else split8(v, pl);
   uint16_t* dst = img + d[5] + (unit - d[6]) * (PG_B_BYTES / 2);
 #pragma unroll
   for (int q = 0; q < 3; ++q)
-    *reinterpret_cast<u32x4*>(dst + q * GT * 16 + n * 16 + 8 * (hh ^ ((n >> 3) & 1))) = pl[q];
+    if (q == 0 || !one) *reinterpret_cast<u32x4*>(dst + q * GT * 16 + n * 16 + 8 * (hh ^ ((n >> 3) & 1))) = pl[q];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1366,12 +1386,14 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
   OT_SPEC(true, OT_AX_NONE, OT_EPI_RMSNORM_BWD | OT_EPI_DROPOUT)
 #undef OT_SPEC
   // plane GEMM: split mode, pre-split B image given, whole tiles, 16-B aligned A rows
-  if (bimg && split && !one && !edge && mode == OT_GEMM_NT && lda % 4 == 0 && a16(A)) {
+  if (bimg && split && !edge && mode == OT_GEMM_NT && lda % 4 == 0 && a16(A)) {
     OT_REQUIRE(bimg_ntn >= bimg_tn0 + (int)p.ntn && bimg_tn0 >= 0, "ot_mixed_gemm: B image has %d tiles per group, "
                "the GEMM needs %d from tile %d", bimg_ntn, (int)p.ntn, bimg_tn0);
     void (*pk)(GemmArgs) = nullptr;
 #define OT_PSPEC(AX_, EP_) \
-    if (x == AX_ && e == (EP_)) pk = g_plane_cfg == 0 ? plane_gemm_kernel<AX_, EP_, 3, 2> : plane_gemm_kernel<AX_, EP_, 2, 4>;
+    if (x == AX_ && e == (EP_)) \
+      pk = one ? plane_gemm_kernel<AX_, EP_, 3, 4, 1> \
+               : (g_plane_cfg == 0 ? plane_gemm_kernel<AX_, EP_, 3, 2> : plane_gemm_kernel<AX_, EP_, 2, 4>);
     OT_PSPEC(OT_AX_RMSNORM, 0)
     OT_PSPEC(OT_AX_RMSNORM, OT_EPI_BIAS)
     OT_PSPEC(OT_AX_GELU, OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_DROPOUT)
@@ -1393,7 +1415,9 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
   }
   OT_REQUIRE(!p.rowpart || plane, "ot_mixed_gemm_rms: OT_EPI_ROW_RSTD with N = %d > %d needs the plane GEMM "
              "(split mode, a pre-split B image, 16-B aligned A)", N, GT);
-  const size_t launch_shmem = plane ? (size_t)(g_plane_cfg == 0 ? 3 : 2) * PG_STG_BYTES : shmem;
+  const size_t launch_shmem = !plane ? shmem
+                              : one ? std::max((size_t)3 * pg_stage_bytes<1>(), (size_t)(64 * (GT + 4) + 8 * GT) * 4)
+                                    : (size_t)(g_plane_cfg == 0 ? 3 : 2) * PG_STG_BYTES;
   OT_REQUIRE(kern || !rms_flags, "ot_mixed_gemm_rms: no specialised kernel for epilogue flags %d", epi);
   if (!kern) {   // any other combination: generic instantiation (run-time prologue/epilogue)
     if (mode == OT_GEMM_NT && split && one)
@@ -1472,7 +1496,7 @@ extern "C" int ot_split_images(const float* base, const int64_t* desc_dev, int n
   OT_REQUIRE(base && desc_dev && img && ndesc > 0 && total_units >= 0, "ot_split_images: bad args");
   if (total_units == 0) return OT_OK;
   hipLaunchKernelGGL(split_images_kernel, dim3((unsigned)total_units), dim3(256), 0, (hipStream_t)stream, base,
-                     desc_dev, ndesc, img);
+                     desc_dev, ndesc, img, g_matmul_mode == OT_MATMUL_BF16 ? 1 : 0);
   OT_LAUNCH_CHECK("ot_split_images");
   return OT_OK;
 }

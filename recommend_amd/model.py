@@ -465,7 +465,7 @@ class OneTransModel(nn.Module):
         # rebuilt with the transposed shadow after every weight update.  ONETRANS_PLANE_GEMM=0: off
         self.use_plane = os.environ.get('ONETRANS_PLANE_GEMM', '1') != '0'
         self.img = torch.zeros(max(1, self.layout.image_elems), dtype=torch.int16, device=self.device)
-        self._img_valid = False
+        self._img_valid, self._img_mode = False, None
         self._idesc = (torch.from_numpy(self.layout.image_desc.reshape(-1)).to(self.device)
                        if self.layout.image_units else None)
         self.tables: Dict[str, torch.Tensor] = {}
@@ -524,16 +524,17 @@ class OneTransModel(nn.Module):
         """Re-derive the transposed weight banks after any change of the weights (init, load, optimizer)."""
         K.transpose_banks(self.flat.data, self.flatT, self._tdesc, self.layout.transpose_desc.shape[0],
                           self.layout.transpose_tiles)
-        # the plane images only feed the split-mode GEMMs: in another matmul mode they are built lazily,
-        # if the mode is switched to split later (bimg)
+        # the plane images feed the plane GEMMs of the split mode (three planes) and the bf16 mode (plane
+        # 0 rounded to nearest); built for the current matmul mode, rebuilt lazily if it changes (bimg)
         self._img_valid = False
-        if self._idesc is not None and K.matmul_mode() == 'split':
+        if self._idesc is not None and K.matmul_mode() in ('split', 'bf16'):
             self._build_images()
 
     def _build_images(self) -> None:
         K.split_images(self.flat.data, self._idesc, self.layout.image_desc.shape[0], self.layout.image_units,
                        self.img)
         self._img_valid = True
+        self._img_mode = K.matmul_mode()
 
     def fuse_with(self, *images) -> bool:
         """Run the forward row-norm epilogue (OT_EPI_ROW_RSTD) on GEMMs whose B operands are ``images``
@@ -554,9 +555,10 @@ class OneTransModel(nn.Module):
         e = self.layout.images.get((name, orient))
         if e is None:
             return None
-        if not self._img_valid:
-            if K.matmul_mode() != 'split':
-                return None
+        mode = K.matmul_mode()
+        if mode not in ('split', 'bf16'):
+            return None
+        if not self._img_valid or self._img_mode != mode:
             self._build_images()
         off, G, N, K_ = e
         return ((self.img, off), N // TILE, tn0)

@@ -46,6 +46,9 @@ def parse():
     ap.add_argument('--no-probe', action='store_true', help='skip the per-kernel HIP-event (roofline) pass')
     ap.add_argument('--probe-steps', type=int, default=10, help='steps of the roofline pass (0: no roofline)')
     ap.add_argument('--repeats', type=int, default=3, help='timed regions of --steps steps; value = median')
+    ap.add_argument('--no-overlap', action='store_true',
+                    help='weight gradients on the main stream for the whole run (rocprofv3 runs: every kernel '
+                         'standalone, so its trace durations compare with the roofline pass)')
     ap.add_argument('--precision', default='auto', choices=['auto', 'split', 'f32', 'bf16', 'fp8attn'],
                     help="GEMM / attention arithmetic.  auto: the config's stated precision — C5 (BASELINE "
                          "configs[4]) 'fp8attn' (bf16 GEMMs + block-scaled fp8 attention forward), every other "
@@ -168,6 +171,8 @@ def main():
     cfg.compute_dtype = {'fp8attn': 'fp8attn', 'bf16': 'bf16'}.get(precision, 'fp32')
     B = args.batch or cfg._batch
     model = OneTransModel(cfg, device=dev, seed=0)
+    if args.no_overlap:
+        model.overlap_wgrad = False
     trainer = OneTransTrainer(cfg, model=model)
     batches = device_batches(cfg, B, args.nbatches, rank, dev)
     torch.cuda.synchronize()
@@ -291,11 +296,12 @@ def main():
             # the GEMMs issue SPLIT_TERMS bf16 MFMA products per f32 product: their matrix-core
             # ceiling in f32 flops is the bf16 dense peak / SPLIT_TERMS
             gpeak = round(BF16_MFMA_PEAK_TFLOPS / SPLIT_TERMS, 1)
-            gkern = ('mixed_gemm_kernel + wgrad_split_kernel (f32 operands split exactly into 3 bf16 parts, '
-                     f'{SPLIT_TERMS} bf16 MFMA products per f32 product; peak = bf16 dense / {SPLIT_TERMS})')
+            gkern = ('plane_gemm_kernel / mixed_gemm_kernel + wgrad_split_kernel (f32 operands split exactly into '
+                     f'3 bf16 parts, {SPLIT_TERMS} bf16 MFMA products per f32 product; peak = bf16 dense / {SPLIT_TERMS})')
         elif K.matmul_mode() == 'bf16':
             gpeak = BF16_MFMA_PEAK_TFLOPS
-            gkern = 'mixed_gemm_kernel + wgrad_split_kernel (operands rounded to bf16, one bf16 MFMA product)'
+            gkern = ('plane_gemm_kernel / mixed_gemm_kernel + wgrad_split_kernel (operands rounded to bf16, one bf16 '
+                     'MFMA product)')
         else:
             gpeak = FP32_MFMA_PEAK_TFLOPS
             gkern = 'mixed_gemm_kernel + wgrad_kernel (native f32 MFMA)'

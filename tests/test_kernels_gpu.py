@@ -181,6 +181,44 @@ def test_wgrad(dev, matmul, xf):
         torch.testing.assert_close(db[g].double().cpu(), D[rows].sum(0), rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize('xf', [OT_AX_NONE, OT_AX_RMSNORM, OT_AX_GELU])
+@pytest.mark.parametrize('counts', [[1000, 300, 200], [5, 130, 1365]])
+def test_wgrad_bf16(dev, xf, counts):
+    """OT_MATMUL_BF16 weight gradient (C5's precision; 128-row LDS stages of four 32-row rounds, chunks
+    whose row counts are not multiples of 128): against float64 with the bf16 error bound — each
+    product of two bf16-rounded operands is within 2^-8 relative, so |dW - ref| <= 2^-7 sum |a||d|."""
+    old = K.set_matmul_mode('bf16')
+    try:
+        rng = np.random.default_rng(3)
+        G, K_, N = 3, 256, 384
+        M = sum(counts)
+        A = torch.randn(M, K_, dtype=torch.float64)
+        D = torch.randn(M, N, dtype=torch.float64)
+        gamma = 1 + 0.1 * torch.randn(K_, dtype=torch.float64)
+        rstd = 1.0 / torch.sqrt((A * A).mean(1) + 1e-6)
+        per, src, o = [], rng.permutation(M), 0
+        for g in range(G):
+            per.append([src[o:o + counts[g]], src[o:o + counts[g]]])
+            o += counts[g]
+        rm = build_map(per, chunk_rows=256)
+        dd = rm.to(dev)
+        dW = torch.full((G, K_, N), float('nan'), device=dev)
+        db = torch.full((G, N), float('nan'), device=dev)
+        K.wgrad(A.float().to(dev), K_, dd['rows'][0], D.float().to(dev), N, dd['rows'][1], K_, N, dd,
+                rm.chunks.shape[0], G, dW, K_ * N, db, N, a_xform=xf, rstd=rstd.float().to(dev),
+                gamma=gamma.float().to(dev), device=dev)
+        Ax = A * rstd[:, None] * gamma if xf == OT_AX_RMSNORM else (gelu64(A) if xf == OT_AX_GELU else A)
+        for g in range(G):
+            rows = torch.from_numpy(per[g][0]).long()
+            ref = Ax[rows].T @ D[rows]
+            bound = 2.0 ** -7 * (Ax[rows].abs().T @ D[rows].abs()) + 1e-6
+            err = (dW[g].double().cpu() - ref).abs()
+            assert bool((err <= bound).all()), float((err / bound).max())
+            torch.testing.assert_close(db[g].double().cpu(), D[rows].sum(0), rtol=1e-4, atol=1e-3)
+    finally:
+        K.set_matmul_mode(old)
+
+
 def attn_ref(qkv, B, H, I, Kq, hd):
     d = H * hd
     q = qkv[:, :d].reshape(B, I, H, hd)[:, I - Kq:]

@@ -12,6 +12,7 @@
 // Orientation: S^T = K Q^T puts the query on the MFMA column (lane) and keys in registers, so
 // P^T (registers) is directly the B operand of O^T = V^T P^T (the accumulator-as-operand idiom,
 // cdna_hip_programming.md §3) with the k index of step r = the key held in register r.
+#include <cstdlib>
 #include <mutex>
 
 #include "common.h"
@@ -564,36 +565,67 @@ template <int HD>
 constexpr int BWD_WAVES() { return HD >= 128 ? 2 : 4; }
 
 // SEL: queries at selected positions (p.qpos, padded copy in the workspace) instead of the tail.
-template <int HD, bool SEL>
-__global__ __launch_bounds__(64 * BWD_WAVES<HD>(), 2) void attn_bwd_kernel(AttnArgs p) {
+// DS = 2 (head_dim 2 HD, e.g. 64 as two waves of HD = 32): the two waves of a 128-thread block share
+// one (sample, head) and each owns half of its dims — half the dK / dV / dQ accumulators, fragments
+// and LDS tiles, so a wave has the HD = 32 kernel's footprint (2 waves / SIMD instead of 1).  S and dP
+// are sums over all dims: each wave computes its half's partial and the two partials are summed
+// through the wave's dS tile (an LDS exchange, four barriers per (key block, query block) pair); the
+// softmax gradient is then computed identically in both waves.
+template <int HD, bool SEL, int DS = 1>
+__global__ __launch_bounds__(DS == 1 ? 64 * BWD_WAVES<HD>() : 64 * DS, 2)   // 2 waves per SIMD
+void attn_bwd_kernel(AttnArgs p) {
   constexpr int LD = TLD<HD>();
   constexpr int SLD = 36;                  // dS tile row stride (32 keys + pad)
   constexpr int PER_WAVE = 3 * 32 * LD + 32 * SLD;
+  constexpr int NW = DS == 1 ? BWD_WAVES<HD>() : DS;  // waves per block
+  constexpr int HDF = HD * DS;             // head dim
+  static_assert(DS == 1 || (DS == 2 && HD == 32), "attn_bwd_kernel: DS = 2 splits head_dim 64");
   // (HD <= 32: the dQ partial is loaded at the start of a pair; larger HD reads it at the end, as
   // the registers of a live seed would not fit next to the dK / dV accumulators)
   constexpr bool SEED_EARLY = HD <= 32;
-  __shared__ __attribute__((aligned(16))) float lds[BWD_WAVES<HD>() * PER_WAVE];
+  __shared__ __attribute__((aligned(16))) float lds[NW * PER_WAVE];
   const int lane = threadIdx.x & 63, li = lane & 31, hh = lane >> 5;
-  float* tO = lds + (threadIdx.x >> 6) * PER_WAVE;   // dO block   [query][dim]
+  const int wave = threadIdx.x >> 6;
+  float* tO = lds + wave * PER_WAVE;                 // dO block   [query][dim]
   float* tQ = tO + 32 * LD;                          // Q block    [query][dim]
   float* tK = tQ + 32 * LD;                          // K block    [key][dim]
   float* tS = tK + 32 * LD;                          // dS block   [query][key]
-  const int pair = blockIdx.x * BWD_WAVES<HD>() + (threadIdx.x >> 6);
+  const float* tSp = lds + (wave ^ 1) * PER_WAVE + 3 * 32 * LD;   // DS = 2: the partner wave's dS tile
+  const int pair = DS == 1 ? blockIdx.x * NW + wave : blockIdx.x;
+  const int half = DS == 1 ? 0 : wave;
   if (pair >= p.B * p.H) return;
   const int b = pair / p.H, h = pair % p.H;
   const int I = p.I, K = p.K, q_off = I - K, KP = attn_kpad(K);
   const int64_t tok0 = (int64_t)b * I;
-  const float* Q = p.qkv + tok0 * p.ld + h * HD;
+  const int hoff = h * HDF + half * HD;                // this wave's first dim of head h
+  const float* Q = p.qkv + tok0 * p.ld + hoff;
   const float* Kp = Q + p.d;
   const float* V = Q + 2 * p.d;
   const float* Qt = Q + (int64_t)q_off * p.ld;
-  const float* dO = p.dout + (int64_t)b * K * p.d + h * HD;
+  const float* dO = p.dout + (int64_t)b * K * p.d + hoff;
   const int32_t* qpp = reinterpret_cast<const int32_t*>(p.delta + 2 * (int64_t)p.B * p.H * KP) + (int64_t)b * KP;
   const float* lsep = p.delta + (int64_t)pair * KP;                              // padded lse
   const float* dltp = p.delta + ((int64_t)p.B * p.H + pair) * KP;                // padded delta
-  float* dQt = p.dqkv + (tok0 + q_off) * p.ld + h * HD;
-  float* dK = p.dqkv + tok0 * p.ld + p.d + h * HD;
+  float* dQt = p.dqkv + (tok0 + q_off) * p.ld + hoff;
+  float* dK = p.dqkv + tok0 * p.ld + p.d + hoff;
   float* dV = dK + p.d;
+  // DS = 2: S / dP partial exchange through the dS tiles ([4 groups][64 lanes] float4, 4 KiB)
+  auto exchange = [&](f32x16& v) {
+    f32x4* mine = reinterpret_cast<f32x4*>(tS);
+    const f32x4* theirs = reinterpret_cast<const f32x4*>(tSp);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) mine[g * 64 + lane] = f32x4{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 o = theirs[g * 64 + lane];
+      // fixed operand order (lower half's partial first): both waves get bit-identical sums
+      const f32x4 m4 = {v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
+      const f32x4 t4 = half == 0 ? m4 + o : o + m4;
+      v[4 * g] = t4.x; v[4 * g + 1] = t4.y; v[4 * g + 2] = t4.z; v[4 * g + 3] = t4.w;
+    }
+    __syncthreads();                                   // the partner is done reading before the next write
+  };
   const int nqb = KP / 32;
   const int nkb = (I + 31) / 32;
 
@@ -638,7 +670,7 @@ __global__ __launch_bounds__(64 * BWD_WAVES<HD>(), 2) void attn_bwd_kernel(AttnA
       }
       // dQ^T block: lane = query q0 + li, register r = dim 32c + acc_row(r, hh) (4 float4 per lane)
       const int jq = q0 + li;
-      float* dqrow = SEL ? p.dqkv + (tok0 + qpp[jq]) * p.ld + h * HD + 4 * hh
+      float* dqrow = SEL ? p.dqkv + (tok0 + qpp[jq]) * p.ld + hoff + 4 * hh
                          : dQt + (int64_t)(jq < K ? jq : K - 1) * p.ld + 4 * hh;
       f32x16 dq[NB(HD)];
 #pragma unroll
@@ -655,6 +687,10 @@ __global__ __launch_bounds__(64 * BWD_WAVES<HD>(), 2) void attn_bwd_kernel(AttnA
       frag_to_lds<HD>(tQ, qf, li, hh);
       f32x16 s = mm_frag<HD>(qf, kf);                  // S: row = query, col = key
       f32x16 dp = mm_frag<HD>(of, vf);                 // dP: row = query, col = key
+      if constexpr (DS == 2) {                         // whole-head S and dP from the two halves
+        exchange(s);
+        exchange(dp);
+      }
       if (qb + 1 < nqb) load_qblock(q0 + 32);          // prefetch the next query block
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -1246,6 +1282,13 @@ extern "C" int ot_attn_fwd(const float* qkv, int64_t ld, int B, int H, int I, in
   return OT_OK;
 }
 
+// f32-MFMA backward at head_dim 64: 2 = the head split over two waves (default), 1 = one wave per
+// (sample, head) (ONETRANS_ATTN_BWD_DS=1, for A/B timing)
+static int g_attn_bwd_ds = [] {
+  const char* e = std::getenv("ONETRANS_ATTN_BWD_DS");
+  return (e && std::atoi(e) == 1) ? 1 : 2;
+}();
+
 extern "C" size_t ot_attn_bwd_workspace_size(int B, int H, int K) {
   return (2 * (size_t)B * H + B) * attn_kpad(K) * sizeof(float);     // lse, delta (+ padded qpos)
 }
@@ -1280,6 +1323,11 @@ extern "C" int ot_attn_bwd(const float* qkv, int64_t ld, const float* out, const
     else kern = sel ? attn_bwd_split_kernel<64, 1, true, 4> : attn_bwd_split_kernel<64, 1, false, 4>;
     const unsigned grid = ceil_div((int64_t)B * H, waves);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * waves), (size_t)waves * lds, (hipStream_t)stream, p);
+  } else if (head_dim == 64 && g_attn_bwd_ds == 2) {
+    // head_dim 64 as two 32-dim waves per (sample, head): 2 waves / SIMD instead of 1
+    const bool sel = qpos != nullptr;
+    void (*kern)(AttnArgs) = sel ? attn_bwd_kernel<32, true, 2> : attn_bwd_kernel<32, false, 2>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)((int64_t)B * H)), dim3(128), 0, (hipStream_t)stream, p);
   } else {
     const int waves = head_dim >= 128 ? 2 : 4;
     const unsigned grid = ceil_div((int64_t)B * H, waves);

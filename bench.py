@@ -277,6 +277,8 @@ def main():
         'model_tflops': round(fl['fwd_bwd'] * value / 1e12, 2),
         'final_loss': round(loss, 5),
         'repeats': len(times), 'ms_per_step_repeats': [round(1e3 * x / args.steps, 3) for x in times],
+        'peak_hbm_gb': round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2),
+        'recompute': bool(model.recompute),
     }
     if world > 1:
         import torch.distributed as dist

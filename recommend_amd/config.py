@@ -96,6 +96,12 @@ class OneTransConfig:
         self.sparse_features: Dict[str, int] = {}   # build: NS id features -> cardinality
         self.seq_item_vocab = 0              # build: >0 => sequence features are item ids
         self.compute_dtype = 'fp32'          # build: arithmetic of the HIP path (reference is fp32)
+        # build: the behaviour behind two reference flags the reference itself never reads
+        # (use_activation_recompute config.py:69, warmup_steps config.py:36), opt-in so default numerics and
+        # memory match the reference: recompute each block's forward in its backward (keep only the block
+        # input), and a linear warm-up of the dense LR over warmup_steps
+        self.recompute_blocks = False
+        self.apply_warmup = False
         self.sparse_clip_norm = 120.0        # build: paper clip for sparse grads (complete_translation.md:190)
         self.adagrad_initial_accumulator = 0.1   # build: Keras Adagrad default
         self.adagrad_epsilon = 1e-7              # build: Keras Adagrad default

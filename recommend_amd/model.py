@@ -125,6 +125,100 @@ class _Tokenize(torch.autograd.Function):
         return None, None, None
 
 
+def _block_forward(m, l, x, I, Kq, seed, training, rstd_in=None, select=False, need_out=True):
+    """The block's forward kernels (``_Block.forward``; also the backward's recompute with
+    ``need_out=False``, which stops after FFN1: the backward needs u, not the block output).
+    Returns (x2, rstd_out, saved, pos, inv, rate); saved = (x, rstd1, qkv, o, lse, x1, rstd2, u)."""
+    cfg = m.config
+    d, f, H = cfg.hidden_dim, cfg.ffn_dim, cfg.num_heads
+    hd = d // H
+    B = x.shape[0] // I
+    dev = x.device
+    maps = m.maps(B, I, Kq)
+    ma, mt = maps['all'].to(dev), maps['tail'].to(dev)
+    na, nt = maps['all'].ntiles, maps['tail'].ntiles
+    rate = cfg.dropout_rate if training else 0.0
+    dflag = OT_EPI_DROPOUT if rate > 0 else 0
+    wqkv, wo = m.pT(f'blk.{l}.wqkv'), m.pT(f'blk.{l}.wo')          # transposed shadow: [G][N][K]
+    w1, b1, w2, b2 = m.pT(f'blk.{l}.w1'), m.p(f'blk.{l}.b1'), m.pT(f'blk.{l}.w2'), m.p(f'blk.{l}.b2')
+    g1, g2 = m.p(f'blk.{l}.norm1'), m.p(f'blk.{l}.norm2')
+    fuse = m.fuse_with((f'blk.{l}.wo', 'fwd'), (f'blk.{l}.w2', 'fwd'))
+    # norm1 -> rstd only; the QKV GEMM applies it in its A prologue
+    if rstd_in is not None and rstd_in.numel() == B * I:
+        rstd1 = rstd_in
+    else:
+        rstd1 = torch.empty(B * I, device=dev)
+        K.rmsnorm_fwd(x, d, B * I, d, rstd1, eps=RMS_EPS)
+    # pyramid keep (model.py:287-302, 371): the kept query positions come from the wavefront
+    # top-K select (ot_pyramid_select); with no score (reference semantics) they are the tail
+    qrows, pos, inv = mt['rows'][0], None, None
+    if select:
+        pos = torch.empty(B * Kq, dtype=torch.int32, device=dev)
+        inv = torch.empty(B * I, dtype=torch.int32, device=dev)
+        if cfg.pyramid_select == 'norm':
+            # score = token RMS (1/rstd1): keep the largest; the NS tail is always kept and only the
+            # shared-group rows of the tail map change (dedicated_positions='tail', checked in config)
+            nf = min(cfg.num_ns_tokens, Kq)
+            qrows = qrows.clone()
+            K.pyramid_select(B, I, Kq, pos, inv, score=rstd1, sign=-1.0, nforce=nf, map_rows=qrows,
+                             map_per_sample=Kq - nf)
+        else:
+            K.pyramid_select(B, I, Kq, pos, inv)
+    tail = (Kq, I, pos)
+    qkv = torch.empty(B * I, 3 * d, device=dev)
+    if Kq == I:
+        K.gemm(OT_GEMM_NT, x, d, d, ma['rows'][0], wqkv, 3 * d * d, d, 3 * d, ma['tile_group'], na, qkv,
+               3 * d, ma['rows'][0], a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=maps['all'].nrows,
+               bimg=m.bimg(f'blk.{l}.wqkv'))
+    else:
+        K.gemm(OT_GEMM_NT, x, d, d, ma['rows'][0], (wqkv, d * d), 3 * d * d, d, 2 * d, ma['tile_group'], na,
+               (qkv, d), 3 * d, ma['rows'][0], a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=maps['all'].nrows,
+               bimg=m.bimg(f'blk.{l}.wqkv', tn0=d // TILE) if d % TILE == 0 else None)
+        K.gemm(OT_GEMM_NT, x, d, d, qrows, wqkv, 3 * d * d, d, d, mt['tile_group'], nt, qkv,
+               3 * d, qrows, a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=maps['tail'].nrows,
+               bimg=m.bimg(f'blk.{l}.wqkv'))
+    o = torch.empty(B * Kq, d, device=dev)
+    lse = torch.empty(B * H * Kq, device=dev)
+    K.attn_fwd(qkv, 3 * d, B, H, I, Kq, hd, o, lse, qpos=pos, fp8=m.attn_fp8)
+    # x1 = x[tail] + drop(o @ Wo)      (model.py:117, 193)
+    x1 = torch.empty(B * Kq, d, device=dev)
+    rstd2 = torch.empty(B * Kq, device=dev)
+    if fuse:
+        K.gemm_rms(OT_GEMM_NT, o, d, d, mt['rows'][1], wo, 0, d, d, mt['tile_group'], nt, x1, d, mt['rows'][1],
+                   epi=OT_EPI_RESIDUAL | dflag | OT_EPI_ROW_RSTD, res=x, ldres=d, res_tok=1, seed=seed,
+                   site=2 * l, drop=rate, tail=tail, m_rows=maps['tail'].nrows, rstd_out=rstd2, eps=RMS_EPS,
+                   bimg=m.bimg(f'blk.{l}.wo'))
+    else:
+        K.gemm(OT_GEMM_NT, o, d, d, mt['rows'][1], wo, 0, d, d, mt['tile_group'], nt, x1, d, mt['rows'][1],
+               epi=OT_EPI_RESIDUAL | dflag, res=x, ldres=d, res_tok=1, seed=seed, site=2 * l, drop=rate,
+               tail=tail, m_rows=maps['tail'].nrows, bimg=m.bimg(f'blk.{l}.wo'))
+        K.rmsnorm_fwd(x1, d, B * Kq, d, rstd2, eps=RMS_EPS)
+    # u = norm2(x1) @ W1[g] + b1[g]  (pre-activation; GELU applied by its consumers)
+    u = torch.empty(B * Kq, f, device=dev)
+    K.gemm(OT_GEMM_NT, x1, d, d, mt['rows'][1], w1, d * f, d, f, mt['tile_group'], nt, u, f, mt['rows'][1],
+           a_xform=OT_AX_RMSNORM, rstd=rstd2, gamma=g2, bias=b1, bias_gstride=f, epi=OT_EPI_BIAS, m_rows=maps['tail'].nrows,
+           bimg=m.bimg(f'blk.{l}.w1'))
+    saved = (x, rstd1, qkv, o, lse, x1, rstd2, u)
+    if not need_out:
+        return None, None, saved, pos, inv, rate
+    # x2 = x1 + drop(gelu(u) @ W2[g] + b2[g])     (model.py:154-161, 198)
+    x2 = torch.empty(B * Kq, d, device=dev)
+    rstd_out = None
+    if fuse:
+        rstd_out = torch.empty(B * Kq, device=dev)
+        K.gemm_rms(OT_GEMM_NT, u, f, f, mt['rows'][1], w2, f * d, f, d, mt['tile_group'], nt, x2, d,
+                   mt['rows'][1], a_xform=OT_AX_GELU, bias=b2, bias_gstride=d,
+                   epi=OT_EPI_BIAS | OT_EPI_RESIDUAL | dflag | OT_EPI_ROW_RSTD, res=x1, ldres=d, res_tok=0,
+                   seed=seed, site=2 * l + 1, drop=rate, tail=tail, m_rows=maps['tail'].nrows,
+                   rstd_out=rstd_out, eps=RMS_EPS, bimg=m.bimg(f'blk.{l}.w2'))
+    else:
+        K.gemm(OT_GEMM_NT, u, f, f, mt['rows'][1], w2, f * d, f, d, mt['tile_group'], nt, x2, d, mt['rows'][1],
+               a_xform=OT_AX_GELU, bias=b2, bias_gstride=d, epi=OT_EPI_BIAS | OT_EPI_RESIDUAL | dflag, res=x1,
+               ldres=d, res_tok=0, seed=seed, site=2 * l + 1, drop=rate, tail=tail,
+               m_rows=maps['tail'].nrows, bimg=m.bimg(f'blk.{l}.w2'))
+    return x2, rstd_out, saved, pos, inv, rate
+
+
 class _Block(torch.autograd.Function):
     """OneTransBlock.call (model.py:186-200) for the last K of I tokens (pyramid / last-layer DCE).
     x: [B*I, d] -> ([B*K, d], rstd of the output rows).
@@ -135,91 +229,14 @@ class _Block(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, flat, x, m, l, I, Kq, seed, training, rstd_in=None, select=False):
-        cfg = m.config
-        d, f, H = cfg.hidden_dim, cfg.ffn_dim, cfg.num_heads
-        hd = d // H
-        B = x.shape[0] // I
-        dev = x.device
-        maps = m.maps(B, I, Kq)
-        ma, mt = maps['all'].to(dev), maps['tail'].to(dev)
-        na, nt = maps['all'].ntiles, maps['tail'].ntiles
-        rate = cfg.dropout_rate if training else 0.0
-        dflag = OT_EPI_DROPOUT if rate > 0 else 0
-        wqkv, wo = m.pT(f'blk.{l}.wqkv'), m.pT(f'blk.{l}.wo')          # transposed shadow: [G][N][K]
-        w1, b1, w2, b2 = m.pT(f'blk.{l}.w1'), m.p(f'blk.{l}.b1'), m.pT(f'blk.{l}.w2'), m.p(f'blk.{l}.b2')
-        g1, g2 = m.p(f'blk.{l}.norm1'), m.p(f'blk.{l}.norm2')
-        fuse = m.fuse_with((f'blk.{l}.wo', 'fwd'), (f'blk.{l}.w2', 'fwd'))
-        # norm1 -> rstd only; the QKV GEMM applies it in its A prologue
-        if rstd_in is not None and rstd_in.numel() == B * I:
-            rstd1 = rstd_in
+        x2, rstd_out, saved, pos, inv, rate = _block_forward(m, l, x, I, Kq, seed, training, rstd_in, select)
+        if m.recompute:
+            # activation recompute: keep the block input (and its rstd); the backward re-runs the
+            # forward kernels up to FFN1 (dropout masks and pyramid keeps are deterministic)
+            ctx.save_for_backward(saved[0], saved[1])
+            ctx.fwd_args = (training, select)
         else:
-            rstd1 = torch.empty(B * I, device=dev)
-            K.rmsnorm_fwd(x, d, B * I, d, rstd1, eps=RMS_EPS)
-        # pyramid keep (model.py:287-302, 371): the kept query positions come from the wavefront
-        # top-K select (ot_pyramid_select); with no score (reference semantics) they are the tail
-        qrows, pos, inv = mt['rows'][0], None, None
-        if select:
-            pos = torch.empty(B * Kq, dtype=torch.int32, device=dev)
-            inv = torch.empty(B * I, dtype=torch.int32, device=dev)
-            if cfg.pyramid_select == 'norm':
-                # score = token RMS (1/rstd1): keep the largest; the NS tail is always kept and only the
-                # shared-group rows of the tail map change (dedicated_positions='tail', checked in config)
-                nf = min(cfg.num_ns_tokens, Kq)
-                qrows = qrows.clone()
-                K.pyramid_select(B, I, Kq, pos, inv, score=rstd1, sign=-1.0, nforce=nf, map_rows=qrows,
-                                 map_per_sample=Kq - nf)
-            else:
-                K.pyramid_select(B, I, Kq, pos, inv)
-        tail = (Kq, I, pos)
-        qkv = torch.empty(B * I, 3 * d, device=dev)
-        if Kq == I:
-            K.gemm(OT_GEMM_NT, x, d, d, ma['rows'][0], wqkv, 3 * d * d, d, 3 * d, ma['tile_group'], na, qkv,
-                   3 * d, ma['rows'][0], a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=maps['all'].nrows,
-                   bimg=m.bimg(f'blk.{l}.wqkv'))
-        else:
-            K.gemm(OT_GEMM_NT, x, d, d, ma['rows'][0], (wqkv, d * d), 3 * d * d, d, 2 * d, ma['tile_group'], na,
-                   (qkv, d), 3 * d, ma['rows'][0], a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=maps['all'].nrows,
-                   bimg=m.bimg(f'blk.{l}.wqkv', tn0=d // TILE) if d % TILE == 0 else None)
-            K.gemm(OT_GEMM_NT, x, d, d, qrows, wqkv, 3 * d * d, d, d, mt['tile_group'], nt, qkv,
-                   3 * d, qrows, a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=maps['tail'].nrows,
-                   bimg=m.bimg(f'blk.{l}.wqkv'))
-        o = torch.empty(B * Kq, d, device=dev)
-        lse = torch.empty(B * H * Kq, device=dev)
-        K.attn_fwd(qkv, 3 * d, B, H, I, Kq, hd, o, lse, qpos=pos, fp8=m.attn_fp8)
-        # x1 = x[tail] + drop(o @ Wo)      (model.py:117, 193)
-        x1 = torch.empty(B * Kq, d, device=dev)
-        rstd2 = torch.empty(B * Kq, device=dev)
-        if fuse:
-            K.gemm_rms(OT_GEMM_NT, o, d, d, mt['rows'][1], wo, 0, d, d, mt['tile_group'], nt, x1, d, mt['rows'][1],
-                       epi=OT_EPI_RESIDUAL | dflag | OT_EPI_ROW_RSTD, res=x, ldres=d, res_tok=1, seed=seed,
-                       site=2 * l, drop=rate, tail=tail, m_rows=maps['tail'].nrows, rstd_out=rstd2, eps=RMS_EPS,
-                       bimg=m.bimg(f'blk.{l}.wo'))
-        else:
-            K.gemm(OT_GEMM_NT, o, d, d, mt['rows'][1], wo, 0, d, d, mt['tile_group'], nt, x1, d, mt['rows'][1],
-                   epi=OT_EPI_RESIDUAL | dflag, res=x, ldres=d, res_tok=1, seed=seed, site=2 * l, drop=rate,
-                   tail=tail, m_rows=maps['tail'].nrows, bimg=m.bimg(f'blk.{l}.wo'))
-            K.rmsnorm_fwd(x1, d, B * Kq, d, rstd2, eps=RMS_EPS)
-        # u = norm2(x1) @ W1[g] + b1[g]  (pre-activation; GELU applied by its consumers)
-        u = torch.empty(B * Kq, f, device=dev)
-        K.gemm(OT_GEMM_NT, x1, d, d, mt['rows'][1], w1, d * f, d, f, mt['tile_group'], nt, u, f, mt['rows'][1],
-               a_xform=OT_AX_RMSNORM, rstd=rstd2, gamma=g2, bias=b1, bias_gstride=f, epi=OT_EPI_BIAS, m_rows=maps['tail'].nrows,
-               bimg=m.bimg(f'blk.{l}.w1'))
-        # x2 = x1 + drop(gelu(u) @ W2[g] + b2[g])     (model.py:154-161, 198)
-        x2 = torch.empty(B * Kq, d, device=dev)
-        rstd_out = None
-        if fuse:
-            rstd_out = torch.empty(B * Kq, device=dev)
-            K.gemm_rms(OT_GEMM_NT, u, f, f, mt['rows'][1], w2, f * d, f, d, mt['tile_group'], nt, x2, d,
-                       mt['rows'][1], a_xform=OT_AX_GELU, bias=b2, bias_gstride=d,
-                       epi=OT_EPI_BIAS | OT_EPI_RESIDUAL | dflag | OT_EPI_ROW_RSTD, res=x1, ldres=d, res_tok=0,
-                       seed=seed, site=2 * l + 1, drop=rate, tail=tail, m_rows=maps['tail'].nrows,
-                       rstd_out=rstd_out, eps=RMS_EPS, bimg=m.bimg(f'blk.{l}.w2'))
-        else:
-            K.gemm(OT_GEMM_NT, u, f, f, mt['rows'][1], w2, f * d, f, d, mt['tile_group'], nt, x2, d, mt['rows'][1],
-                   a_xform=OT_AX_GELU, bias=b2, bias_gstride=d, epi=OT_EPI_BIAS | OT_EPI_RESIDUAL | dflag, res=x1,
-                   ldres=d, res_tok=0, seed=seed, site=2 * l + 1, drop=rate, tail=tail,
-                   m_rows=maps['tail'].nrows, bimg=m.bimg(f'blk.{l}.w2'))
-        ctx.save_for_backward(x, rstd1, qkv, o, lse, x1, rstd2, u)
+            ctx.save_for_backward(*saved)
         ctx.m, ctx.l, ctx.I, ctx.Kq, ctx.seed, ctx.rate = m, l, I, Kq, seed, rate
         ctx.pos, ctx.inv = pos, inv
         if rstd_out is None:
@@ -229,9 +246,16 @@ class _Block(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dx2, _drstd=None):
-        x, rstd1, qkv, o, lse, x1, rstd2, u = ctx.saved_tensors
         m, l, I, Kq, seed, rate = ctx.m, ctx.l, ctx.I, ctx.Kq, ctx.seed, ctx.rate
         pos, inv = ctx.pos, ctx.inv
+        if m.recompute:
+            xin, rstd_in = ctx.saved_tensors
+            training, select = ctx.fwd_args
+            _, _, saved, pos, inv, _ = _block_forward(m, l, xin, I, Kq, seed, training, rstd_in, select,
+                                                      need_out=False)
+            x, rstd1, qkv, o, lse, x1, rstd2, u = saved
+        else:
+            x, rstd1, qkv, o, lse, x1, rstd2, u = ctx.saved_tensors
         tail = (Kq, I, pos)
         cfg = m.config
         d, f, H = cfg.hidden_dim, cfg.ffn_dim, cfg.num_heads
@@ -312,6 +336,7 @@ class _Block(torch.autograd.Function):
             K.rmsnorm_bwd(dxn1, d, x, d, m.p(f'blk.{l}.norm1'), rstd1, dx, d, B * I, d, dres=dx1, lddres=d,
                           dres_tail=(Kq, I, inv) if Kq < I else (0, 0), dgamma=m.g(f'blk.{l}.norm1'), accumulate=acc,
                           device=dev)
+        m.side_block_done()
         if m.grad_ready is not None:
             m.grad_ready(l)                     # this block's banks are final: the DP exchange may start
         return None, dx, None, None, None, None, None, None, None, None
@@ -447,6 +472,9 @@ class OneTransModel(nn.Module):
         # ONETRANS_ATTN=fp8 selects the fp8 forward too.
         if getattr(cfg, 'compute_dtype', 'fp32') not in ('fp32', 'bf16', 'fp8attn'):
             raise ValueError(f"compute_dtype {cfg.compute_dtype!r}: expected 'fp32', 'bf16' or 'fp8attn'")
+        # activation recompute (config.recompute_blocks / ONETRANS_RECOMPUTE=1): a block keeps only its
+        # input for backward and re-runs its forward kernels there (_Block)
+        self.recompute = bool(getattr(cfg, 'recompute_blocks', False)) or os.environ.get('ONETRANS_RECOMPUTE') == '1'
         self.attn_fp8 = (getattr(cfg, 'compute_dtype', 'fp32') == 'fp8attn'
                          or os.environ.get('ONETRANS_ATTN', '') == 'fp8')
         if self.attn_fp8 and cfg.hidden_dim // cfg.num_heads not in (64, 128):
@@ -486,6 +514,7 @@ class OneTransModel(nn.Module):
         self._side = None
         self._side_used = False
         self._side_keep: List[torch.Tensor] = []
+        self._side_fifo: List = []
         self.kv_cache = None                      # model.py:333 (reference attribute; never populated)
         self._pending_sparse: List = []
         self._plans: Dict = {}
@@ -849,12 +878,28 @@ class OneTransModel(nn.Module):
         self._side_used = True
         return torch.cuda.stream(self._side)
 
+    def side_block_done(self, depth: int = 2):
+        """End of one block's backward: the tensors its side-stream launches read are released once the
+        side stream has finished them — the main stream waits on an event recorded after the block's
+        weight gradients, ``depth`` blocks later (by then the side stream has normally finished them, so
+        nothing stalls), instead of holding every block's backward temporaries until the join."""
+        if self._side is None or not self._side_keep:
+            return
+        ev = torch.cuda.Event()
+        ev.record(self._side)
+        self._side_fifo.append((ev, self._side_keep))
+        self._side_keep = []
+        while len(self._side_fifo) > depth:
+            ev0, _ = self._side_fifo.pop(0)
+            torch.cuda.current_stream(self.device).wait_event(ev0)
+
     def join_side_stream(self):
         """The main stream waits for every weight gradient launched on the side stream."""
         if self._side is not None and self._side_used:
             torch.cuda.current_stream(self.device).wait_stream(self._side)
             self._side_used = False
         self._side_keep = []
+        self._side_fifo = []
 
     # ---------------------------------------------------------------- reference API
     def reset_kv_cache(self):

@@ -50,6 +50,10 @@ class OneTransOptimizer:
         self.model = model
         oc = config.optimizer_config
         self.lr = float(oc.get('dense_lr', config.learning_rate))
+        # linear warm-up of the dense learning rate over config.warmup_steps (config.py:36; the
+        # reference defines warmup_steps but never applies it, so this is opt-in: apply_warmup)
+        self.warmup = int(config.warmup_steps) if getattr(config, 'apply_warmup', False) else 0
+        self.steps_done = 0
         self.momentum = float(oc.get('momentum', 0.0))
         self.rho = float(config.rmsprop_rho)
         self.eps = float(config.rmsprop_epsilon)
@@ -69,6 +73,13 @@ class OneTransOptimizer:
         # diagnostics (bench.py, N > 1): when a list, every step appends HIP-event pairs bracketing the
         # main stream's waits for the gradient exchange, i.e. the exchange time NOT hidden by backward
         self.exchange_events = None
+
+    def current_lr(self) -> float:
+        """Dense learning rate of the step being applied (``steps_done`` counts it): lr * min(1, step /
+        warmup_steps) under ``apply_warmup``, else lr."""
+        if self.warmup > 0:
+            return self.lr * min(1.0, self.steps_done / self.warmup)
+        return self.lr
 
     def _mark(self):
         if self.exchange_events is None:
@@ -152,8 +163,9 @@ class OneTransOptimizer:
             otdist.allreduce_dense(m.flat.grad)
         if ev_a is not None:
             self.exchange_events.append((ev_a, self._mark()))
+        self.steps_done += 1
         K.clip_rmsprop(m.flat.data, m.flat.grad, self.v, self.m, self.segs, self.nseg, m.layout.max_seg_elems,
-                       self.lr, self.rho, self.eps, self.momentum, self.clip, device=m.flat.device)
+                       self.current_lr(), self.rho, self.eps, self.momentum, self.clip, device=m.flat.device)
         m.refresh_shadow()
         for (name, keys, grads) in m._pending_sparse:
             table = m.tables[name]

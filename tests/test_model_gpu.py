@@ -243,3 +243,56 @@ def test_bf16_mode_forward_and_train(dev, dtype):
         assert torch.isfinite(o['total_loss']).item()
     finally:
         K.set_matmul_mode(old)
+
+
+@pytest.mark.parametrize('case', ['criteo_d128_pyramid', 'criteo_norm_pyramid', 'criteo_d256_pyramid'])
+def test_recompute_matches_saved(dev, case):
+    """Activation recompute (config.recompute_blocks): the backward re-runs each block's forward kernels
+    from its input — dropout masks and pyramid keeps are deterministic, so the loss and every gradient
+    equal the saved-activation run bit for bit, and the activations held between forward and backward
+    shrink to the block inputs."""
+    cfg = CASES[case]()
+    P, model, batch = setup(cfg, 41, dev)
+    ns, seq, lab = batch
+    y = stack_labels(lab, cfg.tasks, dev)
+    res = []
+    for rc in (False, True):
+        model.recompute = rc
+        model.flat.grad.zero_()
+        model._step = 0
+        torch.cuda.synchronize()
+        base = torch.cuda.memory_allocated(dev)
+        loss = keras_bce_loss(y, model.forward_probs(ns_t(ns, dev), ns_t(seq, dev), training=True))
+        torch.cuda.synchronize()
+        held = torch.cuda.memory_allocated(dev) - base          # activations kept for backward
+        loss.backward()
+        sparse = [(k, keys.clone(), g.clone()) for (k, keys, g) in model._pending_sparse]
+        res.append((loss.item(), model.flat.grad.clone(), sparse, held))
+    assert res[0][0] == res[1][0]
+    assert torch.equal(res[0][1], res[1][1])
+    for (k0, keys0, g0), (k1, keys1, g1) in zip(res[0][2], res[1][2]):
+        assert k0 == k1 and torch.equal(keys0, keys1) and torch.equal(g0, g1)
+    assert res[1][3] < res[0][3], (res[1][3], res[0][3])
+
+
+def test_lr_warmup(dev):
+    """apply_warmup: the dense update of step s uses lr * min(1, s / warmup_steps) (config.py:36; the
+    reference never applies its warmup_steps, so this is opt-in) — step 1 of a 4-step warm-up equals a
+    plain step at lr / 4, bit for bit."""
+    cfg = CASES['criteo_head']()
+    cfg.optimizer_config = dict(cfg.optimizer_config, dense_lr=0.004, momentum=0.9)
+    batch = make_batch(37, cfg, seed=2000)
+    out = []
+    for warm in (True, False):
+        c = copy.deepcopy(cfg)
+        if warm:
+            c.apply_warmup, c.warmup_steps = True, 4
+        else:
+            c.optimizer_config = dict(c.optimizer_config, dense_lr=0.001)
+        P, model, _ = setup(c, 37, dev)
+        tr = OneTransTrainer(c, model=model)
+        tr.train_step(batch)
+        out.append(model.flat.data.clone())
+        if warm:
+            assert tr.optimizer.current_lr() == pytest.approx(0.001)
+    assert torch.equal(out[0], out[1])

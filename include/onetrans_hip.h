@@ -57,8 +57,14 @@ extern "C" {
 #define OT_EPI_ACCUMULATE 32 /* C += result */
 /* row-norm epilogues (ot_mixed_gemm_rms only): N == 128 (one tile holds whole output rows); OT_EPI_ROW_RSTD
  * also N = 256, 384, ... on the plane GEMM (split mode, ot_mixed_gemm_rms_img; per-tile row sums of
- * squares in the workspace, ot_mixed_gemm_rms_workspace_size(ntiles, N), then a finishing pass) */
+ * squares in the workspace, ot_mixed_gemm_rms_workspace_size(ntiles, N), then a finishing pass);
+ * OT_EPI_RMSNORM_BWD also N = 256, 384, ... given the row dots' partials (ot_rms_epilogue.rowdot) */
 #define OT_EPI_ROW_RSTD 64      /* rstd_out[out_row] = 1/sqrt(mean_n(C[out_row]^2) + eps), C as above */
+#define OT_EPI_ROWDOT 256       /* with OT_EPI_GELU_BWD (ot_mixed_gemm_rms, N % 128 == 0): also
+                                   rowdot[out_row * rowdot_n + n / 128] = sum over the tile's columns of
+                                   C * (aux - bias[g]) — for the FFN2 dgrad (C = dU, aux = U, bias = b1)
+                                   this is the FFN1 norm backward's row dot: sum_f dU_f (U_f - b1_f) =
+                                   rstd * <gamma dy, x> (no row-wide reduction needed at d > 128) */
 #define OT_EPI_RMSNORM_BWD 128  /* the product is dL/dy of y = RMSNorm(x) * gamma: C = dL/dx (+ dres);
                                    with OT_EPI_DROPOUT also dx_masked = mask(C) (C itself unmasked) */
 
@@ -111,6 +117,9 @@ typedef struct ot_rms_epilogue {
   float* dx_masked; int64_t lddxm;                     /*   with OT_EPI_DROPOUT: GEMM seed/site/rate/tail */
   float* dgamma; int accumulate_dgamma;                /*   dgamma (+)= sum_rows dy * x * rstd */
   void* workspace; size_t ws_bytes;                    /*   ot_mixed_gemm_rms_workspace_size(ntiles, N) */
+  float* rowdot; int rowdot_n;                         /* OT_EPI_ROWDOT: output partials [out rows][rowdot_n];
+                                                          OT_EPI_RMSNORM_BWD with N > 128: their input (the row
+                                                          dot = sum_j rowdot[out_row][j] / rstd) */
 } ot_rms_epilogue;
 size_t ot_mixed_gemm_rms_workspace_size(int ntiles, int N);
 int ot_mixed_gemm_rms(int mode, const float* A, int64_t lda, int K, const int32_t* in_rows,

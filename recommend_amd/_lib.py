@@ -19,7 +19,7 @@ OT_GEMM_NN, OT_GEMM_NT = 0, 1
 OT_AX_NONE, OT_AX_RMSNORM, OT_AX_GELU = 0, 1, 2
 OT_EPI_BIAS, OT_EPI_GELU_BWD, OT_EPI_GELU = 1, 2, 4
 OT_EPI_DROPOUT, OT_EPI_RESIDUAL, OT_EPI_ACCUMULATE = 8, 16, 32
-OT_EPI_ROW_RSTD, OT_EPI_RMSNORM_BWD = 64, 128
+OT_EPI_ROW_RSTD, OT_EPI_RMSNORM_BWD, OT_EPI_ROWDOT = 64, 128, 256
 OT_MATMUL_F32, OT_MATMUL_SPLIT_BF16, OT_MATMUL_BF16 = 0, 1, 2
 MATMUL_MODES = {'f32': OT_MATMUL_F32, 'split': OT_MATMUL_SPLIT_BF16, 'bf16': OT_MATMUL_BF16}
 
@@ -32,7 +32,8 @@ class RmsEpilogue(ctypes.Structure):
                 ('dres_tail_inv', c_void_p),
                 ('dx_masked', c_void_p), ('lddxm', c_int64),
                 ('dgamma', c_void_p), ('accumulate_dgamma', c_int),
-                ('workspace', c_void_p), ('ws_bytes', c_size_t)]
+                ('workspace', c_void_p), ('ws_bytes', c_size_t),
+                ('rowdot', c_void_p), ('rowdot_n', c_int)]
 
 P = c_void_p
 I64 = c_int64

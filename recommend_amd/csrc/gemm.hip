@@ -80,6 +80,7 @@ struct GemmArgs {
   const float* dres; int64_t lddres; int dres_K, dres_I; const int32_t* dres_inv;
   float* dxm; int64_t lddxm; float* dgpart;
   float* rowpart;                               // OT_EPI_ROW_RSTD with N > GT: [ntm*GT][ntn] row sums of squares
+  float* rowdot; int rowdot_n;                  // OT_EPI_ROWDOT output / OT_EPI_RMSNORM_BWD (N > GT) input
   const int32_t* tail_pos;                      // kept positions (ot_pyramid_select) or null (tail)
   // plane GEMM: pre-split B image (ot_split_images), its tiles per group and the first tile used
   const uint16_t* bimg; int bimg_ntn, bimg_tn0;
@@ -139,6 +140,9 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
     const bool need_tok = (epi & OT_EPI_DROPOUT) || ((epi & OT_EPI_RESIDUAL) && p.res_tok);
     constexpr bool RMSBWD = EPIT >= 0 && (EPIT & OT_EPI_RMSNORM_BWD);
     constexpr bool ROWRSTD = EPIT >= 0 && (EPIT & OT_EPI_ROW_RSTD);
+    constexpr bool ROWDOT = EPIT >= 0 && (EPIT & OT_EPI_ROWDOT);
+    f32x4 rdb4 = {0.f, 0.f, 0.f, 0.f};                 // OT_EPI_ROWDOT: the bias subtracted from aux
+    if (ROWDOT) rdb4 = *reinterpret_cast<const f32x4*>(p.bias + (int64_t)g * p.bias_gstride + col);
     // dgamma partials live in a thread-private LDS slot behind ct (a register accumulator here
     // costs the whole kernel ~70 VGPRs of occupancy): dgs[rb][4 c4 .. 4 c4 + 3]
     float* dgs = ct + 64 * CLD;
@@ -210,6 +214,11 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
           if (epi & OT_EPI_GELU_BWD) {
             v.x *= gelu_erf_grad(aux4[i].x); v.y *= gelu_erf_grad(aux4[i].y);
             v.z *= gelu_erf_grad(aux4[i].z); v.w *= gelu_erf_grad(aux4[i].w);
+            if (ROWDOT) {                                      // this tile's part of sum_f dU_f (U_f - b_f)
+              const f32x4 ub = aux4[i] - rdb4;
+              const float sd = row32_sum(v.x * ub.x + v.y * ub.y + v.z * ub.z + v.w * ub.w);
+              if (orr >= 0 && c4 == 0) p.rowdot[(int64_t)orr * p.rowdot_n + n0 / GT] = sd;
+            }
           }
           if (epi & OT_EPI_GELU) {
             v.x = gelu_erf(v.x); v.y = gelu_erf(v.y); v.z = gelu_erf(v.z); v.w = gelu_erf(v.w);
@@ -218,8 +227,15 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
             // v = dL/dy of y = x * rstd * gamma:  dx = rstd * (g - x * rstd^2 * <g, x> / N) + dres
             const f32x4 gv = v * ngam;
             const float r = nr[i];
-            float sdot = gv.x * x4[i].x + gv.y * x4[i].y + gv.z * x4[i].z + gv.w * x4[i].w;
-            sdot = row32_sum(sdot);
+            float sdot;
+            if (p.rowdot) {                                    // N > GT: <g dy, x> = sum of the partials / rstd
+              float t = 0.f;
+              const float* rp = p.rowdot + (int64_t)(orr < 0 ? 0 : orr) * p.rowdot_n;
+              for (int j = 0; j < p.rowdot_n; ++j) t += rp[j];
+              sdot = t / r;
+            } else {
+              sdot = row32_sum(gv.x * x4[i].x + gv.y * x4[i].y + gv.z * x4[i].z + gv.w * x4[i].w);
+            }
             const float coef = r * r * r * sdot / (float)p.N;
             if (orr >= 0) {
               f32x4* q = reinterpret_cast<f32x4*>(dgs + rb * GT + 4 * c4);
@@ -268,7 +284,7 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
       float a = 0.f;
 #pragma unroll
       for (int k = 0; k < 8; ++k) a += dgs[k * GT + t];
-      p.dgpart[(int64_t)tm * GT + t] = a;
+      p.dgpart[(int64_t)tm * p.N + n0 + t] = a;
     }
 }
 
@@ -1294,7 +1310,7 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
                            const ot_rms_epilogue* rms, const uint16_t* bimg, int bimg_ntn, int bimg_tn0,
                            void* stream) {
   OT_REQUIRE(A && W && C, "ot_mixed_gemm: null operand");
-  const int rms_flags = epi & (OT_EPI_ROW_RSTD | OT_EPI_RMSNORM_BWD);
+  const int rms_flags = epi & (OT_EPI_ROW_RSTD | OT_EPI_RMSNORM_BWD | OT_EPI_ROWDOT);
   OT_REQUIRE(!rms_flags || rms, "ot_mixed_gemm: row-norm epilogue flags need ot_mixed_gemm_rms");
   OT_REQUIRE(K > 0 && N > 0 && ntiles >= 0, "ot_mixed_gemm: bad sizes K=%d N=%d ntiles=%d", K, N, ntiles);
   OT_REQUIRE(K % 4 == 0 && lda % 4 == 0, "ot_mixed_gemm: K and lda must be multiples of 4");
@@ -1307,10 +1323,17 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
   OT_REQUIRE(a_xform != OT_AX_RMSNORM || (a_rstd && a_gamma), "ot_mixed_gemm: rmsnorm prologue needs rstd/gamma");
   OT_REQUIRE(!((epi & OT_EPI_DROPOUT) || res_tok) || (tail_K > 0 && tail_I >= tail_K), "ot_mixed_gemm: bad tail map");
   if (rms_flags) {
-    OT_REQUIRE(mode == OT_GEMM_NT && (N == GT || (!(epi & OT_EPI_RMSNORM_BWD) && N % GT == 0)),
-               "ot_mixed_gemm_rms: row-norm epilogues need NT mode and N == %d (OT_EPI_ROW_RSTD: N %% %d == 0)", GT, GT);
-    OT_REQUIRE(N == GT || (rms->workspace && rms->ws_bytes >= ot_mixed_gemm_rms_workspace_size(ntiles, N)),
+    OT_REQUIRE(mode == OT_GEMM_NT && N % GT == 0 &&
+                   (N == GT || !(epi & OT_EPI_RMSNORM_BWD) || (rms->rowdot && rms->rowdot_n > 0)),
+               "ot_mixed_gemm_rms: row-norm epilogues need NT mode and N %% %d == 0 (OT_EPI_RMSNORM_BWD with N > %d: "
+               "the row-dot partials)", GT, GT);
+    OT_REQUIRE(N == GT || !(epi & OT_EPI_ROW_RSTD) ||
+                   (rms->workspace && rms->ws_bytes >= ot_mixed_gemm_rms_workspace_size(ntiles, N)),
                "ot_mixed_gemm_rms: OT_EPI_ROW_RSTD with N > %d needs the workspace", GT);
+    OT_REQUIRE(!(epi & OT_EPI_ROWDOT) || ((epi & OT_EPI_GELU_BWD) && !(epi & ~(OT_EPI_GELU_BWD | OT_EPI_ROWDOT)) &&
+                                          rms->rowdot && rms->rowdot_n == N / GT && bias),
+               "ot_mixed_gemm_rms: OT_EPI_ROWDOT goes with OT_EPI_GELU_BWD only and needs rowdot[rows][N / %d] and "
+               "the bias", GT);
     OT_REQUIRE(!(epi & OT_EPI_ROW_RSTD) || rms->rstd_out, "ot_mixed_gemm_rms: rstd_out missing");
     OT_REQUIRE(!(epi & OT_EPI_RMSNORM_BWD) || (rms->x && rms->gamma && rms->rstd && rms->ldx % 4 == 0),
                "ot_mixed_gemm_rms: RMSNorm backward needs x / gamma / rstd");
@@ -1336,6 +1359,10 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
     p.dres_inv = rms->dres_tail_inv;
     p.dxm = rms->dx_masked; p.lddxm = rms->lddxm;
     if ((epi & OT_EPI_ROW_RSTD) && N > GT) p.rowpart = (float*)rms->workspace;
+    if ((epi & OT_EPI_ROWDOT) || ((epi & OT_EPI_RMSNORM_BWD) && N > GT)) {
+      p.rowdot = rms->rowdot;
+      p.rowdot_n = rms->rowdot_n;
+    }
     if (epi & OT_EPI_RMSNORM_BWD) {
       // without dgamma the partials still need a home: the caller's workspace or nothing
       dgpart = rms->dgamma ? (float*)rms->workspace : nullptr;
@@ -1354,7 +1381,7 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
   auto a16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
   const bool vec_ok = ldc % 4 == 0 && a16(C) && (!(epi & OT_EPI_RESIDUAL) || (ldres % 4 == 0 && a16(res))) &&
                       (!(epi & OT_EPI_GELU_BWD) || (ldaux % 4 == 0 && a16(aux))) &&
-                      (!(epi & OT_EPI_BIAS) || (bias_gstride % 4 == 0 && a16(bias)));
+                      (!(epi & (OT_EPI_BIAS | OT_EPI_ROWDOT)) || (bias_gstride % 4 == 0 && a16(bias)));
   const bool edge = (K % GBK) != 0 || (N % GT) != 0 || !vec_ok;
   OT_REQUIRE(!rms_flags || !edge, "ot_mixed_gemm_rms: needs K %% %d == 0 and 16-B aligned operands", GBK);
   const unsigned nwg = (unsigned)ntiles * p.ntn;
@@ -1376,6 +1403,7 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
   OT_SPEC(true, OT_AX_NONE, OT_EPI_RESIDUAL)
   OT_SPEC(true, OT_AX_NONE, OT_EPI_BIAS)
   OT_SPEC(true, OT_AX_NONE, OT_EPI_GELU_BWD)
+  OT_SPEC(true, OT_AX_NONE, OT_EPI_GELU_BWD | OT_EPI_ROWDOT)
   OT_SPEC(true, OT_AX_NONE, 0)
   OT_SPEC(true, OT_AX_NONE, OT_EPI_ACCUMULATE)
   OT_SPEC(true, OT_AX_NONE, OT_EPI_RESIDUAL | OT_EPI_DROPOUT | OT_EPI_ROW_RSTD)
@@ -1404,6 +1432,7 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
     OT_PSPEC(OT_AX_NONE, OT_EPI_RESIDUAL)
     OT_PSPEC(OT_AX_NONE, OT_EPI_BIAS)
     OT_PSPEC(OT_AX_NONE, OT_EPI_GELU_BWD)
+    OT_PSPEC(OT_AX_NONE, OT_EPI_GELU_BWD | OT_EPI_ROWDOT)
     OT_PSPEC(OT_AX_NONE, 0)
     OT_PSPEC(OT_AX_NONE, OT_EPI_ACCUMULATE)
     OT_PSPEC(OT_AX_NONE, OT_EPI_RESIDUAL | OT_EPI_DROPOUT | OT_EPI_ROW_RSTD)

@@ -147,20 +147,23 @@ def gemm_rms(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish,
              rstd_out: Ptrish = None, eps: float = 1e-6, nx: Ptrish = None, ldnx: int = 0,
              ngamma: Ptrish = None, nrstd: Ptrish = None, dres: Ptrish = None, lddres: int = 0,
              dres_tail: Tuple[int, int] = (0, 0), dx_masked: Ptrish = None, lddxm: int = 0,
-             dgamma: Ptrish = None, accumulate_dgamma: bool = False, device=None, bimg=None) -> None:
+             dgamma: Ptrish = None, accumulate_dgamma: bool = False, device=None, bimg=None,
+             aux: Ptrish = None, ldaux: int = 0, rowdot: Ptrish = None, rowdot_n: int = 0) -> None:
     """ot_mixed_gemm_rms: the GEMM with a row-norm epilogue (OT_EPI_ROW_RSTD: emit the next RMSNorm's
-    rstd; OT_EPI_RMSNORM_BWD: apply the RMSNorm backward to the product, + dres, dgamma)."""
+    rstd; OT_EPI_RMSNORM_BWD: apply the RMSNorm backward to the product, + dres, dgamma, taking
+    <gamma dy, x> from ``rowdot`` when N > 128; OT_EPI_GELU_BWD | OT_EPI_ROWDOT: also write each 128-column
+    tile's sum of dU (aux - bias) into rowdot[row][tile])."""
     need_ws = dgamma is not None or (rstd_out is not None and N > 128)     # dgamma / row-sum partials
     ws = workspace(size('ot_mixed_gemm_rms_workspace_size', ntiles, N) if need_ws else 16,
                    device if device is not None else (C[0] if isinstance(C, tuple) else C).device)
     e = _lib.RmsEpilogue(ptr(rstd_out), float(eps), ptr(nx), ldnx, ptr(ngamma), ptr(nrstd), ptr(dres), lddres,
                          dres_tail[0], dres_tail[1], _sel(dres_tail), ptr(dx_masked), lddxm, ptr(dgamma),
-                         int(accumulate_dgamma), ptr(ws), ws.numel())
+                         int(accumulate_dgamma), ptr(ws), ws.numel(), ptr(rowdot), int(rowdot_n))
     ev = _probe.begin() if _probe is not None else None
     args = (mode, ptr(A), lda, K, ptr(in_rows), a_xform, ptr(rstd), ptr(gamma), ptr(W),
             w_gstride, ldw, N, ptr(tile_group), ntiles, ptr(bias), bias_gstride, ptr(C), ldc, ptr(out_rows), epi,
-            ptr(res), ldres, res_tok, None, 0, seed & 0xFFFFFFFF, site, float(drop), tail[0], tail[1], _sel(tail),
-            ctypes.byref(e))
+            ptr(res), ldres, res_tok, ptr(aux), ldaux, seed & 0xFFFFFFFF, site, float(drop), tail[0], tail[1],
+            _sel(tail), ctypes.byref(e))
     if bimg is not None:
         call('ot_mixed_gemm_rms_img', *args, ptr(bimg[0]), bimg[1], bimg[2], stream())
     else:

@@ -28,7 +28,8 @@ import torch.nn as nn
 from . import _lib
 from . import kernels as K
 from ._lib import (OT_AX_GELU, OT_AX_RMSNORM, OT_EPI_ACCUMULATE, OT_EPI_BIAS, OT_EPI_DROPOUT, OT_EPI_GELU_BWD,
-                   OT_EPI_RESIDUAL, OT_EPI_RMSNORM_BWD, OT_EPI_ROW_RSTD, OT_GEMM_NN, OT_GEMM_NT, NS_FIELD_BYTES)
+                   OT_EPI_RESIDUAL, OT_EPI_RMSNORM_BWD, OT_EPI_ROW_RSTD, OT_EPI_ROWDOT, OT_GEMM_NN, OT_GEMM_NT,
+                   NS_FIELD_BYTES)
 from .config import OneTransConfig, check_pyramid_select, get_model_config
 from .layout import TILE, FlatLayout, RowMap, build_map, head_map, identity_map, layer_maps, round_up
 from .params import init_params, ns_table_offsets
@@ -281,9 +282,18 @@ class _Block(torch.autograd.Function):
                     m.g(f'blk.{l}.b2'), d, a_xform=OT_AX_GELU, accumulate=acc, device=dev,
                     m_rows=maps['tail'].nrows, rowmap=maps['tail'])
         du = torch.empty(B * Kq, f, device=dev)
-        K.gemm(OT_GEMM_NT, dy2, d, d, mt['rows'][1], m.p(f'blk.{l}.w2'), f * d, d, f, mt['tile_group'], nt, du, f,
-               mt['rows'][1], epi=OT_EPI_GELU_BWD, aux=u, ldaux=f, m_rows=maps['tail'].nrows,
-               bimg=m.bimg(f'blk.{l}.w2', 'dgrad'))
+        rowdot = None
+        if m.fuse_bwd2 and not m.fuse_bwd and f % TILE == 0:
+            # d > 128: the FFN2 dgrad also emits rowdot[row][f-tile] = sum dU (U - b1) for the norm2 backward
+            rowdot = torch.empty(B * Kq, f // TILE, device=dev)
+            K.gemm_rms(OT_GEMM_NT, dy2, d, d, mt['rows'][1], m.p(f'blk.{l}.w2'), f * d, d, f, mt['tile_group'], nt,
+                       du, f, mt['rows'][1], epi=OT_EPI_GELU_BWD | OT_EPI_ROWDOT, aux=u, ldaux=f,
+                       bias=m.p(f'blk.{l}.b1'), bias_gstride=f, rowdot=rowdot, rowdot_n=f // TILE,
+                       m_rows=maps['tail'].nrows, device=dev, bimg=m.bimg(f'blk.{l}.w2', 'dgrad'))
+        else:
+            K.gemm(OT_GEMM_NT, dy2, d, d, mt['rows'][1], m.p(f'blk.{l}.w2'), f * d, d, f, mt['tile_group'], nt, du,
+                   f, mt['rows'][1], epi=OT_EPI_GELU_BWD, aux=u, ldaux=f, m_rows=maps['tail'].nrows,
+                   bimg=m.bimg(f'blk.{l}.w2', 'dgrad'))
         with m.side(x1, du, rstd2):
             K.wgrad(x1, d, mt['rows'][1], du, f, mt['rows'][1], d, f, mt, nct, G, m.g(f'blk.{l}.w1'), d * f,
                     m.g(f'blk.{l}.b1'), f, a_xform=OT_AX_RMSNORM, rstd=rstd2, gamma=m.p(f'blk.{l}.norm2'),
@@ -291,13 +301,14 @@ class _Block(torch.autograd.Function):
         # FFN1 dgrad -> norm2 backward + residual; emit mask(dx1) for the attention branch
         dx1 = torch.empty(B * Kq, d, device=dev)
         dyo = torch.empty(B * Kq, d, device=dev) if rate > 0 else dx1
-        if m.fuse_bwd:         # FFN1 dgrad -> norm2 backward in the epilogue (d == 128: the tile holds whole rows)
+        if m.fuse_bwd or rowdot is not None:   # FFN1 dgrad -> norm2 backward in the epilogue
             K.gemm_rms(OT_GEMM_NT, du, f, f, mt['rows'][1], m.p(f'blk.{l}.w1'), d * f, f, d, mt['tile_group'], nt,
                        dx1, d, mt['rows'][1], epi=OT_EPI_RMSNORM_BWD | (OT_EPI_DROPOUT if rate > 0 else 0),
                        seed=seed, site=2 * l, drop=rate, tail=tail, m_rows=maps['tail'].nrows, nx=x1, ldnx=d,
                        ngamma=m.p(f'blk.{l}.norm2'), nrstd=rstd2, dres=dx2, lddres=d,
                        dx_masked=dyo if rate > 0 else None, lddxm=d, dgamma=m.g(f'blk.{l}.norm2'),
-                       accumulate_dgamma=acc, device=dev, bimg=m.bimg(f'blk.{l}.w1', 'dgrad'))
+                       accumulate_dgamma=acc, device=dev, bimg=m.bimg(f'blk.{l}.w1', 'dgrad'),
+                       rowdot=rowdot, rowdot_n=f // TILE if rowdot is not None else 0)
         else:
             dxn2 = torch.empty(B * Kq, d, device=dev)
             K.gemm(OT_GEMM_NT, du, f, f, mt['rows'][1], m.p(f'blk.{l}.w1'), d * f, f, d, mt['tile_group'], nt, dxn2,
@@ -504,11 +515,14 @@ class OneTransModel(nn.Module):
         # fuse the RMSNorms into the neighbouring GEMM epilogues.  d == 128 (a tile holds whole rows, every
         # matmul mode): the forward rstd (Wo / FFN2 epilogues) and the norm backward (FFN1 / QKV dgrad
         # epilogues).  d = 256, 512, ...: the forward rstd only, on the split-mode plane GEMM (per-tile row
-        # sums + a finishing pass, ``fuse_with``); the norm backward stays row-wise there — a row-complete
-        # epilogue (each workgroup looping over the row's column tiles, two passes) measured slower than
-        # the row-wise kernel at T
+        # sums + a finishing pass, ``fuse_with``).  The norm2 backward is fused at every d % 128 == 0
+        # (``fuse_bwd2``): the FFN2 dgrad epilogue emits per-tile partials of sum_f dU_f (U_f - b1_f)
+        # = rstd2 <gamma2 dy, x1>, the one row reduction the FFN1 dgrad epilogue cannot see.  norm1's
+        # backward stays row-wise at d > 128 — a row-complete epilogue (each workgroup looping over the
+        # row's column tiles, two passes) measured slower than the row-wise kernel at T
         self.fuse_norms = (config.hidden_dim % TILE == 0 and os.environ.get('ONETRANS_FUSE_NORMS', '1') != '0')
         self.fuse_bwd = self.fuse_norms and config.hidden_dim == TILE
+        self.fuse_bwd2 = self.fuse_norms and os.environ.get('ONETRANS_FUSE_NORM2_BWD', '1') != '0'
         # block weight gradients run on a second stream, overlapping the dgrad chain
         self.overlap_wgrad = os.environ.get('ONETRANS_OVERLAP_WGRAD', '1') != '0'
         self._side = None

@@ -56,7 +56,7 @@ CASES = {
     # d = 256 (hd 64, as T/C3/C5): weights of >= 8 output tiles take the larger wgrad chunk budget
     'criteo_d256_pyramid': lambda: small_criteo('tail', pyramid=True, layers=2, d=256, H=4, f=1024, Lns=4,
                                                 seq_lens=(12, 9, 7)),
-    # d = 512 (C5's width, hd 64): the row-complete plane GEMM's norm epilogues span 4 column tiles
+    # d = 512 (C5's width, hd 64): the fused norm epilogues span 4 column tiles (per-tile partials)
     'criteo_d512_pyramid': lambda: small_criteo('tail', pyramid=True, layers=2, d=512, H=8, f=1024, Lns=4,
                                                 seq_lens=(12, 9, 7)),
 }
@@ -197,8 +197,8 @@ def test_auc_parity(dev):
 def test_fused_norms_match_unfused(dev, case, B):
     """The GEMM-epilogue RMSNorms give the same loss and gradients as the row-wise kernels: d == 128 (one
     tile holds whole rows: forward rstd and norm backward) and d = 256 / 512 (forward rstd from the plane
-    GEMM's per-tile row sums over 2 / 4 column tiles), dropout on, pyramid tail maps, and a batch one
-    row past whole tiles."""
+    GEMM's per-tile row sums over 2 / 4 column tiles; norm2 backward from the FFN2 dgrad's per-tile
+    sum dU (U - b1) partials), dropout on, pyramid tail maps, and a batch one row past whole tiles."""
     cfg = CASES[case]()
     P, model, batch = setup(cfg, B, dev)
     assert model.fuse_with(('blk.0.wo', 'fwd'), ('blk.0.w2', 'fwd'))
@@ -208,6 +208,7 @@ def test_fused_norms_match_unfused(dev, case, B):
     for fuse in (True, False):
         model.fuse_norms = fuse
         model.fuse_bwd = fuse and cfg.hidden_dim == 128
+        model.fuse_bwd2 = fuse
         model.flat.grad.zero_()
         model._step = 0
         loss = keras_bce_loss(y, model.forward_probs(ns_t(ns, dev), ns_t(seq, dev), training=True))

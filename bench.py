@@ -251,7 +251,10 @@ def main():
         torch.cuda.synchronize()
         K.set_probe(None)
         model.overlap_wgrad = overlap
-        rep = probe.report(args.probe_steps)
+        mm = K.matmul_mode()
+        gpk = (BF16_MFMA_PEAK_TFLOPS / SPLIT_TERMS if mm == 'split' else
+               BF16_MFMA_PEAK_TFLOPS if mm == 'bf16' else FP32_MFMA_PEAK_TFLOPS)
+        rep = probe.report(args.probe_steps, gpk, HBM_PEAK_GBS)
 
     if rank != 0:
         if world > 1:
@@ -308,15 +311,32 @@ def main():
             gpeak = FP32_MFMA_PEAK_TFLOPS
             gkern = 'mixed_gemm_kernel + wgrad_kernel (native f32 MFMA)'
         res['matmul'] = K.matmul_mode()
-        res['roofline'] = {'bound': 'mfma', 'kernel': gkern,
-                           'achieved': round(dom['tflops'], 2), 'peak': gpeak, 'unit': 'TFLOP/s',
-                           'frac': round(dom['tflops'] / gpeak, 4), 'traffic': traffic,
+        # the family's binding roof: each launch is floored by max(flops / MFMA peak, bytes / HBM peak);
+        # 'bound' is the roof that holds the larger share of that floor over the family's launches
+        # (C2's K = 128 GEMMs sit right of the ridge on HBM; C5's bf16 GEMMs on MFMA)
+        hbm_bound = dom['floor_hbm_ms_per_step'] > dom['floor_mfma_ms_per_step']
+        mfma = {'achieved': round(dom['tflops'], 2), 'peak': gpeak, 'unit': 'TFLOP/s',
+                'frac': round(dom['tflops'] / gpeak, 4)}
+        hbm = {'achieved': round(dom['gbs'], 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+               'frac': round(dom['gbs'] / HBM_PEAK_GBS, 4)}
+        res['roofline'] = {'bound': 'hbm' if hbm_bound else 'mfma', 'kernel': gkern,
+                           **(hbm if hbm_bound else mfma), 'traffic': traffic,
                            'traffic_unit': 'HBM bytes per launch (PMC FETCH_SIZE + WRITE_SIZE, calibrated)',
                            'traffic_source': tsrc,
-                           'avg_launch_us': round(dom['avg_us'], 2), 'launches_per_step': dom['launches_per_step'],
+                           'algorithmic_bytes_per_launch': round(dom['gbyte_per_launch'] * 1e9),
                            'gflop_per_launch': round(dom['gflop_per_launch'], 3),
+                           'avg_launch_us': round(dom['avg_us'], 2), 'launches_per_step': dom['launches_per_step'],
+                           'mfma': mfma, 'hbm': hbm,
+                           'floor_ms_per_step': round(dom['floor_ms_per_step'], 3),
+                           'floor_frac': round(dom['floor_ms_per_step'] / dom['ms_per_step'], 4),
+                           'floor_split_ms': {'mfma_bound_launches': round(dom['floor_mfma_ms_per_step'], 3),
+                                              'hbm_bound_launches': round(dom['floor_hbm_ms_per_step'], 3)},
                            'measured': f'HIP events per launch, {args.probe_steps}-step pass after the timed region, '
-                                       'wgrad side stream off (standalone kernel durations)'}
+                                       'wgrad side stream off (standalone kernel durations); algorithmic bytes = '
+                                       'A (+ rstd) read once, C written once, each [M, N] epilogue operand read once, '
+                                       'wgrad A + D read once and dW written once (weights of the forward / dgrad '
+                                       'launches left out); floor = sum over launches of max(flops / MFMA peak, '
+                                       'bytes / HBM peak), floor_frac = floor / measured family time'}
         res['kernel_time_ms_per_step'] = {k: round(v['ms_per_step'], 3) for k, v in rep['families'].items()}
         # north_star "MFMA utilisation on OneTrans attention" (standalone attention at
         # L~140 is memory-heavy, so the block's matrix work is reported beside the core): achieved

@@ -28,16 +28,16 @@ class Probe:
         ev.record()
         return ev
 
-    def end(self, family: str, flops: float, ev0, label: str = '') -> None:
+    def end(self, family: str, flops: float, ev0, label: str = '', nbytes: float = 0.0) -> None:
         ev1 = torch.cuda.Event(enable_timing=True)
         ev1.record()
-        self.recs.append((family, flops, ev0, ev1, label))
+        self.recs.append((family, flops, ev0, ev1, label, nbytes))
 
     def by_label(self, steps: int):
         """Per-launch-shape breakdown: {label: (launches/step, avg us, TF/s)} (tools/gemm_shapes.py)."""
         torch.cuda.synchronize()
         agg = {}
-        for (f, fl, a, b, lab) in self.recs:
+        for (f, fl, a, b, lab, _) in self.recs:
             d = agg.setdefault(f'{f} {lab}', [0, 0.0, 0.0])
             d[0] += 1
             d[1] += a.elapsed_time(b)
@@ -45,23 +45,46 @@ class Probe:
         return {k: (n / steps, 1e3 * ms / n, fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0)
                 for k, (n, ms, fl) in agg.items()}
 
-    def report(self, steps: int):
-        torch.cuda.synchronize()
+    def report(self, steps: int, mfma_peak_tflops: float = 0.0, hbm_peak_gbs: float = 0.0):
+        """Per family: time, launches, algorithmic FLOPs and bytes per launch; with the peaks given, also
+        the family's roofline floor sum_i max(flops_i / mfma peak, bytes_i / HBM peak) over its launches
+        (each launch bound by whichever roof it meets first) and the MFMA / HBM parts of it."""
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
         fam = {}
-        for (f, fl, a, b, _) in self.recs:
-            d = fam.setdefault(f, {'ms': 0.0, 'flops': 0.0, 'n': 0})
+        for (f, fl, a, b, _, nb) in self.recs:
+            d = fam.setdefault(f, {'ms': 0.0, 'flops': 0.0, 'bytes': 0.0, 'n': 0, 'floor': 0.0, 'fl_mfma': 0.0,
+                                   'fl_hbm': 0.0})
             d['ms'] += a.elapsed_time(b)
             d['flops'] += fl
+            d['bytes'] += nb
             d['n'] += 1
+            if mfma_peak_tflops > 0 and hbm_peak_gbs > 0:
+                tm, th = fl / (mfma_peak_tflops * 1e9), nb / (hbm_peak_gbs * 1e6)     # ms
+                d['floor'] += max(tm, th)
+                d['fl_mfma' if tm >= th else 'fl_hbm'] += max(tm, th)
         out = {}
         for f, d in fam.items():
             out[f] = {'ms_per_step': d['ms'] / steps, 'avg_us': 1e3 * d['ms'] / d['n'],
                       'launches_per_step': d['n'] / steps, 'gflop_per_launch': d['flops'] / d['n'] / 1e9,
-                      'tflops': d['flops'] / (d['ms'] * 1e-3) / 1e12 if d['ms'] > 0 else 0.0}
+                      'gbyte_per_launch': d['bytes'] / d['n'] / 1e9,
+                      'tflops': d['flops'] / (d['ms'] * 1e-3) / 1e12 if d['ms'] > 0 else 0.0,
+                      'gbs': d['bytes'] / (d['ms'] * 1e-3) / 1e9 if d['ms'] > 0 else 0.0,
+                      'floor_ms_per_step': d['floor'] / steps, 'floor_mfma_ms_per_step': d['fl_mfma'] / steps,
+                      'floor_hbm_ms_per_step': d['fl_hbm'] / steps}
         return {'families': out}
 
 
 _probe = None
+
+
+def gemm_bytes(M: int, K: int, N: int, a_xform: int, epi: int) -> float:
+    """Algorithmic HBM bytes of one forward / dgrad GEMM launch over M valid rows: A read once (+ its
+    rstd for the RMSNorm prologue), C written once, each [M, N] epilogue operand read once.  Weights
+    (at most a few MB of L2-resident images) are left out."""
+    mn = (1 + bool(epi & _lib.OT_EPI_RESIDUAL) + bool(epi & _lib.OT_EPI_GELU_BWD)
+          + bool(epi & _lib.OT_EPI_ACCUMULATE))
+    return 4.0 * M * (K + (a_xform == _lib.OT_AX_RMSNORM)) + 4.0 * M * N * mn
 
 
 def set_probe(p) -> None:
@@ -135,8 +158,9 @@ def gemm(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish, w_g
     else:
         call('ot_mixed_gemm', *args, stream())
     if ev is not None:
-        _probe.end('mixed_gemm', 2.0 * (m_rows or ntiles * 128) * K * N, ev,
-                   f'gemm mode{mode} ax{a_xform} epi{epi} M{m_rows or ntiles * 128} K{K} N{N}')
+        M = m_rows or ntiles * 128
+        _probe.end('mixed_gemm', 2.0 * M * K * N, ev, f'gemm mode{mode} ax{a_xform} epi{epi} M{M} K{K} N{N}',
+                   gemm_bytes(M, K, N, a_xform, epi))
 
 
 def gemm_rms(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish, w_gstride: int, ldw: int,
@@ -169,8 +193,11 @@ def gemm_rms(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish,
     else:
         call('ot_mixed_gemm_rms', *args, stream())
     if ev is not None:
-        _probe.end('mixed_gemm', 2.0 * (m_rows or ntiles * 128) * K * N, ev,
-                   f'gemm_rms mode{mode} ax{a_xform} epi{epi} M{m_rows or ntiles * 128} K{K} N{N}')
+        M = m_rows or ntiles * 128
+        extra = (nx is not None) + (dres is not None) + (dx_masked is not None)   # norm-backward operands
+        _probe.end('mixed_gemm', 2.0 * M * K * N, ev, f'gemm_rms mode{mode} ax{a_xform} epi{epi} M{M} K{K} N{N}',
+                   gemm_bytes(M, K, N, a_xform, epi) + 4.0 * M * N * extra
+                   + 4.0 * M * ((rstd_out is not None) + (nrstd is not None)))
 
 
 def wgrad(A: Ptrish, lda: int, a_rows: Ptrish, D: Ptrish, ldd: int, d_rows: Ptrish, K: int, N: int, rmap_dev,
@@ -190,7 +217,8 @@ def wgrad(A: Ptrish, lda: int, a_rows: Ptrish, D: Ptrish, ldd: int, d_rows: Ptri
          ptr(d_rows), K, N, ptr(rmap_dev['chunks']), nchunks, ptr(rmap_dev['gchunk']), ngroups, ptr(dW),
          dw_gstride, ptr(db), db_gstride, int(accumulate), ptr(ws), ws.numel(), stream())
     if ev is not None:
-        _probe.end('mixed_gemm', 2.0 * m_rows * K * N, ev, f'wgrad ax{a_xform} M{m_rows} K{K} N{N} ch{nchunks}')
+        _probe.end('mixed_gemm', 2.0 * m_rows * K * N, ev, f'wgrad ax{a_xform} M{m_rows} K{K} N{N} ch{nchunks}',
+                   4.0 * m_rows * (K + N + (a_xform == _lib.OT_AX_RMSNORM)) + 4.0 * ngroups * K * N)
 
 
 def transpose_banks(src, dst, banks_dev, nbanks, total_tiles) -> None:

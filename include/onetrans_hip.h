@@ -213,6 +213,14 @@ size_t ot_attn_bwd_workspace_size(int B, int H, int K);
 int ot_attn_bwd(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
                 int B, int H, int I, int K, const int32_t* qpos, int head_dim, float* dqkv, float* delta_ws,
                 void* stream);
+/* ot_attn_bwd with a sized workspace: given ot_attn_bwd_ex_workspace_size(B, H, I, K, head_dim,
+ * qpos != NULL) bytes, the bf16-mode backward splits each (sample, head)'s key blocks over several
+ * waves when B*H alone cannot fill the chip (C5: 4 slices), their dQ partials summed in a fixed
+ * order (deterministic); with ot_attn_bwd_workspace_size bytes it runs as ot_attn_bwd. */
+size_t ot_attn_bwd_ex_workspace_size(int B, int H, int I, int K, int head_dim, int selected);
+int ot_attn_bwd_ex(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
+                   int B, int H, int I, int K, const int32_t* qpos, int head_dim, float* dqkv, void* workspace,
+                   size_t ws_bytes, void* stream);
 
 /* Two-stage cached serving (paper §3.5.1; replaces the reference's defective cache path
  * model.py:94-98, 359-381, D6): candidate c (request req[c]) attends with the last Kq of its n

@@ -43,6 +43,10 @@ struct AttnArgs {
   int B, H, I, K;
   float scale;
   const int32_t* qpos;      // kept query positions [B*K] (ot_pyramid_select) or null: I - K + j
+  // key-grouped backward (attn_bwd_group_kernel): kslices workgroups per (sample, head), workgroup s
+  // owning key blocks kgroup*s .. kgroup*s + kgroup-1; slice 0 writes dQ into dqkv, slice s > 0 into
+  // dqpart[s - 1] ([B*K][d]), summed into dqkv by attn_dq_reduce_kernel
+  int kslices, kgroup; float* dqpart;
 };
 
 // position of kept query j (< K) of the sample whose qpos slice is qp (null: the tail rule)
@@ -793,7 +797,10 @@ void attn_bwd_kernel(AttnArgs p) {
 //                                  P / dS, which are the B operands straight from the registers)
 //   dQ^T += K^T dS^T              A = K^T from the [key][dim] image, B = dS^T from a [key][query]
 //                                  image the lanes write as 8-byte runs (k = key, natural order)
-// Planes: 3 (split, TERMS = 6) or 1 (bf16).  LDS per wave: (3 x 32 x HD + 32 x 32) x 2 B x planes.
+// K and V fragments (the B operands of S and dP) are re-read from the wave's [key][dim] plane images
+// each pair instead of living in registers for the whole key block: at HD 64 the kernel fits 256
+// registers, i.e. 2 waves / SIMD instead of 1 (C5 backward 17.4 -> see DESIGN.md).
+// Planes: 3 (split, TERMS = 6) or 1 (bf16).  LDS per wave: (4 x 32 x HD + 32 x 32) x 2 B x planes.
 
 // two ds_read_b64_tr_b16 reads -> one 32x32x16 operand fragment: elements 0-3 from rows ra .. ra+3,
 // 4-7 from rows rb .. rb+3, the lane's column colbase + (lane & 31) (row stride rs bytes)
@@ -809,10 +816,10 @@ __device__ __forceinline__ u32x4 tr16_frag(const char* img, int rs, int ra, int 
 }
 
 template <int HD, int TERMS>
-constexpr int BWDS_LDS() { return (TERMS == 1 ? 1 : 3) * (3 * 32 * HD + 32 * 32) * 2; }
+constexpr int BWDS_LDS() { return (TERMS == 1 ? 1 : 3) * (4 * 32 * HD + 32 * 32) * 2; }
 
 template <int HD, int TERMS, bool SEL, int WAVES>
-__global__ __launch_bounds__(64 * WAVES) void attn_bwd_split_kernel(AttnArgs p) {
+__global__ __launch_bounds__(64 * WAVES, TERMS == 1 ? 2 : 1) void attn_bwd_split_kernel(AttnArgs p) {
   static_assert(HD == 32 || HD == 64, "split backward: HD 32 or 64");
   constexpr int NPL = TERMS == 1 ? 1 : 3;
   constexpr int NS = HD / 16;                          // k-steps over the head dim
@@ -824,6 +831,7 @@ __global__ __launch_bounds__(64 * WAVES) void attn_bwd_split_kernel(AttnArgs p) 
   char* qimg = kimg + NPL * IMG;
   char* oimg = qimg + NPL * IMG;
   char* simg = oimg + NPL * IMG;
+  char* vimg = simg + NPL * SIMG;
   const int pair = blockIdx.x * WAVES + (threadIdx.x >> 6);
   if (pair >= p.B * p.H) return;                       // wave-uniform
   const int b = pair / p.H, h = pair % p.H;
@@ -845,18 +853,20 @@ __global__ __launch_bounds__(64 * WAVES) void attn_bwd_split_kernel(AttnArgs p) 
   for (int kb = 0; kb < nkb; ++kb) {
     const int key0 = 32 * kb;
     const int kpos = key0 + li;
-    u32x4 kB[NS][3], vB[NS][3];
     {
       float kf[HD / 2], vf[HD / 2];
       load_frag<HD>(kf, Kp, p.ld, kpos, I, hh);        // rows >= I: zeros (masked below)
       load_frag<HD>(vf, V, p.ld, kpos, I, hh);
 #pragma unroll
       for (int t = 0; t < NS; ++t) {
-        split8t<TERMS>(kf + 8 * t, kB[t]);
-        split8t<TERMS>(vf + 8 * t, vB[t]);
+        u32x4 kB[3], vB[3];
+        split8t<TERMS>(kf + 8 * t, kB);
+        split8t<TERMS>(vf + 8 * t, vB);
 #pragma unroll
-        for (int pl = 0; pl < NPL; ++pl)
-          *reinterpret_cast<u32x4*>(kimg + pl * IMG + (li * HD + (HD / 2) * hh + 8 * t) * 2) = kB[t][pl];
+        for (int pl = 0; pl < NPL; ++pl) {
+          *reinterpret_cast<u32x4*>(kimg + pl * IMG + (li * HD + (HD / 2) * hh + 8 * t) * 2) = kB[pl];
+          *reinterpret_cast<u32x4*>(vimg + pl * IMG + (li * HD + (HD / 2) * hh + 8 * t) * 2) = vB[pl];
+        }
       }
     }
     f32x16 dk[NB(HD)], dv[NB(HD)];
@@ -897,8 +907,14 @@ __global__ __launch_bounds__(64 * WAVES) void attn_bwd_split_kernel(AttnArgs p) 
       for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
 #pragma unroll
       for (int t = 0; t < NS; ++t) {
-        s = mfma_terms<TERMS>(qA[t], kB[t], s);         // S: row = query, col = key
-        dp = mfma_terms<TERMS>(oA[t], vB[t], dp);       // dP
+        u32x4 kB[3], vB[3];                              // this lane's key row, dims 8t.. (its own writes)
+#pragma unroll
+        for (int pl = 0; pl < NPL; ++pl) {
+          kB[pl] = *reinterpret_cast<const u32x4*>(kimg + pl * IMG + (li * HD + (HD / 2) * hh + 8 * t) * 2);
+          vB[pl] = *reinterpret_cast<const u32x4*>(vimg + pl * IMG + (li * HD + (HD / 2) * hh + 8 * t) * 2);
+        }
+        s = mfma_terms<TERMS>(qA[t], kB, s);            // S: row = query, col = key
+        dp = mfma_terms<TERMS>(oA[t], vB, dp);          // dP
       }
       // softmax gradient (rows = queries acc_row(r, hh), column = this lane's key)
 #pragma unroll
@@ -997,6 +1013,236 @@ __global__ __launch_bounds__(64 * WAVES) void attn_bwd_split_kernel(AttnArgs p) 
         }
     }
   }
+}
+
+// Key-grouped bf16 backward for long tails (C5: 33 key blocks per (sample, head)).  The per-pair
+// kernel above walks every key block with one wave and re-reads the (sample, head)'s Q / dO rows and
+// read-modify-writes its dQ rows once per key block — at L = 1036 that is ~70 GB of L2-missing
+// traffic per layer.  Here a workgroup of NW waves owns NW consecutive key blocks (one per wave: dK /
+// dV accumulators in registers) and streams the query blocks once: each query block's Q / dO rows are
+// loaded by the whole workgroup into shared bf16 images (the next block's loads in flight during the
+// current block's MFMAs), every wave runs S / dP / softmax gradient / dV / dK for its key block, and
+// the NW dQ contributions are summed through LDS in a fixed order and stored once per (slice, query
+// block) — slice 0 into dqkv, slice s > 0 into dqpart[s - 1] (attn_dq_reduce_kernel adds them).
+// Tail queries only (no selection map), TERMS = 1 (OT_MATMUL_BF16).
+template <int HD, int NW>
+constexpr int BWDG_LDS() { return 2 * 32 * HD * 2 + NW * (2 * 32 * HD * 2 + 32 * 32 * 2) + NW * 32 * HD * 4; }
+
+template <int HD, int NW>
+__global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kernel(AttnArgs p) {
+  static_assert(HD == 64 || HD == 32, "grouped backward: HD 32 or 64");
+  constexpr int NS = HD / 16;                          // k-steps over the head dim
+  constexpr int IMG = 32 * HD * 2;                     // one [32][HD] bf16 image
+  constexpr int SIMG = 32 * 32 * 2;
+  constexpr int NT = 64 * NW;
+  constexpr int F4 = 32 * HD / 4;                      // float4 per [32][HD] block
+  constexpr int PT = (F4 + NT - 1) / NT;               // float4 per thread per operand
+  extern __shared__ __attribute__((aligned(16))) char lds_g[];
+  const int t = threadIdx.x, lane = t & 63, li = lane & 31, hh = lane >> 5, w = t >> 6;
+  char* qimg = lds_g;                                  // shared [query][dim] images of the query block
+  char* oimg = qimg + IMG;
+  char* kimg = oimg + IMG + w * (2 * IMG + SIMG);      // this wave's key block
+  char* vimg = kimg + IMG;
+  char* simg = vimg + IMG;                             // this wave's dS^T [key][query]
+  float* dqbuf = reinterpret_cast<float*>(lds_g + 2 * IMG + NW * (2 * IMG + SIMG));   // [NW][NB][16][64]
+  const int S = p.kslices;
+  const int pair = blockIdx.x / S, slice = blockIdx.x - pair * S;
+  const int b = pair / p.H, h = pair % p.H;
+  const int I = p.I, K = p.K, q_off = I - K, KP = attn_kpad(K);
+  const int64_t tok0 = (int64_t)b * I;
+  const float* Q = p.qkv + tok0 * p.ld + h * HD;
+  const float* Kp = Q + p.d;
+  const float* V = Q + 2 * p.d;
+  const float* dO = p.dout + (int64_t)b * K * p.d + h * HD;
+  const float* lsep = p.delta + (int64_t)pair * KP;
+  const float* dltp = p.delta + ((int64_t)p.B * p.H + pair) * KP;
+  float* dK = p.dqkv + tok0 * p.ld + p.d + h * HD;
+  float* dV = dK + p.d;
+  const int nqb = KP / 32;
+  const int kb = slice * NW + w;                       // this wave's key block (>= nkb: an idle wave, P = 0)
+  const int key0 = 32 * kb;
+  const int kpos = key0 + li;
+  {
+    float kf[HD / 2], vf[HD / 2];
+    load_frag<HD>(kf, Kp, p.ld, kpos, I, hh);          // rows >= I: zeros (masked below)
+    load_frag<HD>(vf, V, p.ld, kpos, I, hh);
+#pragma unroll
+    for (int st = 0; st < NS; ++st) {
+      u32x4 kB[3], vB[3];
+      split8t<1>(kf + 8 * st, kB);
+      split8t<1>(vf + 8 * st, vB);
+      *reinterpret_cast<u32x4*>(kimg + (li * HD + (HD / 2) * hh + 8 * st) * 2) = kB[0];
+      *reinterpret_cast<u32x4*>(vimg + (li * HD + (HD / 2) * hh + 8 * st) * 2) = vB[0];
+    }
+  }
+  f32x16 dk[NB(HD)], dv[NB(HD)];
+#pragma unroll
+  for (int c = 0; c < NB(HD); ++c)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { dk[c][r] = 0.f; dv[c][r] = 0.f; }
+  int qbs = 32 * slice * NW - q_off;                   // first query block that sees the group's first key
+  qbs = qbs < 0 ? 0 : qbs / 32;
+  // cooperative Q / dO block loads: thread t takes float4 e = t + NT i of the [32][HD] block
+  f32x4 pq[PT], po[PT];
+  auto load_q = [&](int qb) {
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      const int e = t + NT * i;
+      const int row = e / (HD / 4), c4 = e % (HD / 4);
+      const int j = 32 * qb + row;
+      const int jj = j < K ? j : K - 1;                // padded queries: a real row (lse = +inf masks it)
+      pq[i] = e < F4 ? *reinterpret_cast<const f32x4*>(Q + (int64_t)(q_off + jj) * p.ld + 4 * c4) : f32x4{0.f, 0.f, 0.f, 0.f};
+      po[i] = e < F4 ? *reinterpret_cast<const f32x4*>(dO + (int64_t)jj * p.d + 4 * c4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto store_q = [&]() {
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      const int e = t + NT * i;
+      if (e < F4) {
+        *reinterpret_cast<u32x2*>(qimg + e * 8) = bf16_rne4(pq[i]);
+        *reinterpret_cast<u32x2*>(oimg + e * 8) = bf16_rne4(po[i]);
+      }
+    }
+  };
+  load_q(qbs);
+  for (int qb = qbs; qb < nqb; ++qb) {
+    const int q0 = 32 * qb;
+    store_q();
+    __syncthreads();                                   // images of block qb (and the previous reduce done)
+    if (qb + 1 < nqb) load_q(qb + 1);                  // in flight during this block's MFMAs
+    u32x4 qA[NS][3], oA[NS][3];
+#pragma unroll
+    for (int st = 0; st < NS; ++st) {
+      qA[st][0] = *reinterpret_cast<const u32x4*>(qimg + (li * HD + (HD / 2) * hh + 8 * st) * 2);
+      oA[st][0] = *reinterpret_cast<const u32x4*>(oimg + (li * HD + (HD / 2) * hh + 8 * st) * 2);
+    }
+    f32x16 s, dp;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
+#pragma unroll
+    for (int st = 0; st < NS; ++st) {
+      u32x4 kB[3], vB[3];
+      kB[0] = *reinterpret_cast<const u32x4*>(kimg + (li * HD + (HD / 2) * hh + 8 * st) * 2);
+      vB[0] = *reinterpret_cast<const u32x4*>(vimg + (li * HD + (HD / 2) * hh + 8 * st) * 2);
+      s = mfma_terms<1>(qA[st], kB, s);                // S: row = query, col = key
+      dp = mfma_terms<1>(oA[st], vB, dp);              // dP
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 l4 = *reinterpret_cast<const f32x4*>(lsep + q0 + 8 * g + 4 * hh);
+      const f32x4 d4 = *reinterpret_cast<const f32x4*>(dltp + q0 + 8 * g + 4 * hh);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int r = 4 * g + e, j = q0 + 8 * g + 4 * hh + e;
+        const float ex = __expf(s[r] * p.scale - l4[e]);
+        const float P = kpos <= q_off + j ? ex : 0.f;
+        s[r] = P;
+        dp[r] = P * (dp[r] - d4[e]) * p.scale;          // dS, pre-scaled by 1/sqrt(hd)
+      }
+    }
+    u32x4 pB[2][3], sB[2][3];
+    {
+      float pv[16], sv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { pv[r] = s[r]; sv[r] = dp[r]; }
+      split8t<1>(pv, pB[0]); split8t<1>(pv + 8, pB[1]);
+      split8t<1>(sv, sB[0]); split8t<1>(sv + 8, sB[1]);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const u32x4 wv = sB[g >> 1][0];
+        const u32x2 two = (g & 1) ? u32x2{wv.z, wv.w} : u32x2{wv.x, wv.y};
+        *reinterpret_cast<u32x2*>(simg + (li * 32 + 8 * g + 4 * hh) * 2) = two;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int c = 0; c < NB(HD); ++c)
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        u32x4 oT[3], qT[3];
+        oT[0] = tr16_frag(oimg, HD * 2, 16 * st + 4 * hh, 16 * st + 8 + 4 * hh, 32 * c, lane);
+        qT[0] = tr16_frag(qimg, HD * 2, 16 * st + 4 * hh, 16 * st + 8 + 4 * hh, 32 * c, lane);
+        dv[c] = mfma_terms<1>(oT, pB[st], dv[c]);      // dV^T += dO^T P
+        dk[c] = mfma_terms<1>(qT, sB[st], dk[c]);      // dK^T += Q^T dS
+      }
+    f32x16 dq[NB(HD)];
+#pragma unroll
+    for (int c = 0; c < NB(HD); ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dq[c][r] = 0.f;
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      u32x4 sT[3];
+      sT[0] = tr16_frag(simg, 64, 16 * st + 8 * hh, 16 * st + 8 * hh + 4, 0, lane);
+#pragma unroll
+      for (int c = 0; c < NB(HD); ++c) {
+        u32x4 kT[3];
+        kT[0] = tr16_frag(kimg, HD * 2, 16 * st + 8 * hh, 16 * st + 8 * hh + 4, 32 * c, lane);
+        dq[c] = mfma_terms<1>(kT, sT, dq[c]);           // dQ^T += K^T dS^T
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < NB(HD); ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dqbuf[((w * NB(HD) + c) * 16 + r) * 64 + lane] = dq[c][r];
+    __syncthreads();                                   // every wave's dQ contribution is in LDS
+    // fixed-order sum over the NW waves: float4 u = (lane, c, g) -> query q0 + (lane & 31), dims
+    // 32c + 8g + 4 (lane >> 5) + 0..3; stored once per (slice, query block)
+    for (int u = t; u < NB(HD) * 4 * 64; u += NT) {
+      const int ln = u & 63, cg = u >> 6, c = cg >> 2, g = cg & 3;
+      f32x4 a = {0.f, 0.f, 0.f, 0.f};
+      for (int v = 0; v < NW; ++v) {
+        const float* bb = dqbuf + ((v * NB(HD) + c) * 16 + 4 * g) * 64 + ln;
+        a += f32x4{bb[0], bb[64], bb[128], bb[192]};
+      }
+      const int jq = q0 + (ln & 31);
+      const int dd = 32 * c + 8 * g + 4 * (ln >> 5);
+      if (jq < K && dd < HD) {
+        float* dst = slice == 0 ? p.dqkv + (tok0 + q_off + jq) * p.ld + h * HD + dd
+                                : p.dqpart + ((int64_t)(slice - 1) * p.B * K + (int64_t)b * K + jq) * p.d + h * HD + dd;
+        *reinterpret_cast<f32x4*>(dst) = a;
+      }
+    }
+  }
+  if (kpos < I) {
+#pragma unroll
+    for (int c = 0; c < NB(HD); ++c)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int dd = 32 * c + 8 * g + 4 * hh;
+        if (dd < HD) {
+          f32x4 a = {dk[c][4 * g], dk[c][4 * g + 1], dk[c][4 * g + 2], dk[c][4 * g + 3]};
+          f32x4 v = {dv[c][4 * g], dv[c][4 * g + 1], dv[c][4 * g + 2], dv[c][4 * g + 3]};
+          *reinterpret_cast<f32x4*>(dK + (int64_t)kpos * p.ld + dd) = a;
+          *reinterpret_cast<f32x4*>(dV + (int64_t)kpos * p.ld + dd) = v;
+        }
+      }
+  }
+}
+
+// dQ of the key-grouped backward: dqkv[q row] += sum over slices s = 1 .. S-1 whose first key block
+// (kgroup * s) the query's block sees of dqpart[s - 1] (fixed slice order: deterministic).  One thread
+// per float4 of the [B*K, d] tail dQ.
+__global__ __launch_bounds__(256) void attn_dq_reduce_kernel(AttnArgs p) {
+  const int64_t e4 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  const int64_t n = (int64_t)p.B * p.K * p.d;
+  if (e4 >= n) return;
+  const int64_t row = e4 / p.d;
+  const int col = (int)(e4 - row * p.d);
+  const int b = (int)(row / p.K), j = (int)(row - (int64_t)b * p.K);
+  const int q_off = p.I - p.K, qb = j / 32;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  bool any = false;
+  for (int s = 1; s < p.kslices; ++s) {
+    const int f = 32 * p.kgroup * s - q_off;           // first query block that sees the slice's first key
+    if ((f < 0 ? 0 : f / 32) > qb) break;              // later slices start later still
+    acc += *reinterpret_cast<const f32x4*>(p.dqpart + (int64_t)(s - 1) * n + e4);
+    any = true;
+  }
+  if (!any) return;
+  f32x4* dst = reinterpret_cast<f32x4*>(p.dqkv + ((int64_t)b * p.I + q_off + j) * p.ld + col);
+  *dst = *dst + acc;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1293,9 +1539,50 @@ extern "C" size_t ot_attn_bwd_workspace_size(int B, int H, int K) {
   return (2 * (size_t)B * H + B) * attn_kpad(K) * sizeof(float);     // lse, delta (+ padded qpos)
 }
 
+// key-grouped bf16 backward (attn_bwd_group_kernel): long tails only — at C2-like lengths (<= 8 key
+// blocks) the per-pair kernel re-reads little and has more parallelism
+// (4 waves per workgroup measured faster than 8 at C5: 7.19 vs 8.66 ms per layer, 18.36 per pair)
+static int g_attn_bwd_group = [] {
+  const char* e = getenv("ONETRANS_ATTN_BWD_GROUP");
+  return e ? atoi(e) : 4;
+}();
+static int attn_bwd_kgroup(int I, int K, int head_dim, bool sel) {
+  if (sel || K <= SMALL_K || ot_get_matmul_mode() != OT_MATMUL_BF16 || (head_dim != 32 && head_dim != 64)) return 0;
+  if ((I + 31) / 32 <= 8 || (g_attn_bwd_group != 4 && g_attn_bwd_group != 8)) return 0;
+  return g_attn_bwd_group;
+}
+static int attn_bwd_kslices(int B, int H, int I, int K, int head_dim, bool sel) {
+  const int g = attn_bwd_kgroup(I, K, head_dim, sel);
+  return g ? ((I + 31) / 32 + g - 1) / g : 1;
+}
+
+extern "C" size_t ot_attn_bwd_ex_workspace_size(int B, int H, int I, int K, int head_dim, int selected) {
+  const int S = attn_bwd_kslices(B, H, I, K, head_dim, selected != 0);
+  return ot_attn_bwd_workspace_size(B, H, K) + (size_t)(S - 1) * B * K * H * head_dim * sizeof(float);
+}
+
+static int attn_bwd_impl(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
+                         int B, int H, int I, int K, const int32_t* qpos, int head_dim, float* dqkv,
+                         float* delta_ws, size_t ws_bytes, void* stream);
+
 extern "C" int ot_attn_bwd(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
                            int B, int H, int I, int K, const int32_t* qpos, int head_dim, float* dqkv,
                            float* delta_ws, void* stream) {
+  return attn_bwd_impl(qkv, ld, out, dout, lse, B, H, I, K, qpos, head_dim, dqkv, delta_ws,
+                       ot_attn_bwd_workspace_size(B, H, K), stream);
+}
+
+extern "C" int ot_attn_bwd_ex(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
+                              int B, int H, int I, int K, const int32_t* qpos, int head_dim, float* dqkv,
+                              void* workspace, size_t ws_bytes, void* stream) {
+  OT_REQUIRE(ws_bytes >= ot_attn_bwd_workspace_size(B, H, K), "ot_attn_bwd_ex: workspace too small");
+  return attn_bwd_impl(qkv, ld, out, dout, lse, B, H, I, K, qpos, head_dim, dqkv, (float*)workspace, ws_bytes,
+                       stream);
+}
+
+static int attn_bwd_impl(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
+                         int B, int H, int I, int K, const int32_t* qpos, int head_dim, float* dqkv,
+                         float* delta_ws, size_t ws_bytes, void* stream) {
   OT_REQUIRE(qkv && out && dout && lse && dqkv && delta_ws, "ot_attn_bwd: null operand");
   OT_REQUIRE(B >= 0 && H > 0 && I > 0 && K > 0 && K <= I, "ot_attn_bwd: bad sizes");
   OT_REQUIRE(ld % 4 == 0 && ld >= 3 * H * head_dim, "ot_attn_bwd: bad ld");
@@ -1312,8 +1599,33 @@ extern "C" int ot_attn_bwd(const float* qkv, int64_t ld, const float* out, const
   if (K <= SMALL_K) {
     OT_ATTN_DISPATCH(attn_bwd_small_kernel, head_dim, dim3(ceil_div((int64_t)B * H, 4)), dim3(256), 0,
                      (hipStream_t)stream, p);
+  } else if (mm == OT_MATMUL_BF16 && (head_dim == 32 || head_dim == 64) &&
+             attn_bwd_kgroup(I, K, head_dim, qpos != nullptr) &&
+             ws_bytes >= ot_attn_bwd_ex_workspace_size(B, H, I, K, head_dim, 0)) {
+    // bf16 mode, long tails: key-grouped workgroups (dQ partials in the ot_attn_bwd_ex workspace)
+    const int G = attn_bwd_kgroup(I, K, head_dim, false), S = attn_bwd_kslices(B, H, I, K, head_dim, false);
+    p.kslices = S;
+    p.kgroup = G;
+    p.dqpart = delta_ws + ot_attn_bwd_workspace_size(B, H, K) / sizeof(float);
+    void (*kern)(AttnArgs) = G == 8 ? (head_dim == 32 ? attn_bwd_group_kernel<32, 8> : attn_bwd_group_kernel<64, 8>)
+                                    : (head_dim == 32 ? attn_bwd_group_kernel<32, 4> : attn_bwd_group_kernel<64, 4>);
+    const size_t lds = G == 8 ? (head_dim == 32 ? BWDG_LDS<32, 8>() : BWDG_LDS<64, 8>())
+                              : (head_dim == 32 ? BWDG_LDS<32, 4>() : BWDG_LDS<64, 4>());
+    static std::once_flag glds_once;
+    std::call_once(glds_once, [] {
+      for (void (*k)(AttnArgs) : {attn_bwd_group_kernel<32, 8>, attn_bwd_group_kernel<64, 8>,
+                                  attn_bwd_group_kernel<32, 4>, attn_bwd_group_kernel<64, 4>})
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, BWDG_LDS<64, 8>());
+      (void)hipGetLastError();
+    });
+    hipLaunchKernelGGL(kern, dim3((unsigned)((int64_t)B * H * S)), dim3(64 * G), lds, (hipStream_t)stream, p);
+    if (S > 1) {
+      OT_LAUNCH_CHECK("ot_attn_bwd");
+      hipLaunchKernelGGL(attn_dq_reduce_kernel, dim3(ceil_div((int64_t)B * K * p.d / 4, 256)), dim3(256), 0,
+                         (hipStream_t)stream, p);
+    }
   } else if (mm == OT_MATMUL_BF16 && (head_dim == 32 || head_dim == 64)) {
-    // bf16 mode: one-plane bf16 MFMA, 4 waves / block (C5 shape: 24 -> 18 ms).  The six-term split
+    // bf16 mode: one-plane bf16 MFMA, one wave per (sample, head), 4 waves / block.  The six-term split
     // form of the same kernel measured slower than the f32 kernel at hd 32 (1.42 vs 1.34 ms at C2:
     // the pass is latency-bound, not MFMA-bound), so split mode keeps the f32 backward.
     void (*kern)(AttnArgs) = nullptr;
@@ -1322,6 +1634,13 @@ extern "C" int ot_attn_bwd(const float* qkv, int64_t ld, const float* out, const
     if (head_dim == 32) kern = sel ? attn_bwd_split_kernel<32, 1, true, 4> : attn_bwd_split_kernel<32, 1, false, 4>;
     else kern = sel ? attn_bwd_split_kernel<64, 1, true, 4> : attn_bwd_split_kernel<64, 1, false, 4>;
     const unsigned grid = ceil_div((int64_t)B * H, waves);
+    static std::once_flag lds_once;                    // hd 64: 72 KiB per 4-wave block (> 64 KiB default)
+    std::call_once(lds_once, [] {
+      for (void (*k)(AttnArgs) : {attn_bwd_split_kernel<32, 1, true, 4>, attn_bwd_split_kernel<32, 1, false, 4>,
+                                  attn_bwd_split_kernel<64, 1, true, 4>, attn_bwd_split_kernel<64, 1, false, 4>})
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * BWDS_LDS<64, 1>());
+      (void)hipGetLastError();
+    });
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * waves), (size_t)waves * lds, (hipStream_t)stream, p);
   } else if (head_dim == 64 && g_attn_bwd_ds == 2) {
     // head_dim 64 as two 32-dim waves per (sample, head): 2 waves / SIMD instead of 1

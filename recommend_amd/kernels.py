@@ -251,10 +251,10 @@ def attn_fwd(qkv: torch.Tensor, ld: int, B: int, H: int, I: int, K: int, hd: int
 
 
 def attn_bwd(qkv, ld, out, dout, lse, B, H, I, K, hd, dqkv, qpos=None) -> None:
-    delta = workspace(size('ot_attn_bwd_workspace_size', B, H, K), qkv.device)
+    ws = workspace(size('ot_attn_bwd_ex_workspace_size', B, H, I, K, hd, int(qpos is not None)), qkv.device)
     ev = _probe.begin() if _probe is not None else None
-    call('ot_attn_bwd', ptr(qkv), ld, ptr(out), ptr(dout), ptr(lse), B, H, I, K, ptr(qpos), hd, ptr(dqkv),
-         ptr(delta), stream())
+    call('ot_attn_bwd_ex', ptr(qkv), ld, ptr(out), ptr(dout), ptr(lse), B, H, I, K, ptr(qpos), hd, ptr(dqkv),
+         ptr(ws), ws.numel(), stream())
     if ev is not None:
         _probe.end('attention', 8.0 * (K * I - K * (K - 1) / 2) * hd * H * B, ev, f'bwd I{I} K{K} hd{hd}')
 

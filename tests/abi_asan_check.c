@@ -42,6 +42,8 @@ int main(void) {
   expect_error("ot_attn_fwd_fp8 head_dim 32", ot_attn_fwd_fp8(f, 96, 1, 1, 4, 4, NULL, 32, f, f, f, 64, NULL));
   expect_error("ot_attn_fwd_fp8 workspace too small", ot_attn_fwd_fp8(f, 192, 1, 1, 4, 4, NULL, 64, f, f, f, 16, NULL));
   expect_error("ot_attn_bwd null operand", ot_attn_bwd(f, 96, f, NULL, f, 1, 1, 4, 4, NULL, 32, f, f, NULL));
+  expect_error("ot_attn_bwd_ex workspace too small",
+               ot_attn_bwd_ex(f, 96, f, f, f, 1, 1, 4, 4, NULL, 32, f, f, 16, NULL));
   expect_error("ot_attn_fwd_cached bad sizes", ot_attn_fwd_cached(f, 96, f, 64, ids, 1, 1, 2, 4, 5, 32, f, NULL));
   expect_error("ot_pyramid_select K > I", ot_pyramid_select(NULL, 1.f, 1, 4, 5, 0, ids, NULL, NULL, 0, NULL));
   expect_error("ot_sparse_adagrad E not a multiple of 4",
@@ -52,7 +54,8 @@ int main(void) {
   /* workspace queries at edge sizes (pure host arithmetic) */
   if (ot_attn_bwd_workspace_size(1, 1, 1) == 0 || ot_mixed_gemm_rms_workspace_size(0, 128) == 0 ||
       ot_attn_fwd_fp8_workspace_size(1, 1, 1, 64) == 0 || ot_attn_fwd_fp8_workspace_size(1, 1, 1, 32) != 0 ||
-      ot_sparse_adagrad_workspace_size(0, 16) == 0) {
+      ot_sparse_adagrad_workspace_size(0, 16) == 0 ||
+      ot_attn_bwd_ex_workspace_size(1, 1, 4, 4, 32, 0) < ot_attn_bwd_workspace_size(1, 1, 4)) {
     printf("FAIL workspace sizes\n");
     ++failures;
   }

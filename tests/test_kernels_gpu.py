@@ -607,3 +607,43 @@ def test_attention_backward_modes(dev, mode, B, H, I, Kq, hd, sel):
             assert (got - qkv_r.grad).abs().max().item() < 3e-2 * qkv_r.grad.abs().max().item()
     finally:
         K.set_matmul_mode(old)
+
+
+@pytest.mark.parametrize('B,H,I,Kq,hd', [(2, 2, 300, 300, 64), (1, 2, 300, 200, 64), (2, 4, 260, 77, 32),
+                                         (1, 1, 1036, 1036, 64)])
+def test_attn_bwd_key_slices(dev, B, H, I, Kq, hd):
+    """bf16 key-grouped backward (ot_attn_bwd_ex at long tails, C5's path: workgroups of 4 waves own 4
+    consecutive key blocks and stream the query blocks once, dQ partials of later groups reduced after):
+    dK / dV bit-identical to the one-wave-per-pair backward (ot_attn_bwd), dQ equal up to the f32 order
+    of the groups' partial sums; tail offsets (Kq < I) exercise which groups a query block sees, idle
+    waves (key blocks past the end) and padded query blocks."""
+    from recommend_amd import _lib
+    old = K.set_matmul_mode('bf16')
+    try:
+        S_ws = _lib.load().ot_attn_bwd_ex_workspace_size(B, H, I, Kq, hd, 0)
+        assert S_ws > K.size('ot_attn_bwd_workspace_size', B, H, Kq)       # slices are used
+        g = torch.Generator().manual_seed(I + Kq)
+        d = H * hd
+        qkv = torch.randn(B * I, 3 * d, generator=g).to(dev)
+        out = torch.empty(B * Kq, d, device=dev)
+        lse = torch.empty(B * H * Kq, device=dev)
+        K.attn_fwd(qkv, 3 * d, B, H, I, Kq, hd, out, lse)
+        dout = torch.randn(B * Kq, d, generator=g).to(dev)
+        res = []
+        for sliced in (True, False):
+            dqkv = torch.zeros(B * I, 3 * d, device=dev)
+            if sliced:
+                K.attn_bwd(qkv, 3 * d, out, dout, lse, B, H, I, Kq, hd, dqkv)
+            else:
+                ws = K.workspace(K.size('ot_attn_bwd_workspace_size', B, H, Kq), dev)
+                K.call('ot_attn_bwd', K.ptr(qkv), 3 * d, K.ptr(out), K.ptr(dout), K.ptr(lse), B, H, I, Kq, None,
+                       hd, K.ptr(dqkv), K.ptr(ws), K.stream())
+            torch.cuda.synchronize()
+            res.append(dqkv.cpu())
+        a, b = res
+        assert torch.equal(a[:, d:], b[:, d:])                                # dK, dV
+        scale = b[:, :d].abs().max().item()
+        assert (a[:, :d] - b[:, :d]).abs().max().item() <= 1e-5 * scale       # dQ
+        assert torch.isfinite(a).all()
+    finally:
+        K.set_matmul_mode(old)

@@ -22,7 +22,10 @@ def run(B, H, I, Kq, hd):
         ms = float(np.median(ts))
         print(f'B{B} H{H} I{I} K{Kq} hd{hd} {name}: {ms*1e3:8.1f} us  {f/ms/1e9:6.1f} TF/s (algorithmic)')
 cfgs = [(4096, 4, 140, 140, 32), (4096, 4, 140, 1, 32), (4096, 4, 140, 140, 64)]
-if len(sys.argv) > 1:                      # e.g. `attn_bench.py 4096,4,140,140,32`
-    cfgs = [tuple(int(x) for x in a.split(',')) for a in sys.argv[1:]]
+args = sys.argv[1:]
+if args and args[0] in ('--bf16', '--split', '--f32'):   # GEMM / attention arithmetic (default split)
+    K.set_matmul_mode(args.pop(0)[2:])
+if args:                                   # e.g. `attn_bench.py 4096,4,140,140,32`
+    cfgs = [tuple(int(x) for x in a.split(',')) for a in args]
 for cfg in cfgs:
     run(*cfg)

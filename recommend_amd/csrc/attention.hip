@@ -1111,6 +1111,13 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kerne
     store_q();
     __syncthreads();                                   // images of block qb (and the previous reduce done)
     if (qb + 1 < nqb) load_q(qb + 1);                  // in flight during this block's MFMAs
+    // a wave whose key block lies wholly after this query block (or past the end) contributes zeros
+    if (key0 > q_off + q0 + 31 || key0 >= I) {
+#pragma unroll
+      for (int c = 0; c < NB(HD); ++c)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dqbuf[((w * NB(HD) + c) * 16 + r) * 64 + lane] = 0.f;
+    } else {
     u32x4 qA[NS][3], oA[NS][3];
 #pragma unroll
     for (int st = 0; st < NS; ++st) {
@@ -1186,6 +1193,7 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kerne
     for (int c = 0; c < NB(HD); ++c)
 #pragma unroll
       for (int r = 0; r < 16; ++r) dqbuf[((w * NB(HD) + c) * 16 + r) * 64 + lane] = dq[c][r];
+    }
     __syncthreads();                                   // every wave's dQ contribution is in LDS
     // fixed-order sum over the NW waves: float4 u = (lane, c, g) -> query q0 + (lane & 31), dims
     // 32c + 8g + 4 (lane >> 5) + 0..3; stored once per (slice, query block)

@@ -69,6 +69,9 @@ class OneTransOptimizer:
         self.acc = {k: torch.full_like(t, float(config.adagrad_initial_accumulator)) for k, t in model.tables.items()}
         # data-parallel exchange of replicated tables: dense all-reduce up to this size, else all-gather
         self.dense_exchange_bytes = int(float(os.environ.get('ONETRANS_DENSE_EXCHANGE_MB', '512')) * 2 ** 20)
+        # ... and of those, all-reduce only the rows some rank touched (the union, from a 1-byte-per-row
+        # max all-reduce) when it is under 60% of the table ('auto'), always ('1') or never ('0')
+        self.compact_exchange = os.environ.get('ONETRANS_COMPACT_EXCHANGE', 'auto')
         self._dense_grad: Dict[str, torch.Tensor] = {}
         # diagnostics (bench.py, N > 1): when a list, every step appends HIP-event pairs bracketing the
         # main stream's waits for the gradient exchange, i.e. the exchange time NOT hidden by backward
@@ -132,6 +135,25 @@ class OneTransOptimizer:
         with torch.cuda.stream(self._comm):
             self._works.append(otdist.allreduce_sum_async(m.flat.grad[lo:hi]))
 
+    def _start_table_exchange(self, g: torch.Tensor, keys: torch.Tensor):
+        """Start the sum over ranks of a replicated table's dense gradient ``g``.  C2's 1M-row item table
+        is 256 MB, but a rank's batch touches ~1/6 of its rows: the ranks first agree on the union of
+        touched rows (uint8 mask, max all-reduce, 1 B per row) and all-reduce only those rows
+        (``ONETRANS_COMPACT_EXCHANGE``).  Rows outside the union are zero on every rank, so the result
+        is the dense all-reduce's.  Returns (g, work, union rows or None, compact rows or None)."""
+        import torch.distributed as dist
+        rows = g.shape[0]
+        if self.compact_exchange != '0':
+            mask = torch.zeros(rows, dtype=torch.uint8, device=g.device)
+            k = keys.reshape(-1)
+            mask[k[(k >= 0) & (k < rows)]] = 1
+            dist.all_reduce(mask, op=dist.ReduceOp.MAX)
+            idx = torch.nonzero(mask).reshape(-1)        # host sync: the union's size
+            if self.compact_exchange == '1' or idx.numel() < 0.6 * rows:
+                cg = g.index_select(0, idx)
+                return g, otdist.allreduce_sum_async(cg), idx, cg
+        return g, otdist.allreduce_sum_async(g), None, None
+
     def step(self) -> None:
         m = self.model
         # replicated tables small enough to exchange densely: scatter the de-duplicated gradient and
@@ -150,7 +172,7 @@ class OneTransOptimizer:
                 else:
                     g.zero_()
                 K.sparse_grad_dense(E, rows, keys, grads, keys.numel(), g, device=table.device)
-                early[name] = (g, otdist.allreduce_sum_async(g))
+                early[name] = self._start_table_exchange(g, keys)
         if m.grad_ready is not None:
             for w in self._works:                        # the current stream waits for each exchange
                 w.wait()
@@ -177,11 +199,13 @@ class OneTransOptimizer:
             elif name in early:
                 # one all-reduce of the de-duplicated dense gradient (started above) instead of
                 # all-gathering every rank's rows
-                g, work = early[name]
+                g, work, idx, cg = early[name]
                 ev_c = self._mark()
                 work.wait()
                 if ev_c is not None:
                     self.exchange_events.append((ev_c, self._mark()))
+                if idx is not None:                      # the union's summed rows back into the dense gradient
+                    g.index_copy_(0, idx, cg)
                 g.mul_(1.0 / otdist.world())
                 K.dense_adagrad(table, self.acc[name], g, rows, E, self.sparse_lr, self.sparse_eps,
                                 self.sparse_clip, device=table.device)

@@ -64,7 +64,9 @@ def _lookup_update(rank, world, dev):
 def _worker(rank, world, port, q, sharding='row'):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
-    os.environ['ONETRANS_TABLE_SHARDING'] = sharding
+    os.environ['ONETRANS_TABLE_SHARDING'] = 'none' if sharding.startswith('none') else sharding
+    # 'none-compact': the replicated table's gradient exchanged as the union of touched rows only
+    os.environ['ONETRANS_COMPACT_EXCHANGE'] = '1' if sharding == 'none-compact' else '0'
     dist.init_process_group('gloo', rank=rank, world_size=world)
     try:
         dev = torch.device('cuda:0')
@@ -133,10 +135,10 @@ def _worker(rank, world, port, q, sharding='row'):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('sharding', ['row', 'none'])
+@pytest.mark.parametrize('sharding', ['row', 'none', 'none-compact'])
 def test_row_sharded_table_two_ranks(sharding):
     """'row': the item table row-sharded over the ranks; 'none': replicated, exchanged as a dense
-    all-reduced gradient.  Either way three DP steps equal the oracle's full-batch steps (and the
+    all-reduced gradient ('none-compact': only the rows some rank touched are all-reduced).  Either way three DP steps equal the oracle's full-batch steps (and the
     dense gradients are all-reduced per block during the backward)."""
     ctx = mp.get_context('spawn')
     q = ctx.Queue()

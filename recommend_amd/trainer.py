@@ -70,7 +70,7 @@ class OneTransOptimizer:
         # data-parallel exchange of replicated tables: dense all-reduce up to this size, else all-gather
         self.dense_exchange_bytes = int(float(os.environ.get('ONETRANS_DENSE_EXCHANGE_MB', '512')) * 2 ** 20)
         # ... and of those, all-reduce only the rows some rank touched (the union, from a 1-byte-per-row
-        # max all-reduce) when it is under 60% of the table ('auto'), always ('1') or never ('0')
+        # max all-reduce) when it is under 60% of a >= 128 MB table ('auto'), always ('1') or never ('0')
         self.compact_exchange = os.environ.get('ONETRANS_COMPACT_EXCHANGE', 'auto')
         self._dense_grad: Dict[str, torch.Tensor] = {}
         # diagnostics (bench.py, N > 1): when a list, every step appends HIP-event pairs bracketing the
@@ -143,7 +143,8 @@ class OneTransOptimizer:
         is the dense all-reduce's.  Returns (g, work, union rows or None, compact rows or None)."""
         import torch.distributed as dist
         rows = g.shape[0]
-        if self.compact_exchange != '0':
+        # (auto: tables of >= 128 MB only — each compaction costs a mask all-reduce and a host sync)
+        if self.compact_exchange == '1' or (self.compact_exchange == 'auto' and g.numel() * 4 >= 2 ** 27):
             mask = torch.zeros(rows, dtype=torch.uint8, device=g.device)
             k = keys.reshape(-1)
             mask[k[(k >= 0) & (k < rows)]] = 1

@@ -346,6 +346,21 @@ int ot_sparse_finish(float* table, float* accum, int E, int64_t n, float lr, flo
 size_t ot_shard_route_workspace_size(int64_t n);
 int ot_shard_route(const int64_t* ids, int64_t n, int64_t num_rows, int world, int32_t* perm, int64_t* send_local,
                    int32_t* counts, void* workspace, size_t ws_bytes, void* stream);
+/* De-duplicating route (replaces ot_shard_route in ShardedTable.lookup; same owner rule): the n ids
+ * sorted by (owner, local row), stable, with equal ids merged into U unique entries in owner order.
+ * uniq_local[u] = local row of unique u at its owner (-1: every id outside [0, num_rows) merges into
+ * one entry routed to rank 0); counts[r] = unique ids owned by rank r (U = their sum); inv[i] = the
+ * unique entry of id i (int64: the idx of ot_gather_rows that expands the U fetched rows to the n
+ * tokens); order[j] = position of the j-th id in sorted order and run_start[u] = first j of unique
+ * u (run_start[U] = n), the runs of ot_segment_rows_sum.  Arrays sized n (run_start n + 1). */
+size_t ot_shard_route_unique_workspace_size(int64_t n);
+int ot_shard_route_unique(const int64_t* ids, int64_t n, int64_t num_rows, int world, int64_t* uniq_local,
+                          int64_t* inv, int32_t* order, int32_t* run_start, int32_t* counts, void* workspace,
+                          size_t ws_bytes, void* stream);
+/* out[u] = sum of src[order[j]] for j in [run_start[u], run_start[u+1]), ascending j (deterministic):
+ * the per-token gradient rows of a de-duplicated route summed per unique id before they travel */
+int ot_segment_rows_sum(const float* src, const int32_t* order, const int32_t* run_start, int64_t U, int E,
+                        float* out, void* stream);
 /* out[i] = table[idx[i]] (zeros for idx < 0) */
 int ot_gather_rows(const float* table, int E, const int64_t* idx, int64_t n, float* out, void* stream);
 /* inverse = 0: dst[j] = src[perm[j]]; inverse = 1: dst[perm[j]] = src[j] */

@@ -3,10 +3,13 @@
 //   route (bucket the ids by owner, stable) -> all-to-all ids -> gather local rows -> all-to-all rows
 //   back -> unpermute,
 // and the update sends the gradient rows the same way to their owners, which apply the sparse
-// Adagrad on their shard.  The all-to-alls are RCCL (torch.distributed); these kernels are the
-// on-device halves.  All are HBM-bound row moves (16-B accesses), deterministic.
+// Adagrad on their shard.  ot_shard_route_unique routes each distinct id once (Zipf batches repeat
+// hot ids: a C2-shape batch has ~175k distinct of 516k), so the ids, rows and gradient rows that
+// cross xGMI shrink by that factor; ot_segment_rows_sum pre-sums the repeats' gradients.  The
+// all-to-alls are RCCL (torch.distributed); these kernels are the on-device halves.  All are HBM-bound row moves (16-B accesses), deterministic.
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 
 #include "common.h"
 
@@ -101,6 +104,98 @@ struct RouteWs {
 
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// ---- de-duplicating route (ot_shard_route_unique) -----------------------------------------
+// Sort key of an id: owner in bits 40.., local row + 1 in bits 0..39 (invalid ids: owner 0, 0), so
+// one radix sort orders the ids by owner and brings equal ids together; the stable sort keeps the
+// original positions ascending inside every run (fixed summation order for ot_segment_rows_sum).
+constexpr int UKEY_LOCAL_BITS = 40;
+
+__global__ void ukeys_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t num_rows, int world, uint64_t* key,
+                             int32_t* pos) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t id = ids[i];
+  const bool ok = id >= 0 && id < num_rows;
+  key[i] = ok ? ((uint64_t)(id % world) << UKEY_LOCAL_BITS) | (uint64_t)(id / world + 1) : 0ull;
+  pos[i] = (int32_t)i;
+}
+
+// head[j] = 1 where sorted key j starts a run of equal ids
+__global__ void uheads_kernel(const uint64_t* __restrict__ ks, int64_t n, int32_t* head) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  head[j] = (j == 0 || ks[j] != ks[j - 1]) ? 1 : 0;
+}
+
+// uidx[j] = inclusive count of heads (unique index + 1).  Writes inv (token -> unique), the unique
+// ids' local rows, the run starts (run_start[U] = n) and per-owner unique counts (run boundaries of
+// the sorted owner field, no atomics).
+__global__ void ufinish_kernel(const uint64_t* __restrict__ ks, const int32_t* __restrict__ order,
+                               const int32_t* __restrict__ uidx, int64_t n, int64_t* inv, int64_t* uniq_local,
+                               int32_t* run_start, int32_t* counts) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint64_t k = ks[j];
+  const int32_t u = uidx[j] - 1;
+  inv[order[j]] = u;
+  if (j == 0 || k != ks[j - 1]) {
+    uniq_local[u] = (int64_t)(k & ((1ull << UKEY_LOCAL_BITS) - 1)) - 1;
+    run_start[u] = (int32_t)j;
+  }
+  if (j == n - 1) run_start[u + 1] = (int32_t)n;
+  const uint64_t o = k >> UKEY_LOCAL_BITS;
+  if (j == n - 1 || (ks[j + 1] >> UKEY_LOCAL_BITS) != o) {
+    int64_t lo = 0, hi = j;                       // first sorted index of owner o
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if ((ks[mid] >> UKEY_LOCAL_BITS) < o) lo = mid + 1; else hi = mid;
+    }
+    counts[o] = uidx[j] - (lo > 0 ? uidx[lo - 1] : 0);
+  }
+}
+
+// out[u] = sum of src[order[j]] over j in [run_start[u], run_start[u + 1]), ascending j: one float4
+// column of one unique row per thread
+__global__ void segment_rows_sum_kernel(const float* __restrict__ src, const int32_t* __restrict__ order,
+                                        const int32_t* __restrict__ run_start, int64_t U, int E, float* out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c4 = E / 4;
+  if (t >= U * c4) return;
+  const int64_t u = t / c4;
+  const int c = 4 * (int)(t % c4);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int32_t j = run_start[u]; j < run_start[u + 1]; ++j)
+    acc += *reinterpret_cast<const f32x4*>(src + (int64_t)order[j] * E + c);
+  *reinterpret_cast<f32x4*>(out + u * E + c) = acc;
+}
+
+struct URouteWs {
+  uint64_t *key_in, *key_out;
+  int32_t *pos_in, *head, *uidx;
+  void *sort_tmp, *scan_tmp;
+  size_t sort_bytes, scan_bytes, total;
+};
+
+URouteWs carve_uroute(void* base, int64_t n) {
+  URouteWs w{};
+  (void)rocprim::radix_sort_pairs(nullptr, w.sort_bytes, (uint64_t*)nullptr, (uint64_t*)nullptr, (int32_t*)nullptr,
+                                  (int32_t*)nullptr, (size_t)n, 0, 64);
+  (void)rocprim::inclusive_scan(nullptr, w.scan_bytes, (int32_t*)nullptr, (int32_t*)nullptr, (size_t)n,
+                                rocprim::plus<int32_t>());
+  char* p = (char*)base;
+  size_t off = 0;
+  auto take = [&](size_t bytes) { char* r = p ? p + off : nullptr; off += al256(bytes); return (void*)r; };
+  w.key_in = (uint64_t*)take(n * 8);
+  w.key_out = (uint64_t*)take(n * 8);
+  w.pos_in = (int32_t*)take(n * 4);
+  w.head = (int32_t*)take(n * 4);
+  w.uidx = (int32_t*)take(n * 4);
+  w.sort_tmp = take(w.sort_bytes);
+  w.scan_tmp = take(w.scan_bytes);
+  w.total = off;
+  return w;
+}
+
 RouteWs carve_route(void* base, int64_t n) {
   RouteWs w{};
   size_t sort_bytes = 0;
@@ -126,7 +221,7 @@ extern "C" size_t ot_shard_route_workspace_size(int64_t n) { return n > 0 ? carv
 
 extern "C" int ot_shard_route(const int64_t* ids, int64_t n, int64_t num_rows, int world, int32_t* perm,
                               int64_t* send_local, int32_t* counts, void* workspace, size_t ws_bytes, void* stream) {
-  OT_REQUIRE(ids && perm && send_local && counts, "ot_shard_route: null operand");
+  OT_REQUIRE((ids || n == 0) && perm && send_local && counts, "ot_shard_route: null operand");
   OT_REQUIRE(world >= 1 && world <= 1024, "ot_shard_route: world %d out of range", world);
   OT_REQUIRE(n >= 0 && n < 2147483647LL && num_rows > 0, "ot_shard_route: bad sizes");
   hipStream_t s = (hipStream_t)stream;
@@ -146,6 +241,58 @@ extern "C" int ot_shard_route(const int64_t* ids, int64_t n, int64_t num_rows, i
   hipLaunchKernelGGL(shard_route_kernel, dim3(g), dim3(256), 0, s, ids, n, num_rows, world, w.owner_out, perm,
                      send_local, counts);
   OT_LAUNCH_CHECK("ot_shard_route(route)");
+  return OT_OK;
+}
+
+extern "C" size_t ot_shard_route_unique_workspace_size(int64_t n) {
+  return n > 0 ? carve_uroute(nullptr, n).total : 256;
+}
+
+extern "C" int ot_shard_route_unique(const int64_t* ids, int64_t n, int64_t num_rows, int world, int64_t* uniq_local,
+                                     int64_t* inv, int32_t* order, int32_t* run_start, int32_t* counts,
+                                     void* workspace, size_t ws_bytes, void* stream) {
+  OT_REQUIRE((ids || n == 0) && uniq_local && inv && order && run_start && counts,
+             "ot_shard_route_unique: null operand");
+  OT_REQUIRE(world >= 1 && world <= 1024, "ot_shard_route_unique: world %d out of range", world);
+  OT_REQUIRE(n >= 0 && n < 2147483647LL, "ot_shard_route_unique: bad n");
+  OT_REQUIRE(num_rows > 0 && num_rows / world + 1 < (1LL << UKEY_LOCAL_BITS),
+             "ot_shard_route_unique: num_rows out of range");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(zero_i32_kernel, dim3(ceil_div(world, 256)), dim3(256), 0, s, counts, world);
+  if (n == 0) {
+    hipLaunchKernelGGL(zero_i32_kernel, dim3(1), dim3(256), 0, s, run_start, 1);
+    OT_LAUNCH_CHECK("ot_shard_route_unique(empty)");
+    return OT_OK;
+  }
+  URouteWs w = carve_uroute(workspace, n);
+  OT_REQUIRE(ws_bytes >= w.total, "ot_shard_route_unique: workspace too small (%zu < %zu)", ws_bytes, w.total);
+  const unsigned g = ceil_div(n, 256);
+  hipLaunchKernelGGL(ukeys_kernel, dim3(g), dim3(256), 0, s, ids, n, num_rows, world, w.key_in, w.pos_in);
+  OT_LAUNCH_CHECK("ot_shard_route_unique(keys)");
+  int end_bit = UKEY_LOCAL_BITS;
+  while ((1 << (end_bit - UKEY_LOCAL_BITS)) < world) ++end_bit;
+  size_t sb = w.sort_bytes;
+  hipError_t e = rocprim::radix_sort_pairs(w.sort_tmp, sb, w.key_in, w.key_out, w.pos_in, order, (size_t)n, 0,
+                                           end_bit, s);
+  if (e != hipSuccess) return fail(OT_ERR_HIP, "ot_shard_route_unique(sort): %s", hipGetErrorString(e));
+  hipLaunchKernelGGL(uheads_kernel, dim3(g), dim3(256), 0, s, w.key_out, n, w.head);
+  OT_LAUNCH_CHECK("ot_shard_route_unique(heads)");
+  size_t cb = w.scan_bytes;
+  e = rocprim::inclusive_scan(w.scan_tmp, cb, w.head, w.uidx, (size_t)n, rocprim::plus<int32_t>(), s);
+  if (e != hipSuccess) return fail(OT_ERR_HIP, "ot_shard_route_unique(scan): %s", hipGetErrorString(e));
+  hipLaunchKernelGGL(ufinish_kernel, dim3(g), dim3(256), 0, s, w.key_out, order, w.uidx, n, inv, uniq_local,
+                     run_start, counts);
+  OT_LAUNCH_CHECK("ot_shard_route_unique(finish)");
+  return OT_OK;
+}
+
+extern "C" int ot_segment_rows_sum(const float* src, const int32_t* order, const int32_t* run_start, int64_t U, int E,
+                                   float* out, void* stream) {
+  OT_REQUIRE(src && order && run_start && out && E > 0 && E % 4 == 0 && U >= 0, "ot_segment_rows_sum: bad args");
+  if (U == 0) return OT_OK;
+  hipLaunchKernelGGL(segment_rows_sum_kernel, dim3(ceil_div(U * (E / 4), 256)), dim3(256), 0, (hipStream_t)stream,
+                     src, order, run_start, U, E, out);
+  OT_LAUNCH_CHECK("ot_segment_rows_sum");
   return OT_OK;
 }
 

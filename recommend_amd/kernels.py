@@ -413,6 +413,16 @@ def shard_route(ids, n, num_rows, world, perm, send_local, counts) -> None:
          stream())
 
 
+def shard_route_unique(ids, n, num_rows, world, uniq_local, inv, order, run_start, counts) -> None:
+    ws = workspace(size('ot_shard_route_unique_workspace_size', n), ids.device)
+    call('ot_shard_route_unique', ptr(ids), n, num_rows, world, ptr(uniq_local), ptr(inv), ptr(order), ptr(run_start),
+         ptr(counts), ptr(ws), ws.numel(), stream())
+
+
+def segment_rows_sum(src, order, run_start, U, E, out) -> None:
+    call('ot_segment_rows_sum', ptr(src), ptr(order), ptr(run_start), U, E, ptr(out), stream())
+
+
 def gather_rows(table, E, idx, n, out) -> None:
     call('ot_gather_rows', ptr(table), E, ptr(idx), n, ptr(out), stream())
 

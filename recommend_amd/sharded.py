@@ -4,11 +4,15 @@ A table of ``num_rows`` rows is split over the ``world`` ranks of a node: row ``
 ``id % world`` at local row ``id // world`` (the modulo spreads Zipf-hot ids over every GPU).  The
 transformer stays data-parallel; only the table is partitioned:
 
-* lookup:   route the batch's ids by owner (``ot_shard_route``, stable) -> RCCL all-to-all of the
-  counts and of the local row indices -> each owner gathers its rows (``ot_gather_rows``) ->
-  all-to-all of the rows back -> unpermute into the batch's order (``ot_permute_rows``).
-* update:   the gradient rows travel the same routes to their owners (all-to-all), are scaled by
-  1/world (each rank's loss is a mean over its local batch), de-duplicated, and applied with the
+* lookup:   route the batch's distinct ids by owner (``ot_shard_route_unique``: one sort by (owner,
+  local row) merges repeats — Zipf batches repeat hot ids, ~3x at the C2/C4 shapes) -> RCCL
+  all-to-all of the counts and of the local row indices -> each owner gathers its rows
+  (``ot_gather_rows``) -> all-to-all of the rows back -> expanded to the batch's tokens through the
+  inverse map (``ot_gather_rows`` again).  ``dedup=False`` (``ONETRANS_SHARD_DEDUP=0``) routes every
+  id (``ot_shard_route`` + ``ot_permute_rows``).
+* update:   the tokens' gradient rows are summed per distinct id (``ot_segment_rows_sum``, fixed
+  order) and travel the same routes to their owners (all-to-all), are scaled by 1/world (each
+  rank's loss is a mean over its local batch), de-duplicated across ranks, and applied with the
   sparse Keras Adagrad; the per-table ``clip_by_norm`` uses the global norm (an all-reduce of each
   owner's squared norm between ``ot_sparse_prepare`` and ``ot_sparse_finish``).
 
@@ -19,6 +23,8 @@ from __future__ import annotations
 
 from typing import Optional
 
+import os
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -28,7 +34,11 @@ from . import kernels as K
 
 class ShardedTable:
     def __init__(self, name: str, num_rows: int, E: int, world: int, rank: int, device, seed: int = 0,
-                 full_init: Optional[np.ndarray] = None, lo: float = -0.05, hi: float = 0.05):
+                 full_init: Optional[np.ndarray] = None, lo: float = -0.05, hi: float = 0.05,
+                 dedup: Optional[bool] = None):
+        if dedup is None:
+            dedup = os.environ.get('ONETRANS_SHARD_DEDUP', '1') != '0'
+        self.dedup = bool(dedup)
         self.name, self.num_rows, self.E = name, int(num_rows), int(E)
         self.world, self.rank, self.device = int(world), int(rank), device
         self.local_rows = (self.num_rows - self.rank + self.world - 1) // self.world
@@ -43,6 +53,7 @@ class ShardedTable:
         else:
             K.hash_uniform_rows(self.table, self.local_rows, self.E, self.rank, self.world, seed, lo, hi)
         self.last_route = None
+        self.sent_rows = 0         # ids (rows) the last lookup sent to their owners
         self.events = None        # diagnostics: a list collects HIP-event pairs around lookup / update
 
     def _mark(self):
@@ -63,29 +74,45 @@ class ShardedTable:
         else:
             dist.all_to_all_single(out, inp, out_splits, in_splits)
 
+    def _splits(self, counts):
+        recv_counts = torch.empty_like(counts)
+        self._a2a(recv_counts, counts, None, None)
+        both = torch.cat([counts, recv_counts]).cpu().tolist()      # the one host sync: split sizes
+        return both[:self.world], both[self.world:]
+
     def lookup(self, ids: torch.Tensor) -> torch.Tensor:
         """Rows of ``ids`` (int64 [n]) in order -> [n, E] fp32 (zeros for ids outside the table)."""
         ev0 = self._mark()
         ids = ids.reshape(-1).contiguous()
         n, E, dev = ids.numel(), self.E, self.device
-        perm = torch.empty(max(1, n), dtype=torch.int32, device=dev)
-        send_local = torch.empty(max(1, n), dtype=torch.int64, device=dev)
         counts = torch.empty(self.world, dtype=torch.int32, device=dev)
-        K.shard_route(ids, n, self.num_rows, self.world, perm, send_local, counts)
-        recv_counts = torch.empty_like(counts)
-        self._a2a(recv_counts, counts, None, None)
-        both = torch.cat([counts, recv_counts]).cpu().tolist()      # the one host sync: split sizes
-        send_splits, recv_splits = both[:self.world], both[self.world:]
+        if self.dedup:
+            send_local = torch.empty(max(1, n), dtype=torch.int64, device=dev)
+            inv = torch.empty(max(1, n), dtype=torch.int64, device=dev)
+            order = torch.empty(max(1, n), dtype=torch.int32, device=dev)
+            run_start = torch.empty(n + 1, dtype=torch.int32, device=dev)
+            K.shard_route_unique(ids, n, self.num_rows, self.world, send_local, inv, order, run_start, counts)
+        else:
+            perm = torch.empty(max(1, n), dtype=torch.int32, device=dev)
+            send_local = torch.empty(max(1, n), dtype=torch.int64, device=dev)
+            K.shard_route(ids, n, self.num_rows, self.world, perm, send_local, counts)
+        send_splits, recv_splits = self._splits(counts)
+        S = sum(send_splits)                  # ids this rank sends: distinct ids (dedup) or n
         R = sum(recv_splits)
         recv_local = torch.empty(max(1, R), dtype=torch.int64, device=dev)
-        self._a2a(recv_local[:R], send_local[:n], recv_splits, send_splits)
+        self._a2a(recv_local[:R], send_local[:S], recv_splits, send_splits)
         rows = torch.empty(max(1, R), E, device=dev)
         K.gather_rows(self.table, E, recv_local, R, rows)
-        back = torch.empty(max(1, n), E, device=dev)
-        self._a2a(back[:n], rows[:R], send_splits, recv_splits)
+        back = torch.empty(max(1, S), E, device=dev)
+        self._a2a(back[:S], rows[:R], send_splits, recv_splits)
         out = torch.empty(n, E, device=dev)
-        K.permute_rows(back, perm, n, E, True, out)
-        self.last_route = (n, perm, send_splits, recv_splits, recv_local, R)
+        if self.dedup:
+            K.gather_rows(back, E, inv, n, out)          # token i <- its distinct id's row
+            self.last_route = (n, ('dedup', order, run_start, S), send_splits, recv_splits, recv_local, R)
+        else:
+            K.permute_rows(back, perm, n, E, True, out)
+            self.last_route = (n, perm, send_splits, recv_splits, recv_local, R)
+        self.sent_rows = S
         if ev0 is not None:
             self.events.append((ev0, self._mark()))
         return out
@@ -101,10 +128,16 @@ class ShardedTable:
             raise ValueError(f'{self.name}: {grads.shape[0]} gradient rows for a route of {n} ids')
         E, dev = self.E, self.device
         ev0 = self._mark()
-        send = torch.empty(max(1, n), E, device=dev)
-        K.permute_rows(grads.contiguous(), perm, n, E, False, send)
+        if isinstance(perm, tuple):                      # de-duplicated route: sum repeats first
+            _, order, run_start, S = perm
+            send = torch.empty(max(1, S), E, device=dev)
+            K.segment_rows_sum(grads.contiguous(), order, run_start, S, E, send)
+        else:
+            S = n
+            send = torch.empty(max(1, n), E, device=dev)
+            K.permute_rows(grads.contiguous(), perm, n, E, False, send)
         recv = torch.empty(max(1, R), E, device=dev)
-        self._a2a(recv[:R], send[:n], recv_splits, send_splits)
+        self._a2a(recv[:R], send[:S], recv_splits, send_splits)
         if self.world > 1:
             recv.mul_(1.0 / self.world)
         ws = K.sparse_workspace(R, E, dev)

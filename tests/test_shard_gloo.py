@@ -2,8 +2,8 @@
 split sizes, the all-to-all exchanges, the route back, the global-norm clip — with peers that send
 no ids and peers that own none of the ids in flight.
 
-The device kernels the class calls (ot_shard_route, ot_gather_rows, ot_permute_rows,
-ot_sparse_prepare/finish; their GPU parity is tests/test_sharded_gpu.py) are replaced here by small
+The device kernels the class calls (ot_shard_route[_unique], ot_gather_rows, ot_permute_rows,
+ot_segment_rows_sum, ot_sparse_prepare/finish; their GPU parity is tests/test_sharded_gpu.py) are replaced here by small
 torch stand-ins that follow their header contracts (include/onetrans_hip.h), so only the exchange
 plumbing is under test."""
 
@@ -12,6 +12,7 @@ import socket
 import types
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -38,6 +39,31 @@ def _cpu_kernels():
         loc = torch.where(ok, ids // world, torch.full_like(ids, -1))
         send_local[:n] = loc[order]
         counts.copy_(torch.bincount(owner, minlength=world).to(torch.int32))
+
+    def shard_route_unique(ids, n, num_rows, world, uniq_local, inv, order, run_start, counts):
+        ids = ids[:n]
+        ok = (ids >= 0) & (ids < num_rows)
+        owner = torch.where(ok, ids % world, torch.zeros_like(ids))
+        loc1 = torch.where(ok, ids // world + 1, torch.zeros_like(ids))     # invalid: (owner 0, 0)
+        key = owner * (1 << 40) + loc1
+        srt = torch.sort(key, stable=True)
+        order[:n] = srt.indices.to(torch.int32)
+        uk, u_of_sorted = torch.unique_consecutive(srt.values, return_inverse=True)
+        U = len(uk)
+        inv[srt.indices] = u_of_sorted
+        uniq_local[:U] = (uk % (1 << 40)) - 1
+        heads = torch.ones(n, dtype=torch.bool)
+        heads[1:] = srt.values[1:] != srt.values[:-1]
+        run_start[:U] = torch.nonzero(heads).reshape(-1).to(torch.int32)
+        run_start[U] = n
+        counts.copy_(torch.bincount(uk // (1 << 40), minlength=world).to(torch.int32))
+
+    def segment_rows_sum(src, order, run_start, U, E, out):
+        for u in range(U):
+            acc = torch.zeros(E)
+            for j in range(int(run_start[u]), int(run_start[u + 1])):
+                acc += src[int(order[j])]
+            out[u] = acc
 
     def gather_rows(table, E, idx, n, out):
         idx = idx[:n]
@@ -70,6 +96,7 @@ def _cpu_kernels():
         table[uk] = (table[uk].double() - lr * g / torch.sqrt(a + eps)).float()
 
     K.shard_route, K.gather_rows, K.permute_rows = shard_route, gather_rows, permute_rows
+    K.shard_route_unique, K.segment_rows_sum = shard_route_unique, segment_rows_sum
     K.sparse_workspace, K.sparse_prepare, K.sparse_finish = sparse_workspace, sparse_prepare, sparse_finish
     return K
 
@@ -83,7 +110,7 @@ def _ids_of(rank, num_rows, world, rng):
     return np.concatenate([ids, ids[:5], [-1, num_rows + 2]]).astype(np.int64)
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, dedup):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
     dist.init_process_group('gloo', rank=rank, world_size=world)
@@ -93,7 +120,7 @@ def _worker(rank, world, port, q):
         num_rows, E = 203, 8
         rng = np.random.default_rng(11)
         full = rng.uniform(-0.05, 0.05, (num_rows, E)).astype(np.float32)
-        st = sharded.ShardedTable('t', num_rows, E, world, rank, torch.device('cpu'), full_init=full)
+        st = sharded.ShardedTable('t', num_rows, E, world, rank, torch.device('cpu'), full_init=full, dedup=dedup)
         ids_all = [_ids_of(r, num_rows, world, np.random.default_rng(100 + r)) for r in range(world)]
         grads_all = [np.random.default_rng(200 + r).standard_normal((len(i), E)).astype(np.float32)
                      for r, i in enumerate(ids_all)]
@@ -115,17 +142,19 @@ def _worker(rank, world, port, q):
         l2 = np.sqrt((g * g).sum())
         g = g * clip / max(l2, clip)
         ref = full - lr * g / np.sqrt(0.1 + g * g + eps)
-        q.put((rank, len(ids), recv, err_lookup, float(np.abs(new - ref).max())))
+        distinct = len(np.unique(np.where(ok, ids, -1))) if len(ids) else 0
+        q.put((rank, len(ids), recv, err_lookup, float(np.abs(new - ref).max()), st.sent_rows, distinct))
     finally:
         dist.destroy_process_group()
 
 
-def test_sharded_exchange_world4_with_empty_peers():
+@pytest.mark.parametrize('dedup', [True, False])
+def test_sharded_exchange_world4_with_empty_peers(dedup):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
     world = 4
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, dedup)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -134,7 +163,10 @@ def test_sharded_exchange_world4_with_empty_peers():
         if p.exitcode is None:
             p.kill()
         assert p.exitcode == 0, p.exitcode
-    res = {r: (n, recv, el, ea) for (r, n, recv, el, ea) in (q.get(timeout=10) for _ in range(world))}
+    out = [q.get(timeout=10) for _ in range(world)]
+    res = {r: (n, recv, el, ea) for (r, n, recv, el, ea, _, _) in out}
+    for (r, n, _, _, _, sent, distinct) in out:       # dedup: each distinct id (invalid ids: one) sent once
+        assert sent == (distinct if dedup else n), (r, sent, distinct, n)
     assert res[2][0] == 0                         # rank 2 sent nothing
     assert res[3][1] == 0                         # rank 3 received nothing
     for r, (n, recv, el, ea) in res.items():

@@ -64,7 +64,9 @@ def _lookup_update(rank, world, dev):
 def _worker(rank, world, port, q, sharding='row'):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
-    os.environ['ONETRANS_TABLE_SHARDING'] = 'none' if sharding.startswith('none') else sharding
+    os.environ['ONETRANS_TABLE_SHARDING'] = 'none' if sharding.startswith('none') else 'row'
+    # 'row-nodedup': every id routed (no de-duplication before the all-to-all)
+    os.environ['ONETRANS_SHARD_DEDUP'] = '0' if sharding == 'row-nodedup' else '1'
     # 'none-compact': the replicated table's gradient exchanged as the union of touched rows only
     os.environ['ONETRANS_COMPACT_EXCHANGE'] = '1' if sharding == 'none-compact' else '0'
     dist.init_process_group('gloo', rank=rank, world_size=world)
@@ -84,8 +86,9 @@ def _worker(rank, world, port, q, sharding='row'):
         cfg.optimizer_config = dict(cfg.optimizer_config, dense_lr=0.001, momentum=0.9)
         P = init_params(cfg, cfg.ns_input_width(), seed=0, perturb=True)
         model = OneTransModel(cfg, device=dev, init=P)
-        if sharding == 'row':
+        if sharding.startswith('row'):
             assert 'emb.seq_item' in model.sharded
+            assert model.sharded['emb.seq_item'].dedup == (sharding == 'row')
             assert model.sharded['emb.seq_item'].local_rows == (cfg.seq_item_vocab - rank + 1) // 2
         else:                                            # replicated: dense-gradient all-reduce exchange
             assert not model.sharded
@@ -135,7 +138,7 @@ def _worker(rank, world, port, q, sharding='row'):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('sharding', ['row', 'none', 'none-compact'])
+@pytest.mark.parametrize('sharding', ['row', 'row-nodedup', 'none', 'none-compact'])
 def test_row_sharded_table_two_ranks(sharding):
     """'row': the item table row-sharded over the ranks; 'none': replicated, exchanged as a dense
     all-reduced gradient ('none-compact': only the rows some rank touched are all-reduced).  Either way three DP steps equal the oracle's full-batch steps (and the
@@ -167,3 +170,47 @@ def test_row_sharded_table_two_ranks(sharding):
     assert not bad, bad
     if sharding == 'row':
         assert res['ckpt'] == 0.0 and res['ckpt_fwd'] == 0.0, (res['ckpt'], res['ckpt_fwd'])
+
+
+@pytest.mark.parametrize('world', [1, 3, 8])
+@pytest.mark.parametrize('n', [0, 1, 5000])
+def test_shard_route_unique_kernel(world, n):
+    """ot_shard_route_unique / ot_segment_rows_sum against numpy: distinct ids in (owner, local row)
+    order, every invalid id merged into one entry at owner 0, per-owner counts, the inverse map, and
+    the per-distinct-id gradient sums (fixed order: equal to a float64 sum within f32 rounding)."""
+    from recommend_amd import kernels as K
+    dev = torch.device('cuda:0')
+    num_rows, E = 100_003, 16
+    rng = np.random.default_rng(n + world)
+    ids = ((rng.zipf(1.2, n) - 1) % num_rows).astype(np.int64)
+    if n > 2:
+        ids[:3] = [-5, num_rows, num_rows + 7]                 # invalid ids
+    t = torch.from_numpy(ids).to(dev)
+    uniq_local = torch.full((max(1, n),), -99, dtype=torch.int64, device=dev)
+    inv = torch.empty(max(1, n), dtype=torch.int64, device=dev)
+    order = torch.empty(max(1, n), dtype=torch.int32, device=dev)
+    run_start = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    counts = torch.full((world,), -1, dtype=torch.int32, device=dev)
+    K.shard_route_unique(t, n, num_rows, world, uniq_local, inv, order, run_start, counts)
+    ok = (ids >= 0) & (ids < num_rows)
+    owner = np.where(ok, ids % world, 0)
+    loc = np.where(ok, ids // world, -1)
+    keys = sorted(set(zip(owner.tolist(), loc.tolist())))
+    U = len(keys)
+    c = counts.cpu().numpy()
+    assert c.sum() == U
+    assert c.tolist() == [sum(1 for o, _ in keys if o == r) for r in range(world)]
+    assert uniq_local[:U].cpu().numpy().tolist() == [l for _, l in keys]
+    pos = {k: u for u, k in enumerate(keys)}
+    assert inv[:n].cpu().numpy().tolist() == [pos[(o, l)] for o, l in zip(owner.tolist(), loc.tolist())]
+    rs = run_start.cpu().numpy()
+    assert rs[U] == n and (np.diff(rs[:U + 1]) > 0).all()
+    grads = rng.standard_normal((n, E)).astype(np.float32)
+    out = torch.empty(max(1, U), E, device=dev)
+    K.segment_rows_sum(torch.from_numpy(grads).to(dev) if n else torch.zeros(1, E, device=dev), order, run_start,
+                       U, E, out)
+    exp = np.zeros((U, E))
+    inv_np = inv[:n].cpu().numpy()
+    np.add.at(exp, inv_np, grads.astype(np.float64))
+    if U:
+        assert np.abs(out[:U].cpu().numpy() - exp).max() < 1e-4

@@ -274,7 +274,9 @@ def main():
         'dtype': 'bf16' if K.matmul_mode() == 'bf16' else 'f32', 'data': 'synthetic', 'precision': precision,
         'config': {'workload': f'{args.config}: OneTrans {cfg.num_layers}L d{cfg.hidden_dim} H{cfg.num_heads} f{cfg.ffn_dim} '
                                f'L_NS{cfg.num_ns_tokens} L_S{sum(seq_lens) + 2} (seq 3x{seq_lens[0]}), '
-                               f'Criteo-shape 13 dense + 26 ids, replicated tables, fwd+bwd+optimizer',
+                               f'Criteo-shape 13 dense + 26 ids, '
+                               f'{"row-sharded " + ", ".join(sorted(model.sharded)) if model.sharded else "replicated tables"}, '
+                               f'fwd+bwd+optimizer',
                    'global_batch': B * world, 'per_gpu_batch': B, 'seq_len': sum(seq_lens) + 2,
                    'parallelism': f'dp{world}'},
         'model_tflops': round(fl['fwd_bwd'] * value / 1e12, 2),
@@ -291,6 +293,10 @@ def main():
                        'exposed_exchange_ms_per_step_max': round(max(exposed_ranks), 3),
                        'exposed_exchange_ms_per_step_min': round(min(exposed_ranks), 3),
                        'sharded_tables': sorted(model.sharded),
+                       # per row-sharded table: rows this rank sent to their owners in the last lookup
+                       # (distinct ids when de-duplicated) and the ids of that lookup
+                       'sharded_rows_sent_of_ids': {k: [t.sent_rows, t.last_route[0] if t.last_route else 0]
+                                                    for k, t in sorted(model.sharded.items())},
                        'note': 'exposed exchange = HIP-event time the main stream waits for the dense '
                                'gradient all-reduce and the replicated-table exchange after backward, plus the '
                                'row-sharded tables\' all-to-all lookups and updates (median repeat)'}

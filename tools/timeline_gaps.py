@@ -1,0 +1,52 @@
+"""GPU idle time per training step from a rocprofv3 kernel trace (CSV).
+
+Steps are delimited by the once-per-step optimizer kernel (rmsprop_kernel); inside each step the
+union of all kernels' [start, end) intervals (any stream) is the busy time, the rest is idle — host
+launch latency, host syncs, or stream waits.  Also lists the largest idle gaps of the last step.
+
+usage: python tools/timeline_gaps.py run_kernel_trace.csv [marker]
+"""
+import csv
+import sys
+
+
+def main():
+    path = sys.argv[1]
+    marker = sys.argv[2] if len(sys.argv) > 2 else 'rmsprop_kernel'
+    rows = list(csv.DictReader(open(path)))
+    ks = sorted((int(r['Start_Timestamp']), int(r['End_Timestamp']), r['Kernel_Name']) for r in rows)
+    ends = [e for s, e, n in ks if marker in n]
+    if len(ends) < 3:
+        print(f'fewer than 3 {marker} launches')
+        return 1
+    print(f'{len(ks)} kernels, {len(ends)} steps (marker {marker})')
+    print('step  wall_ms  busy_ms  idle_ms  idle%  kernels')
+    last_gaps = []
+    for i in range(1, len(ends)):
+        t0, t1 = ends[i - 1], ends[i]
+        iv = [(max(s, t0), min(e, t1), n) for s, e, n in ks if e > t0 and s < t1]
+        busy, cur_s, cur_e, gaps, prev_name = 0, None, None, [], None
+        for s, e, n in iv:
+            if cur_e is None or s > cur_e:
+                if cur_e is not None:
+                    busy += cur_e - cur_s
+                    gaps.append((s - cur_e, prev_name, n))
+                elif s > t0:
+                    gaps.append((s - t0, marker, n))
+                cur_s, cur_e = s, e
+            else:
+                cur_e = max(cur_e, e)
+            prev_name = n if cur_e == e else prev_name
+        if cur_e is not None:
+            busy += cur_e - cur_s
+        wall = t1 - t0
+        print(f'{i:4d} {wall / 1e6:8.3f} {busy / 1e6:8.3f} {(wall - busy) / 1e6:8.3f} {100 * (wall - busy) / wall:5.1f}%  {len(iv)}')
+        last_gaps = gaps
+    print('largest idle gaps of the last step (us, after -> before):')
+    for g, a, b in sorted(last_gaps, reverse=True)[:15]:
+        print(f'  {g / 1e3:8.1f}  {a[:60]}  ->  {b[:60]}')
+    return 0
+
+
+if __name__ == '__main__':
+    sys.exit(main())

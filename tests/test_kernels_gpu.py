@@ -274,6 +274,32 @@ def attn_ref_sel(qkv, B, H, I, qpos, hd):
     return torch.einsum('bhqk,bkhd->bqhd', torch.softmax(s, -1), v).reshape(B * Kq, d)
 
 
+@pytest.mark.parametrize('hd', [16, 32])
+def test_attention_fwd_spread_block_queries(dev, hd):
+    """Shared-K/V forward with the kept queries of one query block spread over the sequence (40 .. 139:
+    its early queries see none of the later key blocks, which stay fully masked for them); the
+    output and the log-sum-exp against float64."""
+    B, H, I = 2, 4, 140
+    qpos = np.array([list(range(32)) + [40, 60, 80, 100, 120, 130, 135, 139]] * B)
+    Kq = qpos.shape[1]
+    torch.manual_seed(3)
+    d = H * hd
+    qkv = torch.randn(B * I, 3 * d, dtype=torch.float64)
+    qp_d = torch.from_numpy(qpos.astype(np.int32).reshape(-1)).to(dev)
+    out = torch.empty(B * Kq, d, device=dev)
+    lse = torch.empty(B * H * Kq, device=dev)
+    K.attn_fwd(qkv.float().to(dev), 3 * d, B, H, I, Kq, hd, out, lse, qpos=qp_d)
+    ref = attn_ref_sel(qkv, B, H, I, torch.from_numpy(qpos), hd)
+    torch.testing.assert_close(out.double().cpu(), ref, rtol=1e-4, atol=1e-5)
+    bi = torch.arange(B)[:, None]
+    q = qkv[:, :d].reshape(B, I, H, hd)[bi, torch.from_numpy(qpos)]
+    k = qkv[:, d:2 * d].reshape(B, I, H, hd)
+    sc = torch.einsum('bqhd,bkhd->bhqk', q, k) / math.sqrt(hd)
+    mask = torch.arange(I)[None, None, None, :] <= torch.from_numpy(qpos)[:, None, :, None]
+    ref_lse = torch.logsumexp(torch.where(mask, sc, torch.tensor(-math.inf, dtype=sc.dtype)), -1)
+    torch.testing.assert_close(lse.double().cpu().reshape(B, H, Kq), ref_lse, rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize('B,H,I,Kq,hd', [(3, 4, 140, 70, 32), (2, 2, 70, 33, 64), (3, 4, 40, 12, 16),
                                          (1, 2, 33, 17, 128), (2, 4, 140, 3, 32), (2, 2, 70, 4, 64),
                                          (2, 4, 150, 100, 32), (2, 2, 524, 262, 64), (2, 4, 9, 9, 32)])

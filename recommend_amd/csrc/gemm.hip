@@ -53,6 +53,10 @@ constexpr int GLD = GBK + 4;      // LDS row stride (floats)
 #ifndef OT_GEMM_SPLIT_SCHED
 #define OT_GEMM_SPLIT_SCHED 0     // >0: interleave this many VALU ops after each MFMA (sched_group_barrier)
 #endif
+#ifndef OT_GEMM_NT_STORE
+#define OT_GEMM_NT_STORE 1        // epilogue output rows written with non-temporal (streaming) stores
+                                  // (C2 +0.5%, T +0.5%: profiles/r02/gemm_nt_store.txt); 0: plain stores
+#endif
 constexpr int SPLIT_TERMS = OT_GEMM_SPLIT;
 constexpr int SRS = 3 * 16 + 8;   // split LDS row stride (ushorts): 3 planes x 16 k + pad = 112 B
 static_assert(SPLIT_TERMS == 3 || SPLIT_TERMS == 6 || SPLIT_TERMS == 9, "OT_GEMM_SPLIT");
@@ -119,6 +123,11 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 // LAYOUT 0: 2x2 waves, acc[2m + n] = rows 64 (wave >> 1) + 32 m, cols 64 (wave & 1) + 32 n;
 // LAYOUT 1: 4x1 waves, acc[nb] = rows 32 wave, cols 32 nb.  ROWSCALE: multiply row r by
 // a_rstd[in_rows[r]] first (the plane GEMM's RMSNorm prologue, folded into the weights).
+__device__ __forceinline__ void store_out4(float* dst, f32x4 v) {
+  if (OT_GEMM_NT_STORE) __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(dst));
+  else *reinterpret_cast<f32x4*>(dst) = v;
+}
+
 template <int EPIT, int LAYOUT, bool ROWSCALE, int RBN = 8>
 __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x16 (&acc)[4], float* smem, int tm,
                                                   int n0, int g) {
@@ -242,7 +251,7 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
               *q = *q + v * x4[i] * r;
             }
             v = gv * r - x4[i] * coef + dr4[i];
-            if (orr >= 0) *reinterpret_cast<f32x4*>(p.C + (int64_t)orr * p.ldc + col) = v;
+            if (orr >= 0) store_out4(p.C + (int64_t)orr * p.ldc + col, v);
             if ((epi & OT_EPI_DROPOUT) && orr >= 0) {          // mask(dx) for the dropout site upstream
               const uint32_t idx = (uint32_t)(tok[i] * p.drop_width + col);
               f32x4 mv;
@@ -250,7 +259,7 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
               mv.y = drop_keep(p.seed, p.site, idx + 1, p.drop_thr) ? v.y * p.drop_scale : 0.f;
               mv.z = drop_keep(p.seed, p.site, idx + 2, p.drop_thr) ? v.z * p.drop_scale : 0.f;
               mv.w = drop_keep(p.seed, p.site, idx + 3, p.drop_thr) ? v.w * p.drop_scale : 0.f;
-              *reinterpret_cast<f32x4*>(p.dxm + (int64_t)orr * p.lddxm + col) = mv;
+              store_out4(p.dxm + (int64_t)orr * p.lddxm + col, mv);
             }
             continue;
           }
@@ -275,7 +284,7 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
               p.rstd_out[orr] = rsqrtf(ss / (float)p.N + p.eps);
             }
           }
-          if (orr >= 0) *reinterpret_cast<f32x4*>(p.C + (int64_t)orr * p.ldc + col) = v;
+          if (orr >= 0) store_out4(p.C + (int64_t)orr * p.ldc + col, v);
         }
       }
       __syncthreads();                                  // ct is rewritten by the next half

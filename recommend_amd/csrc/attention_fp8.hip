@@ -86,14 +86,14 @@ inline size_t fp8_pack_bytes(int64_t BH, int I, int HD) {
   return (size_t)(BH * Ip * HD * 2 + BH * Ip * (HD / 32) + BH * (Ip / 64) * HD);
 }
 
-// grid (Ip/64, B*H), 256 threads.  Keys >= I are zeros (the causal mask removes them).
+// grid (B*H, Ip/64), 256 threads (B*H on x: up to 2^31 - 1 heads).  Keys >= I are zeros (the causal mask removes them).
 template <int HD>
 __global__ __launch_bounds__(256) void attn_fp8_pack_kernel(const float* __restrict__ qkv, int64_t ld, int H, int I,
                                                             Fp8Pack f) {
   constexpr int VLD = HD + 1;
   __shared__ float vs_f[64 * VLD];
   __shared__ __attribute__((aligned(16))) uint8_t vt_img[HD * 64];
-  const int kb = blockIdx.x, bh = blockIdx.y;
+  const int kb = blockIdx.y, bh = blockIdx.x;
   const int b = bh / H, h = bh % H, d = H * HD;
   const int64_t Ip = fp8_ipad(I);
   const int t = threadIdx.x;
@@ -374,8 +374,9 @@ extern "C" int ot_attn_fwd_fp8(const float* qkv, int64_t ld, int B, int H, int I
              ((uintptr_t)workspace % 16) == 0, "ot_attn_fwd_fp8: workspace");
   const int64_t BH = (int64_t)B * H;
   const Fp8Pack f = fp8_pack_layout(workspace, BH, I, head_dim);
-  OT_REQUIRE(BH <= 65535, "ot_attn_fwd_fp8: B*H = %lld > 65535", (long long)BH);
-  const dim3 pg((unsigned)(fp8_ipad(I) / 64), (unsigned)BH);
+  OT_REQUIRE(BH < 2147483647LL && fp8_ipad(I) / 64 <= 65535, "ot_attn_fwd_fp8: B*H = %lld, I = %d out of range",
+             (long long)BH, I);
+  const dim3 pg((unsigned)BH, (unsigned)(fp8_ipad(I) / 64));
   hipStream_t s = (hipStream_t)stream;
   if (head_dim == 64) hipLaunchKernelGGL(attn_fp8_pack_kernel<64>, pg, dim3(256), 0, s, qkv, ld, H, I, f);
   else hipLaunchKernelGGL(attn_fp8_pack_kernel<128>, pg, dim3(256), 0, s, qkv, ld, H, I, f);

@@ -126,6 +126,14 @@ class _Tokenize(torch.autograd.Function):
         return None, None, None
 
 
+def layer_seed(seed: int, b0: int, I: int, d: int) -> int:
+    """Dropout seed of a layer whose local sample b is global sample b0 + b.  The mask hashes the 32-bit
+    element index (b*I + p)*d + n as idx * 0x9E3779B1 + seed (common.h drop_keep), so shifting every
+    index by b0*I*d is the same as adding b0*I*d*0x9E3779B1 to the seed (mod 2^32): the kernels keep
+    local indices and the masks equal the full batch's (oracle dropout_scale's ``b0``)."""
+    return (seed + b0 * I * d * 0x9E3779B1) & 0xFFFFFFFF if b0 else seed
+
+
 def _attn_qpos(cfg, pos):
     """Kept-query positions for the attention kernels: None (the tail rule, I - K + j) when the keep is
     the reference's tail — ot_pyramid_select returns exactly that set there, in order."""
@@ -545,6 +553,7 @@ class OneTransModel(nn.Module):
         self._aux_maps: Dict = {}
         self._step = 0
         self.dropout_seed = 0x5EED0000 ^ seed
+        self.sample_offset: Optional[int] = None      # global index of the local batch's first sample
         # row-sharded tables (data-parallel runs): 'emb.seq_item' lives partitioned over the ranks
         self.sharded: Dict[str, 'ShardedTable'] = {}
         shard_seq = self._shard_seq_table()
@@ -874,13 +883,26 @@ class OneTransModel(nn.Module):
         x = _Tokenize.apply(self.flat, self, plan)
         sched = self.config.pyramid_schedule(plan['L0'])
         nl = len(sched)
+        b0 = self.batch_offset(plan['B']) if training else 0
         rstd = None
         for l, s in enumerate(sched):
             Kq = s['keep'] if l < nl - 1 else 1
             select = l < nl - 1 and Kq < s['in_len']         # a pyramid keep (the last layer: DCE, tail)
             select = select and (self.pyramid_kernel or self.config.pyramid_select != 'tail')
-            x, rstd = _Block.apply(self.flat, x, self, l, s['in_len'], Kq, seed, training, rstd, select)
+            x, rstd = _Block.apply(self.flat, x, self, l, s['in_len'], Kq, layer_seed(seed, b0, s['in_len'],
+                                   self.config.hidden_dim), training, rstd, select)
         return _Head.apply(self.flat, x, self)
+
+    def batch_offset(self, B: int) -> int:
+        """Index of this process's first sample in the global batch (dropout masks are a function of the
+        global sample index, so a data-parallel step draws the masks of the equivalent full-batch step).
+        ``sample_offset`` when set; else rank * B under torch.distributed (equal local batches)."""
+        if self.sample_offset is not None:
+            return int(self.sample_offset)
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            return dist.get_rank() * B
+        return 0
 
     # ---------------------------------------------------------------- side stream (wgrad overlap)
     def side(self, *tensors):

@@ -25,7 +25,7 @@ from . import dist as otdist
 from . import kernels as K
 from .config import OneTransConfig, get_model_config
 from .metrics import auc, keras_auc
-from .model import OneTransModel, keras_bce_loss
+from .model import BINARY_TASKS, OneTransModel, keras_bce_loss
 
 
 def _to_dev(d: Dict, dev) -> Dict[str, torch.Tensor]:
@@ -254,7 +254,9 @@ class OneTransTrainer:
         return {'total_loss': loss, 'probs': probs}
 
     def evaluate(self, batches) -> Dict[str, float]:
-        """AUC per task over a list of batches (exact rank AUC + Keras 200-threshold AUC)."""
+        """Per task over a list of batches: 'ctr' / 'cvr' (BCE tasks) the exact rank AUC + the Keras
+        200-threshold AUC; any other task (trained with MSE, train.py:88-91) mse and mae, as the
+        reference reports for regression tasks (train.py:106, evaluate.py:52-54)."""
         ps, ys = [], []
         for b in batches:
             out = self.val_step(b)
@@ -263,8 +265,13 @@ class OneTransTrainer:
         P, Y = np.concatenate(ps, 1), np.concatenate(ys, 1)
         res = {}
         for i, t in enumerate(self.config.tasks):
-            res[f'{t}_auc'] = auc(Y[i], P[i])
-            res[f'{t}_keras_auc'] = keras_auc(Y[i], P[i])
+            if t in BINARY_TASKS:
+                res[f'{t}_auc'] = auc(Y[i], P[i])
+                res[f'{t}_keras_auc'] = keras_auc(Y[i], P[i])
+            else:
+                e = P[i].astype(np.float64) - Y[i].astype(np.float64)
+                res[f'{t}_mse'] = float(np.mean(e * e))
+                res[f'{t}_mae'] = float(np.mean(np.abs(e)))
         return res
 
     def train(self, train_batches, val_batches=None, epochs: int = 1) -> Dict:
@@ -286,7 +293,9 @@ class OneTransTrainer:
         with open(path / 'config.json', 'w') as f:
             json.dump(self.config.to_dict(), f, indent=2)
         with open(path / 'training_history.json', 'w') as f:
-            json.dump(self.history, f, indent=2, default=float)
+            # the dense optimizer's step count travels with the history, so a resumed run continues the
+            # LR warm-up ramp (apply_warmup) where it stopped
+            json.dump(dict(self.history, optimizer_steps=self.optimizer.steps_done), f, indent=2, default=float)
 
     def load_model(self, model_path: str) -> None:
         path = Path(model_path)
@@ -300,6 +309,7 @@ class OneTransTrainer:
         if (path / 'training_history.json').exists():
             with open(path / 'training_history.json') as f:
                 self.history = json.load(f)
+            self.optimizer.steps_done = int(self.history.pop('optimizer_steps', 0))
 
 
 def train_one_trans_model(config_name: str = 'small', batches=None, epochs: int = 10,

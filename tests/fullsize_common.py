@@ -46,14 +46,20 @@ def table_values_np(rows: np.ndarray, E: int, seed: int) -> np.ndarray:
     return (((h >> 8) - (1 << 23)).astype(np.float32) * np.float32(2.0 ** -27))
 
 
-def fill_table_device(t, seed: int, chunk_rows: int = 1 << 22) -> None:
+def fill_table_device(t, seed: int, chunk_rows: int = 1 << 22, row0: int = 0, row_stride: int = 1,
+                      nrows: int = -1) -> None:
     """The same values for every row of the device table ``t`` [rows, E] (torch int64 arithmetic;
-    the products are masked to 32 bits, so two's-complement wrap-around does not matter)."""
+    the products are masked to 32 bits, so two's-complement wrap-around does not matter).  Local row
+    j holds global row ``row0 + j * row_stride`` (a row-sharded table: row0 = rank, stride = world),
+    for the first ``nrows`` rows (all when negative)."""
     import torch
     rows, E = t.shape
+    if nrows >= 0:
+        rows = nrows
     col = torch.arange(E, device=t.device, dtype=torch.int64)[None, :]
     for r0 in range(0, rows, chunk_rows):
         r = torch.arange(r0, min(rows, r0 + chunk_rows), device=t.device, dtype=torch.int64)[:, None]
+        r = r * row_stride + row0
         idx = r * E + col
         h = ((idx & 0xFFFFFFFF) * 0x9E3779B1 + seed) & 0xFFFFFFFF
         h = _mix(h ^ ((idx >> 32) * 0x85EBCA77 & 0xFFFFFFFF), torch)
@@ -67,17 +73,27 @@ def compact_problem(cfg, batch) -> Tuple[object, tuple, Dict[str, np.ndarray], D
     the item vocabulary shrunk to the touched ids; ``obatch`` = the batch with remapped ids;
     ``tables`` = compact 'emb.ns' / 'emb.seq_item' (float64) with the full tables' values;
     ``rowmap[name][j]`` = full-table row of compact row j."""
+    ocfg, obatches, tables, rowmap = compact_problem_multi(cfg, [batch])
+    return ocfg, obatches[0], tables, rowmap
+
+
+def compact_problem_multi(cfg, batches) -> Tuple[object, list, Dict[str, np.ndarray], Dict[str, np.ndarray]]:
+    """compact_problem over several batches sharing ONE compact table (the union of the rows any of them
+    touches): a multi-step oracle run.  Rows no batch touches never receive a gradient, and Adagrad
+    leaves zero-gradient rows (and the tables' clip norms) unchanged, so training on the compact
+    tables is training on the full ones."""
     import copy
     from recommend_amd.params import ns_table_offsets
-    ns, seq, lab = batch
     ocfg = copy.deepcopy(cfg)
     full_off = ns_table_offsets(cfg)
-    ons = dict(ns)
+    obatches = [(dict(ns), dict(seq), lab) for (ns, seq, lab) in batches]
     rows_ns, card = [], {}
     for name in cfg.ns_feature_names():
-        if name in cfg.sparse_features and name in ns:
-            u, inv = np.unique(ns[name].reshape(-1), return_inverse=True)
-            ons[name] = inv.reshape(ns[name].shape).astype(np.int64)
+        if name in cfg.sparse_features and any(name in b[0] for b in batches):
+            u = np.unique(np.concatenate([b[0][name].reshape(-1) for b in batches if name in b[0]]))
+            for ob in obatches:
+                if name in ob[0]:
+                    ob[0][name] = np.searchsorted(u, ob[0][name]).astype(np.int64)
             card[name] = len(u)
             rows_ns.append(full_off[name] + u)
     ocfg.sparse_features = {k: card.get(k, 1) for k in cfg.sparse_features}
@@ -85,16 +101,15 @@ def compact_problem(cfg, batch) -> Tuple[object, tuple, Dict[str, np.ndarray], D
     if rows_ns:
         rowmap['emb.ns'] = np.concatenate(rows_ns)
         tables['emb.ns'] = table_values_np(rowmap['emb.ns'], cfg.ns_embedding_dim, TABLE_SEED['emb.ns']).astype(np.float64)
-    oseq = dict(seq)
-    if cfg.seq_item_vocab and seq:
-        allids = np.concatenate([v.reshape(-1) for v in seq.values()])
-        u = np.unique(allids)
-        for k, v in seq.items():
-            oseq[k] = np.searchsorted(u, v).astype(np.int64)
+    if cfg.seq_item_vocab and any(b[1] for b in batches):
+        u = np.unique(np.concatenate([v.reshape(-1) for b in batches for v in b[1].values()]))
+        for ob in obatches:
+            for k, v in ob[1].items():
+                ob[1][k] = np.searchsorted(u, v).astype(np.int64)
         ocfg.seq_item_vocab = len(u)
         rowmap['emb.seq_item'] = u
         tables['emb.seq_item'] = table_values_np(u, cfg.seq_feature_dim, TABLE_SEED['emb.seq_item']).astype(np.float64)
-    return ocfg, (ons, oseq, lab), tables, rowmap
+    return ocfg, obatches, tables, rowmap
 
 
 def bank_samples(name: str, size: int) -> np.ndarray:

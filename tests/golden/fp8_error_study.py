@@ -9,7 +9,7 @@ import sys, math, time, os
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(os.path.dirname(HERE))); sys.path.insert(0, os.path.dirname(HERE))
 import numpy as np, torch
-torch.set_num_threads(8)
+torch.set_num_threads(int(os.environ.get('THREADS', '8')))
 from fullsize_common import BATCH_SEED, MODEL_SEED, compact_problem, setup_config
 from oracle import onetrans_ref as R
 from recommend_amd.data import make_batch
@@ -33,6 +33,16 @@ def ein(eq, *ops):
         return orig(eq, q, k)
     if MODE and eq == 'bhqk,bkhd->bqhd':
         w, v = ops
+        if MODE in ('qk32_pfp8', 'qk32_vfp8', 'qk32_v32k', 'qk32_pv_fp8'):
+            if MODE in ('qk32_pfp8', 'qk32_pv_fp8'):
+                w = (w * 256).to(E4).to(w.dtype) / 256
+            if MODE in ('qk32_vfp8', 'qk32_v32k', 'qk32_pv_fp8'):
+                blk = 32 if MODE == 'qk32_v32k' else 64
+                B, I, H, hd = v.shape
+                Ip = (I + blk - 1) // blk * blk
+                vp = torch.zeros(B, Ip, H, hd, dtype=v.dtype); vp[:, :I] = v
+                v = qrows(vp.permute(0, 2, 3, 1).contiguous(), blk).permute(0, 3, 1, 2)[:, :I]
+            return orig(eq, w, v)
         if MODE in ('fp8', 'smooth', 'qkbf16'):
             w = (w * 256).to(E4).to(w.dtype) / 256
             B, I, H, hd = v.shape
@@ -59,6 +69,6 @@ def run(mode):
         out = R.forward(Pt, ocfg, R.to_torch(ons, dtype=torch.float32), R.to_torch(oseq, dtype=torch.float32), training=False)
     return torch.stack([out['logits'][t].reshape(-1) for t in cfg.tasks])
 t0 = time.time(); ref = run(None); print('ref', time.time() - t0, flush=True)
-for m in ['fp8', 'smooth', 'qkbf16', 'fp8_pbf16', 'bf16']:
+for m in os.environ.get('MODES', 'fp8,smooth,qkbf16,fp8_pbf16,bf16').split(','):
     lg = run(m)
     print(m, 'max |d logit|', float((lg - ref).abs().max()), 'mean', float((lg - ref).abs().mean()), flush=True)

@@ -4,7 +4,11 @@ oracle (oracle/onetrans_ref.py, float64) in the build container:
 
     python tests/golden/make_fullsize_golden.py C2      # -> tests/golden/fullsize_C2.npz
     python tests/golden/make_fullsize_golden.py C4      # -> tests/golden/fullsize_C4.npz
-    python tests/golden/make_fullsize_golden.py C5 fwd  # -> tests/golden/fullsize_C5_fwd.npz (forward only)
+    python tests/golden/make_fullsize_golden.py C3      # -> tests/golden/fullsize_C3.npz (pyramid stress)
+    python tests/golden/make_fullsize_golden.py C5 fwd  # -> tests/golden/fullsize_C5_fwd.npz (forward only,
+                                                        #    C5's global batch: 8 ranks x 512 = 4096 samples)
+    python tests/golden/make_fullsize_golden.py C5 train32  # -> tests/golden/fullsize_C5_train32.npz (one
+                                                        #    train step, float32 oracle: the bf16 gradient check)
 
 The step (tests/fullsize_common.py): BASELINE batch and model shape, perturbed Keras init (seed 0),
 Criteo-shape batch (seed BATCH_SEED), dropout on (the model's first training step seed), loss =
@@ -36,7 +40,7 @@ from recommend_amd.data import make_batch  # noqa: E402
 from recommend_amd.params import init_params, keras_variables  # noqa: E402
 
 
-def main(name: str, slice_size: int = 128, threads: int = 0) -> None:
+def main(name: str, slice_size: int = 128, threads: int = 0, dtype=torch.float64, suffix: str = '') -> None:
     if threads:
         torch.set_num_threads(threads)
     t0 = time.time()
@@ -46,9 +50,10 @@ def main(name: str, slice_size: int = 128, threads: int = 0) -> None:
     batch = make_batch(B, cfg, seed=BATCH_SEED)
     ocfg, (ns, seq, lab), tables, rowmap = compact_problem(cfg, batch)
     Pall = dict(P, **tables)
-    Pt = R.to_torch(Pall)
+    Pt = R.to_torch(Pall, dtype=dtype)
     seed = dropout_seed()
-    loss, grads, out = R.loss_and_grads_sliced(Pt, ocfg, R.to_torch(ns), R.to_torch(seq), R.to_torch(lab),
+    loss, grads, out = R.loss_and_grads_sliced(Pt, ocfg, R.to_torch(ns, dtype=dtype), R.to_torch(seq, dtype=dtype),
+                                               R.to_torch(lab, dtype=dtype),
                                                training=True, seed=seed, slice_size=slice_size)
     print(f'{name}: loss {float(loss):.6f} ({time.time() - t0:.0f}s)', flush=True)
     state = R.init_state(Pt, ocfg)
@@ -60,6 +65,7 @@ def main(name: str, slice_size: int = 128, threads: int = 0) -> None:
         g = grads[k].reshape(-1).numpy()
         idx = bank_samples(k, g.size)
         res[f'g_idx.{k}'] = idx
+        g = g.astype(np.float64)
         res[f'g.{k}'] = g[idx]
         res[f'g_norm.{k}'] = np.array(np.sqrt((g * g).sum()))
         res[f'g_max.{k}'] = np.array(np.abs(g).max())
@@ -74,17 +80,20 @@ def main(name: str, slice_size: int = 128, threads: int = 0) -> None:
         res[f't_rows.{k}'] = rows[pick]
         res[f't_g.{k}'] = g[pick]
         res[f't_w1.{k}'] = newP[k].numpy()[pick]
-    out_path = os.path.join(HERE, f'fullsize_{name}.npz')
+    res = {k: (v.astype(np.float64) if v.dtype == np.float32 else v) for k, v in res.items()}
+    out_path = os.path.join(HERE, f'fullsize_{name}{suffix}.npz')
     np.savez_compressed(out_path, **res)
     print(f'wrote {out_path} ({os.path.getsize(out_path) / 1e6:.1f} MB, {time.time() - t0:.0f}s)')
 
 
-def main_forward(name: str, slice_size: int = 8) -> None:
+def main_forward(name: str, slice_size: int = 8, replicas: int = 8) -> None:
     """Inference-mode forward only (the C5 bf16 / fp8-attention parity point): logits and probabilities of
-    the full BASELINE batch, float32 oracle (the compared path is bf16, whose error is far above f32's)."""
+    the configuration's GLOBAL batch (``replicas`` GPUs x the per-GPU batch: C5 is 8 x 512 = 4096 samples,
+    enough that the exact AUC's pair-flip noise is well under north_star's 1e-3), float32 oracle (the
+    compared path is bf16, whose error is far above f32's)."""
     t0 = time.time()
     cfg = setup_config(name)
-    B = cfg._batch
+    B = cfg._batch * replicas
     P = init_params(cfg, cfg.ns_input_width(), seed=MODEL_SEED, perturb=True, with_tables=False)
     batch = make_batch(B, cfg, seed=BATCH_SEED)
     ocfg, (ns, seq, lab), tables, rowmap = compact_problem(cfg, batch)
@@ -100,7 +109,8 @@ def main_forward(name: str, slice_size: int = 8) -> None:
             probs.append(torch.stack([out['probs'][t].reshape(-1) for t in cfg.tasks]))
             if s0 % (8 * slice_size) == 0:
                 print(f'{name} forward: {sl.stop}/{B} samples ({time.time() - t0:.0f}s)', flush=True)
-    res = {'config': np.array(name), 'B': np.array(B), 'logits': torch.cat(logits, 1).double().numpy(),
+    res = {'config': np.array(name), 'B': np.array(B), 'B_gpu': np.array(cfg._batch),
+           'logits': torch.cat(logits, 1).double().numpy(),
            'probs': torch.cat(probs, 1).double().numpy()}
     out_path = os.path.join(HERE, f'fullsize_{name}_fwd.npz')
     np.savez_compressed(out_path, **res)
@@ -110,5 +120,7 @@ def main_forward(name: str, slice_size: int = 8) -> None:
 if __name__ == '__main__':
     if len(sys.argv) > 2 and sys.argv[2] == 'fwd':
         main_forward(sys.argv[1])
+    elif len(sys.argv) > 2 and sys.argv[2] == 'train32':
+        main(sys.argv[1], 8, dtype=torch.float32, suffix='_train32')
     else:
         main(sys.argv[1] if len(sys.argv) > 1 else 'C2', int(sys.argv[2]) if len(sys.argv) > 2 else 128)

@@ -36,12 +36,32 @@ def test_save_load_roundtrip(dev, tmp_path):
     for k in a:
         assert np.array_equal(a[k], b[k]), k
     assert tr2.history['train_loss'] == [1.25]
+    assert tr2.optimizer.steps_done == tr.optimizer.steps_done == 1     # the warm-up ramp resumes
+    assert 'optimizer_steps' not in tr2.history
     ns, seq, _ = batch
     with torch.no_grad():
         pa = tr.model((ns_t(ns, dev), ns_t(seq, dev)))
         pb = tr2.model((ns_t(ns, dev), ns_t(seq, dev)))
     for t in cfg.tasks:
         assert torch.equal(pa[t], pb[t])
+
+
+def test_evaluate_reports_regression_tasks(dev):
+    """evaluate(): AUC for the BCE tasks, mse / mae for a task trained with MSE (train.py:106,
+    evaluate.py:52-54)."""
+    cfg = small_criteo('head')
+    cfg.tasks = ['ctr', 'watch_time']
+    tr = OneTransTrainer(cfg, model=OneTransModel(cfg, device=dev, seed=0))
+    batches = [make_batch(24, cfg, seed=300 + i) for i in range(2)]
+    for b in batches:
+        b[2]['watch_time'] = np.linspace(0.0, 1.0, 24, dtype=np.float32).reshape(-1, 1)
+    res = tr.evaluate(batches)
+    assert set(res) == {'ctr_auc', 'ctr_keras_auc', 'watch_time_mse', 'watch_time_mae'}
+    with torch.no_grad():
+        p = torch.cat([tr.val_step(b)['probs'][1].cpu() for b in batches]).double().numpy()
+    y = np.concatenate([b[2]['watch_time'].reshape(-1) for b in batches]).astype(np.float64)
+    assert abs(res['watch_time_mse'] - np.mean((p - y) ** 2)) < 1e-9
+    assert abs(res['watch_time_mae'] - np.mean(np.abs(p - y))) < 1e-9
 
 
 def test_device_prefetcher_feeds_training(dev):

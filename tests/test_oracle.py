@@ -83,6 +83,24 @@ def test_dropout_mask_properties():
     assert int(km.fmix32(np.array([1], np.uint32))[0]) == 0x514E28B7
 
 
+@pytest.mark.parametrize('b0,I,d', [(0, 140, 128), (1024, 140, 256), (2048 * 3, 1036, 512), (7, 33, 64)])
+def test_layer_seed_equals_global_sample_index(b0, I, d):
+    """A data-parallel rank whose local sample b is global sample b0 + b draws the full batch's dropout
+    mask by seed alone (recommend_amd.model.layer_seed; the kernels hash local indices)."""
+    from recommend_amd.model import layer_seed
+    seed, site, B = 0x5EED0000 + 0x9E3779B9, 3, 5
+    b = np.arange(B, dtype=np.uint64)[:, None, None]
+    p = np.arange(0, I, max(1, I // 7), dtype=np.uint64)[None, :, None]
+    n = np.arange(d, dtype=np.uint64)[None, None, :]
+    local = (b * np.uint64(I) + p) * np.uint64(d) + n
+    glob = ((b + np.uint64(b0)) * np.uint64(I) + p) * np.uint64(d) + n
+    got = km.dropout_keep(layer_seed(seed, b0, I, d), site, local, 0.1)
+    assert np.array_equal(got, km.dropout_keep(seed, site, glob, 0.1))
+    np.testing.assert_array_equal(
+        R.dropout_scale(layer_seed(seed, b0, I, d), site, B, I, d, p.reshape(-1), 0.1, torch.float64).numpy(),
+        R.dropout_scale(seed, site, B, I, d, p.reshape(-1), 0.1, torch.float64, b0=b0).numpy())
+
+
 def test_bce_clip_rmsprop_kat():
     assert abs(km.keras_bce(np.array([1.0]), np.array([0.5])) - (-math.log(0.5 + 1e-7))) < 1e-15
     # p clipped to 1-1e-7 then log(1 - p + eps) = log(2e-7)

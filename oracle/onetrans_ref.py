@@ -10,7 +10,7 @@ Follows ``rank/scaling_up/oneTrans/practice/model.py`` and ``train.py``:
                        Python loops (``for i in range(seq_len)``, model.py:84-88, 154-161),
                        the -1e9 causal fill (model.py:109-110) and the group rule of
                        ``_get_projection_weights`` (model.py:67-74)
-* ``block_vectorized`` the same math as grouped einsums, computing only the tail queries a
+* ``block_vectorized`` the same math as one matmul per weight group, computing only the tail queries a
                        layer keeps (exactness lemma)
 * ``forward``          model.py:335-393 (pyramid gather at :356/:371 with the D2 fix,
                        output_norm, last-token heads Dense(d/2, gelu) -> Dense(1, sigmoid))
@@ -107,6 +107,25 @@ def tokenizer(P: Dict[str, Tensor], cfg, ns: Dict[str, Tensor], seq: Dict[str, T
 
 
 # ----------------------------------------------------------------------------- blocks
+def _grouped_mm(x: Tensor, W: Tensor, groups: Tensor, bias: Optional[Tensor] = None) -> Tensor:
+    """Mixed-parameter Dense (model.py:84-88, 154-161): row r of x [..., k] times W[groups[r]] (+ bias),
+    groups broadcast against x's leading dims.  One matmul per weight group over the rows of that group
+    (the per-token products of the reference loop, without materialising W[groups])."""
+    lead, k = x.shape[:-1], x.shape[-1]
+    xf = x.reshape(-1, k)
+    gf = torch.as_tensor(groups).expand(lead).reshape(-1)
+    parts, idx_parts = [], []
+    for g in torch.unique(gf).tolist():
+        idx = torch.nonzero(gf == g).reshape(-1)
+        y = xf[idx] @ W[g]
+        parts.append(y if bias is None else y + bias[g])
+        idx_parts.append(idx)
+    idx = torch.cat(idx_parts)
+    inv = torch.empty_like(idx)
+    inv[idx] = torch.arange(idx.numel())
+    return torch.cat(parts, 0)[inv].reshape(*lead, -1)
+
+
 def _attn_full(q: Tensor, k: Tensor, v: Tensor, H: int) -> Tensor:
     """model.py:100-114: [B,L,d] x3 -> [B,L,d], causal, -1e9 fill."""
     B, L, d = q.shape
@@ -179,8 +198,8 @@ def block_vectorized(P, cfg, l: int, x: Tensor, keep: int, training: bool, seed:
     gt = groups[I - keep:]
     xn = rmsnorm(x, P[f'blk.{l}.norm1'])
     W = P[f'blk.{l}.wqkv']
-    kv = torch.einsum('bid,ide->bie', xn, W[groups][:, :, d:])
-    q = torch.einsum('bid,ide->bie', xn[:, I - keep:], W[gt][:, :, :d])
+    kv = _grouped_mm(xn, W[:, :, d:], groups)
+    q = _grouped_mm(xn[:, I - keep:], W[:, :, :d], gt)
     k, v = kv[..., :d], kv[..., d:]
     qh = q.reshape(B, keep, H, hd); kh = k.reshape(B, I, H, hd); vh = v.reshape(B, I, H, hd)
     s = torch.einsum('bqhd,bkhd->bhqk', qh, kh) / math.sqrt(hd)
@@ -191,8 +210,8 @@ def block_vectorized(P, cfg, l: int, x: Tensor, keep: int, training: bool, seed:
     a = o @ P[f'blk.{l}.wo']
     xt = x[:, I - keep:] + apply_dropout(a, training, rate, seed, 2 * l, I, tail)
     xn2 = rmsnorm(xt, P[f'blk.{l}.norm2'])
-    h = gelu(torch.einsum('bid,idf->bif', xn2, P[f'blk.{l}.w1'][gt]) + P[f'blk.{l}.b1'][gt])
-    f = torch.einsum('bif,ifd->bid', h, P[f'blk.{l}.w2'][gt]) + P[f'blk.{l}.b2'][gt]
+    h = gelu(_grouped_mm(xn2, P[f'blk.{l}.w1'], gt, P[f'blk.{l}.b1']))
+    f = _grouped_mm(h, P[f'blk.{l}.w2'], gt, P[f'blk.{l}.b2'])
     return xt + apply_dropout(f, training, rate, seed, 2 * l + 1, I, tail)
 
 
@@ -210,8 +229,8 @@ def _block_selected(P, cfg, l: int, x: Tensor, sel: np.ndarray, training: bool, 
     bidx = torch.arange(B)[:, None]
     xn = rmsnorm(x, P[f'blk.{l}.norm1'])
     W = P[f'blk.{l}.wqkv']
-    kv = torch.einsum('bid,ide->bie', xn, W[groups][:, :, d:])
-    q = torch.einsum('bjd,bjde->bje', xn[bidx, st], W[gt][..., :d])
+    kv = _grouped_mm(xn, W[:, :, d:], groups)
+    q = _grouped_mm(xn[bidx, st], W[:, :, :d], gt)
     k, v = kv[..., :d], kv[..., d:]
     qh = q.reshape(B, K, H, hd); kh = k.reshape(B, I, H, hd); vh = v.reshape(B, I, H, hd)
     s = torch.einsum('bqhd,bkhd->bhqk', qh, kh) / math.sqrt(hd)
@@ -221,8 +240,8 @@ def _block_selected(P, cfg, l: int, x: Tensor, sel: np.ndarray, training: bool, 
     a = o @ P[f'blk.{l}.wo']
     xt = x[bidx, st] + apply_dropout(a, training, rate, seed, 2 * l, I, sel)
     xn2 = rmsnorm(xt, P[f'blk.{l}.norm2'])
-    h = gelu(torch.einsum('bjd,bjdf->bjf', xn2, P[f'blk.{l}.w1'][gt]) + P[f'blk.{l}.b1'][gt])
-    f = torch.einsum('bjf,bjfd->bjd', h, P[f'blk.{l}.w2'][gt]) + P[f'blk.{l}.b2'][gt]
+    h = gelu(_grouped_mm(xn2, P[f'blk.{l}.w1'], gt, P[f'blk.{l}.b1']))
+    f = _grouped_mm(h, P[f'blk.{l}.w2'], gt, P[f'blk.{l}.b2'])
     return xt + apply_dropout(f, training, rate, seed, 2 * l + 1, I, sel)
 
 

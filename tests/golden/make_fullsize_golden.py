@@ -86,7 +86,7 @@ def main(name: str, slice_size: int = 128, threads: int = 0, dtype=torch.float64
     print(f'wrote {out_path} ({os.path.getsize(out_path) / 1e6:.1f} MB, {time.time() - t0:.0f}s)')
 
 
-def main_forward(name: str, slice_size: int = 8, replicas: int = 8) -> None:
+def main_forward(name: str, slice_size: int = 32, replicas: int = 8) -> None:
     """Inference-mode forward only (the C5 bf16 / fp8-attention parity point): logits and probabilities of
     the configuration's GLOBAL batch (``replicas`` GPUs x the per-GPU batch: C5 is 8 x 512 = 4096 samples,
     enough that the exact AUC's pair-flip noise is well under north_star's 1e-3), float32 oracle (the

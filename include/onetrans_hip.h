@@ -207,6 +207,13 @@ int ot_attn_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, const 
 size_t ot_attn_fwd_fp8_workspace_size(int B, int H, int I, int head_dim);
 int ot_attn_fwd_fp8(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos,
                     int head_dim, float* out, float* lse, void* workspace, size_t ws_bytes, void* stream);
+/* flags of ot_attn_fwd_fp8_ex */
+#define OT_FP8_DEQUANT 1 /* training: overwrite qkv's Q (kept query rows), K and V with their dequantised fp8
+                          * values (e4m3 x block scale: exact in bf16), so ot_attn_bwd in the bf16 GEMM mode
+                          * recomputes S from the products the fp8 forward summed (its P matches this lse; the
+                          * straight-through gradient of the forward that ran) */
+int ot_attn_fwd_fp8_ex(float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos, int head_dim,
+                       float* out, float* lse, void* workspace, size_t ws_bytes, int flags, void* stream);
 /* dqkv: like qkv (dq written on the K kept query rows only; dk, dv on all rows);
  * ws: ot_attn_bwd_workspace_size(B, H, K) bytes (row stats padded to 32 queries per (b, h)) */
 size_t ot_attn_bwd_workspace_size(int B, int H, int K);

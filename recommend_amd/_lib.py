@@ -21,6 +21,7 @@ OT_EPI_BIAS, OT_EPI_GELU_BWD, OT_EPI_GELU = 1, 2, 4
 OT_EPI_DROPOUT, OT_EPI_RESIDUAL, OT_EPI_ACCUMULATE = 8, 16, 32
 OT_EPI_ROW_RSTD, OT_EPI_RMSNORM_BWD, OT_EPI_ROWDOT = 64, 128, 256
 OT_MATMUL_F32, OT_MATMUL_SPLIT_BF16, OT_MATMUL_BF16 = 0, 1, 2
+OT_FP8_DEQUANT = 1
 MATMUL_MODES = {'f32': OT_MATMUL_F32, 'split': OT_MATMUL_SPLIT_BF16, 'bf16': OT_MATMUL_BF16}
 
 
@@ -67,6 +68,7 @@ SIGNATURES = {
     'ot_attn_fwd': (c_int, [P, I64, c_int, c_int, c_int, c_int, P, c_int, P, P, P]),
     'ot_attn_fwd_fp8_workspace_size': (c_size_t, [c_int, c_int, c_int, c_int]),
     'ot_attn_fwd_fp8': (c_int, [P, I64, c_int, c_int, c_int, c_int, P, c_int, P, P, P, c_size_t, P]),
+    'ot_attn_fwd_fp8_ex': (c_int, [P, I64, c_int, c_int, c_int, c_int, P, c_int, P, P, P, c_size_t, c_int, P]),
     'ot_attn_bwd_workspace_size': (c_size_t, [c_int, c_int, c_int]),
     'ot_attn_bwd': (c_int, [P, I64, P, P, P, c_int, c_int, c_int, c_int, P, c_int, P, P, P]),
     'ot_attn_bwd_ex_workspace_size': (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),

@@ -9,12 +9,20 @@
 //     ([dim][key], keys permuted inside each 64-key block into the order the P operand holds them).
 //  2. attn_fwd_fp8_kernel — one wave per (sample, head) as attn_fwd_split_kernel, 32 queries x 64 keys
 //     per step:  S^T = K Q^T  (one 32x32x64 MFMA per 32-key tile and 64 dims; Q quantised in registers
-//     once per query block with one scale per (query, 32 dims), pre-scaled by log2(e)/sqrt(hd)),
-//     online softmax in f32,
+//     once per query block with one scale per (query, 32 dims), the accumulator scaled by
+//     log2(e)/sqrt(hd) in f32), online softmax in f32,
 //     O^T += V^T P^T  (P^T is the two S^T accumulators converted to e4m3 in place: lane half hh, element
 //     j = 16t + r <-> key 32t + acc_row(r, hh); the V^T image holds the same keys at byte 32hh + j).
 //     P is kept as P * 2^8 (exp2(s - m + 8): [0, 256], inside e4m3's range, small values stay normal)
 //     and the row sum l in the same units, so O = sum(P V) / l needs no extra scale.
+//
+// OT_FP8_DEQUANT (training): both launches also write the dequantised operands back into qkv (each
+// Q / K / V element replaced by its e4m3 value times its block scale — exactly representable in bf16),
+// so the backward (ot_attn_bwd in the bf16 GEMM mode) recomputes S from the very products the fp8
+// forward summed: its P matches the forward's log-sum-exp and delta = rowsum(dO o O) is the
+// straight-through gradient of the forward that ran (P's own e4m3 rounding aside).  Without it the
+// backward would recompute S from unquantised operands against the fp8 forward's statistics (rows of
+// P off by up to the fp8 lse error).
 //
 // Operand layout of the 32x32x64 scaled MFMA, measured on the box (tools/micro/fp8_probe.hip): A lane l
 // holds row l&31, B lane l column l&31; byte j of lane half h meets byte j of the other operand's lane
@@ -53,6 +61,13 @@ __device__ __forceinline__ f32x16 mfma_fp8(const i32x8& a, const i32x8& b, f32x1
   return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 0, 0, 0, sa, 0, sb);
 }
 
+// e4m3 bytes of v (element 0 in the low byte) back to f32, times the block scale 2^e
+__device__ __forceinline__ f32x4 unpack4(int v, float sc) {
+  typedef float v2f __attribute__((ext_vector_type(2)));
+  const v2f lo = __builtin_amdgcn_cvt_pk_f32_fp8(v, false), hi = __builtin_amdgcn_cvt_pk_f32_fp8(v, true);
+  return f32x4{lo.x * sc, lo.y * sc, hi.x * sc, hi.y * sc};
+}
+
 // 16 bytes at p (operand bytes 0-15) and 16 at p + gap (bytes 16-31)
 __device__ __forceinline__ i32x8 load32(const uint8_t* p, int gap = 16) {
   const i32x4 lo = *reinterpret_cast<const i32x4*>(p);
@@ -88,8 +103,8 @@ inline size_t fp8_pack_bytes(int64_t BH, int I, int HD) {
 
 // grid (B*H, Ip/64), 256 threads (B*H on x: up to 2^31 - 1 heads).  Keys >= I are zeros (the causal mask removes them).
 template <int HD>
-__global__ __launch_bounds__(256) void attn_fp8_pack_kernel(const float* __restrict__ qkv, int64_t ld, int H, int I,
-                                                            Fp8Pack f) {
+__global__ __launch_bounds__(256) void attn_fp8_pack_kernel(float* qkv, int64_t ld, int H, int I, Fp8Pack f,
+                                                            int dequant) {
   constexpr int VLD = HD + 1;
   __shared__ float vs_f[64 * VLD];
   __shared__ __attribute__((aligned(16))) uint8_t vt_img[HD * 64];
@@ -97,7 +112,7 @@ __global__ __launch_bounds__(256) void attn_fp8_pack_kernel(const float* __restr
   const int b = bh / H, h = bh % H, d = H * HD;
   const int64_t Ip = fp8_ipad(I);
   const int t = threadIdx.x;
-  const float* base = qkv + (int64_t)b * I * ld + h * HD;
+  float* base = qkv + (int64_t)b * I * ld + h * HD;
 
   // ---- K: thread = (key, 16 dims); a 32-dim scale block = 2 adjacent lanes
   constexpr int TPK = HD / 16, KPP = 256 / TPK;
@@ -131,6 +146,12 @@ __global__ __launch_bounds__(256) void attn_fp8_pack_kernel(const float* __restr
     const int64_t row = (int64_t)bh * Ip + key;
     *reinterpret_cast<i32x4*>(f.k8 + row * HD + 16 * part) = o;
     if ((part & 1) == 0) f.ks[row * (HD / 32) + part / 2] = (uint8_t)(e + 127);
+    if (dequant && key < I) {
+      const float sc = fp8::pow2f(e);
+      f32x4* dst = reinterpret_cast<f32x4*>(base + (int64_t)key * ld + d + 16 * part);
+      dst[0] = fp8::unpack4(o.x, sc); dst[1] = fp8::unpack4(o.y, sc);
+      dst[2] = fp8::unpack4(o.z, sc); dst[3] = fp8::unpack4(o.w, sc);
+    }
   }
 
   // ---- V: stage the [64 keys][HD] tile, then thread = (dim, KPT keys)
@@ -157,6 +178,11 @@ __global__ __launch_bounds__(256) void attn_fp8_pack_kernel(const float* __restr
     for (int i = 0; i < KPT; i += 2) {
       const int k0 = g * KPT + i;
       const int v2 = __builtin_amdgcn_cvt_pk_fp8_f32(vs_f[k0 * VLD + c] * inv, vs_f[(k0 + 1) * VLD + c] * inv, 0, false);
+      if (dequant) {            // this thread owns (dim c, keys k0, k0 + 1) of the staged tile
+        const f32x4 dv = fp8::unpack4(v2, fp8::pow2f(e));
+        vs_f[k0 * VLD + c] = dv.x;
+        vs_f[(k0 + 1) * VLD + c] = dv.y;
+      }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int k = k0 + u, kk = k & 31;
@@ -173,15 +199,24 @@ __global__ __launch_bounds__(256) void attn_fp8_pack_kernel(const float* __restr
     *reinterpret_cast<i32x4*>(f.vt8 + ((int64_t)bh * HD + c) * Ip + 64 * kb + 16 * q) =
         *reinterpret_cast<const i32x4*>(vt_img + c * 64 + 16 * q);
   }
+  if (dequant) {
+    for (int i = t; i < 64 * HD / 4; i += 256) {
+      const int kk = i / (HD / 4), c4 = i % (HD / 4);
+      const int key = 64 * kb + kk;
+      const float* src = vs_f + kk * VLD + 4 * c4;
+      if (key < I) *reinterpret_cast<f32x4*>(base + (int64_t)key * ld + 2 * d + 4 * c4) = f32x4{src[0], src[1], src[2], src[3]};
+    }
+  }
 }
 
 struct Fp8AttnArgs {
-  const float* qkv; int64_t ld; int d;
+  float* qkv; int64_t ld; int d;
   float* out; float* lse;
   int B, H, I, K;
   float scale;
   const int32_t* qpos;
   Fp8Pack f;
+  int dequant;
 };
 
 // one wave per (b, h), 4 waves per block
@@ -196,7 +231,7 @@ __global__ __launch_bounds__(256) void attn_fwd_fp8_kernel(Fp8AttnArgs p) {
   const int b = pair / p.H, h = pair % p.H;
   const int I = p.I, K = p.K, q_off = I - K;
   const int64_t Ip = fp8_ipad(I);
-  const float* Q = p.qkv + (int64_t)b * I * p.ld + h * HD;
+  float* Q = p.qkv + (int64_t)b * I * p.ld + h * HD;
   const uint8_t* k8 = p.f.k8 + (int64_t)pair * Ip * HD + 16 * hh;
   const uint8_t* ksc = p.f.ks + (int64_t)pair * Ip * (HD / 32) + hh;
   const uint8_t* vt8 = p.f.vt8 + (int64_t)pair * HD * Ip + 32 * hh;
@@ -216,12 +251,12 @@ __global__ __launch_bounds__(256) void attn_fwd_fp8_kernel(Fp8AttnArgs p) {
     int qs[NKS];
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
-      const float* src = Q + (int64_t)qpos * p.ld + 64 * ks + 16 * hh;
+      float* src = Q + (int64_t)qpos * p.ld + 64 * ks + 16 * hh;
       float x[32];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const f32x4 v = *reinterpret_cast<const f32x4*>(src + 4 * (q & 3) + 32 * (q >> 2));
-        x[4 * q] = v.x * qscale; x[4 * q + 1] = v.y * qscale; x[4 * q + 2] = v.z * qscale; x[4 * q + 3] = v.w * qscale;
+        x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
       }
       float am0 = 0.f, am1 = 0.f;
 #pragma unroll
@@ -237,6 +272,14 @@ __global__ __launch_bounds__(256) void attn_fwd_fp8_kernel(Fp8AttnArgs p) {
                                         x[19 + 4 * w] * inv1);
       }
       qs[ks] = (hh ? e1 : e0) + 127;
+      if (p.dequant && j < K) {          // this lane's 32 elements of query row qpos, dequantised in place
+        const float s0 = fp8::pow2f(e0), s1 = fp8::pow2f(e1);
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          *reinterpret_cast<f32x4*>(src + 4 * w) = fp8::unpack4(qa[ks][w], s0);
+          *reinterpret_cast<f32x4*>(src + 32 + 4 * w) = fp8::unpack4(qa[ks][4 + w], s1);
+        }
+      }
     }
     f32x16 oacc[NC];
 #pragma unroll
@@ -280,6 +323,8 @@ __global__ __launch_bounds__(256) void attn_fwd_fp8_kernel(Fp8AttnArgs p) {
         for (int r = 0; r < 16; ++r) s[t2][r] = 0.f;
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) s[t2] = fp8::mfma_fp8(kf[t2][ks], qa[ks], s[t2], kscale[t2][ks], qs[ks]);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[t2][r] *= qscale;          // log2 domain
       }
 #ifdef OT_FP8_DEBUG
       if (qb == 0 && kb == 0 && pair == 0) {
@@ -363,9 +408,12 @@ extern "C" size_t ot_attn_fwd_fp8_workspace_size(int B, int H, int I, int head_d
   return fp8_pack_bytes((int64_t)B * H, I, head_dim);
 }
 
-extern "C" int ot_attn_fwd_fp8(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos,
-                               int head_dim, float* out, float* lse, void* workspace, size_t ws_bytes, void* stream) {
+extern "C" int ot_attn_fwd_fp8_ex(float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos,
+                                  int head_dim, float* out, float* lse, void* workspace, size_t ws_bytes, int flags,
+                                  void* stream) {
   OT_REQUIRE(qkv && out && lse, "ot_attn_fwd_fp8: null operand");
+  OT_REQUIRE((flags & ~OT_FP8_DEQUANT) == 0, "ot_attn_fwd_fp8: unknown flags 0x%x", flags);
+  const int dq = (flags & OT_FP8_DEQUANT) ? 1 : 0;
   OT_REQUIRE(B >= 0 && H > 0 && I > 0 && K > 0 && K <= I, "ot_attn_fwd_fp8: bad sizes B=%d H=%d I=%d K=%d", B, H, I, K);
   OT_REQUIRE(head_dim == 64 || head_dim == 128, "ot_attn_fwd_fp8: head_dim %d (64 or 128)", head_dim);
   OT_REQUIRE(ld % 4 == 0 && ld >= 3 * H * head_dim, "ot_attn_fwd_fp8: ld must be >= 3d and a multiple of 4");
@@ -378,13 +426,20 @@ extern "C" int ot_attn_fwd_fp8(const float* qkv, int64_t ld, int B, int H, int I
              (long long)BH, I);
   const dim3 pg((unsigned)BH, (unsigned)(fp8_ipad(I) / 64));
   hipStream_t s = (hipStream_t)stream;
-  if (head_dim == 64) hipLaunchKernelGGL(attn_fp8_pack_kernel<64>, pg, dim3(256), 0, s, qkv, ld, H, I, f);
-  else hipLaunchKernelGGL(attn_fp8_pack_kernel<128>, pg, dim3(256), 0, s, qkv, ld, H, I, f);
+  if (head_dim == 64) hipLaunchKernelGGL(attn_fp8_pack_kernel<64>, pg, dim3(256), 0, s, qkv, ld, H, I, f, dq);
+  else hipLaunchKernelGGL(attn_fp8_pack_kernel<128>, pg, dim3(256), 0, s, qkv, ld, H, I, f, dq);
   OT_LAUNCH_CHECK("ot_attn_fwd_fp8(pack)");
-  Fp8AttnArgs p{qkv, ld, H * head_dim, out, lse, B, H, I, K, 1.f / sqrtf((float)head_dim), qpos, f};
+  Fp8AttnArgs p{qkv, ld, H * head_dim, out, lse, B, H, I, K, 1.f / sqrtf((float)head_dim), qpos, f, dq};
   const unsigned grid = ceil_div(BH, 4);
   if (head_dim == 64) hipLaunchKernelGGL(attn_fwd_fp8_kernel<64>, dim3(grid), dim3(256), 0, s, p);
   else hipLaunchKernelGGL(attn_fwd_fp8_kernel<128>, dim3(grid), dim3(256), 0, s, p);
   OT_LAUNCH_CHECK("ot_attn_fwd_fp8");
   return OT_OK;
+}
+
+extern "C" int ot_attn_fwd_fp8(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos,
+                               int head_dim, float* out, float* lse, void* workspace, size_t ws_bytes, void* stream) {
+  // flags 0: qkv is only read
+  return ot_attn_fwd_fp8_ex(const_cast<float*>(qkv), ld, B, H, I, K, qpos, head_dim, out, lse, workspace, ws_bytes,
+                            0, stream);
 }

@@ -234,15 +234,18 @@ def split_images(base, desc_dev, ndesc, total_units, img) -> None:
 
 
 def attn_fwd(qkv: torch.Tensor, ld: int, B: int, H: int, I: int, K: int, hd: int, out: torch.Tensor,
-             lse: torch.Tensor, qpos: Optional[torch.Tensor] = None, fp8: bool = False) -> None:
-    """ot_attn_fwd, or with ``fp8`` (head_dim 64/128) ot_attn_fwd_fp8: QK^T and PV on block-scaled fp8 MFMA."""
+             lse: torch.Tensor, qpos: Optional[torch.Tensor] = None, fp8: bool = False,
+             dequant: bool = False) -> None:
+    """ot_attn_fwd, or with ``fp8`` (head_dim 64/128) ot_attn_fwd_fp8_ex: QK^T and PV on block-scaled fp8
+    MFMA; ``dequant`` (training) also overwrites qkv's operands with their dequantised fp8 values
+    (OT_FP8_DEQUANT) for the backward."""
     ws = None
     if fp8:
         ws = workspace(size('ot_attn_fwd_fp8_workspace_size', B, H, I, hd), qkv.device)
     ev = _probe.begin() if _probe is not None else None
     if fp8:
-        call('ot_attn_fwd_fp8', ptr(qkv), ld, B, H, I, K, ptr(qpos), hd, ptr(out), ptr(lse), ptr(ws), ws.numel(),
-             stream())
+        call('ot_attn_fwd_fp8_ex', ptr(qkv), ld, B, H, I, K, ptr(qpos), hd, ptr(out), ptr(lse), ptr(ws),
+             ws.numel(), _lib.OT_FP8_DEQUANT if dequant else 0, stream())
     else:
         call('ot_attn_fwd', ptr(qkv), ld, B, H, I, K, ptr(qpos), hd, ptr(out), ptr(lse), stream())
     if ev is not None:

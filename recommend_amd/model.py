@@ -197,7 +197,10 @@ def _block_forward(m, l, x, I, Kq, seed, training, rstd_in=None, select=False, n
     # a 'tail' keep (reference rule) is the contiguous tail, which the attention kernels address
     # arithmetically (no per-query position loads; C3 attention 20.2 -> 18.3 ms/step); the select map
     # still drives the GEMM row maps and epilogues
-    K.attn_fwd(qkv, 3 * d, B, H, I, Kq, hd, o, lse, qpos=_attn_qpos(cfg, pos), fp8=m.attn_fp8)
+    # fp8 training forward: qkv's operands are replaced by their dequantised fp8 values, so the backward
+    # differentiates the forward that ran (OT_FP8_DEQUANT)
+    K.attn_fwd(qkv, 3 * d, B, H, I, Kq, hd, o, lse, qpos=_attn_qpos(cfg, pos), fp8=m.attn_fp8,
+               dequant=m.attn_fp8 and training)
     # x1 = x[tail] + drop(o @ Wo)      (model.py:117, 193)
     x1 = torch.empty(B * Kq, d, device=dev)
     rstd2 = torch.empty(B * Kq, device=dev)
@@ -496,7 +499,8 @@ class OneTransModel(nn.Module):
         check_pyramid_select(cfg)
         # compute_dtype (build knob): 'fp32' (the reference's arithmetic; GEMM precision is the process-wide
         # ot_set_matmul_mode / ONETRANS_MATMUL), 'bf16', or 'fp8attn' = BASELINE configs[4]'s attention on
-        # block-scaled fp8 MFMA (forward QK^T and PV; the backward recomputes in the GEMM mode's precision).
+        # block-scaled fp8 MFMA (forward QK^T and PV; the backward recomputes in the GEMM mode's precision from
+        # the dequantised fp8 operands the training forward leaves in qkv: the straight-through gradient).
         # ONETRANS_ATTN=fp8 selects the fp8 forward too.
         if getattr(cfg, 'compute_dtype', 'fp32') not in ('fp32', 'bf16', 'fp8attn'):
             raise ValueError(f"compute_dtype {cfg.compute_dtype!r}: expected 'fp32', 'bf16' or 'fp8attn'")

@@ -41,6 +41,7 @@ int main(void) {
   expect_error("ot_attn_fwd unsupported head_dim", ot_attn_fwd(f, 24, 1, 1, 4, 4, NULL, 8, f, f, NULL));
   expect_error("ot_attn_fwd_fp8 head_dim 32", ot_attn_fwd_fp8(f, 96, 1, 1, 4, 4, NULL, 32, f, f, f, 64, NULL));
   expect_error("ot_attn_fwd_fp8 workspace too small", ot_attn_fwd_fp8(f, 192, 1, 1, 4, 4, NULL, 64, f, f, f, 16, NULL));
+  expect_error("ot_attn_fwd_fp8_ex unknown flag", ot_attn_fwd_fp8_ex(f, 192, 1, 1, 4, 4, NULL, 64, f, f, f, 1 << 20, 2, NULL));
   expect_error("ot_attn_bwd null operand", ot_attn_bwd(f, 96, f, NULL, f, 1, 1, 4, 4, NULL, 32, f, f, NULL));
   expect_error("ot_attn_bwd_ex workspace too small",
                ot_attn_bwd_ex(f, 96, f, f, f, 1, 1, 4, 4, NULL, 32, f, f, 16, NULL));

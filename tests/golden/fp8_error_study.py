@@ -27,12 +27,27 @@ orig = torch.einsum
 def ein(eq, *ops):
     if MODE and eq == 'bqhd,bkhd->bhqk':
         q, k = ops
-        if MODE in ('fp8', 'fp8_pbf16'): q, k = qrows(q, 32), qrows(k, 32)
+        if MODE in ('fp8', 'fp8_pbf16', 'fp8n', 'fp8nvs'): q, k = qrows(q, 32), qrows(k, 32)
         elif MODE == 'smooth': k = k - k.mean(1, keepdim=True); q, k = qrows(q, 32), qrows(k, 32)
         elif MODE in ('qkbf16', 'bf16'): q, k = bf(q), bf(k)
         return orig(eq, q, k)
     if MODE and eq == 'bhqk,bkhd->bqhd':
         w, v = ops
+        if MODE in ('fp8n', 'fp8nvs', 'pfp8n', 'vs'):
+            # P quantised as the kernel does (P * 2^8 in e4m3) and renormalised by the sum of the quantised
+            # weights; 'vs': V smoothed (per (sample, head, dim) mean over the keys subtracted before the
+            # quantisation and added back: exact, the weights sum to 1)
+            if MODE != 'vs':
+                w = (w * 256).to(E4).to(w.dtype)
+                w = w / w.sum(-1, keepdim=True)
+            if MODE == 'pfp8n':
+                return orig(eq, w, v)
+            B, I, H, hd = v.shape
+            vm = v.mean(1, keepdim=True) if MODE in ('fp8nvs', 'vs') else torch.zeros_like(v[:, :1])
+            Ip = (I + 63) // 64 * 64
+            vp = torch.zeros(B, Ip, H, hd, dtype=v.dtype); vp[:, :I] = v - vm
+            vq = qrows(vp.permute(0, 2, 3, 1).contiguous(), 64).permute(0, 3, 1, 2)[:, :I]
+            return orig(eq, w, vq) + vm
         if MODE in ('qk32_pfp8', 'qk32_vfp8', 'qk32_v32k', 'qk32_pv_fp8'):
             if MODE in ('qk32_pfp8', 'qk32_pv_fp8'):
                 w = (w * 256).to(E4).to(w.dtype) / 256

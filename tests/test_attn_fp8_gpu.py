@@ -35,23 +35,28 @@ def _q_rows(x, block):
     return q.reshape(sh)
 
 
-def emulate(qkv, B, H, I, qpos, hd):
-    """float64 attention from fp8-quantised operands (the kernel's quantisation, see module docstring)."""
+def quantised(qkv, B, H, I, qpos, hd):
+    """The operands as the kernel quantises them: (q8 [B, Kq, H, hd], k8, v8 [B, I, H, hd]) float64."""
     d = H * hd
-    Kq = qpos.shape[1]
     bi = torch.arange(B)[:, None]
-    scale = math.log2(math.e) / math.sqrt(hd)
-    q = (qkv[:, :d].reshape(B, I, H, hd)[bi, qpos] * scale).float().double()
+    q = qkv[:, :d].reshape(B, I, H, hd)[bi, qpos]
     k = qkv[:, d:2 * d].reshape(B, I, H, hd)
     v = qkv[:, 2 * d:].reshape(B, I, H, hd)
     Ip = (I + 63) // 64 * 64
-    q8 = _q_rows(q, 32)
-    k8 = _q_rows(k, 32)
     vp = torch.zeros(B, Ip, H, hd, dtype=torch.float64)
     vp[:, :I] = v
     # V: one scale per (dim, 64 keys): quantise the [B, H, hd, Ip] transpose along keys in blocks of 64
     v8 = _q_rows(vp.permute(0, 2, 3, 1).contiguous(), 64).permute(0, 3, 1, 2)[:, :I]
-    s = torch.einsum('bqhd,bkhd->bhqk', q8, k8)                      # log2 units
+    return _q_rows(q, 32), _q_rows(k, 32), v8
+
+
+def emulate(qkv, B, H, I, qpos, hd):
+    """float64 attention from fp8-quantised operands (the kernel's quantisation, see module docstring)."""
+    d = H * hd
+    Kq = qpos.shape[1]
+    scale = math.log2(math.e) / math.sqrt(hd)
+    q8, k8, v8 = quantised(qkv, B, H, I, qpos, hd)
+    s = torch.einsum('bqhd,bkhd->bhqk', q8, k8) * scale               # log2 units
     mask = torch.arange(I)[None, None, None, :] <= qpos[:, None, :, None]
     s = torch.where(mask, s, torch.tensor(-math.inf, dtype=s.dtype))
     m = s.amax(-1, keepdim=True)
@@ -119,6 +124,79 @@ def test_attn_fwd_fp8_bounds(dev, B, H, I, Kq, hd, sel, qscale):
     assert e_kernel <= 1.5 * e_quant + 1e-3, (e_kernel, e_quant)
     assert e_kernel < 0.12
     assert dl <= 1.5 * dl_q + 0.01 and dl < 0.25, (dl, dl_q)
+
+
+@pytest.mark.parametrize('B,H,I,Kq,sel', [(2, 8, 1036, 1036, False), (3, 2, 300, 37, False), (2, 2, 257, 40, True)])
+def test_attn_fp8_training_backward(dev, B, H, I, Kq, sel):
+    """Training with fp8 attention (OT_FP8_DEQUANT): the forward leaves the dequantised operands in qkv —
+    bit-equal to the kernel's documented quantisation (torch.float8_e4m3fn emulation) — and the bf16
+    backward run on them is the straight-through gradient of the forward that ran: with p = exp(s - lse)
+    (s from the quantised operands, lse from the fp8 forward), dS = p (dO.v8 - dO.O_fp8), dQ / dK from dS,
+    dV = sum_q p8 dO with p8 the forward's e4m3 weights.  Bound: the bf16 backward's own rounding (3e-2 of
+    max|g|, as tests/test_kernels_gpu.py::test_attention_backward_modes), against that float64 reference.
+    The gradient against the exact (unquantised) attention is reported: the fp8 mode's gradient bias."""
+    hd = 64
+    g = torch.Generator().manual_seed(I * 7 + Kq)
+    d = H * hd
+    qkv = torch.randn(B * I, 3 * d, generator=g, dtype=torch.float64).float().double()
+    qkv[:, 2 * d:] *= torch.exp(0.5 * torch.randn(B * I, 1, generator=g, dtype=torch.float64)).float().double()
+    if sel:
+        rng = np.random.default_rng(9)
+        qpos = np.stack([np.append(np.sort(rng.choice(I - 1, Kq - 1, replace=False)), I - 1) for _ in range(B)])
+    else:
+        qpos = np.tile(np.arange(I - Kq, I), (B, 1))
+    qpos_t = torch.from_numpy(qpos)
+    qp_d = torch.from_numpy(qpos.astype(np.int32).reshape(-1)).to(dev) if sel else None
+    qkv_d = qkv.float().to(dev)
+    out = torch.empty(B * Kq, d, device=dev)
+    lse = torch.empty(B * H * Kq, device=dev)
+    old = K.set_matmul_mode('bf16')
+    try:
+        K.attn_fwd(qkv_d, 3 * d, B, H, I, Kq, hd, out, lse, qpos=qp_d, fp8=True, dequant=True)
+        dout = torch.randn(B * Kq, d, generator=g, dtype=torch.float64).float()
+        dqkv = torch.full((B * I, 3 * d), float('nan'), device=dev)
+        dqkv[:, :d].zero_()
+        K.attn_bwd(qkv_d, 3 * d, out, dout.to(dev), lse, B, H, I, Kq, hd, dqkv, qpos=qp_d)
+    finally:
+        K.set_matmul_mode(old)
+    got_qkv = qkv_d.double().cpu().reshape(B, I, 3, H, hd)
+    q8, k8, v8 = quantised(qkv, B, H, I, qpos_t, hd)
+    bi = torch.arange(B)[:, None]
+    assert torch.equal(got_qkv[:, :, 1], k8) and torch.equal(got_qkv[:, :, 2], v8)
+    assert torch.equal(got_qkv[:, :, 0][bi, qpos_t], q8)
+    # straight-through reference (float64)
+    sc = 1.0 / math.sqrt(hd)
+    s = torch.einsum('bqhd,bkhd->bhqk', q8, k8) * sc
+    mask = torch.arange(I)[None, None, None, :] <= qpos_t[:, None, :, None]
+    s = torch.where(mask, s, torch.tensor(-math.inf, dtype=s.dtype))
+    m = s.amax(-1, keepdim=True)
+    pt = torch.exp(s - m)
+    p = pt / pt.sum(-1, keepdim=True)
+    p8 = (pt * 256).float().to(E4M3).double() / (256 * pt.sum(-1, keepdim=True))   # the forward's PV weights
+    o_fwd = torch.einsum('bhqk,bkhd->bqhd', p8, v8)
+    do = dout.double().reshape(B, Kq, H, hd)
+    dp = torch.einsum('bqhd,bkhd->bhqk', do, v8)
+    delta = torch.einsum('bqhd,bqhd->bhq', do, o_fwd)[..., None]
+    ds = p * (dp - delta) * sc
+    ref = torch.zeros(B, I, 3, H, hd, dtype=torch.float64)
+    ref[:, :, 0][bi, qpos_t] = torch.einsum('bhqk,bkhd->bqhd', ds, k8)
+    ref[:, :, 1] = torch.einsum('bhqk,bqhd->bkhd', ds, q8)
+    ref[:, :, 2] = torch.einsum('bhqk,bqhd->bkhd', p8, do)
+    got = dqkv.double().cpu().reshape(B, I, 3, H, hd)
+    gmax = ref.abs().max().item()
+    err = (got - ref).abs().max().item() / gmax
+    # the same gradient of the exact attention (unquantised operands): the fp8 mode's bias
+    qkv_r = qkv.clone().requires_grad_(True)
+    q = qkv_r[:, :d].reshape(B, I, H, hd)[bi, qpos_t]
+    k = qkv_r[:, d:2 * d].reshape(B, I, H, hd)
+    v = qkv_r[:, 2 * d:].reshape(B, I, H, hd)
+    se = torch.where(mask, torch.einsum('bqhd,bkhd->bhqk', q, k) * sc, torch.tensor(-1e9, dtype=torch.float64))
+    torch.einsum('bhqk,bkhd->bqhd', torch.softmax(se, -1), v).reshape(B * Kq, d).backward(dout.double())
+    bias = (got.reshape(B * I, 3 * d) - qkv_r.grad).abs().max().item() / qkv_r.grad.abs().max().item()
+    print(f'fp8 training backward B{B} H{H} I{I} K{Kq}: max err / max|g| vs the straight-through reference '
+          f'{err:.4f}; vs the exact attention gradient {bias:.4f}')
+    assert torch.isfinite(got).all()
+    assert err < 3e-2, err
 
 
 def test_attn_fwd_fp8_rejects_bad_head_dim(dev):

@@ -33,6 +33,10 @@ namespace ot {
 #ifndef OT_GEMM_RMS_EARLY
 #define OT_GEMM_RMS_EARLY 1
 #endif
+#ifndef OT_WGRAD_BF16_RS          // 32-row groups per stage of the bf16-mode weight-gradient kernel
+#define OT_WGRAD_BF16_RS 2
+#endif
+constexpr int WGRAD_BF16_RS = OT_WGRAD_BF16_RS;
 #ifndef OT_WGRAD_DBUF
 #define OT_WGRAD_DBUF 0
 #endif
@@ -1009,8 +1013,18 @@ __device__ __forceinline__ v4i16 ds_tr16(const char* base, int off) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + off));
 }
 
+// RS: 32-row groups per stage.  The bf16 mode (TERMS = 1: one plane, 8 MFMAs per 32 rows per wave) takes
+// 64-row stages (RS = 2): twice the MFMAs between the stage's two barriers, the two row groups' planes in
+// the space the split mode's three planes use (the swizzle depends on r & 15, so row r + 32 keeps it).
+template <int TERMS>
+constexpr int wgrad_rs() { return WGRAD_BF16_RS > 0 && TERMS == 1 ? WGRAD_BF16_RS : 1; }
+
 template <int AXT, int TERMS>
 __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(WgradArgs p) {
+  constexpr int RS = wgrad_rs<TERMS>();
+  static_assert(RS * WSPLANE <= WSOP && (TERMS == 1 || RS == 1), "wgrad stage LDS");
+  constexpr int BR = WBR * RS;                   // rows per stage
+  constexpr int NPL = TERMS == 1 ? 1 : 3;
   extern __shared__ __attribute__((aligned(16))) char smem_c[];
   const int ax = AXT >= 0 ? AXT : p.a_xform;
   const int per_chunk = p.ntk * p.ntn;
@@ -1023,7 +1037,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(WgradArgs p) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int h = lane >> 5, li = lane & 31;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
-  const int sr = t >> 3, sc = t & 7;       // staging: row sr of the stage, float4 columns sc + 8i
+  const int sr = t >> 3, sc = t & 7;       // staging: rows sr + 32 j of the stage, float4 columns sc + 8i
   const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
   char* As = smem_c;
   char* Ds = smem_c + WSOP;
@@ -1037,59 +1051,74 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(WgradArgs p) {
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
   const bool do_bias = p.bslab && tk == 0;
   f32x4 bsum[4] = {zero4, zero4, zero4, zero4};
-
-  auto rows_of = [&](int rs, int& ar, int& dr) {
-    const int lr = rs + sr;
-    const int64_t mi = (int64_t)row_begin + (lr < row_count ? lr : 0);
-    ar = p.a_rows ? p.a_rows[mi] : (int)mi;
-    dr = p.d_rows ? p.d_rows[mi] : (int)mi;
-  };
-  f32x4 va[4], vd[4], gv[4];
-  float rsd = 1.f;
-  bool inr = false;
-  auto load_stage = [&](int st, int ar, int dr) {
-    inr = st * WBR + sr < row_count && ar >= 0 && dr >= 0;
-    const float* pa = p.A + (int64_t)(inr ? ar : 0) * p.lda;
-    const float* pd = p.D + (int64_t)(inr ? dr : 0) * p.ldd;
-    if (ax == OT_AX_RMSNORM) rsd = p.a_rstd[inr ? ar : 0];
+  f32x4 gv[4];                                   // RMSNorm gamma of this thread's k columns (stage-invariant)
+  if (ax == OT_AX_RMSNORM) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int k = k0 + 4 * (sc + 8 * i), n = n0 + 4 * (sc + 8 * i);
-      const int kc = k < p.K ? k : 0, nc = n < p.N ? n : 0;
-      va[i] = *reinterpret_cast<const f32x4*>(pa + kc);
-      vd[i] = *reinterpret_cast<const f32x4*>(pd + nc);
-      if (ax == OT_AX_RMSNORM) gv[i] = *reinterpret_cast<const f32x4*>(p.a_gamma + kc);
+      const int k = k0 + 4 * (sc + 8 * i);
+      gv[i] = *reinterpret_cast<const f32x4*>(p.a_gamma + (k < p.K ? k : 0));
+    }
+  }
+
+  auto rows_of = [&](int rs, int (&ar)[RS], int (&dr)[RS]) {
+#pragma unroll
+    for (int j = 0; j < RS; ++j) {
+      const int lr = rs + sr + WBR * j;
+      const int64_t mi = (int64_t)row_begin + (lr < row_count ? lr : 0);
+      ar[j] = p.a_rows ? p.a_rows[mi] : (int)mi;
+      dr[j] = p.d_rows ? p.d_rows[mi] : (int)mi;
+    }
+  };
+  f32x4 va[RS][4], vd[RS][4];
+  float rsd[RS];
+  bool inr[RS];
+  auto load_stage = [&](int st, const int (&ar)[RS], const int (&dr)[RS]) {
+#pragma unroll
+    for (int j = 0; j < RS; ++j) {
+      inr[j] = st * BR + sr + WBR * j < row_count && ar[j] >= 0 && dr[j] >= 0;
+      const float* pa = p.A + (int64_t)(inr[j] ? ar[j] : 0) * p.lda;
+      const float* pd = p.D + (int64_t)(inr[j] ? dr[j] : 0) * p.ldd;
+      rsd[j] = ax == OT_AX_RMSNORM ? p.a_rstd[inr[j] ? ar[j] : 0] : 1.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = k0 + 4 * (sc + 8 * i), n = n0 + 4 * (sc + 8 * i);
+        const int kc = k < p.K ? k : 0, nc = n < p.N ? n : 0;
+        va[j][i] = *reinterpret_cast<const f32x4*>(pa + kc);
+        vd[j][i] = *reinterpret_cast<const f32x4*>(pd + nc);
+      }
     }
   };
   auto store_stage = [&]() {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int cc = sc + 8 * i;                      // float4 column index 0..31
-      f32x4 a = va[i], dv = vd[i];
-      if (ax == OT_AX_RMSNORM) {
-        a = a * gv[i] * rsd;
-      } else if (ax == OT_AX_GELU) {
-        a.x = gelu_erf(a.x); a.y = gelu_erf(a.y); a.z = gelu_erf(a.z); a.w = gelu_erf(a.w);
+    for (int j = 0; j < RS; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int cc = sc + 8 * i;                      // float4 column index 0..31
+        f32x4 a = va[j][i], dv = vd[j][i];
+        if (ax == OT_AX_RMSNORM) {
+          a = a * gv[i] * rsd[j];
+        } else if (ax == OT_AX_GELU) {
+          a.x = gelu_erf(a.x); a.y = gelu_erf(a.y); a.z = gelu_erf(a.z); a.w = gelu_erf(a.w);
+        }
+        if (!(inr[j] && k0 + 4 * cc < p.K)) a = zero4;
+        if (!(inr[j] && n0 + 4 * cc < p.N)) dv = zero4;
+        if (do_bias) bsum[i] += dv;
+        const int off = wsw_off(sr + WBR * j, cc >> 1) + 8 * (cc & 1);
+        if constexpr (TERMS == 1) {
+          *reinterpret_cast<u32x2*>(As + off) = bf16_rne4(a);
+          *reinterpret_cast<u32x2*>(Ds + off) = bf16_rne4(dv);
+          continue;
+        }
+        u32x2 q0, q1, q2;
+        split3(a, q0, q1, q2);
+        *reinterpret_cast<u32x2*>(As + off) = q0;
+        *reinterpret_cast<u32x2*>(As + WSPLANE + off) = q1;
+        *reinterpret_cast<u32x2*>(As + 2 * WSPLANE + off) = q2;
+        split3(dv, q0, q1, q2);
+        *reinterpret_cast<u32x2*>(Ds + off) = q0;
+        *reinterpret_cast<u32x2*>(Ds + WSPLANE + off) = q1;
+        *reinterpret_cast<u32x2*>(Ds + 2 * WSPLANE + off) = q2;
       }
-      if (!(inr && k0 + 4 * cc < p.K)) a = zero4;
-      if (!(inr && n0 + 4 * cc < p.N)) dv = zero4;
-      if (do_bias) bsum[i] += dv;
-      const int off = wsw_off(sr, cc >> 1) + 8 * (cc & 1);
-      if constexpr (TERMS == 1) {
-        *reinterpret_cast<u32x2*>(As + off) = bf16_rne4(a);
-        *reinterpret_cast<u32x2*>(Ds + off) = bf16_rne4(dv);
-        continue;
-      }
-      u32x2 q0, q1, q2;
-      split3(a, q0, q1, q2);
-      *reinterpret_cast<u32x2*>(As + off) = q0;
-      *reinterpret_cast<u32x2*>(As + WSPLANE + off) = q1;
-      *reinterpret_cast<u32x2*>(As + 2 * WSPLANE + off) = q2;
-      split3(dv, q0, q1, q2);
-      *reinterpret_cast<u32x2*>(Ds + off) = q0;
-      *reinterpret_cast<u32x2*>(Ds + WSPLANE + off) = q1;
-      *reinterpret_cast<u32x2*>(Ds + 2 * WSPLANE + off) = q2;
-    }
   };
   // transposed-read addresses (stage-invariant): lane 4q+pp of its 16-lane group reads row
   // r0 + q, chunk c0 + (pp >> 1), half pp & 1; r0 = 16 t2 + 8 h + 4 rd, c0 = (col0 + 16 (g & 1)) / 8
@@ -1104,27 +1133,27 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(WgradArgs p) {
       doff[m][rd] = wsw_off(r, (wn + 32 * m + 16 * g1) / 8 + (pp >> 1)) + 8 * (pp & 1);
     }
 
-  const int nst = (row_count + WBR - 1) / WBR;
-  int ar, dr, ar2 = -1, dr2 = -1;
+  const int nst = (row_count + BR - 1) / BR;
+  int ar[RS], dr[RS], ar2[RS], dr2[RS];
   rows_of(0, ar, dr);
-  if (nst > 1) rows_of(WBR, ar2, dr2);
+  if (nst > 1) rows_of(BR, ar2, dr2);
   load_stage(0, ar, dr);
   store_stage();
   __syncthreads();
   for (int st = 0; st < nst; ++st) {
     const bool more = st + 1 < nst;
-    int ar3 = -1, dr3 = -1;
+    int ar3[RS], dr3[RS];
     if (more) {
       load_stage(st + 1, ar2, dr2);
-      if (st + 2 < nst) rows_of((st + 2) * WBR, ar3, dr3);
+      if (st + 2 < nst) rows_of((st + 2) * BR, ar3, dr3);
     }
 #pragma unroll
-    for (int t2 = 0; t2 < 2; ++t2) {                    // two 16-row MFMA k-steps per stage
+    for (int t2 = 0; t2 < 2 * RS; ++t2) {               // 16-row MFMA k-steps of the stage
       u32x4 fa[2][3], fb[2][3];
 #pragma unroll
       for (int m = 0; m < 2; ++m)
 #pragma unroll
-        for (int pl = 0; pl < (TERMS == 1 ? 1 : 3); ++pl) {
+        for (int pl = 0; pl < NPL; ++pl) {
           const int po = pl * WSPLANE + t2 * 16 * 256;   // row r -> r + 16 keeps the swizzle (r & 15)
           const v4i16 a0 = ds_tr16(As + po, aoff[m][0]), a1 = ds_tr16(As + po, aoff[m][1]);
           const v4i16 d0 = ds_tr16(Ds + po, doff[m][0]), d1 = ds_tr16(Ds + po, doff[m][1]);
@@ -1159,7 +1188,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(WgradArgs p) {
     __syncthreads();
     if (more) store_stage();
     __syncthreads();
-    ar2 = ar3; dr2 = dr3;
+#pragma unroll
+    for (int j = 0; j < RS; ++j) { ar2[j] = ar3[j]; dr2[j] = dr3[j]; }
   }
   float* slab = p.slab + (int64_t)c * p.K * p.N;
 #pragma unroll

@@ -176,6 +176,7 @@ def main():
     trainer = OneTransTrainer(cfg, model=model)
     batches = device_batches(cfg, B, args.nbatches, rank, dev)
     torch.cuda.synchronize()
+    model.inputs_ready = True           # resident, complete batches: a row-sharded lookup routes them at once
 
     def step(i):
         ns, seq, y = batches[i % len(batches)]

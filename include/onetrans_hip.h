@@ -368,6 +368,12 @@ int ot_shard_route_unique(const int64_t* ids, int64_t n, int64_t num_rows, int w
  * the per-token gradient rows of a de-duplicated route summed per unique id before they travel */
 int ot_segment_rows_sum(const float* src, const int32_t* order, const int32_t* run_start, int64_t U, int E,
                         float* out, void* stream);
+/* The same sums, balanced for Zipf-hot ids (runs cut into pieces of <= 64 positions, piece partials added
+ * in piece order: deterministic); n = the routed id count (run_start[U]).  ws:
+ * ot_segment_rows_sum_workspace_size(U, n, E) bytes. */
+size_t ot_segment_rows_sum_workspace_size(int64_t U, int64_t n, int E);
+int ot_segment_rows_sum_ex(const float* src, const int32_t* order, const int32_t* run_start, int64_t U, int64_t n,
+                           int E, float* out, void* workspace, size_t ws_bytes, void* stream);
 /* out[i] = table[idx[i]] (zeros for idx < 0) */
 int ot_gather_rows(const float* table, int E, const int64_t* idx, int64_t n, float* out, void* stream);
 /* inverse = 0: dst[j] = src[perm[j]]; inverse = 1: dst[perm[j]] = src[j] */

@@ -106,6 +106,8 @@ SIGNATURES = {
     'ot_shard_route_unique_workspace_size': (c_size_t, [I64]),
     'ot_shard_route_unique': (c_int, [P, I64, I64, c_int, P, P, P, P, P, P, c_size_t, P]),
     'ot_segment_rows_sum': (c_int, [P, P, P, I64, c_int, P, P]),
+    'ot_segment_rows_sum_workspace_size': (c_size_t, [I64, I64, c_int]),
+    'ot_segment_rows_sum_ex': (c_int, [P, P, P, I64, I64, c_int, P, P, c_size_t, P]),
     'ot_gather_rows': (c_int, [P, c_int, P, I64, P, P]),
     'ot_permute_rows': (c_int, [P, P, I64, c_int, c_int, P, P]),
     'ot_hash_uniform_rows': (c_int, [P, I64, c_int, c_int, c_int, c_uint32, c_float, c_float, P]),

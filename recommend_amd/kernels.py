@@ -422,8 +422,14 @@ def shard_route_unique(ids, n, num_rows, world, uniq_local, inv, order, run_star
          ptr(counts), ptr(ws), ws.numel(), stream())
 
 
-def segment_rows_sum(src, order, run_start, U, E, out) -> None:
-    call('ot_segment_rows_sum', ptr(src), ptr(order), ptr(run_start), U, E, ptr(out), stream())
+def segment_rows_sum(src, order, run_start, U, E, out, n: Optional[int] = None) -> None:
+    """Per distinct id the sum of its repeats' rows (ot_segment_rows_sum_ex: hot runs split into pieces);
+    ``n`` = the routed id count (run_start[U]; default: src's rows)."""
+    n = int(src.shape[0]) if n is None else int(n)
+    n = max(n, int(U))
+    ws = workspace(size('ot_segment_rows_sum_workspace_size', U, n, E), src.device)
+    call('ot_segment_rows_sum_ex', ptr(src), ptr(order), ptr(run_start), U, n, E, ptr(out), ptr(ws), ws.numel(),
+         stream())
 
 
 def gather_rows(table, E, idx, n, out) -> None:

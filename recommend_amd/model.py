@@ -558,6 +558,9 @@ class OneTransModel(nn.Module):
         self._step = 0
         self.dropout_seed = 0x5EED0000 ^ seed
         self.sample_offset: Optional[int] = None      # global index of the local batch's first sample
+        # producer of device-resident input ids (row-sharded lookups route them on a side stream): None =
+        # the current stream, a HIP event, or True = already complete (resident batches, bench.py)
+        self.inputs_ready = None
         # row-sharded tables (data-parallel runs): 'emb.seq_item' lives partitioned over the ranks
         self.sharded: Dict[str, 'ShardedTable'] = {}
         shard_seq = self._shard_seq_table()
@@ -567,8 +570,10 @@ class OneTransModel(nn.Module):
             import torch.distributed as dist
             full = params.get('emb.seq_item') if init is not None else None
             params = {k: v for k, v in params.items() if k != 'emb.seq_item'}
-            st = ShardedTable('emb.seq_item', cfg.seq_item_vocab, cfg.seq_feature_dim, dist.get_world_size(),
-                              dist.get_rank(), self.device, seed=seed + 2, full_init=full)
+            dist_on = dist.is_available() and dist.is_initialized()
+            st = ShardedTable('emb.seq_item', cfg.seq_item_vocab, cfg.seq_feature_dim,
+                              dist.get_world_size() if dist_on else 1, dist.get_rank() if dist_on else 0,
+                              self.device, seed=seed + 2, full_init=full)
             self.sharded['emb.seq_item'] = st
             self.tables['emb.seq_item'] = st.table
         self.load_param_dict(params)
@@ -670,17 +675,18 @@ class OneTransModel(nn.Module):
 
     def _shard_seq_table(self) -> bool:
         """Row-shard the sequence-item table?  ``config.table_sharding`` (env ONETRANS_TABLE_SHARDING
-        overrides): 'row' under torch.distributed with world > 1; 'auto' (default) when the table
-        exceeds 1 GiB (C4's 100M rows; C2's 1M-row table is replicated and exchanged densely)."""
+        overrides): 'row' always (world 1 outside torch.distributed: one shard, the route as a copy);
+        'auto' (default) under torch.distributed with world > 1 when the table exceeds 1 GiB (C4's 100M
+        rows; C2's 1M-row table is replicated and exchanged densely)."""
         import torch.distributed as dist
         cfg = self.config
         mode = os.environ.get('ONETRANS_TABLE_SHARDING', getattr(cfg, 'table_sharding', 'auto'))
         if not cfg.seq_item_vocab or mode == 'none':
             return False
+        if mode == 'row':
+            return True          # (a single process holds the one shard: the route runs, as a copy)
         if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
             return False
-        if mode == 'row':
-            return True
         return cfg.seq_item_vocab * cfg.seq_feature_dim * 4 > 2 ** 30
 
     def _init_tables_device(self, seed: int) -> None:
@@ -758,11 +764,15 @@ class OneTransModel(nn.Module):
         if plan['seq_map'] is not None:
             if id_seq and 'emb.seq_item' in self.sharded:
                 # row-sharded table: the rows arrive through the all-to-all lookup in token order, and
-                # the projection reads them through the static (identity) row map
-                ids = [seq[n].to(dev, torch.int64).contiguous() for (_, n, _) in present]
-                plan['seq_ids'] = torch.cat([t.reshape(-1) for t in ids])
-                plan['seq_A'] = self.sharded['emb.seq_item'].lookup(plan['seq_ids'])
-                plan['seq_route'] = self.sharded['emb.seq_item'].last_route
+                # the projection reads them through the static (identity) row map; the ids are staged
+                # and routed on the table's route stream (host ids copied there, device ids after
+                # ``inputs_ready``), so its one host wait does not drain the main stream
+                st = self.sharded['emb.seq_item']
+                ids = [seq[n] if isinstance(seq[n], torch.Tensor) else torch.from_numpy(np.asarray(seq[n]))
+                       for (_, n, _) in present]
+                plan['seq_A'] = st.lookup(ids, ready=self.inputs_ready)
+                plan['seq_ids'] = st.last_ids
+                plan['seq_route'] = st.last_route
             elif id_seq:
                 ids = [seq[n].to(dev, torch.int64).contiguous() for (_, n, _) in present]
                 for (i, n, L), t, off in zip(present, ids, plan['seq_seg_off']):

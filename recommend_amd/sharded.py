@@ -16,7 +16,13 @@ transformer stays data-parallel; only the table is partitioned:
   sparse Keras Adagrad; the per-table ``clip_by_norm`` uses the global norm (an all-reduce of each
   owner's squared norm between ``ot_sparse_prepare`` and ``ot_sparse_finish``).
 
-All bytes move on device; the only host traffic is the ``world`` split sizes the all-to-alls need.
+All bytes move on device; the only host traffic is the ``world`` split sizes the all-to-alls need.  That
+one host wait is taken off the main stream: the ids are staged, routed and their per-owner counts
+exchanged on the table's own route stream (host ids are copied there; device ids wait only for the event
+the caller names as their producer, ``ready``), so the host waits for those few kernels — not for the
+previous step's backward and optimizer still queued on the main stream — and the GPU keeps running them
+while it does.  The gather that follows stays on the main stream (it reads the table the previous step's
+sparse update wrote).
 """
 
 from __future__ import annotations
@@ -30,6 +36,14 @@ import torch
 import torch.distributed as dist
 
 from . import kernels as K
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
 
 
 class ShardedTable:
@@ -54,6 +68,11 @@ class ShardedTable:
             K.hash_uniform_rows(self.table, self.local_rows, self.E, self.rank, self.world, seed, lo, hi)
         self.last_route = None
         self.sent_rows = 0         # ids (rows) the last lookup sent to their owners
+        is_cuda = torch.device(device).type == 'cuda'
+        # ONETRANS_ROUTE_STREAM=0: route on the current stream (the host wait then drains it; A/B switch)
+        side = is_cuda and os.environ.get('ONETRANS_ROUTE_STREAM', '1') != '0'
+        self.route_stream = torch.cuda.Stream(device=device) if side else None
+        self._counts_host = torch.empty(2 * self.world, dtype=torch.int32, pin_memory=is_cuda)
         self.events = None        # diagnostics: a list collects HIP-event pairs around lookup / update
 
     def _mark(self):
@@ -74,31 +93,67 @@ class ShardedTable:
         else:
             dist.all_to_all_single(out, inp, out_splits, in_splits)
 
-    def _splits(self, counts):
-        recv_counts = torch.empty_like(counts)
-        self._a2a(recv_counts, counts, None, None)
-        both = torch.cat([counts, recv_counts]).cpu().tolist()      # the one host sync: split sizes
-        return both[:self.world], both[self.world:]
+    def _route(self, ids, ready):
+        """Stage ``ids`` (a tensor or a list concatenated in order; host or device) and route them by owner
+        on the route stream; returns (ids on the device, route buffers, send splits, recv splits) after the
+        host has waited for that stream alone (the split sizes)."""
+        dev, rs = self.device, self.route_stream
+        parts = list(ids) if isinstance(ids, (list, tuple)) else [ids]
+        host = all(t.device.type == 'cpu' for t in parts)
+        if rs is not None and not host:
+            if ready is None:
+                rs.wait_stream(torch.cuda.current_stream(dev))     # producer unknown: after the main stream
+            elif ready is not True:
+                rs.wait_event(ready)                                # the named producer event only
+        ctx = torch.cuda.stream(rs) if rs is not None else _nullctx()
+        with ctx:
+            if host:
+                h = torch.cat([t.reshape(-1).to(torch.int64) for t in parts])
+                ids_d = (h.pin_memory() if rs is not None else h).to(dev, non_blocking=True)
+            else:
+                ids_d = torch.cat([t.reshape(-1).to(dev, torch.int64) for t in parts])
+            n = ids_d.numel()
+            counts = torch.empty(self.world, dtype=torch.int32, device=dev)
+            if self.dedup:
+                send_local = torch.empty(max(1, n), dtype=torch.int64, device=dev)
+                inv = torch.empty(max(1, n), dtype=torch.int64, device=dev)
+                order = torch.empty(max(1, n), dtype=torch.int32, device=dev)
+                run_start = torch.empty(n + 1, dtype=torch.int32, device=dev)
+                K.shard_route_unique(ids_d, n, self.num_rows, self.world, send_local, inv, order, run_start, counts)
+                bufs = (send_local, inv, order, run_start)
+            else:
+                perm = torch.empty(max(1, n), dtype=torch.int32, device=dev)
+                send_local = torch.empty(max(1, n), dtype=torch.int64, device=dev)
+                K.shard_route(ids_d, n, self.num_rows, self.world, perm, send_local, counts)
+                bufs = (send_local, perm)
+            recv_counts = torch.empty_like(counts)
+            self._a2a(recv_counts, counts, None, None)
+            both = torch.cat([counts, recv_counts])
+            self._counts_host.copy_(both, non_blocking=rs is not None)
+            if rs is not None:
+                done = torch.cuda.Event()
+                done.record(rs)
+        if rs is not None:
+            done.synchronize()                       # the one host wait: this stream's few kernels only
+            main = torch.cuda.current_stream(dev)
+            main.wait_stream(rs)
+            for t in (ids_d, *bufs):                 # allocated on the route stream, used on the main one
+                t.record_stream(main)
+        both = self._counts_host.tolist()
+        return ids_d, bufs, both[:self.world], both[self.world:]
 
-    def lookup(self, ids: torch.Tensor) -> torch.Tensor:
-        """Rows of ``ids`` (int64 [n]) in order -> [n, E] fp32 (zeros for ids outside the table)."""
+    def lookup(self, ids, ready=None) -> torch.Tensor:
+        """Rows of ``ids`` (int64 [n], or a list of id tensors taken in order; host or device) -> [n, E] fp32
+        (zeros for ids outside the table); the staged device ids are kept in ``last_ids``.  ``ready``:
+        for device ids, the HIP event after which they are valid (True: already complete, e.g. resident
+        batches; None: wait for the current stream)."""
         ev0 = self._mark()
-        ids = ids.reshape(-1).contiguous()
-        n, E, dev = ids.numel(), self.E, self.device
-        counts = torch.empty(self.world, dtype=torch.int32, device=dev)
-        if self.dedup:
-            send_local = torch.empty(max(1, n), dtype=torch.int64, device=dev)
-            inv = torch.empty(max(1, n), dtype=torch.int64, device=dev)
-            order = torch.empty(max(1, n), dtype=torch.int32, device=dev)
-            run_start = torch.empty(n + 1, dtype=torch.int32, device=dev)
-            K.shard_route_unique(ids, n, self.num_rows, self.world, send_local, inv, order, run_start, counts)
-        else:
-            perm = torch.empty(max(1, n), dtype=torch.int32, device=dev)
-            send_local = torch.empty(max(1, n), dtype=torch.int64, device=dev)
-            K.shard_route(ids, n, self.num_rows, self.world, perm, send_local, counts)
-        send_splits, recv_splits = self._splits(counts)
+        E, dev = self.E, self.device
+        ids_d, bufs, send_splits, recv_splits = self._route(ids, ready)
+        n = ids_d.numel()
         S = sum(send_splits)                  # ids this rank sends: distinct ids (dedup) or n
         R = sum(recv_splits)
+        send_local = bufs[0]
         recv_local = torch.empty(max(1, R), dtype=torch.int64, device=dev)
         self._a2a(recv_local[:R], send_local[:S], recv_splits, send_splits)
         rows = torch.empty(max(1, R), E, device=dev)
@@ -107,11 +162,14 @@ class ShardedTable:
         self._a2a(back[:S], rows[:R], send_splits, recv_splits)
         out = torch.empty(n, E, device=dev)
         if self.dedup:
+            _, inv, order, run_start = bufs
             K.gather_rows(back, E, inv, n, out)          # token i <- its distinct id's row
             self.last_route = (n, ('dedup', order, run_start, S), send_splits, recv_splits, recv_local, R)
         else:
+            perm = bufs[1]
             K.permute_rows(back, perm, n, E, True, out)
             self.last_route = (n, perm, send_splits, recv_splits, recv_local, R)
+        self.last_ids = ids_d
         self.sent_rows = S
         if ev0 is not None:
             self.events.append((ev0, self._mark()))

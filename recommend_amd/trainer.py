@@ -36,6 +36,14 @@ def _to_dev(d: Dict, dev) -> Dict[str, torch.Tensor]:
     return out
 
 
+def _seq_inputs(model, seq: Dict, dev) -> Dict[str, torch.Tensor]:
+    """Sequence features for forward_probs: with a row-sharded item table the id sequences stay host
+    tensors — the lookup copies them on the table's route stream, off the main stream (sharded.py)."""
+    if not getattr(model, 'sharded', None):
+        return _to_dev(seq, dev)
+    return {k: v if isinstance(v, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(v)) for k, v in seq.items()}
+
+
 def stack_labels(labels: Dict, tasks, dev) -> torch.Tensor:
     """{task: [B,1]} -> [T, B] float32 on device."""
     return torch.stack([torch.as_tensor(labels[t]).reshape(-1).to(dev, torch.float32) for t in tasks])
@@ -236,7 +244,7 @@ class OneTransTrainer:
         dev = self.device
         y = labels if isinstance(labels, torch.Tensor) else stack_labels(labels, self.config.tasks, dev)
         self.model.train()
-        probs = self.model.forward_probs(_to_dev(non_seq, dev), _to_dev(seq, dev), training=True)
+        probs = self.model.forward_probs(_to_dev(non_seq, dev), _seq_inputs(self.model, seq, dev), training=True)
         loss = keras_bce_loss(y, probs, self.config.tasks)
         self.optimizer.begin_backward()
         loss.backward()
@@ -249,7 +257,7 @@ class OneTransTrainer:
         non_seq, seq, labels = batch_data
         dev = self.device
         y = labels if isinstance(labels, torch.Tensor) else stack_labels(labels, self.config.tasks, dev)
-        probs = self.model.forward_probs(_to_dev(non_seq, dev), _to_dev(seq, dev), training=False)
+        probs = self.model.forward_probs(_to_dev(non_seq, dev), _seq_inputs(self.model, seq, dev), training=False)
         loss = keras_bce_loss(y, probs, self.config.tasks)
         return {'total_loss': loss, 'probs': probs}
 

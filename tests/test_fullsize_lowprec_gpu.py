@@ -1,8 +1,9 @@
-"""C5 (BASELINE configs[4]: 12L d512 H8 f2048, L0 = 1036, B = 512) at full size in its stated reduced
-precision — bf16 GEMMs, and bf16 GEMMs + block-scaled fp8 attention (``compute_dtype='fp8attn'``) — and
-in the default f32-accurate mode, against the float32 oracle forward of the whole batch
-(tests/golden/fullsize_C5_fwd.npz, tests/golden/make_fullsize_golden.py: perturbed Keras init seed 0,
-hash-valued full tables, Criteo-shape batch BATCH_SEED, inference mode).
+"""C5 (BASELINE configs[4]: 12L d512 H8 f2048, L0 = 1036, 512 samples per GPU x 8 GPUs) at full size in its
+stated reduced precision — bf16 GEMMs, and bf16 GEMMs + block-scaled fp8 attention
+(``compute_dtype='fp8attn'``) — and in the default f32-accurate mode, against the float32 oracle forward of
+C5's GLOBAL batch: 4096 samples (tests/golden/fullsize_C5_fwd.npz, tests/golden/make_fullsize_golden.py:
+perturbed Keras init seed 0, hash-valued full tables, Criteo-shape batch BATCH_SEED, inference mode), run
+here as the 8 per-GPU slices of 512 one after the other (inference: samples are independent).
 
 Bounds (stated per mode; |logit| <= 1.5 at this init):
 * split (f32-accurate):   max |d logit| < 1e-3 (north_star's bound), AUC difference < 1e-4
@@ -45,8 +46,8 @@ def test_c5_fullsize_precision(dev, mode):
     G = np.load(os.path.join(GOLDEN, 'fullsize_C5_fwd.npz'))
     cfg = setup_config('C5')
     cfg.compute_dtype = 'fp8attn' if mode == 'fp8attn' else ('bf16' if mode == 'bf16' else 'fp32')
-    B = cfg._batch
-    assert int(G['B']) == B
+    B = int(G['B'])
+    assert B == 8 * cfg._batch and int(G['B_gpu']) == cfg._batch
     old = K.set_matmul_mode('split' if mode == 'split' else 'bf16')
     try:
         P = init_params(cfg, cfg.ns_input_width(), seed=MODEL_SEED, perturb=True, with_tables=False)
@@ -54,11 +55,16 @@ def test_c5_fullsize_precision(dev, mode):
         for k, t in model.tables.items():
             fill_table_device(t, TABLE_SEED[k])
         ns, seq, lab = make_batch(B, cfg, seed=BATCH_SEED)
-        tdev = lambda d: {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in d.items()}
+        Bg = cfg._batch
+        tdev = lambda d, sl: {k: torch.from_numpy(np.ascontiguousarray(v[sl])).to(dev) for k, v in d.items()}
         model.eval()
+        parts = []
         with torch.no_grad():
-            model((tdev(ns), tdev(seq)), training=False)
-        logits = model._last_logits.double().cpu().numpy()          # [T, B]
+            for s0 in range(0, B, Bg):                               # the 8 GPUs' slices
+                sl = slice(s0, s0 + Bg)
+                model((tdev(ns, sl), tdev(seq, sl)), training=False)
+                parts.append(model._last_logits.double().cpu().numpy())
+        logits = np.concatenate(parts, 1)                            # [T, B]
     finally:
         K.set_matmul_mode(old)
     assert np.isfinite(logits).all()

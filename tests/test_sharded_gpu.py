@@ -173,7 +173,7 @@ def test_row_sharded_table_two_ranks(sharding):
 
 
 @pytest.mark.parametrize('world', [1, 3, 8])
-@pytest.mark.parametrize('n', [0, 1, 5000])
+@pytest.mark.parametrize("n", [0, 1, 5000, 300000])
 def test_shard_route_unique_kernel(world, n):
     """ot_shard_route_unique / ot_segment_rows_sum against numpy: distinct ids in (owner, local row)
     order, every invalid id merged into one entry at owner 0, per-owner counts, the inverse map, and
@@ -210,7 +210,10 @@ def test_shard_route_unique_kernel(world, n):
     K.segment_rows_sum(torch.from_numpy(grads).to(dev) if n else torch.zeros(1, E, device=dev), order, run_start,
                        U, E, out)
     exp = np.zeros((U, E))
+    mag = np.zeros((U, E))
     inv_np = inv[:n].cpu().numpy()
     np.add.at(exp, inv_np, grads.astype(np.float64))
+    np.add.at(mag, inv_np, np.abs(grads).astype(np.float64))
     if U:
-        assert np.abs(out[:U].cpu().numpy() - exp).max() < 1e-4
+        # f32 summation (pieces of 64 positions, then the pieces in order): within 1e-6 of sum |g| per entry
+        assert (np.abs(out[:U].cpu().numpy() - exp) <= 1e-5 + 1e-6 * mag).all()

@@ -212,6 +212,9 @@ int ot_attn_fwd_fp8(const float* qkv, int64_t ld, int B, int H, int I, int K, co
                           * values (e4m3 x block scale: exact in bf16), so ot_attn_bwd in the bf16 GEMM mode
                           * recomputes S from the products the fp8 forward summed (its P matches this lse; the
                           * straight-through gradient of the forward that ran) */
+#define OT_FP8_TWO_TERM 2 /* two-term e4m3 operands: every Q / K / V / P element as hi = e4m3(x) plus lo =
+                           * e4m3(x - hi), each with its own block scale; QK^T and PV as three fp8 MFMA
+                           * products (hi.hi + hi.lo + lo.hi): ~7 significant bits per operand */
 int ot_attn_fwd_fp8_ex(float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos, int head_dim,
                        float* out, float* lse, void* workspace, size_t ws_bytes, int flags, void* stream);
 /* dqkv: like qkv (dq written on the K kept query rows only; dk, dv on all rows);

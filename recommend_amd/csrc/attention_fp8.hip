@@ -77,37 +77,65 @@ __device__ __forceinline__ i32x8 load32(const uint8_t* p, int gap = 16) {
 
 }  // namespace fp8
 
-// Workspace of one call (all u8), Ip = I rounded up to 64 keys:
+// Workspace of one call (all u8), Ip = I rounded up to 64 keys, for each term t (hi; lo with T8 = 2):
 //   k8 [BH][Ip][HD]   ks [BH][Ip][HD/32]   vt8 [BH][HD][Ip]   vs [BH][Ip/64][HD]
 struct Fp8Pack {
-  uint8_t *k8, *ks, *vt8, *vs;
+  uint8_t *k8, *ks, *vt8, *vs;          // hi term
+  uint8_t *k8l, *ksl, *vt8l, *vsl;      // lo term (two-term operands)
 };
 
 __host__ __device__ inline int64_t fp8_ipad(int I) { return ((int64_t)I + 63) / 64 * 64; }
+
+inline size_t fp8_term_bytes(int64_t BH, int I, int HD) {
+  const int64_t Ip = fp8_ipad(I);
+  return (size_t)(BH * Ip * HD * 2 + BH * Ip * (HD / 32) + BH * (Ip / 64) * HD);
+}
 
 inline Fp8Pack fp8_pack_layout(void* ws, int64_t BH, int I, int HD) {
   const int64_t Ip = fp8_ipad(I);
   uint8_t* p = static_cast<uint8_t*>(ws);
   Fp8Pack f;
+  uint8_t* q = p + fp8_term_bytes(BH, I, HD);
   f.k8 = p;  p += BH * Ip * HD;
   f.vt8 = p; p += BH * Ip * HD;
   f.ks = p;  p += BH * Ip * (HD / 32);
   f.vs = p;
+  f.k8l = q;  q += BH * Ip * HD;
+  f.vt8l = q; q += BH * Ip * HD;
+  f.ksl = q;  q += BH * Ip * (HD / 32);
+  f.vsl = q;
   return f;
 }
 
-inline size_t fp8_pack_bytes(int64_t BH, int I, int HD) {
-  const int64_t Ip = fp8_ipad(I);
-  return (size_t)(BH * Ip * HD * 2 + BH * Ip * (HD / 32) + BH * (Ip / 64) * HD);
+// both terms' space (the one-term form uses the first half)
+inline size_t fp8_pack_bytes(int64_t BH, int I, int HD) { return 2 * fp8_term_bytes(BH, I, HD); }
+
+// 16 floats -> 16 e4m3 bytes at scale 2^-e, and their dequantised values into r (r = x - q(x) 2^e when
+// resid: the lo term's input)
+__device__ __forceinline__ i32x4 quant16(const float (&x)[16], int e, float (&r)[16], bool resid) {
+  const float inv = fp8::pow2f(-e), sc = fp8::pow2f(e);
+  i32x4 o;
+  int* ow = reinterpret_cast<int*>(&o);
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    ow[w] = (int)fp8::pack4(x[4 * w] * inv, x[4 * w + 1] * inv, x[4 * w + 2] * inv, x[4 * w + 3] * inv);
+    const f32x4 d = fp8::unpack4(ow[w], sc);
+    r[4 * w] = resid ? x[4 * w] - d.x : d.x;
+    r[4 * w + 1] = resid ? x[4 * w + 1] - d.y : d.y;
+    r[4 * w + 2] = resid ? x[4 * w + 2] - d.z : d.z;
+    r[4 * w + 3] = resid ? x[4 * w + 3] - d.w : d.w;
+  }
+  return o;
 }
 
 // grid (B*H, Ip/64), 256 threads (B*H on x: up to 2^31 - 1 heads).  Keys >= I are zeros (the causal mask removes them).
-template <int HD>
+// T8 = 2: every element also gets a lo term, lo = e4m3(x - hi) with its own block scale (same blocks).
+template <int HD, int T8>
 __global__ __launch_bounds__(256) void attn_fp8_pack_kernel(float* qkv, int64_t ld, int H, int I, Fp8Pack f,
                                                             int dequant) {
   constexpr int VLD = HD + 1;
   __shared__ float vs_f[64 * VLD];
-  __shared__ __attribute__((aligned(16))) uint8_t vt_img[HD * 64];
+  __shared__ __attribute__((aligned(16))) uint8_t vt_img[T8][HD * 64];
   const int kb = blockIdx.y, bh = blockIdx.x;
   const int b = bh / H, h = bh % H, d = H * HD;
   const int64_t Ip = fp8_ipad(I);
@@ -120,7 +148,7 @@ __global__ __launch_bounds__(256) void attn_fp8_pack_kernel(float* qkv, int64_t 
   for (int pass = 0; pass < 64 / KPP; ++pass) {
     const int kk = pass * KPP + t / TPK, part = t % TPK;
     const int key = 64 * kb + kk;
-    float x[16];
+    float x[16], r[16];
     if (key < I) {
       const float* src = base + (int64_t)key * ld + d + 16 * part;
 #pragma unroll
@@ -137,20 +165,27 @@ __global__ __launch_bounds__(256) void attn_fp8_pack_kernel(float* qkv, int64_t 
     for (int j = 0; j < 16; ++j) am = fmaxf(am, fabsf(x[j]));
     am = fmaxf(am, __shfl_xor(am, 1, 64));
     const int e = fp8::block_exp(am);
-    const float inv = fp8::pow2f(-e);
-    i32x4 o;
-    o.x = (int)fp8::pack4(x[0] * inv, x[1] * inv, x[2] * inv, x[3] * inv);
-    o.y = (int)fp8::pack4(x[4] * inv, x[5] * inv, x[6] * inv, x[7] * inv);
-    o.z = (int)fp8::pack4(x[8] * inv, x[9] * inv, x[10] * inv, x[11] * inv);
-    o.w = (int)fp8::pack4(x[12] * inv, x[13] * inv, x[14] * inv, x[15] * inv);
+    const i32x4 o = quant16(x, e, r, T8 == 2);
     const int64_t row = (int64_t)bh * Ip + key;
     *reinterpret_cast<i32x4*>(f.k8 + row * HD + 16 * part) = o;
     if ((part & 1) == 0) f.ks[row * (HD / 32) + part / 2] = (uint8_t)(e + 127);
+    if constexpr (T8 == 2) {
+      float aml = 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) aml = fmaxf(aml, fabsf(r[j]));
+      aml = fmaxf(aml, __shfl_xor(aml, 1, 64));
+      const int el = fp8::block_exp(aml);
+      float rl[16];
+      const i32x4 ol = quant16(r, el, rl, false);
+      *reinterpret_cast<i32x4*>(f.k8l + row * HD + 16 * part) = ol;
+      if ((part & 1) == 0) f.ksl[row * (HD / 32) + part / 2] = (uint8_t)(el + 127);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) r[j] = x[j] - r[j] + rl[j];      // hi + lo (dequantised)
+    }
     if (dequant && key < I) {
-      const float sc = fp8::pow2f(e);
       f32x4* dst = reinterpret_cast<f32x4*>(base + (int64_t)key * ld + d + 16 * part);
-      dst[0] = fp8::unpack4(o.x, sc); dst[1] = fp8::unpack4(o.y, sc);
-      dst[2] = fp8::unpack4(o.z, sc); dst[3] = fp8::unpack4(o.w, sc);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dst[q] = f32x4{r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]};
     }
   }
 
@@ -173,31 +208,60 @@ __global__ __launch_bounds__(256) void attn_fp8_pack_kernel(float* qkv, int64_t 
 #pragma unroll
     for (int o = 1; o < G; o <<= 1) am = fmaxf(am, __shfl_xor(am, o, 64));
     const int e = fp8::block_exp(am);
-    const float inv = fp8::pow2f(-e);
-#pragma unroll
-    for (int i = 0; i < KPT; i += 2) {
-      const int k0 = g * KPT + i;
-      const int v2 = __builtin_amdgcn_cvt_pk_fp8_f32(vs_f[k0 * VLD + c] * inv, vs_f[(k0 + 1) * VLD + c] * inv, 0, false);
-      if (dequant) {            // this thread owns (dim c, keys k0, k0 + 1) of the staged tile
-        const f32x4 dv = fp8::unpack4(v2, fp8::pow2f(e));
-        vs_f[k0 * VLD + c] = dv.x;
-        vs_f[(k0 + 1) * VLD + c] = dv.y;
-      }
+    const float inv = fp8::pow2f(-e), sc = fp8::pow2f(e);
+    float deq[KPT];                                  // this thread's keys' dequantised hi values
+    auto put = [&](int term, int k0, int v2) {
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int k = k0 + u, kk = k & 31;
         // key k of the block sits at byte 32 hh + 16 t + (kk & 3) + 4 (kk >> 3) of the P order
         const int pos = 32 * ((kk >> 2) & 1) + 16 * (k >> 5) + (kk & 3) + 4 * (kk >> 3);
-        vt_img[c * 64 + pos] = (uint8_t)((v2 >> (8 * u)) & 0xff);
+        vt_img[term][c * 64 + pos] = (uint8_t)((v2 >> (8 * u)) & 0xff);
       }
+    };
+#pragma unroll
+    for (int i = 0; i < KPT; i += 2) {
+      const int k0 = g * KPT + i;
+      const int v2 = __builtin_amdgcn_cvt_pk_fp8_f32(vs_f[k0 * VLD + c] * inv, vs_f[(k0 + 1) * VLD + c] * inv, 0, false);
+      const f32x4 dv = fp8::unpack4(v2, sc);
+      deq[i] = dv.x;
+      deq[i + 1] = dv.y;
+      put(0, k0, v2);
     }
     if (g == 0) f.vs[((int64_t)bh * (Ip / 64) + kb) * HD + c] = (uint8_t)(e + 127);
+    if constexpr (T8 == 2) {
+      float aml = 0.f;
+#pragma unroll
+      for (int i = 0; i < KPT; ++i) aml = fmaxf(aml, fabsf(vs_f[(g * KPT + i) * VLD + c] - deq[i]));
+#pragma unroll
+      for (int o = 1; o < G; o <<= 1) aml = fmaxf(aml, __shfl_xor(aml, o, 64));
+      const int el = fp8::block_exp(aml);
+      const float invl = fp8::pow2f(-el), scl = fp8::pow2f(el);
+#pragma unroll
+      for (int i = 0; i < KPT; i += 2) {
+        const int k0 = g * KPT + i;
+        const float r0 = vs_f[k0 * VLD + c] - deq[i], r1 = vs_f[(k0 + 1) * VLD + c] - deq[i + 1];
+        const int v2 = __builtin_amdgcn_cvt_pk_fp8_f32(r0 * invl, r1 * invl, 0, false);
+        const f32x4 dv = fp8::unpack4(v2, scl);
+        deq[i] += dv.x;
+        deq[i + 1] += dv.y;
+        put(1, k0, v2);
+      }
+      if (g == 0) f.vsl[((int64_t)bh * (Ip / 64) + kb) * HD + c] = (uint8_t)(el + 127);
+    }
+    if (dequant) {            // this thread owns (dim c, its keys) of the staged tile
+#pragma unroll
+      for (int i = 0; i < KPT; ++i) vs_f[(g * KPT + i) * VLD + c] = deq[i];
+    }
   }
   __syncthreads();
   for (int i = t; i < HD * 4; i += 256) {
     const int c = i / 4, q = i % 4;
     *reinterpret_cast<i32x4*>(f.vt8 + ((int64_t)bh * HD + c) * Ip + 64 * kb + 16 * q) =
-        *reinterpret_cast<const i32x4*>(vt_img + c * 64 + 16 * q);
+        *reinterpret_cast<const i32x4*>(vt_img[0] + c * 64 + 16 * q);
+    if constexpr (T8 == 2)
+      *reinterpret_cast<i32x4*>(f.vt8l + ((int64_t)bh * HD + c) * Ip + 64 * kb + 16 * q) =
+          *reinterpret_cast<const i32x4*>(vt_img[T8 - 1] + c * 64 + 16 * q);
   }
   if (dequant) {
     for (int i = t; i < 64 * HD / 4; i += 256) {
@@ -219,8 +283,10 @@ struct Fp8AttnArgs {
   int dequant;
 };
 
-// one wave per (b, h), 4 waves per block
-template <int HD>
+// one wave per (b, h), 4 waves per block.  T8 = 2: two-term operands, S^T = Kh Qh + Kh Ql + Kl Qh and
+// O^T += Vh Ph + Vh Pl + Vl Ph (the lo x lo products dropped: below the e4m3 pair's own rounding); P's lo
+// term is e4m3((P 2^8 - Ph) 2^4) at MFMA scale 2^-4.
+template <int HD, int T8>
 __global__ __launch_bounds__(256) void attn_fwd_fp8_kernel(Fp8AttnArgs p) {
   static_assert(HD == 64 || HD == 128, "fp8 attention: head_dim 64 or 128");
   constexpr int NKS = HD / 64;                   // 64-dim k steps of S^T
@@ -232,10 +298,12 @@ __global__ __launch_bounds__(256) void attn_fwd_fp8_kernel(Fp8AttnArgs p) {
   const int I = p.I, K = p.K, q_off = I - K;
   const int64_t Ip = fp8_ipad(I);
   float* Q = p.qkv + (int64_t)b * I * p.ld + h * HD;
-  const uint8_t* k8 = p.f.k8 + (int64_t)pair * Ip * HD + 16 * hh;
-  const uint8_t* ksc = p.f.ks + (int64_t)pair * Ip * (HD / 32) + hh;
-  const uint8_t* vt8 = p.f.vt8 + (int64_t)pair * HD * Ip + 32 * hh;
-  const uint8_t* vsc = p.f.vs + (int64_t)pair * (Ip / 64) * HD;
+  const int64_t kofs = (int64_t)pair * Ip * HD + 16 * hh, ksofs = (int64_t)pair * Ip * (HD / 32) + hh;
+  const int64_t vofs = (int64_t)pair * HD * Ip + 32 * hh, vsofs = (int64_t)pair * (Ip / 64) * HD;
+  const uint8_t* k8[2] = {p.f.k8 + kofs, p.f.k8l + kofs};
+  const uint8_t* ksc[2] = {p.f.ks + ksofs, p.f.ksl + ksofs};
+  const uint8_t* vt8[2] = {p.f.vt8 + vofs, p.f.vt8l + vofs};
+  const uint8_t* vsc[2] = {p.f.vs + vsofs, p.f.vsl + vsofs};
   const int32_t* qp = p.qpos ? p.qpos + (int64_t)b * K : nullptr;
   const int nqb = (K + 31) / 32;
   const float qscale = p.scale * 1.4426950408889634f;   // log2(e) / sqrt(hd)
@@ -247,37 +315,60 @@ __global__ __launch_bounds__(256) void attn_fwd_fp8_kernel(Fp8AttnArgs p) {
     // Q fragment of k-step ks: bytes 0-15 = dims 64 ks + 16 hh .. +15 (k-block 0), bytes 16-31 =
     // dims 64 ks + 32 + 16 hh .. +15 (k-block 1); each block's amax is completed across the two
     // half-lanes, and lane half hh supplies block hh's scale
-    i32x8 qa[NKS];
-    int qs[NKS];
+    i32x8 qa[T8][NKS];
+    int qs[T8][NKS];
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
       float* src = Q + (int64_t)qpos * p.ld + 64 * ks + 16 * hh;
-      float x[32];
+      float x[2][16];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const f32x4 v = *reinterpret_cast<const f32x4*>(src + 4 * (q & 3) + 32 * (q >> 2));
-        x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
+        float* xx = x[q >> 2] + 4 * (q & 3);
+        xx[0] = v.x; xx[1] = v.y; xx[2] = v.z; xx[3] = v.w;
       }
-      float am0 = 0.f, am1 = 0.f;
 #pragma unroll
-      for (int s = 0; s < 16; ++s) { am0 = fmaxf(am0, fabsf(x[s])); am1 = fmaxf(am1, fabsf(x[16 + s])); }
-      am0 = fmaxf(am0, __shfl_xor(am0, 32, 64));
-      am1 = fmaxf(am1, __shfl_xor(am1, 32, 64));
-      const int e0 = fp8::block_exp(am0), e1 = fp8::block_exp(am1);
-      const float inv0 = fp8::pow2f(-e0), inv1 = fp8::pow2f(-e1);
+      for (int term = 0; term < T8; ++term) {
+        float am[2] = {0.f, 0.f};
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        qa[ks][w] = (int)fp8::pack4(x[4 * w] * inv0, x[4 * w + 1] * inv0, x[4 * w + 2] * inv0, x[4 * w + 3] * inv0);
-        qa[ks][4 + w] = (int)fp8::pack4(x[16 + 4 * w] * inv1, x[17 + 4 * w] * inv1, x[18 + 4 * w] * inv1,
-                                        x[19 + 4 * w] * inv1);
+        for (int blk = 0; blk < 2; ++blk) {
+#pragma unroll
+          for (int s = 0; s < 16; ++s) am[blk] = fmaxf(am[blk], fabsf(x[blk][s]));
+          am[blk] = fmaxf(am[blk], __shfl_xor(am[blk], 32, 64));
+        }
+        const int e0 = fp8::block_exp(am[0]), e1 = fp8::block_exp(am[1]);
+        float r[2][16];
+        const i32x4 o0 = quant16(x[0], e0, r[0], true), o1 = quant16(x[1], e1, r[1], true);
+        qa[term][ks] = i32x8{o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
+        qs[term][ks] = (hh ? e1 : e0) + 127;
+#pragma unroll
+        for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+          for (int s = 0; s < 16; ++s) x[blk][s] = r[blk][s];            // the residual: next term's input
       }
-      qs[ks] = (hh ? e1 : e0) + 127;
       if (p.dequant && j < K) {          // this lane's 32 elements of query row qpos, dequantised in place
-        const float s0 = fp8::pow2f(e0), s1 = fp8::pow2f(e1);
+        float dq[2][16];
+#pragma unroll
+        for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+          for (int s = 0; s < 16; ++s) dq[blk][s] = 0.f;
+#pragma unroll
+        for (int term = 0; term < T8; ++term) {
+          // lane half hh holds block hh's scale; the other block's is the partner's
+          const int eo = __shfl_xor(qs[term][ks], 32, 64);
+          const float s0 = fp8::pow2f((hh ? eo : qs[term][ks]) - 127), s1 = fp8::pow2f((hh ? qs[term][ks] : eo) - 127);
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            const f32x4 a = fp8::unpack4(qa[term][ks][w], s0), c = fp8::unpack4(qa[term][ks][4 + w], s1);
+            dq[0][4 * w] += a.x; dq[0][4 * w + 1] += a.y; dq[0][4 * w + 2] += a.z; dq[0][4 * w + 3] += a.w;
+            dq[1][4 * w] += c.x; dq[1][4 * w + 1] += c.y; dq[1][4 * w + 2] += c.z; dq[1][4 * w + 3] += c.w;
+          }
+        }
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
-          *reinterpret_cast<f32x4*>(src + 4 * w) = fp8::unpack4(qa[ks][w], s0);
-          *reinterpret_cast<f32x4*>(src + 32 + 4 * w) = fp8::unpack4(qa[ks][4 + w], s1);
+          *reinterpret_cast<f32x4*>(src + 4 * w) = f32x4{dq[0][4 * w], dq[0][4 * w + 1], dq[0][4 * w + 2], dq[0][4 * w + 3]};
+          *reinterpret_cast<f32x4*>(src + 32 + 4 * w) =
+              f32x4{dq[1][4 * w], dq[1][4 * w + 1], dq[1][4 * w + 2], dq[1][4 * w + 3]};
         }
       }
     }
@@ -292,28 +383,32 @@ __global__ __launch_bounds__(256) void attn_fwd_fp8_kernel(Fp8AttnArgs p) {
     const int first_masked = (qp ? qp[32 * qb] : q_off + 32 * qb) / 64;
 
     // fragments of key block kb: K tiles t (keys 64 kb + 32 t + li), V^T chunks c (dims 32 c + li)
-    i32x8 kf[2][NKS], vf[NC];
-    int kscale[2][NKS], vscale[NC];
-    auto load_kv = [&](int kb, i32x8 (&kf_)[2][NKS], i32x8 (&vf_)[NC], int (&ksc_)[2][NKS], int (&vsc_)[NC]) {
+    i32x8 kf[T8][2][NKS], vf[T8][NC];
+    int kscale[T8][2][NKS], vscale[T8][NC];
+    auto load_kv = [&](int kb, i32x8 (&kf_)[T8][2][NKS], i32x8 (&vf_)[T8][NC], int (&ksc_)[T8][2][NKS],
+                       int (&vsc_)[T8][NC]) {
 #pragma unroll
-      for (int t2 = 0; t2 < 2; ++t2) {
-        const int64_t key = 64 * kb + 32 * t2 + li;
+      for (int term = 0; term < T8; ++term) {
 #pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) {
-          kf_[t2][ks] = fp8::load32(k8 + key * HD + 64 * ks, 32);      // dims 16hh.. | 32+16hh..
-          ksc_[t2][ks] = ksc[key * (HD / 32) + 2 * ks];
+        for (int t2 = 0; t2 < 2; ++t2) {
+          const int64_t key = 64 * kb + 32 * t2 + li;
+#pragma unroll
+          for (int ks = 0; ks < NKS; ++ks) {
+            kf_[term][t2][ks] = fp8::load32(k8[term] + key * HD + 64 * ks, 32);      // dims 16hh.. | 32+16hh..
+            ksc_[term][t2][ks] = ksc[term][key * (HD / 32) + 2 * ks];
+          }
         }
-      }
 #pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        vf_[c] = fp8::load32(vt8 + (int64_t)(32 * c + li) * Ip + 64 * kb);
-        vsc_[c] = vsc[(int64_t)kb * HD + 32 * c + li];
+        for (int c = 0; c < NC; ++c) {
+          vf_[term][c] = fp8::load32(vt8[term] + (int64_t)(32 * c + li) * Ip + 64 * kb);
+          vsc_[term][c] = vsc[term][(int64_t)kb * HD + 32 * c + li];
+        }
       }
     };
     load_kv(0, kf, vf, kscale, vscale);
     for (int kb = 0; kb < nkb; ++kb) {
-      i32x8 kn[2][NKS], vn[NC];
-      int kscn[2][NKS], vscn[NC];
+      i32x8 kn[T8][2][NKS], vn[T8][NC];
+      int kscn[T8][2][NKS], vscn[T8][NC];
       load_kv(min(kb + 1, nkb - 1), kn, vn, kscn, vscn);   // unconditional: the wait before this block's
                                                               // MFMAs can leave the prefetch in flight
       f32x16 s[2];
@@ -322,19 +417,16 @@ __global__ __launch_bounds__(256) void attn_fwd_fp8_kernel(Fp8AttnArgs p) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) s[t2][r] = 0.f;
 #pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) s[t2] = fp8::mfma_fp8(kf[t2][ks], qa[ks], s[t2], kscale[t2][ks], qs[ks]);
+        for (int ks = 0; ks < NKS; ++ks) {
+          s[t2] = fp8::mfma_fp8(kf[0][t2][ks], qa[0][ks], s[t2], kscale[0][t2][ks], qs[0][ks]);
+          if constexpr (T8 == 2) {
+            s[t2] = fp8::mfma_fp8(kf[0][t2][ks], qa[1][ks], s[t2], kscale[0][t2][ks], qs[1][ks]);
+            s[t2] = fp8::mfma_fp8(kf[1][t2][ks], qa[0][ks], s[t2], kscale[1][t2][ks], qs[0][ks]);
+          }
+        }
 #pragma unroll
         for (int r = 0; r < 16; ++r) s[t2][r] *= qscale;          // log2 domain
       }
-#ifdef OT_FP8_DEBUG
-      if (qb == 0 && kb == 0 && pair == 0) {
-        for (int t2 = 0; t2 < 2; ++t2)
-          for (int r = 0; r < 16; ++r) p.out[(32 * t2 + fp8::acc_row(r, hh)) * 32 + li] = s[t2][r];
-        if (li == 0) for (int ks = 0; ks < NKS; ++ks) p.out[4096 + hh] = (float)qs[ks];
-        p.out[4100 + lane] = (float)kscale[0][0];
-        return;
-      }
-#endif
       if (kb >= first_masked) {
 #pragma unroll
         for (int t2 = 0; t2 < 2; ++t2)
@@ -363,23 +455,35 @@ __global__ __launch_bounds__(256) void attn_fwd_fp8_kernel(Fp8AttnArgs p) {
       lsum += __shfl_xor(lsum, 32, 64);
       l = l * corr + lsum;
       m = mnew;
-      i32x8 pb;
+      i32x8 pb[T8];
 #pragma unroll
       for (int w = 0; w < 8; ++w) {
         const int t2 = w >> 2, r = 4 * (w & 3);
-        pb[w] = (int)fp8::pack4(s[t2][r], s[t2][r + 1], s[t2][r + 2], s[t2][r + 3]);
+        pb[0][w] = (int)fp8::pack4(s[t2][r], s[t2][r + 1], s[t2][r + 2], s[t2][r + 3]);
+        if constexpr (T8 == 2) {
+          const f32x4 q = fp8::unpack4(pb[0][w], 1.f);
+          pb[T8 - 1][w] = (int)fp8::pack4((s[t2][r] - q.x) * 16.f, (s[t2][r + 1] - q.y) * 16.f,
+                                          (s[t2][r + 2] - q.z) * 16.f, (s[t2][r + 3] - q.w) * 16.f);
+        }
       }
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         oacc[c] *= corr;
-        oacc[c] = fp8::mfma_fp8(vf[c], pb, oacc[c], vscale[c], 127);   // O^T += V^T P^T
+        oacc[c] = fp8::mfma_fp8(vf[0][c], pb[0], oacc[c], vscale[0][c], 127);   // O^T += V^T P^T
+        if constexpr (T8 == 2) {
+          oacc[c] = fp8::mfma_fp8(vf[0][c], pb[T8 - 1], oacc[c], vscale[0][c], 127 - 4);
+          oacc[c] = fp8::mfma_fp8(vf[T8 - 1][c], pb[0], oacc[c], vscale[T8 - 1][c], 127);
+        }
       }
 #pragma unroll
-      for (int t2 = 0; t2 < 2; ++t2)
+      for (int term = 0; term < T8; ++term) {
 #pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) { kf[t2][ks] = kn[t2][ks]; kscale[t2][ks] = kscn[t2][ks]; }
+        for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
-      for (int c = 0; c < NC; ++c) { vf[c] = vn[c]; vscale[c] = vscn[c]; }
+          for (int ks = 0; ks < NKS; ++ks) { kf[term][t2][ks] = kn[term][t2][ks]; kscale[term][t2][ks] = kscn[term][t2][ks]; }
+#pragma unroll
+        for (int c = 0; c < NC; ++c) { vf[term][c] = vn[term][c]; vscale[term][c] = vscn[term][c]; }
+      }
     }
     if (j < K) {
       const float inv = 1.f / l;
@@ -412,8 +516,9 @@ extern "C" int ot_attn_fwd_fp8_ex(float* qkv, int64_t ld, int B, int H, int I, i
                                   int head_dim, float* out, float* lse, void* workspace, size_t ws_bytes, int flags,
                                   void* stream) {
   OT_REQUIRE(qkv && out && lse, "ot_attn_fwd_fp8: null operand");
-  OT_REQUIRE((flags & ~OT_FP8_DEQUANT) == 0, "ot_attn_fwd_fp8: unknown flags 0x%x", flags);
+  OT_REQUIRE((flags & ~(OT_FP8_DEQUANT | OT_FP8_TWO_TERM)) == 0, "ot_attn_fwd_fp8: unknown flags 0x%x", flags);
   const int dq = (flags & OT_FP8_DEQUANT) ? 1 : 0;
+  const bool two = (flags & OT_FP8_TWO_TERM) != 0;
   OT_REQUIRE(B >= 0 && H > 0 && I > 0 && K > 0 && K <= I, "ot_attn_fwd_fp8: bad sizes B=%d H=%d I=%d K=%d", B, H, I, K);
   OT_REQUIRE(head_dim == 64 || head_dim == 128, "ot_attn_fwd_fp8: head_dim %d (64 or 128)", head_dim);
   OT_REQUIRE(ld % 4 == 0 && ld >= 3 * H * head_dim, "ot_attn_fwd_fp8: ld must be >= 3d and a multiple of 4");
@@ -426,13 +531,15 @@ extern "C" int ot_attn_fwd_fp8_ex(float* qkv, int64_t ld, int B, int H, int I, i
              (long long)BH, I);
   const dim3 pg((unsigned)BH, (unsigned)(fp8_ipad(I) / 64));
   hipStream_t s = (hipStream_t)stream;
-  if (head_dim == 64) hipLaunchKernelGGL(attn_fp8_pack_kernel<64>, pg, dim3(256), 0, s, qkv, ld, H, I, f, dq);
-  else hipLaunchKernelGGL(attn_fp8_pack_kernel<128>, pg, dim3(256), 0, s, qkv, ld, H, I, f, dq);
+  auto pk = head_dim == 64 ? (two ? attn_fp8_pack_kernel<64, 2> : attn_fp8_pack_kernel<64, 1>)
+                           : (two ? attn_fp8_pack_kernel<128, 2> : attn_fp8_pack_kernel<128, 1>);
+  hipLaunchKernelGGL(pk, pg, dim3(256), 0, s, qkv, ld, H, I, f, dq);
   OT_LAUNCH_CHECK("ot_attn_fwd_fp8(pack)");
   Fp8AttnArgs p{qkv, ld, H * head_dim, out, lse, B, H, I, K, 1.f / sqrtf((float)head_dim), qpos, f, dq};
   const unsigned grid = ceil_div(BH, 4);
-  if (head_dim == 64) hipLaunchKernelGGL(attn_fwd_fp8_kernel<64>, dim3(grid), dim3(256), 0, s, p);
-  else hipLaunchKernelGGL(attn_fwd_fp8_kernel<128>, dim3(grid), dim3(256), 0, s, p);
+  auto fk = head_dim == 64 ? (two ? attn_fwd_fp8_kernel<64, 2> : attn_fwd_fp8_kernel<64, 1>)
+                           : (two ? attn_fwd_fp8_kernel<128, 2> : attn_fwd_fp8_kernel<128, 1>);
+  hipLaunchKernelGGL(fk, dim3(grid), dim3(256), 0, s, p);
   OT_LAUNCH_CHECK("ot_attn_fwd_fp8");
   return OT_OK;
 }

@@ -235,17 +235,21 @@ def split_images(base, desc_dev, ndesc, total_units, img) -> None:
 
 def attn_fwd(qkv: torch.Tensor, ld: int, B: int, H: int, I: int, K: int, hd: int, out: torch.Tensor,
              lse: torch.Tensor, qpos: Optional[torch.Tensor] = None, fp8: bool = False,
-             dequant: bool = False) -> None:
+             dequant: bool = False, fp8_terms: int = 1) -> None:
     """ot_attn_fwd, or with ``fp8`` (head_dim 64/128) ot_attn_fwd_fp8_ex: QK^T and PV on block-scaled fp8
-    MFMA; ``dequant`` (training) also overwrites qkv's operands with their dequantised fp8 values
-    (OT_FP8_DEQUANT) for the backward."""
+    MFMA, operands as one e4m3 term or two (``fp8_terms`` 2: hi + lo, OT_FP8_TWO_TERM); ``dequant``
+    (training) also overwrites qkv's operands with their dequantised fp8 values (OT_FP8_DEQUANT) for the
+    backward."""
+    if fp8 and fp8_terms not in (1, 2):
+        raise ValueError(f'fp8_terms {fp8_terms}: 1 or 2')
     ws = None
     if fp8:
         ws = workspace(size('ot_attn_fwd_fp8_workspace_size', B, H, I, hd), qkv.device)
     ev = _probe.begin() if _probe is not None else None
     if fp8:
         call('ot_attn_fwd_fp8_ex', ptr(qkv), ld, B, H, I, K, ptr(qpos), hd, ptr(out), ptr(lse), ptr(ws),
-             ws.numel(), _lib.OT_FP8_DEQUANT if dequant else 0, stream())
+             ws.numel(), (_lib.OT_FP8_DEQUANT if dequant else 0) | (_lib.OT_FP8_TWO_TERM if fp8_terms == 2 else 0),
+             stream())
     else:
         call('ot_attn_fwd', ptr(qkv), ld, B, H, I, K, ptr(qpos), hd, ptr(out), ptr(lse), stream())
     if ev is not None:

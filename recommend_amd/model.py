@@ -200,7 +200,7 @@ def _block_forward(m, l, x, I, Kq, seed, training, rstd_in=None, select=False, n
     # fp8 training forward: qkv's operands are replaced by their dequantised fp8 values, so the backward
     # differentiates the forward that ran (OT_FP8_DEQUANT)
     K.attn_fwd(qkv, 3 * d, B, H, I, Kq, hd, o, lse, qpos=_attn_qpos(cfg, pos), fp8=m.attn_fp8,
-               dequant=m.attn_fp8 and training)
+               dequant=m.attn_fp8 and training, fp8_terms=m.fp8_terms)
     # x1 = x[tail] + drop(o @ Wo)      (model.py:117, 193)
     x1 = torch.empty(B * Kq, d, device=dev)
     rstd2 = torch.empty(B * Kq, device=dev)
@@ -511,6 +511,11 @@ class OneTransModel(nn.Module):
                          or os.environ.get('ONETRANS_ATTN', '') == 'fp8')
         if self.attn_fp8 and cfg.hidden_dim // cfg.num_heads not in (64, 128):
             raise ValueError('fp8 attention needs head_dim 64 or 128')
+        # e4m3 terms per attention operand: 2 (default; hi + lo, AUC within north_star's 1e-3 at C5) or 1
+        # (plain e4m3); config fp8_terms, env ONETRANS_FP8_TERMS
+        self.fp8_terms = int(os.environ.get('ONETRANS_FP8_TERMS', getattr(cfg, 'fp8_terms', 2)))
+        if self.fp8_terms not in (1, 2):
+            raise ValueError(f'fp8_terms {self.fp8_terms}: 1 or 2')
         # diagnostics only: ONETRANS_PYRAMID_KERNEL=0 addresses a 'tail' keep arithmetically instead of
         # through ot_pyramid_select's position map (same kept set; for A/B timing of the map plumbing)
         self.pyramid_kernel = os.environ.get('ONETRANS_PYRAMID_KERNEL', '1') != '0'

@@ -30,13 +30,31 @@ def _q_rows(x, block):
     sh = x.shape
     xb = x.reshape(*sh[:-1], sh[-1] // block, block)
     am = xb.abs().amax(-1, keepdim=True).float()
-    e = torch.where(am > 0, torch.floor(torch.log2(am)) - 7, torch.full_like(am, -120)).clamp(-120, 120).double()
+    # floor(log2 amax) from the exponent bits (frexp: am = m 2^E, m in [0.5, 1)), as the kernel reads it;
+    # a float32 log2 rounds up to the next integer just below a power of two (e.g. a lo term's residual of
+    # half an e4m3 ulp)
+    e = torch.where(am > 0, torch.frexp(am)[1].double() - 1 - 7, torch.full_like(am, -120).double()).clamp(-120, 120)
     q = (xb * torch.exp2(-e)).float().to(E4M3).double() * torch.exp2(e)
     return q.reshape(sh)
 
 
-def quantised(qkv, B, H, I, qpos, hd):
+def _q2_rows(x, block):
+    """Two-term form (OT_FP8_TWO_TERM): hi = _q_rows(x), plus lo = _q_rows(x - hi) with its own scales."""
+    hi = _q_rows(x, block)
+    return hi + _q_rows(x - hi, block)
+
+
+def _q_p(p, terms):
+    """P * 2^8 as the kernel rounds it: e4m3, plus (two terms) e4m3 of the residual * 2^4, / 2^4."""
+    ph = p.float().to(E4M3).double()
+    if terms == 1:
+        return ph
+    return ph + ((p - ph) * 16).float().to(E4M3).double() / 16
+
+
+def quantised(qkv, B, H, I, qpos, hd, terms=1):
     """The operands as the kernel quantises them: (q8 [B, Kq, H, hd], k8, v8 [B, I, H, hd]) float64."""
+    qr = _q_rows if terms == 1 else _q2_rows
     d = H * hd
     bi = torch.arange(B)[:, None]
     q = qkv[:, :d].reshape(B, I, H, hd)[bi, qpos]
@@ -46,23 +64,23 @@ def quantised(qkv, B, H, I, qpos, hd):
     vp = torch.zeros(B, Ip, H, hd, dtype=torch.float64)
     vp[:, :I] = v
     # V: one scale per (dim, 64 keys): quantise the [B, H, hd, Ip] transpose along keys in blocks of 64
-    v8 = _q_rows(vp.permute(0, 2, 3, 1).contiguous(), 64).permute(0, 3, 1, 2)[:, :I]
-    return _q_rows(q, 32), _q_rows(k, 32), v8
+    v8 = qr(vp.permute(0, 2, 3, 1).contiguous(), 64).permute(0, 3, 1, 2)[:, :I]
+    return qr(q, 32), qr(k, 32), v8
 
 
-def emulate(qkv, B, H, I, qpos, hd):
+def emulate(qkv, B, H, I, qpos, hd, terms=1):
     """float64 attention from fp8-quantised operands (the kernel's quantisation, see module docstring)."""
     d = H * hd
     Kq = qpos.shape[1]
     scale = math.log2(math.e) / math.sqrt(hd)
-    q8, k8, v8 = quantised(qkv, B, H, I, qpos, hd)
+    q8, k8, v8 = quantised(qkv, B, H, I, qpos, hd, terms)
     s = torch.einsum('bqhd,bkhd->bhqk', q8, k8) * scale               # log2 units
     mask = torch.arange(I)[None, None, None, :] <= qpos[:, None, :, None]
     s = torch.where(mask, s, torch.tensor(-math.inf, dtype=s.dtype))
     m = s.amax(-1, keepdim=True)
     p = torch.exp2(s - m + 8)                                        # P * 2^8
     l = p.sum(-1, keepdim=True)
-    p8 = p.float().to(E4M3).double()
+    p8 = _q_p(p, terms)
     o = torch.einsum('bhqk,bkhd->bqhd', p8, v8) / l.permute(0, 2, 1, 3)
     lse = (m[..., 0] - 8) * math.log(2) + torch.log(l[..., 0])      # [B, H, Kq], the kernel's formula
     return o.reshape(B * Kq, d), lse.reshape(-1)
@@ -82,6 +100,7 @@ def exact(qkv, B, H, I, qpos, hd):
     return o.reshape(-1, d), lse.reshape(-1)
 
 
+@pytest.mark.parametrize('terms', [1, 2])
 @pytest.mark.parametrize('B,H,I,Kq,hd,sel,qscale', [
     (3, 2, 200, 200, 64, False, 1.0),     # full query set, I not a multiple of 64
     (2, 8, 1036, 1036, 64, False, 1.0),   # C5's layer-0 length and head count
@@ -91,7 +110,7 @@ def exact(qkv, B, H, I, qpos, hd):
     (5, 3, 7, 1, 64, False, 1.0),         # last layer after DCE: one query, one partial key block
     (1, 1, 64, 64, 64, False, 0.05),      # nearly uniform softmax
 ])
-def test_attn_fwd_fp8_bounds(dev, B, H, I, Kq, hd, sel, qscale):
+def test_attn_fwd_fp8_bounds(dev, B, H, I, Kq, hd, sel, qscale, terms):
     g = torch.Generator().manual_seed(I * 31 + Kq)
     d = H * hd
     qkv = torch.randn(B * I, 3 * d, generator=g, dtype=torch.float64)
@@ -107,27 +126,35 @@ def test_attn_fwd_fp8_bounds(dev, B, H, I, Kq, hd, sel, qscale):
     out = torch.full((B * Kq, d), float('nan'), device=dev)
     lse = torch.full((B * H * Kq,), float('nan'), device=dev)
     qp_d = torch.from_numpy(qpos.astype(np.int32).reshape(-1)).to(dev) if sel else None
-    K.attn_fwd(qkv_d, 3 * d, B, H, I, Kq, hd, out, lse, qpos=qp_d, fp8=True)
+    K.attn_fwd(qkv_d, 3 * d, B, H, I, Kq, hd, out, lse, qpos=qp_d, fp8=True, fp8_terms=terms)
     got = out.double().cpu()
     assert torch.isfinite(got).all()
     ref, lse_ref = exact(qkv.float().double(), B, H, I, qpos_t, hd)
-    emu, lse_emu = emulate(qkv.float().double(), B, H, I, qpos_t, hd)
+    emu, lse_emu = emulate(qkv.float().double(), B, H, I, qpos_t, hd, terms)
     omax = float(ref.abs().max())
     e_kernel = float((got - ref).abs().max()) / omax
     e_quant = float((emu - ref).abs().max()) / omax
     e_vs_emu = float((got - emu).abs().max()) / omax
     dl = float((lse.double().cpu() - lse_ref).abs().max())
     dl_q = float((lse_emu - lse_ref).abs().max())
-    print(f'fp8 attention B{B} H{H} I{I} K{Kq} hd{hd}: max err/max|O| kernel {e_kernel:.4f}, '
+    print(f'fp8 attention ({terms} term) B{B} H{H} I{I} K{Kq} hd{hd}: max err/max|O| kernel {e_kernel:.4f}, '
           f'quantisation {e_quant:.4f}, kernel vs emulation {e_vs_emu:.4f}; max |d lse| {dl:.4f} '
           f'(quantisation {dl_q:.4f})')
-    assert e_kernel <= 1.5 * e_quant + 1e-3, (e_kernel, e_quant)
-    assert e_kernel < 0.12
-    assert dl <= 1.5 * dl_q + 0.01 and dl < 0.25, (dl, dl_q)
+    if terms == 1:
+        assert e_kernel <= 1.5 * e_quant + 1e-3, (e_kernel, e_quant)
+        assert e_kernel < 0.12
+        assert dl <= 1.5 * dl_q + 0.01 and dl < 0.25, (dl, dl_q)
+    else:
+        # two terms: ~7 significant bits per operand; the kernel's f32 accumulation order and the dropped
+        # lo x lo products are then of the emulation's own size
+        assert e_kernel <= 2.0 * e_quant + 2e-3, (e_kernel, e_quant)
+        assert e_kernel < 0.02
+        assert dl <= 2.0 * dl_q + 2e-3 and dl < 0.02, (dl, dl_q)
 
 
+@pytest.mark.parametrize('terms', [1, 2])
 @pytest.mark.parametrize('B,H,I,Kq,sel', [(2, 8, 1036, 1036, False), (3, 2, 300, 37, False), (2, 2, 257, 40, True)])
-def test_attn_fp8_training_backward(dev, B, H, I, Kq, sel):
+def test_attn_fp8_training_backward(dev, B, H, I, Kq, sel, terms):
     """Training with fp8 attention (OT_FP8_DEQUANT): the forward leaves the dequantised operands in qkv —
     bit-equal to the kernel's documented quantisation (torch.float8_e4m3fn emulation) — and the bf16
     backward run on them is the straight-through gradient of the forward that ran: with p = exp(s - lse)
@@ -140,6 +167,7 @@ def test_attn_fp8_training_backward(dev, B, H, I, Kq, sel):
     d = H * hd
     qkv = torch.randn(B * I, 3 * d, generator=g, dtype=torch.float64).float().double()
     qkv[:, 2 * d:] *= torch.exp(0.5 * torch.randn(B * I, 1, generator=g, dtype=torch.float64)).float().double()
+    qkv = qkv.float().double()                 # the f32 values the kernel reads
     if sel:
         rng = np.random.default_rng(9)
         qpos = np.stack([np.append(np.sort(rng.choice(I - 1, Kq - 1, replace=False)), I - 1) for _ in range(B)])
@@ -152,7 +180,7 @@ def test_attn_fp8_training_backward(dev, B, H, I, Kq, sel):
     lse = torch.empty(B * H * Kq, device=dev)
     old = K.set_matmul_mode('bf16')
     try:
-        K.attn_fwd(qkv_d, 3 * d, B, H, I, Kq, hd, out, lse, qpos=qp_d, fp8=True, dequant=True)
+        K.attn_fwd(qkv_d, 3 * d, B, H, I, Kq, hd, out, lse, qpos=qp_d, fp8=True, dequant=True, fp8_terms=terms)
         dout = torch.randn(B * Kq, d, generator=g, dtype=torch.float64).float()
         dqkv = torch.full((B * I, 3 * d), float('nan'), device=dev)
         dqkv[:, :d].zero_()
@@ -160,8 +188,14 @@ def test_attn_fp8_training_backward(dev, B, H, I, Kq, sel):
     finally:
         K.set_matmul_mode(old)
     got_qkv = qkv_d.double().cpu().reshape(B, I, 3, H, hd)
-    q8, k8, v8 = quantised(qkv, B, H, I, qpos_t, hd)
+    q8, k8, v8 = quantised(qkv, B, H, I, qpos_t, hd, terms)
     bi = torch.arange(B)[:, None]
+    for name, g_, e_ in (('K', got_qkv[:, :, 1], k8), ('V', got_qkv[:, :, 2], v8)):
+        if not torch.equal(g_, e_):
+            bad = (g_ != e_).nonzero()
+            print(f'{name}: {bad.shape[0]} of {g_.numel()} dequantised values differ; first {bad[:4].tolist()}: '
+                  f'kernel {g_[tuple(bad[:4].T)].tolist()} emulation {e_[tuple(bad[:4].T)].tolist()} '
+                  f'input {qkv.reshape(B, I, 3, H, hd)[:, :, 1 if name == "K" else 2][tuple(bad[:4].T)].tolist()}')
     assert torch.equal(got_qkv[:, :, 1], k8) and torch.equal(got_qkv[:, :, 2], v8)
     assert torch.equal(got_qkv[:, :, 0][bi, qpos_t], q8)
     # straight-through reference (float64)
@@ -172,7 +206,7 @@ def test_attn_fp8_training_backward(dev, B, H, I, Kq, sel):
     m = s.amax(-1, keepdim=True)
     pt = torch.exp(s - m)
     p = pt / pt.sum(-1, keepdim=True)
-    p8 = (pt * 256).float().to(E4M3).double() / (256 * pt.sum(-1, keepdim=True))   # the forward's PV weights
+    p8 = _q_p(pt * 256, terms) / (256 * pt.sum(-1, keepdim=True))   # the forward's PV weights
     o_fwd = torch.einsum('bhqk,bkhd->bqhd', p8, v8)
     do = dout.double().reshape(B, Kq, H, hd)
     dp = torch.einsum('bqhd,bkhd->bhqk', do, v8)
@@ -193,7 +227,7 @@ def test_attn_fp8_training_backward(dev, B, H, I, Kq, sel):
     se = torch.where(mask, torch.einsum('bqhd,bkhd->bhqk', q, k) * sc, torch.tensor(-1e9, dtype=torch.float64))
     torch.einsum('bhqk,bkhd->bqhd', torch.softmax(se, -1), v).reshape(B * Kq, d).backward(dout.double())
     bias = (got.reshape(B * I, 3 * d) - qkv_r.grad).abs().max().item() / qkv_r.grad.abs().max().item()
-    print(f'fp8 training backward B{B} H{H} I{I} K{Kq}: max err / max|g| vs the straight-through reference '
+    print(f'fp8 training backward ({terms} term) B{B} H{H} I{I} K{Kq}: max err / max|g| vs the straight-through reference '
           f'{err:.4f}; vs the exact attention gradient {bias:.4f}')
     assert torch.isfinite(got).all()
     assert err < 3e-2, err

@@ -11,7 +11,10 @@ Bounds (stated per mode; |logit| <= 1.51 at this init), measured on the 4096-sam
 * bf16:                   max |d logit| < 0.05, AUC difference < 1e-3 = north_star's AUC bound (measured
                           1.8e-2 / 3.7e-4: bf16 operand rounding moves logits by ~1e-2, which at 4096
                           samples reorders few enough positive/negative pairs);
-* bf16 + fp8 attention:   see FP8 below.
+* bf16 + fp8 attention:   max |d logit| < 0.05, AUC difference < 1e-3 (measured 1.8e-2 / 3.7e-4) with the
+                          default two-term e4m3 operands (fp8_terms 2: hi + lo per element, three fp8 MFMA
+                          products per QK^T / PV); plain e4m3 (fp8_terms 1) measured 9.9e-2 / 1.25e-3 — its
+                          3-bit mantissa cannot meet north_star's AUC bound (tests/golden/fp8_error_study.py).
 The AUC is the exact rank AUC (recommend_amd.metrics.auc) of each task against the batch's labels."""
 
 import os
@@ -30,8 +33,8 @@ from recommend_amd.model import OneTransModel
 from recommend_amd.params import init_params
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
-LOGIT_BOUND = {'split': 1e-3, 'bf16': 0.05, 'fp8attn': 0.15}
-AUC_BOUND = {'split': 1e-4, 'bf16': 1e-3, 'fp8attn': 2e-3}
+LOGIT_BOUND = {'split': 1e-3, 'bf16': 0.05, 'fp8attn': 0.05}
+AUC_BOUND = {'split': 1e-4, 'bf16': 1e-3, 'fp8attn': 1e-3}
 
 
 @pytest.mark.parametrize('mode', ['split', 'bf16', 'fp8attn'])
@@ -73,8 +76,10 @@ def test_c5_fullsize_precision(dev, mode):
 
 # --------------------------------------------------------------- one C5 training step in bf16 / fp8attn
 TRAIN_BOUND = {   # (probs, loss, bank gradient max err / max|g|, bank gradient L2 norm, table gradient L2 norm)
-    'bf16': (1e-2, 1e-2, 0.1, 2e-2, 2e-2),
-    'fp8attn': (3e-2, 2e-2, 0.3, 5e-2, 5e-2),
+    # measured bf16: 3.9e-3, 6.8e-4, 1.5e-2 (median 4.5e-3), 7.6e-3, 2.1e-3; fp8attn (two-term): 4.6e-3,
+    # 6.3e-4, 1.5e-2 (median 4.4e-3), 7.8e-3, 2.0e-3
+    'bf16': (1e-2, 2e-3, 5e-2, 2e-2, 1e-2),
+    'fp8attn': (1e-2, 2e-3, 5e-2, 2e-2, 1e-2),
 }
 
 

@@ -788,171 +788,6 @@ void attn_bwd_kernel(AttnArgs p) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Backward on 16 x 16 blocks (v_mfma_f32_16x16x4_f32: f32-exact like the 32 x 32 kernel) for the tail rule
-// (no selection map).  Same pass as attn_bwd_kernel — one wave per (sample, head), key blocks outer, the
-// query blocks that see them inner, the dQ partial read-modify-written in dqkv — but every block is 16
-// tokens: the causal triangle and the padding of I = 140 leave 0.857 of the issued MFMA flops useful
-// (9 blocks, 45 pairs) against 0.643 with 32-token blocks, and a wave's working set (16 x 16 accumulators
-// of 4 registers, 8 KiB of LDS tiles at head_dim 32) fits 4 waves per SIMD instead of 2.
-//   S = Q K^T, dP = dO V^T       A = Q / dO rows (lane & 15 = query), B = K / V rows (lane & 15 = key); the
-//                                k index of step s and lane group g = lane >> 4 is dim (HD/4) g + s, so a
-//                                lane's fragment is HD/4 contiguous dims of one row (float4 loads)
-//   (results: lane (c = lane & 15, g) holds S[query 4g + r][key c], r < 4)
-//   dV^T += dO^T P, dK^T += Q^T dS   accumulator as the B operand: instruction r takes register r of P /
-//                                dS (k = g <-> query 4g + r); A = dO / Q block [query][dim] from LDS
-//   dQ^T += K^T dS^T              A = K block [key][dim] (LDS), B = dS [query][key] (LDS), k = g <-> key 4s + g
-template <int HD>
-constexpr int B16_PER_WAVE() { return 3 * 16 * (HD + 4) + 16 * 20; }
-
-template <int HD>
-__global__ __launch_bounds__(256, HD <= 32 ? 3 : 2) void attn_bwd16_kernel(AttnArgs p) {
-  static_assert(HD == 32 || HD == 64, "attn_bwd16_kernel: head_dim 32 or 64");
-  constexpr int LD = HD + 4;               // K / Q / dO tile row stride (floats)
-  constexpr int SLD = 20;                  // dS tile [16 queries][16 keys + 4]
-  constexpr int NS = HD / 4;               // k-steps over the head dim
-  constexpr int ND = HD / 16;              // 16-dim blocks of dK / dV / dQ
-  constexpr int PW = B16_PER_WAVE<HD>();
-  __shared__ __attribute__((aligned(16))) float lds[4 * PW];
-  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
-  const int wave = threadIdx.x >> 6;
-  float* tK = lds + wave * PW;             // K block  [key][dim]
-  float* tQ = tK + 16 * LD;                // Q block  [query][dim]
-  float* tO = tQ + 16 * LD;                // dO block [query][dim]
-  float* tS = tO + 16 * LD;                // dS block [query][key]
-  const int pair = blockIdx.x * 4 + wave;
-  if (pair >= p.B * p.H) return;
-  const int b = pair / p.H, h = pair % p.H;
-  const int I = p.I, K = p.K, q_off = I - K, KP = attn_kpad(K);
-  const int64_t tok0 = (int64_t)b * I;
-  const float* Q = p.qkv + tok0 * p.ld + h * HD;
-  const float* Kp = Q + p.d;
-  const float* V = Q + 2 * p.d;
-  const float* Qt = Q + (int64_t)q_off * p.ld;
-  const float* dO = p.dout + (int64_t)b * K * p.d + h * HD;
-  const float* lsep = p.delta + (int64_t)pair * KP;                       // padded lse (+inf past K)
-  const float* dltp = p.delta + ((int64_t)p.B * p.H + pair) * KP;         // padded delta
-  float* dQt = p.dqkv + (tok0 + q_off) * p.ld + h * HD;
-  float* dK = p.dqkv + tok0 * p.ld + p.d + h * HD;
-  float* dV = dK + p.d;
-  const int nqb = (K + 15) / 16, nkb = (I + 15) / 16;
-  const int dg = (HD / 4) * g;             // this lane group's first dim of the S / dP fragments
-
-  auto load_row = [&](float (&f)[NS], const float* base, int64_t ld, int row, int nrows) {
-    if (row < nrows) {
-      const float* src = base + (int64_t)row * ld + dg;
-#pragma unroll
-      for (int q = 0; q < NS / 4; ++q) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(src + 4 * q);
-        f[4 * q] = v.x; f[4 * q + 1] = v.y; f[4 * q + 2] = v.z; f[4 * q + 3] = v.w;
-      }
-    } else {
-#pragma unroll
-      for (int s = 0; s < NS; ++s) f[s] = 0.f;
-    }
-  };
-  auto to_tile = [&](float* tile, const float (&f)[NS]) {
-#pragma unroll
-    for (int q = 0; q < NS / 4; ++q)
-      *reinterpret_cast<f32x4*>(tile + c * LD + dg + 4 * q) = f32x4{f[4 * q], f[4 * q + 1], f[4 * q + 2], f[4 * q + 3]};
-  };
-
-  for (int kb = 0; kb < nkb; ++kb) {
-    const int key0 = 16 * kb, kpos = key0 + c;
-    float kf[NS], vf[NS];
-    load_row(kf, Kp, p.ld, kpos, I);
-    load_row(vf, V, p.ld, kpos, I);
-    to_tile(tK, kf);
-    f32x4 dk[ND], dv[ND];
-#pragma unroll
-    for (int db = 0; db < ND; ++db) { dk[db] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[db] = dk[db]; }
-    int qb0 = key0 - q_off - 15;                       // first query block whose last query sees key0
-    qb0 = qb0 <= 0 ? 0 : (qb0 + 15) / 16;
-    // everything a pair reads from memory is loaded one pair ahead: the Q / dO fragments, the row
-    // statistics and the running dQ partial (dQ^T block: lane (c, g) holds dQ[query q0 + c][dim 16 db + 4 g + r])
-    float qf[NS], of[NS];
-    f32x4 l4, d4, dq[ND];
-    auto load_pair = [&](int qbn) {
-      const int q0n = 16 * qbn, jn = q0n + c;
-      load_row(qf, Qt, p.ld, jn, K);
-      load_row(of, dO, p.d, jn, K);
-      l4 = *reinterpret_cast<const f32x4*>(lsep + q0n + 4 * g);
-      d4 = *reinterpret_cast<const f32x4*>(dltp + q0n + 4 * g);
-      const float* src = dQt + (int64_t)(jn < K ? jn : K - 1) * p.ld + 4 * g;
-#pragma unroll
-      for (int db = 0; db < ND; ++db)
-        dq[db] = kb > 0 ? *reinterpret_cast<const f32x4*>(src + 16 * db) : f32x4{0.f, 0.f, 0.f, 0.f};
-    };
-    load_pair(qb0);
-    for (int qb = qb0; qb < nqb; ++qb) {
-      const int q0 = 16 * qb;
-      const int jq = q0 + c;
-      float* dqrow = dQt + (int64_t)(jq < K ? jq : K - 1) * p.ld + 4 * g;
-      __builtin_amdgcn_wave_barrier();
-      to_tile(tQ, qf);
-      to_tile(tO, of);
-      f32x4 sp = {0.f, 0.f, 0.f, 0.f}, dp = sp;
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        sp = __builtin_amdgcn_mfma_f32_16x16x4f32(qf[s], kf[s], sp, 0, 0, 0);   // S: row query, col key
-        dp = __builtin_amdgcn_mfma_f32_16x16x4f32(of[s], vf[s], dp, 0, 0, 0);   // dP
-      }
-      const f32x4 lc = l4, dc = d4;
-      f32x4 dqc[ND];
-#pragma unroll
-      for (int db = 0; db < ND; ++db) dqc[db] = dq[db];
-      if (qb + 1 < nqb) load_pair(qb + 1);              // the next pair's operands, in flight from here
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int qpos = q_off + q0 + 4 * g + r;
-        const float ex = __expf(sp[r] * p.scale - lc[r]);
-        const float P = kpos <= qpos ? ex : 0.f;       // padded queries: lse = +inf -> 0; padded keys masked
-        sp[r] = P;
-        dp[r] = P * (dp[r] - dc[r]) * p.scale;         // dS, pre-scaled by 1/sqrt(hd)
-        tS[(4 * g + r) * SLD + c] = dp[r];
-      }
-      __builtin_amdgcn_wave_barrier();
-      // dV^T += dO^T P, dK^T += Q^T dS (instruction r: k = g <-> query 4g + r)
-      float ao[4][ND], aq[4][ND];
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int db = 0; db < ND; ++db) {
-          ao[r][db] = tO[(4 * g + r) * LD + 16 * db + c];
-          aq[r][db] = tQ[(4 * g + r) * LD + 16 * db + c];
-        }
-      // dQ^T += K^T dS^T (instruction s: k = g <-> key 4s + g)
-      float bk[4][ND], bs[4];
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        bs[s] = tS[c * SLD + 4 * s + g];
-#pragma unroll
-        for (int db = 0; db < ND; ++db) bk[s][db] = tK[(4 * s + g) * LD + 16 * db + c];
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int db = 0; db < ND; ++db) {
-          dv[db] = __builtin_amdgcn_mfma_f32_16x16x4f32(ao[r][db], sp[r], dv[db], 0, 0, 0);
-          dk[db] = __builtin_amdgcn_mfma_f32_16x16x4f32(aq[r][db], dp[r], dk[db], 0, 0, 0);
-          dqc[db] = __builtin_amdgcn_mfma_f32_16x16x4f32(bk[r][db], bs[r], dqc[db], 0, 0, 0);
-        }
-      if (jq < K) {
-#pragma unroll
-        for (int db = 0; db < ND; ++db) *reinterpret_cast<f32x4*>(dqrow + 16 * db) = dqc[db];
-      }
-    }
-    if (kpos < I) {
-#pragma unroll
-      for (int db = 0; db < ND; ++db) {
-        *reinterpret_cast<f32x4*>(dK + (int64_t)kpos * p.ld + 16 * db + 4 * g) = dk[db];
-        *reinterpret_cast<f32x4*>(dV + (int64_t)kpos * p.ld + 16 * db + 4 * g) = dv[db];
-      }
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------------
 // bf16 backward (TERMS = 1, OT_MATMUL_BF16; the kernel also builds with TERMS = 6 split planes, which
 // measured slower than attn_bwd_kernel and is not dispatched).
 // Same pass structure as attn_bwd_kernel (one wave per (sample, head), key blocks outer, the query
@@ -1710,19 +1545,6 @@ static int g_attn_bwd_ds = [] {
   return (e && std::atoi(e) == 1) ? 1 : 2;
 }();
 
-// f32-MFMA backward on 16 x 16 blocks (attn_bwd16_kernel) for the tail rule up to this many tokens
-// (ONETRANS_ATTN_BWD16_MAX_I, default 160: at I = 140 it measured 2% faster than the 32 x 32 kernel at
-// head_dim 32 and 64; at C3's I = 262 / 524 11-20% slower: its 3x more (query block, key block) pairs
-// re-read Q / dO and read-modify-write dQ 3x as often); ONETRANS_ATTN_BWD16=0 keeps the 32 x 32 kernel
-static int g_attn_bwd16 = [] {
-  const char* e = std::getenv("ONETRANS_ATTN_BWD16");
-  return (e && std::atoi(e) == 0) ? 0 : 1;
-}();
-static int g_attn_bwd16_max_i = [] {
-  const char* e = std::getenv("ONETRANS_ATTN_BWD16_MAX_I");
-  return e ? std::atoi(e) : 160;
-}();
-
 extern "C" size_t ot_attn_bwd_workspace_size(int B, int H, int K) {
   return (2 * (size_t)B * H + B) * attn_kpad(K) * sizeof(float);     // lse, delta (+ padded qpos)
 }
@@ -1834,10 +1656,6 @@ static int attn_bwd_impl(const float* qkv, int64_t ld, const float* out, const f
       (void)hipGetLastError();
     });
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * waves), (size_t)waves * lds, (hipStream_t)stream, p);
-  } else if (g_attn_bwd16 && qpos == nullptr && (head_dim == 32 || head_dim == 64) && I <= g_attn_bwd16_max_i) {
-    // f32-accurate, tail rule: 16 x 16 blocks (see attn_bwd16_kernel)
-    void (*kern)(AttnArgs) = head_dim == 32 ? attn_bwd16_kernel<32> : attn_bwd16_kernel<64>;
-    hipLaunchKernelGGL(kern, dim3(ceil_div((int64_t)B * H, 4)), dim3(256), 0, (hipStream_t)stream, p);
   } else if (head_dim == 64 && g_attn_bwd_ds == 2) {
     // head_dim 64 as two 32-dim waves per (sample, head): 2 waves / SIMD instead of 1
     const bool sel = qpos != nullptr;

@@ -795,126 +795,6 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
   gemm_vec_epilogue<EPIT, 1, AXT == OT_AX_RMSNORM, MINW >= 4 ? 4 : 8>(p, acc, smem, tm, n0, g);
 }
 
-// Plane GEMM on 256 x 128 tiles (two consecutive 128-row tiles of the row map, tm0 = 2 tp and tm0 + 1):
-// each wave owns 32 rows of BOTH halves, so every B fragment it reads from LDS feeds twice the MFMAs of
-// plane_gemm_kernel — the B planes (12 KiB per wave per stage in split mode) dominated the LDS traffic
-// (~99 of 128 B/clk per CU at 4 workgroups x 4 waves), now ~60 B/clk.  Two 28 KiB stages (2 workgroups,
-// 2 waves / SIMD).  Pairs whose halves belong to different weight groups (row maps not padded to 256 rows
-// per group: build_map pads them, so the model's never do) run the k-loop once per half.
-template <int TERMS>
-constexpr int pg2_stage_bytes() { return 2 * PG_A_BYTES + (TERMS == 1 ? GT * 16 * 2 : PG_B_BYTES); }
-
-template <int AXT, int EPIT, int TERMS = 6>
-__global__ __launch_bounds__(256, 2) void plane_gemm2_kernel(GemmArgs p) {
-  static_assert(TERMS == 6 || TERMS == 1, "plane GEMM terms");
-  constexpr int STG = pg2_stage_bytes<TERMS>();
-  constexpr int AB = 2 * PG_A_BYTES;                 // A image: 256 rows x 16 f32
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  char* lds = reinterpret_cast<char*>(smem);
-  const int npair = p.ntm >> 1;
-  const int nwg = npair * p.ntn;
-  const int wg = xcd_remap(blockIdx.x, nwg);
-  const int tp = wg / p.ntn, tn = wg % p.ntn;
-  const int tm0 = 2 * tp;
-  const int g0 = p.tile_group ? p.tile_group[tm0] : 0;
-  const int g1 = p.tile_group ? p.tile_group[tm0 + 1] : 0;
-  const int n0 = tn * GT;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int h = lane >> 5, li = lane & 31;
-  const int nk = p.K >> 4;
-
-  // A glds: wave w's instruction i fills LDS KiB 4w + i of the A image = rows 16 (4w + i) .. +15 of the pair
-  const float* asrc[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = (4 * wave + i) * 16 + (lane >> 2);
-    const int64_t gr = (int64_t)tm0 * GT + r;
-    int ir = p.in_rows ? p.in_rows[gr] : (int)gr;
-    ir = ir < 0 ? 0 : ir;
-    const int lc = (lane & 3) ^ ((r >> 2) & 3);
-    asrc[i] = p.A + (int64_t)ir * p.lda + 4 * lc;
-  }
-  auto bimg_of = [&](int g) {
-    const int gb = p.w_gstride ? g : 0;
-    return reinterpret_cast<const char*>(p.bimg) + ((int64_t)gb * p.bimg_ntn + p.bimg_tn0 + tn) * nk * PG_B_BYTES;
-  };
-
-  f32x16 acc[2][4];
-#pragma unroll
-  for (int hb = 0; hb < 2; ++hb)
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[hb][a][r] = 0.f;
-
-  const int boff = AB + li * 32 + 16 * (h ^ ((li >> 3) & 1));
-  // one k-loop over the stages; mask: which halves (bit hb) accumulate, bimg0: the B image of their group
-  auto kloop = [&](const char* bimg0, int mask) {
-    const char* bsrc = bimg0 + (3 * wave) * 1024 + 16 * lane;
-    const char* bsrc1 = bimg0 + wave * 1024 + 16 * lane;
-    auto issue = [&](int ks, int buf) {
-      char* sb = lds + buf * STG;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + 16 * ks), (lds_void_t*)(sb + (4 * wave + i) * 1024),
-                                         16, 0, 0);
-      if (TERMS == 1) {
-        __builtin_amdgcn_global_load_lds((const void*)(bsrc1 + (int64_t)ks * PG_B_BYTES),
-                                         (lds_void_t*)(sb + AB + wave * 1024), 16, 0, 0);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-          __builtin_amdgcn_global_load_lds((const void*)(bsrc + (int64_t)ks * PG_B_BYTES + i * 1024),
-                                           (lds_void_t*)(sb + AB + (3 * wave + i) * 1024), 16, 0, 0);
-      }
-    };
-    issue(0, 0);
-    for (int kt = 0; kt < nk; ++kt) {
-      // this wave's copies of stage kt are done, every wave's after the barrier, which also retires
-      // every read of the buffer stage kt + 1 overwrites (last read in iteration kt - 1)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
-      const char* sb = lds + (kt & 1) * STG;
-      u32x4 fb[4][3];
-#pragma unroll
-      for (int nb = 0; nb < 4; ++nb)
-#pragma unroll
-        for (int q = 0; q < (TERMS == 1 ? 1 : 3); ++q)
-          fb[nb][q] = *reinterpret_cast<const u32x4*>(sb + boff + q * 4096 + nb * 1024);
-#pragma unroll
-      for (int hb = 0; hb < 2; ++hb) {
-        if (!((mask >> hb) & 1)) continue;
-        const int ra = 128 * hb + 32 * wave + li;      // this lane's A row (fragment row li of half hb)
-        f32x4 a0 = *reinterpret_cast<const f32x4*>(sb + ra * 64 + 16 * ((2 * h) ^ ((li >> 2) & 3)));
-        f32x4 a1 = *reinterpret_cast<const f32x4*>(sb + ra * 64 + 16 * ((2 * h + 1) ^ ((li >> 2) & 3)));
-        if (AXT == OT_AX_GELU) {
-          a0.x = gelu_erf(a0.x); a0.y = gelu_erf(a0.y); a0.z = gelu_erf(a0.z); a0.w = gelu_erf(a0.w);
-          a1.x = gelu_erf(a1.x); a1.y = gelu_erf(a1.y); a1.z = gelu_erf(a1.z); a1.w = gelu_erf(a1.w);
-        }
-        const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-        u32x4 fa[3];
-        split8t<TERMS == 1 ? 1 : 6>(av, fa);
-#pragma unroll
-        for (int nb = 0; nb < 4; ++nb) acc[hb][nb] = mfma_terms<TERMS == 1 ? 1 : 6>(fa, fb[nb], acc[hb][nb]);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __syncthreads();                                  // the buffers are reused (next loop / epilogue)
-  };
-  if (g0 == g1) {
-    kloop(bimg_of(g0), 3);
-  } else {
-    kloop(bimg_of(g0), 1);
-    kloop(bimg_of(g1), 2);
-  }
-  gemm_vec_epilogue<EPIT, 1, AXT == OT_AX_RMSNORM, 4>(p, acc[0], smem, tm0, n0, g0);
-  __syncthreads();                                    // the first tile's dgamma partial read its LDS slots last
-  gemm_vec_epilogue<EPIT, 1, AXT == OT_AX_RMSNORM, 4>(p, acc[1], smem, tm0 + 1, n0, g1);
-}
-
 // Pre-split B images (ot_split_images).  desc [nd][10] int64: {src_off, sn, sk, gstride, kscale_off
 // (-1: none), dst_off (ushorts), first_unit, G, N, K}; B[g][n][k] = src[g*gstride + n*sn + k*sk]
 // (* kscale[k]); one unit = one (g, n tile, 16-k stage) block of 3 x 128 x 16 bf16, one thread per
@@ -1432,12 +1312,6 @@ static int g_plane_cfg = [] {
   const char* e = getenv("ONETRANS_PLANE_CFG");
   return e ? atoi(e) : 1;
 }();
-// plane GEMM on 256 x 128 tiles (plane_gemm2_kernel) when the row map has an even tile count
-// (environment ONETRANS_PLANE_256; 0 keeps the 128 x 128 kernel)
-static int g_plane256 = [] {
-  const char* e = getenv("ONETRANS_PLANE_256");
-  return e ? atoi(e) : 1;
-}();
 
 }  // namespace ot
 
@@ -1552,7 +1426,7 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
   const unsigned nwg = (unsigned)ntiles * p.ntn;
   hipStream_t s = (hipStream_t)stream;
   void (*kern)(GemmArgs) = nullptr;
-  bool plane = false, plane2 = false;
+  bool plane = false;
   const int e = epi, x = a_xform;
 #define OT_SPEC(NT_, AX_, EP_)                                                                  \
   if (mode == (NT_ ? OT_GEMM_NT : OT_GEMM_NN) && x == AX_ && e == (EP_))                         \
@@ -1606,37 +1480,11 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
     OT_PSPEC(OT_AX_NONE, OT_EPI_RMSNORM_BWD | OT_EPI_DROPOUT)
 #undef OT_PSPEC
     if (pk) { kern = pk; plane = true; }
-    if (pk && g_plane256 && (p.ntm & 1) == 0) {
-      void (*pk2)(GemmArgs) = nullptr;
-#define OT_P2SPEC(AX_, EP_) \
-      if (x == AX_ && e == (EP_)) pk2 = one ? plane_gemm2_kernel<AX_, EP_, 1> : plane_gemm2_kernel<AX_, EP_, 6>;
-      OT_P2SPEC(OT_AX_RMSNORM, 0)
-      OT_P2SPEC(OT_AX_RMSNORM, OT_EPI_BIAS)
-      OT_P2SPEC(OT_AX_GELU, OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_DROPOUT)
-      OT_P2SPEC(OT_AX_GELU, OT_EPI_BIAS | OT_EPI_RESIDUAL)
-      OT_P2SPEC(OT_AX_GELU, OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_DROPOUT | OT_EPI_ROW_RSTD)
-      OT_P2SPEC(OT_AX_GELU, OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_ROW_RSTD)
-      OT_P2SPEC(OT_AX_NONE, OT_EPI_RESIDUAL | OT_EPI_DROPOUT)
-      OT_P2SPEC(OT_AX_NONE, OT_EPI_RESIDUAL)
-      OT_P2SPEC(OT_AX_NONE, OT_EPI_BIAS)
-      OT_P2SPEC(OT_AX_NONE, OT_EPI_GELU_BWD)
-      OT_P2SPEC(OT_AX_NONE, OT_EPI_GELU_BWD | OT_EPI_ROWDOT)
-      OT_P2SPEC(OT_AX_NONE, 0)
-      OT_P2SPEC(OT_AX_NONE, OT_EPI_ACCUMULATE)
-      OT_P2SPEC(OT_AX_NONE, OT_EPI_RESIDUAL | OT_EPI_DROPOUT | OT_EPI_ROW_RSTD)
-      OT_P2SPEC(OT_AX_NONE, OT_EPI_RESIDUAL | OT_EPI_ROW_RSTD)
-      OT_P2SPEC(OT_AX_NONE, OT_EPI_RMSNORM_BWD)
-      OT_P2SPEC(OT_AX_NONE, OT_EPI_RMSNORM_BWD | OT_EPI_DROPOUT)
-#undef OT_P2SPEC
-      if (pk2) { kern = pk2; plane2 = true; }
-    }
   }
   OT_REQUIRE(!p.rowpart || plane, "ot_mixed_gemm_rms: OT_EPI_ROW_RSTD with N = %d > %d needs the plane GEMM "
              "(split mode, a pre-split B image, 16-B aligned A)", N, GT);
-  const size_t epi_lds = (size_t)(64 * (GT + 4) + 8 * GT) * 4;
   const size_t launch_shmem = !plane ? shmem
-                              : plane2 ? std::max((size_t)2 * (one ? pg2_stage_bytes<1>() : pg2_stage_bytes<6>()), epi_lds)
-                              : one ? std::max((size_t)3 * pg_stage_bytes<1>(), epi_lds)
+                              : one ? std::max((size_t)3 * pg_stage_bytes<1>(), (size_t)(64 * (GT + 4) + 8 * GT) * 4)
                                     : (size_t)(g_plane_cfg == 0 ? 3 : 2) * PG_STG_BYTES;
   OT_REQUIRE(kern || !rms_flags, "ot_mixed_gemm_rms: no specialised kernel for epilogue flags %d", epi);
   if (!kern) {   // any other combination: generic instantiation (run-time prologue/epilogue)
@@ -1660,7 +1508,7 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
       (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     (void)hipGetLastError();
   });
-  hipLaunchKernelGGL(kern, dim3(plane2 ? nwg / 2 : nwg), dim3(256), launch_shmem, s, p);
+  hipLaunchKernelGGL(kern, dim3(nwg), dim3(256), launch_shmem, s, p);
   OT_LAUNCH_CHECK("ot_mixed_gemm");
   if (dgpart) {
     launch_colsum_reduce(dgpart, ntiles, N, rms->dgamma, rms->accumulate_dgamma, s, dgpart + (int64_t)ntiles * N);

@@ -24,9 +24,6 @@ from .config import OneTransConfig
 from .params import dense_param_shapes, keras_variables
 
 TILE = 128
-# weight groups of a row map are padded to whole 256-row tile pairs: the plane GEMM's 256 x 128 tiles
-# (gemm.hip plane_gemm2_kernel) then never straddle two groups
-GROUP_PAD = 2 * TILE
 ALIGN = 64
 IMAGE_UNIT_ELEMS = 3 * TILE * 16      # one (group, column tile, 16-k stage) block of a B image (bf16)
 # wgrad workgroups per launch (chunk sizing), by output tiles per chunk.  Small weights (< 8 tiles:
@@ -155,7 +152,7 @@ class RowMap:
         import torch
         key = (tiles_per_chunk, str(device))
         if key not in self._chunk_cache:
-            padded = [round_up(n, GROUP_PAD) for n in self.group_rows]
+            padded = [round_up(n, TILE) for n in self.group_rows]
             # every nonempty group needs a chunk of its own: on top of them, the budget of one round
             # (with as many groups as budget slots -- C5's 13 groups x 64 output tiles -- a budget of
             # one round would leave the shared group a single chunk, 64 workgroups on 256 CUs)
@@ -190,7 +187,7 @@ class RowMap:
 
 def build_map(per_group: Sequence[Sequence[np.ndarray]], chunk_rows: int = 0) -> RowMap:
     """``per_group[g]`` = list (one per index space) of equal-length int arrays of rows of group g.
-    Each group is padded to a multiple of GROUP_PAD (two tiles); wgrad chunks split each group into runs of
+    Each group is padded to a multiple of TILE; wgrad chunks split each group into runs of
     ``chunk_rows`` (a multiple of TILE; 0 = auto, ~256 chunks overall)."""
     G = len(per_group)
     nspace = len(per_group[0]) if G else 0
@@ -202,7 +199,7 @@ def build_map(per_group: Sequence[Sequence[np.ndarray]], chunk_rows: int = 0) ->
     base = 0
     for g, pg in enumerate(per_group):
         n = len(pg[0])
-        npad = round_up(n, GROUP_PAD)
+        npad = round_up(n, TILE)
         for s in range(nspace):
             r = np.full(npad, -1, dtype=np.int32)
             r[:n] = pg[s]

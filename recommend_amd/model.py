@@ -31,7 +31,7 @@ from ._lib import (OT_AX_GELU, OT_AX_RMSNORM, OT_EPI_ACCUMULATE, OT_EPI_BIAS, OT
                    OT_EPI_RESIDUAL, OT_EPI_RMSNORM_BWD, OT_EPI_ROW_RSTD, OT_EPI_ROWDOT, OT_GEMM_NN, OT_GEMM_NT,
                    NS_FIELD_BYTES)
 from .config import OneTransConfig, check_pyramid_select, get_model_config
-from .layout import GROUP_PAD, TILE, FlatLayout, RowMap, build_map, head_map, identity_map, layer_maps, round_up
+from .layout import TILE, FlatLayout, RowMap, build_map, head_map, identity_map, layer_maps, round_up
 from .params import init_params, ns_table_offsets
 
 RMS_EPS = 1e-6   # RMSNorm eps, model.py:14
@@ -837,7 +837,7 @@ class OneTransModel(nn.Module):
             plan['seq_M'] = cmp_off
             # segment offsets of each present sequence inside the padded map (for ot_seq_rows)
             offs = []
-            starts = np.concatenate([[0], np.cumsum([round_up(len(pg[0]), GROUP_PAD) for pg in per_group])])
+            starts = np.concatenate([[0], np.cumsum([round_up(len(pg[0]), TILE) for pg in per_group])])
             for (i, p0, L) in seq_groups:
                 offs.append(int(starts[i]))
             plan['seq_seg_off'] = offs

@@ -19,3 +19,14 @@ def dev():
     if not torch.cuda.is_available():
         pytest.fail('gpu-marked test run without a ROCm GPU')
     return torch.device('cuda', 0)
+
+
+def release_device_cache():
+    """Return the memory this process's caching allocator holds to the device (multi-rank GPU tests
+    spawn processes that allocate their own full-size tables on the same GPU)."""
+    import gc
+    import torch
+    gc.collect()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()

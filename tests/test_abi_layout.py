@@ -9,7 +9,7 @@ import pytest
 
 from recommend_amd import _lib
 from recommend_amd.config import workload_config
-from recommend_amd.layout import GROUP_PAD, TILE, FlatLayout, build_map, head_map, layer_maps
+from recommend_amd.layout import TILE, FlatLayout, build_map, head_map, layer_maps
 
 
 def _prototypes():
@@ -110,7 +110,7 @@ def test_flat_layout():
 
 def test_head_map():
     m = head_map(300, 2)
-    assert m.ntiles == 2 * 4          # each group padded to whole 256-row tile pairs (layout.GROUP_PAD)
+    assert m.ntiles == 2 * 3
     assert np.array_equal(m.rows[1][m.rows[1] >= 0], np.arange(600))
 
 
@@ -126,7 +126,7 @@ def test_wgrad_chunks_partition_and_budget(name, tiles):
     mp = layer_maps(cfg, B, I, I)['all']
     ch, gc, n = mp.chunks_for(tiles, 'cpu')
     ch, gc = ch.numpy(), gc.numpy()
-    padded = [(r + GROUP_PAD - 1) // GROUP_PAD * GROUP_PAD for r in mp.group_rows]
+    padded = [(r + TILE - 1) // TILE * TILE for r in mp.group_rows]
     groups = sum(1 for p in padded if p > 0)
     assert n == len(ch) and n * tiles <= L.wgrad_slots(tiles) + groups * tiles
     base = 0

@@ -29,6 +29,8 @@ import numpy as np
 import pytest
 import torch
 
+from conftest import release_device_cache
+
 pytestmark = pytest.mark.gpu
 
 from fullsize_common import BATCH_SEED, MODEL_SEED, TABLE_SEED, dropout_seed, fill_table_device, setup_config, \
@@ -225,6 +227,7 @@ def test_fullsize_train_step_c4_row_sharded():
     G = np.load(os.path.join(GOLDEN, 'fullsize_C4.npz'))
     cfg = setup_config('C4')
     world = 2
+    release_device_cache()             # the ranks' tables need the memory this process's allocator still caches
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()

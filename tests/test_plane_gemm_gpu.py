@@ -17,7 +17,7 @@ from recommend_amd import kernels as K
 from recommend_amd._lib import (OT_AX_GELU, OT_AX_NONE, OT_AX_RMSNORM, OT_EPI_ACCUMULATE, OT_EPI_BIAS,
                                 OT_EPI_DROPOUT, OT_EPI_GELU_BWD, OT_EPI_RESIDUAL, OT_EPI_RMSNORM_BWD,
                                 OT_EPI_ROW_RSTD, OT_GEMM_NT)
-from recommend_amd.layout import IMAGE_UNIT_ELEMS, RowMap, build_map
+from recommend_amd.layout import IMAGE_UNIT_ELEMS, build_map
 
 
 MODE = {'m': 'split'}
@@ -92,37 +92,6 @@ def test_plane_gemm_prologues(dev, K_, N, tn0, ncols, xf):
     torch.cuda.synchronize()
     assert not torch.isnan(outs[1]).any()
     close(outs[1], outs[0], K_)
-
-
-def test_plane_gemm_tile_pairs_of_two_groups(dev):
-    """The 256-row plane GEMM (two consecutive 128-row tiles per workgroup) on a row map whose tile pairs
-    mix weight groups (build_map pads groups to whole pairs; a hand-built map need not): such a pair runs
-    its k-loop once per half with each half's B image.  Odd tile counts take the 128-row kernel."""
-    rng = np.random.default_rng(11)
-    K_, N, G = 256, 256, 3
-    for groups in ([0, 1, 1, 2, 0, 2], [2, 2, 0, 1, 1]):
-        nt = len(groups)
-        M = nt * 128 - 37
-        src = np.full(nt * 128, -1, np.int32)
-        dst = np.full(nt * 128, -1, np.int32)
-        keep = rng.permutation(nt * 128)[:M]
-        src[keep] = rng.permutation(M)
-        dst[keep] = rng.permutation(M)
-        rm = RowMap([src, dst], np.array(groups, np.int32), np.zeros((0, 3), np.int32), np.zeros((G, 2), np.int32), M)
-        d = rm.to(dev)
-        A = torch.randn(M, K_, device=dev)
-        W = torch.randn(G, N, K_) / math.sqrt(K_)
-        bias = torch.randn(G, N, device=dev)
-        img, ntn = make_image(W, dev)
-        outs = []
-        for b in (None, (img, ntn, 0)):
-            C = torch.full((M, N), float('nan'), device=dev)
-            K.gemm(OT_GEMM_NT, A, K_, K_, d['rows'][0], W.to(dev), N * K_, K_, N, d['tile_group'], nt, C, N,
-                   d['rows'][1], bias=bias, bias_gstride=N, epi=OT_EPI_BIAS, bimg=b)
-            outs.append(C)
-        torch.cuda.synchronize()
-        assert not torch.isnan(outs[1]).any()
-        close(outs[1], outs[0], K_)
 
 
 @pytest.mark.parametrize('case', ['res_drop', 'res', 'res_rstd', 'res_drop_rstd', 'gelu_bias_res_drop',

@@ -19,6 +19,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+from conftest import release_device_cache
+
 pytestmark = pytest.mark.gpu
 
 
@@ -143,6 +145,7 @@ def test_row_sharded_table_two_ranks(sharding):
     """'row': the item table row-sharded over the ranks; 'none': replicated, exchanged as a dense
     all-reduced gradient ('none-compact': only the rows some rank touched are all-reduced).  Either way three DP steps equal the oracle's full-batch steps (and the
     dense gradients are all-reduced per block during the backward)."""
+    release_device_cache()             # the ranks' tables need the memory this process's allocator still caches
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()

@@ -47,6 +47,8 @@ extern "C" {
 #define OT_AX_NONE 0
 #define OT_AX_RMSNORM 1 /* a * rstd[in_row] * gamma[k]  (RMSNorm fused into the consumer GEMM) */
 #define OT_AX_GELU 2    /* gelu_erf(a)                   (FFN hidden recomputed from its pre-activation) */
+#define OT_AX_BF16 4    /* ot_mixed_gemm_wgrad only: A holds bf16 values (uint16 bits, lda in elements), used
+                           as they are (OT_MATMUL_BF16 / split modes; the stored GELU of ot_rms_epilogue) */
 
 /* GEMM epilogue flags (applied in this order) */
 #define OT_EPI_BIAS 1        /* + bias[g][n] */
@@ -120,6 +122,10 @@ typedef struct ot_rms_epilogue {
   float* rowdot; int rowdot_n;                         /* OT_EPI_ROWDOT: output partials [out rows][rowdot_n];
                                                           OT_EPI_RMSNORM_BWD with N > 128: their input (the row
                                                           dot = sum_j rowdot[out_row][j] / rstd) */
+  uint16_t* gelu_out; int64_t ldgelu;                  /* with OT_EPI_GELU_BWD (optional): also gelu_erf(aux)
+                                                          rounded to bf16 at [out_row][n] — the FFN2 weight
+                                                          gradient's A operand in the bf16 mode (OT_AX_BF16),
+                                                          so that GEMM neither re-reads f32 U nor re-evaluates erf */
 } ot_rms_epilogue;
 size_t ot_mixed_gemm_rms_workspace_size(int ntiles, int N);
 int ot_mixed_gemm_rms(int mode, const float* A, int64_t lda, int K, const int32_t* in_rows,

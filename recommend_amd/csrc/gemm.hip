@@ -89,6 +89,7 @@ struct GemmArgs {
   float* dxm; int64_t lddxm; float* dgpart;
   float* rowpart;                               // OT_EPI_ROW_RSTD with N > GT: [ntm*GT][ntn] row sums of squares
   float* rowdot; int rowdot_n;                  // OT_EPI_ROWDOT output / OT_EPI_RMSNORM_BWD (N > GT) input
+  uint16_t* gelu_out; int64_t ldgelu;           // with OT_EPI_GELU_BWD: bf16 gelu_erf(aux) (optional)
   const int32_t* tail_pos;                      // kept positions (ot_pyramid_select) or null (tail)
   // plane GEMM: pre-split B image (ot_split_images), its tiles per group and the first tile used
   const uint16_t* bimg; int bimg_ntn, bimg_tn0;
@@ -227,6 +228,10 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
           if (epi & OT_EPI_GELU_BWD) {
             v.x *= gelu_erf_grad(aux4[i].x); v.y *= gelu_erf_grad(aux4[i].y);
             v.z *= gelu_erf_grad(aux4[i].z); v.w *= gelu_erf_grad(aux4[i].w);
+            if (p.gelu_out && orr >= 0) {                      // the stored GELU (W2 weight gradient's A)
+              const f32x4 hv = {gelu_erf(aux4[i].x), gelu_erf(aux4[i].y), gelu_erf(aux4[i].z), gelu_erf(aux4[i].w)};
+              *reinterpret_cast<u32x2*>(p.gelu_out + (int64_t)orr * p.ldgelu + col) = bf16_rne4(hv);
+            }
             if (ROWDOT) {                                      // this tile's part of sum_f dU_f (U_f - b_f)
               const f32x4 ub = aux4[i] - rdb4;
               const float sd = row32_sum(v.x * ub.x + v.y * ub.y + v.z * ub.z + v.w * ub.w);
@@ -1077,13 +1082,20 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(WgradArgs p) {
     for (int j = 0; j < RS; ++j) {
       inr[j] = st * BR + sr + WBR * j < row_count && ar[j] >= 0 && dr[j] >= 0;
       const float* pa = p.A + (int64_t)(inr[j] ? ar[j] : 0) * p.lda;
+      const uint16_t* pa16 = reinterpret_cast<const uint16_t*>(p.A) + (int64_t)(inr[j] ? ar[j] : 0) * p.lda;
       const float* pd = p.D + (int64_t)(inr[j] ? dr[j] : 0) * p.ldd;
       rsd[j] = ax == OT_AX_RMSNORM ? p.a_rstd[inr[j] ? ar[j] : 0] : 1.f;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int k = k0 + 4 * (sc + 8 * i), n = n0 + 4 * (sc + 8 * i);
         const int kc = k < p.K ? k : 0, nc = n < p.N ? n : 0;
-        va[j][i] = *reinterpret_cast<const f32x4*>(pa + kc);
+        if (AXT == OT_AX_BF16) {                       // bf16 values: exact in f32 (and in the planes)
+          const u32x2 w = *reinterpret_cast<const u32x2*>(pa16 + kc);
+          va[j][i] = f32x4{__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u),
+                           __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u)};
+        } else {
+          va[j][i] = *reinterpret_cast<const f32x4*>(pa + kc);
+        }
         vd[j][i] = *reinterpret_cast<const f32x4*>(pd + nc);
       }
     }
@@ -1360,6 +1372,11 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
   OT_REQUIRE(!(epi & OT_EPI_RESIDUAL) || res, "ot_mixed_gemm: residual missing");
   OT_REQUIRE(!(epi & OT_EPI_GELU_BWD) || aux, "ot_mixed_gemm: aux missing");
   OT_REQUIRE(a_xform != OT_AX_RMSNORM || (a_rstd && a_gamma), "ot_mixed_gemm: rmsnorm prologue needs rstd/gamma");
+  OT_REQUIRE(a_xform == OT_AX_NONE || a_xform == OT_AX_RMSNORM || a_xform == OT_AX_GELU,
+             "ot_mixed_gemm: a_xform %d (OT_AX_BF16 is a weight-gradient operand form)", a_xform);
+  OT_REQUIRE(!rms || !rms->gelu_out || ((epi & OT_EPI_GELU_BWD) && rms->ldgelu % 4 == 0 &&
+                                        ((uintptr_t)rms->gelu_out % 8) == 0),
+             "ot_mixed_gemm_rms: gelu_out needs OT_EPI_GELU_BWD, ldgelu %% 4 == 0 and 8-B alignment");
   OT_REQUIRE(!((epi & OT_EPI_DROPOUT) || res_tok) || (tail_K > 0 && tail_I >= tail_K), "ot_mixed_gemm: bad tail map");
   if (rms_flags) {
     OT_REQUIRE(mode == OT_GEMM_NT && N % GT == 0 &&
@@ -1391,6 +1408,10 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
   p.tail_pos = tail_pos;
   p.bimg = bimg; p.bimg_ntn = bimg_ntn; p.bimg_tn0 = bimg_tn0;
   float* dgpart = nullptr;
+  if (rms && (epi & OT_EPI_GELU_BWD)) {                // the stored GELU (optional)
+    p.gelu_out = rms->gelu_out;
+    p.ldgelu = rms->ldgelu;
+  }
   if (rms_flags) {
     p.rstd_out = rms->rstd_out; p.eps = rms->eps;
     p.nx = rms->x; p.ldnx = rms->ldx; p.ngamma = rms->gamma; p.nrstd = rms->rstd;
@@ -1630,8 +1651,12 @@ extern "C" int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a
                 (int)ceil_div(K, GT), (int)ceil_div(N, GT)};
     const size_t shmem = (OT_WGRAD_DBUF ? 4 : 2) * WBR * WLD * sizeof(float);
     const bool split = g_matmul_mode != OT_MATMUL_F32;
+    OT_REQUIRE(a_xform != OT_AX_BF16 || (g_matmul_mode != OT_MATMUL_F32 && lda % 4 == 0 && ((uintptr_t)A % 8) == 0),
+               "ot_mixed_gemm_wgrad: OT_AX_BF16 needs the split / bf16 mode and 8-B aligned rows");
     void (*kern)(WgradArgs) =
-        g_matmul_mode == OT_MATMUL_BF16
+        a_xform == OT_AX_BF16 ? (g_matmul_mode == OT_MATMUL_BF16 ? wgrad_split_kernel<OT_AX_BF16, 1>
+                                                                : wgrad_split_kernel<OT_AX_BF16, SPLIT_TERMS>)
+        : g_matmul_mode == OT_MATMUL_BF16
             ? (a_xform == OT_AX_NONE      ? wgrad_split_kernel<OT_AX_NONE, 1>
                : a_xform == OT_AX_RMSNORM ? wgrad_split_kernel<OT_AX_RMSNORM, 1>
                : a_xform == OT_AX_GELU    ? wgrad_split_kernel<OT_AX_GELU, 1>

@@ -172,17 +172,20 @@ def gemm_rms(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish,
              ngamma: Ptrish = None, nrstd: Ptrish = None, dres: Ptrish = None, lddres: int = 0,
              dres_tail: Tuple[int, int] = (0, 0), dx_masked: Ptrish = None, lddxm: int = 0,
              dgamma: Ptrish = None, accumulate_dgamma: bool = False, device=None, bimg=None,
-             aux: Ptrish = None, ldaux: int = 0, rowdot: Ptrish = None, rowdot_n: int = 0) -> None:
+             aux: Ptrish = None, ldaux: int = 0, rowdot: Ptrish = None, rowdot_n: int = 0,
+             gelu_out: Ptrish = None, ldgelu: int = 0) -> None:
     """ot_mixed_gemm_rms: the GEMM with a row-norm epilogue (OT_EPI_ROW_RSTD: emit the next RMSNorm's
     rstd; OT_EPI_RMSNORM_BWD: apply the RMSNorm backward to the product, + dres, dgamma, taking
     <gamma dy, x> from ``rowdot`` when N > 128; OT_EPI_GELU_BWD | OT_EPI_ROWDOT: also write each 128-column
-    tile's sum of dU (aux - bias) into rowdot[row][tile])."""
+    tile's sum of dU (aux - bias) into rowdot[row][tile]); with OT_EPI_GELU_BWD and ``gelu_out`` (bf16 bits,
+    [rows][ldgelu]) also gelu(aux) rounded to bf16 (the W2 weight gradient's OT_AX_BF16 operand)."""
     need_ws = dgamma is not None or (rstd_out is not None and N > 128)     # dgamma / row-sum partials
     ws = workspace(size('ot_mixed_gemm_rms_workspace_size', ntiles, N) if need_ws else 16,
                    device if device is not None else (C[0] if isinstance(C, tuple) else C).device)
     e = _lib.RmsEpilogue(ptr(rstd_out), float(eps), ptr(nx), ldnx, ptr(ngamma), ptr(nrstd), ptr(dres), lddres,
                          dres_tail[0], dres_tail[1], _sel(dres_tail), ptr(dx_masked), lddxm, ptr(dgamma),
-                         int(accumulate_dgamma), ptr(ws), ws.numel(), ptr(rowdot), int(rowdot_n))
+                         int(accumulate_dgamma), ptr(ws), ws.numel(), ptr(rowdot), int(rowdot_n),
+                         ptr(gelu_out), int(ldgelu))
     ev = _probe.begin() if _probe is not None else None
     args = (mode, ptr(A), lda, K, ptr(in_rows), a_xform, ptr(rstd), ptr(gamma), ptr(W),
             w_gstride, ldw, N, ptr(tile_group), ntiles, ptr(bias), bias_gstride, ptr(C), ldc, ptr(out_rows), epi,
@@ -196,7 +199,7 @@ def gemm_rms(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish,
         M = m_rows or ntiles * 128
         extra = (nx is not None) + (dres is not None) + (dx_masked is not None)   # norm-backward operands
         _probe.end('mixed_gemm', 2.0 * M * K * N, ev, f'gemm_rms mode{mode} ax{a_xform} epi{epi} M{M} K{K} N{N}',
-                   gemm_bytes(M, K, N, a_xform, epi) + 4.0 * M * N * extra
+                   gemm_bytes(M, K, N, a_xform, epi) + 4.0 * M * N * extra + 2.0 * M * N * (gelu_out is not None)
                    + 4.0 * M * ((rstd_out is not None) + (nrstd is not None)))
 
 
@@ -218,7 +221,8 @@ def wgrad(A: Ptrish, lda: int, a_rows: Ptrish, D: Ptrish, ldd: int, d_rows: Ptri
          dw_gstride, ptr(db), db_gstride, int(accumulate), ptr(ws), ws.numel(), stream())
     if ev is not None:
         _probe.end('mixed_gemm', 2.0 * m_rows * K * N, ev, f'wgrad ax{a_xform} M{m_rows} K{K} N{N} ch{nchunks}',
-                   4.0 * m_rows * (K + N + (a_xform == _lib.OT_AX_RMSNORM)) + 4.0 * ngroups * K * N)
+                   (2.0 if a_xform == _lib.OT_AX_BF16 else 4.0) * m_rows * K
+                   + 4.0 * m_rows * (N + (a_xform == _lib.OT_AX_RMSNORM)) + 4.0 * ngroups * K * N)
 
 
 def transpose_banks(src, dst, banks_dev, nbanks, total_tiles) -> None:

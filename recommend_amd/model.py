@@ -27,7 +27,7 @@ import torch.nn as nn
 
 from . import _lib
 from . import kernels as K
-from ._lib import (OT_AX_GELU, OT_AX_RMSNORM, OT_EPI_ACCUMULATE, OT_EPI_BIAS, OT_EPI_DROPOUT, OT_EPI_GELU_BWD,
+from ._lib import (OT_AX_BF16, OT_AX_GELU, OT_AX_RMSNORM, OT_EPI_ACCUMULATE, OT_EPI_BIAS, OT_EPI_DROPOUT, OT_EPI_GELU_BWD,
                    OT_EPI_RESIDUAL, OT_EPI_RMSNORM_BWD, OT_EPI_ROW_RSTD, OT_EPI_ROWDOT, OT_GEMM_NN, OT_GEMM_NT,
                    NS_FIELD_BYTES)
 from .config import OneTransConfig, check_pyramid_select, get_model_config
@@ -296,20 +296,32 @@ class _Block(torch.autograd.Function):
             K.dropout_apply(dx2, d, dy2, d, B * Kq, d, seed, 2 * l + 1, rate, tail)
         else:
             dy2 = dx2
-        side = m.side(u, dy2)          # weight gradients overlap the dgrad chain on a second stream
-        with side:
-            K.wgrad(u, f, mt['rows'][1], dy2, d, mt['rows'][1], f, d, mt, nct, G, m.g(f'blk.{l}.w2'), f * d,
-                    m.g(f'blk.{l}.b2'), d, a_xform=OT_AX_GELU, accumulate=acc, device=dev,
-                    m_rows=maps['tail'].nrows, rowmap=maps['tail'])
         du = torch.empty(B * Kq, f, device=dev)
         rowdot = None
-        if m.fuse_bwd2 and not m.fuse_bwd and f % TILE == 0:
+        fused2 = m.fuse_bwd2 and not m.fuse_bwd and f % TILE == 0
+        # bf16 mode with the fused norm2 backward (C5): the FFN2 dgrad epilogue, which reads U for GELU'
+        # anyway, also stores gelu(U) in bf16 — the W2 weight gradient then reads 2 B per element instead of
+        # U's 4 and evaluates no erf (it did, once per output column tile: 4x at f = 2048, d = 512)
+        hbf = (torch.empty(B * Kq, f, dtype=torch.int16, device=dev)
+               if fused2 and m.store_gelu and K.matmul_mode() == 'bf16' else None)
+        if hbf is None:
+            with m.side(u, dy2):       # weight gradients overlap the dgrad chain on a second stream
+                K.wgrad(u, f, mt['rows'][1], dy2, d, mt['rows'][1], f, d, mt, nct, G, m.g(f'blk.{l}.w2'), f * d,
+                        m.g(f'blk.{l}.b2'), d, a_xform=OT_AX_GELU, accumulate=acc, device=dev,
+                        m_rows=maps['tail'].nrows, rowmap=maps['tail'])
+        if fused2:
             # d > 128: the FFN2 dgrad also emits rowdot[row][f-tile] = sum dU (U - b1) for the norm2 backward
             rowdot = torch.empty(B * Kq, f // TILE, device=dev)
             K.gemm_rms(OT_GEMM_NT, dy2, d, d, mt['rows'][1], m.p(f'blk.{l}.w2'), f * d, d, f, mt['tile_group'], nt,
                        du, f, mt['rows'][1], epi=OT_EPI_GELU_BWD | OT_EPI_ROWDOT, aux=u, ldaux=f,
                        bias=m.p(f'blk.{l}.b1'), bias_gstride=f, rowdot=rowdot, rowdot_n=f // TILE,
-                       m_rows=maps['tail'].nrows, device=dev, bimg=m.bimg(f'blk.{l}.w2', 'dgrad'))
+                       m_rows=maps['tail'].nrows, device=dev, bimg=m.bimg(f'blk.{l}.w2', 'dgrad'),
+                       gelu_out=hbf, ldgelu=f)
+            if hbf is not None:
+                with m.side(hbf, dy2):
+                    K.wgrad(hbf, f, mt['rows'][1], dy2, d, mt['rows'][1], f, d, mt, nct, G, m.g(f'blk.{l}.w2'),
+                            f * d, m.g(f'blk.{l}.b2'), d, a_xform=OT_AX_BF16, accumulate=acc, device=dev,
+                            m_rows=maps['tail'].nrows, rowmap=maps['tail'])
         else:
             K.gemm(OT_GEMM_NT, dy2, d, d, mt['rows'][1], m.p(f'blk.{l}.w2'), f * d, d, f, mt['tile_group'], nt, du,
                    f, mt['rows'][1], epi=OT_EPI_GELU_BWD, aux=u, ldaux=f, m_rows=maps['tail'].nrows,
@@ -549,6 +561,9 @@ class OneTransModel(nn.Module):
         self.fuse_norms = (config.hidden_dim % TILE == 0 and os.environ.get('ONETRANS_FUSE_NORMS', '1') != '0')
         self.fuse_bwd = self.fuse_norms and config.hidden_dim == TILE
         self.fuse_bwd2 = self.fuse_norms and os.environ.get('ONETRANS_FUSE_NORM2_BWD', '1') != '0'
+        # bf16 mode: the FFN2 dgrad stores gelu(U) in bf16 for the W2 weight gradient (ONETRANS_STORE_GELU=0:
+        # that GEMM recomputes GELU from f32 U)
+        self.store_gelu = os.environ.get('ONETRANS_STORE_GELU', '1') != '0'
         # block weight gradients run on a second stream, overlapping the dgrad chain
         self.overlap_wgrad = os.environ.get('ONETRANS_OVERLAP_WGRAD', '1') != '0'
         self._side = None

@@ -673,3 +673,48 @@ def test_attn_bwd_key_slices(dev, B, H, I, Kq, hd):
         assert torch.isfinite(a).all()
     finally:
         K.set_matmul_mode(old)
+
+
+@pytest.mark.parametrize('mode', ['bf16', 'split'])
+def test_stored_gelu_weight_gradient(dev, mode):
+    """The FFN2 dgrad epilogue's stored GELU (ot_rms_epilogue.gelu_out: bf16 gelu(U)) and the W2 weight
+    gradient that reads it (OT_AX_BF16): the stored values equal gelu(U) rounded to bf16 (torch, float64
+    erf; at most one bf16 ulp apart from the device erf), and in the bf16 mode the weight gradient from the
+    stored operand is bit-identical to the one that recomputes GELU from f32 U (OT_AX_GELU: the same
+    rounding of the same values)."""
+    from recommend_amd import layout
+    from recommend_amd._lib import OT_AX_BF16
+    rng = np.random.default_rng(3)
+    G, M, d, f = 2, 1000, 128, 256
+    cuts = [0, 430, M]
+    perm = rng.permutation(M)
+    rm = layout.build_map([[perm[cuts[g]:cuts[g + 1]], perm[cuts[g]:cuts[g + 1]]] for g in range(G)])
+    dm = rm.to(dev)
+    g = torch.Generator().manual_seed(5)
+    U = torch.randn(M, f, generator=g).to(dev)
+    dy = torch.randn(M, d, generator=g).to(dev)
+    W2 = (torch.randn(G, f, d, generator=g) * 0.05).to(dev)
+    old = K.set_matmul_mode(mode)
+    try:
+        du = torch.empty(M, f, device=dev)
+        h = torch.zeros(M, f, dtype=torch.int16, device=dev)
+        K.gemm_rms(OT_GEMM_NT, dy, d, d, dm['rows'][1], W2, f * d, d, f, dm['tile_group'], rm.ntiles, du, f,
+                   dm['rows'][1], epi=OT_EPI_GELU_BWD, aux=U, ldaux=f, gelu_out=h, ldgelu=f, device=dev)
+        dW = [torch.empty(G, f, d, device=dev) for _ in range(2)]
+        db = [torch.empty(G, d, device=dev) for _ in range(2)]
+        for i, (A, ax) in enumerate(((U, OT_AX_GELU), (h, OT_AX_BF16))):
+            K.wgrad(A, f, dm['rows'][1], dy, d, dm['rows'][1], f, d, dm, rm.chunks.shape[0], G, dW[i], f * d,
+                    db[i], d, a_xform=ax, device=dev, m_rows=M, rowmap=rm)
+        torch.cuda.synchronize()
+    finally:
+        K.set_matmul_mode(old)
+    ref = (0.5 * U.double() * (1 + torch.erf(U.double() / math.sqrt(2)))).float().to(torch.bfloat16)
+    got = h.view(torch.bfloat16).cpu()
+    diff = (got.float() - ref.cpu().float()).abs()
+    ulp = ref.cpu().float().abs() * 2 ** -7 + 1e-30
+    assert (diff <= ulp).all(), float((diff / ulp).max())
+    if mode == 'bf16':
+        assert torch.equal(dW[0], dW[1]) and torch.equal(db[0], db[1])
+    else:                       # split: the stored operand is bf16 (8 bits), the recomputed one f32-exact
+        scale = dW[0].abs().max().item()
+        assert (dW[0] - dW[1]).abs().max().item() < 2e-2 * scale

@@ -47,8 +47,11 @@ extern "C" {
 #define OT_AX_NONE 0
 #define OT_AX_RMSNORM 1 /* a * rstd[in_row] * gamma[k]  (RMSNorm fused into the consumer GEMM) */
 #define OT_AX_GELU 2    /* gelu_erf(a)                   (FFN hidden recomputed from its pre-activation) */
-#define OT_AX_BF16 4    /* ot_mixed_gemm_wgrad only: A holds bf16 values (uint16 bits, lda in elements), used
-                           as they are (OT_MATMUL_BF16 / split modes; the stored GELU of ot_rms_epilogue) */
+#define OT_AX_BF16 4    /* A holds bf16 values (uint16 bits, lda in elements), used as they are (the stored
+                           GELU of ot_rms_epilogue.gelu_out).  ot_mixed_gemm_wgrad: OT_MATMUL_BF16 / split
+                           modes; forward GEMMs: OT_MATMUL_BF16, NT mode, a B image (the plane GEMM), lda % 8
+                           == 0, 16-B aligned A, epilogue OT_EPI_BIAS | OT_EPI_RESIDUAL [| OT_EPI_DROPOUT]
+                           [| OT_EPI_ROW_RSTD] (the FFN2 GEMM) */
 
 /* GEMM epilogue flags (applied in this order) */
 #define OT_EPI_BIAS 1        /* + bias[g][n] */
@@ -122,10 +125,12 @@ typedef struct ot_rms_epilogue {
   float* rowdot; int rowdot_n;                         /* OT_EPI_ROWDOT: output partials [out rows][rowdot_n];
                                                           OT_EPI_RMSNORM_BWD with N > 128: their input (the row
                                                           dot = sum_j rowdot[out_row][j] / rstd) */
-  uint16_t* gelu_out; int64_t ldgelu;                  /* with OT_EPI_GELU_BWD (optional): also gelu_erf(aux)
-                                                          rounded to bf16 at [out_row][n] — the FFN2 weight
-                                                          gradient's A operand in the bf16 mode (OT_AX_BF16),
-                                                          so that GEMM neither re-reads f32 U nor re-evaluates erf */
+  uint16_t* gelu_out; int64_t ldgelu;                  /* optional, whole tiles: also gelu_erf(aux) (with
+                                                          OT_EPI_GELU_BWD) or gelu_erf(C) (epi == OT_EPI_BIAS: the
+                                                          FFN1 forward, C = U) rounded to bf16 at [out_row][n] —
+                                                          the FFN2 GEMM's and its weight gradient's A operand in
+                                                          the bf16 mode (OT_AX_BF16): they neither read f32 U nor
+                                                          re-evaluate erf.  No other row-norm field is needed */
 } ot_rms_epilogue;
 size_t ot_mixed_gemm_rms_workspace_size(int ntiles, int N);
 int ot_mixed_gemm_rms(int mode, const float* A, int64_t lda, int K, const int32_t* in_rows,

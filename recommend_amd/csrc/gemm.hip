@@ -89,7 +89,8 @@ struct GemmArgs {
   float* dxm; int64_t lddxm; float* dgpart;
   float* rowpart;                               // OT_EPI_ROW_RSTD with N > GT: [ntm*GT][ntn] row sums of squares
   float* rowdot; int rowdot_n;                  // OT_EPI_ROWDOT output / OT_EPI_RMSNORM_BWD (N > GT) input
-  uint16_t* gelu_out; int64_t ldgelu;           // with OT_EPI_GELU_BWD: bf16 gelu_erf(aux) (optional)
+  uint16_t* gelu_out; int64_t ldgelu;           // bf16 gelu_erf(aux) with OT_EPI_GELU_BWD, bf16 gelu_erf(C) with
+                                                // epi == OT_EPI_BIAS (optional)
   const int32_t* tail_pos;                      // kept positions (ot_pyramid_select) or null (tail)
   // plane GEMM: pre-split B image (ot_split_images), its tiles per group and the first tile used
   const uint16_t* bimg; int bimg_ntn, bimg_tn0;
@@ -155,6 +156,7 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
     constexpr bool RMSBWD = EPIT >= 0 && (EPIT & OT_EPI_RMSNORM_BWD);
     constexpr bool ROWRSTD = EPIT >= 0 && (EPIT & OT_EPI_ROW_RSTD);
     constexpr bool ROWDOT = EPIT >= 0 && (EPIT & OT_EPI_ROWDOT);
+    constexpr bool GSTORE = EPIT == OT_EPI_BIAS;        // gelu_out of a bias-only epilogue: gelu(C)
     f32x4 rdb4 = {0.f, 0.f, 0.f, 0.f};                 // OT_EPI_ROWDOT: the bias subtracted from aux
     if (ROWDOT) rdb4 = *reinterpret_cast<const f32x4*>(p.bias + (int64_t)g * p.bias_gstride + col);
     // dgamma partials live in a thread-private LDS slot behind ct (a register accumulator here
@@ -292,6 +294,10 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
             } else if (orr >= 0 && c4 == 0) {
               p.rstd_out[orr] = rsqrtf(ss / (float)p.N + p.eps);
             }
+          }
+          if (GSTORE && p.gelu_out && orr >= 0) {              // FFN1 forward: also gelu(U) in bf16
+            const f32x4 hv = {gelu_erf(v.x), gelu_erf(v.y), gelu_erf(v.z), gelu_erf(v.w)};
+            *reinterpret_cast<u32x2*>(p.gelu_out + (int64_t)orr * p.ldgelu + col) = bf16_rne4(hv);
           }
           if (orr >= 0) store_out4(p.C + (int64_t)orr * p.ldc + col, v);
         }
@@ -700,6 +706,10 @@ template <int AXT, int EPIT, int NSTG, int MINW, int TERMS = 6>
 __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
   static_assert(NSTG == 2 || NSTG == 3, "plane GEMM stages");
   static_assert(TERMS == 6 || TERMS == 1, "plane GEMM terms");
+  // OT_AX_BF16: A holds bf16 values (the FFN1 epilogue's stored gelu(U)): 32 B per row and stage, the
+  // lane's fragment is one 16-B LDS read, no conversion (bf16 mode only)
+  constexpr bool ABF = AXT == OT_AX_BF16;
+  static_assert(!ABF || TERMS == 1, "bf16 A operands go with OT_MATMUL_BF16");
   constexpr int STG = pg_stage_bytes<TERMS>();
   extern __shared__ __attribute__((aligned(16))) float smem[];
   char* lds = reinterpret_cast<char*>(smem);
@@ -725,6 +735,16 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
     const int lc = (lane & 3) ^ ((r >> 2) & 3);
     asrc[i] = p.A + (int64_t)ir * p.lda + 4 * lc;
   }
+  // bf16 A: one instruction per wave = rows 32w .. +31, lane j -> row + j/2, physical 16-B half j%2 =
+  // logical half (j%2) ^ ((row >> 3) & 1) (rows li and li + 8 of a fragment read then hit other banks)
+  const char* asrcb;
+  {
+    const int r = 32 * wave + (lane >> 1);
+    const int64_t gr = (int64_t)tm * GT + r;
+    int ir = p.in_rows ? p.in_rows[gr] : (int)gr;
+    ir = ir < 0 ? 0 : ir;
+    asrcb = reinterpret_cast<const char*>(p.A) + ((int64_t)ir * p.lda + 8 * ((lane & 1) ^ ((r >> 3) & 1))) * 2;
+  }
   // B: the (g, tile) image is nk consecutive 12-KiB stage blocks; wave w copies KiB 3w .. 3w+2 (a
   // weight shared by every group, w_gstride 0 like Wo, has one group's image)
   const int gb = p.w_gstride ? g : 0;
@@ -734,10 +754,14 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
 
   auto issue = [&](int ks, int buf) {
     char* sb = lds + buf * STG;
+    if (ABF) {
+      __builtin_amdgcn_global_load_lds((const void*)(asrcb + 32 * ks), (lds_void_t*)(sb + wave * 1024), 16, 0, 0);
+    } else {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + 16 * ks), (lds_void_t*)(sb + (2 * wave + i) * 1024),
-                                       16, 0, 0);
+      for (int i = 0; i < 2; ++i)
+        __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + 16 * ks), (lds_void_t*)(sb + (2 * wave + i) * 1024),
+                                         16, 0, 0);
+    }
     if (TERMS == 1) {                                 // plane 0 only: wave w copies its KiB w
       __builtin_amdgcn_global_load_lds((const void*)(bsrc1 + (int64_t)ks * PG_B_BYTES),
                                        (lds_void_t*)(sb + PG_A_BYTES + wave * 1024), 16, 0, 0);
@@ -759,6 +783,7 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
   const int aoff0 = ra * 64 + 16 * ((2 * h) ^ ((li >> 2) & 3));
   const int aoff1 = ra * 64 + 16 * ((2 * h + 1) ^ ((li >> 2) & 3));
   const int boff = PG_A_BYTES + li * 32 + 16 * (h ^ ((li >> 3) & 1));
+  const int aoffb = ra * 32 + 16 * (h ^ ((li >> 3) & 1));  // bf16 A
 
   issue(0, 0);
   if (NSTG == 3 && nk > 1) issue(1, 1);
@@ -767,7 +792,8 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
     // still fly), every wave's after the barrier; the barrier also retires every read of the buffer
     // that the copies of stage kt+NSTG-1 then overwrite (last read in iteration kt-1)
     if (NSTG == 3 && kt + 1 < nk) {
-      if (TERMS == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      if (ABF) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else if (TERMS == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -777,14 +803,21 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
     asm volatile("" ::: "memory");
     if (kt + NSTG - 1 < nk) issue(kt + NSTG - 1, (kt + NSTG - 1) % NSTG);
     const char* sb = lds + (kt % NSTG) * STG;
-    f32x4 a0 = *reinterpret_cast<const f32x4*>(sb + aoff0);
-    f32x4 a1 = *reinterpret_cast<const f32x4*>(sb + aoff1);
     u32x4 fb[4][3];
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb)
 #pragma unroll
       for (int q = 0; q < (TERMS == 1 ? 1 : 3); ++q)
         fb[nb][q] = *reinterpret_cast<const u32x4*>(sb + boff + q * 4096 + nb * 1024);
+    if constexpr (ABF) {
+      u32x4 fa[3];
+      fa[0] = *reinterpret_cast<const u32x4*>(sb + aoffb);
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) acc[nb] = mfma_bf16(fa[0], fb[nb][0], acc[nb]);
+      continue;
+    }
+    f32x4 a0 = *reinterpret_cast<const f32x4*>(sb + aoff0);
+    f32x4 a1 = *reinterpret_cast<const f32x4*>(sb + aoff1);
     if (AXT == OT_AX_GELU) {
       a0.x = gelu_erf(a0.x); a0.y = gelu_erf(a0.y); a0.z = gelu_erf(a0.z); a0.w = gelu_erf(a0.w);
       a1.x = gelu_erf(a1.x); a1.y = gelu_erf(a1.y); a1.z = gelu_erf(a1.z); a1.w = gelu_erf(a1.w);
@@ -1372,11 +1405,16 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
   OT_REQUIRE(!(epi & OT_EPI_RESIDUAL) || res, "ot_mixed_gemm: residual missing");
   OT_REQUIRE(!(epi & OT_EPI_GELU_BWD) || aux, "ot_mixed_gemm: aux missing");
   OT_REQUIRE(a_xform != OT_AX_RMSNORM || (a_rstd && a_gamma), "ot_mixed_gemm: rmsnorm prologue needs rstd/gamma");
-  OT_REQUIRE(a_xform == OT_AX_NONE || a_xform == OT_AX_RMSNORM || a_xform == OT_AX_GELU,
-             "ot_mixed_gemm: a_xform %d (OT_AX_BF16 is a weight-gradient operand form)", a_xform);
-  OT_REQUIRE(!rms || !rms->gelu_out || ((epi & OT_EPI_GELU_BWD) && rms->ldgelu % 4 == 0 &&
+  OT_REQUIRE(a_xform == OT_AX_NONE || a_xform == OT_AX_RMSNORM || a_xform == OT_AX_GELU || a_xform == OT_AX_BF16,
+             "ot_mixed_gemm: bad a_xform %d", a_xform);
+  OT_REQUIRE(a_xform != OT_AX_BF16 || (g_matmul_mode == OT_MATMUL_BF16 && bimg && mode == OT_GEMM_NT &&
+                                       lda % 8 == 0 && ((uintptr_t)A % 16) == 0),
+             "ot_mixed_gemm: OT_AX_BF16 (bf16 A) needs the bf16 mode, a B image (plane GEMM), NT mode and 16-B "
+             "aligned rows");
+  OT_REQUIRE(!rms || !rms->gelu_out || (((epi & OT_EPI_GELU_BWD) || epi == OT_EPI_BIAS) && rms->ldgelu % 4 == 0 &&
                                         ((uintptr_t)rms->gelu_out % 8) == 0),
-             "ot_mixed_gemm_rms: gelu_out needs OT_EPI_GELU_BWD, ldgelu %% 4 == 0 and 8-B alignment");
+             "ot_mixed_gemm_rms: gelu_out needs OT_EPI_GELU_BWD or epi == OT_EPI_BIAS, ldgelu %% 4 == 0 and 8-B "
+             "alignment");
   OT_REQUIRE(!((epi & OT_EPI_DROPOUT) || res_tok) || (tail_K > 0 && tail_I >= tail_K), "ot_mixed_gemm: bad tail map");
   if (rms_flags) {
     OT_REQUIRE(mode == OT_GEMM_NT && N % GT == 0 &&
@@ -1408,7 +1446,7 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
   p.tail_pos = tail_pos;
   p.bimg = bimg; p.bimg_ntn = bimg_ntn; p.bimg_tn0 = bimg_tn0;
   float* dgpart = nullptr;
-  if (rms && (epi & OT_EPI_GELU_BWD)) {                // the stored GELU (optional)
+  if (rms && ((epi & OT_EPI_GELU_BWD) || epi == OT_EPI_BIAS)) {   // the stored GELU (optional)
     p.gelu_out = rms->gelu_out;
     p.ldgelu = rms->ldgelu;
   }
@@ -1500,8 +1538,17 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
     OT_PSPEC(OT_AX_NONE, OT_EPI_RMSNORM_BWD)
     OT_PSPEC(OT_AX_NONE, OT_EPI_RMSNORM_BWD | OT_EPI_DROPOUT)
 #undef OT_PSPEC
+#define OT_PSPEC_BF(EP_) if (one && x == OT_AX_BF16 && e == (EP_)) pk = plane_gemm_kernel<OT_AX_BF16, EP_, 3, 4, 1>;
+    OT_PSPEC_BF(OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_DROPOUT)
+    OT_PSPEC_BF(OT_EPI_BIAS | OT_EPI_RESIDUAL)
+    OT_PSPEC_BF(OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_DROPOUT | OT_EPI_ROW_RSTD)
+    OT_PSPEC_BF(OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_ROW_RSTD)
+#undef OT_PSPEC_BF
     if (pk) { kern = pk; plane = true; }
   }
+  OT_REQUIRE(x != OT_AX_BF16 || plane, "ot_mixed_gemm: no plane GEMM for OT_AX_BF16 with epilogue %d (or edge tiles)",
+             epi);
+  OT_REQUIRE(!p.gelu_out || (!edge && (kern != nullptr)), "ot_mixed_gemm_rms: gelu_out needs whole tiles");
   OT_REQUIRE(!p.rowpart || plane, "ot_mixed_gemm_rms: OT_EPI_ROW_RSTD with N = %d > %d needs the plane GEMM "
              "(split mode, a pre-split B image, 16-B aligned A)", N, GT);
   const size_t launch_shmem = !plane ? shmem

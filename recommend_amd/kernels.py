@@ -84,7 +84,8 @@ def gemm_bytes(M: int, K: int, N: int, a_xform: int, epi: int) -> float:
     (at most a few MB of L2-resident images) are left out."""
     mn = (1 + bool(epi & _lib.OT_EPI_RESIDUAL) + bool(epi & _lib.OT_EPI_GELU_BWD)
           + bool(epi & _lib.OT_EPI_ACCUMULATE))
-    return 4.0 * M * (K + (a_xform == _lib.OT_AX_RMSNORM)) + 4.0 * M * N * mn
+    a_bytes = 2.0 if a_xform == _lib.OT_AX_BF16 else 4.0           # OT_AX_BF16: the stored bf16 gelu(U)
+    return a_bytes * M * K + 4.0 * M * (a_xform == _lib.OT_AX_RMSNORM) + 4.0 * M * N * mn
 
 
 def set_probe(p) -> None:
@@ -177,8 +178,9 @@ def gemm_rms(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish,
     """ot_mixed_gemm_rms: the GEMM with a row-norm epilogue (OT_EPI_ROW_RSTD: emit the next RMSNorm's
     rstd; OT_EPI_RMSNORM_BWD: apply the RMSNorm backward to the product, + dres, dgamma, taking
     <gamma dy, x> from ``rowdot`` when N > 128; OT_EPI_GELU_BWD | OT_EPI_ROWDOT: also write each 128-column
-    tile's sum of dU (aux - bias) into rowdot[row][tile]); with OT_EPI_GELU_BWD and ``gelu_out`` (bf16 bits,
-    [rows][ldgelu]) also gelu(aux) rounded to bf16 (the W2 weight gradient's OT_AX_BF16 operand)."""
+    tile's sum of dU (aux - bias) into rowdot[row][tile]); ``gelu_out`` (bf16 bits, [rows][ldgelu]) also
+    receives gelu(aux) (with OT_EPI_GELU_BWD) or gelu(C) (epi == OT_EPI_BIAS: the FFN1 forward) rounded to
+    bf16 — the OT_AX_BF16 operand of the FFN2 GEMM and the W2 weight gradient."""
     need_ws = dgamma is not None or (rstd_out is not None and N > 128)     # dgamma / row-sum partials
     ws = workspace(size('ot_mixed_gemm_rms_workspace_size', ntiles, N) if need_ws else 16,
                    device if device is not None else (C[0] if isinstance(C, tuple) else C).device)

@@ -143,7 +143,8 @@ def _attn_qpos(cfg, pos):
 def _block_forward(m, l, x, I, Kq, seed, training, rstd_in=None, select=False, need_out=True):
     """The block's forward kernels (``_Block.forward``; also the backward's recompute with
     ``need_out=False``, which stops after FFN1: the backward needs u, not the block output).
-    Returns (x2, rstd_out, saved, pos, inv, rate); saved = (x, rstd1, qkv, o, lse, x1, rstd2, u)."""
+    Returns (x2, rstd_out, saved, pos, inv, rate); saved = (x, rstd1, qkv, o, lse, x1, rstd2, u, h);
+    h = the stored bf16 gelu(u) (bf16 mode) or None."""
     cfg = m.config
     d, f, H = cfg.hidden_dim, cfg.ffn_dim, cfg.num_heads
     hd = d // H
@@ -216,27 +217,39 @@ def _block_forward(m, l, x, I, Kq, seed, training, rstd_in=None, select=False, n
         K.rmsnorm_fwd(x1, d, B * Kq, d, rstd2, eps=RMS_EPS)
     # u = norm2(x1) @ W1[g] + b1[g]  (pre-activation; GELU applied by its consumers)
     u = torch.empty(B * Kq, f, device=dev)
-    K.gemm(OT_GEMM_NT, x1, d, d, mt['rows'][1], w1, d * f, d, f, mt['tile_group'], nt, u, f, mt['rows'][1],
-           a_xform=OT_AX_RMSNORM, rstd=rstd2, gamma=g2, bias=b1, bias_gstride=f, epi=OT_EPI_BIAS, m_rows=maps['tail'].nrows,
-           bimg=m.bimg(f'blk.{l}.w1'))
-    saved = (x, rstd1, qkv, o, lse, x1, rstd2, u)
+    # bf16 mode: the FFN1 epilogue also stores h = gelu(u) rounded to bf16 — exactly the operand the bf16
+    # FFN2 GEMM would form at fragment time — so FFN2 reads 2 B per element and evaluates no erf (it did,
+    # once per output column tile), and the W2 weight gradient reuses h
+    w2img = m.bimg(f'blk.{l}.w2')
+    h = (torch.empty(B * Kq, f, dtype=torch.int16, device=dev)
+         if m.store_gelu_fwd and K.matmul_mode() == 'bf16' and w2img is not None and f % 8 == 0 else None)
+    if h is not None:
+        K.gemm_rms(OT_GEMM_NT, x1, d, d, mt['rows'][1], w1, d * f, d, f, mt['tile_group'], nt, u, f, mt['rows'][1],
+                   a_xform=OT_AX_RMSNORM, rstd=rstd2, gamma=g2, bias=b1, bias_gstride=f, epi=OT_EPI_BIAS,
+                   m_rows=maps['tail'].nrows, bimg=m.bimg(f'blk.{l}.w1'), gelu_out=h, ldgelu=f)
+    else:
+        K.gemm(OT_GEMM_NT, x1, d, d, mt['rows'][1], w1, d * f, d, f, mt['tile_group'], nt, u, f, mt['rows'][1],
+               a_xform=OT_AX_RMSNORM, rstd=rstd2, gamma=g2, bias=b1, bias_gstride=f, epi=OT_EPI_BIAS,
+               m_rows=maps['tail'].nrows, bimg=m.bimg(f'blk.{l}.w1'))
+    saved = (x, rstd1, qkv, o, lse, x1, rstd2, u, h)
     if not need_out:
         return None, None, saved, pos, inv, rate
     # x2 = x1 + drop(gelu(u) @ W2[g] + b2[g])     (model.py:154-161, 198)
     x2 = torch.empty(B * Kq, d, device=dev)
     rstd_out = None
+    a2, ax2 = (h, OT_AX_BF16) if h is not None else (u, OT_AX_GELU)
     if fuse:
         rstd_out = torch.empty(B * Kq, device=dev)
-        K.gemm_rms(OT_GEMM_NT, u, f, f, mt['rows'][1], w2, f * d, f, d, mt['tile_group'], nt, x2, d,
-                   mt['rows'][1], a_xform=OT_AX_GELU, bias=b2, bias_gstride=d,
+        K.gemm_rms(OT_GEMM_NT, a2, f, f, mt['rows'][1], w2, f * d, f, d, mt['tile_group'], nt, x2, d,
+                   mt['rows'][1], a_xform=ax2, bias=b2, bias_gstride=d,
                    epi=OT_EPI_BIAS | OT_EPI_RESIDUAL | dflag | OT_EPI_ROW_RSTD, res=x1, ldres=d, res_tok=0,
                    seed=seed, site=2 * l + 1, drop=rate, tail=tail, m_rows=maps['tail'].nrows,
-                   rstd_out=rstd_out, eps=RMS_EPS, bimg=m.bimg(f'blk.{l}.w2'))
+                   rstd_out=rstd_out, eps=RMS_EPS, bimg=w2img)
     else:
-        K.gemm(OT_GEMM_NT, u, f, f, mt['rows'][1], w2, f * d, f, d, mt['tile_group'], nt, x2, d, mt['rows'][1],
-               a_xform=OT_AX_GELU, bias=b2, bias_gstride=d, epi=OT_EPI_BIAS | OT_EPI_RESIDUAL | dflag, res=x1,
+        K.gemm(OT_GEMM_NT, a2, f, f, mt['rows'][1], w2, f * d, f, d, mt['tile_group'], nt, x2, d, mt['rows'][1],
+               a_xform=ax2, bias=b2, bias_gstride=d, epi=OT_EPI_BIAS | OT_EPI_RESIDUAL | dflag, res=x1,
                ldres=d, res_tok=0, seed=seed, site=2 * l + 1, drop=rate, tail=tail,
-               m_rows=maps['tail'].nrows, bimg=m.bimg(f'blk.{l}.w2'))
+               m_rows=maps['tail'].nrows, bimg=w2img)
     return x2, rstd_out, saved, pos, inv, rate
 
 
@@ -274,9 +287,9 @@ class _Block(torch.autograd.Function):
             training, select = ctx.fwd_args
             _, _, saved, pos, inv, _ = _block_forward(m, l, xin, I, Kq, seed, training, rstd_in, select,
                                                       need_out=False)
-            x, rstd1, qkv, o, lse, x1, rstd2, u = saved
+            x, rstd1, qkv, o, lse, x1, rstd2, u, h = saved
         else:
-            x, rstd1, qkv, o, lse, x1, rstd2, u = ctx.saved_tensors
+            x, rstd1, qkv, o, lse, x1, rstd2, u, h = ctx.saved_tensors
         tail = (Kq, I, pos)
         cfg = m.config
         d, f, H = cfg.hidden_dim, cfg.ffn_dim, cfg.num_heads
@@ -302,12 +315,14 @@ class _Block(torch.autograd.Function):
         # bf16 mode with the fused norm2 backward (C5): the FFN2 dgrad epilogue, which reads U for GELU'
         # anyway, also stores gelu(U) in bf16 — the W2 weight gradient then reads 2 B per element instead of
         # U's 4 and evaluates no erf (it did, once per output column tile: 4x at f = 2048, d = 512)
+        # (the forward's FFN1 epilogue stored it already when h is not None)
         hbf = (torch.empty(B * Kq, f, dtype=torch.int16, device=dev)
-               if fused2 and m.store_gelu and K.matmul_mode() == 'bf16' else None)
+               if h is None and fused2 and m.store_gelu and K.matmul_mode() == 'bf16' else None)
         if hbf is None:
-            with m.side(u, dy2):       # weight gradients overlap the dgrad chain on a second stream
-                K.wgrad(u, f, mt['rows'][1], dy2, d, mt['rows'][1], f, d, mt, nct, G, m.g(f'blk.{l}.w2'), f * d,
-                        m.g(f'blk.{l}.b2'), d, a_xform=OT_AX_GELU, accumulate=acc, device=dev,
+            with m.side(u if h is None else h, dy2):   # weight gradients overlap the dgrad chain on a second stream
+                K.wgrad(u if h is None else h, f, mt['rows'][1], dy2, d, mt['rows'][1], f, d, mt, nct, G,
+                        m.g(f'blk.{l}.w2'), f * d, m.g(f'blk.{l}.b2'), d,
+                        a_xform=OT_AX_GELU if h is None else OT_AX_BF16, accumulate=acc, device=dev,
                         m_rows=maps['tail'].nrows, rowmap=maps['tail'])
         if fused2:
             # d > 128: the FFN2 dgrad also emits rowdot[row][f-tile] = sum dU (U - b1) for the norm2 backward
@@ -561,9 +576,12 @@ class OneTransModel(nn.Module):
         self.fuse_norms = (config.hidden_dim % TILE == 0 and os.environ.get('ONETRANS_FUSE_NORMS', '1') != '0')
         self.fuse_bwd = self.fuse_norms and config.hidden_dim == TILE
         self.fuse_bwd2 = self.fuse_norms and os.environ.get('ONETRANS_FUSE_NORM2_BWD', '1') != '0'
-        # bf16 mode: the FFN2 dgrad stores gelu(U) in bf16 for the W2 weight gradient (ONETRANS_STORE_GELU=0:
-        # that GEMM recomputes GELU from f32 U)
-        self.store_gelu = os.environ.get('ONETRANS_STORE_GELU', '1') != '0'
+        # bf16 mode: the FFN1 forward epilogue stores h = bf16(gelu(U)), which the FFN2 GEMM and the W2 weight
+        # gradient read (ONETRANS_STORE_GELU=bwd: only the FFN2 dgrad epilogue stores it, for the weight
+        # gradient; 0: both GEMMs recompute GELU from f32 U)
+        sg = os.environ.get('ONETRANS_STORE_GELU', '1')
+        self.store_gelu = sg != '0'
+        self.store_gelu_fwd = sg not in ('0', 'bwd')
         # block weight gradients run on a second stream, overlapping the dgrad chain
         self.overlap_wgrad = os.environ.get('ONETRANS_OVERLAP_WGRAD', '1') != '0'
         self._side = None

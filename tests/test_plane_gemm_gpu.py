@@ -178,3 +178,68 @@ def test_plane_gemm_rmsnorm_bwd(dev, K_, drop):
         close(outs[1][1], outs[0][1], K_)
     tol = 3e-2 if MODE['m'] == 'bf16' else 1e-4
     torch.testing.assert_close(outs[1][2], outs[0][2], rtol=tol, atol=10 * tol)
+
+
+@pytest.mark.parametrize('f,N', [(256, 128), (512, 256)])
+@pytest.mark.parametrize('rstd_epi', [False, True])
+def test_plane_gemm_stored_gelu(dev, plane_mode, f, N, rstd_epi):
+    """The FFN1 epilogue's stored GELU (ot_rms_epilogue.gelu_out with epi == OT_EPI_BIAS: bf16 gelu(U)) and
+    the FFN2 plane GEMM reading it (OT_AX_BF16 A): U is unchanged by the extra store, h is gelu(U) rounded
+    to bf16 (torch float64 erf: at most one bf16 ulp apart), and in the bf16 mode the FFN2 output (and the
+    next norm's rstd) from h is bit-identical to the one that forms gelu(U) at fragment time (OT_AX_GELU:
+    the same rounding of the same values).  The split mode refuses a bf16 A operand."""
+    from recommend_amd._lib import OT_AX_BF16, OneTransHipError
+    rng = np.random.default_rng(f + N)
+    G, B, I, Kq, d = 3, 53, 9, 5, N
+    M = B * Kq
+    rm = ragged_map(rng, M, G)
+    dm = rm.to(dev)
+    x = torch.randn(M, d, device=dev)
+    W1 = torch.randn(G, f, d) / math.sqrt(d)
+    W2 = torch.randn(G, N, f) / math.sqrt(f)
+    gamma = 1 + 0.1 * torch.randn(d)
+    rstd = torch.rand(M, device=dev) + 0.5
+    b1, b2 = torch.randn(G, f, device=dev), torch.randn(G, N, device=dev)
+    res = torch.randn(M, N, device=dev)
+    img1, ntn1 = make_image(W1, dev, gamma)
+    img2, ntn2 = make_image(W2, dev)
+    rows = dm['rows'][1]
+    kw1 = dict(a_xform=OT_AX_RMSNORM, rstd=rstd, gamma=gamma.to(dev), bias=b1, bias_gstride=f, epi=OT_EPI_BIAS,
+               bimg=(img1, ntn1, 0))
+    U0 = torch.full((M, f), float('nan'), device=dev)
+    K.gemm(OT_GEMM_NT, x, d, d, dm['rows'][0], W1.to(dev), f * d, d, f, dm['tile_group'], rm.ntiles, U0, f, rows, **kw1)
+    U = torch.full((M, f), float('nan'), device=dev)
+    h = torch.zeros(M, f, dtype=torch.int16, device=dev)
+    K.gemm_rms(OT_GEMM_NT, x, d, d, dm['rows'][0], W1.to(dev), f * d, d, f, dm['tile_group'], rm.ntiles, U, f, rows,
+               gelu_out=h, ldgelu=f, device=dev, **kw1)
+    torch.cuda.synchronize()
+    assert torch.equal(U, U0)
+    ref = (0.5 * U.double() * (1 + torch.erf(U.double() / math.sqrt(2)))).float().to(torch.bfloat16).cpu().float()
+    got = h.view(torch.bfloat16).cpu().float()
+    # (+ 1e-6 absolute: for U < -3 the f32 1 + erf(U / sqrt 2) cancels; gelu there is below 2e-3)
+    assert ((got - ref).abs() <= ref.abs() * 2 ** -7 + 1e-6).all(), float((got - ref).abs().max())
+    epi = OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_DROPOUT | (OT_EPI_ROW_RSTD if rstd_epi else 0)
+    kw2 = dict(bias=b2, bias_gstride=N, epi=epi, res=res, ldres=N, res_tok=0, seed=7, site=1, drop=0.1,
+               tail=(Kq, I), bimg=(img2, ntn2, 0))
+    if plane_mode != 'bf16':
+        with pytest.raises(OneTransHipError, match='OT_AX_BF16'):
+            K.gemm(OT_GEMM_NT, h, f, f, rows, W2.to(dev), N * f, f, N, dm['tile_group'], rm.ntiles,
+                   torch.empty(M, N, device=dev), N, rows, a_xform=OT_AX_BF16,
+                   **dict(kw2, epi=epi & ~OT_EPI_ROW_RSTD))
+        return
+    outs = []
+    for A, ax in ((U, OT_AX_GELU), (h, OT_AX_BF16)):
+        C = torch.full((M, N), float('nan'), device=dev)
+        rs = torch.full((M,), float('nan'), device=dev)
+        if rstd_epi:
+            K.gemm_rms(OT_GEMM_NT, A, f, f, rows, W2.to(dev), N * f, f, N, dm['tile_group'], rm.ntiles, C, N, rows,
+                       a_xform=ax, rstd_out=rs, eps=1e-6, device=dev, **kw2)
+        else:
+            K.gemm(OT_GEMM_NT, A, f, f, rows, W2.to(dev), N * f, f, N, dm['tile_group'], rm.ntiles, C, N, rows,
+                   a_xform=ax, **kw2)
+        outs.append((C, rs))
+    torch.cuda.synchronize()
+    assert not torch.isnan(outs[1][0]).any()
+    assert torch.equal(outs[0][0], outs[1][0])
+    if rstd_epi:
+        assert torch.equal(outs[0][1], outs[1][1])

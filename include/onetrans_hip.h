@@ -72,6 +72,13 @@ extern "C" {
                                    rstd * <gamma dy, x> (no row-wide reduction needed at d > 128) */
 #define OT_EPI_RMSNORM_BWD 128  /* the product is dL/dy of y = RMSNorm(x) * gamma: C = dL/dx (+ dres);
                                    with OT_EPI_DROPOUT also dx_masked = mask(C) (C itself unmasked) */
+#define OT_EPI_C_BF16 512       /* C is stored rounded to bf16 (uint16 bits, ldc in elements; 8-B aligned
+                                   rows).  Plane GEMM in the bf16 mode, with OT_EPI_GELU_BWD [| OT_EPI_ROWDOT]
+                                   only (the FFN2 dgrad: dU, whose consumers — the FFN1 dgrad and the W1
+                                   weight gradient — round it to bf16 anyway) */
+/* ot_mixed_gemm_wgrad: or'ed into a_xform, D holds bf16 values (uint16 bits, ldd in elements; 8-B aligned
+ * rows; OT_MATMUL_BF16 / split modes) — dU stored by OT_EPI_C_BF16 */
+#define OT_WG_D_BF16 8
 
 int ot_version(void);
 const char* ot_get_last_error_string(void);

@@ -157,6 +157,7 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
     constexpr bool ROWRSTD = EPIT >= 0 && (EPIT & OT_EPI_ROW_RSTD);
     constexpr bool ROWDOT = EPIT >= 0 && (EPIT & OT_EPI_ROWDOT);
     constexpr bool GSTORE = EPIT == OT_EPI_BIAS;        // gelu_out of a bias-only epilogue: gelu(C)
+    constexpr bool CBF = EPIT >= 0 && (EPIT & OT_EPI_C_BF16);
     f32x4 rdb4 = {0.f, 0.f, 0.f, 0.f};                 // OT_EPI_ROWDOT: the bias subtracted from aux
     if (ROWDOT) rdb4 = *reinterpret_cast<const f32x4*>(p.bias + (int64_t)g * p.bias_gstride + col);
     // dgamma partials live in a thread-private LDS slot behind ct (a register accumulator here
@@ -299,7 +300,11 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
             const f32x4 hv = {gelu_erf(v.x), gelu_erf(v.y), gelu_erf(v.z), gelu_erf(v.w)};
             *reinterpret_cast<u32x2*>(p.gelu_out + (int64_t)orr * p.ldgelu + col) = bf16_rne4(hv);
           }
-          if (orr >= 0) store_out4(p.C + (int64_t)orr * p.ldc + col, v);
+          if (CBF) {                                           // C in bf16 (the FFN2 dgrad's dU)
+            if (orr >= 0) *reinterpret_cast<u32x2*>(reinterpret_cast<uint16_t*>(p.C) + (int64_t)orr * p.ldc + col) = bf16_rne4(v);
+          } else if (orr >= 0) {
+            store_out4(p.C + (int64_t)orr * p.ldc + col, v);
+          }
         }
       }
       __syncthreads();                                  // ct is rewritten by the next half
@@ -1057,7 +1062,8 @@ __device__ __forceinline__ v4i16 ds_tr16(const char* base, int off) {
 template <int TERMS>
 constexpr int wgrad_rs() { return WGRAD_BF16_RS > 0 && TERMS == 1 ? WGRAD_BF16_RS : 1; }
 
-template <int AXT, int TERMS>
+// DBF: D holds bf16 values (OT_WG_D_BF16: the FFN2 dgrad's bf16 dU)
+template <int AXT, int TERMS, bool DBF = false>
 __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(WgradArgs p) {
   constexpr int RS = wgrad_rs<TERMS>();
   static_assert(RS * WSPLANE <= WSOP && (TERMS == 1 || RS == 1), "wgrad stage LDS");
@@ -1129,7 +1135,14 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(WgradArgs p) {
         } else {
           va[j][i] = *reinterpret_cast<const f32x4*>(pa + kc);
         }
-        vd[j][i] = *reinterpret_cast<const f32x4*>(pd + nc);
+        if (DBF) {
+          const u32x2 w = *reinterpret_cast<const u32x2*>(reinterpret_cast<const uint16_t*>(p.D) +
+                                                          (int64_t)(inr[j] ? dr[j] : 0) * p.ldd + nc);
+          vd[j][i] = f32x4{__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u),
+                           __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u)};
+        } else {
+          vd[j][i] = *reinterpret_cast<const f32x4*>(pd + nc);
+        }
       }
     }
   };
@@ -1424,7 +1437,7 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
     OT_REQUIRE(N == GT || !(epi & OT_EPI_ROW_RSTD) ||
                    (rms->workspace && rms->ws_bytes >= ot_mixed_gemm_rms_workspace_size(ntiles, N)),
                "ot_mixed_gemm_rms: OT_EPI_ROW_RSTD with N > %d needs the workspace", GT);
-    OT_REQUIRE(!(epi & OT_EPI_ROWDOT) || ((epi & OT_EPI_GELU_BWD) && !(epi & ~(OT_EPI_GELU_BWD | OT_EPI_ROWDOT)) &&
+    OT_REQUIRE(!(epi & OT_EPI_ROWDOT) || ((epi & OT_EPI_GELU_BWD) && !(epi & ~(OT_EPI_GELU_BWD | OT_EPI_ROWDOT | OT_EPI_C_BF16)) &&
                                           rms->rowdot && rms->rowdot_n == N / GT && bias),
                "ot_mixed_gemm_rms: OT_EPI_ROWDOT goes with OT_EPI_GELU_BWD only and needs rowdot[rows][N / %d] and "
                "the bias", GT);
@@ -1538,16 +1551,24 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
     OT_PSPEC(OT_AX_NONE, OT_EPI_RMSNORM_BWD)
     OT_PSPEC(OT_AX_NONE, OT_EPI_RMSNORM_BWD | OT_EPI_DROPOUT)
 #undef OT_PSPEC
+    if (one && x == OT_AX_NONE && e == (OT_EPI_GELU_BWD | OT_EPI_ROWDOT | OT_EPI_C_BF16))
+      pk = plane_gemm_kernel<OT_AX_NONE, OT_EPI_GELU_BWD | OT_EPI_ROWDOT | OT_EPI_C_BF16, 3, 4, 1>;
+    if (one && x == OT_AX_NONE && e == (OT_EPI_GELU_BWD | OT_EPI_C_BF16))
+      pk = plane_gemm_kernel<OT_AX_NONE, OT_EPI_GELU_BWD | OT_EPI_C_BF16, 3, 4, 1>;
 #define OT_PSPEC_BF(EP_) if (one && x == OT_AX_BF16 && e == (EP_)) pk = plane_gemm_kernel<OT_AX_BF16, EP_, 3, 4, 1>;
     OT_PSPEC_BF(OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_DROPOUT)
     OT_PSPEC_BF(OT_EPI_BIAS | OT_EPI_RESIDUAL)
     OT_PSPEC_BF(OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_DROPOUT | OT_EPI_ROW_RSTD)
     OT_PSPEC_BF(OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_ROW_RSTD)
+    OT_PSPEC_BF(OT_EPI_RMSNORM_BWD)
+    OT_PSPEC_BF(OT_EPI_RMSNORM_BWD | OT_EPI_DROPOUT)
 #undef OT_PSPEC_BF
     if (pk) { kern = pk; plane = true; }
   }
   OT_REQUIRE(x != OT_AX_BF16 || plane, "ot_mixed_gemm: no plane GEMM for OT_AX_BF16 with epilogue %d (or edge tiles)",
              epi);
+  OT_REQUIRE(!(epi & OT_EPI_C_BF16) || plane, "ot_mixed_gemm: OT_EPI_C_BF16 needs the bf16-mode plane GEMM with "
+             "OT_EPI_GELU_BWD [| OT_EPI_ROWDOT] (epilogue %d)", epi);
   OT_REQUIRE(!p.gelu_out || (!edge && (kern != nullptr)), "ot_mixed_gemm_rms: gelu_out needs whole tiles");
   OT_REQUIRE(!p.rowpart || plane, "ot_mixed_gemm_rms: OT_EPI_ROW_RSTD with N = %d > %d needs the plane GEMM "
              "(split mode, a pre-split B image, 16-B aligned A)", N, GT);
@@ -1689,7 +1710,13 @@ extern "C" int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a
   OT_REQUIRE(K % 4 == 0 && N % 4 == 0 && lda % 4 == 0 && ldd % 4 == 0 && dw_gstride % 4 == 0,
              "ot_mixed_gemm_wgrad: K, N, lda, ldd, dw_gstride must be multiples of 4");
   OT_REQUIRE(ws_bytes >= ot_wgrad_workspace_size(nchunks, K, N), "ot_mixed_gemm_wgrad: workspace too small");
+  const bool dbf = (a_xform & OT_WG_D_BF16) != 0;
+  a_xform &= ~OT_WG_D_BF16;
   OT_REQUIRE(a_xform != OT_AX_RMSNORM || (a_rstd && a_gamma), "ot_mixed_gemm_wgrad: rmsnorm prologue needs rstd/gamma");
+  OT_REQUIRE(!dbf || (g_matmul_mode == OT_MATMUL_BF16 && (a_xform == OT_AX_NONE || a_xform == OT_AX_RMSNORM) &&
+                      ((uintptr_t)D % 8) == 0),
+             "ot_mixed_gemm_wgrad: OT_WG_D_BF16 needs the bf16 mode, A form OT_AX_NONE / OT_AX_RMSNORM and 8-B "
+             "aligned D rows");
   hipStream_t s = (hipStream_t)stream;
   float* slab = (float*)workspace;
   float* bslab = db ? slab + (size_t)nchunks * K * N : nullptr;
@@ -1701,7 +1728,8 @@ extern "C" int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a
     OT_REQUIRE(a_xform != OT_AX_BF16 || (g_matmul_mode != OT_MATMUL_F32 && lda % 4 == 0 && ((uintptr_t)A % 8) == 0),
                "ot_mixed_gemm_wgrad: OT_AX_BF16 needs the split / bf16 mode and 8-B aligned rows");
     void (*kern)(WgradArgs) =
-        a_xform == OT_AX_BF16 ? (g_matmul_mode == OT_MATMUL_BF16 ? wgrad_split_kernel<OT_AX_BF16, 1>
+        dbf ? (a_xform == OT_AX_NONE ? wgrad_split_kernel<OT_AX_NONE, 1, true> : wgrad_split_kernel<OT_AX_RMSNORM, 1, true>)
+        : a_xform == OT_AX_BF16 ? (g_matmul_mode == OT_MATMUL_BF16 ? wgrad_split_kernel<OT_AX_BF16, 1>
                                                                 : wgrad_split_kernel<OT_AX_BF16, SPLIT_TERMS>)
         : g_matmul_mode == OT_MATMUL_BF16
             ? (a_xform == OT_AX_NONE      ? wgrad_split_kernel<OT_AX_NONE, 1>

@@ -85,7 +85,8 @@ def gemm_bytes(M: int, K: int, N: int, a_xform: int, epi: int) -> float:
     mn = (1 + bool(epi & _lib.OT_EPI_RESIDUAL) + bool(epi & _lib.OT_EPI_GELU_BWD)
           + bool(epi & _lib.OT_EPI_ACCUMULATE))
     a_bytes = 2.0 if a_xform == _lib.OT_AX_BF16 else 4.0           # OT_AX_BF16: the stored bf16 gelu(U)
-    return a_bytes * M * K + 4.0 * M * (a_xform == _lib.OT_AX_RMSNORM) + 4.0 * M * N * mn
+    c_less = 2.0 * M * N if epi & _lib.OT_EPI_C_BF16 else 0.0       # OT_EPI_C_BF16: C written in bf16
+    return a_bytes * M * K + 4.0 * M * (a_xform == _lib.OT_AX_RMSNORM) + 4.0 * M * N * mn - c_less
 
 
 def set_probe(p) -> None:
@@ -223,8 +224,9 @@ def wgrad(A: Ptrish, lda: int, a_rows: Ptrish, D: Ptrish, ldd: int, d_rows: Ptri
          dw_gstride, ptr(db), db_gstride, int(accumulate), ptr(ws), ws.numel(), stream())
     if ev is not None:
         _probe.end('mixed_gemm', 2.0 * m_rows * K * N, ev, f'wgrad ax{a_xform} M{m_rows} K{K} N{N} ch{nchunks}',
-                   (2.0 if a_xform == _lib.OT_AX_BF16 else 4.0) * m_rows * K
-                   + 4.0 * m_rows * (N + (a_xform == _lib.OT_AX_RMSNORM)) + 4.0 * ngroups * K * N)
+                   (2.0 if (a_xform & ~_lib.OT_WG_D_BF16) == _lib.OT_AX_BF16 else 4.0) * m_rows * K
+                   + (2.0 if a_xform & _lib.OT_WG_D_BF16 else 4.0) * m_rows * N
+                   + 4.0 * m_rows * ((a_xform & ~_lib.OT_WG_D_BF16) == _lib.OT_AX_RMSNORM) + 4.0 * ngroups * K * N)
 
 
 def transpose_banks(src, dst, banks_dev, nbanks, total_tiles) -> None:

@@ -27,9 +27,9 @@ import torch.nn as nn
 
 from . import _lib
 from . import kernels as K
-from ._lib import (OT_AX_BF16, OT_AX_GELU, OT_AX_RMSNORM, OT_EPI_ACCUMULATE, OT_EPI_BIAS, OT_EPI_DROPOUT, OT_EPI_GELU_BWD,
-                   OT_EPI_RESIDUAL, OT_EPI_RMSNORM_BWD, OT_EPI_ROW_RSTD, OT_EPI_ROWDOT, OT_GEMM_NN, OT_GEMM_NT,
-                   NS_FIELD_BYTES)
+from ._lib import (OT_AX_BF16, OT_AX_GELU, OT_AX_RMSNORM, OT_EPI_ACCUMULATE, OT_EPI_BIAS, OT_EPI_C_BF16, OT_EPI_DROPOUT,
+                   OT_EPI_GELU_BWD, OT_EPI_RESIDUAL, OT_EPI_RMSNORM_BWD, OT_EPI_ROW_RSTD, OT_EPI_ROWDOT, OT_GEMM_NN,
+                   OT_GEMM_NT, OT_WG_D_BF16, NS_FIELD_BYTES)
 from .config import OneTransConfig, check_pyramid_select, get_model_config
 from .layout import TILE, FlatLayout, RowMap, build_map, head_map, identity_map, layer_maps, round_up
 from .params import init_params, ns_table_offsets
@@ -309,9 +309,14 @@ class _Block(torch.autograd.Function):
             K.dropout_apply(dx2, d, dy2, d, B * Kq, d, seed, 2 * l + 1, rate, tail)
         else:
             dy2 = dx2
-        du = torch.empty(B * Kq, f, device=dev)
         rowdot = None
         fused2 = m.fuse_bwd2 and not m.fuse_bwd and f % TILE == 0
+        # bf16 mode (C5): dU is stored in bf16 by the FFN2 dgrad epilogue (OT_EPI_C_BF16); its two consumers,
+        # the FFN1 dgrad (bf16 A, plane GEMM) and the W1 weight gradient (OT_WG_D_BF16), rounded it to bf16 at
+        # fragment / staging time anyway, so only b1's gradient (a column sum of dU) sees the rounding
+        du_bf = (fused2 and h is not None and m.du_bf16 and m.bimg(f'blk.{l}.w1', 'dgrad') is not None)
+        du = torch.empty(B * Kq, f, device=dev, dtype=torch.int16 if du_bf else torch.float32)
+        cbf = OT_EPI_C_BF16 if du_bf else 0
         # bf16 mode with the fused norm2 backward (C5): the FFN2 dgrad epilogue, which reads U for GELU'
         # anyway, also stores gelu(U) in bf16 — the W2 weight gradient then reads 2 B per element instead of
         # U's 4 and evaluates no erf (it did, once per output column tile: 4x at f = 2048, d = 512)
@@ -328,7 +333,7 @@ class _Block(torch.autograd.Function):
             # d > 128: the FFN2 dgrad also emits rowdot[row][f-tile] = sum dU (U - b1) for the norm2 backward
             rowdot = torch.empty(B * Kq, f // TILE, device=dev)
             K.gemm_rms(OT_GEMM_NT, dy2, d, d, mt['rows'][1], m.p(f'blk.{l}.w2'), f * d, d, f, mt['tile_group'], nt,
-                       du, f, mt['rows'][1], epi=OT_EPI_GELU_BWD | OT_EPI_ROWDOT, aux=u, ldaux=f,
+                       du, f, mt['rows'][1], epi=OT_EPI_GELU_BWD | OT_EPI_ROWDOT | cbf, aux=u, ldaux=f,
                        bias=m.p(f'blk.{l}.b1'), bias_gstride=f, rowdot=rowdot, rowdot_n=f // TILE,
                        m_rows=maps['tail'].nrows, device=dev, bimg=m.bimg(f'blk.{l}.w2', 'dgrad'),
                        gelu_out=hbf, ldgelu=f)
@@ -343,7 +348,8 @@ class _Block(torch.autograd.Function):
                    bimg=m.bimg(f'blk.{l}.w2', 'dgrad'))
         with m.side(x1, du, rstd2):
             K.wgrad(x1, d, mt['rows'][1], du, f, mt['rows'][1], d, f, mt, nct, G, m.g(f'blk.{l}.w1'), d * f,
-                    m.g(f'blk.{l}.b1'), f, a_xform=OT_AX_RMSNORM, rstd=rstd2, gamma=m.p(f'blk.{l}.norm2'),
+                    m.g(f'blk.{l}.b1'), f, a_xform=OT_AX_RMSNORM | (OT_WG_D_BF16 if du_bf else 0), rstd=rstd2,
+                    gamma=m.p(f'blk.{l}.norm2'),
                     accumulate=acc, device=dev, m_rows=maps['tail'].nrows, rowmap=maps['tail'])
         # FFN1 dgrad -> norm2 backward + residual; emit mask(dx1) for the attention branch
         dx1 = torch.empty(B * Kq, d, device=dev)
@@ -351,6 +357,7 @@ class _Block(torch.autograd.Function):
         if m.fuse_bwd or rowdot is not None:   # FFN1 dgrad -> norm2 backward in the epilogue
             K.gemm_rms(OT_GEMM_NT, du, f, f, mt['rows'][1], m.p(f'blk.{l}.w1'), d * f, f, d, mt['tile_group'], nt,
                        dx1, d, mt['rows'][1], epi=OT_EPI_RMSNORM_BWD | (OT_EPI_DROPOUT if rate > 0 else 0),
+                       a_xform=OT_AX_BF16 if du_bf else 0,
                        seed=seed, site=2 * l, drop=rate, tail=tail, m_rows=maps['tail'].nrows, nx=x1, ldnx=d,
                        ngamma=m.p(f'blk.{l}.norm2'), nrstd=rstd2, dres=dx2, lddres=d,
                        dx_masked=dyo if rate > 0 else None, lddxm=d, dgamma=m.g(f'blk.{l}.norm2'),
@@ -582,6 +589,8 @@ class OneTransModel(nn.Module):
         sg = os.environ.get('ONETRANS_STORE_GELU', '1')
         self.store_gelu = sg != '0'
         self.store_gelu_fwd = sg not in ('0', 'bwd')
+        # bf16 mode with the stored GELU: dU in bf16 (ONETRANS_DU_BF16=0: f32)
+        self.du_bf16 = os.environ.get('ONETRANS_DU_BF16', '1') != '0'
         # block weight gradients run on a second stream, overlapping the dgrad chain
         self.overlap_wgrad = os.environ.get('ONETRANS_OVERLAP_WGRAD', '1') != '0'
         self._side = None

@@ -243,3 +243,72 @@ def test_plane_gemm_stored_gelu(dev, plane_mode, f, N, rstd_epi):
     assert torch.equal(outs[0][0], outs[1][0])
     if rstd_epi:
         assert torch.equal(outs[0][1], outs[1][1])
+
+
+def test_plane_gemm_bf16_du(dev, plane_mode):
+    """bf16 mode: dU stored in bf16 by the FFN2 dgrad epilogue (OT_EPI_C_BF16) is dU rounded to nearest
+    even, bit for bit, with the same row-dot partials; the FFN1 dgrad (RMSNorm backward epilogue) from the
+    bf16 dU (OT_AX_BF16) and the W1 weight gradient from it (OT_WG_D_BF16) are bit-identical to the ones
+    from f32 dU (both round it to bf16 at fragment / staging time); b1's gradient (a column sum) is within
+    bf16 rounding.  The split mode refuses both forms."""
+    from recommend_amd import layout
+    from recommend_amd._lib import OT_AX_BF16, OT_EPI_C_BF16, OT_EPI_ROWDOT, OT_WG_D_BF16, OneTransHipError
+    rng = np.random.default_rng(21)
+    G, B, I, Kq, d, f = 3, 47, 9, 5, 256, 512
+    M = B * Kq
+    rm = ragged_map(rng, M, G)
+    dm = rm.to(dev)
+    rows = dm['rows'][1]
+    dy = torch.randn(M, d, device=dev)
+    U = torch.randn(M, f, device=dev)
+    b1 = torch.randn(G, f, device=dev)
+    W2 = torch.randn(G, f, d) / math.sqrt(d)          # dgrad B[g][n = f][k = d]
+    W1 = torch.randn(G, d, f) / math.sqrt(f)          # dgrad B[g][n = d][k = f]
+    img2, ntn2 = make_image(W2, dev)
+    img1, ntn1 = make_image(W1, dev)
+    x1 = torch.randn(M, d, device=dev)
+    gamma = 1 + 0.1 * torch.randn(d, device=dev)
+    rstd = torch.rsqrt((x1 * x1).mean(1) + 1e-6)
+    dres = torch.randn(M, d, device=dev)
+    kw = dict(epi=OT_EPI_GELU_BWD | OT_EPI_ROWDOT, aux=U, ldaux=f, bias=b1, bias_gstride=f, rowdot_n=f // 128,
+              device=dev, bimg=(img2, ntn2, 0))
+    if plane_mode != 'bf16':
+        with pytest.raises(OneTransHipError, match='OT_EPI_C_BF16'):
+            K.gemm_rms(OT_GEMM_NT, dy, d, d, rows, W2.to(dev), f * d, d, f, dm['tile_group'], rm.ntiles,
+                       torch.empty(M, f, dtype=torch.int16, device=dev), f, rows,
+                       rowdot=torch.empty(M, f // 128, device=dev), **dict(kw, epi=kw['epi'] | OT_EPI_C_BF16))
+        return
+    dus, rds = [], []
+    for cbf in (0, OT_EPI_C_BF16):
+        du = torch.zeros(M, f, device=dev, dtype=torch.int16 if cbf else torch.float32)
+        rd = torch.full((M, f // 128), float('nan'), device=dev)
+        K.gemm_rms(OT_GEMM_NT, dy, d, d, rows, W2.to(dev), f * d, d, f, dm['tile_group'], rm.ntiles, du, f, rows,
+                   rowdot=rd, **dict(kw, epi=kw['epi'] | cbf))
+        dus.append(du)
+        rds.append(rd)
+    torch.cuda.synchronize()
+    assert torch.equal(rds[0], rds[1])
+    assert torch.equal(dus[0].to(torch.bfloat16).view(torch.int16), dus[1])
+    # FFN1 dgrad -> norm2 backward, from f32 dU and from bf16 dU
+    outs = []
+    for du, ax in ((dus[0], 0), (dus[1], OT_AX_BF16)):
+        dx = torch.full((M, d), float('nan'), device=dev)
+        dg = torch.zeros(d, device=dev)
+        K.gemm_rms(OT_GEMM_NT, du, f, f, rows, W1.to(dev), d * f, f, d, dm['tile_group'], rm.ntiles, dx, d, rows,
+                   epi=OT_EPI_RMSNORM_BWD, a_xform=ax, nx=x1, ldnx=d, ngamma=gamma, nrstd=rstd, dres=dres, lddres=d,
+                   dgamma=dg, device=dev, bimg=(img1, ntn1, 0), rowdot=rds[0], rowdot_n=f // 128)
+        outs.append((dx, dg))
+    # W1 weight gradient (RMSNorm prologue on x1), D = f32 dU / bf16 dU
+    wg = []
+    for du, dflag in ((dus[0], 0), (dus[1], OT_WG_D_BF16)):
+        dW = torch.empty(G, d, f, device=dev)
+        db = torch.empty(G, f, device=dev)
+        K.wgrad(x1, d, rows, du, f, rows, d, f, dm, rm.chunks.shape[0], G, dW, d * f, db, f,
+                a_xform=OT_AX_RMSNORM | dflag, rstd=rstd, gamma=gamma, device=dev, m_rows=M, rowmap=rm)
+        wg.append((dW, db))
+    torch.cuda.synchronize()
+    assert not torch.isnan(outs[1][0]).any()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert torch.equal(wg[0][0], wg[1][0])
+    scale = wg[0][1].abs().max().item()
+    assert (wg[0][1] - wg[1][1]).abs().max().item() < 1e-2 * scale

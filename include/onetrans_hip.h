@@ -249,6 +249,17 @@ size_t ot_attn_bwd_ex_workspace_size(int B, int H, int I, int K, int head_dim, i
 int ot_attn_bwd_ex(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
                    int B, int H, int I, int K, const int32_t* qpos, int head_dim, float* dqkv, void* workspace,
                    size_t ws_bytes, void* stream);
+/* ot_attn_bwd_ex with output flags.  OT_ATTN_DQKV_BF16: dqkv holds bf16 (uint16 bits, ld in elements,
+ * 8-B aligned) — the bf16 mode's consumers (the QKV dgrad's A operand, the Wqkv weight gradient's D) round
+ * it to bf16 anyway, so the values they use are unchanged (each element is the f32 result rounded once).
+ * Key-grouped backward only (ot_attn_bwd_dqkv_bf16_supported); workspace
+ * ot_attn_bwd_flags_workspace_size (one more [B*K][H*head_dim] f32 dQ slot: slice 0's). */
+#define OT_ATTN_DQKV_BF16 1
+int ot_attn_bwd_dqkv_bf16_supported(int I, int K, int head_dim, int selected);
+size_t ot_attn_bwd_flags_workspace_size(int B, int H, int I, int K, int head_dim, int selected, int flags);
+int ot_attn_bwd_flags(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
+                      int B, int H, int I, int K, const int32_t* qpos, int head_dim, void* dqkv, int flags,
+                      void* workspace, size_t ws_bytes, void* stream);
 
 /* Two-stage cached serving (paper §3.5.1; replaces the reference's defective cache path
  * model.py:94-98, 359-381, D6): candidate c (request req[c]) attends with the last Kq of its n

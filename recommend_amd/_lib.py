@@ -21,6 +21,7 @@ OT_EPI_BIAS, OT_EPI_GELU_BWD, OT_EPI_GELU = 1, 2, 4
 OT_EPI_DROPOUT, OT_EPI_RESIDUAL, OT_EPI_ACCUMULATE = 8, 16, 32
 OT_EPI_ROW_RSTD, OT_EPI_RMSNORM_BWD, OT_EPI_ROWDOT = 64, 128, 256
 OT_EPI_C_BF16 = 512
+OT_ATTN_DQKV_BF16 = 1
 OT_WG_D_BF16 = 8
 OT_MATMUL_F32, OT_MATMUL_SPLIT_BF16, OT_MATMUL_BF16 = 0, 1, 2
 OT_FP8_DEQUANT, OT_FP8_TWO_TERM = 1, 2
@@ -76,6 +77,9 @@ SIGNATURES = {
     'ot_attn_bwd': (c_int, [P, I64, P, P, P, c_int, c_int, c_int, c_int, P, c_int, P, P, P]),
     'ot_attn_bwd_ex_workspace_size': (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
     'ot_attn_bwd_ex': (c_int, [P, I64, P, P, P, c_int, c_int, c_int, c_int, P, c_int, P, P, c_size_t, P]),
+    'ot_attn_bwd_dqkv_bf16_supported': (c_int, [c_int, c_int, c_int, c_int]),
+    'ot_attn_bwd_flags_workspace_size': (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int, c_int]),
+    'ot_attn_bwd_flags': (c_int, [P, I64, P, P, P, c_int, c_int, c_int, c_int, P, c_int, P, c_int, P, c_size_t, P]),
     'ot_attn_fwd_cached': (c_int, [P, I64, P, I64, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
     'ot_pyramid_select': (c_int, [P, c_float, c_int, c_int, c_int, c_int, P, P, P, c_int, P]),
     'ot_rmsnorm_fwd': (c_int, [P, I64, P, P, I64, P, I64, c_int, c_float, P]),

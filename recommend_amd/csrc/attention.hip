@@ -47,6 +47,10 @@ struct AttnArgs {
   // owning key blocks kgroup*s .. kgroup*s + kgroup-1; slice 0 writes dQ into dqkv, slice s > 0 into
   // dqpart[s - 1] ([B*K][d]), summed into dqkv by attn_dq_reduce_kernel
   int kslices, kgroup; float* dqpart;
+  // OT_ATTN_DQKV_BF16 (key-grouped backward only): dqkv holds bf16 (uint16 bits, ld in elements); every
+  // slice s writes its dQ into dqpart[s] and attn_dq_reduce_kernel stores the rounded sum (slice 0 first,
+  // then the later slices in order: the f32 path's sum, rounded once)
+  int dq_bf16;
 };
 
 // position of kept query j (< K) of the sample whose qpos slice is qp (null: the tail rule)
@@ -1209,8 +1213,9 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kerne
       const int jq = q0 + (ln & 31);
       const int dd = 32 * c + 8 * g + 4 * (ln >> 5);
       if (jq < K && dd < HD) {
-        float* dst = slice == 0 ? p.dqkv + (tok0 + q_off + jq) * p.ld + h * HD + dd
-                                : p.dqpart + ((int64_t)(slice - 1) * p.B * K + (int64_t)b * K + jq) * p.d + h * HD + dd;
+        const int ps = p.dq_bf16 ? slice : slice - 1;  // dqpart slot (bf16 output: slice 0 too)
+        float* dst = ps < 0 ? p.dqkv + (tok0 + q_off + jq) * p.ld + h * HD + dd
+                            : p.dqpart + ((int64_t)ps * p.B * K + (int64_t)b * K + jq) * p.d + h * HD + dd;
         *reinterpret_cast<f32x4*>(dst) = a;
       }
     }
@@ -1224,8 +1229,14 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kerne
         if (dd < HD) {
           f32x4 a = {dk[c][4 * g], dk[c][4 * g + 1], dk[c][4 * g + 2], dk[c][4 * g + 3]};
           f32x4 v = {dv[c][4 * g], dv[c][4 * g + 1], dv[c][4 * g + 2], dv[c][4 * g + 3]};
-          *reinterpret_cast<f32x4*>(dK + (int64_t)kpos * p.ld + dd) = a;
-          *reinterpret_cast<f32x4*>(dV + (int64_t)kpos * p.ld + dd) = v;
+          if (p.dq_bf16) {
+            uint16_t* dK16 = reinterpret_cast<uint16_t*>(p.dqkv) + tok0 * p.ld + p.d + h * HD;
+            *reinterpret_cast<u32x2*>(dK16 + (int64_t)kpos * p.ld + dd) = bf16_rne4(a);
+            *reinterpret_cast<u32x2*>(dK16 + p.d + (int64_t)kpos * p.ld + dd) = bf16_rne4(v);
+          } else {
+            *reinterpret_cast<f32x4*>(dK + (int64_t)kpos * p.ld + dd) = a;
+            *reinterpret_cast<f32x4*>(dV + (int64_t)kpos * p.ld + dd) = v;
+          }
         }
       }
   }
@@ -1242,16 +1253,23 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(AttnArgs p) {
   const int col = (int)(e4 - row * p.d);
   const int b = (int)(row / p.K), j = (int)(row - (int64_t)b * p.K);
   const int q_off = p.I - p.K, qb = j / 32;
+  const int o = p.dq_bf16 ? 0 : 1;                     // dqpart slot of slice s: s - o
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   bool any = false;
   for (int s = 1; s < p.kslices; ++s) {
     const int f = 32 * p.kgroup * s - q_off;           // first query block that sees the slice's first key
     if ((f < 0 ? 0 : f / 32) > qb) break;              // later slices start later still
-    acc += *reinterpret_cast<const f32x4*>(p.dqpart + (int64_t)(s - 1) * n + e4);
+    acc += *reinterpret_cast<const f32x4*>(p.dqpart + (int64_t)(s - o) * n + e4);
     any = true;
   }
+  const int64_t di = ((int64_t)b * p.I + q_off + j) * p.ld + col;
+  if (p.dq_bf16) {
+    const f32x4 d0 = *reinterpret_cast<const f32x4*>(p.dqpart + e4);
+    *reinterpret_cast<u32x2*>(reinterpret_cast<uint16_t*>(p.dqkv) + di) = bf16_rne4(any ? d0 + acc : d0);
+    return;
+  }
   if (!any) return;
-  f32x4* dst = reinterpret_cast<f32x4*>(p.dqkv + ((int64_t)b * p.I + q_off + j) * p.ld + col);
+  f32x4* dst = reinterpret_cast<f32x4*>(p.dqkv + di);
   *dst = *dst + acc;
 }
 
@@ -1575,9 +1593,19 @@ extern "C" size_t ot_attn_bwd_ex_workspace_size(int B, int H, int I, int K, int 
   return ot_attn_bwd_workspace_size(B, H, K) + (size_t)(S - 1) * B * K * H * head_dim * sizeof(float);
 }
 
+extern "C" int ot_attn_bwd_dqkv_bf16_supported(int I, int K, int head_dim, int selected) {
+  return attn_bwd_kgroup(I, K, head_dim, selected != 0) != 0;
+}
+
+extern "C" size_t ot_attn_bwd_flags_workspace_size(int B, int H, int I, int K, int head_dim, int selected, int flags) {
+  const int S = attn_bwd_kslices(B, H, I, K, head_dim, selected != 0);
+  const int slots = (flags & OT_ATTN_DQKV_BF16) ? S : S - 1;
+  return ot_attn_bwd_workspace_size(B, H, K) + (size_t)slots * B * K * H * head_dim * sizeof(float);
+}
+
 static int attn_bwd_impl(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
                          int B, int H, int I, int K, const int32_t* qpos, int head_dim, float* dqkv,
-                         float* delta_ws, size_t ws_bytes, void* stream);
+                         float* delta_ws, size_t ws_bytes, void* stream, int flags = 0);
 
 extern "C" int ot_attn_bwd(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
                            int B, int H, int I, int K, const int32_t* qpos, int head_dim, float* dqkv,
@@ -1594,9 +1622,23 @@ extern "C" int ot_attn_bwd_ex(const float* qkv, int64_t ld, const float* out, co
                        stream);
 }
 
+extern "C" int ot_attn_bwd_flags(const float* qkv, int64_t ld, const float* out, const float* dout,
+                                 const float* lse, int B, int H, int I, int K, const int32_t* qpos, int head_dim,
+                                 void* dqkv, int flags, void* workspace, size_t ws_bytes, void* stream) {
+  OT_REQUIRE(!(flags & ~OT_ATTN_DQKV_BF16), "ot_attn_bwd_flags: unknown flags %d", flags);
+  OT_REQUIRE(ws_bytes >= ot_attn_bwd_flags_workspace_size(B, H, I, K, head_dim, qpos != nullptr, flags),
+             "ot_attn_bwd_flags: workspace too small");
+  OT_REQUIRE(!(flags & OT_ATTN_DQKV_BF16) || ot_attn_bwd_dqkv_bf16_supported(I, K, head_dim, qpos != nullptr),
+             "ot_attn_bwd_flags: OT_ATTN_DQKV_BF16 needs the key-grouped bf16 backward (bf16 mode, tail queries, "
+             "head_dim 32 / 64, long tails: ot_attn_bwd_dqkv_bf16_supported)");
+  OT_REQUIRE(!(flags & OT_ATTN_DQKV_BF16) || ((uintptr_t)dqkv % 8) == 0, "ot_attn_bwd_flags: dqkv alignment");
+  return attn_bwd_impl(qkv, ld, out, dout, lse, B, H, I, K, qpos, head_dim, (float*)dqkv, (float*)workspace,
+                       ws_bytes, stream, flags);
+}
+
 static int attn_bwd_impl(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
                          int B, int H, int I, int K, const int32_t* qpos, int head_dim, float* dqkv,
-                         float* delta_ws, size_t ws_bytes, void* stream) {
+                         float* delta_ws, size_t ws_bytes, void* stream, int flags) {
   OT_REQUIRE(qkv && out && dout && lse && dqkv && delta_ws, "ot_attn_bwd: null operand");
   OT_REQUIRE(B >= 0 && H > 0 && I > 0 && K > 0 && K <= I, "ot_attn_bwd: bad sizes");
   OT_REQUIRE(ld % 4 == 0 && ld >= 3 * H * head_dim, "ot_attn_bwd: bad ld");
@@ -1621,6 +1663,7 @@ static int attn_bwd_impl(const float* qkv, int64_t ld, const float* out, const f
     p.kslices = S;
     p.kgroup = G;
     p.dqpart = delta_ws + ot_attn_bwd_workspace_size(B, H, K) / sizeof(float);
+    p.dq_bf16 = (flags & OT_ATTN_DQKV_BF16) ? 1 : 0;
     void (*kern)(AttnArgs) = G == 8 ? (head_dim == 32 ? attn_bwd_group_kernel<32, 8> : attn_bwd_group_kernel<64, 8>)
                                     : (head_dim == 32 ? attn_bwd_group_kernel<32, 4> : attn_bwd_group_kernel<64, 4>);
     const size_t lds = G == 8 ? (head_dim == 32 ? BWDG_LDS<32, 8>() : BWDG_LDS<64, 8>())
@@ -1633,7 +1676,7 @@ static int attn_bwd_impl(const float* qkv, int64_t ld, const float* out, const f
       (void)hipGetLastError();
     });
     hipLaunchKernelGGL(kern, dim3((unsigned)((int64_t)B * H * S)), dim3(64 * G), lds, (hipStream_t)stream, p);
-    if (S > 1) {
+    if (S > 1 || p.dq_bf16) {
       OT_LAUNCH_CHECK("ot_attn_bwd");
       hipLaunchKernelGGL(attn_dq_reduce_kernel, dim3(ceil_div((int64_t)B * K * p.d / 4, 256)), dim3(256), 0,
                          (hipStream_t)stream, p);

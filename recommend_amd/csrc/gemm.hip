@@ -1562,6 +1562,7 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
     OT_PSPEC_BF(OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_ROW_RSTD)
     OT_PSPEC_BF(OT_EPI_RMSNORM_BWD)
     OT_PSPEC_BF(OT_EPI_RMSNORM_BWD | OT_EPI_DROPOUT)
+    OT_PSPEC_BF(0)
 #undef OT_PSPEC_BF
     if (pk) { kern = pk; plane = true; }
   }

@@ -265,11 +265,19 @@ def attn_fwd(qkv: torch.Tensor, ld: int, B: int, H: int, I: int, K: int, hd: int
                    f'fwd{"_fp8" if fp8 else ""} I{I} K{K} hd{hd}')
 
 
+def attn_bwd_bf16_supported(I, K, hd, qpos=None) -> bool:
+    """ot_attn_bwd_dqkv_bf16_supported: can the backward emit dqkv in bf16 (key-grouped bf16 kernel)?"""
+    return bool(_lib.load().ot_attn_bwd_dqkv_bf16_supported(I, K, hd, int(qpos is not None)))
+
+
 def attn_bwd(qkv, ld, out, dout, lse, B, H, I, K, hd, dqkv, qpos=None) -> None:
-    ws = workspace(size('ot_attn_bwd_ex_workspace_size', B, H, I, K, hd, int(qpos is not None)), qkv.device)
+    """dqkv float32, or int16 (bf16 bits: OT_ATTN_DQKV_BF16, see attn_bwd_bf16_supported)."""
+    flags = _lib.OT_ATTN_DQKV_BF16 if dqkv.dtype == torch.int16 else 0
+    ws = workspace(size('ot_attn_bwd_flags_workspace_size', B, H, I, K, hd, int(qpos is not None), flags),
+                   qkv.device)
     ev = _probe.begin() if _probe is not None else None
-    call('ot_attn_bwd_ex', ptr(qkv), ld, ptr(out), ptr(dout), ptr(lse), B, H, I, K, ptr(qpos), hd, ptr(dqkv),
-         ptr(ws), ws.numel(), stream())
+    call('ot_attn_bwd_flags', ptr(qkv), ld, ptr(out), ptr(dout), ptr(lse), B, H, I, K, ptr(qpos), hd, ptr(dqkv),
+         flags, ptr(ws), ws.numel(), stream())
     if ev is not None:
         _probe.end('attention', 8.0 * (K * I - K * (K - 1) / 2) * hd * H * B, ev, f'bwd I{I} K{K} hd{hd}')
 

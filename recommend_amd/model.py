@@ -377,18 +377,25 @@ class _Block(torch.autograd.Function):
         K.gemm(OT_GEMM_NT, dyo, d, d, mt['rows'][1], m.p(f'blk.{l}.wo'), 0, d, d, mt['tile_group'], nt, do, d,
                mt['rows'][1], m_rows=maps['tail'].nrows, bimg=m.bimg(f'blk.{l}.wo', 'dgrad'))
         # attention
-        dqkv = torch.empty(B * I, 3 * d, device=dev)
+        # bf16 mode, key-grouped backward (C5): dQKV in bf16 (OT_ATTN_DQKV_BF16) — the QKV dgrad (bf16 A) and
+        # the Wqkv weight gradient (OT_WG_D_BF16) round it to bf16 anyway: the same values, half the bytes
+        qp = _attn_qpos(cfg, pos)
+        dq_bf = (m.dqkv_bf16 and K.matmul_mode() == 'bf16' and K.attn_bwd_bf16_supported(I, Kq, hd, qp)
+                 and m.bimg(f'blk.{l}.wqkv', 'dgrad') is not None)
+        dqkv = torch.empty(B * I, 3 * d, device=dev, dtype=torch.int16 if dq_bf else torch.float32)
         if Kq < I:
             dqkv[:, :d].zero_()
-        K.attn_bwd(qkv, 3 * d, o, do, lse, B, H, I, Kq, hd, dqkv, qpos=_attn_qpos(cfg, pos))
+        K.attn_bwd(qkv, 3 * d, o, do, lse, B, H, I, Kq, hd, dqkv, qpos=qp)
         with m.side(x, dqkv, rstd1):
             K.wgrad(x, d, ma['rows'][0], dqkv, 3 * d, ma['rows'][0], d, 3 * d, ma, nca, G, m.g(f'blk.{l}.wqkv'),
-                    3 * d * d, None, 0, a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=m.p(f'blk.{l}.norm1'),
-                    accumulate=acc, device=dev, m_rows=maps['all'].nrows, rowmap=maps['all'])
+                    3 * d * d, None, 0, a_xform=OT_AX_RMSNORM | (OT_WG_D_BF16 if dq_bf else 0), rstd=rstd1,
+                    gamma=m.p(f'blk.{l}.norm1'), accumulate=acc, device=dev, m_rows=maps['all'].nrows,
+                    rowmap=maps['all'])
+        ax_dq = OT_AX_BF16 if dq_bf else 0
         dx = torch.empty(B * I, d, device=dev)
         if m.fuse_bwd:         # QKV dgrad -> norm1 backward + residual (dx1 on the kept tail rows)
             K.gemm_rms(OT_GEMM_NT, dqkv, 3 * d, 3 * d, ma['rows'][0], m.p(f'blk.{l}.wqkv'), 3 * d * d, 3 * d, d,
-                       ma['tile_group'], na, dx, d, ma['rows'][0], epi=OT_EPI_RMSNORM_BWD,
+                       ma['tile_group'], na, dx, d, ma['rows'][0], epi=OT_EPI_RMSNORM_BWD, a_xform=ax_dq,
                        m_rows=maps['all'].nrows, nx=x, ldnx=d, ngamma=m.p(f'blk.{l}.norm1'), nrstd=rstd1,
                        dres=dx1, lddres=d, dres_tail=(Kq, I, inv) if Kq < I else (0, 0),
                        dgamma=m.g(f'blk.{l}.norm1'), accumulate_dgamma=acc, device=dev,
@@ -396,7 +403,7 @@ class _Block(torch.autograd.Function):
         else:
             dxn1 = torch.empty(B * I, d, device=dev)
             K.gemm(OT_GEMM_NT, dqkv, 3 * d, 3 * d, ma['rows'][0], m.p(f'blk.{l}.wqkv'), 3 * d * d, 3 * d, d,
-                   ma['tile_group'], na, dxn1, d, ma['rows'][0], m_rows=maps['all'].nrows,
+                   ma['tile_group'], na, dxn1, d, ma['rows'][0], m_rows=maps['all'].nrows, a_xform=ax_dq,
                    bimg=m.bimg(f'blk.{l}.wqkv', 'dgrad'))
             K.rmsnorm_bwd(dxn1, d, x, d, m.p(f'blk.{l}.norm1'), rstd1, dx, d, B * I, d, dres=dx1, lddres=d,
                           dres_tail=(Kq, I, inv) if Kq < I else (0, 0), dgamma=m.g(f'blk.{l}.norm1'), accumulate=acc,
@@ -591,6 +598,8 @@ class OneTransModel(nn.Module):
         self.store_gelu_fwd = sg not in ('0', 'bwd')
         # bf16 mode with the stored GELU: dU in bf16 (ONETRANS_DU_BF16=0: f32)
         self.du_bf16 = os.environ.get('ONETRANS_DU_BF16', '1') != '0'
+        # bf16 mode, key-grouped attention backward: dQKV in bf16 (ONETRANS_DQKV_BF16=0: f32)
+        self.dqkv_bf16 = os.environ.get('ONETRANS_DQKV_BF16', '1') != '0'
         # block weight gradients run on a second stream, overlapping the dgrad chain
         self.overlap_wgrad = os.environ.get('ONETRANS_OVERLAP_WGRAD', '1') != '0'
         self._side = None

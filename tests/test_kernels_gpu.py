@@ -642,7 +642,8 @@ def test_attn_bwd_key_slices(dev, B, H, I, Kq, hd):
     consecutive key blocks and stream the query blocks once, dQ partials of later groups reduced after):
     dK / dV bit-identical to the one-wave-per-pair backward (ot_attn_bwd), dQ equal up to the f32 order
     of the groups' partial sums; tail offsets (Kq < I) exercise which groups a query block sees, idle
-    waves (key blocks past the end) and padded query blocks."""
+    waves (key blocks past the end) and padded query blocks.  The bf16 output form (OT_ATTN_DQKV_BF16) is
+    the sliced f32 result rounded to nearest even, bit for bit."""
     from recommend_amd import _lib
     old = K.set_matmul_mode('bf16')
     try:
@@ -671,6 +672,12 @@ def test_attn_bwd_key_slices(dev, B, H, I, Kq, hd):
         scale = b[:, :d].abs().max().item()
         assert (a[:, :d] - b[:, :d]).abs().max().item() <= 1e-5 * scale       # dQ
         assert torch.isfinite(a).all()
+        # bf16 dqkv (OT_ATTN_DQKV_BF16): each element the sliced f32 result rounded to nearest even
+        assert K.attn_bwd_bf16_supported(I, Kq, hd)
+        d16 = torch.zeros(B * I, 3 * d, dtype=torch.int16, device=dev)
+        K.attn_bwd(qkv, 3 * d, out, dout, lse, B, H, I, Kq, hd, d16)
+        torch.cuda.synchronize()
+        assert torch.equal(d16.cpu(), a.to(torch.bfloat16).view(torch.int16))
     finally:
         K.set_matmul_mode(old)
 

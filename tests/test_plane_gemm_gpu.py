@@ -312,3 +312,29 @@ def test_plane_gemm_bf16_du(dev, plane_mode):
     assert torch.equal(wg[0][0], wg[1][0])
     scale = wg[0][1].abs().max().item()
     assert (wg[0][1] - wg[1][1]).abs().max().item() < 1e-2 * scale
+
+
+@pytest.mark.parametrize('K_,N', [(1536, 512), (384, 128)])
+def test_plane_gemm_bf16_a_plain(dev, plane_mode, K_, N):
+    """bf16 mode, no prologue / epilogue (the QKV dgrad from the attention backward's bf16 dQKV): a bf16 A
+    operand (OT_AX_BF16) gives the same C, bit for bit, as its f32 source (rounded at fragment time)."""
+    if plane_mode != 'bf16':
+        pytest.skip('bf16 A operands are a bf16-mode form')
+    from recommend_amd._lib import OT_AX_BF16
+    rng = np.random.default_rng(K_)
+    G, M = 3, 901
+    rm = ragged_map(rng, M, G)
+    dm = rm.to(dev)
+    A = torch.randn(M, K_, device=dev)
+    A16 = A.to(torch.bfloat16).view(torch.int16)
+    W = torch.randn(G, N, K_) / math.sqrt(K_)
+    img, ntn = make_image(W, dev)
+    outs = []
+    for a, ax in ((A, OT_AX_NONE), (A16, OT_AX_BF16)):
+        C = torch.full((M, N), float('nan'), device=dev)
+        K.gemm(OT_GEMM_NT, a, K_, K_, dm['rows'][0], W.to(dev), N * K_, K_, N, dm['tile_group'], rm.ntiles, C, N,
+               dm['rows'][1], a_xform=ax, bimg=(img, ntn, 0))
+        outs.append(C)
+    torch.cuda.synchronize()
+    assert not torch.isnan(outs[1]).any()
+    assert torch.equal(outs[0], outs[1])

@@ -74,8 +74,11 @@ extern "C" {
                                    with OT_EPI_DROPOUT also dx_masked = mask(C) (C itself unmasked) */
 #define OT_EPI_C_BF16 512       /* C is stored rounded to bf16 (uint16 bits, ldc in elements; 8-B aligned
                                    rows).  Plane GEMM in the bf16 mode, with OT_EPI_GELU_BWD [| OT_EPI_ROWDOT]
-                                   only (the FFN2 dgrad: dU, whose consumers — the FFN1 dgrad and the W1
-                                   weight gradient — round it to bf16 anyway) */
+                                   [| OT_EPI_AUX_BF16] (the FFN2 dgrad: dU, whose consumers — the FFN1 dgrad
+                                   and the W1 weight gradient — round it to bf16 anyway) or with OT_EPI_BIAS
+                                   alone (the FFN1 forward: U, read only by the FFN2 dgrad's GELU') */
+#define OT_EPI_AUX_BF16 1024    /* with OT_EPI_GELU_BWD: aux holds bf16 (uint16 bits, ldaux in elements) — the
+                                   bf16 mode's stored pre-activation U (plane GEMM, OT_MATMUL_BF16 only) */
 /* ot_mixed_gemm_wgrad: or'ed into a_xform, D holds bf16 values (uint16 bits, ldd in elements; 8-B aligned
  * rows; OT_MATMUL_BF16 / split modes) — dU stored by OT_EPI_C_BF16 */
 #define OT_WG_D_BF16 8

@@ -21,6 +21,7 @@ OT_EPI_BIAS, OT_EPI_GELU_BWD, OT_EPI_GELU = 1, 2, 4
 OT_EPI_DROPOUT, OT_EPI_RESIDUAL, OT_EPI_ACCUMULATE = 8, 16, 32
 OT_EPI_ROW_RSTD, OT_EPI_RMSNORM_BWD, OT_EPI_ROWDOT = 64, 128, 256
 OT_EPI_C_BF16 = 512
+OT_EPI_AUX_BF16 = 1024
 OT_ATTN_DQKV_BF16 = 1
 OT_WG_D_BF16 = 8
 OT_MATMUL_F32, OT_MATMUL_SPLIT_BF16, OT_MATMUL_BF16 = 0, 1, 2

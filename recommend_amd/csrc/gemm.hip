@@ -156,8 +156,10 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
     constexpr bool RMSBWD = EPIT >= 0 && (EPIT & OT_EPI_RMSNORM_BWD);
     constexpr bool ROWRSTD = EPIT >= 0 && (EPIT & OT_EPI_ROW_RSTD);
     constexpr bool ROWDOT = EPIT >= 0 && (EPIT & OT_EPI_ROWDOT);
-    constexpr bool GSTORE = EPIT == OT_EPI_BIAS;        // gelu_out of a bias-only epilogue: gelu(C)
+    // gelu_out of a bias-only epilogue: gelu(C) (C in f32 or bf16)
+    constexpr bool GSTORE = EPIT == OT_EPI_BIAS || EPIT == (OT_EPI_BIAS | OT_EPI_C_BF16);
     constexpr bool CBF = EPIT >= 0 && (EPIT & OT_EPI_C_BF16);
+    constexpr bool AUXBF = EPIT >= 0 && (EPIT & OT_EPI_AUX_BF16);
     f32x4 rdb4 = {0.f, 0.f, 0.f, 0.f};                 // OT_EPI_ROWDOT: the bias subtracted from aux
     if (ROWDOT) rdb4 = *reinterpret_cast<const f32x4*>(p.bias + (int64_t)g * p.bias_gstride + col);
     // dgamma partials live in a thread-private LDS slot behind ct (a register accumulator here
@@ -217,7 +219,13 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
               if (dr >= 0) dr4[i] = *reinterpret_cast<const f32x4*>(p.dres + (int64_t)dr * p.lddres + col);
             }
           }
-          if (epi & OT_EPI_GELU_BWD) aux4[i] = *reinterpret_cast<const f32x4*>(p.aux + o * p.ldaux + col);
+          if (AUXBF) {
+            const u32x2 w = *reinterpret_cast<const u32x2*>(reinterpret_cast<const uint16_t*>(p.aux) + o * p.ldaux + col);
+            aux4[i] = f32x4{__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u),
+                            __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u)};
+          } else if (epi & OT_EPI_GELU_BWD) {
+            aux4[i] = *reinterpret_cast<const f32x4*>(p.aux + o * p.ldaux + col);
+          }
           if (epi & OT_EPI_RESIDUAL)
             res4[i] = *reinterpret_cast<const f32x4*>(p.res + (p.res_tok ? tok[i] : o) * p.ldres + col);
           if (epi & OT_EPI_ACCUMULATE) cp4[i] = *reinterpret_cast<const f32x4*>(p.C + o * p.ldc + col);
@@ -1424,7 +1432,8 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
                                        lda % 8 == 0 && ((uintptr_t)A % 16) == 0),
              "ot_mixed_gemm: OT_AX_BF16 (bf16 A) needs the bf16 mode, a B image (plane GEMM), NT mode and 16-B "
              "aligned rows");
-  OT_REQUIRE(!rms || !rms->gelu_out || (((epi & OT_EPI_GELU_BWD) || epi == OT_EPI_BIAS) && rms->ldgelu % 4 == 0 &&
+  OT_REQUIRE(!rms || !rms->gelu_out || (((epi & OT_EPI_GELU_BWD) || (epi & ~OT_EPI_C_BF16) == OT_EPI_BIAS) &&
+                                        rms->ldgelu % 4 == 0 &&
                                         ((uintptr_t)rms->gelu_out % 8) == 0),
              "ot_mixed_gemm_rms: gelu_out needs OT_EPI_GELU_BWD or epi == OT_EPI_BIAS, ldgelu %% 4 == 0 and 8-B "
              "alignment");
@@ -1437,7 +1446,8 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
     OT_REQUIRE(N == GT || !(epi & OT_EPI_ROW_RSTD) ||
                    (rms->workspace && rms->ws_bytes >= ot_mixed_gemm_rms_workspace_size(ntiles, N)),
                "ot_mixed_gemm_rms: OT_EPI_ROW_RSTD with N > %d needs the workspace", GT);
-    OT_REQUIRE(!(epi & OT_EPI_ROWDOT) || ((epi & OT_EPI_GELU_BWD) && !(epi & ~(OT_EPI_GELU_BWD | OT_EPI_ROWDOT | OT_EPI_C_BF16)) &&
+    OT_REQUIRE(!(epi & OT_EPI_ROWDOT) || ((epi & OT_EPI_GELU_BWD) &&
+                                          !(epi & ~(OT_EPI_GELU_BWD | OT_EPI_ROWDOT | OT_EPI_C_BF16 | OT_EPI_AUX_BF16)) &&
                                           rms->rowdot && rms->rowdot_n == N / GT && bias),
                "ot_mixed_gemm_rms: OT_EPI_ROWDOT goes with OT_EPI_GELU_BWD only and needs rowdot[rows][N / %d] and "
                "the bias", GT);
@@ -1459,7 +1469,7 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
   p.tail_pos = tail_pos;
   p.bimg = bimg; p.bimg_ntn = bimg_ntn; p.bimg_tn0 = bimg_tn0;
   float* dgpart = nullptr;
-  if (rms && ((epi & OT_EPI_GELU_BWD) || epi == OT_EPI_BIAS)) {   // the stored GELU (optional)
+  if (rms && ((epi & OT_EPI_GELU_BWD) || (epi & ~OT_EPI_C_BF16) == OT_EPI_BIAS)) {   // the stored GELU (optional)
     p.gelu_out = rms->gelu_out;
     p.ldgelu = rms->ldgelu;
   }
@@ -1555,6 +1565,14 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
       pk = plane_gemm_kernel<OT_AX_NONE, OT_EPI_GELU_BWD | OT_EPI_ROWDOT | OT_EPI_C_BF16, 3, 4, 1>;
     if (one && x == OT_AX_NONE && e == (OT_EPI_GELU_BWD | OT_EPI_C_BF16))
       pk = plane_gemm_kernel<OT_AX_NONE, OT_EPI_GELU_BWD | OT_EPI_C_BF16, 3, 4, 1>;
+    if (one && x == OT_AX_NONE && e == (OT_EPI_GELU_BWD | OT_EPI_ROWDOT | OT_EPI_C_BF16 | OT_EPI_AUX_BF16))
+      pk = plane_gemm_kernel<OT_AX_NONE, OT_EPI_GELU_BWD | OT_EPI_ROWDOT | OT_EPI_C_BF16 | OT_EPI_AUX_BF16, 3, 4, 1>;
+    if (one && x == OT_AX_NONE && e == (OT_EPI_GELU_BWD | OT_EPI_C_BF16 | OT_EPI_AUX_BF16))
+      pk = plane_gemm_kernel<OT_AX_NONE, OT_EPI_GELU_BWD | OT_EPI_C_BF16 | OT_EPI_AUX_BF16, 3, 4, 1>;
+    if (one && x == OT_AX_NONE && e == (OT_EPI_GELU_BWD | OT_EPI_ROWDOT | OT_EPI_AUX_BF16))
+      pk = plane_gemm_kernel<OT_AX_NONE, OT_EPI_GELU_BWD | OT_EPI_ROWDOT | OT_EPI_AUX_BF16, 3, 4, 1>;
+    if (one && x == OT_AX_RMSNORM && e == (OT_EPI_BIAS | OT_EPI_C_BF16))
+      pk = plane_gemm_kernel<OT_AX_RMSNORM, OT_EPI_BIAS | OT_EPI_C_BF16, 3, 4, 1>;
 #define OT_PSPEC_BF(EP_) if (one && x == OT_AX_BF16 && e == (EP_)) pk = plane_gemm_kernel<OT_AX_BF16, EP_, 3, 4, 1>;
     OT_PSPEC_BF(OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_DROPOUT)
     OT_PSPEC_BF(OT_EPI_BIAS | OT_EPI_RESIDUAL)
@@ -1568,8 +1586,9 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
   }
   OT_REQUIRE(x != OT_AX_BF16 || plane, "ot_mixed_gemm: no plane GEMM for OT_AX_BF16 with epilogue %d (or edge tiles)",
              epi);
-  OT_REQUIRE(!(epi & OT_EPI_C_BF16) || plane, "ot_mixed_gemm: OT_EPI_C_BF16 needs the bf16-mode plane GEMM with "
-             "OT_EPI_GELU_BWD [| OT_EPI_ROWDOT] (epilogue %d)", epi);
+  OT_REQUIRE(!(epi & (OT_EPI_C_BF16 | OT_EPI_AUX_BF16)) || plane,
+             "ot_mixed_gemm: OT_EPI_C_BF16 / OT_EPI_AUX_BF16 need the bf16-mode plane GEMM with OT_EPI_GELU_BWD "
+             "[| OT_EPI_ROWDOT] or OT_EPI_BIAS alone (epilogue %d)", epi);
   OT_REQUIRE(!p.gelu_out || (!edge && (kern != nullptr)), "ot_mixed_gemm_rms: gelu_out needs whole tiles");
   OT_REQUIRE(!p.rowpart || plane, "ot_mixed_gemm_rms: OT_EPI_ROW_RSTD with N = %d > %d needs the plane GEMM "
              "(split mode, a pre-split B image, 16-B aligned A)", N, GT);

@@ -27,9 +27,9 @@ import torch.nn as nn
 
 from . import _lib
 from . import kernels as K
-from ._lib import (OT_AX_BF16, OT_AX_GELU, OT_AX_RMSNORM, OT_EPI_ACCUMULATE, OT_EPI_BIAS, OT_EPI_C_BF16, OT_EPI_DROPOUT,
-                   OT_EPI_GELU_BWD, OT_EPI_RESIDUAL, OT_EPI_RMSNORM_BWD, OT_EPI_ROW_RSTD, OT_EPI_ROWDOT, OT_GEMM_NN,
-                   OT_GEMM_NT, OT_WG_D_BF16, NS_FIELD_BYTES)
+from ._lib import (OT_AX_BF16, OT_AX_GELU, OT_AX_RMSNORM, OT_EPI_ACCUMULATE, OT_EPI_AUX_BF16, OT_EPI_BIAS,
+                   OT_EPI_C_BF16, OT_EPI_DROPOUT, OT_EPI_GELU_BWD, OT_EPI_RESIDUAL, OT_EPI_RMSNORM_BWD,
+                   OT_EPI_ROW_RSTD, OT_EPI_ROWDOT, OT_GEMM_NN, OT_GEMM_NT, OT_WG_D_BF16, NS_FIELD_BYTES)
 from .config import OneTransConfig, check_pyramid_select, get_model_config
 from .layout import TILE, FlatLayout, RowMap, build_map, head_map, identity_map, layer_maps, round_up
 from .params import init_params, ns_table_offsets
@@ -216,16 +216,20 @@ def _block_forward(m, l, x, I, Kq, seed, training, rstd_in=None, select=False, n
                tail=tail, m_rows=maps['tail'].nrows, bimg=m.bimg(f'blk.{l}.wo'))
         K.rmsnorm_fwd(x1, d, B * Kq, d, rstd2, eps=RMS_EPS)
     # u = norm2(x1) @ W1[g] + b1[g]  (pre-activation; GELU applied by its consumers)
-    u = torch.empty(B * Kq, f, device=dev)
     # bf16 mode: the FFN1 epilogue also stores h = gelu(u) rounded to bf16 — exactly the operand the bf16
     # FFN2 GEMM would form at fragment time — so FFN2 reads 2 B per element and evaluates no erf (it did,
     # once per output column tile), and the W2 weight gradient reuses h
     w2img = m.bimg(f'blk.{l}.w2')
     h = (torch.empty(B * Kq, f, dtype=torch.int16, device=dev)
          if m.store_gelu_fwd and K.matmul_mode() == 'bf16' and w2img is not None and f % 8 == 0 else None)
+    # ... and u itself in bf16 (as a bf16 Keras policy stores it): its one reader is then the FFN2 dgrad's
+    # GELU' / row-dot epilogue (OT_EPI_AUX_BF16), which needs the fused norm2 backward's bf16-dU form
+    u_bf = h is not None and m.u_bf16 and m.du_bf16 and m.fuse_bwd2 and not m.fuse_bwd and f % TILE == 0
+    u = torch.empty(B * Kq, f, device=dev, dtype=torch.int16 if u_bf else torch.float32)
     if h is not None:
         K.gemm_rms(OT_GEMM_NT, x1, d, d, mt['rows'][1], w1, d * f, d, f, mt['tile_group'], nt, u, f, mt['rows'][1],
-                   a_xform=OT_AX_RMSNORM, rstd=rstd2, gamma=g2, bias=b1, bias_gstride=f, epi=OT_EPI_BIAS,
+                   a_xform=OT_AX_RMSNORM, rstd=rstd2, gamma=g2, bias=b1, bias_gstride=f,
+                   epi=OT_EPI_BIAS | (OT_EPI_C_BF16 if u_bf else 0),
                    m_rows=maps['tail'].nrows, bimg=m.bimg(f'blk.{l}.w1'), gelu_out=h, ldgelu=f)
     else:
         K.gemm(OT_GEMM_NT, x1, d, d, mt['rows'][1], w1, d * f, d, f, mt['tile_group'], nt, u, f, mt['rows'][1],
@@ -333,7 +337,8 @@ class _Block(torch.autograd.Function):
             # d > 128: the FFN2 dgrad also emits rowdot[row][f-tile] = sum dU (U - b1) for the norm2 backward
             rowdot = torch.empty(B * Kq, f // TILE, device=dev)
             K.gemm_rms(OT_GEMM_NT, dy2, d, d, mt['rows'][1], m.p(f'blk.{l}.w2'), f * d, d, f, mt['tile_group'], nt,
-                       du, f, mt['rows'][1], epi=OT_EPI_GELU_BWD | OT_EPI_ROWDOT | cbf, aux=u, ldaux=f,
+                       du, f, mt['rows'][1], aux=u, ldaux=f,
+                       epi=OT_EPI_GELU_BWD | OT_EPI_ROWDOT | cbf | (OT_EPI_AUX_BF16 if u.dtype == torch.int16 else 0),
                        bias=m.p(f'blk.{l}.b1'), bias_gstride=f, rowdot=rowdot, rowdot_n=f // TILE,
                        m_rows=maps['tail'].nrows, device=dev, bimg=m.bimg(f'blk.{l}.w2', 'dgrad'),
                        gelu_out=hbf, ldgelu=f)
@@ -600,6 +605,8 @@ class OneTransModel(nn.Module):
         self.du_bf16 = os.environ.get('ONETRANS_DU_BF16', '1') != '0'
         # bf16 mode, key-grouped attention backward: dQKV in bf16 (ONETRANS_DQKV_BF16=0: f32)
         self.dqkv_bf16 = os.environ.get('ONETRANS_DQKV_BF16', '1') != '0'
+        # bf16 mode with the stored GELU and bf16 dU: the FFN1 pre-activation U in bf16 (ONETRANS_U_BF16=0: f32)
+        self.u_bf16 = os.environ.get('ONETRANS_U_BF16', '1') != '0'
         # block weight gradients run on a second stream, overlapping the dgrad chain
         self.overlap_wgrad = os.environ.get('ONETRANS_OVERLAP_WGRAD', '1') != '0'
         self._side = None

@@ -188,7 +188,7 @@ def test_plane_gemm_stored_gelu(dev, plane_mode, f, N, rstd_epi):
     to bf16 (torch float64 erf: at most one bf16 ulp apart), and in the bf16 mode the FFN2 output (and the
     next norm's rstd) from h is bit-identical to the one that forms gelu(U) at fragment time (OT_AX_GELU:
     the same rounding of the same values).  The split mode refuses a bf16 A operand."""
-    from recommend_amd._lib import OT_AX_BF16, OneTransHipError
+    from recommend_amd._lib import OT_AX_BF16, OT_EPI_C_BF16, OneTransHipError
     rng = np.random.default_rng(f + N)
     G, B, I, Kq, d = 3, 53, 9, 5, N
     M = B * Kq
@@ -212,8 +212,15 @@ def test_plane_gemm_stored_gelu(dev, plane_mode, f, N, rstd_epi):
     h = torch.zeros(M, f, dtype=torch.int16, device=dev)
     K.gemm_rms(OT_GEMM_NT, x, d, d, dm['rows'][0], W1.to(dev), f * d, d, f, dm['tile_group'], rm.ntiles, U, f, rows,
                gelu_out=h, ldgelu=f, device=dev, **kw1)
+    if plane_mode == 'bf16':            # U itself in bf16 (OT_EPI_C_BF16): U rounded, the same h
+        U16 = torch.zeros(M, f, dtype=torch.int16, device=dev)
+        h2 = torch.zeros(M, f, dtype=torch.int16, device=dev)
+        K.gemm_rms(OT_GEMM_NT, x, d, d, dm['rows'][0], W1.to(dev), f * d, d, f, dm['tile_group'], rm.ntiles, U16, f,
+                   rows, gelu_out=h2, ldgelu=f, device=dev, **dict(kw1, epi=OT_EPI_BIAS | OT_EPI_C_BF16))
     torch.cuda.synchronize()
     assert torch.equal(U, U0)
+    if plane_mode == 'bf16':
+        assert torch.equal(U16, U.to(torch.bfloat16).view(torch.int16)) and torch.equal(h2, h)
     ref = (0.5 * U.double() * (1 + torch.erf(U.double() / math.sqrt(2)))).float().to(torch.bfloat16).cpu().float()
     got = h.view(torch.bfloat16).cpu().float()
     # (+ 1e-6 absolute: for U < -3 the f32 1 + erf(U / sqrt 2) cancels; gelu there is below 2e-3)
@@ -289,6 +296,18 @@ def test_plane_gemm_bf16_du(dev, plane_mode):
     torch.cuda.synchronize()
     assert torch.equal(rds[0], rds[1])
     assert torch.equal(dus[0].to(torch.bfloat16).view(torch.int16), dus[1])
+    # U in bf16 (OT_EPI_AUX_BF16): the same dU / row dots as from its values widened to f32
+    from recommend_amd._lib import OT_EPI_AUX_BF16
+    U16 = U.to(torch.bfloat16)
+    aux_outs = []
+    for aux, af in ((U16.float(), 0), (U16.view(torch.int16), OT_EPI_AUX_BF16)):
+        du = torch.zeros(M, f, device=dev, dtype=torch.int16)
+        rd = torch.full((M, f // 128), float('nan'), device=dev)
+        K.gemm_rms(OT_GEMM_NT, dy, d, d, rows, W2.to(dev), f * d, d, f, dm['tile_group'], rm.ntiles, du, f, rows,
+                   rowdot=rd, **dict(kw, aux=aux, epi=kw['epi'] | OT_EPI_C_BF16 | af))
+        aux_outs.append((du, rd))
+    torch.cuda.synchronize()
+    assert torch.equal(aux_outs[0][0], aux_outs[1][0]) and torch.equal(aux_outs[0][1], aux_outs[1][1])
     # FFN1 dgrad -> norm2 backward, from f32 dU and from bf16 dU
     outs = []
     for du, ax in ((dus[0], 0), (dus[1], OT_AX_BF16)):

@@ -141,6 +141,12 @@ typedef struct ot_rms_epilogue {
                                                           the FFN2 GEMM's and its weight gradient's A operand in
                                                           the bf16 mode (OT_AX_BF16): they neither read f32 U nor
                                                           re-evaluate erf.  No other row-norm field is needed */
+  uint16_t* xn_out; int64_t ldxn;                      /* optional, with the RMSNorm prologue on the plane GEMM:
+                                                          also bf16((A * gamma) * rstd) of every A row [in_row][k]
+                                                          (written by the first column tile's workgroups) — the
+                                                          normalised operand of the bf16-mode weight gradient
+                                                          (OT_AX_BF16), so it neither re-reads f32 A nor
+                                                          re-applies the norm */
 } ot_rms_epilogue;
 size_t ot_mixed_gemm_rms_workspace_size(int ntiles, int N);
 int ot_mixed_gemm_rms(int mode, const float* A, int64_t lda, int K, const int32_t* in_rows,

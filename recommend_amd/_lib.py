@@ -39,7 +39,8 @@ class RmsEpilogue(ctypes.Structure):
                 ('dgamma', c_void_p), ('accumulate_dgamma', c_int),
                 ('workspace', c_void_p), ('ws_bytes', c_size_t),
                 ('rowdot', c_void_p), ('rowdot_n', c_int),
-                ('gelu_out', c_void_p), ('ldgelu', c_int64)]
+                ('gelu_out', c_void_p), ('ldgelu', c_int64),
+                ('xn_out', c_void_p), ('ldxn', c_int64)]
 
 P = c_void_p
 I64 = c_int64

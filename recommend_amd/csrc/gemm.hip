@@ -94,6 +94,9 @@ struct GemmArgs {
   const int32_t* tail_pos;                      // kept positions (ot_pyramid_select) or null (tail)
   // plane GEMM: pre-split B image (ot_split_images), its tiles per group and the first tile used
   const uint16_t* bimg; int bimg_ntn, bimg_tn0;
+  // plane GEMM with the RMSNorm prologue: the first column tile's workgroups also store bf16(a * gamma * rstd)
+  // of their A rows (the bf16 weight gradient's normalised A operand)
+  uint16_t* xn_out; int64_t ldxn;
 };
 
 // sum over the 32 lanes that hold one output row in the vector epilogue (same order as the
@@ -798,6 +801,20 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
   const int boff = PG_A_BYTES + li * 32 + 16 * (h ^ ((li >> 3) & 1));
   const int aoffb = ra * 32 + 16 * (h ^ ((li >> 3) & 1));  // bf16 A
 
+  // normalised-A side output (AXT == OT_AX_RMSNORM, first column tile): this lane's fragment row ra
+  bool xnw = false;
+  float xrs = 0.f;
+  uint16_t* xnp = nullptr;
+  if (AXT == OT_AX_RMSNORM && p.xn_out && tn == 0) {
+    const int64_t xgr = (int64_t)tm * GT + ra;
+    const int xir = p.in_rows ? p.in_rows[xgr] : (int)xgr;
+    xnw = xir >= 0;
+    if (xnw) {
+      xrs = p.a_rstd[xir];
+      xnp = p.xn_out + (int64_t)xir * p.ldxn + 8 * h;
+    }
+  }
+
   issue(0, 0);
   if (NSTG == 3 && nk > 1) issue(1, 1);
   for (int kt = 0; kt < nk; ++kt) {
@@ -831,6 +848,13 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
     }
     f32x4 a0 = *reinterpret_cast<const f32x4*>(sb + aoff0);
     f32x4 a1 = *reinterpret_cast<const f32x4*>(sb + aoff1);
+    if (AXT == OT_AX_RMSNORM && xnw) {                  // k = 16 kt + 8 h .. + 7: (a * gamma) * rstd, rounded
+      const float* gp = p.a_gamma + 16 * kt + 8 * h;
+      const f32x4 v0 = a0 * *reinterpret_cast<const f32x4*>(gp) * xrs;
+      const f32x4 v1 = a1 * *reinterpret_cast<const f32x4*>(gp + 4) * xrs;
+      const u32x2 b0 = bf16_rne4(v0), b1 = bf16_rne4(v1);
+      *reinterpret_cast<u32x4*>(xnp + 16 * kt) = u32x4{b0.x, b0.y, b1.x, b1.y};
+    }
     if (AXT == OT_AX_GELU) {
       a0.x = gelu_erf(a0.x); a0.y = gelu_erf(a0.y); a0.z = gelu_erf(a0.z); a0.w = gelu_erf(a0.w);
       a1.x = gelu_erf(a1.x); a1.y = gelu_erf(a1.y); a1.z = gelu_erf(a1.z); a1.w = gelu_erf(a1.w);
@@ -1287,6 +1311,167 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(WgradArgs p) {
 }
 
 
+// Weight gradient with both operands in bf16 (a_xform OT_AX_BF16 | OT_WG_D_BF16, OT_MATMUL_BF16: the stored
+// normalised inputs / GELU and the bf16 dU / dQKV).  The stage images are plain copies of the rows, so they
+// go global -> LDS by global_load_lds straight into the swizzled layout the transposed fragment reads use
+// (no VGPR staging, no conversion) through a ring of WG_NST 32-row stages, WG_NST - 1 of them in flight
+// (the register-staged kernel keeps one; it waits on load latency, not MFMA: 10% MFMA busy at C5).  The
+// row indices of a stage are loaded one iteration before its copies are issued.  Rows past the chunk or
+// with a negative row index read a zero D row (A x 0 = 0; their A source is row 0, finite).  Columns past
+// K / N read column 0 (their outputs are not stored).  IDL: row maps given (a_rows == d_rows).
+#ifndef OT_WGRAD_NST
+#define OT_WGRAD_NST 4
+#endif
+constexpr int WG_NST = OT_WGRAD_NST;
+constexpr int WG_IMG = WBR * 256;                 // one 32-row x 128-column bf16 image
+constexpr int WG_STB = 2 * WG_IMG;                // A + D per stage
+__device__ __attribute__((aligned(16))) uint16_t g_zero_row[GT];   // zero-initialised with the module
+
+template <bool IDL>
+__global__ __launch_bounds__(256, 2) void wgrad_bf16_kernel(WgradArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem_c[];
+  const int per_chunk = p.ntk * p.ntn;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int c = wg / per_chunk, rem = wg % per_chunk;
+  const int tk = rem / p.ntn, tn = rem % p.ntn;
+  const int k0 = tk * GT, n0 = tn * GT;
+  const int row_begin = p.chunks[3 * c + 1], row_count = p.chunks[3 * c + 2];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int h = lane >> 5, li = lane & 31;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const uint16_t* A16 = reinterpret_cast<const uint16_t*>(p.A);
+  const uint16_t* D16 = reinterpret_cast<const uint16_t*>(p.D);
+  // copy lanes: instruction i of wave w fills image bytes [(2w + i) KiB, +1 KiB) = row 4 (2w + i) + lane / 16,
+  // physical 16-B chunk lane % 16 = logical chunk (lane % 16) ^ swizzle(row) (wsw_off)
+  int lrow[2], acol[2], dcol[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = 4 * (2 * wave + i) + (lane >> 4);
+    const int lc = (lane & 15) ^ (((r & 3) << 2) | ((r >> 2) & 3));
+    lrow[i] = r;
+    acol[i] = k0 + 8 * lc < p.K ? k0 + 8 * lc : 0;
+    dcol[i] = n0 + 8 * lc < p.N ? n0 + 8 * lc : 0;
+  }
+  const int nst = (row_count + WBR - 1) / WBR;
+  auto load_ids = [&](int st, int (&ids)[2]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = st * WBR + lrow[i];
+      const int64_t mi = (int64_t)row_begin + (r < row_count ? r : 0);
+      ids[i] = IDL ? p.a_rows[mi] : (int)mi;
+    }
+  };
+  auto issue = [&](int st, const int (&ids)[2]) {
+    char* sb = smem_c + (st % WG_NST) * WG_STB;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bool ok = st * WBR + lrow[i] < row_count && ids[i] >= 0;
+      const uint16_t* sa = A16 + (int64_t)(ok ? ids[i] : 0) * p.lda + acol[i];
+      const uint16_t* sd = ok ? D16 + (int64_t)ids[i] * p.ldd + dcol[i] : g_zero_row + 8 * (lane & 15);
+      __builtin_amdgcn_global_load_lds((const void*)sa, (lds_void_t*)(sb + (2 * wave + i) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)sd, (lds_void_t*)(sb + WG_IMG + (2 * wave + i) * 1024), 16, 0,
+                                       0);
+    }
+  };
+  // transposed-read addresses, as in wgrad_split_kernel
+  const int gi = lane & 15, q = gi >> 2, pp = gi & 3, g1 = (lane >> 4) & 1;
+  int aoff[2][2], doff[2][2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int rd = 0; rd < 2; ++rd) {
+      const int r = 8 * h + 4 * rd + q;
+      aoff[m][rd] = wsw_off(r, (wm + 32 * m + 16 * g1) / 8 + (pp >> 1)) + 8 * (pp & 1);
+      doff[m][rd] = wsw_off(r, (wn + 32 * m + 16 * g1) / 8 + (pp >> 1)) + 8 * (pp & 1);
+    }
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  // bias (tk == 0): thread t sums columns 2 (t & 63) + {0, 1} over rows 8 (t >> 6) .. + 7 of every stage
+  const bool do_bias = p.bslab && tk == 0;
+  const int bcp = t & 63, brs = t >> 6;
+  float bs0 = 0.f, bs1 = 0.f;
+
+  int ids[2];
+  for (int s = 0; s < WG_NST - 1; ++s)
+    if (s < nst) { load_ids(s, ids); issue(s, ids); }
+  load_ids(WG_NST - 1, ids);                          // ids of the next stage to issue
+  // in flight after stage st's copies when its wait comes: the id loads and copies of the stages issued
+  // after it (in order: vector memory loads retire in issue order)
+  constexpr int IDN = IDL ? 2 : 0;
+  for (int st = 0; st < nst; ++st) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (st + WG_NST - 1 <= nst) {
+      if constexpr (IDL) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(IDN + (WG_NST - 2) * (4 + IDN)) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" :: "n"((WG_NST - 2) * 4) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();                     // every wave's copies of stage st are in; slot
+    asm volatile("" ::: "memory");                    // (st - 1) % NST is no longer read
+    if (st + WG_NST - 1 < nst) {
+      issue(st + WG_NST - 1, ids);
+      load_ids(st + WG_NST, ids);
+    }
+    const char* As = smem_c + (st % WG_NST) * WG_STB;
+    const char* Ds = As + WG_IMG;
+    if (do_bias) {
+#pragma unroll
+      for (int r8 = 0; r8 < 8; ++r8) {
+        const int r = 8 * brs + r8;
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(Ds + wsw_off(r, bcp >> 2) + 4 * (bcp & 3));
+        bs0 += __uint_as_float(w << 16);
+        bs1 += __uint_as_float(w & 0xffff0000u);
+      }
+    }
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2) {
+      u32x4 fa[2], fb[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const int po = t2 * 16 * 256;
+        const v4i16 a0 = ds_tr16(As + po, aoff[m][0]), a1 = ds_tr16(As + po, aoff[m][1]);
+        const v4i16 d0 = ds_tr16(Ds + po, doff[m][0]), d1 = ds_tr16(Ds + po, doff[m][1]);
+        const u32x2 a0u = __builtin_bit_cast(u32x2, a0), a1u = __builtin_bit_cast(u32x2, a1);
+        const u32x2 d0u = __builtin_bit_cast(u32x2, d0), d1u = __builtin_bit_cast(u32x2, d1);
+        fa[m] = u32x4{a0u.x, a0u.y, a1u.x, a1u.y};
+        fb[m] = u32x4{d0u.x, d0u.y, d1u.x, d1u.y};
+      }
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) acc[m][n] = mfma_bf16(fa[m], fb[n], acc[m][n]);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float* slab = p.slab + (int64_t)c * p.K * p.N;
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int k = k0 + wm + 32 * m + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (k >= p.K) continue;
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        const int col = n0 + wn + 32 * n + li;
+        if (col < p.N) slab[(int64_t)k * p.N + col] = acc[m][n][r];
+      }
+    }
+  if (do_bias) {                                      // fixed-order sum of the 4 row sets per column
+    __syncthreads();                                  // every wave is done with the ring
+    float* bl = reinterpret_cast<float*>(smem_c);     // [4][128]
+    bl[brs * GT + 2 * bcp] = bs0;
+    bl[brs * GT + 2 * bcp + 1] = bs1;
+    __syncthreads();
+    if (t < GT && n0 + t < p.N)
+      p.bslab[(int64_t)c * p.N + n0 + t] = ((bl[t] + bl[GT + t]) + bl[2 * GT + t]) + bl[3 * GT + t];
+  }
+}
+
 // Sum the slabs of each group's chunks (chunks of one group are contiguous) into dW[g] (and db).
 // Block = 16 float4 columns x 16 chunk lanes; chunk lane c sums chunks c, c+16, ... and the 16
 // partials are combined in a fixed order through LDS (deterministic).
@@ -1469,6 +1654,10 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
   p.tail_pos = tail_pos;
   p.bimg = bimg; p.bimg_ntn = bimg_ntn; p.bimg_tn0 = bimg_tn0;
   float* dgpart = nullptr;
+  if (rms && rms->xn_out) {
+    p.xn_out = rms->xn_out;
+    p.ldxn = rms->ldxn;
+  }
   if (rms && ((epi & OT_EPI_GELU_BWD) || (epi & ~OT_EPI_C_BF16) == OT_EPI_BIAS)) {   // the stored GELU (optional)
     p.gelu_out = rms->gelu_out;
     p.ldgelu = rms->ldgelu;
@@ -1590,6 +1779,10 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
              "ot_mixed_gemm: OT_EPI_C_BF16 / OT_EPI_AUX_BF16 need the bf16-mode plane GEMM with OT_EPI_GELU_BWD "
              "[| OT_EPI_ROWDOT] or OT_EPI_BIAS alone (epilogue %d)", epi);
   OT_REQUIRE(!p.gelu_out || (!edge && (kern != nullptr)), "ot_mixed_gemm_rms: gelu_out needs whole tiles");
+  OT_REQUIRE(!p.xn_out || (plane && x == OT_AX_RMSNORM && a_rstd && a_gamma && p.ldxn % 8 == 0 &&
+                           ((uintptr_t)p.xn_out % 16) == 0),
+             "ot_mixed_gemm_rms: xn_out needs the plane GEMM with the RMSNorm prologue, ldxn %% 8 == 0 and 16-B "
+             "alignment");
   OT_REQUIRE(!p.rowpart || plane, "ot_mixed_gemm_rms: OT_EPI_ROW_RSTD with N = %d > %d needs the plane GEMM "
              "(split mode, a pre-split B image, 16-B aligned A)", N, GT);
   const size_t launch_shmem = !plane ? shmem
@@ -1716,6 +1909,11 @@ extern "C" int ot_mixed_gemm_rms_img(int mode, const float* A, int64_t lda, int 
                          site, drop_rate, tail_K, tail_I, tail_pos, rms, b_image, image_ntn, image_tn0, stream);
 }
 
+static int g_wgrad_copy = [] {
+  const char* e = std::getenv("ONETRANS_WGRAD_COPY");
+  return e ? std::atoi(e) : 1;
+}();
+
 extern "C" size_t ot_wgrad_workspace_size(int nchunks, int K, int N) {
   return ((size_t)nchunks * K * N + (size_t)nchunks * N) * sizeof(float);
 }
@@ -1733,7 +1931,8 @@ extern "C" int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a
   const bool dbf = (a_xform & OT_WG_D_BF16) != 0;
   a_xform &= ~OT_WG_D_BF16;
   OT_REQUIRE(a_xform != OT_AX_RMSNORM || (a_rstd && a_gamma), "ot_mixed_gemm_wgrad: rmsnorm prologue needs rstd/gamma");
-  OT_REQUIRE(!dbf || (g_matmul_mode == OT_MATMUL_BF16 && (a_xform == OT_AX_NONE || a_xform == OT_AX_RMSNORM) &&
+  OT_REQUIRE(!dbf || (g_matmul_mode == OT_MATMUL_BF16 &&
+                      (a_xform == OT_AX_NONE || a_xform == OT_AX_RMSNORM || a_xform == OT_AX_BF16) &&
                       ((uintptr_t)D % 8) == 0),
              "ot_mixed_gemm_wgrad: OT_WG_D_BF16 needs the bf16 mode, A form OT_AX_NONE / OT_AX_RMSNORM and 8-B "
              "aligned D rows");
@@ -1747,8 +1946,15 @@ extern "C" int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a
     const bool split = g_matmul_mode != OT_MATMUL_F32;
     OT_REQUIRE(a_xform != OT_AX_BF16 || (g_matmul_mode != OT_MATMUL_F32 && lda % 4 == 0 && ((uintptr_t)A % 8) == 0),
                "ot_mixed_gemm_wgrad: OT_AX_BF16 needs the split / bf16 mode and 8-B aligned rows");
+    // both operands bf16 with whole 16-B column chunks: the copy-staged kernel (ONETRANS_WGRAD_COPY=0: the
+    // register-staged one)
+    const bool copy = dbf && a_xform == OT_AX_BF16 && g_wgrad_copy && K % 8 == 0 && N % 8 == 0 && lda % 8 == 0 &&
+                      ldd % 8 == 0 && ((uintptr_t)A % 16) == 0 && ((uintptr_t)D % 16) == 0 && a_rows == d_rows;
     void (*kern)(WgradArgs) =
-        dbf ? (a_xform == OT_AX_NONE ? wgrad_split_kernel<OT_AX_NONE, 1, true> : wgrad_split_kernel<OT_AX_RMSNORM, 1, true>)
+        copy ? (a_rows ? wgrad_bf16_kernel<true> : wgrad_bf16_kernel<false>)
+        : dbf ? (a_xform == OT_AX_NONE      ? wgrad_split_kernel<OT_AX_NONE, 1, true>
+                 : a_xform == OT_AX_BF16    ? wgrad_split_kernel<OT_AX_BF16, 1, true>
+                                            : wgrad_split_kernel<OT_AX_RMSNORM, 1, true>)
         : a_xform == OT_AX_BF16 ? (g_matmul_mode == OT_MATMUL_BF16 ? wgrad_split_kernel<OT_AX_BF16, 1>
                                                                 : wgrad_split_kernel<OT_AX_BF16, SPLIT_TERMS>)
         : g_matmul_mode == OT_MATMUL_BF16
@@ -1772,7 +1978,17 @@ extern "C" int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * WBR * WLD * 4);
       (void)hipGetLastError();
     });
-    hipLaunchKernelGGL(kern, dim3((unsigned)nchunks * p.ntk * p.ntn), dim3(256), split ? split_shmem : shmem, s, p);
+    const size_t copy_shmem = (size_t)WG_NST * WG_STB;
+    if (copy && copy_shmem > 64 * 1024) {
+      static std::once_flag copy_once;
+      std::call_once(copy_once, [] {
+        for (void (*k)(WgradArgs) : {wgrad_bf16_kernel<true>, wgrad_bf16_kernel<false>})
+          (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, WG_NST * WG_STB);
+        (void)hipGetLastError();
+      });
+    }
+    hipLaunchKernelGGL(kern, dim3((unsigned)nchunks * p.ntk * p.ntn), dim3(256),
+                       copy ? copy_shmem : split ? split_shmem : shmem, s, p);
     OT_LAUNCH_CHECK("ot_mixed_gemm_wgrad");
   }
   const int wblocks = (int)ceil_div((int64_t)K * N / 4, 16);

@@ -175,20 +175,22 @@ def gemm_rms(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish,
              dres_tail: Tuple[int, int] = (0, 0), dx_masked: Ptrish = None, lddxm: int = 0,
              dgamma: Ptrish = None, accumulate_dgamma: bool = False, device=None, bimg=None,
              aux: Ptrish = None, ldaux: int = 0, rowdot: Ptrish = None, rowdot_n: int = 0,
-             gelu_out: Ptrish = None, ldgelu: int = 0) -> None:
+             gelu_out: Ptrish = None, ldgelu: int = 0, xn_out: Ptrish = None, ldxn: int = 0) -> None:
     """ot_mixed_gemm_rms: the GEMM with a row-norm epilogue (OT_EPI_ROW_RSTD: emit the next RMSNorm's
     rstd; OT_EPI_RMSNORM_BWD: apply the RMSNorm backward to the product, + dres, dgamma, taking
     <gamma dy, x> from ``rowdot`` when N > 128; OT_EPI_GELU_BWD | OT_EPI_ROWDOT: also write each 128-column
     tile's sum of dU (aux - bias) into rowdot[row][tile]); ``gelu_out`` (bf16 bits, [rows][ldgelu]) also
     receives gelu(aux) (with OT_EPI_GELU_BWD) or gelu(C) (epi == OT_EPI_BIAS: the FFN1 forward) rounded to
-    bf16 — the OT_AX_BF16 operand of the FFN2 GEMM and the W2 weight gradient."""
+    bf16 — the OT_AX_BF16 operand of the FFN2 GEMM and the W2 weight gradient.  ``xn_out`` (bf16 bits,
+    [in rows][ldxn]; RMSNorm prologue, plane GEMM) receives bf16((A * gamma) * rstd): the normalised A
+    operand of the bf16 weight gradient."""
     need_ws = dgamma is not None or (rstd_out is not None and N > 128)     # dgamma / row-sum partials
     ws = workspace(size('ot_mixed_gemm_rms_workspace_size', ntiles, N) if need_ws else 16,
                    device if device is not None else (C[0] if isinstance(C, tuple) else C).device)
     e = _lib.RmsEpilogue(ptr(rstd_out), float(eps), ptr(nx), ldnx, ptr(ngamma), ptr(nrstd), ptr(dres), lddres,
                          dres_tail[0], dres_tail[1], _sel(dres_tail), ptr(dx_masked), lddxm, ptr(dgamma),
                          int(accumulate_dgamma), ptr(ws), ws.numel(), ptr(rowdot), int(rowdot_n),
-                         ptr(gelu_out), int(ldgelu))
+                         ptr(gelu_out), int(ldgelu), ptr(xn_out), int(ldxn))
     ev = _probe.begin() if _probe is not None else None
     args = (mode, ptr(A), lda, K, ptr(in_rows), a_xform, ptr(rstd), ptr(gamma), ptr(W),
             w_gstride, ldw, N, ptr(tile_group), ntiles, ptr(bias), bias_gstride, ptr(C), ldc, ptr(out_rows), epi,
@@ -203,6 +205,7 @@ def gemm_rms(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish,
         extra = (nx is not None) + (dres is not None) + (dx_masked is not None)   # norm-backward operands
         _probe.end('mixed_gemm', 2.0 * M * K * N, ev, f'gemm_rms mode{mode} ax{a_xform} epi{epi} M{M} K{K} N{N}',
                    gemm_bytes(M, K, N, a_xform, epi) + 4.0 * M * N * extra + 2.0 * M * N * (gelu_out is not None)
+                   + 2.0 * M * K * (xn_out is not None)
                    + 4.0 * M * ((rstd_out is not None) + (nrstd is not None)))
 
 

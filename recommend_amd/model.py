@@ -143,8 +143,8 @@ def _attn_qpos(cfg, pos):
 def _block_forward(m, l, x, I, Kq, seed, training, rstd_in=None, select=False, need_out=True):
     """The block's forward kernels (``_Block.forward``; also the backward's recompute with
     ``need_out=False``, which stops after FFN1: the backward needs u, not the block output).
-    Returns (x2, rstd_out, saved, pos, inv, rate); saved = (x, rstd1, qkv, o, lse, x1, rstd2, u, h);
-    h = the stored bf16 gelu(u) (bf16 mode) or None."""
+    Returns (x2, rstd_out, saved, pos, inv, rate); saved = (x, rstd1, qkv, o, lse, x1, rstd2, u, h, xn1, x1n);
+    h = the stored bf16 gelu(u), xn1 / x1n = the bf16 normalised QKV / FFN1 inputs (bf16 mode) or None."""
     cfg = m.config
     d, f, H = cfg.hidden_dim, cfg.ffn_dim, cfg.num_heads
     hd = d // H
@@ -182,7 +182,24 @@ def _block_forward(m, l, x, I, Kq, seed, training, rstd_in=None, select=False, n
             K.pyramid_select(B, I, Kq, pos, inv)
     tail = (Kq, I, pos)
     qkv = torch.empty(B * I, 3 * d, device=dev)
-    if Kq == I:
+    # bf16 mode, training: the QKV / FFN1 GEMMs also store their normalised A rows in bf16 (ot_rms_epilogue
+    # .xn_out) for the copy-staged bf16 weight gradients of Wqkv / W1 (operands read once, no norm re-applied)
+    xn_on = (training and m.xn_bf16 and K.matmul_mode() == 'bf16' and d % TILE == 0
+             and m.bimg(f'blk.{l}.wqkv') is not None)
+    xn1 = torch.empty(B * I, d, dtype=torch.int16, device=dev) if xn_on else None
+    x1n = torch.empty(B * Kq, d, dtype=torch.int16, device=dev) if xn_on else None
+    if xn1 is not None:
+        full = Kq == I
+        K.gemm_rms(OT_GEMM_NT, x, d, d, ma['rows'][0], wqkv if full else (wqkv, d * d), 3 * d * d, d,
+                   3 * d if full else 2 * d, ma['tile_group'], na, qkv if full else (qkv, d), 3 * d, ma['rows'][0],
+                   epi=0, a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=maps['all'].nrows, device=dev,
+                   bimg=m.bimg(f'blk.{l}.wqkv') if full else m.bimg(f'blk.{l}.wqkv', tn0=d // TILE),
+                   xn_out=xn1, ldxn=d)
+        if not full:
+            K.gemm(OT_GEMM_NT, x, d, d, qrows, wqkv, 3 * d * d, d, d, mt['tile_group'], nt, qkv,
+                   3 * d, qrows, a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=maps['tail'].nrows,
+                   bimg=m.bimg(f'blk.{l}.wqkv'))
+    elif Kq == I:
         K.gemm(OT_GEMM_NT, x, d, d, ma['rows'][0], wqkv, 3 * d * d, d, 3 * d, ma['tile_group'], na, qkv,
                3 * d, ma['rows'][0], a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=maps['all'].nrows,
                bimg=m.bimg(f'blk.{l}.wqkv'))
@@ -230,12 +247,15 @@ def _block_forward(m, l, x, I, Kq, seed, training, rstd_in=None, select=False, n
         K.gemm_rms(OT_GEMM_NT, x1, d, d, mt['rows'][1], w1, d * f, d, f, mt['tile_group'], nt, u, f, mt['rows'][1],
                    a_xform=OT_AX_RMSNORM, rstd=rstd2, gamma=g2, bias=b1, bias_gstride=f,
                    epi=OT_EPI_BIAS | (OT_EPI_C_BF16 if u_bf else 0),
-                   m_rows=maps['tail'].nrows, bimg=m.bimg(f'blk.{l}.w1'), gelu_out=h, ldgelu=f)
+                   m_rows=maps['tail'].nrows, bimg=m.bimg(f'blk.{l}.w1'), gelu_out=h, ldgelu=f,
+                   xn_out=x1n, ldxn=d)
     else:
         K.gemm(OT_GEMM_NT, x1, d, d, mt['rows'][1], w1, d * f, d, f, mt['tile_group'], nt, u, f, mt['rows'][1],
                a_xform=OT_AX_RMSNORM, rstd=rstd2, gamma=g2, bias=b1, bias_gstride=f, epi=OT_EPI_BIAS,
                m_rows=maps['tail'].nrows, bimg=m.bimg(f'blk.{l}.w1'))
-    saved = (x, rstd1, qkv, o, lse, x1, rstd2, u, h)
+    if x1n is not None and h is None:                # the FFN1 GEMM above did not store it
+        x1n = None
+    saved = (x, rstd1, qkv, o, lse, x1, rstd2, u, h, xn1, x1n)
     if not need_out:
         return None, None, saved, pos, inv, rate
     # x2 = x1 + drop(gelu(u) @ W2[g] + b2[g])     (model.py:154-161, 198)
@@ -291,9 +311,9 @@ class _Block(torch.autograd.Function):
             training, select = ctx.fwd_args
             _, _, saved, pos, inv, _ = _block_forward(m, l, xin, I, Kq, seed, training, rstd_in, select,
                                                       need_out=False)
-            x, rstd1, qkv, o, lse, x1, rstd2, u, h = saved
+            x, rstd1, qkv, o, lse, x1, rstd2, u, h, xn1, x1n = saved
         else:
-            x, rstd1, qkv, o, lse, x1, rstd2, u, h = ctx.saved_tensors
+            x, rstd1, qkv, o, lse, x1, rstd2, u, h, xn1, x1n = ctx.saved_tensors
         tail = (Kq, I, pos)
         cfg = m.config
         d, f, H = cfg.hidden_dim, cfg.ffn_dim, cfg.num_heads
@@ -351,9 +371,11 @@ class _Block(torch.autograd.Function):
             K.gemm(OT_GEMM_NT, dy2, d, d, mt['rows'][1], m.p(f'blk.{l}.w2'), f * d, d, f, mt['tile_group'], nt, du,
                    f, mt['rows'][1], epi=OT_EPI_GELU_BWD, aux=u, ldaux=f, m_rows=maps['tail'].nrows,
                    bimg=m.bimg(f'blk.{l}.w2', 'dgrad'))
-        with m.side(x1, du, rstd2):
-            K.wgrad(x1, d, mt['rows'][1], du, f, mt['rows'][1], d, f, mt, nct, G, m.g(f'blk.{l}.w1'), d * f,
-                    m.g(f'blk.{l}.b1'), f, a_xform=OT_AX_RMSNORM | (OT_WG_D_BF16 if du_bf else 0), rstd=rstd2,
+        a1n = x1n is not None and du_bf               # both operands bf16: the copy-staged weight gradient
+        with m.side(x1n if a1n else x1, du, rstd2):
+            K.wgrad(x1n if a1n else x1, d, mt['rows'][1], du, f, mt['rows'][1], d, f, mt, nct, G, m.g(f'blk.{l}.w1'),
+                    d * f, m.g(f'blk.{l}.b1'), f,
+                    a_xform=(OT_AX_BF16 if a1n else OT_AX_RMSNORM) | (OT_WG_D_BF16 if du_bf else 0), rstd=rstd2,
                     gamma=m.p(f'blk.{l}.norm2'),
                     accumulate=acc, device=dev, m_rows=maps['tail'].nrows, rowmap=maps['tail'])
         # FFN1 dgrad -> norm2 backward + residual; emit mask(dx1) for the attention branch
@@ -391,9 +413,11 @@ class _Block(torch.autograd.Function):
         if Kq < I:
             dqkv[:, :d].zero_()
         K.attn_bwd(qkv, 3 * d, o, do, lse, B, H, I, Kq, hd, dqkv, qpos=qp)
-        with m.side(x, dqkv, rstd1):
-            K.wgrad(x, d, ma['rows'][0], dqkv, 3 * d, ma['rows'][0], d, 3 * d, ma, nca, G, m.g(f'blk.{l}.wqkv'),
-                    3 * d * d, None, 0, a_xform=OT_AX_RMSNORM | (OT_WG_D_BF16 if dq_bf else 0), rstd=rstd1,
+        an1 = xn1 is not None and dq_bf
+        with m.side(xn1 if an1 else x, dqkv, rstd1):
+            K.wgrad(xn1 if an1 else x, d, ma['rows'][0], dqkv, 3 * d, ma['rows'][0], d, 3 * d, ma, nca, G,
+                    m.g(f'blk.{l}.wqkv'), 3 * d * d, None, 0,
+                    a_xform=(OT_AX_BF16 if an1 else OT_AX_RMSNORM) | (OT_WG_D_BF16 if dq_bf else 0), rstd=rstd1,
                     gamma=m.p(f'blk.{l}.norm1'), accumulate=acc, device=dev, m_rows=maps['all'].nrows,
                     rowmap=maps['all'])
         ax_dq = OT_AX_BF16 if dq_bf else 0
@@ -607,6 +631,9 @@ class OneTransModel(nn.Module):
         self.dqkv_bf16 = os.environ.get('ONETRANS_DQKV_BF16', '1') != '0'
         # bf16 mode with the stored GELU and bf16 dU: the FFN1 pre-activation U in bf16 (ONETRANS_U_BF16=0: f32)
         self.u_bf16 = os.environ.get('ONETRANS_U_BF16', '1') != '0'
+        # bf16 mode, training: bf16 normalised QKV / FFN1 inputs for the Wqkv / W1 weight gradients
+        # (ONETRANS_XN_BF16=0: those re-read the f32 inputs and re-apply the norm)
+        self.xn_bf16 = os.environ.get('ONETRANS_XN_BF16', '1') != '0'
         # block weight gradients run on a second stream, overlapping the dgrad chain
         self.overlap_wgrad = os.environ.get('ONETRANS_OVERLAP_WGRAD', '1') != '0'
         self._side = None

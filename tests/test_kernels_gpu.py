@@ -725,3 +725,46 @@ def test_stored_gelu_weight_gradient(dev, mode):
     else:                       # split: the stored operand is bf16 (8 bits), the recomputed one f32-exact
         scale = dW[0].abs().max().item()
         assert (dW[0] - dW[1]).abs().max().item() < 2e-2 * scale
+
+
+@pytest.mark.parametrize('K_,N', [(512, 2048), (512, 1536), (136, 200)])
+def test_wgrad_copy_staged_bf16(dev, K_, N):
+    """bf16 mode, both weight-gradient operands bf16 (OT_AX_BF16 | OT_WG_D_BF16: the stored normalised
+    inputs with bf16 dU / dQKV): the copy-staged kernel (global_load_lds ring) gives dW bit-identical to the
+    register-staged kernel on the same values (A widened to f32: the same MFMA sequence), over ragged
+    weight groups, padded rows (-1) and partial column tiles; db (a column sum in another order) within f32
+    rounding."""
+    from recommend_amd import layout
+    from recommend_amd._lib import OT_AX_BF16, OT_WG_D_BF16
+    rng = np.random.default_rng(K_ + N)
+    G, M = 3, 3000
+    cuts = [0, 1100, 1900, M]
+    perm = rng.permutation(M)
+    rm = layout.build_map([[perm[cuts[g]:cuts[g + 1]], perm[cuts[g]:cuts[g + 1]]] for g in range(G)])
+    dm = rm.to(dev)
+    g = torch.Generator().manual_seed(K_ + N)
+    A16 = torch.randn(M, K_, generator=g).to(torch.bfloat16).to(dev)
+    D16 = torch.randn(M, N, generator=g).to(torch.bfloat16).to(dev)
+    old = K.set_matmul_mode('bf16')
+    try:
+        res = []
+        for A, ax in ((A16.view(torch.int16), OT_AX_BF16), (A16.float(), 0)):
+            dW = torch.full((G, K_, N), float('nan'), device=dev)
+            db = torch.full((G, N), float('nan'), device=dev)
+            K.wgrad(A, K_, dm['rows'][1], D16.view(torch.int16), N, dm['rows'][1], K_, N, dm, rm.chunks.shape[0], G,
+                    dW, K_ * N, db, N, a_xform=ax | OT_WG_D_BF16, device=dev, m_rows=M, rowmap=rm)
+            res.append((dW, db))
+        torch.cuda.synchronize()
+    finally:
+        K.set_matmul_mode(old)
+    assert torch.equal(res[0][0], res[1][0])
+    torch.testing.assert_close(res[0][1], res[1][1], rtol=1e-5, atol=1e-4)
+    # and against float64 group sums
+    rows = dm['rows'][1].cpu().numpy()
+    tg = rm.tile_group
+    Ad, Dd = A16.double().cpu(), D16.double().cpu()
+    for gi in range(G):
+        sel = np.concatenate([rows[t * 128:(t + 1) * 128] for t in range(rm.ntiles) if tg[t] == gi])
+        sel = torch.from_numpy(sel[sel >= 0]).long()
+        ref = Ad[sel].T @ Dd[sel]
+        assert (res[0][0][gi].double().cpu() - ref).abs().max().item() <= 1e-4 * ref.abs().max().item() + 1e-3

@@ -357,3 +357,31 @@ def test_plane_gemm_bf16_a_plain(dev, plane_mode, K_, N):
     torch.cuda.synchronize()
     assert not torch.isnan(outs[1]).any()
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize('N', [1536, 128])
+def test_plane_gemm_xn_out(dev, plane_mode, N):
+    """ot_rms_epilogue.xn_out on the plane GEMM's RMSNorm prologue: the first column tile's workgroups store
+    bf16((A * gamma) * rstd) of every mapped A row — the same f32 products, rounded once, that torch forms
+    — and C is unchanged by it."""
+    rng = np.random.default_rng(N)
+    G, M, K_ = 3, 700, 512
+    rm = ragged_map(rng, M, G)
+    dm = rm.to(dev)
+    A = torch.randn(M, K_, device=dev)
+    W = torch.randn(G, N, K_) / math.sqrt(K_)
+    gamma = 1 + 0.1 * torch.randn(K_)
+    rstd = torch.rand(M, device=dev) + 0.5
+    img, ntn = make_image(W, dev, gamma)
+    outs = []
+    xn = torch.zeros(M, K_, dtype=torch.int16, device=dev)
+    for with_xn in (False, True):
+        C = torch.full((M, N), float('nan'), device=dev)
+        K.gemm_rms(OT_GEMM_NT, A, K_, K_, dm['rows'][0], W.to(dev), N * K_, K_, N, dm['tile_group'], rm.ntiles, C, N,
+                   dm['rows'][1], epi=0, a_xform=OT_AX_RMSNORM, rstd=rstd, gamma=gamma.to(dev), device=dev,
+                   bimg=(img, ntn, 0), xn_out=xn if with_xn else None, ldxn=K_)
+        outs.append(C)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    ref = ((A * gamma.to(dev)) * rstd[:, None]).to(torch.bfloat16).view(torch.int16)
+    assert torch.equal(xn, ref)

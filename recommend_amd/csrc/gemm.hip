@@ -801,11 +801,16 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
   const int boff = PG_A_BYTES + li * 32 + 16 * (h ^ ((li >> 3) & 1));
   const int aoffb = ra * 32 + 16 * (h ^ ((li >> 3) & 1));  // bf16 A
 
-  // normalised-A side output (AXT == OT_AX_RMSNORM, first column tile): this lane's fragment row ra
+  // normalised-A side output (AXT == OT_AX_RMSNORM, first column tile): this lane's fragment row ra; gamma
+  // is copied to LDS behind the stage buffers first (a global load in the loop would make the compiler
+  // wait for every outstanding stage copy)
   bool xnw = false;
   float xrs = 0.f;
   uint16_t* xnp = nullptr;
+  float* gsm = reinterpret_cast<float*>(lds + NSTG * STG);
   if (AXT == OT_AX_RMSNORM && p.xn_out && tn == 0) {
+    for (int k = 4 * t; k < p.K; k += 4 * 256)
+      *reinterpret_cast<f32x4*>(gsm + k) = *reinterpret_cast<const f32x4*>(p.a_gamma + k);
     const int64_t xgr = (int64_t)tm * GT + ra;
     const int xir = p.in_rows ? p.in_rows[xgr] : (int)xgr;
     xnw = xir >= 0;
@@ -849,7 +854,7 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
     f32x4 a0 = *reinterpret_cast<const f32x4*>(sb + aoff0);
     f32x4 a1 = *reinterpret_cast<const f32x4*>(sb + aoff1);
     if (AXT == OT_AX_RMSNORM && xnw) {                  // k = 16 kt + 8 h .. + 7: (a * gamma) * rstd, rounded
-      const float* gp = p.a_gamma + 16 * kt + 8 * h;
+      const float* gp = gsm + 16 * kt + 8 * h;
       const f32x4 v0 = a0 * *reinterpret_cast<const f32x4*>(gp) * xrs;
       const f32x4 v1 = a1 * *reinterpret_cast<const f32x4*>(gp + 4) * xrs;
       const u32x2 b0 = bf16_rne4(v0), b1 = bf16_rne4(v1);
@@ -1322,13 +1327,39 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(WgradArgs p) {
 #ifndef OT_WGRAD_NST
 #define OT_WGRAD_NST 4
 #endif
+#ifndef OT_WGRAD_SR
+#define OT_WGRAD_SR 32                            // rows per stage (16 or 32)
+#endif
+#ifndef OT_WGRAD_COPY_MINW
+#define OT_WGRAD_COPY_MINW 2
+#endif
 constexpr int WG_NST = OT_WGRAD_NST;
-constexpr int WG_IMG = WBR * 256;                 // one 32-row x 128-column bf16 image
+constexpr int WG_SR = OT_WGRAD_SR;
+constexpr int WG_NI = WG_SR / 16;                 // copies per wave per operand and stage (4 rows each)
+constexpr int WG_IMG = WG_SR * 256;               // one stage's rows x 128-column bf16 image
 constexpr int WG_STB = 2 * WG_IMG;                // A + D per stage
+static_assert(WG_SR == 16 || WG_SR == 32, "copy-staged wgrad stage rows");
+constexpr int WG_IDB = 16;                        // loop iterations per row-id block
+constexpr int WG_IDR = WG_IDB * WG_SR;            // ids per block (a multiple of 256: two / thread at SR 32)
+constexpr int WG_LDS = WG_NST * WG_STB + 2 * WG_IDR * 4;
 __device__ __attribute__((aligned(16))) uint16_t g_zero_row[GT];   // zero-initialised with the module
 
+// ds_read_b64_tr_b16 as inline asm: the intrinsic makes the compiler wait for every outstanding
+// global_load_lds (vmcnt(0)) before it, which would drain the copy ring each stage.  The caller waits for
+// the results itself (tr16_wait) before using them.
+__device__ __forceinline__ v4i16 ds_tr16_nowait(const char* base, int off) {
+  typedef __attribute__((address_space(3))) const char lds_cchar;
+  const uint32_t a = (uint32_t)(uintptr_t)(lds_cchar*)(base + off);
+  v4i16 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a) : "memory");
+  return r;
+}
+__device__ __forceinline__ void tr16_wait(v4i16& a, v4i16& b, v4i16& c, v4i16& d) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) :: "memory");
+}
+
 template <bool IDL>
-__global__ __launch_bounds__(256, 2) void wgrad_bf16_kernel(WgradArgs p) {
+__global__ __launch_bounds__(256, OT_WGRAD_COPY_MINW) void wgrad_bf16_kernel(WgradArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem_c[];
   const int per_chunk = p.ntk * p.ntn;
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
@@ -1343,34 +1374,45 @@ __global__ __launch_bounds__(256, 2) void wgrad_bf16_kernel(WgradArgs p) {
   const uint16_t* D16 = reinterpret_cast<const uint16_t*>(p.D);
   // copy lanes: instruction i of wave w fills image bytes [(2w + i) KiB, +1 KiB) = row 4 (2w + i) + lane / 16,
   // physical 16-B chunk lane % 16 = logical chunk (lane % 16) ^ swizzle(row) (wsw_off)
-  int lrow[2], acol[2], dcol[2];
+  int lrow[WG_NI], acol[WG_NI], dcol[WG_NI];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int r = 4 * (2 * wave + i) + (lane >> 4);
+  for (int i = 0; i < WG_NI; ++i) {
+    const int r = 4 * (WG_NI * wave + i) + (lane >> 4);
     const int lc = (lane & 15) ^ (((r & 3) << 2) | ((r >> 2) & 3));
     lrow[i] = r;
     acol[i] = k0 + 8 * lc < p.K ? k0 + 8 * lc : 0;
     dcol[i] = n0 + 8 * lc < p.N ? n0 + 8 * lc : 0;
   }
-  const int nst = (row_count + WBR - 1) / WBR;
-  auto load_ids = [&](int st, int (&ids)[2]) {
+  const int nst = (row_count + WG_SR - 1) / WG_SR;
+  auto row_id = [&](int st, int i) -> int {           // direct lookup (prologue; identity maps)
+    const int r = st * WG_SR + lrow[i];
+    const int64_t mi = (int64_t)row_begin + (r < row_count ? r : 0);
+    return IDL ? p.a_rows[mi] : (int)mi;
+  };
+  // Row-id blocks (row maps): the ids of the copies issued in iterations [16 b, 16 b + 16) — stages
+  // 16 b + NST - 1 .. + 15 — go through an LDS double buffer behind the ring, loaded into registers one block
+  // ahead and written at the block's first iteration.  (An id load per stage in the loop made the compiler
+  // wait for every outstanding copy before the copies that use it.)
+  int* idbuf = reinterpret_cast<int*>(smem_c + WG_NST * WG_STB);   // [2][WG_IDR]
+  int pre[WG_IDR / 256];
+  auto prefetch_block = [&](int b) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int r = st * WBR + lrow[i];
+    for (int j = 0; j < WG_IDR / 256; ++j) {
+      const int r = (WG_IDB * b + WG_NST - 1) * WG_SR + t + 256 * j;
       const int64_t mi = (int64_t)row_begin + (r < row_count ? r : 0);
-      ids[i] = IDL ? p.a_rows[mi] : (int)mi;
+      pre[j] = p.a_rows[mi];
     }
   };
-  auto issue = [&](int st, const int (&ids)[2]) {
+  auto issue = [&](int st, const int (&ids)[WG_NI]) {
     char* sb = smem_c + (st % WG_NST) * WG_STB;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const bool ok = st * WBR + lrow[i] < row_count && ids[i] >= 0;
+    for (int i = 0; i < WG_NI; ++i) {
+      const bool ok = st * WG_SR + lrow[i] < row_count && ids[i] >= 0;
       const uint16_t* sa = A16 + (int64_t)(ok ? ids[i] : 0) * p.lda + acol[i];
       const uint16_t* sd = ok ? D16 + (int64_t)ids[i] * p.ldd + dcol[i] : g_zero_row + 8 * (lane & 15);
-      __builtin_amdgcn_global_load_lds((const void*)sa, (lds_void_t*)(sb + (2 * wave + i) * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)sd, (lds_void_t*)(sb + WG_IMG + (2 * wave + i) * 1024), 16, 0,
-                                       0);
+      __builtin_amdgcn_global_load_lds((const void*)sa, (lds_void_t*)(sb + (WG_NI * wave + i) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)sd, (lds_void_t*)(sb + WG_IMG + (WG_NI * wave + i) * 1024), 16,
+                                       0, 0);
     }
   };
   // transposed-read addresses, as in wgrad_split_kernel
@@ -1391,51 +1433,66 @@ __global__ __launch_bounds__(256, 2) void wgrad_bf16_kernel(WgradArgs p) {
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-  // bias (tk == 0): thread t sums columns 2 (t & 63) + {0, 1} over rows 8 (t >> 6) .. + 7 of every stage
+  // bias (tk == 0): thread t sums columns 2 (t & 63) + {0, 1} over rows (SR / 4) (t >> 6) .. of every stage
   const bool do_bias = p.bslab && tk == 0;
   const int bcp = t & 63, brs = t >> 6;
   float bs0 = 0.f, bs1 = 0.f;
 
-  int ids[2];
-  for (int s = 0; s < WG_NST - 1; ++s)
-    if (s < nst) { load_ids(s, ids); issue(s, ids); }
-  load_ids(WG_NST - 1, ids);                          // ids of the next stage to issue
-  // in flight after stage st's copies when its wait comes: the id loads and copies of the stages issued
-  // after it (in order: vector memory loads retire in issue order)
-  constexpr int IDN = IDL ? 2 : 0;
+  for (int s0 = 0; s0 < WG_NST - 1; ++s0)
+    if (s0 < nst) {
+      int ids[WG_NI];
+#pragma unroll
+      for (int i = 0; i < WG_NI; ++i) ids[i] = row_id(s0, i);
+      issue(s0, ids);
+    }
+  if (IDL) prefetch_block(0);
+  // in flight after stage st's copies when its wait comes: the copies of the NST - 2 stages issued after it
+  // (vector memory loads retire in issue order; the id-block loads only add to the count, so the wait
+  // is conservative around them)
   for (int st = 0; st < nst; ++st) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (st + WG_NST - 1 <= nst) {
-      if constexpr (IDL) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(IDN + (WG_NST - 2) * (4 + IDN)) : "memory");
-      else asm volatile("s_waitcnt vmcnt(%0)" :: "n"((WG_NST - 2) * 4) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" :: "n"((WG_NST - 2) * 2 * WG_NI) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    const bool blk = IDL && (st % WG_IDB) == 0;
+    if (blk) {                                        // this block's ids into LDS
+      int* ib = idbuf + ((st / WG_IDB) & 1) * WG_IDR;
+#pragma unroll
+      for (int j = 0; j < WG_IDR / 256; ++j) ib[t + 256 * j] = pre[j];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_s_barrier();                     // every wave's copies of stage st are in; slot
     asm volatile("" ::: "memory");                    // (st - 1) % NST is no longer read
+    if (blk) prefetch_block(st / WG_IDB + 1);
     if (st + WG_NST - 1 < nst) {
+      int ids[WG_NI];
+      const int* ib = idbuf + ((st / WG_IDB) & 1) * WG_IDR + (st % WG_IDB) * WG_SR;
+#pragma unroll
+      for (int i = 0; i < WG_NI; ++i) ids[i] = IDL ? ib[lrow[i]] : row_id(st + WG_NST - 1, i);
       issue(st + WG_NST - 1, ids);
-      load_ids(st + WG_NST, ids);
     }
     const char* As = smem_c + (st % WG_NST) * WG_STB;
     const char* Ds = As + WG_IMG;
     if (do_bias) {
 #pragma unroll
-      for (int r8 = 0; r8 < 8; ++r8) {
-        const int r = 8 * brs + r8;
+      for (int r8 = 0; r8 < WG_SR / 4; ++r8) {
+        const int r = (WG_SR / 4) * brs + r8;
         const uint32_t w = *reinterpret_cast<const uint32_t*>(Ds + wsw_off(r, bcp >> 2) + 4 * (bcp & 3));
         bs0 += __uint_as_float(w << 16);
         bs1 += __uint_as_float(w & 0xffff0000u);
       }
     }
 #pragma unroll
-    for (int t2 = 0; t2 < 2; ++t2) {
+    for (int t2 = 0; t2 < WG_SR / 16; ++t2) {
       u32x4 fa[2], fb[2];
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
         const int po = t2 * 16 * 256;
-        const v4i16 a0 = ds_tr16(As + po, aoff[m][0]), a1 = ds_tr16(As + po, aoff[m][1]);
-        const v4i16 d0 = ds_tr16(Ds + po, doff[m][0]), d1 = ds_tr16(Ds + po, doff[m][1]);
+        v4i16 a0 = ds_tr16_nowait(As + po, aoff[m][0]), a1 = ds_tr16_nowait(As + po, aoff[m][1]);
+        v4i16 d0 = ds_tr16_nowait(Ds + po, doff[m][0]), d1 = ds_tr16_nowait(Ds + po, doff[m][1]);
+        tr16_wait(a0, a1, d0, d1);
         const u32x2 a0u = __builtin_bit_cast(u32x2, a0), a1u = __builtin_bit_cast(u32x2, a1);
         const u32x2 d0u = __builtin_bit_cast(u32x2, d0), d1u = __builtin_bit_cast(u32x2, d1);
         fa[m] = u32x4{a0u.x, a0u.y, a1u.x, a1u.y};
@@ -1779,15 +1836,17 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
              "ot_mixed_gemm: OT_EPI_C_BF16 / OT_EPI_AUX_BF16 need the bf16-mode plane GEMM with OT_EPI_GELU_BWD "
              "[| OT_EPI_ROWDOT] or OT_EPI_BIAS alone (epilogue %d)", epi);
   OT_REQUIRE(!p.gelu_out || (!edge && (kern != nullptr)), "ot_mixed_gemm_rms: gelu_out needs whole tiles");
-  OT_REQUIRE(!p.xn_out || (plane && x == OT_AX_RMSNORM && a_rstd && a_gamma && p.ldxn % 8 == 0 &&
+  OT_REQUIRE(!p.xn_out || (plane && x == OT_AX_RMSNORM && a_rstd && a_gamma && p.ldxn % 8 == 0 && K <= 1024 &&
                            ((uintptr_t)p.xn_out % 16) == 0),
-             "ot_mixed_gemm_rms: xn_out needs the plane GEMM with the RMSNorm prologue, ldxn %% 8 == 0 and 16-B "
+             "ot_mixed_gemm_rms: xn_out needs the plane GEMM with the RMSNorm prologue, K <= 1024, ldxn %% 8 == 0 and 16-B "
              "alignment");
   OT_REQUIRE(!p.rowpart || plane, "ot_mixed_gemm_rms: OT_EPI_ROW_RSTD with N = %d > %d needs the plane GEMM "
              "(split mode, a pre-split B image, 16-B aligned A)", N, GT);
+  // (+ K floats of gamma behind the stage buffers for the xn_out side output)
+  const size_t xn_lds = p.xn_out ? (size_t)K * 4 : 0;
   const size_t launch_shmem = !plane ? shmem
-                              : one ? std::max((size_t)3 * pg_stage_bytes<1>(), (size_t)(64 * (GT + 4) + 8 * GT) * 4)
-                                    : (size_t)(g_plane_cfg == 0 ? 3 : 2) * PG_STG_BYTES;
+                              : one ? std::max((size_t)3 * pg_stage_bytes<1>() + xn_lds, (size_t)(64 * (GT + 4) + 8 * GT) * 4)
+                                    : (size_t)(g_plane_cfg == 0 ? 3 : 2) * PG_STG_BYTES + xn_lds;
   OT_REQUIRE(kern || !rms_flags, "ot_mixed_gemm_rms: no specialised kernel for epilogue flags %d", epi);
   if (!kern) {   // any other combination: generic instantiation (run-time prologue/epilogue)
     if (mode == OT_GEMM_NT && split && one)
@@ -1978,12 +2037,12 @@ extern "C" int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * WBR * WLD * 4);
       (void)hipGetLastError();
     });
-    const size_t copy_shmem = (size_t)WG_NST * WG_STB;
+    const size_t copy_shmem = (size_t)WG_LDS;
     if (copy && copy_shmem > 64 * 1024) {
       static std::once_flag copy_once;
       std::call_once(copy_once, [] {
         for (void (*k)(WgradArgs) : {wgrad_bf16_kernel<true>, wgrad_bf16_kernel<false>})
-          (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, WG_NST * WG_STB);
+          (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, WG_LDS);
         (void)hipGetLastError();
       });
     }

@@ -307,6 +307,12 @@ int ot_rmsnorm_bwd(const float* dy, int64_t lddy, const float* x, int64_t ldx, c
 int ot_dropout_apply(const float* src, int64_t lds, float* dst, int64_t ldd, int64_t rows, int d,
                      uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
                      const int32_t* tail_pos, void* stream);
+/* ot_dropout_apply with the masked rows stored rounded to bf16 (uint16 bits, ldd in elements): the bf16
+ * mode's dY of the FFN2 GEMM, whose consumers (the FFN2 dgrad's A operand, the W2 weight gradient's D)
+ * round it to bf16 anyway */
+int ot_dropout_apply_bf16(const float* src, int64_t lds, uint16_t* dst, int64_t ldd, int64_t rows, int d,
+                          uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
+                          const int32_t* tail_pos, void* stream);
 size_t ot_rows_colsum_workspace_size(int64_t nrows, int ncols);
 int ot_rows_colsum(const float* src, int64_t ld, const int32_t* rows, int64_t nrows, int ncols,
                    float* out, int accumulate, void* workspace, size_t ws_bytes, void* stream);

@@ -89,6 +89,7 @@ SIGNATURES = {
     'ot_rmsnorm_bwd': (c_int, [P, I64, P, I64, P, P, P, I64, c_int, c_int, P, P, I64, P, I64, c_uint32,
                                c_uint32, c_float, c_int, c_int, P, P, c_int, I64, c_int, P, c_size_t, P]),
     'ot_dropout_apply': (c_int, [P, I64, P, I64, I64, c_int, c_uint32, c_uint32, c_float, c_int, c_int, P, P]),
+    'ot_dropout_apply_bf16': (c_int, [P, I64, P, I64, I64, c_int, c_uint32, c_uint32, c_float, c_int, c_int, P, P]),
     'ot_rows_colsum_workspace_size': (c_size_t, [I64, c_int]),
     'ot_rows_colsum': (c_int, [P, I64, P, I64, c_int, P, c_int, P, c_size_t, P]),
     'ot_ns_assemble': (c_int, [P, c_int, P, c_int, P, I64, P]),

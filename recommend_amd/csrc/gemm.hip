@@ -1827,6 +1827,8 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
     OT_PSPEC_BF(OT_EPI_RMSNORM_BWD)
     OT_PSPEC_BF(OT_EPI_RMSNORM_BWD | OT_EPI_DROPOUT)
     OT_PSPEC_BF(0)
+    OT_PSPEC_BF(OT_EPI_GELU_BWD | OT_EPI_ROWDOT | OT_EPI_C_BF16 | OT_EPI_AUX_BF16)
+    OT_PSPEC_BF(OT_EPI_GELU_BWD | OT_EPI_ROWDOT | OT_EPI_C_BF16)
 #undef OT_PSPEC_BF
     if (pk) { kern = pk; plane = true; }
   }

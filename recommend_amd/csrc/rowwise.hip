@@ -171,7 +171,10 @@ __global__ void rows_colsum_kernel(const float* __restrict__ src, int64_t ld, co
   part[(int64_t)blockIdx.y * ncols + c] = s;
 }
 
-__global__ void dropout_apply_kernel(const float* __restrict__ src, int64_t lds, float* dst, int64_t ldd,
+// OUT: float (f32 rows) or uint16_t (bf16 rows, rounded to nearest even: the bf16 mode's FFN2 dgrad A operand
+// and W2 weight-gradient D operand, which round it so anyway)
+template <typename OUT>
+__global__ void dropout_apply_kernel(const float* __restrict__ src, int64_t lds, OUT* dst, int64_t ldd,
                                      int64_t rows, int d, uint32_t seed, uint32_t site, uint32_t thr, float scale,
                                      int tail_K, int tail_I, const int32_t* tail_pos) {
   const int64_t i4 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
@@ -185,7 +188,8 @@ __global__ void dropout_apply_kernel(const float* __restrict__ src, int64_t lds,
   v.y = drop_keep(seed, site, base + 1, thr) ? v.y * scale : 0.f;
   v.z = drop_keep(seed, site, base + 2, thr) ? v.z * scale : 0.f;
   v.w = drop_keep(seed, site, base + 3, thr) ? v.w * scale : 0.f;
-  *reinterpret_cast<f32x4*>(dst + r * ldd + c) = v;
+  if constexpr (sizeof(OUT) == 2) *reinterpret_cast<u32x2*>(dst + r * ldd + c) = bf16_rne4(v);
+  else *reinterpret_cast<f32x4*>(dst + r * ldd + c) = v;
 }
 
 inline int tpr_for(int d) {
@@ -277,10 +281,24 @@ extern "C" int ot_dropout_apply(const float* src, int64_t lds, float* dst, int64
   OT_REQUIRE(src && dst && d % 4 == 0 && lds % 4 == 0 && ldd % 4 == 0, "ot_dropout_apply: bad args");
   OT_REQUIRE(tail_K > 0 && tail_I >= tail_K, "ot_dropout_apply: bad tail map");
   if (rows == 0) return OT_OK;
-  hipLaunchKernelGGL(dropout_apply_kernel, dim3(ceil_div(rows * d / 4, 256)), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(dropout_apply_kernel<float>, dim3(ceil_div(rows * d / 4, 256)), dim3(256), 0, (hipStream_t)stream,
                      src, lds, dst, ldd, rows, d, seed, site, drop_threshold(drop_rate),
                      drop_rate < 1.f ? 1.f / (1.f - drop_rate) : 0.f, tail_K, tail_I, tail_pos);
   OT_LAUNCH_CHECK("ot_dropout_apply");
+  return OT_OK;
+}
+
+extern "C" int ot_dropout_apply_bf16(const float* src, int64_t lds, uint16_t* dst, int64_t ldd, int64_t rows, int d,
+                                     uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
+                                     const int32_t* tail_pos, void* stream) {
+  OT_REQUIRE(src && dst && d % 4 == 0 && lds % 4 == 0 && ldd % 4 == 0 && ((uintptr_t)dst % 8) == 0,
+             "ot_dropout_apply_bf16: bad args");
+  OT_REQUIRE(tail_K > 0 && tail_I >= tail_K, "ot_dropout_apply_bf16: bad tail map");
+  if (rows == 0) return OT_OK;
+  hipLaunchKernelGGL(dropout_apply_kernel<uint16_t>, dim3(ceil_div(rows * d / 4, 256)), dim3(256), 0,
+                     (hipStream_t)stream, src, lds, dst, ldd, rows, d, seed, site, drop_threshold(drop_rate),
+                     drop_rate < 1.f ? 1.f / (1.f - drop_rate) : 0.f, tail_K, tail_I, tail_pos);
+  OT_LAUNCH_CHECK("ot_dropout_apply_bf16");
   return OT_OK;
 }
 

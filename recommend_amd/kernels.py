@@ -317,8 +317,10 @@ def rmsnorm_bwd(dy: Ptrish, lddy: int, x: Ptrish, ldx: int, gamma: Ptrish, rstd:
 
 
 def dropout_apply(src, lds, dst, ldd, rows, d, seed, site, drop, tail) -> None:
+    """dst float32, or int16 (bf16 bits: ot_dropout_apply_bf16)."""
     ev = _probe.begin() if _probe is not None else None
-    call('ot_dropout_apply', ptr(src), lds, ptr(dst), ldd, rows, d, seed & 0xFFFFFFFF, site, float(drop), tail[0],
+    fn = 'ot_dropout_apply_bf16' if getattr(dst, 'dtype', None) == torch.int16 else 'ot_dropout_apply'
+    call(fn, ptr(src), lds, ptr(dst), ldd, rows, d, seed & 0xFFFFFFFF, site, float(drop), tail[0],
          tail[1], _sel(tail), stream())
     if ev is not None:
         _probe.end('rowwise', 0.0, ev)

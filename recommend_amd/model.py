@@ -327,18 +327,20 @@ class _Block(torch.autograd.Function):
         nca, nct = maps['all'].chunks.shape[0], maps['tail'].chunks.shape[0]
         G = cfg.num_groups
         dx2 = dx2.contiguous()
-        # FFN branch: dY2 = mask(dx2)
+        rowdot = None
+        fused2 = m.fuse_bwd2 and not m.fuse_bwd and f % TILE == 0
+        du_bf = (fused2 and h is not None and m.du_bf16 and m.bimg(f'blk.{l}.w1', 'dgrad') is not None)
+        # FFN branch: dY2 = mask(dx2) — in bf16 with the bf16 dU path (its two readers, the FFN2 dgrad's A and
+        # the W2 weight gradient's D, round it to bf16; the latter then runs copy-staged)
         if rate > 0:
-            dy2 = torch.empty_like(dx2)
+            dy2 = torch.empty(B * Kq, d, device=dev, dtype=torch.int16 if du_bf and m.dy_bf16 else torch.float32)
             K.dropout_apply(dx2, d, dy2, d, B * Kq, d, seed, 2 * l + 1, rate, tail)
         else:
             dy2 = dx2
-        rowdot = None
-        fused2 = m.fuse_bwd2 and not m.fuse_bwd and f % TILE == 0
+        dy_bf = dy2.dtype == torch.int16
         # bf16 mode (C5): dU is stored in bf16 by the FFN2 dgrad epilogue (OT_EPI_C_BF16); its two consumers,
         # the FFN1 dgrad (bf16 A, plane GEMM) and the W1 weight gradient (OT_WG_D_BF16), rounded it to bf16 at
         # fragment / staging time anyway, so only b1's gradient (a column sum of dU) sees the rounding
-        du_bf = (fused2 and h is not None and m.du_bf16 and m.bimg(f'blk.{l}.w1', 'dgrad') is not None)
         du = torch.empty(B * Kq, f, device=dev, dtype=torch.int16 if du_bf else torch.float32)
         cbf = OT_EPI_C_BF16 if du_bf else 0
         # bf16 mode with the fused norm2 backward (C5): the FFN2 dgrad epilogue, which reads U for GELU'
@@ -351,13 +353,14 @@ class _Block(torch.autograd.Function):
             with m.side(u if h is None else h, dy2):   # weight gradients overlap the dgrad chain on a second stream
                 K.wgrad(u if h is None else h, f, mt['rows'][1], dy2, d, mt['rows'][1], f, d, mt, nct, G,
                         m.g(f'blk.{l}.w2'), f * d, m.g(f'blk.{l}.b2'), d,
-                        a_xform=OT_AX_GELU if h is None else OT_AX_BF16, accumulate=acc, device=dev,
+                        a_xform=(OT_AX_GELU if h is None else OT_AX_BF16) | (OT_WG_D_BF16 if dy_bf else 0),
+                        accumulate=acc, device=dev,
                         m_rows=maps['tail'].nrows, rowmap=maps['tail'])
         if fused2:
             # d > 128: the FFN2 dgrad also emits rowdot[row][f-tile] = sum dU (U - b1) for the norm2 backward
             rowdot = torch.empty(B * Kq, f // TILE, device=dev)
             K.gemm_rms(OT_GEMM_NT, dy2, d, d, mt['rows'][1], m.p(f'blk.{l}.w2'), f * d, d, f, mt['tile_group'], nt,
-                       du, f, mt['rows'][1], aux=u, ldaux=f,
+                       du, f, mt['rows'][1], aux=u, ldaux=f, a_xform=OT_AX_BF16 if dy_bf else 0,
                        epi=OT_EPI_GELU_BWD | OT_EPI_ROWDOT | cbf | (OT_EPI_AUX_BF16 if u.dtype == torch.int16 else 0),
                        bias=m.p(f'blk.{l}.b1'), bias_gstride=f, rowdot=rowdot, rowdot_n=f // TILE,
                        m_rows=maps['tail'].nrows, device=dev, bimg=m.bimg(f'blk.{l}.w2', 'dgrad'),
@@ -634,6 +637,8 @@ class OneTransModel(nn.Module):
         # bf16 mode, training: bf16 normalised QKV / FFN1 inputs for the Wqkv / W1 weight gradients
         # (ONETRANS_XN_BF16=0: those re-read the f32 inputs and re-apply the norm)
         self.xn_bf16 = os.environ.get('ONETRANS_XN_BF16', '1') != '0'
+        # ... and the FFN2 dgrad's dY in bf16 (ONETRANS_DY_BF16=0: f32)
+        self.dy_bf16 = os.environ.get('ONETRANS_DY_BF16', '1') != '0'
         # block weight gradients run on a second stream, overlapping the dgrad chain
         self.overlap_wgrad = os.environ.get('ONETRANS_OVERLAP_WGRAD', '1') != '0'
         self._side = None

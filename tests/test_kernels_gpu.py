@@ -768,3 +768,18 @@ def test_wgrad_copy_staged_bf16(dev, K_, N):
         sel = torch.from_numpy(sel[sel >= 0]).long()
         ref = Ad[sel].T @ Dd[sel]
         assert (res[0][0][gi].double().cpu() - ref).abs().max().item() <= 1e-4 * ref.abs().max().item() + 1e-3
+
+
+def test_dropout_apply_bf16(dev):
+    """ot_dropout_apply_bf16: the masked, rescaled rows of ot_dropout_apply rounded to nearest even (the bf16
+    mode's FFN2 dY), bit for bit, through a pyramid tail map."""
+    B, I, Kq, d = 23, 11, 6, 256
+    g = torch.Generator().manual_seed(9)
+    src = torch.randn(B * Kq, d, generator=g).to(dev)
+    ref = torch.empty(B * Kq, d, device=dev)
+    out = torch.zeros(B * Kq, d, dtype=torch.int16, device=dev)
+    K.dropout_apply(src, d, ref, d, B * Kq, d, 1234, 7, 0.1, (Kq, I))
+    K.dropout_apply(src, d, out, d, B * Kq, d, 1234, 7, 0.1, (Kq, I))
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref.to(torch.bfloat16).view(torch.int16))
+    assert 0.05 < (ref == 0).float().mean().item() < 0.15

@@ -286,14 +286,19 @@ struct Fp8AttnArgs {
 // one wave per (b, h), 4 waves per block.  T8 = 2: two-term operands, S^T = Kh Qh + Kh Ql + Kl Qh and
 // O^T += Vh Ph + Vh Pl + Vl Ph (the lo x lo products dropped: below the e4m3 pair's own rounding); P's lo
 // term is e4m3((P 2^8 - Ph) 2^4) at MFMA scale 2^-4.
-template <int HD, int T8>
-__global__ __launch_bounds__(256) void attn_fwd_fp8_kernel(Fp8AttnArgs p) {
+// PW > 1: one workgroup of PW waves per (b, h), wave w taking query blocks w, w + PW, ...: the waves sweep the
+// pair's key blocks at about the same time, so its K / V packs are read from L2 by PW waves instead of
+// from the Infinity Cache by one (PW = 1, one pair per wave, 4 per block: 21 GB of L3 fetch per C5 layer,
+// the kernel bound at ~7 TB/s).
+template <int HD, int T8, int PW>
+__global__ __launch_bounds__(PW > 1 ? 64 * PW : 256) void attn_fwd_fp8_kernel(Fp8AttnArgs p) {
   static_assert(HD == 64 || HD == 128, "fp8 attention: head_dim 64 or 128");
   constexpr int NKS = HD / 64;                   // 64-dim k steps of S^T
   constexpr int NC = HD / 32;                    // 32-dim output chunks
   const int lane = threadIdx.x & 63, li = lane & 31, hh = lane >> 5;
-  const int pair = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int pair = PW > 1 ? (int)blockIdx.x : (int)(blockIdx.x * 4 + (threadIdx.x >> 6));
   if (pair >= p.B * p.H) return;
+  const int qb0 = PW > 1 ? (int)(threadIdx.x >> 6) : 0;
   const int b = pair / p.H, h = pair % p.H;
   const int I = p.I, K = p.K, q_off = I - K;
   const int64_t Ip = fp8_ipad(I);
@@ -308,7 +313,7 @@ __global__ __launch_bounds__(256) void attn_fwd_fp8_kernel(Fp8AttnArgs p) {
   const int nqb = (K + 31) / 32;
   const float qscale = p.scale * 1.4426950408889634f;   // log2(e) / sqrt(hd)
 
-  for (int qb = 0; qb < nqb; ++qb) {
+  for (int qb = qb0; qb < nqb; qb += (PW > 1 ? PW : 1)) {
     const int j = 32 * qb + li;
     const int jc = j < K ? j : K - 1;
     const int qpos = qp ? qp[jc] : q_off + jc;
@@ -536,10 +541,18 @@ extern "C" int ot_attn_fwd_fp8_ex(float* qkv, int64_t ld, int B, int H, int I, i
   hipLaunchKernelGGL(pk, pg, dim3(256), 0, s, qkv, ld, H, I, f, dq);
   OT_LAUNCH_CHECK("ot_attn_fwd_fp8(pack)");
   Fp8AttnArgs p{qkv, ld, H * head_dim, out, lse, B, H, I, K, 1.f / sqrtf((float)head_dim), qpos, f, dq};
-  const unsigned grid = ceil_div(BH, 4);
-  auto fk = head_dim == 64 ? (two ? attn_fwd_fp8_kernel<64, 2> : attn_fwd_fp8_kernel<64, 1>)
-                           : (two ? attn_fwd_fp8_kernel<128, 2> : attn_fwd_fp8_kernel<128, 1>);
-  hipLaunchKernelGGL(fk, dim3(grid), dim3(256), 0, s, p);
+  // waves per (b, h): ONETRANS_FP8_FWD_WAVES (1: one pair per wave; 4 / 8: a workgroup per pair)
+  static const int pw = [] {
+    const char* e = std::getenv("ONETRANS_FP8_FWD_WAVES");
+    const int v = e ? std::atoi(e) : 8;
+    return (v == 1 || v == 4) ? v : 8;
+  }();
+#define OT_FP8K(PW_) (head_dim == 64 ? (two ? attn_fwd_fp8_kernel<64, 2, PW_> : attn_fwd_fp8_kernel<64, 1, PW_>) \
+                                     : (two ? attn_fwd_fp8_kernel<128, 2, PW_> : attn_fwd_fp8_kernel<128, 1, PW_>))
+  auto fk = pw == 1 ? OT_FP8K(1) : pw == 4 ? OT_FP8K(4) : OT_FP8K(8);
+#undef OT_FP8K
+  const unsigned grid = pw == 1 ? (unsigned)ceil_div(BH, 4) : (unsigned)BH;
+  hipLaunchKernelGGL(fk, dim3(grid), dim3(pw == 1 ? 256 : 64 * pw), 0, s, p);
   OT_LAUNCH_CHECK("ot_attn_fwd_fp8");
   return OT_OK;
 }

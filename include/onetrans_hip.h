@@ -244,6 +244,12 @@ int ot_attn_fwd_fp8(const float* qkv, int64_t ld, int B, int H, int I, int K, co
                            * products (hi.hi + hi.lo + lo.hi): ~7 significant bits per operand */
 int ot_attn_fwd_fp8_ex(float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos, int head_dim,
                        float* out, float* lse, void* workspace, size_t ws_bytes, int flags, void* stream);
+/* ot_attn_fwd_fp8_ex with OT_FP8_DEQUANT implied and the dequantised Q (kept rows) / K / V written rounded to
+ * bf16 into deq16 ([B*I][ld] uint16, the qkv layout; 16-B aligned, ld % 8 == 0) instead of in place: the
+ * bf16 backward's operands (OT_ATTN_QKV_BF16), which it would round so anyway; qkv is only read */
+int ot_attn_fwd_fp8_deq16(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos,
+                          int head_dim, float* out, float* lse, void* workspace, size_t ws_bytes, int flags,
+                          uint16_t* deq16, void* stream);
 /* dqkv: like qkv (dq written on the K kept query rows only; dk, dv on all rows);
  * ws: ot_attn_bwd_workspace_size(B, H, K) bytes (row stats padded to 32 queries per (b, h)) */
 size_t ot_attn_bwd_workspace_size(int B, int H, int K);
@@ -264,6 +270,9 @@ int ot_attn_bwd_ex(const float* qkv, int64_t ld, const float* out, const float* 
  * Key-grouped backward only (ot_attn_bwd_dqkv_bf16_supported); workspace
  * ot_attn_bwd_flags_workspace_size (one more [B*K][H*head_dim] f32 dQ slot: slice 0's). */
 #define OT_ATTN_DQKV_BF16 1
+/* OT_ATTN_QKV_BF16: qkv holds bf16 (uint16 bits, ld in elements, 16-B aligned): the fp8 forward's dequantised
+ * operands from ot_attn_fwd_fp8_deq16 (same key-grouped condition) */
+#define OT_ATTN_QKV_BF16 2
 int ot_attn_bwd_dqkv_bf16_supported(int I, int K, int head_dim, int selected);
 size_t ot_attn_bwd_flags_workspace_size(int B, int H, int I, int K, int head_dim, int selected, int flags);
 int ot_attn_bwd_flags(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,

@@ -23,6 +23,7 @@ OT_EPI_ROW_RSTD, OT_EPI_RMSNORM_BWD, OT_EPI_ROWDOT = 64, 128, 256
 OT_EPI_C_BF16 = 512
 OT_EPI_AUX_BF16 = 1024
 OT_ATTN_DQKV_BF16 = 1
+OT_ATTN_QKV_BF16 = 2
 OT_WG_D_BF16 = 8
 OT_MATMUL_F32, OT_MATMUL_SPLIT_BF16, OT_MATMUL_BF16 = 0, 1, 2
 OT_FP8_DEQUANT, OT_FP8_TWO_TERM = 1, 2
@@ -75,6 +76,7 @@ SIGNATURES = {
     'ot_attn_fwd_fp8_workspace_size': (c_size_t, [c_int, c_int, c_int, c_int]),
     'ot_attn_fwd_fp8': (c_int, [P, I64, c_int, c_int, c_int, c_int, P, c_int, P, P, P, c_size_t, P]),
     'ot_attn_fwd_fp8_ex': (c_int, [P, I64, c_int, c_int, c_int, c_int, P, c_int, P, P, P, c_size_t, c_int, P]),
+    'ot_attn_fwd_fp8_deq16': (c_int, [P, I64, c_int, c_int, c_int, c_int, P, c_int, P, P, P, c_size_t, c_int, P, P]),
     'ot_attn_bwd_workspace_size': (c_size_t, [c_int, c_int, c_int]),
     'ot_attn_bwd': (c_int, [P, I64, P, P, P, c_int, c_int, c_int, c_int, P, c_int, P, P, P]),
     'ot_attn_bwd_ex_workspace_size': (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),

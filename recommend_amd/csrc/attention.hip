@@ -51,6 +51,9 @@ struct AttnArgs {
   // slice s writes its dQ into dqpart[s] and attn_dq_reduce_kernel stores the rounded sum (slice 0 first,
   // then the later slices in order: the f32 path's sum, rounded once)
   int dq_bf16;
+  // OT_ATTN_QKV_BF16 (key-grouped backward only): qkv holds bf16 (uint16 bits, ld in elements) — the fp8
+  // forward's dequantised operands, which the bf16 backward would round to bf16 anyway
+  int qkv_bf16;
 };
 
 // position of kept query j (< K) of the sample whose qpos slice is qp (null: the tail rule)
@@ -1034,7 +1037,7 @@ __global__ __launch_bounds__(64 * WAVES, TERMS == 1 ? 2 : 1) void attn_bwd_split
 template <int HD, int NW>
 constexpr int BWDG_LDS() { return 2 * 32 * HD * 2 + NW * (2 * 32 * HD * 2 + 32 * 32 * 2) + NW * 32 * HD * 4; }
 
-template <int HD, int NW>
+template <int HD, int NW, bool QB = false>
 __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kernel(AttnArgs p) {
   static_assert(HD == 64 || HD == 32, "grouped backward: HD 32 or 64");
   constexpr int NS = HD / 16;                          // k-steps over the head dim
@@ -1068,7 +1071,18 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kerne
   const int kb = slice * NW + w;                       // this wave's key block (>= nkb: an idle wave, P = 0)
   const int key0 = 32 * kb;
   const int kpos = key0 + li;
-  {
+  const uint16_t* Q16 = reinterpret_cast<const uint16_t*>(p.qkv) + tok0 * p.ld + h * HD;
+  if constexpr (QB) {                                  // bf16 operands: the images are copies
+    const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int st = 0; st < NS; ++st) {
+      const int64_t o = (int64_t)kpos * p.ld + (HD / 2) * hh + 8 * st;
+      const u32x4 kB = kpos < I ? *reinterpret_cast<const u32x4*>(Q16 + p.d + o) : z;
+      const u32x4 vB = kpos < I ? *reinterpret_cast<const u32x4*>(Q16 + 2 * p.d + o) : z;
+      *reinterpret_cast<u32x4*>(kimg + (li * HD + (HD / 2) * hh + 8 * st) * 2) = kB;
+      *reinterpret_cast<u32x4*>(vimg + (li * HD + (HD / 2) * hh + 8 * st) * 2) = vB;
+    }
+  } else {
     float kf[HD / 2], vf[HD / 2];
     load_frag<HD>(kf, Kp, p.ld, kpos, I, hh);          // rows >= I: zeros (masked below)
     load_frag<HD>(vf, V, p.ld, kpos, I, hh);
@@ -1090,6 +1104,7 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kerne
   qbs = qbs < 0 ? 0 : qbs / 32;
   // cooperative Q / dO block loads: thread t takes float4 e = t + NT i of the [32][HD] block
   f32x4 pq[PT], po[PT];
+  u32x2 pq16[PT];
   auto load_q = [&](int qb) {
 #pragma unroll
     for (int i = 0; i < PT; ++i) {
@@ -1097,7 +1112,10 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kerne
       const int row = e / (HD / 4), c4 = e % (HD / 4);
       const int j = 32 * qb + row;
       const int jj = j < K ? j : K - 1;                // padded queries: a real row (lse = +inf masks it)
-      pq[i] = e < F4 ? *reinterpret_cast<const f32x4*>(Q + (int64_t)(q_off + jj) * p.ld + 4 * c4) : f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (QB)
+        pq16[i] = e < F4 ? *reinterpret_cast<const u32x2*>(Q16 + (int64_t)(q_off + jj) * p.ld + 4 * c4) : u32x2{0u, 0u};
+      else
+        pq[i] = e < F4 ? *reinterpret_cast<const f32x4*>(Q + (int64_t)(q_off + jj) * p.ld + 4 * c4) : f32x4{0.f, 0.f, 0.f, 0.f};
       po[i] = e < F4 ? *reinterpret_cast<const f32x4*>(dO + (int64_t)jj * p.d + 4 * c4) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   };
@@ -1106,7 +1124,8 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kerne
     for (int i = 0; i < PT; ++i) {
       const int e = t + NT * i;
       if (e < F4) {
-        *reinterpret_cast<u32x2*>(qimg + e * 8) = bf16_rne4(pq[i]);
+        if constexpr (QB) *reinterpret_cast<u32x2*>(qimg + e * 8) = pq16[i];
+        else *reinterpret_cast<u32x2*>(qimg + e * 8) = bf16_rne4(pq[i]);
         *reinterpret_cast<u32x2*>(oimg + e * 8) = bf16_rne4(po[i]);
       }
     }
@@ -1625,7 +1644,10 @@ extern "C" int ot_attn_bwd_ex(const float* qkv, int64_t ld, const float* out, co
 extern "C" int ot_attn_bwd_flags(const float* qkv, int64_t ld, const float* out, const float* dout,
                                  const float* lse, int B, int H, int I, int K, const int32_t* qpos, int head_dim,
                                  void* dqkv, int flags, void* workspace, size_t ws_bytes, void* stream) {
-  OT_REQUIRE(!(flags & ~OT_ATTN_DQKV_BF16), "ot_attn_bwd_flags: unknown flags %d", flags);
+  OT_REQUIRE(!(flags & ~(OT_ATTN_DQKV_BF16 | OT_ATTN_QKV_BF16)), "ot_attn_bwd_flags: unknown flags %d", flags);
+  OT_REQUIRE(!(flags & OT_ATTN_QKV_BF16) || (ot_attn_bwd_dqkv_bf16_supported(I, K, head_dim, qpos != nullptr) &&
+                                             ((uintptr_t)qkv % 16) == 0 && ld % 8 == 0),
+             "ot_attn_bwd_flags: OT_ATTN_QKV_BF16 needs the key-grouped bf16 backward, 16-B aligned qkv, ld %% 8 == 0");
   OT_REQUIRE(ws_bytes >= ot_attn_bwd_flags_workspace_size(B, H, I, K, head_dim, qpos != nullptr, flags),
              "ot_attn_bwd_flags: workspace too small");
   OT_REQUIRE(!(flags & OT_ATTN_DQKV_BF16) || ot_attn_bwd_dqkv_bf16_supported(I, K, head_dim, qpos != nullptr),
@@ -1664,14 +1686,20 @@ static int attn_bwd_impl(const float* qkv, int64_t ld, const float* out, const f
     p.kgroup = G;
     p.dqpart = delta_ws + ot_attn_bwd_workspace_size(B, H, K) / sizeof(float);
     p.dq_bf16 = (flags & OT_ATTN_DQKV_BF16) ? 1 : 0;
-    void (*kern)(AttnArgs) = G == 8 ? (head_dim == 32 ? attn_bwd_group_kernel<32, 8> : attn_bwd_group_kernel<64, 8>)
-                                    : (head_dim == 32 ? attn_bwd_group_kernel<32, 4> : attn_bwd_group_kernel<64, 4>);
+    p.qkv_bf16 = (flags & OT_ATTN_QKV_BF16) ? 1 : 0;
+    void (*kern)(AttnArgs) =
+        p.qkv_bf16 ? (G == 8 ? (head_dim == 32 ? attn_bwd_group_kernel<32, 8, true> : attn_bwd_group_kernel<64, 8, true>)
+                             : (head_dim == 32 ? attn_bwd_group_kernel<32, 4, true> : attn_bwd_group_kernel<64, 4, true>))
+                   : (G == 8 ? (head_dim == 32 ? attn_bwd_group_kernel<32, 8> : attn_bwd_group_kernel<64, 8>)
+                             : (head_dim == 32 ? attn_bwd_group_kernel<32, 4> : attn_bwd_group_kernel<64, 4>));
     const size_t lds = G == 8 ? (head_dim == 32 ? BWDG_LDS<32, 8>() : BWDG_LDS<64, 8>())
                               : (head_dim == 32 ? BWDG_LDS<32, 4>() : BWDG_LDS<64, 4>());
     static std::once_flag glds_once;
     std::call_once(glds_once, [] {
       for (void (*k)(AttnArgs) : {attn_bwd_group_kernel<32, 8>, attn_bwd_group_kernel<64, 8>,
-                                  attn_bwd_group_kernel<32, 4>, attn_bwd_group_kernel<64, 4>})
+                                  attn_bwd_group_kernel<32, 4>, attn_bwd_group_kernel<64, 4>,
+                                  attn_bwd_group_kernel<32, 8, true>, attn_bwd_group_kernel<64, 8, true>,
+                                  attn_bwd_group_kernel<32, 4, true>, attn_bwd_group_kernel<64, 4, true>})
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, BWDG_LDS<64, 8>());
       (void)hipGetLastError();
     });

@@ -132,7 +132,7 @@ __device__ __forceinline__ i32x4 quant16(const float (&x)[16], int e, float (&r)
 // T8 = 2: every element also gets a lo term, lo = e4m3(x - hi) with its own block scale (same blocks).
 template <int HD, int T8>
 __global__ __launch_bounds__(256) void attn_fp8_pack_kernel(float* qkv, int64_t ld, int H, int I, Fp8Pack f,
-                                                            int dequant) {
+                                                            int dequant, uint16_t* deq16) {
   constexpr int VLD = HD + 1;
   __shared__ float vs_f[64 * VLD];
   __shared__ __attribute__((aligned(16))) uint8_t vt_img[T8][HD * 64];
@@ -183,9 +183,19 @@ __global__ __launch_bounds__(256) void attn_fp8_pack_kernel(float* qkv, int64_t 
       for (int j = 0; j < 16; ++j) r[j] = x[j] - r[j] + rl[j];      // hi + lo (dequantised)
     }
     if (dequant && key < I) {
-      f32x4* dst = reinterpret_cast<f32x4*>(base + (int64_t)key * ld + d + 16 * part);
+      if (deq16) {                                   // bf16 copy (the backward rounds to bf16 anyway)
+        uint16_t* dst = deq16 + ((int64_t)b * I + key) * ld + h * HD + d + 16 * part;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) dst[q] = f32x4{r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]};
+        for (int q = 0; q < 4; q += 2) {
+          const u32x2 lo = bf16_rne4(f32x4{r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]});
+          const u32x2 hi = bf16_rne4(f32x4{r[4 * q + 4], r[4 * q + 5], r[4 * q + 6], r[4 * q + 7]});
+          *reinterpret_cast<u32x4*>(dst + 4 * q) = u32x4{lo.x, lo.y, hi.x, hi.y};
+        }
+      } else {
+        f32x4* dst = reinterpret_cast<f32x4*>(base + (int64_t)key * ld + d + 16 * part);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dst[q] = f32x4{r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]};
+      }
     }
   }
 
@@ -268,7 +278,13 @@ __global__ __launch_bounds__(256) void attn_fp8_pack_kernel(float* qkv, int64_t 
       const int kk = i / (HD / 4), c4 = i % (HD / 4);
       const int key = 64 * kb + kk;
       const float* src = vs_f + kk * VLD + 4 * c4;
-      if (key < I) *reinterpret_cast<f32x4*>(base + (int64_t)key * ld + 2 * d + 4 * c4) = f32x4{src[0], src[1], src[2], src[3]};
+      if (key < I) {
+        if (deq16)
+          *reinterpret_cast<u32x2*>(deq16 + ((int64_t)b * I + key) * ld + h * HD + 2 * d + 4 * c4) =
+              bf16_rne4(f32x4{src[0], src[1], src[2], src[3]});
+        else
+          *reinterpret_cast<f32x4*>(base + (int64_t)key * ld + 2 * d + 4 * c4) = f32x4{src[0], src[1], src[2], src[3]};
+      }
     }
   }
 }
@@ -281,6 +297,7 @@ struct Fp8AttnArgs {
   const int32_t* qpos;
   Fp8Pack f;
   int dequant;
+  uint16_t* deq16;           // dequantised operands in bf16 here (ld as qkv) instead of in place, or null
 };
 
 // one wave per (b, h), 4 waves per block.  T8 = 2: two-term operands, S^T = Kh Qh + Kh Ql + Kl Qh and
@@ -369,11 +386,23 @@ __global__ __launch_bounds__(PW > 1 ? 64 * PW : 256) void attn_fwd_fp8_kernel(Fp
             dq[1][4 * w] += c.x; dq[1][4 * w + 1] += c.y; dq[1][4 * w + 2] += c.z; dq[1][4 * w + 3] += c.w;
           }
         }
+        if (p.deq16) {
+          uint16_t* d16 = p.deq16 + ((int64_t)b * I + qpos) * p.ld + h * HD + 64 * ks + 16 * hh;
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
-          *reinterpret_cast<f32x4*>(src + 4 * w) = f32x4{dq[0][4 * w], dq[0][4 * w + 1], dq[0][4 * w + 2], dq[0][4 * w + 3]};
-          *reinterpret_cast<f32x4*>(src + 32 + 4 * w) =
-              f32x4{dq[1][4 * w], dq[1][4 * w + 1], dq[1][4 * w + 2], dq[1][4 * w + 3]};
+          for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+            for (int w = 0; w < 4; w += 2) {
+              const u32x2 lo = bf16_rne4(f32x4{dq[blk][4 * w], dq[blk][4 * w + 1], dq[blk][4 * w + 2], dq[blk][4 * w + 3]});
+              const u32x2 hi = bf16_rne4(f32x4{dq[blk][4 * w + 4], dq[blk][4 * w + 5], dq[blk][4 * w + 6], dq[blk][4 * w + 7]});
+              *reinterpret_cast<u32x4*>(d16 + 32 * blk + 4 * w) = u32x4{lo.x, lo.y, hi.x, hi.y};
+            }
+        } else {
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            *reinterpret_cast<f32x4*>(src + 4 * w) = f32x4{dq[0][4 * w], dq[0][4 * w + 1], dq[0][4 * w + 2], dq[0][4 * w + 3]};
+            *reinterpret_cast<f32x4*>(src + 32 + 4 * w) =
+                f32x4{dq[1][4 * w], dq[1][4 * w + 1], dq[1][4 * w + 2], dq[1][4 * w + 3]};
+          }
         }
       }
     }
@@ -517,9 +546,28 @@ extern "C" size_t ot_attn_fwd_fp8_workspace_size(int B, int H, int I, int head_d
   return fp8_pack_bytes((int64_t)B * H, I, head_dim);
 }
 
+static int attn_fwd_fp8_impl(float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos, int head_dim,
+                             float* out, float* lse, void* workspace, size_t ws_bytes, int flags, uint16_t* deq16,
+                             void* stream);
+
 extern "C" int ot_attn_fwd_fp8_ex(float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos,
                                   int head_dim, float* out, float* lse, void* workspace, size_t ws_bytes, int flags,
                                   void* stream) {
+  return attn_fwd_fp8_impl(qkv, ld, B, H, I, K, qpos, head_dim, out, lse, workspace, ws_bytes, flags, nullptr, stream);
+}
+
+extern "C" int ot_attn_fwd_fp8_deq16(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos,
+                                     int head_dim, float* out, float* lse, void* workspace, size_t ws_bytes,
+                                     int flags, uint16_t* deq16, void* stream) {
+  OT_REQUIRE(deq16 && ((uintptr_t)deq16 % 16) == 0 && ld % 8 == 0,
+             "ot_attn_fwd_fp8_deq16: deq16 needs 16-B alignment and ld %% 8 == 0");
+  return attn_fwd_fp8_impl(const_cast<float*>(qkv), ld, B, H, I, K, qpos, head_dim, out, lse, workspace, ws_bytes,
+                           flags | OT_FP8_DEQUANT, deq16, stream);
+}
+
+static int attn_fwd_fp8_impl(float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos, int head_dim,
+                             float* out, float* lse, void* workspace, size_t ws_bytes, int flags, uint16_t* deq16,
+                             void* stream) {
   OT_REQUIRE(qkv && out && lse, "ot_attn_fwd_fp8: null operand");
   OT_REQUIRE((flags & ~(OT_FP8_DEQUANT | OT_FP8_TWO_TERM)) == 0, "ot_attn_fwd_fp8: unknown flags 0x%x", flags);
   const int dq = (flags & OT_FP8_DEQUANT) ? 1 : 0;
@@ -538,9 +586,9 @@ extern "C" int ot_attn_fwd_fp8_ex(float* qkv, int64_t ld, int B, int H, int I, i
   hipStream_t s = (hipStream_t)stream;
   auto pk = head_dim == 64 ? (two ? attn_fp8_pack_kernel<64, 2> : attn_fp8_pack_kernel<64, 1>)
                            : (two ? attn_fp8_pack_kernel<128, 2> : attn_fp8_pack_kernel<128, 1>);
-  hipLaunchKernelGGL(pk, pg, dim3(256), 0, s, qkv, ld, H, I, f, dq);
+  hipLaunchKernelGGL(pk, pg, dim3(256), 0, s, qkv, ld, H, I, f, dq, deq16);
   OT_LAUNCH_CHECK("ot_attn_fwd_fp8(pack)");
-  Fp8AttnArgs p{qkv, ld, H * head_dim, out, lse, B, H, I, K, 1.f / sqrtf((float)head_dim), qpos, f, dq};
+  Fp8AttnArgs p{qkv, ld, H * head_dim, out, lse, B, H, I, K, 1.f / sqrtf((float)head_dim), qpos, f, dq, deq16};
   // waves per (b, h): ONETRANS_FP8_FWD_WAVES (1: one pair per wave; 4 / 8: a workgroup per pair)
   static const int pw = [] {
     const char* e = std::getenv("ONETRANS_FP8_FWD_WAVES");

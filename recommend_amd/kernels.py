@@ -246,18 +246,22 @@ def split_images(base, desc_dev, ndesc, total_units, img) -> None:
 
 def attn_fwd(qkv: torch.Tensor, ld: int, B: int, H: int, I: int, K: int, hd: int, out: torch.Tensor,
              lse: torch.Tensor, qpos: Optional[torch.Tensor] = None, fp8: bool = False,
-             dequant: bool = False, fp8_terms: int = 1) -> None:
+             dequant: bool = False, fp8_terms: int = 1, deq16: Optional[torch.Tensor] = None) -> None:
     """ot_attn_fwd, or with ``fp8`` (head_dim 64/128) ot_attn_fwd_fp8_ex: QK^T and PV on block-scaled fp8
     MFMA, operands as one e4m3 term or two (``fp8_terms`` 2: hi + lo, OT_FP8_TWO_TERM); ``dequant``
     (training) also overwrites qkv's operands with their dequantised fp8 values (OT_FP8_DEQUANT) for the
-    backward."""
+    backward — or, given ``deq16`` (int16 [rows, ld]: bf16 bits), writes them rounded to bf16 there
+    (ot_attn_fwd_fp8_deq16; qkv is then only read)."""
     if fp8 and fp8_terms not in (1, 2):
         raise ValueError(f'fp8_terms {fp8_terms}: 1 or 2')
     ws = None
     if fp8:
         ws = workspace(size('ot_attn_fwd_fp8_workspace_size', B, H, I, hd), qkv.device)
     ev = _probe.begin() if _probe is not None else None
-    if fp8:
+    if fp8 and deq16 is not None:
+        call('ot_attn_fwd_fp8_deq16', ptr(qkv), ld, B, H, I, K, ptr(qpos), hd, ptr(out), ptr(lse), ptr(ws),
+             ws.numel(), _lib.OT_FP8_TWO_TERM if fp8_terms == 2 else 0, ptr(deq16), stream())
+    elif fp8:
         call('ot_attn_fwd_fp8_ex', ptr(qkv), ld, B, H, I, K, ptr(qpos), hd, ptr(out), ptr(lse), ptr(ws),
              ws.numel(), (_lib.OT_FP8_DEQUANT if dequant else 0) | (_lib.OT_FP8_TWO_TERM if fp8_terms == 2 else 0),
              stream())
@@ -274,8 +278,10 @@ def attn_bwd_bf16_supported(I, K, hd, qpos=None) -> bool:
 
 
 def attn_bwd(qkv, ld, out, dout, lse, B, H, I, K, hd, dqkv, qpos=None) -> None:
-    """dqkv float32, or int16 (bf16 bits: OT_ATTN_DQKV_BF16, see attn_bwd_bf16_supported)."""
-    flags = _lib.OT_ATTN_DQKV_BF16 if dqkv.dtype == torch.int16 else 0
+    """dqkv float32, or int16 (bf16 bits: OT_ATTN_DQKV_BF16, see attn_bwd_bf16_supported); qkv likewise
+    (int16: OT_ATTN_QKV_BF16, the fp8 forward's bf16 dequantised operands)."""
+    flags = ((_lib.OT_ATTN_DQKV_BF16 if dqkv.dtype == torch.int16 else 0)
+             | (_lib.OT_ATTN_QKV_BF16 if qkv.dtype == torch.int16 else 0))
     ws = workspace(size('ot_attn_bwd_flags_workspace_size', B, H, I, K, hd, int(qpos is not None), flags),
                    qkv.device)
     ev = _probe.begin() if _probe is not None else None

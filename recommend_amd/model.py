@@ -217,8 +217,15 @@ def _block_forward(m, l, x, I, Kq, seed, training, rstd_in=None, select=False, n
     # still drives the GEMM row maps and epilogues
     # fp8 training forward: qkv's operands are replaced by their dequantised fp8 values, so the backward
     # differentiates the forward that ran (OT_FP8_DEQUANT)
-    K.attn_fwd(qkv, 3 * d, B, H, I, Kq, hd, o, lse, qpos=_attn_qpos(cfg, pos), fp8=m.attn_fp8,
-               dequant=m.attn_fp8 and training, fp8_terms=m.fp8_terms)
+    # with the key-grouped bf16 backward, the dequantised operands go to a bf16 copy that replaces qkv as the
+    # backward's saved operand (the backward rounds them to bf16 anyway)
+    qp_f = _attn_qpos(cfg, pos)
+    qkv16 = (torch.empty(B * I, 3 * d, dtype=torch.int16, device=dev)
+             if m.attn_fp8 and training and m.qkv_bf16 and K.attn_bwd_bf16_supported(I, Kq, hd, qp_f) else None)
+    K.attn_fwd(qkv, 3 * d, B, H, I, Kq, hd, o, lse, qpos=qp_f, fp8=m.attn_fp8,
+               dequant=m.attn_fp8 and training, fp8_terms=m.fp8_terms, deq16=qkv16)
+    if qkv16 is not None:
+        qkv = qkv16
     # x1 = x[tail] + drop(o @ Wo)      (model.py:117, 193)
     x1 = torch.empty(B * Kq, d, device=dev)
     rstd2 = torch.empty(B * Kq, device=dev)
@@ -639,6 +646,9 @@ class OneTransModel(nn.Module):
         self.xn_bf16 = os.environ.get('ONETRANS_XN_BF16', '1') != '0'
         # ... and the FFN2 dgrad's dY in bf16 (ONETRANS_DY_BF16=0: f32)
         self.dy_bf16 = os.environ.get('ONETRANS_DY_BF16', '1') != '0'
+        # fp8 attention, training: the dequantised Q / K / V kept in bf16 for the backward (ONETRANS_QKV_BF16=0:
+        # written back into qkv in f32)
+        self.qkv_bf16 = os.environ.get('ONETRANS_QKV_BF16', '1') != '0'
         # block weight gradients run on a second stream, overlapping the dgrad chain
         self.overlap_wgrad = os.environ.get('ONETRANS_OVERLAP_WGRAD', '1') != '0'
         self._side = None

@@ -239,3 +239,42 @@ def test_attn_fwd_fp8_rejects_bad_head_dim(dev):
     with pytest.raises(OneTransHipError, match='head_dim'):
         K.attn_fwd(qkv, 96, 1, 1, 64, 64, 32, torch.empty(64, 32, device=dev), torch.empty(64, device=dev),
                    fp8=True)
+
+
+@pytest.mark.parametrize('B,H,I,Kq', [(2, 2, 1036, 1036), (3, 2, 300, 200)])
+def test_attn_fp8_deq16_backward(dev, B, H, I, Kq):
+    """ot_attn_fwd_fp8_deq16: the dequantised Q (kept rows) / K / V written rounded to bf16 into a copy
+    (qkv only read) equal the in-place f32 write-back rounded to nearest even, and the key-grouped bf16
+    backward from that copy (OT_ATTN_QKV_BF16) gives dQKV bit-identical to the backward from the f32
+    write-back (it rounds those values to bf16 itself)."""
+    hd = 64
+    d = H * hd
+    g = torch.Generator().manual_seed(I + Kq)
+    qkv = torch.randn(B * I, 3 * d, generator=g).to(dev)
+    dout = torch.randn(B * Kq, d, generator=g).to(dev)
+    old = K.set_matmul_mode('bf16')
+    try:
+        assert K.attn_bwd_bf16_supported(I, Kq, hd)
+        res = []
+        for use16 in (False, True):
+            q = qkv.clone()
+            out = torch.empty(B * Kq, d, device=dev)
+            lse = torch.empty(B * H * Kq, device=dev)
+            q16 = torch.zeros(B * I, 3 * d, dtype=torch.int16, device=dev) if use16 else None
+            K.attn_fwd(q, 3 * d, B, H, I, Kq, hd, out, lse, fp8=True, dequant=True, fp8_terms=2, deq16=q16)
+            dqkv = torch.zeros(B * I, 3 * d, device=dev)
+            K.attn_bwd(q16 if use16 else q, 3 * d, out, dout, lse, B, H, I, Kq, hd, dqkv)
+            torch.cuda.synchronize()
+            res.append((q, q16, out, dqkv))
+    finally:
+        K.set_matmul_mode(old)
+    (qf, _, of, df), (qo, q16, o16, d16) = res
+    assert torch.equal(qo, qkv)                                   # qkv only read
+    assert torch.equal(of, o16)
+    ref16 = qf.to(torch.bfloat16).view(torch.int16)
+    q_off = I - Kq
+    for b in range(B):                                            # K, V rows; the kept Q rows
+        r0 = b * I
+        assert torch.equal(q16[r0:r0 + I, d:], ref16[r0:r0 + I, d:])
+        assert torch.equal(q16[r0 + q_off:r0 + I, :d], ref16[r0 + q_off:r0 + I, :d])
+    assert torch.equal(df, d16)

@@ -33,6 +33,9 @@ namespace ot {
 #ifndef OT_GEMM_RMS_EARLY
 #define OT_GEMM_RMS_EARLY 1
 #endif
+#ifndef OT_PLANE_EPI_RBN          // epilogue rows per operand-load batch of the 4-workgroup plane GEMMs
+#define OT_PLANE_EPI_RBN 4
+#endif
 #ifndef OT_WGRAD_BF16_RS          // 32-row groups per stage of the bf16-mode weight-gradient kernel
 #define OT_WGRAD_BF16_RS 2
 #endif
@@ -137,7 +140,8 @@ __device__ __forceinline__ void store_out4(float* dst, f32x4 v) {
   else *reinterpret_cast<f32x4*>(dst) = v;
 }
 
-template <int EPIT, int LAYOUT, bool ROWSCALE, int RBN = 8>
+// GS: compile the forward stored-GELU path (bf16-mode plane GEMM only: registers elsewhere)
+template <int EPIT, int LAYOUT, bool ROWSCALE, int RBN = 8, bool GS = false>
 __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x16 (&acc)[4], float* smem, int tm,
                                                   int n0, int g) {
   const int epi = EPIT;
@@ -160,7 +164,7 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
     constexpr bool ROWRSTD = EPIT >= 0 && (EPIT & OT_EPI_ROW_RSTD);
     constexpr bool ROWDOT = EPIT >= 0 && (EPIT & OT_EPI_ROWDOT);
     // gelu_out of a bias-only epilogue: gelu(C) (C in f32 or bf16)
-    constexpr bool GSTORE = EPIT == OT_EPI_BIAS || EPIT == (OT_EPI_BIAS | OT_EPI_C_BF16);
+    constexpr bool GSTORE = GS && (EPIT == OT_EPI_BIAS || EPIT == (OT_EPI_BIAS | OT_EPI_C_BF16));
     constexpr bool CBF = EPIT >= 0 && (EPIT & OT_EPI_C_BF16);
     constexpr bool AUXBF = EPIT >= 0 && (EPIT & OT_EPI_AUX_BF16);
     f32x4 rdb4 = {0.f, 0.f, 0.f, 0.f};                 // OT_EPI_ROWDOT: the bias subtracted from aux
@@ -808,7 +812,8 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
   float xrs = 0.f;
   uint16_t* xnp = nullptr;
   float* gsm = reinterpret_cast<float*>(lds + NSTG * STG);
-  if (AXT == OT_AX_RMSNORM && p.xn_out && tn == 0) {
+  constexpr bool XN = AXT == OT_AX_RMSNORM && TERMS == 1;   // (bf16 mode only: split-mode registers are full)
+  if (XN && p.xn_out && tn == 0) {
     for (int k = 4 * t; k < p.K; k += 4 * 256)
       *reinterpret_cast<f32x4*>(gsm + k) = *reinterpret_cast<const f32x4*>(p.a_gamma + k);
     const int64_t xgr = (int64_t)tm * GT + ra;
@@ -853,7 +858,7 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
     }
     f32x4 a0 = *reinterpret_cast<const f32x4*>(sb + aoff0);
     f32x4 a1 = *reinterpret_cast<const f32x4*>(sb + aoff1);
-    if (AXT == OT_AX_RMSNORM && xnw) {                  // k = 16 kt + 8 h .. + 7: (a * gamma) * rstd, rounded
+    if (XN && xnw) {                                    // k = 16 kt + 8 h .. + 7: (a * gamma) * rstd, rounded
       const float* gp = gsm + 16 * kt + 8 * h;
       const f32x4 v0 = a0 * *reinterpret_cast<const f32x4*>(gp) * xrs;
       const f32x4 v1 = a1 * *reinterpret_cast<const f32x4*>(gp + 4) * xrs;
@@ -872,7 +877,7 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();                                    // the epilogue reuses the stage buffers
-  gemm_vec_epilogue<EPIT, 1, AXT == OT_AX_RMSNORM, MINW >= 4 ? 4 : 8>(p, acc, smem, tm, n0, g);
+  gemm_vec_epilogue<EPIT, 1, AXT == OT_AX_RMSNORM, MINW >= 4 ? OT_PLANE_EPI_RBN : 8, TERMS == 1>(p, acc, smem, tm, n0, g);
 }
 
 // Pre-split B images (ot_split_images).  desc [nd][10] int64: {src_off, sn, sk, gstride, kscale_off
@@ -1837,10 +1842,11 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
   OT_REQUIRE(!(epi & (OT_EPI_C_BF16 | OT_EPI_AUX_BF16)) || plane,
              "ot_mixed_gemm: OT_EPI_C_BF16 / OT_EPI_AUX_BF16 need the bf16-mode plane GEMM with OT_EPI_GELU_BWD "
              "[| OT_EPI_ROWDOT] or OT_EPI_BIAS alone (epilogue %d)", epi);
-  OT_REQUIRE(!p.gelu_out || (!edge && (kern != nullptr)), "ot_mixed_gemm_rms: gelu_out needs whole tiles");
-  OT_REQUIRE(!p.xn_out || (plane && x == OT_AX_RMSNORM && a_rstd && a_gamma && p.ldxn % 8 == 0 && K <= 1024 &&
+  OT_REQUIRE(!p.gelu_out || (!edge && (kern != nullptr) && ((epi & OT_EPI_GELU_BWD) || (plane && one))),
+             "ot_mixed_gemm_rms: gelu_out needs whole tiles (with epi OT_EPI_BIAS: the bf16-mode plane GEMM)");
+  OT_REQUIRE(!p.xn_out || (plane && one && x == OT_AX_RMSNORM && a_rstd && a_gamma && p.ldxn % 8 == 0 && K <= 1024 &&
                            ((uintptr_t)p.xn_out % 16) == 0),
-             "ot_mixed_gemm_rms: xn_out needs the plane GEMM with the RMSNorm prologue, K <= 1024, ldxn %% 8 == 0 and 16-B "
+             "ot_mixed_gemm_rms: xn_out needs the bf16-mode plane GEMM with the RMSNorm prologue, K <= 1024, ldxn %% 8 == 0 and 16-B "
              "alignment");
   OT_REQUIRE(!p.rowpart || plane, "ot_mixed_gemm_rms: OT_EPI_ROW_RSTD with N = %d > %d needs the plane GEMM "
              "(split mode, a pre-split B image, 16-B aligned A)", N, GT);

@@ -184,10 +184,10 @@ def test_plane_gemm_rmsnorm_bwd(dev, K_, drop):
 @pytest.mark.parametrize('rstd_epi', [False, True])
 def test_plane_gemm_stored_gelu(dev, plane_mode, f, N, rstd_epi):
     """The FFN1 epilogue's stored GELU (ot_rms_epilogue.gelu_out with epi == OT_EPI_BIAS: bf16 gelu(U)) and
-    the FFN2 plane GEMM reading it (OT_AX_BF16 A): U is unchanged by the extra store, h is gelu(U) rounded
-    to bf16 (torch float64 erf: at most one bf16 ulp apart), and in the bf16 mode the FFN2 output (and the
-    next norm's rstd) from h is bit-identical to the one that forms gelu(U) at fragment time (OT_AX_GELU:
-    the same rounding of the same values).  The split mode refuses a bf16 A operand."""
+    the FFN2 plane GEMM reading it (OT_AX_BF16 A), bf16 mode: U is unchanged by the extra store, h is gelu(U)
+    rounded to bf16 (torch float64 erf: at most one bf16 ulp apart), and the FFN2 output (and the next
+    norm's rstd) from h is bit-identical to the one that forms gelu(U) at fragment time (OT_AX_GELU: the
+    same rounding of the same values).  The split mode refuses both forms."""
     from recommend_amd._lib import OT_AX_BF16, OT_EPI_C_BF16, OneTransHipError
     rng = np.random.default_rng(f + N)
     G, B, I, Kq, d = 3, 53, 9, 5, N
@@ -210,17 +210,26 @@ def test_plane_gemm_stored_gelu(dev, plane_mode, f, N, rstd_epi):
     K.gemm(OT_GEMM_NT, x, d, d, dm['rows'][0], W1.to(dev), f * d, d, f, dm['tile_group'], rm.ntiles, U0, f, rows, **kw1)
     U = torch.full((M, f), float('nan'), device=dev)
     h = torch.zeros(M, f, dtype=torch.int16, device=dev)
+    if plane_mode != 'bf16':            # a bf16-mode form (compiled into the bf16 plane kernels only)
+        with pytest.raises(OneTransHipError, match='gelu_out'):
+            K.gemm_rms(OT_GEMM_NT, x, d, d, dm['rows'][0], W1.to(dev), f * d, d, f, dm['tile_group'], rm.ntiles, U,
+                       f, rows, gelu_out=h, ldgelu=f, device=dev, **kw1)
+        with pytest.raises(OneTransHipError, match='OT_AX_BF16'):
+            K.gemm(OT_GEMM_NT, h, f, f, rows, W2.to(dev), N * f, f, N, dm['tile_group'], rm.ntiles,
+                   torch.empty(M, N, device=dev), N, rows, a_xform=OT_AX_BF16, bias=b2, bias_gstride=N,
+                   epi=OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_DROPOUT, res=res, ldres=N, res_tok=0, seed=7, site=1,
+                   drop=0.1, tail=(Kq, I), bimg=(img2, ntn2, 0))
+        return
     K.gemm_rms(OT_GEMM_NT, x, d, d, dm['rows'][0], W1.to(dev), f * d, d, f, dm['tile_group'], rm.ntiles, U, f, rows,
                gelu_out=h, ldgelu=f, device=dev, **kw1)
-    if plane_mode == 'bf16':            # U itself in bf16 (OT_EPI_C_BF16): U rounded, the same h
-        U16 = torch.zeros(M, f, dtype=torch.int16, device=dev)
-        h2 = torch.zeros(M, f, dtype=torch.int16, device=dev)
-        K.gemm_rms(OT_GEMM_NT, x, d, d, dm['rows'][0], W1.to(dev), f * d, d, f, dm['tile_group'], rm.ntiles, U16, f,
-                   rows, gelu_out=h2, ldgelu=f, device=dev, **dict(kw1, epi=OT_EPI_BIAS | OT_EPI_C_BF16))
+    # U itself in bf16 (OT_EPI_C_BF16): U rounded, the same h
+    U16 = torch.zeros(M, f, dtype=torch.int16, device=dev)
+    h2 = torch.zeros(M, f, dtype=torch.int16, device=dev)
+    K.gemm_rms(OT_GEMM_NT, x, d, d, dm['rows'][0], W1.to(dev), f * d, d, f, dm['tile_group'], rm.ntiles, U16, f,
+               rows, gelu_out=h2, ldgelu=f, device=dev, **dict(kw1, epi=OT_EPI_BIAS | OT_EPI_C_BF16))
     torch.cuda.synchronize()
     assert torch.equal(U, U0)
-    if plane_mode == 'bf16':
-        assert torch.equal(U16, U.to(torch.bfloat16).view(torch.int16)) and torch.equal(h2, h)
+    assert torch.equal(U16, U.to(torch.bfloat16).view(torch.int16)) and torch.equal(h2, h)
     ref = (0.5 * U.double() * (1 + torch.erf(U.double() / math.sqrt(2)))).float().to(torch.bfloat16).cpu().float()
     got = h.view(torch.bfloat16).cpu().float()
     # (+ 1e-6 absolute: for U < -3 the f32 1 + erf(U / sqrt 2) cancels; gelu there is below 2e-3)
@@ -228,12 +237,6 @@ def test_plane_gemm_stored_gelu(dev, plane_mode, f, N, rstd_epi):
     epi = OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_DROPOUT | (OT_EPI_ROW_RSTD if rstd_epi else 0)
     kw2 = dict(bias=b2, bias_gstride=N, epi=epi, res=res, ldres=N, res_tok=0, seed=7, site=1, drop=0.1,
                tail=(Kq, I), bimg=(img2, ntn2, 0))
-    if plane_mode != 'bf16':
-        with pytest.raises(OneTransHipError, match='OT_AX_BF16'):
-            K.gemm(OT_GEMM_NT, h, f, f, rows, W2.to(dev), N * f, f, N, dm['tile_group'], rm.ntiles,
-                   torch.empty(M, N, device=dev), N, rows, a_xform=OT_AX_BF16,
-                   **dict(kw2, epi=epi & ~OT_EPI_ROW_RSTD))
-        return
     outs = []
     for A, ax in ((U, OT_AX_GELU), (h, OT_AX_BF16)):
         C = torch.full((M, N), float('nan'), device=dev)
@@ -361,9 +364,9 @@ def test_plane_gemm_bf16_a_plain(dev, plane_mode, K_, N):
 
 @pytest.mark.parametrize('N', [1536, 128])
 def test_plane_gemm_xn_out(dev, plane_mode, N):
-    """ot_rms_epilogue.xn_out on the plane GEMM's RMSNorm prologue: the first column tile's workgroups store
-    bf16((A * gamma) * rstd) of every mapped A row — the same f32 products, rounded once, that torch forms
-    — and C is unchanged by it."""
+    """ot_rms_epilogue.xn_out on the bf16-mode plane GEMM's RMSNorm prologue: the first column tile's
+    workgroups store bf16((A * gamma) * rstd) of every mapped A row — the same f32 products, rounded once,
+    that torch forms — and C is unchanged by it.  The split mode refuses it."""
     rng = np.random.default_rng(N)
     G, M, K_ = 3, 700, 512
     rm = ragged_map(rng, M, G)
@@ -375,6 +378,13 @@ def test_plane_gemm_xn_out(dev, plane_mode, N):
     img, ntn = make_image(W, dev, gamma)
     outs = []
     xn = torch.zeros(M, K_, dtype=torch.int16, device=dev)
+    if plane_mode != 'bf16':            # a bf16-mode form (compiled into the bf16 plane kernels only)
+        from recommend_amd._lib import OneTransHipError
+        with pytest.raises(OneTransHipError, match='xn_out'):
+            K.gemm_rms(OT_GEMM_NT, A, K_, K_, dm['rows'][0], W.to(dev), N * K_, K_, N, dm['tile_group'], rm.ntiles,
+                       torch.empty(M, N, device=dev), N, dm['rows'][1], epi=0, a_xform=OT_AX_RMSNORM, rstd=rstd,
+                       gamma=gamma.to(dev), device=dev, bimg=(img, ntn, 0), xn_out=xn, ldxn=K_)
+        return
     for with_xn in (False, True):
         C = torch.full((M, N), float('nan'), device=dev)
         K.gemm_rms(OT_GEMM_NT, A, K_, K_, dm['rows'][0], W.to(dev), N * K_, K_, N, dm['tile_group'], rm.ntiles, C, N,

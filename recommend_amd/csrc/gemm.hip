@@ -1786,7 +1786,9 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
   OT_SPEC(true, OT_AX_NONE, OT_EPI_RMSNORM_BWD | OT_EPI_DROPOUT)
 #undef OT_SPEC
   // plane GEMM: split mode, pre-split B image given, whole tiles, 16-B aligned A rows
-  if (bimg && split && !edge && mode == OT_GEMM_NT && lda % 4 == 0 && a16(A)) {
+  // (the plane GEMM's k-steps are 16 deep: K % 16 suffices, e.g. the NS tokenizer's K = 432)
+  const bool plane_edge = (K % 16) != 0 || (N % GT) != 0 || !vec_ok;
+  if (bimg && split && !plane_edge && mode == OT_GEMM_NT && lda % 4 == 0 && a16(A)) {
     OT_REQUIRE(bimg_ntn >= bimg_tn0 + (int)p.ntn && bimg_tn0 >= 0, "ot_mixed_gemm: B image has %d tiles per group, "
                "the GEMM needs %d from tile %d", bimg_ntn, (int)p.ntn, bimg_tn0);
     void (*pk)(GemmArgs) = nullptr;

@@ -273,6 +273,9 @@ int ot_attn_bwd_ex(const float* qkv, int64_t ld, const float* out, const float* 
 /* OT_ATTN_QKV_BF16: qkv holds bf16 (uint16 bits, ld in elements, 16-B aligned): the fp8 forward's dequantised
  * operands from ot_attn_fwd_fp8_deq16 (same key-grouped condition) */
 #define OT_ATTN_QKV_BF16 2
+/* OT_ATTN_DQ_PART_BF16 (with OT_ATTN_DQKV_BF16): the key slices' dQ partials are kept in bf16 (summed in f32,
+ * then rounded: not the f32 sum rounded once — about one more bf16 rounding of each partial) */
+#define OT_ATTN_DQ_PART_BF16 4
 int ot_attn_bwd_dqkv_bf16_supported(int I, int K, int head_dim, int selected);
 size_t ot_attn_bwd_flags_workspace_size(int B, int H, int I, int K, int head_dim, int selected, int flags);
 int ot_attn_bwd_flags(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,

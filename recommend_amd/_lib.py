@@ -24,6 +24,7 @@ OT_EPI_C_BF16 = 512
 OT_EPI_AUX_BF16 = 1024
 OT_ATTN_DQKV_BF16 = 1
 OT_ATTN_QKV_BF16 = 2
+OT_ATTN_DQ_PART_BF16 = 4
 OT_WG_D_BF16 = 8
 OT_MATMUL_F32, OT_MATMUL_SPLIT_BF16, OT_MATMUL_BF16 = 0, 1, 2
 OT_FP8_DEQUANT, OT_FP8_TWO_TERM = 1, 2

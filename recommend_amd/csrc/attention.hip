@@ -54,6 +54,9 @@ struct AttnArgs {
   // OT_ATTN_QKV_BF16 (key-grouped backward only): qkv holds bf16 (uint16 bits, ld in elements) — the fp8
   // forward's dequantised operands, which the bf16 backward would round to bf16 anyway
   int qkv_bf16;
+  // OT_ATTN_DQ_PART_BF16 (with OT_ATTN_DQKV_BF16): the slices' dQ partials are stored rounded to bf16 (half the
+  // partial traffic; summed in f32 by attn_dq_reduce_kernel, then rounded once more)
+  int dq_part16;
 };
 
 // position of kept query j (< K) of the sample whose qpos slice is qp (null: the tail rule)
@@ -1233,9 +1236,13 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kerne
       const int dd = 32 * c + 8 * g + 4 * (ln >> 5);
       if (jq < K && dd < HD) {
         const int ps = p.dq_bf16 ? slice : slice - 1;  // dqpart slot (bf16 output: slice 0 too)
-        float* dst = ps < 0 ? p.dqkv + (tok0 + q_off + jq) * p.ld + h * HD + dd
-                            : p.dqpart + ((int64_t)ps * p.B * K + (int64_t)b * K + jq) * p.d + h * HD + dd;
-        *reinterpret_cast<f32x4*>(dst) = a;
+        const int64_t pe = ((int64_t)ps * p.B * K + (int64_t)b * K + jq) * p.d + h * HD + dd;
+        if (p.dq_part16) {
+          *reinterpret_cast<u32x2*>(reinterpret_cast<uint16_t*>(p.dqpart) + pe) = bf16_rne4(a);
+        } else {
+          float* dst = ps < 0 ? p.dqkv + (tok0 + q_off + jq) * p.ld + h * HD + dd : p.dqpart + pe;
+          *reinterpret_cast<f32x4*>(dst) = a;
+        }
       }
     }
   }
@@ -1273,17 +1280,24 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(AttnArgs p) {
   const int b = (int)(row / p.K), j = (int)(row - (int64_t)b * p.K);
   const int q_off = p.I - p.K, qb = j / 32;
   const int o = p.dq_bf16 ? 0 : 1;                     // dqpart slot of slice s: s - o
+  const uint16_t* part16 = reinterpret_cast<const uint16_t*>(p.dqpart);
+  auto part = [&](int64_t i) -> f32x4 {
+    if (!p.dq_part16) return *reinterpret_cast<const f32x4*>(p.dqpart + i);
+    const u32x2 w = *reinterpret_cast<const u32x2*>(part16 + i);
+    return f32x4{__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u), __uint_as_float(w.y << 16),
+                 __uint_as_float(w.y & 0xffff0000u)};
+  };
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   bool any = false;
   for (int s = 1; s < p.kslices; ++s) {
     const int f = 32 * p.kgroup * s - q_off;           // first query block that sees the slice's first key
     if ((f < 0 ? 0 : f / 32) > qb) break;              // later slices start later still
-    acc += *reinterpret_cast<const f32x4*>(p.dqpart + (int64_t)(s - o) * n + e4);
+    acc += part((int64_t)(s - o) * n + e4);
     any = true;
   }
   const int64_t di = ((int64_t)b * p.I + q_off + j) * p.ld + col;
   if (p.dq_bf16) {
-    const f32x4 d0 = *reinterpret_cast<const f32x4*>(p.dqpart + e4);
+    const f32x4 d0 = part(e4);
     *reinterpret_cast<u32x2*>(reinterpret_cast<uint16_t*>(p.dqkv) + di) = bf16_rne4(any ? d0 + acc : d0);
     return;
   }
@@ -1644,7 +1658,10 @@ extern "C" int ot_attn_bwd_ex(const float* qkv, int64_t ld, const float* out, co
 extern "C" int ot_attn_bwd_flags(const float* qkv, int64_t ld, const float* out, const float* dout,
                                  const float* lse, int B, int H, int I, int K, const int32_t* qpos, int head_dim,
                                  void* dqkv, int flags, void* workspace, size_t ws_bytes, void* stream) {
-  OT_REQUIRE(!(flags & ~(OT_ATTN_DQKV_BF16 | OT_ATTN_QKV_BF16)), "ot_attn_bwd_flags: unknown flags %d", flags);
+  OT_REQUIRE(!(flags & ~(OT_ATTN_DQKV_BF16 | OT_ATTN_QKV_BF16 | OT_ATTN_DQ_PART_BF16)),
+             "ot_attn_bwd_flags: unknown flags %d", flags);
+  OT_REQUIRE(!(flags & OT_ATTN_DQ_PART_BF16) || (flags & OT_ATTN_DQKV_BF16),
+             "ot_attn_bwd_flags: OT_ATTN_DQ_PART_BF16 goes with OT_ATTN_DQKV_BF16");
   OT_REQUIRE(!(flags & OT_ATTN_QKV_BF16) || (ot_attn_bwd_dqkv_bf16_supported(I, K, head_dim, qpos != nullptr) &&
                                              ((uintptr_t)qkv % 16) == 0 && ld % 8 == 0),
              "ot_attn_bwd_flags: OT_ATTN_QKV_BF16 needs the key-grouped bf16 backward, 16-B aligned qkv, ld %% 8 == 0");
@@ -1687,6 +1704,7 @@ static int attn_bwd_impl(const float* qkv, int64_t ld, const float* out, const f
     p.dqpart = delta_ws + ot_attn_bwd_workspace_size(B, H, K) / sizeof(float);
     p.dq_bf16 = (flags & OT_ATTN_DQKV_BF16) ? 1 : 0;
     p.qkv_bf16 = (flags & OT_ATTN_QKV_BF16) ? 1 : 0;
+    p.dq_part16 = (flags & OT_ATTN_DQ_PART_BF16) ? 1 : 0;
     void (*kern)(AttnArgs) =
         p.qkv_bf16 ? (G == 8 ? (head_dim == 32 ? attn_bwd_group_kernel<32, 8, true> : attn_bwd_group_kernel<64, 8, true>)
                              : (head_dim == 32 ? attn_bwd_group_kernel<32, 4, true> : attn_bwd_group_kernel<64, 4, true>))

@@ -277,11 +277,12 @@ def attn_bwd_bf16_supported(I, K, hd, qpos=None) -> bool:
     return bool(_lib.load().ot_attn_bwd_dqkv_bf16_supported(I, K, hd, int(qpos is not None)))
 
 
-def attn_bwd(qkv, ld, out, dout, lse, B, H, I, K, hd, dqkv, qpos=None) -> None:
+def attn_bwd(qkv, ld, out, dout, lse, B, H, I, K, hd, dqkv, qpos=None, dq_part_bf16: bool = False) -> None:
     """dqkv float32, or int16 (bf16 bits: OT_ATTN_DQKV_BF16, see attn_bwd_bf16_supported); qkv likewise
     (int16: OT_ATTN_QKV_BF16, the fp8 forward's bf16 dequantised operands)."""
     flags = ((_lib.OT_ATTN_DQKV_BF16 if dqkv.dtype == torch.int16 else 0)
-             | (_lib.OT_ATTN_QKV_BF16 if qkv.dtype == torch.int16 else 0))
+             | (_lib.OT_ATTN_QKV_BF16 if qkv.dtype == torch.int16 else 0)
+             | (_lib.OT_ATTN_DQ_PART_BF16 if dq_part_bf16 and dqkv.dtype == torch.int16 else 0))
     ws = workspace(size('ot_attn_bwd_flags_workspace_size', B, H, I, K, hd, int(qpos is not None), flags),
                    qkv.device)
     ev = _probe.begin() if _probe is not None else None

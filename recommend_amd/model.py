@@ -422,7 +422,7 @@ class _Block(torch.autograd.Function):
         dqkv = torch.empty(B * I, 3 * d, device=dev, dtype=torch.int16 if dq_bf else torch.float32)
         if Kq < I:
             dqkv[:, :d].zero_()
-        K.attn_bwd(qkv, 3 * d, o, do, lse, B, H, I, Kq, hd, dqkv, qpos=qp)
+        K.attn_bwd(qkv, 3 * d, o, do, lse, B, H, I, Kq, hd, dqkv, qpos=qp, dq_part_bf16=m.dq_part_bf16)
         an1 = xn1 is not None and dq_bf
         with m.side(xn1 if an1 else x, dqkv, rstd1):
             K.wgrad(xn1 if an1 else x, d, ma['rows'][0], dqkv, 3 * d, ma['rows'][0], d, 3 * d, ma, nca, G,
@@ -649,6 +649,8 @@ class OneTransModel(nn.Module):
         # fp8 attention, training: the dequantised Q / K / V kept in bf16 for the backward (ONETRANS_QKV_BF16=0:
         # written back into qkv in f32)
         self.qkv_bf16 = os.environ.get('ONETRANS_QKV_BF16', '1') != '0'
+        # ... and the key slices' dQ partials in bf16 (ONETRANS_DQ_PART_BF16=0: f32; not bit-identical)
+        self.dq_part_bf16 = os.environ.get('ONETRANS_DQ_PART_BF16', '1') != '0'
         # block weight gradients run on a second stream, overlapping the dgrad chain
         self.overlap_wgrad = os.environ.get('ONETRANS_OVERLAP_WGRAD', '1') != '0'
         self._side = None

@@ -678,6 +678,13 @@ def test_attn_bwd_key_slices(dev, B, H, I, Kq, hd):
         K.attn_bwd(qkv, 3 * d, out, dout, lse, B, H, I, Kq, hd, d16)
         torch.cuda.synchronize()
         assert torch.equal(d16.cpu(), a.to(torch.bfloat16).view(torch.int16))
+        # bf16 dQ partials (OT_ATTN_DQ_PART_BF16): dK / dV unchanged, dQ within two bf16 roundings
+        p16 = torch.zeros(B * I, 3 * d, dtype=torch.int16, device=dev)
+        K.attn_bwd(qkv, 3 * d, out, dout, lse, B, H, I, Kq, hd, p16, dq_part_bf16=True)
+        torch.cuda.synchronize()
+        assert torch.equal(p16[:, d:].cpu(), d16[:, d:].cpu())
+        qa, qb_ = p16[:, :d].view(torch.bfloat16).float().cpu(), d16[:, :d].view(torch.bfloat16).float().cpu()
+        assert (qa - qb_).abs().max().item() <= 2 ** -7 * qb_.abs().max().item()
     finally:
         K.set_matmul_mode(old)
 

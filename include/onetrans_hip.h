@@ -52,6 +52,9 @@ extern "C" {
                            modes; forward GEMMs: OT_MATMUL_BF16, NT mode, a B image (the plane GEMM), lda % 8
                            == 0, 16-B aligned A, epilogue OT_EPI_BIAS | OT_EPI_RESIDUAL [| OT_EPI_DROPOUT]
                            [| OT_EPI_ROW_RSTD] (the FFN2 GEMM) */
+#define OT_AX_BF16_RMSNORM 5 /* plane GEMM, OT_MATMUL_BF16: A holds bf16 x (as OT_AX_BF16) and the RMSNorm is applied
+                                as the RMSNorm prologue is there (gamma folded into the B image, rstd scales the
+                                output rows): the QKV / FFN1 GEMMs from the bf16 copy of their input */
 
 /* GEMM epilogue flags (applied in this order) */
 #define OT_EPI_BIAS 1        /* + bias[g][n] */
@@ -147,6 +150,9 @@ typedef struct ot_rms_epilogue {
                                                           normalised operand of the bf16-mode weight gradient
                                                           (OT_AX_BF16), so it neither re-reads f32 A nor
                                                           re-applies the norm */
+  uint16_t* c16_out; int64_t ldc16;                    /* optional, bf16-mode plane GEMM (not with the norm-backward
+                                                          or bf16-C epilogues): also C rounded to bf16 — the next
+                                                          GEMM's OT_AX_BF16_RMSNORM operand */
 } ot_rms_epilogue;
 size_t ot_mixed_gemm_rms_workspace_size(int ntiles, int N);
 int ot_mixed_gemm_rms(int mode, const float* A, int64_t lda, int K, const int32_t* in_rows,

@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get('ONETRANS_HIP_LIB') or os.path.join(_HERE, 'libonetran
 HEADER = os.path.join(os.path.dirname(_HERE), 'include', 'onetrans_hip.h')
 
 OT_GEMM_NN, OT_GEMM_NT = 0, 1
-OT_AX_NONE, OT_AX_RMSNORM, OT_AX_GELU, OT_AX_BF16 = 0, 1, 2, 4
+OT_AX_NONE, OT_AX_RMSNORM, OT_AX_GELU, OT_AX_BF16, OT_AX_BF16_RMSNORM = 0, 1, 2, 4, 5
 OT_EPI_BIAS, OT_EPI_GELU_BWD, OT_EPI_GELU = 1, 2, 4
 OT_EPI_DROPOUT, OT_EPI_RESIDUAL, OT_EPI_ACCUMULATE = 8, 16, 32
 OT_EPI_ROW_RSTD, OT_EPI_RMSNORM_BWD, OT_EPI_ROWDOT = 64, 128, 256
@@ -42,7 +42,8 @@ class RmsEpilogue(ctypes.Structure):
                 ('workspace', c_void_p), ('ws_bytes', c_size_t),
                 ('rowdot', c_void_p), ('rowdot_n', c_int),
                 ('gelu_out', c_void_p), ('ldgelu', c_int64),
-                ('xn_out', c_void_p), ('ldxn', c_int64)]
+                ('xn_out', c_void_p), ('ldxn', c_int64),
+                ('c16_out', c_void_p), ('ldc16', c_int64)]
 
 P = c_void_p
 I64 = c_int64

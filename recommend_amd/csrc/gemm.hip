@@ -100,6 +100,7 @@ struct GemmArgs {
   // plane GEMM with the RMSNorm prologue: the first column tile's workgroups also store bf16(a * gamma * rstd)
   // of their A rows (the bf16 weight gradient's normalised A operand)
   uint16_t* xn_out; int64_t ldxn;
+  uint16_t* c16_out; int64_t ldc16;             // bf16-mode plane GEMM: also C rounded to bf16 (optional)
 };
 
 // sum over the 32 lanes that hold one output row in the vector epilogue (same order as the
@@ -315,6 +316,8 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
             const f32x4 hv = {gelu_erf(v.x), gelu_erf(v.y), gelu_erf(v.z), gelu_erf(v.w)};
             *reinterpret_cast<u32x2*>(p.gelu_out + (int64_t)orr * p.ldgelu + col) = bf16_rne4(hv);
           }
+          if (GS && p.c16_out && orr >= 0)                     // + a bf16 copy of C (the next GEMM's A)
+            *reinterpret_cast<u32x2*>(p.c16_out + (int64_t)orr * p.ldc16 + col) = bf16_rne4(v);
           if (CBF) {                                           // C in bf16 (the FFN2 dgrad's dU)
             if (orr >= 0) *reinterpret_cast<u32x2*>(reinterpret_cast<uint16_t*>(p.C) + (int64_t)orr * p.ldc + col) = bf16_rne4(v);
           } else if (orr >= 0) {
@@ -728,7 +731,10 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
   static_assert(TERMS == 6 || TERMS == 1, "plane GEMM terms");
   // OT_AX_BF16: A holds bf16 values (the FFN1 epilogue's stored gelu(U)): 32 B per row and stage, the
   // lane's fragment is one 16-B LDS read, no conversion (bf16 mode only)
-  constexpr bool ABF = AXT == OT_AX_BF16;
+  // OT_AX_BF16_RMSNORM: bf16 x with the RMSNorm applied as the RMSNorm prologue does on this kernel (gamma
+  // folded into the B image, rstd as the epilogue's row scale)
+  constexpr bool ABF = AXT == OT_AX_BF16 || AXT == OT_AX_BF16_RMSNORM;
+  constexpr bool RSC = AXT == OT_AX_RMSNORM || AXT == OT_AX_BF16_RMSNORM;
   static_assert(!ABF || TERMS == 1, "bf16 A operands go with OT_MATMUL_BF16");
   constexpr int STG = pg_stage_bytes<TERMS>();
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -812,7 +818,7 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
   float xrs = 0.f;
   uint16_t* xnp = nullptr;
   float* gsm = reinterpret_cast<float*>(lds + NSTG * STG);
-  constexpr bool XN = AXT == OT_AX_RMSNORM && TERMS == 1;   // (bf16 mode only: split-mode registers are full)
+  constexpr bool XN = RSC && TERMS == 1;             // (bf16 mode only: split-mode registers are full)
   if (XN && p.xn_out && tn == 0) {
     for (int k = 4 * t; k < p.K; k += 4 * 256)
       *reinterpret_cast<f32x4*>(gsm + k) = *reinterpret_cast<const f32x4*>(p.a_gamma + k);
@@ -852,6 +858,18 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
     if constexpr (ABF) {
       u32x4 fa[3];
       fa[0] = *reinterpret_cast<const u32x4*>(sb + aoffb);
+      if (XN && xnw) {                                  // from the bf16 x: (x * gamma) * rstd, rounded
+        const float* gp = gsm + 16 * kt + 8 * h;
+        const u32x4 w = fa[0];
+        const f32x4 a0 = {__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u),
+                          __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u)};
+        const f32x4 a1 = {__uint_as_float(w.z << 16), __uint_as_float(w.z & 0xffff0000u),
+                          __uint_as_float(w.w << 16), __uint_as_float(w.w & 0xffff0000u)};
+        const f32x4 v0 = a0 * *reinterpret_cast<const f32x4*>(gp) * xrs;
+        const f32x4 v1 = a1 * *reinterpret_cast<const f32x4*>(gp + 4) * xrs;
+        const u32x2 b0 = bf16_rne4(v0), b1 = bf16_rne4(v1);
+        *reinterpret_cast<u32x4*>(xnp + 16 * kt) = u32x4{b0.x, b0.y, b1.x, b1.y};
+      }
 #pragma unroll
       for (int nb = 0; nb < 4; ++nb) acc[nb] = mfma_bf16(fa[0], fb[nb][0], acc[nb]);
       continue;
@@ -877,7 +895,7 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();                                    // the epilogue reuses the stage buffers
-  gemm_vec_epilogue<EPIT, 1, AXT == OT_AX_RMSNORM, MINW >= 4 ? OT_PLANE_EPI_RBN : 8, TERMS == 1>(p, acc, smem, tm, n0, g);
+  gemm_vec_epilogue<EPIT, 1, RSC, MINW >= 4 ? OT_PLANE_EPI_RBN : 8, TERMS == 1>(p, acc, smem, tm, n0, g);
 }
 
 // Pre-split B images (ot_split_images).  desc [nd][10] int64: {src_off, sn, sk, gstride, kscale_off
@@ -1673,9 +1691,13 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
   OT_REQUIRE(!(epi & OT_EPI_RESIDUAL) || res, "ot_mixed_gemm: residual missing");
   OT_REQUIRE(!(epi & OT_EPI_GELU_BWD) || aux, "ot_mixed_gemm: aux missing");
   OT_REQUIRE(a_xform != OT_AX_RMSNORM || (a_rstd && a_gamma), "ot_mixed_gemm: rmsnorm prologue needs rstd/gamma");
-  OT_REQUIRE(a_xform == OT_AX_NONE || a_xform == OT_AX_RMSNORM || a_xform == OT_AX_GELU || a_xform == OT_AX_BF16,
+  OT_REQUIRE(a_xform == OT_AX_NONE || a_xform == OT_AX_RMSNORM || a_xform == OT_AX_GELU || a_xform == OT_AX_BF16 ||
+                 a_xform == OT_AX_BF16_RMSNORM,
              "ot_mixed_gemm: bad a_xform %d", a_xform);
-  OT_REQUIRE(a_xform != OT_AX_BF16 || (g_matmul_mode == OT_MATMUL_BF16 && bimg && mode == OT_GEMM_NT &&
+  OT_REQUIRE(a_xform != OT_AX_BF16_RMSNORM || (a_rstd && a_gamma),
+             "ot_mixed_gemm: OT_AX_BF16_RMSNORM needs rstd / gamma (gamma folded into the B image)");
+  OT_REQUIRE((a_xform != OT_AX_BF16 && a_xform != OT_AX_BF16_RMSNORM) ||
+                 (g_matmul_mode == OT_MATMUL_BF16 && bimg && mode == OT_GEMM_NT &&
                                        lda % 8 == 0 && ((uintptr_t)A % 16) == 0),
              "ot_mixed_gemm: OT_AX_BF16 (bf16 A) needs the bf16 mode, a B image (plane GEMM), NT mode and 16-B "
              "aligned rows");
@@ -1719,6 +1741,10 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
   if (rms && rms->xn_out) {
     p.xn_out = rms->xn_out;
     p.ldxn = rms->ldxn;
+  }
+  if (rms && rms->c16_out) {
+    p.c16_out = rms->c16_out;
+    p.ldc16 = rms->ldc16;
   }
   if (rms && ((epi & OT_EPI_GELU_BWD) || (epi & ~OT_EPI_C_BF16) == OT_EPI_BIAS)) {   // the stored GELU (optional)
     p.gelu_out = rms->gelu_out;
@@ -1837,16 +1863,26 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
     OT_PSPEC_BF(OT_EPI_GELU_BWD | OT_EPI_ROWDOT | OT_EPI_C_BF16 | OT_EPI_AUX_BF16)
     OT_PSPEC_BF(OT_EPI_GELU_BWD | OT_EPI_ROWDOT | OT_EPI_C_BF16)
 #undef OT_PSPEC_BF
+#define OT_PSPEC_BR(EP_) if (one && x == OT_AX_BF16_RMSNORM && e == (EP_)) pk = plane_gemm_kernel<OT_AX_BF16_RMSNORM, EP_, 3, 4, 1>;
+    OT_PSPEC_BR(0)
+    OT_PSPEC_BR(OT_EPI_BIAS)
+    OT_PSPEC_BR(OT_EPI_BIAS | OT_EPI_C_BF16)
+#undef OT_PSPEC_BR
     if (pk) { kern = pk; plane = true; }
   }
-  OT_REQUIRE(x != OT_AX_BF16 || plane, "ot_mixed_gemm: no plane GEMM for OT_AX_BF16 with epilogue %d (or edge tiles)",
-             epi);
+  OT_REQUIRE((x != OT_AX_BF16 && x != OT_AX_BF16_RMSNORM) || plane,
+             "ot_mixed_gemm: no plane GEMM for a_xform %d with epilogue %d (or edge tiles)", x, epi);
+  OT_REQUIRE(!p.c16_out || (plane && one && p.ldc16 % 4 == 0 && ((uintptr_t)p.c16_out % 8) == 0 &&
+                            !(epi & (OT_EPI_RMSNORM_BWD | OT_EPI_C_BF16))),
+             "ot_mixed_gemm_rms: c16_out needs the bf16-mode plane GEMM (not with OT_EPI_RMSNORM_BWD / C_BF16), "
+             "ldc16 %% 4 == 0 and 8-B alignment");
   OT_REQUIRE(!(epi & (OT_EPI_C_BF16 | OT_EPI_AUX_BF16)) || plane,
              "ot_mixed_gemm: OT_EPI_C_BF16 / OT_EPI_AUX_BF16 need the bf16-mode plane GEMM with OT_EPI_GELU_BWD "
              "[| OT_EPI_ROWDOT] or OT_EPI_BIAS alone (epilogue %d)", epi);
   OT_REQUIRE(!p.gelu_out || (!edge && (kern != nullptr) && ((epi & OT_EPI_GELU_BWD) || (plane && one))),
              "ot_mixed_gemm_rms: gelu_out needs whole tiles (with epi OT_EPI_BIAS: the bf16-mode plane GEMM)");
-  OT_REQUIRE(!p.xn_out || (plane && one && x == OT_AX_RMSNORM && a_rstd && a_gamma && p.ldxn % 8 == 0 && K <= 1024 &&
+  OT_REQUIRE(!p.xn_out || (plane && one && (x == OT_AX_RMSNORM || x == OT_AX_BF16_RMSNORM) && a_rstd && a_gamma &&
+                           p.ldxn % 8 == 0 && K <= 1024 &&
                            ((uintptr_t)p.xn_out % 16) == 0),
              "ot_mixed_gemm_rms: xn_out needs the bf16-mode plane GEMM with the RMSNorm prologue, K <= 1024, ldxn %% 8 == 0 and 16-B "
              "alignment");

@@ -84,7 +84,7 @@ def gemm_bytes(M: int, K: int, N: int, a_xform: int, epi: int) -> float:
     (at most a few MB of L2-resident images) are left out."""
     mn = (1 + bool(epi & _lib.OT_EPI_RESIDUAL) + bool(epi & _lib.OT_EPI_GELU_BWD)
           + bool(epi & _lib.OT_EPI_ACCUMULATE))
-    a_bytes = 2.0 if a_xform == _lib.OT_AX_BF16 else 4.0           # OT_AX_BF16: the stored bf16 gelu(U)
+    a_bytes = 2.0 if a_xform in (_lib.OT_AX_BF16, _lib.OT_AX_BF16_RMSNORM) else 4.0   # bf16 A operands
     c_less = 2.0 * M * N if epi & _lib.OT_EPI_C_BF16 else 0.0       # OT_EPI_C_BF16: C written in bf16
     return a_bytes * M * K + 4.0 * M * (a_xform == _lib.OT_AX_RMSNORM) + 4.0 * M * N * mn - c_less
 
@@ -175,7 +175,8 @@ def gemm_rms(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish,
              dres_tail: Tuple[int, int] = (0, 0), dx_masked: Ptrish = None, lddxm: int = 0,
              dgamma: Ptrish = None, accumulate_dgamma: bool = False, device=None, bimg=None,
              aux: Ptrish = None, ldaux: int = 0, rowdot: Ptrish = None, rowdot_n: int = 0,
-             gelu_out: Ptrish = None, ldgelu: int = 0, xn_out: Ptrish = None, ldxn: int = 0) -> None:
+             gelu_out: Ptrish = None, ldgelu: int = 0, xn_out: Ptrish = None, ldxn: int = 0,
+             c16_out: Ptrish = None, ldc16: int = 0) -> None:
     """ot_mixed_gemm_rms: the GEMM with a row-norm epilogue (OT_EPI_ROW_RSTD: emit the next RMSNorm's
     rstd; OT_EPI_RMSNORM_BWD: apply the RMSNorm backward to the product, + dres, dgamma, taking
     <gamma dy, x> from ``rowdot`` when N > 128; OT_EPI_GELU_BWD | OT_EPI_ROWDOT: also write each 128-column
@@ -190,7 +191,7 @@ def gemm_rms(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish,
     e = _lib.RmsEpilogue(ptr(rstd_out), float(eps), ptr(nx), ldnx, ptr(ngamma), ptr(nrstd), ptr(dres), lddres,
                          dres_tail[0], dres_tail[1], _sel(dres_tail), ptr(dx_masked), lddxm, ptr(dgamma),
                          int(accumulate_dgamma), ptr(ws), ws.numel(), ptr(rowdot), int(rowdot_n),
-                         ptr(gelu_out), int(ldgelu), ptr(xn_out), int(ldxn))
+                         ptr(gelu_out), int(ldgelu), ptr(xn_out), int(ldxn), ptr(c16_out), int(ldc16))
     ev = _probe.begin() if _probe is not None else None
     args = (mode, ptr(A), lda, K, ptr(in_rows), a_xform, ptr(rstd), ptr(gamma), ptr(W),
             w_gstride, ldw, N, ptr(tile_group), ntiles, ptr(bias), bias_gstride, ptr(C), ldc, ptr(out_rows), epi,

@@ -27,7 +27,7 @@ import torch.nn as nn
 
 from . import _lib
 from . import kernels as K
-from ._lib import (OT_AX_BF16, OT_AX_GELU, OT_AX_RMSNORM, OT_EPI_ACCUMULATE, OT_EPI_AUX_BF16, OT_EPI_BIAS,
+from ._lib import (OT_AX_BF16, OT_AX_BF16_RMSNORM, OT_AX_GELU, OT_AX_RMSNORM, OT_EPI_ACCUMULATE, OT_EPI_AUX_BF16, OT_EPI_BIAS,
                    OT_EPI_C_BF16, OT_EPI_DROPOUT, OT_EPI_GELU_BWD, OT_EPI_RESIDUAL, OT_EPI_RMSNORM_BWD,
                    OT_EPI_ROW_RSTD, OT_EPI_ROWDOT, OT_GEMM_NN, OT_GEMM_NT, OT_WG_D_BF16, NS_FIELD_BYTES)
 from .config import OneTransConfig, check_pyramid_select, get_model_config
@@ -181,6 +181,11 @@ def _block_forward(m, l, x, I, Kq, seed, training, rstd_in=None, select=False, n
         else:
             K.pyramid_select(B, I, Kq, pos, inv)
     tail = (Kq, I, pos)
+    # bf16 mode: the block input in bf16 as the previous block's FFN2 epilogue stored it (ot_rms_epilogue
+    # .c16_out) — the QKV GEMM reads it (OT_AX_BF16_RMSNORM: the values its fragments would round x to)
+    x16 = m.take_x16(l, x) if d % TILE == 0 and need_out else None
+    ax1 = OT_AX_BF16_RMSNORM if x16 is not None else OT_AX_RMSNORM
+    xa = x16 if x16 is not None else x
     qkv = torch.empty(B * I, 3 * d, device=dev)
     # bf16 mode, training: the QKV / FFN1 GEMMs also store their normalised A rows in bf16 (ot_rms_epilogue
     # .xn_out) for the copy-staged bf16 weight gradients of Wqkv / W1 (operands read once, no norm re-applied)
@@ -190,25 +195,25 @@ def _block_forward(m, l, x, I, Kq, seed, training, rstd_in=None, select=False, n
     x1n = torch.empty(B * Kq, d, dtype=torch.int16, device=dev) if xn_on else None
     if xn1 is not None:
         full = Kq == I
-        K.gemm_rms(OT_GEMM_NT, x, d, d, ma['rows'][0], wqkv if full else (wqkv, d * d), 3 * d * d, d,
+        K.gemm_rms(OT_GEMM_NT, xa, d, d, ma['rows'][0], wqkv if full else (wqkv, d * d), 3 * d * d, d,
                    3 * d if full else 2 * d, ma['tile_group'], na, qkv if full else (qkv, d), 3 * d, ma['rows'][0],
-                   epi=0, a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=maps['all'].nrows, device=dev,
+                   epi=0, a_xform=ax1, rstd=rstd1, gamma=g1, m_rows=maps['all'].nrows, device=dev,
                    bimg=m.bimg(f'blk.{l}.wqkv') if full else m.bimg(f'blk.{l}.wqkv', tn0=d // TILE),
                    xn_out=xn1, ldxn=d)
         if not full:
-            K.gemm(OT_GEMM_NT, x, d, d, qrows, wqkv, 3 * d * d, d, d, mt['tile_group'], nt, qkv,
-                   3 * d, qrows, a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=maps['tail'].nrows,
+            K.gemm(OT_GEMM_NT, xa, d, d, qrows, wqkv, 3 * d * d, d, d, mt['tile_group'], nt, qkv,
+                   3 * d, qrows, a_xform=ax1, rstd=rstd1, gamma=g1, m_rows=maps['tail'].nrows,
                    bimg=m.bimg(f'blk.{l}.wqkv'))
     elif Kq == I:
-        K.gemm(OT_GEMM_NT, x, d, d, ma['rows'][0], wqkv, 3 * d * d, d, 3 * d, ma['tile_group'], na, qkv,
-               3 * d, ma['rows'][0], a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=maps['all'].nrows,
+        K.gemm(OT_GEMM_NT, xa, d, d, ma['rows'][0], wqkv, 3 * d * d, d, 3 * d, ma['tile_group'], na, qkv,
+               3 * d, ma['rows'][0], a_xform=ax1, rstd=rstd1, gamma=g1, m_rows=maps['all'].nrows,
                bimg=m.bimg(f'blk.{l}.wqkv'))
     else:
-        K.gemm(OT_GEMM_NT, x, d, d, ma['rows'][0], (wqkv, d * d), 3 * d * d, d, 2 * d, ma['tile_group'], na,
-               (qkv, d), 3 * d, ma['rows'][0], a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=maps['all'].nrows,
+        K.gemm(OT_GEMM_NT, xa, d, d, ma['rows'][0], (wqkv, d * d), 3 * d * d, d, 2 * d, ma['tile_group'], na,
+               (qkv, d), 3 * d, ma['rows'][0], a_xform=ax1, rstd=rstd1, gamma=g1, m_rows=maps['all'].nrows,
                bimg=m.bimg(f'blk.{l}.wqkv', tn0=d // TILE) if d % TILE == 0 else None)
-        K.gemm(OT_GEMM_NT, x, d, d, qrows, wqkv, 3 * d * d, d, d, mt['tile_group'], nt, qkv,
-               3 * d, qrows, a_xform=OT_AX_RMSNORM, rstd=rstd1, gamma=g1, m_rows=maps['tail'].nrows,
+        K.gemm(OT_GEMM_NT, xa, d, d, qrows, wqkv, 3 * d * d, d, d, mt['tile_group'], nt, qkv,
+               3 * d, qrows, a_xform=ax1, rstd=rstd1, gamma=g1, m_rows=maps['tail'].nrows,
                bimg=m.bimg(f'blk.{l}.wqkv'))
     o = torch.empty(B * Kq, d, device=dev)
     lse = torch.empty(B * H * Kq, device=dev)
@@ -229,11 +234,13 @@ def _block_forward(m, l, x, I, Kq, seed, training, rstd_in=None, select=False, n
     # x1 = x[tail] + drop(o @ Wo)      (model.py:117, 193)
     x1 = torch.empty(B * Kq, d, device=dev)
     rstd2 = torch.empty(B * Kq, device=dev)
+    x1_16 = None
     if fuse:
+        x1_16 = torch.empty(B * Kq, d, dtype=torch.int16, device=dev) if m.x16_on(d) else None
         K.gemm_rms(OT_GEMM_NT, o, d, d, mt['rows'][1], wo, 0, d, d, mt['tile_group'], nt, x1, d, mt['rows'][1],
                    epi=OT_EPI_RESIDUAL | dflag | OT_EPI_ROW_RSTD, res=x, ldres=d, res_tok=1, seed=seed,
                    site=2 * l, drop=rate, tail=tail, m_rows=maps['tail'].nrows, rstd_out=rstd2, eps=RMS_EPS,
-                   bimg=m.bimg(f'blk.{l}.wo'))
+                   bimg=m.bimg(f'blk.{l}.wo'), c16_out=x1_16, ldc16=d)
     else:
         K.gemm(OT_GEMM_NT, o, d, d, mt['rows'][1], wo, 0, d, d, mt['tile_group'], nt, x1, d, mt['rows'][1],
                epi=OT_EPI_RESIDUAL | dflag, res=x, ldres=d, res_tok=1, seed=seed, site=2 * l, drop=rate,
@@ -251,15 +258,18 @@ def _block_forward(m, l, x, I, Kq, seed, training, rstd_in=None, select=False, n
     u_bf = h is not None and m.u_bf16 and m.du_bf16 and m.fuse_bwd2 and not m.fuse_bwd and f % TILE == 0
     u = torch.empty(B * Kq, f, device=dev, dtype=torch.int16 if u_bf else torch.float32)
     if h is not None:
-        K.gemm_rms(OT_GEMM_NT, x1, d, d, mt['rows'][1], w1, d * f, d, f, mt['tile_group'], nt, u, f, mt['rows'][1],
-                   a_xform=OT_AX_RMSNORM, rstd=rstd2, gamma=g2, bias=b1, bias_gstride=f,
+        K.gemm_rms(OT_GEMM_NT, x1 if x1_16 is None else x1_16, d, d, mt['rows'][1], w1, d * f, d, f,
+                   mt['tile_group'], nt, u, f, mt['rows'][1],
+                   a_xform=OT_AX_RMSNORM if x1_16 is None else OT_AX_BF16_RMSNORM, rstd=rstd2, gamma=g2, bias=b1,
+                   bias_gstride=f,
                    epi=OT_EPI_BIAS | (OT_EPI_C_BF16 if u_bf else 0),
                    m_rows=maps['tail'].nrows, bimg=m.bimg(f'blk.{l}.w1'), gelu_out=h, ldgelu=f,
                    xn_out=x1n, ldxn=d)
     else:
-        K.gemm(OT_GEMM_NT, x1, d, d, mt['rows'][1], w1, d * f, d, f, mt['tile_group'], nt, u, f, mt['rows'][1],
-               a_xform=OT_AX_RMSNORM, rstd=rstd2, gamma=g2, bias=b1, bias_gstride=f, epi=OT_EPI_BIAS,
-               m_rows=maps['tail'].nrows, bimg=m.bimg(f'blk.{l}.w1'))
+        K.gemm(OT_GEMM_NT, x1 if x1_16 is None else x1_16, d, d, mt['rows'][1], w1, d * f, d, f, mt['tile_group'],
+               nt, u, f, mt['rows'][1], a_xform=OT_AX_RMSNORM if x1_16 is None else OT_AX_BF16_RMSNORM, rstd=rstd2,
+               gamma=g2, bias=b1, bias_gstride=f, epi=OT_EPI_BIAS, m_rows=maps['tail'].nrows,
+               bimg=m.bimg(f'blk.{l}.w1'))
     if x1n is not None and h is None:                # the FFN1 GEMM above did not store it
         x1n = None
     saved = (x, rstd1, qkv, o, lse, x1, rstd2, u, h, xn1, x1n)
@@ -271,11 +281,13 @@ def _block_forward(m, l, x, I, Kq, seed, training, rstd_in=None, select=False, n
     a2, ax2 = (h, OT_AX_BF16) if h is not None else (u, OT_AX_GELU)
     if fuse:
         rstd_out = torch.empty(B * Kq, device=dev)
+        x2_16 = torch.empty(B * Kq, d, dtype=torch.int16, device=dev) if m.x16_on(d) and w2img is not None else None
         K.gemm_rms(OT_GEMM_NT, a2, f, f, mt['rows'][1], w2, f * d, f, d, mt['tile_group'], nt, x2, d,
                    mt['rows'][1], a_xform=ax2, bias=b2, bias_gstride=d,
                    epi=OT_EPI_BIAS | OT_EPI_RESIDUAL | dflag | OT_EPI_ROW_RSTD, res=x1, ldres=d, res_tok=0,
                    seed=seed, site=2 * l + 1, drop=rate, tail=tail, m_rows=maps['tail'].nrows,
-                   rstd_out=rstd_out, eps=RMS_EPS, bimg=w2img)
+                   rstd_out=rstd_out, eps=RMS_EPS, bimg=w2img, c16_out=x2_16, ldc16=d)
+        m.put_x16(l + 1, x2, x2_16)
     else:
         K.gemm(OT_GEMM_NT, a2, f, f, mt['rows'][1], w2, f * d, f, d, mt['tile_group'], nt, x2, d, mt['rows'][1],
                a_xform=ax2, bias=b2, bias_gstride=d, epi=OT_EPI_BIAS | OT_EPI_RESIDUAL | dflag, res=x1,
@@ -651,6 +663,9 @@ class OneTransModel(nn.Module):
         self.qkv_bf16 = os.environ.get('ONETRANS_QKV_BF16', '1') != '0'
         # ... and the key slices' dQ partials in bf16 (ONETRANS_DQ_PART_BF16=0: f32; not bit-identical)
         self.dq_part_bf16 = os.environ.get('ONETRANS_DQ_PART_BF16', '1') != '0'
+        # ... and the residual stream's bf16 copies for the QKV / FFN1 GEMMs' A (ONETRANS_X16=0: f32 A)
+        self.x16 = os.environ.get('ONETRANS_X16', '1') != '0'
+        self._x16 = None
         # block weight gradients run on a second stream, overlapping the dgrad chain
         self.overlap_wgrad = os.environ.get('ONETRANS_OVERLAP_WGRAD', '1') != '0'
         self._side = None
@@ -722,6 +737,22 @@ class OneTransModel(nn.Module):
         if self.config.hidden_dim == TILE:
             return True
         return all(self.bimg(n, o) is not None for (n, o) in images)
+
+    def x16_on(self, d: int) -> bool:
+        """Store bf16 copies of the residual stream for the next GEMM's A (bf16 mode, plane GEMMs)?"""
+        return self.x16 and d % TILE == 0 and K.matmul_mode() == 'bf16' and self.use_plane
+
+    def put_x16(self, layer: int, x: torch.Tensor, x16: Optional[torch.Tensor]) -> None:
+        """Block ``layer - 1``'s output x and its bf16 copy, for block ``layer``."""
+        self._x16 = (layer, x, x.data_ptr(), x.numel(), x16) if x16 is not None else None
+
+    def take_x16(self, layer: int, x: torch.Tensor) -> Optional[torch.Tensor]:
+        """The bf16 copy of x that block ``layer - 1``'s FFN2 epilogue stored, if x is that output."""
+        c, self._x16 = self._x16, None
+        if (c is None or c[0] != layer or not self.x16_on(x.shape[-1]) or c[2] != x.data_ptr()
+                or c[3] != x.numel()):
+            return None
+        return c[4]
 
     def bimg(self, name: str, orient: str = 'fwd', tn0: int = 0):
         """(image, column tiles per group, first tile) of a weight bank's pre-split B image for the plane

@@ -395,3 +395,58 @@ def test_plane_gemm_xn_out(dev, plane_mode, N):
     assert torch.equal(outs[0], outs[1])
     ref = ((A * gamma.to(dev)) * rstd[:, None]).to(torch.bfloat16).view(torch.int16)
     assert torch.equal(xn, ref)
+
+
+@pytest.mark.parametrize('N', [1536, 2048])
+def test_plane_gemm_bf16_rmsnorm_a(dev, plane_mode, N):
+    """bf16 mode: the QKV / FFN1 GEMM from the bf16 copy of its input (OT_AX_BF16_RMSNORM: gamma in the
+    image, rstd as the row scale) gives C bit-identical to the f32 input under the RMSNorm prologue (whose
+    fragments round x to the same bf16 values); its xn_out is bf16((bf16(x) * gamma) * rstd); and an
+    epilogue's c16_out (the producer side: Wo / FFN2 with residual, dropout, row rstd) is its C rounded."""
+    if plane_mode != 'bf16':
+        pytest.skip('bf16-mode forms')
+    from recommend_amd._lib import OT_AX_BF16_RMSNORM
+    rng = np.random.default_rng(N + 3)
+    G, M, K_ = 3, 700, 512
+    rm = ragged_map(rng, M, G)
+    dm = rm.to(dev)
+    x = torch.randn(M, K_, device=dev)
+    x16 = x.to(torch.bfloat16).view(torch.int16)
+    W = torch.randn(G, N, K_) / math.sqrt(K_)
+    gamma = 1 + 0.1 * torch.randn(K_)
+    rstd = torch.rand(M, device=dev) + 0.5
+    bias = torch.randn(G, N, device=dev)
+    img, ntn = make_image(W, dev, gamma)
+    outs = []
+    xn = torch.zeros(M, K_, dtype=torch.int16, device=dev)
+    for a, ax in ((x, OT_AX_RMSNORM), (x16, OT_AX_BF16_RMSNORM)):
+        C = torch.full((M, N), float('nan'), device=dev)
+        K.gemm_rms(OT_GEMM_NT, a, K_, K_, dm['rows'][0], W.to(dev), N * K_, K_, N, dm['tile_group'], rm.ntiles, C, N,
+                   dm['rows'][1], epi=OT_EPI_BIAS, a_xform=ax, rstd=rstd, gamma=gamma.to(dev), bias=bias,
+                   bias_gstride=N, device=dev, bimg=(img, ntn, 0), xn_out=xn if ax == OT_AX_BF16_RMSNORM else None,
+                   ldxn=K_)
+        outs.append(C)
+    torch.cuda.synchronize()
+    assert not torch.isnan(outs[1]).any()
+    assert torch.equal(outs[0], outs[1])
+    ref = ((x16.view(torch.bfloat16).float() * gamma.to(dev)) * rstd[:, None]).to(torch.bfloat16).view(torch.int16)
+    assert torch.equal(xn, ref)
+    # producer side: residual + dropout + row rstd epilogue with the bf16 copy of C
+    B, I, Kq, d = 37, 9, 4, 512
+    Mr = B * Kq
+    r = np.arange(Mr)
+    rm2 = build_map([[r[r % 2 == g], r[r % 2 == g]] for g in range(2)])
+    d2 = rm2.to(dev)
+    A = torch.randn(Mr, d, device=dev)
+    W2 = torch.randn(1, d, d) / math.sqrt(d)
+    img2, ntn2 = make_image(W2, dev)
+    res = torch.randn(B * I, d, device=dev)
+    C = torch.empty(Mr, d, device=dev)
+    c16 = torch.zeros(Mr, d, dtype=torch.int16, device=dev)
+    rs = torch.empty(Mr, device=dev)
+    K.gemm_rms(OT_GEMM_NT, A, d, d, d2['rows'][0], W2.to(dev), 0, d, d, d2['tile_group'], rm2.ntiles, C, d,
+               d2['rows'][1], epi=OT_EPI_RESIDUAL | OT_EPI_DROPOUT | OT_EPI_ROW_RSTD, res=res, ldres=d, res_tok=1,
+               seed=3, site=1, drop=0.1, tail=(Kq, I), rstd_out=rs, eps=1e-6, device=dev, bimg=(img2, ntn2, 0),
+               c16_out=c16, ldc16=d)
+    torch.cuda.synchronize()
+    assert torch.equal(c16, C.to(torch.bfloat16).view(torch.int16))

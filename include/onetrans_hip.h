@@ -283,6 +283,9 @@ int ot_attn_bwd_ex(const float* qkv, int64_t ld, const float* out, const float* 
  * then rounded: not the f32 sum rounded once — about one more bf16 rounding of each partial) */
 #define OT_ATTN_DQ_PART_BF16 4
 int ot_attn_bwd_dqkv_bf16_supported(int I, int K, int head_dim, int selected);
+/* the OT_ATTN_*_BF16 flags the backward supports at this shape: all three on the key-grouped bf16 backward,
+ * OT_ATTN_DQKV_BF16 alone on the short-tail kernel (K <= 4: the last layer after DCE), none otherwise */
+int ot_attn_bwd_bf16_forms(int I, int K, int head_dim, int selected);
 size_t ot_attn_bwd_flags_workspace_size(int B, int H, int I, int K, int head_dim, int selected, int flags);
 int ot_attn_bwd_flags(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
                       int B, int H, int I, int K, const int32_t* qpos, int head_dim, void* dqkv, int flags,

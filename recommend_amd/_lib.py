@@ -84,6 +84,7 @@ SIGNATURES = {
     'ot_attn_bwd_ex_workspace_size': (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
     'ot_attn_bwd_ex': (c_int, [P, I64, P, P, P, c_int, c_int, c_int, c_int, P, c_int, P, P, c_size_t, P]),
     'ot_attn_bwd_dqkv_bf16_supported': (c_int, [c_int, c_int, c_int, c_int]),
+    'ot_attn_bwd_bf16_forms': (c_int, [c_int, c_int, c_int, c_int]),
     'ot_attn_bwd_flags_workspace_size': (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int, c_int]),
     'ot_attn_bwd_flags': (c_int, [P, I64, P, P, P, c_int, c_int, c_int, c_int, P, c_int, P, c_int, P, c_size_t, P]),
     'ot_attn_fwd_cached': (c_int, [P, I64, P, I64, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),

@@ -1369,8 +1369,14 @@ __global__ __launch_bounds__(256) void attn_bwd_small_kernel(AttnArgs p) {
       dq[j] += ds * kv;
     }
     if (live) {
-      *reinterpret_cast<f32x4*>(dK + ro) = dk;
-      *reinterpret_cast<f32x4*>(dV + ro) = dv;
+      if (p.dq_bf16) {                                 // bf16 dqkv (OT_ATTN_DQKV_BF16)
+        uint16_t* dK16 = reinterpret_cast<uint16_t*>(p.dqkv) + tok0 * p.ld + p.d + h * HD + 4 * sub;
+        *reinterpret_cast<u32x2*>(dK16 + ro) = bf16_rne4(dk);
+        *reinterpret_cast<u32x2*>(dK16 + p.d + ro) = bf16_rne4(dv);
+      } else {
+        *reinterpret_cast<f32x4*>(dK + ro) = dk;
+        *reinterpret_cast<f32x4*>(dV + ro) = dv;
+      }
     }
   }
 #pragma unroll
@@ -1382,7 +1388,13 @@ __global__ __launch_bounds__(256) void attn_bwd_small_kernel(AttnArgs p) {
       v.x += __shfl_xor(v.x, off, 64); v.y += __shfl_xor(v.y, off, 64);
       v.z += __shfl_xor(v.z, off, 64); v.w += __shfl_xor(v.w, off, 64);
     }
-    if (slot == 0) *reinterpret_cast<f32x4*>(p.dqkv + (tok0 + qpos[j]) * p.ld + h * HD + 4 * sub) = v;
+    if (slot == 0) {
+      if (p.dq_bf16)
+        *reinterpret_cast<u32x2*>(reinterpret_cast<uint16_t*>(p.dqkv) + (tok0 + qpos[j]) * p.ld + h * HD + 4 * sub) =
+            bf16_rne4(v);
+      else
+        *reinterpret_cast<f32x4*>(p.dqkv + (tok0 + qpos[j]) * p.ld + h * HD + 4 * sub) = v;
+    }
   }
 }
 
@@ -1630,6 +1642,13 @@ extern "C" int ot_attn_bwd_dqkv_bf16_supported(int I, int K, int head_dim, int s
   return attn_bwd_kgroup(I, K, head_dim, selected != 0) != 0;
 }
 
+extern "C" int ot_attn_bwd_bf16_forms(int I, int K, int head_dim, int selected) {
+  if (attn_bwd_kgroup(I, K, head_dim, selected != 0))
+    return OT_ATTN_DQKV_BF16 | OT_ATTN_QKV_BF16 | OT_ATTN_DQ_PART_BF16;
+  if (K > 0 && K <= SMALL_K && (head_dim == 32 || head_dim == 64 || head_dim == 128)) return OT_ATTN_DQKV_BF16;
+  return 0;
+}
+
 extern "C" size_t ot_attn_bwd_flags_workspace_size(int B, int H, int I, int K, int head_dim, int selected, int flags) {
   const int S = attn_bwd_kslices(B, H, I, K, head_dim, selected != 0);
   const int slots = (flags & OT_ATTN_DQKV_BF16) ? S : S - 1;
@@ -1662,14 +1681,14 @@ extern "C" int ot_attn_bwd_flags(const float* qkv, int64_t ld, const float* out,
              "ot_attn_bwd_flags: unknown flags %d", flags);
   OT_REQUIRE(!(flags & OT_ATTN_DQ_PART_BF16) || (flags & OT_ATTN_DQKV_BF16),
              "ot_attn_bwd_flags: OT_ATTN_DQ_PART_BF16 goes with OT_ATTN_DQKV_BF16");
+  OT_REQUIRE((flags & ot_attn_bwd_bf16_forms(I, K, head_dim, qpos != nullptr)) == flags,
+             "ot_attn_bwd_flags: flags %d not supported at I %d K %d head_dim %d (ot_attn_bwd_bf16_forms)", flags, I,
+             K, head_dim);
   OT_REQUIRE(!(flags & OT_ATTN_QKV_BF16) || (ot_attn_bwd_dqkv_bf16_supported(I, K, head_dim, qpos != nullptr) &&
                                              ((uintptr_t)qkv % 16) == 0 && ld % 8 == 0),
              "ot_attn_bwd_flags: OT_ATTN_QKV_BF16 needs the key-grouped bf16 backward, 16-B aligned qkv, ld %% 8 == 0");
   OT_REQUIRE(ws_bytes >= ot_attn_bwd_flags_workspace_size(B, H, I, K, head_dim, qpos != nullptr, flags),
              "ot_attn_bwd_flags: workspace too small");
-  OT_REQUIRE(!(flags & OT_ATTN_DQKV_BF16) || ot_attn_bwd_dqkv_bf16_supported(I, K, head_dim, qpos != nullptr),
-             "ot_attn_bwd_flags: OT_ATTN_DQKV_BF16 needs the key-grouped bf16 backward (bf16 mode, tail queries, "
-             "head_dim 32 / 64, long tails: ot_attn_bwd_dqkv_bf16_supported)");
   OT_REQUIRE(!(flags & OT_ATTN_DQKV_BF16) || ((uintptr_t)dqkv % 8) == 0, "ot_attn_bwd_flags: dqkv alignment");
   return attn_bwd_impl(qkv, ld, out, dout, lse, B, H, I, K, qpos, head_dim, (float*)dqkv, (float*)workspace,
                        ws_bytes, stream, flags);
@@ -1691,6 +1710,7 @@ static int attn_bwd_impl(const float* qkv, int64_t ld, const float* out, const f
                      (hipStream_t)stream, out, dout, lse, delta_ws, B, H, K, head_dim, main_blocks, pad_blocks, qpos);
   OT_LAUNCH_CHECK("ot_attn_bwd(prep)");
   const int mm = ot_get_matmul_mode();
+  p.dq_bf16 = (flags & OT_ATTN_DQKV_BF16) ? 1 : 0;
   if (K <= SMALL_K) {
     OT_ATTN_DISPATCH(attn_bwd_small_kernel, head_dim, dim3(ceil_div((int64_t)B * H, 4)), dim3(256), 0,
                      (hipStream_t)stream, p);

@@ -273,6 +273,11 @@ def attn_fwd(qkv: torch.Tensor, ld: int, B: int, H: int, I: int, K: int, hd: int
                    f'fwd{"_fp8" if fp8 else ""} I{I} K{K} hd{hd}')
 
 
+def attn_bwd_bf16_forms(I, K, hd, qpos=None) -> int:
+    """ot_attn_bwd_bf16_forms: the OT_ATTN_*_BF16 flags the backward supports at this shape."""
+    return int(_lib.load().ot_attn_bwd_bf16_forms(I, K, hd, int(qpos is not None)))
+
+
 def attn_bwd_bf16_supported(I, K, hd, qpos=None) -> bool:
     """ot_attn_bwd_dqkv_bf16_supported: can the backward emit dqkv in bf16 (key-grouped bf16 kernel)?"""
     return bool(_lib.load().ot_attn_bwd_dqkv_bf16_supported(I, K, hd, int(qpos is not None)))
@@ -283,7 +288,8 @@ def attn_bwd(qkv, ld, out, dout, lse, B, H, I, K, hd, dqkv, qpos=None, dq_part_b
     (int16: OT_ATTN_QKV_BF16, the fp8 forward's bf16 dequantised operands)."""
     flags = ((_lib.OT_ATTN_DQKV_BF16 if dqkv.dtype == torch.int16 else 0)
              | (_lib.OT_ATTN_QKV_BF16 if qkv.dtype == torch.int16 else 0)
-             | (_lib.OT_ATTN_DQ_PART_BF16 if dq_part_bf16 and dqkv.dtype == torch.int16 else 0))
+             | (_lib.OT_ATTN_DQ_PART_BF16 if dq_part_bf16 and dqkv.dtype == torch.int16
+                and attn_bwd_bf16_forms(I, K, hd, qpos) & _lib.OT_ATTN_DQ_PART_BF16 else 0))
     ws = workspace(size('ot_attn_bwd_flags_workspace_size', B, H, I, K, hd, int(qpos is not None), flags),
                    qkv.device)
     ev = _probe.begin() if _probe is not None else None

@@ -429,7 +429,8 @@ class _Block(torch.autograd.Function):
         # bf16 mode, key-grouped backward (C5): dQKV in bf16 (OT_ATTN_DQKV_BF16) — the QKV dgrad (bf16 A) and
         # the Wqkv weight gradient (OT_WG_D_BF16) round it to bf16 anyway: the same values, half the bytes
         qp = _attn_qpos(cfg, pos)
-        dq_bf = (m.dqkv_bf16 and K.matmul_mode() == 'bf16' and K.attn_bwd_bf16_supported(I, Kq, hd, qp)
+        dq_bf = (m.dqkv_bf16 and K.matmul_mode() == 'bf16'
+                 and K.attn_bwd_bf16_forms(I, Kq, hd, qp) & _lib.OT_ATTN_DQKV_BF16
                  and m.bimg(f'blk.{l}.wqkv', 'dgrad') is not None)
         dqkv = torch.empty(B * I, 3 * d, device=dev, dtype=torch.int16 if dq_bf else torch.float32)
         if Kq < I:

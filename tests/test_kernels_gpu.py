@@ -790,3 +790,26 @@ def test_dropout_apply_bf16(dev):
     torch.cuda.synchronize()
     assert torch.equal(out, ref.to(torch.bfloat16).view(torch.int16))
     assert 0.05 < (ref == 0).float().mean().item() < 0.15
+
+
+@pytest.mark.parametrize('K_', [1, 3])
+def test_attn_bwd_small_bf16_dqkv(dev, K_):
+    """Short-tail attention backward (K <= 4, the last layer after DCE) with bf16 dqkv
+    (OT_ATTN_DQKV_BF16, ot_attn_bwd_bf16_forms): each element the f32 result rounded to nearest even."""
+    from recommend_amd._lib import OT_ATTN_DQKV_BF16, OT_ATTN_QKV_BF16
+    B, H, I, hd = 5, 4, 37, 32
+    d = H * hd
+    assert K.attn_bwd_bf16_forms(I, K_, hd) == OT_ATTN_DQKV_BF16
+    assert K.attn_bwd_bf16_forms(I, K_, hd) & OT_ATTN_QKV_BF16 == 0
+    g = torch.Generator().manual_seed(K_)
+    qkv = torch.randn(B * I, 3 * d, generator=g).to(dev)
+    out = torch.empty(B * K_, d, device=dev)
+    lse = torch.empty(B * H * K_, device=dev)
+    K.attn_fwd(qkv, 3 * d, B, H, I, K_, hd, out, lse)
+    dout = torch.randn(B * K_, d, generator=g).to(dev)
+    d32 = torch.zeros(B * I, 3 * d, device=dev)
+    d16 = torch.zeros(B * I, 3 * d, dtype=torch.int16, device=dev)
+    K.attn_bwd(qkv, 3 * d, out, dout, lse, B, H, I, K_, hd, d32)
+    K.attn_bwd(qkv, 3 * d, out, dout, lse, B, H, I, K_, hd, d16, dq_part_bf16=True)
+    torch.cuda.synchronize()
+    assert torch.equal(d16, d32.to(torch.bfloat16).view(torch.int16))

@@ -33,6 +33,10 @@ namespace ot {
 #ifndef OT_GEMM_RMS_EARLY
 #define OT_GEMM_RMS_EARLY 1
 #endif
+#ifndef OT_PLANE_BF16_NSTG         // stage buffers of the bf16-mode plane GEMM (3: 4 workgroups / CU)
+#define OT_PLANE_BF16_NSTG 3
+#endif
+constexpr int PLANE_BF16_NSTG = OT_PLANE_BF16_NSTG;
 #ifndef OT_PLANE_EPI_RBN          // epilogue rows per operand-load batch of the 4-workgroup plane GEMMs
 #define OT_PLANE_EPI_RBN 4
 #endif
@@ -727,7 +731,7 @@ constexpr int pg_stage_bytes() { return PG_A_BYTES + (TERMS == 1 ? GT * 16 * 2 :
 
 template <int AXT, int EPIT, int NSTG, int MINW, int TERMS = 6>
 __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
-  static_assert(NSTG == 2 || NSTG == 3, "plane GEMM stages");
+  static_assert(NSTG >= 2 && NSTG <= 4, "plane GEMM stages");
   static_assert(TERMS == 6 || TERMS == 1, "plane GEMM terms");
   // OT_AX_BF16: A holds bf16 values (the FFN1 epilogue's stored gelu(U)): 32 B per row and stage, the
   // lane's fragment is one 16-B LDS read, no conversion (bf16 mode only)
@@ -832,18 +836,17 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
   }
 
   issue(0, 0);
-  if (NSTG == 3 && nk > 1) issue(1, 1);
+  if (NSTG >= 3 && nk > 1) issue(1, 1);
+  if (NSTG >= 4 && nk > 2) issue(2, 2);
   for (int kt = 0; kt < nk; ++kt) {
     // this wave's copies of stage kt are done (with 3 stages the 5 (TERMS 1: 3) of stage kt+1 may
     // still fly), every wave's after the barrier; the barrier also retires every read of the buffer
     // that the copies of stage kt+NSTG-1 then overwrite (last read in iteration kt-1)
-    if (NSTG == 3 && kt + 1 < nk) {
-      if (ABF) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      else if (TERMS == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    constexpr int OPS = ABF ? 2 : (TERMS == 1 ? 3 : 5);    // copies per wave and stage
+    const int ahead = (NSTG - 2 < nk - 1 - kt) ? NSTG - 2 : nk - 1 - kt;   // later stages that may still fly
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * OPS) : "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(OPS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -1820,7 +1823,7 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
     void (*pk)(GemmArgs) = nullptr;
 #define OT_PSPEC(AX_, EP_) \
     if (x == AX_ && e == (EP_)) \
-      pk = one ? plane_gemm_kernel<AX_, EP_, 3, 4, 1> \
+      pk = one ? plane_gemm_kernel<AX_, EP_, PLANE_BF16_NSTG, 4, 1> \
                : (g_plane_cfg == 0 ? plane_gemm_kernel<AX_, EP_, 3, 2> : plane_gemm_kernel<AX_, EP_, 2, 4>);
     OT_PSPEC(OT_AX_RMSNORM, 0)
     OT_PSPEC(OT_AX_RMSNORM, OT_EPI_BIAS)
@@ -1841,18 +1844,18 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
     OT_PSPEC(OT_AX_NONE, OT_EPI_RMSNORM_BWD | OT_EPI_DROPOUT)
 #undef OT_PSPEC
     if (one && x == OT_AX_NONE && e == (OT_EPI_GELU_BWD | OT_EPI_ROWDOT | OT_EPI_C_BF16))
-      pk = plane_gemm_kernel<OT_AX_NONE, OT_EPI_GELU_BWD | OT_EPI_ROWDOT | OT_EPI_C_BF16, 3, 4, 1>;
+      pk = plane_gemm_kernel<OT_AX_NONE, OT_EPI_GELU_BWD | OT_EPI_ROWDOT | OT_EPI_C_BF16, PLANE_BF16_NSTG, 4, 1>;
     if (one && x == OT_AX_NONE && e == (OT_EPI_GELU_BWD | OT_EPI_C_BF16))
-      pk = plane_gemm_kernel<OT_AX_NONE, OT_EPI_GELU_BWD | OT_EPI_C_BF16, 3, 4, 1>;
+      pk = plane_gemm_kernel<OT_AX_NONE, OT_EPI_GELU_BWD | OT_EPI_C_BF16, PLANE_BF16_NSTG, 4, 1>;
     if (one && x == OT_AX_NONE && e == (OT_EPI_GELU_BWD | OT_EPI_ROWDOT | OT_EPI_C_BF16 | OT_EPI_AUX_BF16))
-      pk = plane_gemm_kernel<OT_AX_NONE, OT_EPI_GELU_BWD | OT_EPI_ROWDOT | OT_EPI_C_BF16 | OT_EPI_AUX_BF16, 3, 4, 1>;
+      pk = plane_gemm_kernel<OT_AX_NONE, OT_EPI_GELU_BWD | OT_EPI_ROWDOT | OT_EPI_C_BF16 | OT_EPI_AUX_BF16, PLANE_BF16_NSTG, 4, 1>;
     if (one && x == OT_AX_NONE && e == (OT_EPI_GELU_BWD | OT_EPI_C_BF16 | OT_EPI_AUX_BF16))
-      pk = plane_gemm_kernel<OT_AX_NONE, OT_EPI_GELU_BWD | OT_EPI_C_BF16 | OT_EPI_AUX_BF16, 3, 4, 1>;
+      pk = plane_gemm_kernel<OT_AX_NONE, OT_EPI_GELU_BWD | OT_EPI_C_BF16 | OT_EPI_AUX_BF16, PLANE_BF16_NSTG, 4, 1>;
     if (one && x == OT_AX_NONE && e == (OT_EPI_GELU_BWD | OT_EPI_ROWDOT | OT_EPI_AUX_BF16))
-      pk = plane_gemm_kernel<OT_AX_NONE, OT_EPI_GELU_BWD | OT_EPI_ROWDOT | OT_EPI_AUX_BF16, 3, 4, 1>;
+      pk = plane_gemm_kernel<OT_AX_NONE, OT_EPI_GELU_BWD | OT_EPI_ROWDOT | OT_EPI_AUX_BF16, PLANE_BF16_NSTG, 4, 1>;
     if (one && x == OT_AX_RMSNORM && e == (OT_EPI_BIAS | OT_EPI_C_BF16))
-      pk = plane_gemm_kernel<OT_AX_RMSNORM, OT_EPI_BIAS | OT_EPI_C_BF16, 3, 4, 1>;
-#define OT_PSPEC_BF(EP_) if (one && x == OT_AX_BF16 && e == (EP_)) pk = plane_gemm_kernel<OT_AX_BF16, EP_, 3, 4, 1>;
+      pk = plane_gemm_kernel<OT_AX_RMSNORM, OT_EPI_BIAS | OT_EPI_C_BF16, PLANE_BF16_NSTG, 4, 1>;
+#define OT_PSPEC_BF(EP_) if (one && x == OT_AX_BF16 && e == (EP_)) pk = plane_gemm_kernel<OT_AX_BF16, EP_, PLANE_BF16_NSTG, 4, 1>;
     OT_PSPEC_BF(OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_DROPOUT)
     OT_PSPEC_BF(OT_EPI_BIAS | OT_EPI_RESIDUAL)
     OT_PSPEC_BF(OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_DROPOUT | OT_EPI_ROW_RSTD)
@@ -1863,7 +1866,7 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
     OT_PSPEC_BF(OT_EPI_GELU_BWD | OT_EPI_ROWDOT | OT_EPI_C_BF16 | OT_EPI_AUX_BF16)
     OT_PSPEC_BF(OT_EPI_GELU_BWD | OT_EPI_ROWDOT | OT_EPI_C_BF16)
 #undef OT_PSPEC_BF
-#define OT_PSPEC_BR(EP_) if (one && x == OT_AX_BF16_RMSNORM && e == (EP_)) pk = plane_gemm_kernel<OT_AX_BF16_RMSNORM, EP_, 3, 4, 1>;
+#define OT_PSPEC_BR(EP_) if (one && x == OT_AX_BF16_RMSNORM && e == (EP_)) pk = plane_gemm_kernel<OT_AX_BF16_RMSNORM, EP_, PLANE_BF16_NSTG, 4, 1>;
     OT_PSPEC_BR(0)
     OT_PSPEC_BR(OT_EPI_BIAS)
     OT_PSPEC_BR(OT_EPI_BIAS | OT_EPI_C_BF16)
@@ -1891,7 +1894,8 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
   // (+ K floats of gamma behind the stage buffers for the xn_out side output)
   const size_t xn_lds = p.xn_out ? (size_t)K * 4 : 0;
   const size_t launch_shmem = !plane ? shmem
-                              : one ? std::max((size_t)3 * pg_stage_bytes<1>() + xn_lds, (size_t)(64 * (GT + 4) + 8 * GT) * 4)
+                              : one ? std::max((size_t)PLANE_BF16_NSTG * pg_stage_bytes<1>() + xn_lds,
+                                               (size_t)(64 * (GT + 4) + 8 * GT) * 4)
                                     : (size_t)(g_plane_cfg == 0 ? 3 : 2) * PG_STG_BYTES + xn_lds;
   OT_REQUIRE(kern || !rms_flags, "ot_mixed_gemm_rms: no specialised kernel for epilogue flags %d", epi);
   if (!kern) {   // any other combination: generic instantiation (run-time prologue/epilogue)

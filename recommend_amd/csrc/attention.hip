@@ -585,9 +585,16 @@ constexpr int BWD_WAVES() { return HD >= 128 ? 2 : 4; }
 // are sums over all dims: each wave computes its half's partial and the two partials are summed
 // through the wave's dS tile (an LDS exchange, four barriers per (key block, query block) pair); the
 // softmax gradient is then computed identically in both waves.
-template <int HD, bool SEL, int DS = 1>
+// FDL (DS = 1, tail queries, K <= FDL_KP): the row statistics come from the kernel itself instead of
+// attn_bwd_prep_kernel — at the first key block (which every query block sees) the wave forms
+// delta = rowsum(dO * O) from the dO block it holds anyway and one read of the O block, and copies the
+// block's lse (+inf past K); both go to a per-wave LDS row that the later key blocks read.  The prep
+// launch and its re-read of dO disappear (C2: 87 us per layer).
+constexpr int FDL_KP = 160;
+template <int HD, bool SEL, int DS = 1, bool FDL = false>
 __global__ __launch_bounds__(DS == 1 ? 64 * BWD_WAVES<HD>() : 64 * DS, 2)   // 2 waves per SIMD
 void attn_bwd_kernel(AttnArgs p) {
+  static_assert(!FDL || (DS == 1 && !SEL), "attn_bwd_kernel: in-kernel row statistics need DS = 1, tail queries");
   constexpr int LD = TLD<HD>();
   constexpr int SLD = 36;                  // dS tile row stride (32 keys + pad)
   constexpr int PER_WAVE = 3 * 32 * LD + 32 * SLD;
@@ -598,6 +605,7 @@ void attn_bwd_kernel(AttnArgs p) {
   // the registers of a live seed would not fit next to the dK / dV accumulators)
   constexpr bool SEED_EARLY = HD <= 32;
   __shared__ __attribute__((aligned(16))) float lds[NW * PER_WAVE];
+  __shared__ __attribute__((aligned(16))) float rstat[FDL ? NW * 2 * FDL_KP : 4];   // FDL: [wave][lse | delta][KP]
   const int lane = threadIdx.x & 63, li = lane & 31, hh = lane >> 5;
   const int wave = threadIdx.x >> 6;
   float* tO = lds + wave * PER_WAVE;                 // dO block   [query][dim]
@@ -675,10 +683,33 @@ void attn_bwd_kernel(AttnArgs p) {
     for (int qb = qb0; qb < nqb; ++qb) {
       const int q0 = 32 * qb;
       f32x4 l4[4], d4[4];
+      if constexpr (FDL) {
+        float* rl = rstat + wave * 2 * FDL_KP;
+        if (kb == 0) {                                 // lane li: query q0 + li, dims (HD / 2) hh ..
+          float ofo[HD / 2];
+          BWD_LOAD<HD>(ofo, p.o + (int64_t)b * K * p.d + hoff, p.d, q0 + li, K, hh);
+          float pd = 0.f;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        l4[g] = *reinterpret_cast<const f32x4*>(lsep + q0 + 8 * g + 4 * hh);
-        d4[g] = *reinterpret_cast<const f32x4*>(dltp + q0 + 8 * g + 4 * hh);
+          for (int s2 = 0; s2 < HD / 2; ++s2) pd += of[s2] * ofo[s2];
+          pd += __shfl_xor(pd, 32, 64);
+          const int j = q0 + li;
+          if (hh == 0) {
+            rl[j] = j < K ? p.lse[(int64_t)pair * K + j] : INFINITY;
+            rl[FDL_KP + j] = j < K ? pd : 0.f;
+          }
+          __builtin_amdgcn_wave_barrier();
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          l4[g] = *reinterpret_cast<const f32x4*>(rl + q0 + 8 * g + 4 * hh);
+          d4[g] = *reinterpret_cast<const f32x4*>(rl + FDL_KP + q0 + 8 * g + 4 * hh);
+        }
+      } else {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          l4[g] = *reinterpret_cast<const f32x4*>(lsep + q0 + 8 * g + 4 * hh);
+          d4[g] = *reinterpret_cast<const f32x4*>(dltp + q0 + 8 * g + 4 * hh);
+        }
       }
       // dQ^T block: lane = query q0 + li, register r = dim 32c + acc_row(r, hh) (4 float4 per lane)
       const int jq = q0 + li;
@@ -1608,6 +1639,13 @@ static int g_attn_bwd_ds = [] {
   return (e && std::atoi(e) == 1) ? 1 : 2;
 }();
 
+// f32-MFMA backward at head_dim 32 with tail queries and K <= FDL_KP: row statistics formed in the kernel
+// (attn_bwd_kernel FDL, no prep launch); ONETRANS_ATTN_BWD_FDL=0 runs the prep kernel (A/B timing)
+static int g_attn_bwd_fdl = [] {
+  const char* e = std::getenv("ONETRANS_ATTN_BWD_FDL");
+  return (e && std::atoi(e) == 0) ? 0 : 1;
+}();
+
 extern "C" size_t ot_attn_bwd_workspace_size(int B, int H, int K) {
   return (2 * (size_t)B * H + B) * attn_kpad(K) * sizeof(float);     // lse, delta (+ padded qpos)
 }
@@ -1703,13 +1741,22 @@ static int attn_bwd_impl(const float* qkv, int64_t ld, const float* out, const f
   if (B == 0) return OT_OK;
   AttnArgs p{qkv, ld, H * head_dim, out, dout, nullptr, const_cast<float*>(lse), dqkv, delta_ws, B, H, I, K,
              1.f / sqrtf((float)head_dim), qpos};
+  const int mm = ot_get_matmul_mode();
+  // the f32 head_dim-32 backward over tail queries forms its own row statistics (no prep launch)
+  const bool fdl = g_attn_bwd_fdl && !qpos && head_dim == 32 && K > SMALL_K && attn_kpad(K) <= FDL_KP &&
+                   mm != OT_MATMUL_BF16;
+  if (fdl) {
+    hipLaunchKernelGGL((attn_bwd_kernel<32, false, 1, true>), dim3(ceil_div((int64_t)B * H, BWD_WAVES<32>())),
+                       dim3(64 * BWD_WAVES<32>()), 0, (hipStream_t)stream, p);
+    OT_LAUNCH_CHECK("ot_attn_bwd");
+    return OT_OK;
+  }
   const int main_blocks = (int)ceil_div((int64_t)B * K * H * head_dim / 4, 256);
   const int pad_blocks = (int)ceil_div((int64_t)B * H * (attn_kpad(K) - K), 256);
   const int qpos_blocks = qpos ? (int)ceil_div((int64_t)B * attn_kpad(K), 256) : 0;
   hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3(main_blocks + pad_blocks + qpos_blocks), dim3(256), 0,
                      (hipStream_t)stream, out, dout, lse, delta_ws, B, H, K, head_dim, main_blocks, pad_blocks, qpos);
   OT_LAUNCH_CHECK("ot_attn_bwd(prep)");
-  const int mm = ot_get_matmul_mode();
   p.dq_bf16 = (flags & OT_ATTN_DQKV_BF16) ? 1 : 0;
   if (K <= SMALL_K) {
     OT_ATTN_DISPATCH(attn_bwd_small_kernel, head_dim, dim3(ceil_div((int64_t)B * H, 4)), dim3(256), 0,

@@ -239,7 +239,10 @@ def attn_ref(qkv, B, H, I, Kq, hd):
                                          # shared-K/V forward (>= 3 query blocks, K/V fit in LDS)
                                          (2, 4, 100, 96, 32), (2, 2, 150, 150, 64), (3, 4, 130, 70, 16),
                                          # split-bf16 forward (I > 256, K/V beyond the shared-K/V LDS)
-                                         (2, 4, 300, 300, 32), (1, 2, 300, 137, 64), (1, 2, 290, 100, 128)])
+                                         (2, 4, 300, 300, 32), (1, 2, 300, 137, 64), (1, 2, 290, 100, 128),
+                                         # hd 32 tail backward with in-kernel row statistics up to K = 160
+                                         # (attn_bwd_kernel FDL), and the prep-kernel form just past it
+                                         (2, 4, 170, 160, 32), (1, 4, 170, 161, 32)])
 def test_attention(dev, B, H, I, Kq, hd):
     torch.manual_seed(0)
     d = H * hd

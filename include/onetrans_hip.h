@@ -126,6 +126,9 @@ int ot_mixed_gemm(int mode, const float* A, int64_t lda, int K, const int32_t* i
  * (model.py:11-23 RMSNorm, applied at 191/196; their tape gradients): the forward GEMM producing the
  * residual stream emits the next norm's rstd, the dgrad GEMM feeding a norm applies its backward. */
 typedef struct ot_rms_epilogue {
+  size_t struct_size;                                  /* sizeof(ot_rms_epilogue) of the caller's header: the
+                                                          library rejects any other value (OT_ERR_INVALID_ARG)
+                                                          instead of reading fields a smaller struct lacks */
   float* rstd_out; float eps;                          /* OT_EPI_ROW_RSTD */
   const float* x; int64_t ldx;                         /* OT_EPI_RMSNORM_BWD: norm input rows (out_row) */
   const float* gamma; const float* rstd;               /*   gamma[N], rstd[out_row] */
@@ -287,6 +290,10 @@ int ot_attn_bwd_dqkv_bf16_supported(int I, int K, int head_dim, int selected);
  * OT_ATTN_DQKV_BF16 alone on the short-tail kernel (K <= 4: the last layer after DCE), none otherwise */
 int ot_attn_bwd_bf16_forms(int I, int K, int head_dim, int selected);
 size_t ot_attn_bwd_flags_workspace_size(int B, int H, int I, int K, int head_dim, int selected, int flags);
+/* 1 when the f32-accurate mode (OT_MATMUL_SPLIT_BF16) runs this shape's forward and backward as one
+ * workgroup per (sample, head) slice on split-bf16 MFMA (attention_slice.hip: head_dim 32 / 64, I <= 192,
+ * tail queries for the backward, the slice's planes and dS store within LDS), else 0 */
+int ot_attn_slice_supported(int I, int K, int head_dim, int selected);
 int ot_attn_bwd_flags(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
                       int B, int H, int I, int K, const int32_t* qpos, int head_dim, void* dqkv, int flags,
                       void* workspace, size_t ws_bytes, void* stream);

@@ -33,7 +33,7 @@ MATMUL_MODES = {'f32': OT_MATMUL_F32, 'split': OT_MATMUL_SPLIT_BF16, 'bf16': OT_
 
 class RmsEpilogue(ctypes.Structure):
     """``ot_rms_epilogue`` (include/onetrans_hip.h)."""
-    _fields_ = [('rstd_out', c_void_p), ('eps', c_float),
+    _fields_ = [('struct_size', c_size_t), ('rstd_out', c_void_p), ('eps', c_float),
                 ('x', c_void_p), ('ldx', c_int64), ('gamma', c_void_p), ('rstd', c_void_p),
                 ('dres', c_void_p), ('lddres', c_int64), ('dres_tail_K', c_int), ('dres_tail_I', c_int),
                 ('dres_tail_inv', c_void_p),
@@ -85,6 +85,7 @@ SIGNATURES = {
     'ot_attn_bwd_ex': (c_int, [P, I64, P, P, P, c_int, c_int, c_int, c_int, P, c_int, P, P, c_size_t, P]),
     'ot_attn_bwd_dqkv_bf16_supported': (c_int, [c_int, c_int, c_int, c_int]),
     'ot_attn_bwd_bf16_forms': (c_int, [c_int, c_int, c_int, c_int]),
+    'ot_attn_slice_supported': (c_int, [c_int, c_int, c_int, c_int]),
     'ot_attn_bwd_flags_workspace_size': (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int, c_int]),
     'ot_attn_bwd_flags': (c_int, [P, I64, P, P, P, c_int, c_int, c_int, c_int, P, c_int, P, c_int, P, c_size_t, P]),
     'ot_attn_fwd_cached': (c_int, [P, I64, P, I64, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),

@@ -16,6 +16,7 @@
 #include <mutex>
 
 #include "common.h"
+#include "attn_slice.h"
 
 #ifndef OT_ATTN_FWD_BRANCHLOAD
 #define OT_ATTN_FWD_BRANCHLOAD 1
@@ -1596,6 +1597,10 @@ extern "C" int ot_attn_fwd(const float* qkv, int64_t ld, int B, int H, int I, in
   const size_t kv_bytes = 2 * (size_t)((I + 31) / 32 * 32) * (head_dim + 4) * sizeof(float);
   const bool kv_fits = head_dim <= 64 && kv_bytes <= OT_ATTN_KV_LDS_MAX && (K + 31) / 32 >= 3;
   const int mm = ot_get_matmul_mode();
+  if (mm == OT_MATMUL_SPLIT_BF16 && attn_slice_fwd_supported(I, K, head_dim)) {
+    // short sequence, f32-accurate: one workgroup per (sample, head) slice on split-bf16 MFMA
+    return attn_slice_fwd(qkv, ld, B, H, I, K, qpos, head_dim, out, lse, (hipStream_t)stream);
+  }
   if (head_dim >= 32 && (mm == OT_MATMUL_BF16 || (mm == OT_MATMUL_SPLIT_BF16 && !kv_fits && I > 256))) {
     // split-bf16: long sequences (I > 256), with the next key block prefetched (short ones stay on
     // the f32 kernels below, which measure faster there: profiles/r01/attention_split.md);
@@ -1687,6 +1692,11 @@ extern "C" int ot_attn_bwd_bf16_forms(int I, int K, int head_dim, int selected) 
   return 0;
 }
 
+extern "C" int ot_attn_slice_supported(int I, int K, int head_dim, int selected) {
+  return attn_slice_fwd_supported(I, K, head_dim) &&
+         (K <= SMALL_K || attn_slice_bwd_supported(I, K, head_dim, selected != 0));
+}
+
 extern "C" size_t ot_attn_bwd_flags_workspace_size(int B, int H, int I, int K, int head_dim, int selected, int flags) {
   const int S = attn_bwd_kslices(B, H, I, K, head_dim, selected != 0);
   const int slots = (flags & OT_ATTN_DQKV_BF16) ? S : S - 1;
@@ -1742,6 +1752,8 @@ static int attn_bwd_impl(const float* qkv, int64_t ld, const float* out, const f
   AttnArgs p{qkv, ld, H * head_dim, out, dout, nullptr, const_cast<float*>(lse), dqkv, delta_ws, B, H, I, K,
              1.f / sqrtf((float)head_dim), qpos};
   const int mm = ot_get_matmul_mode();
+  if (mm == OT_MATMUL_SPLIT_BF16 && flags == 0 && K > SMALL_K && attn_slice_bwd_supported(I, K, head_dim, qpos != nullptr))
+    return attn_slice_bwd(qkv, ld, out, dout, lse, B, H, I, K, head_dim, dqkv, (hipStream_t)stream);
   // the f32 head_dim-32 backward over tail queries forms its own row statistics (no prep launch)
   const bool fdl = g_attn_bwd_fdl && !qpos && head_dim == 32 && K > SMALL_K && attn_kpad(K) <= FDL_KP &&
                    mm != OT_MATMUL_BF16;

@@ -1,0 +1,26 @@
+// Short-sequence attention: one workgroup per (sample, head) slice on split-bf16 MFMA
+// (attention_slice.hip).  Dispatched from ot_attn_fwd / ot_attn_bwd (attention.hip) in the
+// f32-accurate mode (OT_MATMUL_SPLIT_BF16) when the slice fits LDS.
+#pragma once
+#include "common.h"
+
+namespace ot {
+
+struct SliceArgs {
+  const float* qkv; int64_t ld; int d;        // qkv [B*I, ld]: q at col 0, k at d, v at 2d; head h at +h*hd
+  const float* o; const float* dout; const float* lse_in;   // backward inputs: O, dO [B*K, d], lse [B*H*K]
+  float* out; float* lse;                     // forward outputs
+  float* dqkv;                                // backward output (dq on the K tail rows, dk / dv on all rows)
+  int B, H, I, K;
+  float scale;
+  const int32_t* qpos;                        // forward only: kept query positions [B*K] or null (tail)
+};
+
+bool attn_slice_fwd_supported(int I, int K, int head_dim);
+bool attn_slice_bwd_supported(int I, int K, int head_dim, bool selected);
+int attn_slice_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos, int head_dim,
+                   float* out, float* lse, hipStream_t stream);
+int attn_slice_bwd(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse, int B, int H,
+                   int I, int K, int head_dim, float* dqkv, hipStream_t stream);
+
+}  // namespace ot

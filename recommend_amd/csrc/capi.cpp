@@ -25,6 +25,6 @@ int fail(int code, const char* fmt, ...) {
 }
 }  // namespace ot
 
-extern "C" int ot_version(void) { return 10000; }   // 1.0.0
+extern "C" int ot_version(void) { return 20000; }   // 2.0.0: ot_rms_epilogue.struct_size (round 4)
 extern "C" const char* ot_get_last_error_string(void) { return ot::g_err; }
 extern "C" int ot_gemm_tile_rows(void) { return 128; }

@@ -1996,6 +1996,9 @@ extern "C" int ot_mixed_gemm_rms(int mode, const float* A, int64_t lda, int K, c
                                  uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
                                  const int32_t* tail_pos, const ot_rms_epilogue* rms, void* stream) {
   OT_REQUIRE(rms, "ot_mixed_gemm_rms: null epilogue operands");
+  OT_REQUIRE(rms->struct_size == sizeof(ot_rms_epilogue),
+             "ot_mixed_gemm_rms: ot_rms_epilogue.struct_size %zu != %zu (header of another ot_version)",
+             rms->struct_size, sizeof(ot_rms_epilogue));
   return mixed_gemm_impl(mode, A, lda, K, in_rows, a_xform, a_rstd, a_gamma, W, w_gstride, ldw, N, tile_group,
                          ntiles, bias, bias_gstride, C, ldc, out_rows, epi, res, ldres, res_tok, aux, ldaux, seed,
                          site, drop_rate, tail_K, tail_I, tail_pos, rms, nullptr, 0, 0, stream);
@@ -2013,6 +2016,9 @@ extern "C" int ot_mixed_gemm_rms_img(int mode, const float* A, int64_t lda, int 
                                      const int32_t* tail_pos, const ot_rms_epilogue* rms, const uint16_t* b_image,
                                      int image_ntn, int image_tn0, void* stream) {
   OT_REQUIRE(rms, "ot_mixed_gemm_rms: null epilogue operands");
+  OT_REQUIRE(rms->struct_size == sizeof(ot_rms_epilogue),
+             "ot_mixed_gemm_rms: ot_rms_epilogue.struct_size %zu != %zu (header of another ot_version)",
+             rms->struct_size, sizeof(ot_rms_epilogue));
   return mixed_gemm_impl(mode, A, lda, K, in_rows, a_xform, a_rstd, a_gamma, W, w_gstride, ldw, N, tile_group,
                          ntiles, bias, bias_gstride, C, ldc, out_rows, epi, res, ldres, res_tok, aux, ldaux, seed,
                          site, drop_rate, tail_K, tail_I, tail_pos, rms, b_image, image_ntn, image_tn0, stream);

@@ -236,7 +236,9 @@ def _block_forward(m, l, x, I, Kq, seed, training, rstd_in=None, select=False, n
     rstd2 = torch.empty(B * Kq, device=dev)
     x1_16 = None
     if fuse:
-        x1_16 = torch.empty(B * Kq, d, dtype=torch.int16, device=dev) if m.x16_on(d) else None
+        # the bf16 residual copy feeds FFN1 only as an OT_AX_BF16_RMSNORM operand, which needs W1's plane image
+        x1_16 = (torch.empty(B * Kq, d, dtype=torch.int16, device=dev)
+                 if m.x16_on(d) and m.bimg(f'blk.{l}.w1') is not None else None)
         K.gemm_rms(OT_GEMM_NT, o, d, d, mt['rows'][1], wo, 0, d, d, mt['tile_group'], nt, x1, d, mt['rows'][1],
                    epi=OT_EPI_RESIDUAL | dflag | OT_EPI_ROW_RSTD, res=x, ldres=d, res_tok=1, seed=seed,
                    site=2 * l, drop=rate, tail=tail, m_rows=maps['tail'].nrows, rstd_out=rstd2, eps=RMS_EPS,
@@ -252,7 +254,8 @@ def _block_forward(m, l, x, I, Kq, seed, training, rstd_in=None, select=False, n
     # once per output column tile), and the W2 weight gradient reuses h
     w2img = m.bimg(f'blk.{l}.w2')
     h = (torch.empty(B * Kq, f, dtype=torch.int16, device=dev)
-         if m.store_gelu_fwd and K.matmul_mode() == 'bf16' and w2img is not None and f % 8 == 0 else None)
+         if m.store_gelu_fwd and K.matmul_mode() == 'bf16' and w2img is not None
+         and m.bimg(f'blk.{l}.w1') is not None and f % TILE == 0 else None)
     # ... and u itself in bf16 (as a bf16 Keras policy stores it): its one reader is then the FFN2 dgrad's
     # GELU' / row-dot epilogue (OT_EPI_AUX_BF16), which needs the fused norm2 backward's bf16-dU form
     u_bf = h is not None and m.u_bf16 and m.du_bf16 and m.fuse_bwd2 and not m.fuse_bwd and f % TILE == 0

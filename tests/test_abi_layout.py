@@ -34,7 +34,7 @@ def test_library_exports_every_symbol():
     lib = _lib.load()
     for s in _lib.header_symbols():
         assert hasattr(lib, s), s
-    assert lib.ot_version() == 10000
+    assert lib.ot_version() == 20000
     assert lib.ot_gemm_tile_rows() == TILE
     # workspace-size queries are host-only (no GPU needed)
     assert lib.ot_wgrad_workspace_size(3, 128, 64) == (3 * 128 * 64 + 3 * 64) * 4
@@ -49,6 +49,13 @@ def test_errors_are_reported_not_crashing():
     with pytest.raises(_lib.OneTransHipError, match='multiples of 4'):
         _lib.call('ot_mixed_gemm', 0, 8, 3, 3, None, 0, None, None, 8, 0, 4, 4, None, 1, None, 0, 8, 4, None, 0,
                   None, 0, 0, None, 0, 0, 0, 0.0, 1, 1, None, None)
+    # an ot_rms_epilogue from another header version (struct_size differs) is refused, not read past its end
+    import ctypes
+    e = _lib.RmsEpilogue()
+    e.struct_size = ctypes.sizeof(_lib.RmsEpilogue) - 24
+    with pytest.raises(_lib.OneTransHipError, match='struct_size'):
+        _lib.call('ot_mixed_gemm_rms', 0, None, 128, 128, None, 0, None, None, None, 0, 128, 128, None, 1, None, 0,
+                  None, 128, None, 0, None, 0, 0, None, 0, 0, 0, 0.0, 1, 1, None, ctypes.byref(e), None)
     with pytest.raises(_lib.OneTransHipError, match='bad sizes'):
         _lib.call('ot_pyramid_select', None, 1.0, 2, 8, 9, 0, 8, None, None, 0, None)    # K > I
     with pytest.raises(_lib.OneTransHipError, match='bad sizes'):

@@ -246,6 +246,38 @@ def test_bf16_mode_forward_and_train(dev, dtype):
         K.set_matmul_mode(old)
 
 
+@pytest.mark.parametrize('d,f', [(128, 320), (256, 320)])
+def test_bf16_mode_ffn_width_without_plane_image(dev, d, f):
+    """bf16 mode with an FFN width that is not a multiple of the 128-column tile: W1 has no plane image,
+    so FFN1 must take the f32 residual x1 (not its bf16 copy) and no stored GELU: the forward
+    within the bf16 tolerance of the f64 oracle and every gradient finite and within 3e-2 of it."""
+    from recommend_amd import kernels as K
+    cfg = small_criteo('head', layers=2, d=d, H=4, f=f, Lns=4, seq_lens=(12, 9, 7))
+    cfg.compute_dtype = 'bf16'
+    old = K.set_matmul_mode('bf16')
+    try:
+        P, model, batch = setup(cfg, 37, dev)
+        assert model.bimg('blk.0.w1') is None
+        ns, seq, lab = batch
+        probs = model.forward_probs(ns_t(ns, dev), ns_t(seq, dev), training=True)
+        seed = (model.dropout_seed + 0x9E3779B9 * model._step) & 0xFFFFFFFF
+        loss = keras_bce_loss(stack_labels(lab, cfg.tasks, dev), probs, cfg.tasks)
+        loss.backward()
+        rl, rg, _ = R.loss_and_grads(R.to_torch(P), cfg, R.to_torch(ns), R.to_torch(seq), R.to_torch(lab),
+                                     training=True, seed=seed)
+        assert abs(loss.item() - rl.item()) < 2e-2
+        for name in model.layout.shapes:
+            g = model.g(name).double().cpu()
+            r = rg[name]
+            if name == 'tok.ns.kernel':
+                g = g[:r.shape[0]]
+            assert torch.isfinite(g).all(), name
+            scale = max(1e-3, r.abs().max().item())
+            assert (g.reshape(r.shape) - r).abs().max().item() / scale < 3e-2, name
+    finally:
+        K.set_matmul_mode(old)
+
+
 @pytest.mark.parametrize('case', ['criteo_d128_pyramid', 'criteo_norm_pyramid', 'criteo_d256_pyramid'])
 def test_recompute_matches_saved(dev, case):
     """Activation recompute (config.recompute_blocks): the backward re-runs each block's forward kernels

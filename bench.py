@@ -103,8 +103,7 @@ def cpu_baseline(cfg_name, seconds):
     from recommend_amd.data import make_batch
     from recommend_amd.params import init_params, keras_variables
     from oracle import onetrans_ref as R
-    cores = len(os.sched_getaffinity(0))
-    cores = min(cores, 64)
+    cores = len(os.sched_getaffinity(0))          # the node's host cores this process may run on
     torch.set_num_threads(cores)
     cfg = workload_config(cfg_name)
     # the oracle's table gradient is dense: cap table cardinalities (transformer work is unchanged)
@@ -131,8 +130,14 @@ def cpu_baseline(cfg_name, seconds):
         rates[variant] = (B * n / el, n, el)
     best = max(rates, key=lambda v: rates[v][0])
     v, n, el = rates[best]
-    return {'value': round(v, 2), 'unit': 'samples/s', 'cores': torch.get_num_threads(),
-            'kind': 'port', 'variant': best,
+    quota = None                                   # cgroup CPU quota (cores' worth), when the container sets one
+    try:
+        q, per = open('/sys/fs/cgroup/cpu.max').read().split()[:2]
+        quota = None if q == 'max' else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return {'value': round(v, 2), 'unit': 'samples/s', 'cores': torch.get_num_threads(), 'affinity_cores': cores,
+            'cgroup_cpu_quota_cores': quota, 'kind': 'port', 'variant': best,
             'variants': {k: round(r[0], 2) for k, r in rates.items()},
             'sample': f'{n} train steps x B={B} of {cfg_name} (full model shape, fp32, {best} oracle '
                       f'restatement of model.py/train.py, the faster of literal/vectorized; tables capped '

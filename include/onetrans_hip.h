@@ -96,7 +96,8 @@ const char* ot_get_last_error_string(void);
  * (tape.gradient, train.py:131).  Tiles are 128 rows (ot_gemm_tile_rows()); tile i multiplies the
  * rows in_rows[128 i .. 128 i + 127] by W + tile_group[i] * w_gstride. */
 int ot_gemm_tile_rows(void);
-/* Matmul arithmetic of the GEMM family (process-wide; set before launching).
+/* Matmul arithmetic: the `precision` argument of every GEMM, weight-gradient, plane-image and attention
+ * entry point (per call: no process-wide state, so models of different precision share the library).
  *   OT_MATMUL_SPLIT_BF16 (default): every f32 operand is split exactly into three bf16 parts
  *     (x = x0 + x1 + x2, 8 significant bits each) and the product is sum_ij ai.bj over the six
  *     largest terms on v_mfma_f32_32x32x16_bf16 (each part product exact in the f32 accumulator;
@@ -110,8 +111,6 @@ int ot_gemm_tile_rows(void);
 #define OT_MATMUL_F32 0
 #define OT_MATMUL_SPLIT_BF16 1
 #define OT_MATMUL_BF16 2
-int ot_set_matmul_mode(int mode);
-int ot_get_matmul_mode(void);
 int ot_mixed_gemm(int mode, const float* A, int64_t lda, int K, const int32_t* in_rows,
                   int a_xform, const float* a_rstd, const float* a_gamma,
                   const float* W, int64_t w_gstride, int64_t ldw, int N,
@@ -121,7 +120,7 @@ int ot_mixed_gemm(int mode, const float* A, int64_t lda, int K, const int32_t* i
                   const float* res, int64_t ldres, int res_tok,
                   const float* aux, int64_t ldaux,
                   uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
-                  const int32_t* tail_pos, void* stream);
+                  const int32_t* tail_pos, int precision, void* stream);
 /* Row-norm epilogue operands for ot_mixed_gemm_rms.  Replaces the RMSNorm layers around the GEMMs
  * (model.py:11-23 RMSNorm, applied at 191/196; their tape gradients): the forward GEMM producing the
  * residual stream emits the next norm's rstd, the dgrad GEMM feeding a norm applies its backward. */
@@ -167,7 +166,7 @@ int ot_mixed_gemm_rms(int mode, const float* A, int64_t lda, int K, const int32_
                       const float* res, int64_t ldres, int res_tok,
                       const float* aux, int64_t ldaux,
                       uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
-                      const int32_t* tail_pos, const ot_rms_epilogue* rms, void* stream);
+                      const int32_t* tail_pos, const ot_rms_epilogue* rms, int precision, void* stream);
 
 /* dW[g] (+)= sum pro(A[a_rows])^T D[d_rows], db[g] (+)= sum D[d_rows] over the rows of every
  * chunk of group g.  chunks: [nchunks][3] {group, row_begin, row_count} indexing the row maps;
@@ -179,7 +178,7 @@ int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a_rows, int 
                         const float* D, int64_t ldd, const int32_t* d_rows, int K, int N,
                         const int32_t* chunks, int nchunks, const int32_t* gchunk, int ngroups,
                         float* dW, int64_t dw_gstride, float* db, int64_t db_gstride,
-                        int accumulate, void* workspace, size_t ws_bytes, void* stream);
+                        int accumulate, void* workspace, size_t ws_bytes, int precision, void* stream);
 
 /* Transposed weight shadow for the forward GEMMs (NT staging reads k-contiguous rows):
  * dst[g][n][k] = src[g][k][n] per bank; banks_dev: [nbanks][6] int64 {src_off, dst_off, G, K, N,
@@ -196,7 +195,7 @@ int ot_transpose_banks(const float* src, float* dst, const int64_t* banks_dev, i
  * G*ceil(N/128)*(K/16) consecutive units of the launch; ot_split_image_elems gives its size. */
 size_t ot_split_image_elems(int G, int N, int K);
 int ot_split_images(const float* base, const int64_t* desc_dev, int ndesc, int64_t total_units, uint16_t* img,
-                    void* stream);
+                    int precision, void* stream);
 /* ot_mixed_gemm / ot_mixed_gemm_rms with the B operand's pre-split image (b_image: the bank's image,
  * image_ntn column tiles per group, the GEMM's columns starting at tile image_tn0).  In split mode,
  * NT, whole tiles and 16-B aligned A rows the plane GEMM runs (B by global_load_lds from the image,
@@ -212,7 +211,7 @@ int ot_mixed_gemm_img(int mode, const float* A, int64_t lda, int K, const int32_
                       const float* aux, int64_t ldaux,
                       uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
                       const int32_t* tail_pos, const uint16_t* b_image, int image_ntn, int image_tn0,
-                      void* stream);
+                      int precision, void* stream);
 int ot_mixed_gemm_rms_img(int mode, const float* A, int64_t lda, int K, const int32_t* in_rows,
                           int a_xform, const float* a_rstd, const float* a_gamma,
                           const float* W, int64_t w_gstride, int64_t ldw, int N,
@@ -223,7 +222,7 @@ int ot_mixed_gemm_rms_img(int mode, const float* A, int64_t lda, int K, const in
                           const float* aux, int64_t ldaux,
                           uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
                           const int32_t* tail_pos, const ot_rms_epilogue* rms, const uint16_t* b_image,
-                          int image_ntn, int image_tn0, void* stream);
+                          int image_ntn, int image_tn0, int precision, void* stream);
 
 /* ---- causal attention with a query tail (attention.hip) ----------------------------------
  * Replaces model.py:100-114 (einsum QK^T/sqrt(hd), band_part mask with -1e9, softmax, einsum PV)
@@ -232,7 +231,7 @@ int ot_mixed_gemm_rms_img(int mode, const float* A, int64_t lda, int K, const in
  * qpos: NULL (query j of a sample sits at position I - K + j) or the ascending kept positions
  * [B*K] of ot_pyramid_select (query j at qpos[b*K + j], causal limit key <= qpos). */
 int ot_attn_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos,
-                int head_dim, float* out, float* lse, void* stream);
+                int head_dim, float* out, float* lse, int precision, void* stream);
 /* The same forward on block-scaled fp8 MFMA (attention_fp8.hip; BASELINE configs[4] "CDNA4 fp8 MFMA
  * attention"): K and Q quantised to OCP e4m3 with one e8m0 scale per (row, 32 dims), V with one scale
  * per (dim, 64 keys), P = exp(s - m) as e4m3 of P * 2^8; v_mfma_scale_f32_32x32x64_f8f6f4 for QK^T and
@@ -264,15 +263,15 @@ int ot_attn_fwd_fp8_deq16(const float* qkv, int64_t ld, int B, int H, int I, int
 size_t ot_attn_bwd_workspace_size(int B, int H, int K);
 int ot_attn_bwd(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
                 int B, int H, int I, int K, const int32_t* qpos, int head_dim, float* dqkv, float* delta_ws,
-                void* stream);
+                int precision, void* stream);
 /* ot_attn_bwd with a sized workspace: given ot_attn_bwd_ex_workspace_size(B, H, I, K, head_dim,
- * qpos != NULL) bytes, the bf16-mode backward splits each (sample, head)'s key blocks over several
+ * qpos != NULL, precision) bytes, the bf16-mode backward splits each (sample, head)'s key blocks over several
  * waves when B*H alone cannot fill the chip (C5: 4 slices), their dQ partials summed in a fixed
  * order (deterministic); with ot_attn_bwd_workspace_size bytes it runs as ot_attn_bwd. */
-size_t ot_attn_bwd_ex_workspace_size(int B, int H, int I, int K, int head_dim, int selected);
+size_t ot_attn_bwd_ex_workspace_size(int B, int H, int I, int K, int head_dim, int selected, int precision);
 int ot_attn_bwd_ex(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
                    int B, int H, int I, int K, const int32_t* qpos, int head_dim, float* dqkv, void* workspace,
-                   size_t ws_bytes, void* stream);
+                   size_t ws_bytes, int precision, void* stream);
 /* ot_attn_bwd_ex with output flags.  OT_ATTN_DQKV_BF16: dqkv holds bf16 (uint16 bits, ld in elements,
  * 8-B aligned) — the bf16 mode's consumers (the QKV dgrad's A operand, the Wqkv weight gradient's D) round
  * it to bf16 anyway, so the values they use are unchanged (each element is the f32 result rounded once).
@@ -285,18 +284,18 @@ int ot_attn_bwd_ex(const float* qkv, int64_t ld, const float* out, const float* 
 /* OT_ATTN_DQ_PART_BF16 (with OT_ATTN_DQKV_BF16): the key slices' dQ partials are kept in bf16 (summed in f32,
  * then rounded: not the f32 sum rounded once — about one more bf16 rounding of each partial) */
 #define OT_ATTN_DQ_PART_BF16 4
-int ot_attn_bwd_dqkv_bf16_supported(int I, int K, int head_dim, int selected);
+int ot_attn_bwd_dqkv_bf16_supported(int I, int K, int head_dim, int selected, int precision);
 /* the OT_ATTN_*_BF16 flags the backward supports at this shape: all three on the key-grouped bf16 backward,
  * OT_ATTN_DQKV_BF16 alone on the short-tail kernel (K <= 4: the last layer after DCE), none otherwise */
-int ot_attn_bwd_bf16_forms(int I, int K, int head_dim, int selected);
-size_t ot_attn_bwd_flags_workspace_size(int B, int H, int I, int K, int head_dim, int selected, int flags);
+int ot_attn_bwd_bf16_forms(int I, int K, int head_dim, int selected, int precision);
+size_t ot_attn_bwd_flags_workspace_size(int B, int H, int I, int K, int head_dim, int selected, int flags, int precision);
 /* 1 when the f32-accurate mode (OT_MATMUL_SPLIT_BF16) runs this shape's forward and backward as one
  * workgroup per (sample, head) slice on split-bf16 MFMA (attention_slice.hip: head_dim 32 / 64, I <= 192,
  * tail queries for the backward, the slice's planes and dS store within LDS), else 0 */
 int ot_attn_slice_supported(int I, int K, int head_dim, int selected);
 int ot_attn_bwd_flags(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
                       int B, int H, int I, int K, const int32_t* qpos, int head_dim, void* dqkv, int flags,
-                      void* workspace, size_t ws_bytes, void* stream);
+                      void* workspace, size_t ws_bytes, int precision, void* stream);
 
 /* Two-stage cached serving (paper §3.5.1; replaces the reference's defective cache path
  * model.py:94-98, 359-381, D6): candidate c (request req[c]) attends with the last Kq of its n

@@ -53,41 +53,39 @@ SIGNATURES = {
     'ot_version': (c_int, []),
     'ot_get_last_error_string': (c_char_p, []),
     'ot_gemm_tile_rows': (c_int, []),
-    'ot_set_matmul_mode': (c_int, [c_int]),
-    'ot_get_matmul_mode': (c_int, []),
     'ot_mixed_gemm': (c_int, [c_int, P, I64, c_int, P, c_int, P, P, P, I64, I64, c_int, P, c_int, P, I64,
                               P, I64, P, c_int, P, I64, c_int, P, I64, c_uint32, c_uint32, c_float, c_int,
-                              c_int, P, P]),
+                              c_int, P, c_int, P]),
     'ot_mixed_gemm_rms_workspace_size': (c_size_t, [c_int, c_int]),
     'ot_mixed_gemm_rms': (c_int, [c_int, P, I64, c_int, P, c_int, P, P, P, I64, I64, c_int, P, c_int, P, I64,
                                   P, I64, P, c_int, P, I64, c_int, P, I64, c_uint32, c_uint32, c_float, c_int,
-                                  c_int, P, P, P]),
+                                  c_int, P, P, c_int, P]),
     'ot_wgrad_workspace_size': (c_size_t, [c_int, c_int, c_int]),
     'ot_mixed_gemm_wgrad': (c_int, [P, I64, P, c_int, P, P, P, I64, P, c_int, c_int, P, c_int, P, c_int, P,
-                                    I64, P, I64, c_int, P, c_size_t, P]),
+                                    I64, P, I64, c_int, P, c_size_t, c_int, P]),
     'ot_transpose_banks': (c_int, [P, P, P, c_int, I64, P]),
     'ot_mixed_gemm_img': (c_int, [c_int, P, I64, c_int, P, c_int, P, P, P, I64, I64, c_int, P, c_int, P, I64,
                                   P, I64, P, c_int, P, I64, c_int, P, I64, c_uint32, c_uint32, c_float, c_int,
-                                  c_int, P, P, c_int, c_int, P]),
+                                  c_int, P, P, c_int, c_int, c_int, P]),
     'ot_mixed_gemm_rms_img': (c_int, [c_int, P, I64, c_int, P, c_int, P, P, P, I64, I64, c_int, P, c_int, P, I64,
                                       P, I64, P, c_int, P, I64, c_int, P, I64, c_uint32, c_uint32, c_float, c_int,
-                                      c_int, P, P, P, c_int, c_int, P]),
+                                      c_int, P, P, P, c_int, c_int, c_int, P]),
     'ot_split_image_elems': (c_size_t, [c_int, c_int, c_int]),
-    'ot_split_images': (c_int, [P, P, c_int, I64, P, P]),
-    'ot_attn_fwd': (c_int, [P, I64, c_int, c_int, c_int, c_int, P, c_int, P, P, P]),
+    'ot_split_images': (c_int, [P, P, c_int, I64, P, c_int, P]),
+    'ot_attn_fwd': (c_int, [P, I64, c_int, c_int, c_int, c_int, P, c_int, P, P, c_int, P]),
     'ot_attn_fwd_fp8_workspace_size': (c_size_t, [c_int, c_int, c_int, c_int]),
     'ot_attn_fwd_fp8': (c_int, [P, I64, c_int, c_int, c_int, c_int, P, c_int, P, P, P, c_size_t, P]),
     'ot_attn_fwd_fp8_ex': (c_int, [P, I64, c_int, c_int, c_int, c_int, P, c_int, P, P, P, c_size_t, c_int, P]),
     'ot_attn_fwd_fp8_deq16': (c_int, [P, I64, c_int, c_int, c_int, c_int, P, c_int, P, P, P, c_size_t, c_int, P, P]),
     'ot_attn_bwd_workspace_size': (c_size_t, [c_int, c_int, c_int]),
-    'ot_attn_bwd': (c_int, [P, I64, P, P, P, c_int, c_int, c_int, c_int, P, c_int, P, P, P]),
-    'ot_attn_bwd_ex_workspace_size': (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
-    'ot_attn_bwd_ex': (c_int, [P, I64, P, P, P, c_int, c_int, c_int, c_int, P, c_int, P, P, c_size_t, P]),
-    'ot_attn_bwd_dqkv_bf16_supported': (c_int, [c_int, c_int, c_int, c_int]),
-    'ot_attn_bwd_bf16_forms': (c_int, [c_int, c_int, c_int, c_int]),
+    'ot_attn_bwd': (c_int, [P, I64, P, P, P, c_int, c_int, c_int, c_int, P, c_int, P, P, c_int, P]),
+    'ot_attn_bwd_ex_workspace_size': (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int, c_int]),
+    'ot_attn_bwd_ex': (c_int, [P, I64, P, P, P, c_int, c_int, c_int, c_int, P, c_int, P, P, c_size_t, c_int, P]),
+    'ot_attn_bwd_dqkv_bf16_supported': (c_int, [c_int, c_int, c_int, c_int, c_int]),
+    'ot_attn_bwd_bf16_forms': (c_int, [c_int, c_int, c_int, c_int, c_int]),
     'ot_attn_slice_supported': (c_int, [c_int, c_int, c_int, c_int]),
-    'ot_attn_bwd_flags_workspace_size': (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int, c_int]),
-    'ot_attn_bwd_flags': (c_int, [P, I64, P, P, P, c_int, c_int, c_int, c_int, P, c_int, P, c_int, P, c_size_t, P]),
+    'ot_attn_bwd_flags_workspace_size': (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int]),
+    'ot_attn_bwd_flags': (c_int, [P, I64, P, P, P, c_int, c_int, c_int, c_int, P, c_int, P, c_int, P, c_size_t, c_int, P]),
     'ot_attn_fwd_cached': (c_int, [P, I64, P, I64, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
     'ot_pyramid_select': (c_int, [P, c_float, c_int, c_int, c_int, c_int, P, P, P, c_int, P]),
     'ot_rmsnorm_fwd': (c_int, [P, I64, P, P, I64, P, I64, c_int, c_float, P]),
@@ -159,12 +157,6 @@ def load():
         fn.restype = res
         fn.argtypes = args
     _lib = lib
-    # GEMM arithmetic (include/onetrans_hip.h ot_set_matmul_mode): ONETRANS_MATMUL=split (default,
-    # exact 3-way bf16 split, f32-accurate) or f32 (native f32 MFMA)
-    mode = os.environ.get('ONETRANS_MATMUL', 'split')
-    if mode not in MATMUL_MODES:
-        raise OneTransHipError(f'ONETRANS_MATMUL={mode!r}: expected one of {sorted(MATMUL_MODES)}')
-    call('ot_set_matmul_mode', MATMUL_MODES[mode])
     return lib
 
 

@@ -1587,7 +1587,9 @@ extern "C" int ot_attn_fwd_cached(const float* qkv, int64_t ld, const float* kv_
 
 
 extern "C" int ot_attn_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos,
-                           int head_dim, float* out, float* lse, void* stream) {
+                           int head_dim, float* out, float* lse, int precision, void* stream) {
+  OT_REQUIRE(precision == OT_MATMUL_F32 || precision == OT_MATMUL_SPLIT_BF16 || precision == OT_MATMUL_BF16,
+             "ot_attn_fwd: unknown precision %d", precision);
   OT_REQUIRE(qkv && out && lse, "ot_attn_fwd: null operand");
   OT_REQUIRE(B >= 0 && H > 0 && I > 0 && K > 0 && K <= I, "ot_attn_fwd: bad sizes B=%d H=%d I=%d K=%d", B, H, I, K);
   OT_REQUIRE(ld % 4 == 0 && ld >= 3 * H * head_dim, "ot_attn_fwd: ld must be >= 3d and a multiple of 4");
@@ -1596,7 +1598,7 @@ extern "C" int ot_attn_fwd(const float* qkv, int64_t ld, int B, int H, int I, in
              1.f / sqrtf((float)head_dim), qpos};
   const size_t kv_bytes = 2 * (size_t)((I + 31) / 32 * 32) * (head_dim + 4) * sizeof(float);
   const bool kv_fits = head_dim <= 64 && kv_bytes <= OT_ATTN_KV_LDS_MAX && (K + 31) / 32 >= 3;
-  const int mm = ot_get_matmul_mode();
+  const int mm = precision;
   if (mm == OT_MATMUL_SPLIT_BF16 && attn_slice_fwd_supported(I, K, head_dim)) {
     // short sequence, f32-accurate: one workgroup per (sample, head) slice on split-bf16 MFMA
     return attn_slice_fwd(qkv, ld, B, H, I, K, qpos, head_dim, out, lse, (hipStream_t)stream);
@@ -1637,20 +1639,6 @@ extern "C" int ot_attn_fwd(const float* qkv, int64_t ld, int B, int H, int I, in
   return OT_OK;
 }
 
-// f32-MFMA backward at head_dim 64: 2 = the head split over two waves (default), 1 = one wave per
-// (sample, head) (ONETRANS_ATTN_BWD_DS=1, for A/B timing)
-static int g_attn_bwd_ds = [] {
-  const char* e = std::getenv("ONETRANS_ATTN_BWD_DS");
-  return (e && std::atoi(e) == 1) ? 1 : 2;
-}();
-
-// f32-MFMA backward at head_dim 32 with tail queries and K <= FDL_KP: row statistics formed in the kernel
-// (attn_bwd_kernel FDL, no prep launch); ONETRANS_ATTN_BWD_FDL=0 runs the prep kernel (A/B timing)
-static int g_attn_bwd_fdl = [] {
-  const char* e = std::getenv("ONETRANS_ATTN_BWD_FDL");
-  return (e && std::atoi(e) == 0) ? 0 : 1;
-}();
-
 extern "C" size_t ot_attn_bwd_workspace_size(int B, int H, int K) {
   return (2 * (size_t)B * H + B) * attn_kpad(K) * sizeof(float);     // lse, delta (+ padded qpos)
 }
@@ -1666,27 +1654,28 @@ static int g_attn_bwd_group_min_kb = [] {       // key blocks from which the gro
   const char* e = getenv("ONETRANS_ATTN_BWD_GROUP_MIN_KB");
   return e ? atoi(e) : 9;
 }();
-static int attn_bwd_kgroup(int I, int K, int head_dim, bool sel) {
-  if (sel || K <= SMALL_K || ot_get_matmul_mode() != OT_MATMUL_BF16 || (head_dim != 32 && head_dim != 64)) return 0;
+static int attn_bwd_kgroup(int I, int K, int head_dim, bool sel, int prec) {
+  if (sel || K <= SMALL_K || prec != OT_MATMUL_BF16 || (head_dim != 32 && head_dim != 64)) return 0;
   if ((I + 31) / 32 < g_attn_bwd_group_min_kb || (g_attn_bwd_group != 4 && g_attn_bwd_group != 8)) return 0;
   return g_attn_bwd_group;
 }
-static int attn_bwd_kslices(int B, int H, int I, int K, int head_dim, bool sel) {
-  const int g = attn_bwd_kgroup(I, K, head_dim, sel);
+static int attn_bwd_kslices(int B, int H, int I, int K, int head_dim, bool sel, int prec) {
+  const int g = attn_bwd_kgroup(I, K, head_dim, sel, prec);
   return g ? ((I + 31) / 32 + g - 1) / g : 1;
 }
 
-extern "C" size_t ot_attn_bwd_ex_workspace_size(int B, int H, int I, int K, int head_dim, int selected) {
-  const int S = attn_bwd_kslices(B, H, I, K, head_dim, selected != 0);
+extern "C" size_t ot_attn_bwd_ex_workspace_size(int B, int H, int I, int K, int head_dim, int selected,
+                                                int precision) {
+  const int S = attn_bwd_kslices(B, H, I, K, head_dim, selected != 0, precision);
   return ot_attn_bwd_workspace_size(B, H, K) + (size_t)(S - 1) * B * K * H * head_dim * sizeof(float);
 }
 
-extern "C" int ot_attn_bwd_dqkv_bf16_supported(int I, int K, int head_dim, int selected) {
-  return attn_bwd_kgroup(I, K, head_dim, selected != 0) != 0;
+extern "C" int ot_attn_bwd_dqkv_bf16_supported(int I, int K, int head_dim, int selected, int precision) {
+  return attn_bwd_kgroup(I, K, head_dim, selected != 0, precision) != 0;
 }
 
-extern "C" int ot_attn_bwd_bf16_forms(int I, int K, int head_dim, int selected) {
-  if (attn_bwd_kgroup(I, K, head_dim, selected != 0))
+extern "C" int ot_attn_bwd_bf16_forms(int I, int K, int head_dim, int selected, int precision) {
+  if (attn_bwd_kgroup(I, K, head_dim, selected != 0, precision))
     return OT_ATTN_DQKV_BF16 | OT_ATTN_QKV_BF16 | OT_ATTN_DQ_PART_BF16;
   if (K > 0 && K <= SMALL_K && (head_dim == 32 || head_dim == 64 || head_dim == 128)) return OT_ATTN_DQKV_BF16;
   return 0;
@@ -1697,65 +1686,69 @@ extern "C" int ot_attn_slice_supported(int I, int K, int head_dim, int selected)
          (K <= SMALL_K || attn_slice_bwd_supported(I, K, head_dim, selected != 0));
 }
 
-extern "C" size_t ot_attn_bwd_flags_workspace_size(int B, int H, int I, int K, int head_dim, int selected, int flags) {
-  const int S = attn_bwd_kslices(B, H, I, K, head_dim, selected != 0);
+extern "C" size_t ot_attn_bwd_flags_workspace_size(int B, int H, int I, int K, int head_dim, int selected, int flags,
+                                                   int precision) {
+  const int S = attn_bwd_kslices(B, H, I, K, head_dim, selected != 0, precision);
   const int slots = (flags & OT_ATTN_DQKV_BF16) ? S : S - 1;
   return ot_attn_bwd_workspace_size(B, H, K) + (size_t)slots * B * K * H * head_dim * sizeof(float);
 }
 
 static int attn_bwd_impl(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
                          int B, int H, int I, int K, const int32_t* qpos, int head_dim, float* dqkv,
-                         float* delta_ws, size_t ws_bytes, void* stream, int flags = 0);
+                         float* delta_ws, size_t ws_bytes, int prec, void* stream, int flags = 0);
 
 extern "C" int ot_attn_bwd(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
                            int B, int H, int I, int K, const int32_t* qpos, int head_dim, float* dqkv,
-                           float* delta_ws, void* stream) {
+                           float* delta_ws, int precision, void* stream) {
   return attn_bwd_impl(qkv, ld, out, dout, lse, B, H, I, K, qpos, head_dim, dqkv, delta_ws,
-                       ot_attn_bwd_workspace_size(B, H, K), stream);
+                       ot_attn_bwd_workspace_size(B, H, K), precision, stream);
 }
 
 extern "C" int ot_attn_bwd_ex(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
                               int B, int H, int I, int K, const int32_t* qpos, int head_dim, float* dqkv,
-                              void* workspace, size_t ws_bytes, void* stream) {
+                              void* workspace, size_t ws_bytes, int precision, void* stream) {
   OT_REQUIRE(ws_bytes >= ot_attn_bwd_workspace_size(B, H, K), "ot_attn_bwd_ex: workspace too small");
   return attn_bwd_impl(qkv, ld, out, dout, lse, B, H, I, K, qpos, head_dim, dqkv, (float*)workspace, ws_bytes,
-                       stream);
+                       precision, stream);
 }
 
 extern "C" int ot_attn_bwd_flags(const float* qkv, int64_t ld, const float* out, const float* dout,
                                  const float* lse, int B, int H, int I, int K, const int32_t* qpos, int head_dim,
-                                 void* dqkv, int flags, void* workspace, size_t ws_bytes, void* stream) {
+                                 void* dqkv, int flags, void* workspace, size_t ws_bytes, int precision,
+                                 void* stream) {
   OT_REQUIRE(!(flags & ~(OT_ATTN_DQKV_BF16 | OT_ATTN_QKV_BF16 | OT_ATTN_DQ_PART_BF16)),
              "ot_attn_bwd_flags: unknown flags %d", flags);
   OT_REQUIRE(!(flags & OT_ATTN_DQ_PART_BF16) || (flags & OT_ATTN_DQKV_BF16),
              "ot_attn_bwd_flags: OT_ATTN_DQ_PART_BF16 goes with OT_ATTN_DQKV_BF16");
-  OT_REQUIRE((flags & ot_attn_bwd_bf16_forms(I, K, head_dim, qpos != nullptr)) == flags,
+  OT_REQUIRE((flags & ot_attn_bwd_bf16_forms(I, K, head_dim, qpos != nullptr, precision)) == flags,
              "ot_attn_bwd_flags: flags %d not supported at I %d K %d head_dim %d (ot_attn_bwd_bf16_forms)", flags, I,
              K, head_dim);
-  OT_REQUIRE(!(flags & OT_ATTN_QKV_BF16) || (ot_attn_bwd_dqkv_bf16_supported(I, K, head_dim, qpos != nullptr) &&
+  OT_REQUIRE(!(flags & OT_ATTN_QKV_BF16) || (ot_attn_bwd_dqkv_bf16_supported(I, K, head_dim, qpos != nullptr, precision) &&
                                              ((uintptr_t)qkv % 16) == 0 && ld % 8 == 0),
              "ot_attn_bwd_flags: OT_ATTN_QKV_BF16 needs the key-grouped bf16 backward, 16-B aligned qkv, ld %% 8 == 0");
-  OT_REQUIRE(ws_bytes >= ot_attn_bwd_flags_workspace_size(B, H, I, K, head_dim, qpos != nullptr, flags),
+  OT_REQUIRE(ws_bytes >= ot_attn_bwd_flags_workspace_size(B, H, I, K, head_dim, qpos != nullptr, flags, precision),
              "ot_attn_bwd_flags: workspace too small");
   OT_REQUIRE(!(flags & OT_ATTN_DQKV_BF16) || ((uintptr_t)dqkv % 8) == 0, "ot_attn_bwd_flags: dqkv alignment");
   return attn_bwd_impl(qkv, ld, out, dout, lse, B, H, I, K, qpos, head_dim, (float*)dqkv, (float*)workspace,
-                       ws_bytes, stream, flags);
+                       ws_bytes, precision, stream, flags);
 }
 
 static int attn_bwd_impl(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
                          int B, int H, int I, int K, const int32_t* qpos, int head_dim, float* dqkv,
-                         float* delta_ws, size_t ws_bytes, void* stream, int flags) {
+                         float* delta_ws, size_t ws_bytes, int prec, void* stream, int flags) {
+  OT_REQUIRE(prec == OT_MATMUL_F32 || prec == OT_MATMUL_SPLIT_BF16 || prec == OT_MATMUL_BF16,
+             "ot_attn_bwd: unknown precision %d", prec);
   OT_REQUIRE(qkv && out && dout && lse && dqkv && delta_ws, "ot_attn_bwd: null operand");
   OT_REQUIRE(B >= 0 && H > 0 && I > 0 && K > 0 && K <= I, "ot_attn_bwd: bad sizes");
   OT_REQUIRE(ld % 4 == 0 && ld >= 3 * H * head_dim, "ot_attn_bwd: bad ld");
   if (B == 0) return OT_OK;
   AttnArgs p{qkv, ld, H * head_dim, out, dout, nullptr, const_cast<float*>(lse), dqkv, delta_ws, B, H, I, K,
              1.f / sqrtf((float)head_dim), qpos};
-  const int mm = ot_get_matmul_mode();
+  const int mm = prec;
   if (mm == OT_MATMUL_SPLIT_BF16 && flags == 0 && K > SMALL_K && attn_slice_bwd_supported(I, K, head_dim, qpos != nullptr))
     return attn_slice_bwd(qkv, ld, out, dout, lse, B, H, I, K, head_dim, dqkv, (hipStream_t)stream);
   // the f32 head_dim-32 backward over tail queries forms its own row statistics (no prep launch)
-  const bool fdl = g_attn_bwd_fdl && !qpos && head_dim == 32 && K > SMALL_K && attn_kpad(K) <= FDL_KP &&
+  const bool fdl = !qpos && head_dim == 32 && K > SMALL_K && attn_kpad(K) <= FDL_KP &&
                    mm != OT_MATMUL_BF16;
   if (fdl) {
     hipLaunchKernelGGL((attn_bwd_kernel<32, false, 1, true>), dim3(ceil_div((int64_t)B * H, BWD_WAVES<32>())),
@@ -1774,10 +1767,10 @@ static int attn_bwd_impl(const float* qkv, int64_t ld, const float* out, const f
     OT_ATTN_DISPATCH(attn_bwd_small_kernel, head_dim, dim3(ceil_div((int64_t)B * H, 4)), dim3(256), 0,
                      (hipStream_t)stream, p);
   } else if (mm == OT_MATMUL_BF16 && (head_dim == 32 || head_dim == 64) &&
-             attn_bwd_kgroup(I, K, head_dim, qpos != nullptr) &&
-             ws_bytes >= ot_attn_bwd_ex_workspace_size(B, H, I, K, head_dim, 0)) {
+             attn_bwd_kgroup(I, K, head_dim, qpos != nullptr, prec) &&
+             ws_bytes >= ot_attn_bwd_ex_workspace_size(B, H, I, K, head_dim, 0, prec)) {
     // bf16 mode, long tails: key-grouped workgroups (dQ partials in the ot_attn_bwd_ex workspace)
-    const int G = attn_bwd_kgroup(I, K, head_dim, false), S = attn_bwd_kslices(B, H, I, K, head_dim, false);
+    const int G = attn_bwd_kgroup(I, K, head_dim, false, prec), S = attn_bwd_kslices(B, H, I, K, head_dim, false, prec);
     p.kslices = S;
     p.kgroup = G;
     p.dqpart = delta_ws + ot_attn_bwd_workspace_size(B, H, K) / sizeof(float);
@@ -1824,7 +1817,7 @@ static int attn_bwd_impl(const float* qkv, int64_t ld, const float* out, const f
       (void)hipGetLastError();
     });
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * waves), (size_t)waves * lds, (hipStream_t)stream, p);
-  } else if (head_dim == 64 && g_attn_bwd_ds == 2) {
+  } else if (head_dim == 64) {
     // head_dim 64 as two 32-dim waves per (sample, head): 2 waves / SIMD instead of 1
     const bool sel = qpos != nullptr;
     void (*kern)(AttnArgs) = sel ? attn_bwd_kernel<32, true, 2> : attn_bwd_kernel<32, false, 2>;
@@ -1837,7 +1830,6 @@ static int attn_bwd_impl(const float* qkv, int64_t ld, const float* out, const f
     switch (head_dim) {
       case 16: kern = sel ? attn_bwd_kernel<16, true> : attn_bwd_kernel<16, false>; break;
       case 32: kern = sel ? attn_bwd_kernel<32, true> : attn_bwd_kernel<32, false>; break;
-      case 64: kern = sel ? attn_bwd_kernel<64, true> : attn_bwd_kernel<64, false>; break;
       case 128: kern = sel ? attn_bwd_kernel<128, true> : attn_bwd_kernel<128, false>; break;
       default: return fail(OT_ERR_UNSUPPORTED, "attention: head_dim %d unsupported", head_dim);
     }

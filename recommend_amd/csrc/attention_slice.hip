@@ -25,6 +25,7 @@
 // ds_read_b128 row reads (16 rows x one chunk per lane group) and the transposed reads are conflict-free.
 #include <algorithm>
 #include <cstdio>
+#include <cstring>
 #include <cstdlib>
 #include <mutex>
 
@@ -87,6 +88,22 @@ __device__ __forceinline__ void tr_frag(u32x4 (&f)[3], const char* img, int pb, 
   }
 }
 
+// max / sum with the lane 16 and 32 apart (the 4 lane groups of a 16x16 accumulator column) on the VALU
+// lane-swap instructions (no LDS round trip as ds_bpermute): each swap hands every lane its own value and
+// its partner's, in some order — max and + are symmetric, so all four groups get identical results
+__device__ __forceinline__ float group_max(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ float group_sum(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
 __device__ __forceinline__ void load8(float (&v)[8], const float* src) {
   const f32x4 a = *reinterpret_cast<const f32x4*>(src), b = *reinterpret_cast<const f32x4*>(src + 4);
   v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
@@ -100,444 +117,561 @@ __device__ __forceinline__ void store_planes(char* img, int pb, int o, const flo
   for (int k = 0; k < 3; ++k) *reinterpret_cast<u32x4*>(img + k * pb + o) = pl[k];
 }
 
-// Work schedule inside a workgroup of NWV waves (4 or 8).  Waves w and w + 4 share SIMD w & 3 (a
-// workgroup's waves go to the SIMDs cyclically, MI355X_MICROARCH.md §LDS), so items (heaviest first) go
-// to the least-loaded SIMD, then to its less-loaded wave (LPT).  Every wave runs the same uniform
-// arithmetic; the result is the item index of `slot` of wave w, or -1.
-template <int NWV, typename F>
-__device__ __forceinline__ int lpt_pick(int slot, int w, int n, F load) {
-  int s0 = 0, s1 = 0, s2 = 0, s3 = 0, w0 = 0, w1 = 0, w2 = 0, w3 = 0, w4 = 0, w5 = 0, w6 = 0, w7 = 0;
-  int cnt = 0;
-  for (int i = 0; i < n; ++i) {
-    const int L = load(i);
-    int s = 0, m = s0;
-    if (s1 < m) { s = 1; m = s1; }
-    if (s2 < m) { s = 2; m = s2; }
-    if (s3 < m) { s = 3; m = s3; }
-    int ww = s;
-    if (NWV == 8) {
-      const int a = s == 0 ? w0 : s == 1 ? w1 : s == 2 ? w2 : w3;
-      const int b = s == 0 ? w4 : s == 1 ? w5 : s == 2 ? w6 : w7;
-      ww = a <= b ? s : s + 4;
-    }
-    s0 += s == 0 ? L : 0; s1 += s == 1 ? L : 0; s2 += s == 2 ? L : 0; s3 += s == 3 ? L : 0;
-    w0 += ww == 0 ? L : 0; w1 += ww == 1 ? L : 0; w2 += ww == 2 ? L : 0; w3 += ww == 3 ? L : 0;
-    w4 += ww == 4 ? L : 0; w5 += ww == 5 ? L : 0; w6 += ww == 6 ? L : 0; w7 += ww == 7 ? L : 0;
-    if (ww == w) {
-      if (cnt == slot) return i;
-      ++cnt;
-    }
-  }
-  return -1;
-}
-
-// tail queries: first 16-query block whose last query sees key block kb
-__device__ __forceinline__ int tail_qf(int kb, int q_off, int K, int nqb) {
-  int f = 0;
-  while (f < nqb && q_off + min(16 * f + 15, K - 1) < 16 * kb) ++f;
-  return f;
+// tail queries: first 16-query block whose last query sees key block kb (query blocks before the last
+// end at 16f + 15 < K, so the first f with q_off + 16f + 15 >= 16 kb, capped at the last block)
+__host__ __device__ inline int tail_qf(int kb, int q_off, int nqb) {
+  const int num = 16 * kb - q_off - 15;
+  const int f = num <= 0 ? 0 : (num + 15) / 16;
+  return f < nqb - 1 ? f : nqb - 1;
 }
 
 // ------------------------------------------------------------------------------------------
-// Forward.  The slice's K and V planes are staged in LDS ([IP][HD] x 3 each); each wave takes whole
-// 16-query blocks (LPT over the SIMDs, heaviest first).  Per query block the wave holds Q (pre-scaled by
-// log2(e)/sqrt(hd), split) as the B operand of S^T = K Q^T (query on the lane) and computes S^T for
-// every visible key block at once (<= 12 x 4 registers), so the softmax is exact in one pass (row max
-// and sum over the 4 lane groups by shuffles, no rescaling); O^T = V^T P^T takes P^T from the S^T
-// registers and V^T by transposed reads.  Every global load is issued ahead of its use: the staging
-// rounds all at once, each wave's first Q block before the staging barrier, the next one while the
-// current block computes.
-template <int HD, int NWV>
+// Plane images have compile-time strides (RMAX rows per plane), so every LDS address is a per-lane base
+// plus an immediate.  hd 64: 144 rows (the backward's LDS limit at I = 140), hd 32: 192.
+template <int HD>
+constexpr int RMAX() { return HD == 64 ? 144 : 192; }
+
+// the wave's schedule row as one uniform 64-bit value (a scalar load at kernel start: an in-loop vector
+// load of the kernel argument would wait, in-order, for every prefetch load issued before it)
+__device__ __forceinline__ uint64_t sched_row(const SliceArgs& p, int phase, int wave) {
+  const uint64_t* rows = reinterpret_cast<const uint64_t*>(&p.sched[0][0][0]);
+  const uint64_t r = rows[phase * 8 + wave];
+  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(r >> 32)) << 32) |
+         (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)r);
+}
+__device__ __forceinline__ int sched_item(uint64_t row, int slot) {
+  return slot < 8 ? (int)(int8_t)(row >> (8 * slot)) : -1;
+}
+
+// Diagnostic build only (-DOT_SLICE_STAMPS=1, a separate library: tools/slice_stamps.py): thread 0 of each
+// workgroup records the shader clock at the phase boundaries of its first two slices.
+#ifndef OT_SLICE_STAMPS
+#define OT_SLICE_STAMPS 0
+#endif
+#if OT_SLICE_STAMPS
+__device__ unsigned long long g_slice_stamps[2][2048][2][8];
+#define SLICE_STAMP(kind, it, k)                                                                   \
+  do {                                                                                           \
+    if (threadIdx.x == 0 && (it) < 2 && blockIdx.x < 2048) g_slice_stamps[kind][blockIdx.x][it][k] = clock64(); \
+  } while (0)
+#else
+#define SLICE_STAMP(kind, it, k) do {} while (0)
+#endif
+
+// Both kernels are persistent: a workgroup walks slices s = blockIdx.x, + gridDim.x, ... (grid = the
+// co-resident workgroups), and the next slice's operands are loaded into registers while the current
+// slice computes — with one or two workgroups per CU (LDS), a non-persistent grid left every CU loading
+// or computing in lock-step (MFMA busy 19% in the backward, profiles/r04).
+
+// ------------------------------------------------------------------------------------------
+// Forward.  The slice's K and V planes are staged in LDS ([RMAX][HD] x 3 each); each wave takes whole
+// 16-query blocks (host LPT schedule over the SIMDs, heaviest first).  Per query block the wave holds Q
+// (pre-scaled by log2(e)/sqrt(hd), split) as the B operand of S^T = K Q^T (query on the lane) and
+// computes S^T for every visible key block at once (<= 12 x 4 registers), so the softmax is exact in one
+// pass (row max and sum over the 4 lane groups by shuffles, no rescaling); O^T = V^T P^T takes P^T from
+// the S^T registers and V^T by transposed reads.  Loads in flight during compute: the next slice's K / V
+// rows (all of them), the next query block's Q (the next slice's first one during the last block).
+// PF: persistent with the next slice's K / V prefetched (hd 64: one workgroup per CU by LDS anyway); without
+// it one workgroup per slice and fewer registers, so more waves per SIMD (hd 32: 4 instead of 2, faster).
+template <int HD, int NWV, bool SEL, bool PF>
 __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_slice_kernel(SliceArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NT = HD / 32, NM = HD / 16, CPR = HD / 8, NTH = 64 * NWV;
-  constexpr int SR = (MAXKB * 16 * CPR + NTH - 1) / NTH;          // staging rounds (upper bound)
+  constexpr int PB = RMAX<HD>() * HD * 2;
+  constexpr int SR = (RMAX<HD>() * CPR + NTH - 1) / NTH;          // staging rounds
   const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform: the schedule runs on SALU
-  const int pair = blockIdx.x, b = pair / p.H, h = pair % p.H;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform
   const int I = p.I, K = p.K, q_off = I - K;
   const int nkb = (I + 15) >> 4, nqb = (K + 15) >> 4, IP = nkb * 16;
-  const int PB = IP * HD * 2;
+  const int nslices = p.B * p.H;
   char* kimg = smem;
   char* vimg = smem + 3 * PB;
-  const int64_t tok0 = (int64_t)b * I;
-  const float* Qg = p.qkv + tok0 * p.ld + h * HD;
-  const float* Kg = Qg + p.d;
-  const float* Vg = Qg + 2 * p.d;
-  const int32_t* qsel = p.qpos ? p.qpos + (int64_t)b * K : nullptr;
-  auto qpos_of = [&](int j) { return qsel ? qsel[j] : q_off + j; };
-  // query block of item idx (heaviest first) and its last visible key block
-  auto kbl_of = [&](int qb) { return qpos_of(min(16 * qb + 15, K - 1)) >> 4; };
-  auto load_of = [&](int idx) { const int kl = kbl_of(nqb - 1 - idx); return NT * (kl + 1) + NM * (kl / 2 + 1); };
-
-  float kr[SR][8], vr[SR][8];
-#pragma unroll
-  for (int r = 0; r < SR; ++r) {
-    const int task = threadIdx.x + r * NTH, row = task / CPR, c = task % CPR;
-    if (task < IP * CPR && row < I) {
-      load8(kr[r], Kg + (int64_t)row * p.ld + 8 * c);
-      load8(vr[r], Vg + (int64_t)row * p.ld + 8 * c);
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) kr[r][e] = vr[r][e] = 0.f;
-    }
-  }
-  float qr[NT][8];
-  int idx = lpt_pick<NWV>(0, wave, nqb, load_of);
-  auto load_q = [&](int ix) {
-    const int j = 16 * (nqb - 1 - ix) + li;
-    const int qp = qpos_of(j < K ? j : K - 1);
-#pragma unroll
-    for (int t = 0; t < NT; ++t) load8(qr[t], Qg + (int64_t)qp * p.ld + 32 * t + 8 * g);
-  };
-  if (idx >= 0) load_q(idx);
-#pragma unroll
-  for (int r = 0; r < SR; ++r) {
-    const int task = threadIdx.x + r * NTH, row = task / CPR, c = task % CPR;
-    if (task < IP * CPR) {
-      const int o = poff<HD>(row, c);
-      store_planes(kimg, PB, o, kr[r]);
-      store_planes(vimg, PB, o, vr[r]);
-    }
-  }
-  __syncthreads();
+  int* qposl = reinterpret_cast<int*>(smem + 6 * PB);                // SEL: the slice's kept positions
   const float qscale = p.scale * L2E;
-#pragma unroll 1
-  for (int slot = 0; idx >= 0; ++slot) {
-    const int qb = nqb - 1 - idx;
-    const int j = 16 * qb + li;                                      // this lane's query
-    const int qpos = qpos_of(j < K ? j : K - 1);
-    const int kbl = kbl_of(qb);
-    u32x4 qp[NT][3];
+  auto qkv_of = [&](int s) { return p.qkv + (int64_t)(s / p.H) * I * p.ld + (s % p.H) * HD; };
+  // query positions: the tail rule, or (SEL) the slice's kept positions staged in LDS with K / V
+  // staging rows past I (and tasks past IP) read row I - 1: finite, zeroed or skipped at store time
+  float kr[SR][8], vr[SR][8], qr[NT][8];
+  auto load_kv = [&](int s) {
+    const float* Q = qkv_of(s);
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) qr[t][e] *= qscale;
-      split8(qr[t], qp[t]);
+    for (int r = 0; r < SR; ++r) {
+      const int task = threadIdx.x + r * NTH, row = min(task / CPR, I - 1), c = task % CPR;
+      load8(kr[r], Q + p.d + (int64_t)row * p.ld + 8 * c);
+      load8(vr[r], Q + 2 * p.d + (int64_t)row * p.ld + 8 * c);
     }
-    idx = lpt_pick<NWV>(slot + 1, wave, nqb, load_of);
-    if (idx >= 0) load_q(idx);                                       // next block's Q, in flight meanwhile
-    f32x4 s[MAXKB];
-    float mx = -INFINITY;
+  };
+  auto qpos_of = [&](int j) { return SEL ? qposl[j] : q_off + j; };
+  auto load_q = [&](int s, int idx) {
+    const float* Q = qkv_of(s);
+    const int j = min(16 * (nqb - 1 - idx) + li, K - 1);
+    const int qp = qpos_of(j);
 #pragma unroll
-    for (int kb = 0; kb < MAXKB; ++kb) {
-      s[kb] = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-      if (kb > kbl) continue;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < NT; ++t) load8(qr[t], Q + (int64_t)qp * p.ld + 32 * t + 8 * g);
+  };
+  const uint64_t srow = sched_row(p, 0, wave);
+  const int idx0 = sched_item(srow, 0);
+  int s = blockIdx.x;
+  if (s < nslices) {
+    load_kv(s);
+    if (!SEL && idx0 >= 0) load_q(s, idx0);
+  }
+#pragma unroll 1
+  for (int it = 0; s < nslices; s += gridDim.x, ++it) {
+    SLICE_STAMP(0, it, 0);
+#pragma unroll
+    for (int r = 0; r < SR; ++r) {
+      const int task = threadIdx.x + r * NTH, row = task / CPR, c = task % CPR;
+      if (task < IP * CPR) {
+        if (row >= I) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) kr[r][e] = vr[r][e] = 0.f;
+        }
+        const int o = poff<HD>(row, c);
+        store_planes(kimg, PB, o, kr[r]);
+        store_planes(vimg, PB, o, vr[r]);
+      }
+    }
+    if (SEL)
+      for (int j = threadIdx.x; j < K; j += NTH) qposl[j] = p.qpos[(int64_t)(s / p.H) * K + j];
+    __syncthreads();
+    SLICE_STAMP(0, it, 1);
+    if (SEL && idx0 >= 0) load_q(s, idx0);                           // (positions of the next slice unknown yet)
+    const int sn = s + gridDim.x;
+    if (PF && sn < nslices) load_kv(sn);                             // next slice's K / V, in flight meanwhile
+    const int b = s / p.H, h = s % p.H;
+#pragma unroll 1
+    for (int slot = 0, idx = idx0; idx >= 0; ++slot) {
+      const int qb = nqb - 1 - idx;
+      const int j = 16 * qb + li;                                    // this lane's query
+      const int qpos = qpos_of(j < K ? j : K - 1);
+      const int kbl = qpos_of(min(16 * qb + 15, K - 1)) >> 4;        // last visible key block
+      u32x4 qp[NT][3];
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        u32x4 fk[3];
-        row_frag<HD>(fk, kimg, PB, 16 * kb + li, t, g);
-        acc = mma6(fk, qp[t], acc);                                   // S^T: row = key, col = query
-      }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        acc[i] = (16 * kb + 4 * g + i <= qpos) ? acc[i] : -INFINITY;
-        mx = fmaxf(mx, acc[i]);
+        for (int e = 0; e < 8; ++e) qr[t][e] *= qscale;
+        split8(qr[t], qp[t]);
       }
-      s[kb] = acc;
+      const int idxn = sched_item(srow, slot + 1);
+      if (idxn >= 0) load_q(s, idxn);                                // next block's Q, in flight meanwhile
+      else if (PF && !SEL && sn < nslices && idx0 >= 0) load_q(sn, idx0);
+      f32x4 sc[MAXKB];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < MAXKB; ++kb) {
+        sc[kb] = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+        if (kb > kbl) continue;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          u32x4 fk[3];
+          row_frag<HD>(fk, kimg, PB, 16 * kb + li, t, g);
+          acc = mma6(fk, qp[t], acc);                                 // S^T: row = key, col = query
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          acc[i] = (16 * kb + 4 * g + i <= qpos) ? acc[i] : -INFINITY;
+          mx = fmaxf(mx, acc[i]);
+        }
+        sc[kb] = acc;
+      }
+      mx = group_max(mx);
+      float l = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < MAXKB; ++kb) {
+        if (kb > kbl) continue;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float e = __builtin_amdgcn_exp2f(sc[kb][i] - mx);
+          sc[kb][i] = e;
+          l += e;
+        }
+      }
+      l = group_sum(l);
+      f32x4 o[NM];
+#pragma unroll
+      for (int m = 0; m < NM; ++m) o[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kb = 0; kb < MAXKB; kb += 2) {
+        if (kb > kbl) continue;
+        const bool two = kb + 1 <= kbl;
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          v[i] = sc[kb][i];
+          v[4 + i] = two ? sc[kb + 1][i] : 0.f;
+        }
+        u32x4 pp[3];
+        split8(v, pp);
+#pragma unroll
+        for (int m = 0; m < NM; ++m) {
+          u32x4 fa[3];
+          tr_frag<HD>(fa, vimg, PB, 16 * kb, two ? 16 * kb + 16 : 16 * kb, m, lane);
+          o[m] = mma6(fa, pp, o[m]);                                  // O^T += V^T P^T
+        }
+      }
+      if (j < K) {
+        const float inv = 1.f / l;
+        float* orow = p.out + ((int64_t)b * K + j) * p.d + h * HD + 4 * g;
+#pragma unroll
+        for (int m = 0; m < NM; ++m) *reinterpret_cast<f32x4*>(orow + 16 * m) = o[m] * inv;
+        if (g == 0) p.lse[(int64_t)s * K + j] = mx * LN2 + __logf(l);
+      }
+      idx = idxn;
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    float l = 0.f;
-#pragma unroll
-    for (int kb = 0; kb < MAXKB; ++kb) {
-      if (kb > kbl) continue;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float e = __builtin_amdgcn_exp2f(s[kb][i] - mx);
-        s[kb][i] = e;
-        l += e;
-      }
-    }
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
-    f32x4 o[NM];
-#pragma unroll
-    for (int m = 0; m < NM; ++m) o[m] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kb = 0; kb < MAXKB; kb += 2) {
-      if (kb > kbl) continue;
-      const bool two = kb + 1 <= kbl;
-      float v[8];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        v[i] = s[kb][i];
-        v[4 + i] = two ? s[kb + 1][i] : 0.f;
-      }
-      u32x4 pp[3];
-      split8(v, pp);
-#pragma unroll
-      for (int m = 0; m < NM; ++m) {
-        u32x4 fa[3];
-        tr_frag<HD>(fa, vimg, PB, 16 * kb, two ? 16 * kb + 16 : 16 * kb, m, lane);
-        o[m] = mma6(fa, pp, o[m]);                                    // O^T += V^T P^T
-      }
-    }
-    if (j < K) {
-      const float inv = 1.f / l;
-      float* orow = p.out + ((int64_t)b * K + j) * p.d + h * HD + 4 * g;
-#pragma unroll
-      for (int m = 0; m < NM; ++m) *reinterpret_cast<f32x4*>(orow + 16 * m) = o[m] * inv;
-      if (g == 0) p.lse[(int64_t)pair * K + j] = mx * LN2 + __logf(l);
-    }
+    SLICE_STAMP(0, it, 2);
+    if constexpr (!PF) break;                                        // one slice per workgroup
+    __syncthreads();                                                 // the planes are rewritten next slice
+    SLICE_STAMP(0, it, 3);
   }
 }
 
 // ------------------------------------------------------------------------------------------
-// Backward (tail queries).  LDS: Q planes [IP][HD] x 3 (phase 2: the K image), dO planes [KP][HD] x 3,
+// Backward (tail queries).  LDS: Q planes [RMAX][HD] x 3 (phase 2: the K image), dO planes x 3,
 // lse (log2 units, +inf padding), delta = rowsum(dO o O) (formed here from one read of O), query
-// positions, per key block its first visible query block and dS-store base, then the dS store: one
-// 1 KiB [16 query][16 key] f32 block per causal block pair.
-//   phase 1, key blocks (LPT over the SIMDs), query steps of two 16-row blocks (a, a+1):
+// positions, then the dS store: one 1 KiB [16 query][16 key] f32 block per causal block pair.
+//   phase 1, key blocks (host LPT schedule), query steps of two 16-row blocks (a, a+1):
 //     S = Q K^T, dP = dO V^T          A = Q / dO rows (ds_read_b128), B = K^T / V^T (registers)
 //     P = exp2(S log2e/sqrt(hd) - lse), dS = P (dP - delta) / sqrt(hd)     (key on the lane)
 //     dV^T += dO^T P, dK^T += Q^T dS  A = dO^T / Q^T (transposed reads), B = P / dS (registers)
 //     dS -> store
 //   phase 2, query blocks: dQ^T = K^T dS^T over the visible key blocks, two per step (K image re-read
 //   from global — L2-warm — into the Q planes' space).
-// Global loads are issued ahead of use: the staging rounds and the first key block's K / V before the
-// staging barrier, the next key block's during the current one, the K image's before the phase barrier.
+// Loads in flight during compute: the next key block's K / V (phase 1), the K image rows (issued by each
+// wave as it leaves phase 1), and the next slice's Q / dO / O rows, lse and first K / V (phase 2).
 template <int HD, int NWV>
 __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NT = HD / 32, NM = HD / 16, CPR = HD / 8, NTH = 64 * NWV;
-  constexpr int SR = (MAXKB * 16 * CPR + NTH - 1) / NTH;
+  constexpr int RM = RMAX<HD>(), PB = RM * HD * 2;
+  constexpr int SR = (RM * CPR + NTH - 1) / NTH;
   const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform: the schedule runs on SALU
-  const int pair = blockIdx.x, b = pair / p.H, h = pair % p.H;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform
   const int I = p.I, K = p.K, q_off = I - K;
   const int nkb = (I + 15) >> 4, nqb = (K + 15) >> 4, IP = nkb * 16, KP = nqb * 16;
-  const int PBQ = IP * HD * 2, PBO = KP * HD * 2;
+  const int nslices = p.B * p.H;
   char* qimg = smem;
-  char* oimg = qimg + 3 * PBQ;
-  float* lse2 = reinterpret_cast<float*>(oimg + 3 * PBO);
-  float* dlt = lse2 + KP;
-  int* qps = reinterpret_cast<int*>(dlt + KP);
-  int* qfb = qps + KP;
-  int* bbase = qfb + MAXKB;
-  char* dss = reinterpret_cast<char*>(bbase + MAXKB);
-  const int64_t tok0 = (int64_t)b * I;
-  const int hoff = h * HD;
-  const float* Qg = p.qkv + tok0 * p.ld + hoff;
-  const float* Kg = Qg + p.d;
-  const float* Vg = Qg + 2 * p.d;
-  const float* dOg = p.dout + (int64_t)b * K * p.d + hoff;
-  const float* Og = p.o + (int64_t)b * K * p.d + hoff;
-  float* dQg = p.dqkv + tok0 * p.ld + hoff;
-  float* dKg = dQg + p.d;
-  float* dVg = dQg + 2 * p.d;
-  auto kload = [&](int kb) { return (nqb - tail_qf(kb, q_off, K, nqb) + 1) >> 1; };   // query steps
-  auto qload = [&](int idx) { return ((q_off + min(16 * (nqb - 1 - idx) + 15, K - 1)) >> 5) + 1; };
-
-  // ---- prologue: every load issued first
-  float qr[SR][8], yr[SR][8], orr[SR][8];
-#pragma unroll
-  for (int r = 0; r < SR; ++r) {
-    const int task = threadIdx.x + r * NTH, j = task / CPR, c = task % CPR;
-    if (task < KP * CPR && j < K) {
-      load8(qr[r], Qg + (int64_t)(q_off + j) * p.ld + 8 * c);
-      load8(yr[r], dOg + (int64_t)j * p.d + 8 * c);
-      load8(orr[r], Og + (int64_t)j * p.d + 8 * c);
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) qr[r][e] = yr[r][e] = orr[r][e] = 0.f;
-    }
+  char* oimg = smem + 3 * PB;
+  float* lse2 = reinterpret_cast<float*>(smem + 6 * PB);
+  float* dlt = lse2 + RM;
+  int* qps = reinterpret_cast<int*>(dlt + RM);
+  int* tab = qps + RM;                             // [16] first visible query block, [16] dS-store base per key block
+  char* dss = reinterpret_cast<char*>(tab + 32);
+  const float c1 = p.scale * L2E;
+  if (threadIdx.x < 16) {
+    tab[threadIdx.x] = p.qf[threadIdx.x];
+    tab[16 + threadIdx.x] = p.bbase[threadIdx.x];
   }
-  // K / V rows of a key block: rows past I read row I - 1 (finite) and are zeroed at split time, so the
-  // loads carry no branch (a branch here kept the arrays in scratch)
+  const uint64_t srow1 = sched_row(p, 1, wave), srow2 = sched_row(p, 2, wave);
+  auto qkv_of = [&](int s) { return p.qkv + (int64_t)(s / p.H) * I * p.ld + (s % p.H) * HD; };
+  auto row_of = [&](int s) { return (int64_t)(s / p.H) * K * p.d + (s % p.H) * HD; };   // O / dO slice
+  // rows past K / I read the last valid row (finite) and are zeroed at use, so no load is predicated
+  float qr[SR][8], yr[SR][8], orr[SR][8], lsev;
   float kr[NT][8], vr[NT][8];
-  auto load_kv = [&](int kb) {
+  auto load_kv = [&](int s, int kb) {
+    const float* Kg = qkv_of(s) + p.d;
     const int krow = min(16 * kb + li, I - 1);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       load8(kr[t], Kg + (int64_t)krow * p.ld + 32 * t + 8 * g);
-      load8(vr[t], Vg + (int64_t)krow * p.ld + 32 * t + 8 * g);
+      load8(vr[t], Kg + p.d + (int64_t)krow * p.ld + 32 * t + 8 * g);
     }
   };
-  int kb = lpt_pick<NWV>(0, wave, nkb, kload);
-  if (HD <= 32 && kb >= 0) load_kv(kb);           // hd 64: after the staging stores (register pressure)
-  for (int j = threadIdx.x; j < KP; j += NTH) {
-    const bool v = j < K;
-    qps[j] = v ? q_off + j : -1;
-    lse2[j] = v ? p.lse_in[(int64_t)pair * K + j] * L2E : INFINITY;
-  }
-  if (threadIdx.x < nkb) {
-    int base = 0;
-    for (int k = 0; k < (int)threadIdx.x; ++k) base += nqb - tail_qf(k, q_off, K, nqb);
-    qfb[threadIdx.x] = tail_qf(threadIdx.x, q_off, K, nqb);
-    bbase[threadIdx.x] = base;
-  }
+  const int kb0 = sched_item(srow1, 0);
+  auto prefetch = [&](int s) {
+    const float* Qg = qkv_of(s);
+    const float* dOg = p.dout + row_of(s);
+    const float* Og = p.o + row_of(s);
 #pragma unroll
-  for (int r = 0; r < SR; ++r) {
-    const int task = threadIdx.x + r * NTH, j = task / CPR, c = task % CPR;
-    float pd = 0.f;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) pd = fmaf(yr[r][e], orr[r][e], pd);
-#pragma unroll
-    for (int off = 1; off < CPR; off <<= 1) pd += __shfl_xor(pd, off, 64);
-    if (task < KP * CPR) {
-      if (c == 0) dlt[j] = pd;
-      const int o = poff<HD>(j, c);
-      store_planes(qimg, PBQ, o, qr[r]);
-      store_planes(oimg, PBO, o, yr[r]);
+    for (int r = 0; r < SR; ++r) {
+      const int task = threadIdx.x + r * NTH, j = min(task / CPR, K - 1), c = task % CPR;
+      load8(qr[r], Qg + (int64_t)(q_off + j) * p.ld + 8 * c);
+      load8(yr[r], dOg + (int64_t)j * p.d + 8 * c);
+      load8(orr[r], Og + (int64_t)j * p.d + 8 * c);
     }
-  }
-  if (HD > 32 && kb >= 0) load_kv(kb);
-  __syncthreads();
+    lsev = p.lse_in[(int64_t)s * K + min((int)threadIdx.x, K - 1)];
+    if (kb0 >= 0) load_kv(s, kb0);
+  };
+  int s = blockIdx.x;
+  if (s < nslices) prefetch(s);
+#pragma unroll 1
+  for (int it = 0; s < nslices; s += gridDim.x, ++it) {
+    SLICE_STAMP(1, it, 0);
+    float* dQg = p.dqkv + (int64_t)(s / p.H) * I * p.ld + (s % p.H) * HD;
+    float* dKg = dQg + p.d;
+    float* dVg = dQg + 2 * p.d;
+    const float* Kg = qkv_of(s) + p.d;
 
-  // ---- phase 1: key-block owners
-  const float c1 = p.scale * L2E;
-#pragma unroll 1
-  for (int slot = 0; kb >= 0; ++slot) {
-    const int krow = 16 * kb + li;                 // this lane's key
-    u32x4 kp[NT][3], vp[NT][3];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        kr[t][e] = krow < I ? kr[t][e] : 0.f;
-        vr[t][e] = krow < I ? vr[t][e] : 0.f;
-      }
-      split8(kr[t], kp[t]);
-      split8(vr[t], vp[t]);
+    // ---- stage the query side from the prefetched registers
+    if ((int)threadIdx.x < KP) {
+      const bool v = (int)threadIdx.x < K;
+      qps[threadIdx.x] = v ? q_off + threadIdx.x : -1;
+      lse2[threadIdx.x] = v ? lsev * L2E : INFINITY;
     }
-    const int kbn = lpt_pick<NWV>(slot + 1, wave, nkb, kload);
-    if (kbn >= 0) load_kv(kbn);                    // next key block's K / V in flight meanwhile
-    f32x4 dk[NM], dv[NM];
 #pragma unroll
-    for (int m = 0; m < NM; ++m) dk[m] = dv[m] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int a0 = qfb[kb], blk0 = bbase[kb];
+    for (int r = 0; r < SR; ++r) {
+      const int task = threadIdx.x + r * NTH, j = task / CPR, c = task % CPR;
+      if (j >= K) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) qr[r][e] = yr[r][e] = orr[r][e] = 0.f;
+      }
+      float pd = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) pd = fmaf(yr[r][e], orr[r][e], pd);
+#pragma unroll
+      for (int off = 1; off < CPR; off <<= 1) pd += __shfl_xor(pd, off, 64);
+      if (task < KP * CPR) {
+        if (c == 0) dlt[j] = pd;
+        const int o = poff<HD>(j, c);
+        store_planes(qimg, PB, o, qr[r]);
+        store_planes(oimg, PB, o, yr[r]);
+      }
+    }
+    __syncthreads();
+    SLICE_STAMP(1, it, 1);
+
+    // ---- phase 1: key-block owners
 #pragma unroll 1
-    for (int a = a0; a < nqb; a += 2) {
-      const bool two = a + 1 < nqb;
-      float P[8], dS[8];
+    for (int slot = 0, kb = kb0; kb >= 0; ++slot) {
+      const int krow = 16 * kb + li;               // this lane's key
+      u32x4 kp[NT][3], vp[NT][3];
 #pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        const int qb = a + half;
+      for (int t = 0; t < NT; ++t) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) P[4 * half + i] = dS[4 * half + i] = 0.f;
-        if (half == 1 && !two) continue;
-        f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+        for (int e = 0; e < 8; ++e) {
+          kr[t][e] = krow < I ? kr[t][e] : 0.f;
+          vr[t][e] = krow < I ? vr[t][e] : 0.f;
+        }
+        split8(kr[t], kp[t]);
+        split8(vr[t], vp[t]);
+      }
+      const int kbn = sched_item(srow1, slot + 1);
+      // next key block's K / V in flight meanwhile (hd 64 at 2 waves / SIMD: loaded at its turn instead —
+      // the 32 registers of the prefetch spill there, and the SIMD's other wave covers the latency)
+      constexpr bool PREFETCH_KV = !(HD == 64 && NWV == 8);
+      if (PREFETCH_KV && kbn >= 0) load_kv(s, kbn);
+      f32x4 dk[NM], dv[NM];
 #pragma unroll
-        for (int t = 0; t < NT; ++t) {
+      for (int m = 0; m < NM; ++m) dk[m] = dv[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int a0 = tab[kb], blk0 = tab[16 + kb];
+#pragma unroll 1
+      for (int a = a0; a < nqb; a += 2) {
+        const bool two = a + 1 < nqb;
+        float P[8], dS[8];
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          const int qb = a + half;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) P[4 * half + i] = dS[4 * half + i] = 0.f;
+          if (half == 1 && !two) continue;
+          f32x4 sacc = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int t = 0; t < NT; ++t) {
+            u32x4 fa[3], fb[3];
+            row_frag<HD>(fa, qimg, PB, 16 * qb + li, t, g);
+            row_frag<HD>(fb, oimg, PB, 16 * qb + li, t, g);
+            sacc = mma6(fa, kp[t], sacc);                             // S: row = query, col = key
+            dp = mma6(fb, vp[t], dp);                                 // dP
+          }
+          const int q0 = 16 * qb + 4 * g;
+          const f32x4 L = *reinterpret_cast<const f32x4*>(lse2 + q0);
+          const f32x4 D = *reinterpret_cast<const f32x4*>(dlt + q0);
+          const i32x4 Qp = *reinterpret_cast<const i32x4*>(qps + q0);
+          char* blk = dss + 1024 * (blk0 + qb - a0);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float e = __builtin_amdgcn_exp2f(fmaf(sacc[i], c1, -L[i]));
+            const float pv = krow <= Qp[i] ? e : 0.f;
+            const float ds = pv * (dp[i] - D[i]) * p.scale;
+            P[4 * half + i] = pv;
+            dS[4 * half + i] = ds;
+            *reinterpret_cast<float*>(blk + poff<32>(4 * g + i, li >> 2) + 4 * (li & 3)) = ds;
+          }
+        }
+        u32x4 pp[3], sp[3];
+        split8(P, pp);
+        split8(dS, sp);
+        const int rb = two ? 16 * a + 16 : 16 * a;
+#pragma unroll
+        for (int m = 0; m < NM; ++m) {
           u32x4 fa[3], fb[3];
-          row_frag<HD>(fa, qimg, PBQ, 16 * qb + li, t, g);
-          row_frag<HD>(fb, oimg, PBO, 16 * qb + li, t, g);
-          s = mma6(fa, kp[t], s);                                     // S: row = query, col = key
-          dp = mma6(fb, vp[t], dp);                                   // dP
-        }
-        const int q0 = 16 * qb + 4 * g;
-        const f32x4 L = *reinterpret_cast<const f32x4*>(lse2 + q0);
-        const f32x4 D = *reinterpret_cast<const f32x4*>(dlt + q0);
-        const i32x4 Qp = *reinterpret_cast<const i32x4*>(qps + q0);
-        char* blk = dss + 1024 * (blk0 + qb - a0);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float e = __builtin_amdgcn_exp2f(fmaf(s[i], c1, -L[i]));
-          const float pv = krow <= Qp[i] ? e : 0.f;
-          const float ds = pv * (dp[i] - D[i]) * p.scale;
-          P[4 * half + i] = pv;
-          dS[4 * half + i] = ds;
-          *reinterpret_cast<float*>(blk + poff<32>(4 * g + i, li >> 2) + 4 * (li & 3)) = ds;
+          tr_frag<HD>(fa, oimg, PB, 16 * a, rb, m, lane);
+          tr_frag<HD>(fb, qimg, PB, 16 * a, rb, m, lane);
+          dv[m] = mma6(fa, pp, dv[m]);                                // dV^T += dO^T P
+          dk[m] = mma6(fb, sp, dk[m]);                                // dK^T += Q^T dS
         }
       }
-      u32x4 pp[3], sp[3];
-      split8(P, pp);
-      split8(dS, sp);
-      const int rb = two ? 16 * a + 16 : 16 * a;
+      if (krow < I) {
 #pragma unroll
-      for (int m = 0; m < NM; ++m) {
-        u32x4 fa[3], fb[3];
-        tr_frag<HD>(fa, oimg, PBO, 16 * a, rb, m, lane);
-        tr_frag<HD>(fb, qimg, PBQ, 16 * a, rb, m, lane);
-        dv[m] = mma6(fa, pp, dv[m]);                                  // dV^T += dO^T P
-        dk[m] = mma6(fb, sp, dk[m]);                                  // dK^T += Q^T dS
+        for (int m = 0; m < NM; ++m) {
+          *reinterpret_cast<f32x4*>(dKg + (int64_t)krow * p.ld + 16 * m + 4 * g) = dk[m];
+          *reinterpret_cast<f32x4*>(dVg + (int64_t)krow * p.ld + 16 * m + 4 * g) = dv[m];
+        }
       }
+      kb = kbn;
+      if (!PREFETCH_KV && kb >= 0) load_kv(s, kb);
     }
-    if (krow < I) {
+    // K image for phase 2: the rows re-read (L2-warm) before the barrier, stored into the Q planes' space after it
+    float kk[SR][8];
 #pragma unroll
-      for (int m = 0; m < NM; ++m) {
-        *reinterpret_cast<f32x4*>(dKg + (int64_t)krow * p.ld + 16 * m + 4 * g) = dk[m];
-        *reinterpret_cast<f32x4*>(dVg + (int64_t)krow * p.ld + 16 * m + 4 * g) = dv[m];
-      }
-    }
-    kb = kbn;
-  }
-  // K image for phase 2: the rows re-read (L2-warm) before the barrier, stored into the Q planes' space after it
-  constexpr int KR = (MAXKB * 16 * CPR + NTH - 1) / NTH;
-  float kk[KR][8];
-#pragma unroll
-  for (int r = 0; r < KR; ++r) {
-    const int task = threadIdx.x + r * NTH, row = task / CPR, c = task % CPR;
-    if (task < IP * CPR && row < I) {
+    for (int r = 0; r < SR; ++r) {
+      const int task = threadIdx.x + r * NTH, row = min(task / CPR, I - 1), c = task % CPR;
       load8(kk[r], Kg + (int64_t)row * p.ld + 8 * c);
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) kk[r][e] = 0.f;
     }
-  }
-  __syncthreads();                                   // dS store complete, Q planes no longer read
+    SLICE_STAMP(1, it, 2);
+    __syncthreads();                               // dS store complete, Q planes no longer read
+    SLICE_STAMP(1, it, 3);
 #pragma unroll
-  for (int r = 0; r < KR; ++r) {
-    const int task = threadIdx.x + r * NTH, row = task / CPR, c = task % CPR;
-    if (task < IP * CPR) store_planes(qimg, PBQ, poff<HD>(row, c), kk[r]);
-  }
-  __syncthreads();
-
-  // ---- phase 2: query-block owners, dQ^T = K^T dS^T
-#pragma unroll 1
-  for (int slot = 0;; ++slot) {
-    const int idx = lpt_pick<NWV>(slot, wave, nqb, qload);
-    if (idx < 0) break;
-    const int qb = nqb - 1 - idx;
-    const int kbl = (q_off + min(16 * qb + 15, K - 1)) >> 4;
-    f32x4 dq[NM];
+    for (int r = 0; r < SR; ++r) {
+      const int task = threadIdx.x + r * NTH, row = task / CPR, c = task % CPR;
+      if (task < IP * CPR) {
+        if (row >= I) {
 #pragma unroll
-    for (int m = 0; m < NM; ++m) dq[m] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-    for (int k2 = 0; k2 <= kbl; k2 += 2) {
-      const bool two = k2 + 1 <= kbl;
-      float v[8];
-      const f32x4 x0 = *reinterpret_cast<const f32x4*>(dss + 1024 * (bbase[k2] + qb - qfb[k2]) + poff<32>(li, g));
-      f32x4 x1 = {0.f, 0.f, 0.f, 0.f};
-      if (two) x1 = *reinterpret_cast<const f32x4*>(dss + 1024 * (bbase[k2 + 1] + qb - qfb[k2 + 1]) + poff<32>(li, g));
-#pragma unroll
-      for (int i = 0; i < 4; ++i) { v[i] = x0[i]; v[4 + i] = x1[i]; }
-      u32x4 bp[3];
-      split8(v, bp);
-#pragma unroll
-      for (int m = 0; m < NM; ++m) {
-        u32x4 fa[3];
-        tr_frag<HD>(fa, qimg, PBQ, 16 * k2, two ? 16 * k2 + 16 : 16 * k2, m, lane);
-        dq[m] = mma6(fa, bp, dq[m]);
+          for (int e = 0; e < 8; ++e) kk[r][e] = 0.f;
+        }
+        store_planes(qimg, PB, poff<HD>(row, c), kk[r]);
       }
     }
-    const int j = 16 * qb + li;
-    if (j < K) {
-      float* drow = dQg + (int64_t)(q_off + j) * p.ld + 4 * g;
+    __syncthreads();
+    SLICE_STAMP(1, it, 4);
+    if (s + (int)gridDim.x < nslices) prefetch(s + gridDim.x);   // next slice, in flight during phase 2
+
+    // ---- phase 2: query-block owners, dQ^T = K^T dS^T
+#pragma unroll 1
+    for (int slot = 0; slot < 8; ++slot) {
+      const int idx = sched_item(srow2, slot);
+      if (idx < 0) break;
+      const int qb = nqb - 1 - idx;
+      const int kbl = (q_off + min(16 * qb + 15, K - 1)) >> 4;
+      f32x4 dq[NM];
 #pragma unroll
-      for (int m = 0; m < NM; ++m) *reinterpret_cast<f32x4*>(drow + 16 * m) = dq[m];
+      for (int m = 0; m < NM; ++m) dq[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+      // two independent accumulator sets over alternate key-block pairs (the pairs' dS reads, splits and
+      // transposed reads overlap), added at the end
+      f32x4 dq2[NM];
+#pragma unroll
+      for (int m = 0; m < NM; ++m) dq2[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+      auto step = [&](int k2, f32x4 (&acc)[NM]) {
+        const bool two = k2 + 1 <= kbl;
+        float v[8];
+        const f32x4 x0 = *reinterpret_cast<const f32x4*>(dss + 1024 * (tab[16 + k2] + qb - tab[k2]) + poff<32>(li, g));
+        f32x4 x1 = {0.f, 0.f, 0.f, 0.f};
+        if (two)
+          x1 = *reinterpret_cast<const f32x4*>(dss + 1024 * (tab[17 + k2] + qb - tab[k2 + 1]) + poff<32>(li, g));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { v[i] = x0[i]; v[4 + i] = x1[i]; }
+        u32x4 bp[3];
+        split8(v, bp);
+#pragma unroll
+        for (int m = 0; m < NM; ++m) {
+          u32x4 fa[3];
+          tr_frag<HD>(fa, qimg, PB, 16 * k2, two ? 16 * k2 + 16 : 16 * k2, m, lane);
+          acc[m] = mma6(fa, bp, acc[m]);
+        }
+      };
+#pragma unroll 1
+      for (int k2 = 0; k2 <= kbl; k2 += 4) {
+        step(k2, dq);
+        if (k2 + 2 <= kbl) step(k2 + 2, dq2);
+      }
+#pragma unroll
+      for (int m = 0; m < NM; ++m) dq[m] += dq2[m];
+      const int j = 16 * qb + li;
+      if (j < K) {
+        float* drow = dQg + (int64_t)(q_off + j) * p.ld + 4 * g;
+#pragma unroll
+        for (int m = 0; m < NM; ++m) *reinterpret_cast<f32x4*>(drow + 16 * m) = dq[m];
+      }
     }
+    SLICE_STAMP(1, it, 5);
+    __syncthreads();                               // LDS is restaged next slice
+    SLICE_STAMP(1, it, 6);
   }
 }
 
-size_t fwd_lds(int I, int hd) { return (size_t)6 * ((I + 15) / 16 * 16) * hd * 2; }
+static int rmax(int hd) { return hd == 64 ? RMAX<64>() : RMAX<32>(); }
+size_t fwd_lds(int I, int hd) { return (size_t)6 * rmax(hd) * hd * 2 + 4 * (size_t)rmax(hd); }
 
 // causal 16 x 16 block pairs of the tail-query backward
 int bwd_pairs(int I, int K) {
   const int nkb = (I + 15) / 16, nqb = (K + 15) / 16, q_off = I - K;
-  int n = 0, f = 0;
-  for (int kb = 0; kb < nkb; ++kb) {
-    while (f < nqb && q_off + std::min(16 * f + 15, K - 1) < 16 * kb) ++f;
-    n += nqb - f;
-  }
+  int n = 0;
+  for (int kb = 0; kb < nkb; ++kb) n += nqb - tail_qf(kb, q_off, nqb);
   return n;
 }
 
 size_t bwd_lds(int I, int K, int hd) {
-  const int IP = (I + 15) / 16 * 16, KP = (K + 15) / 16 * 16;
-  return (size_t)3 * IP * hd * 2 + (size_t)3 * KP * hd * 2 + 12 * (size_t)KP + 8 * MAXKB + 1024 * (size_t)bwd_pairs(I, K);
+  return (size_t)6 * rmax(hd) * hd * 2 + 12 * (size_t)rmax(hd) + 128 + 1024 * (size_t)bwd_pairs(I, K);
+}
+
+// persistent grid: the workgroups that are co-resident (occupancy query, cached per kernel and LDS size),
+// at most one per slice
+static unsigned persistent_grid(const void* kernel, int threads, size_t lds, int64_t slices) {
+  static std::mutex mu;
+  static int cus = 0;
+  static const void* last_k[8] = {};
+  static size_t last_lds[8] = {};
+  static int last_n[8] = {};
+  std::lock_guard<std::mutex> lock(mu);
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  int per = 0;
+  for (int i = 0; i < 8; ++i)
+    if (last_k[i] == kernel && last_lds[i] == lds) per = last_n[i];
+  if (!per) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, threads, lds) != hipSuccess || per <= 0) per = 1;
+    (void)hipGetLastError();
+    for (int i = 0; i < 8; ++i)
+      if (!last_k[i]) { last_k[i] = kernel; last_lds[i] = lds; last_n[i] = per; break; }
+  }
+  return (unsigned)std::min<int64_t>(slices, (int64_t)per * cus);
+}
+
+// LPT over the SIMDs: waves w and w + 4 share SIMD w & 3 (a workgroup's waves go to the SIMDs
+// cyclically, MI355X_MICROARCH.md §LDS), so each item (heaviest first) goes to the least-loaded SIMD,
+// then to its less-loaded wave.  Returns false if a wave would get more than 8 items.
+static bool lpt(int n, const int* load, int nwv, int8_t (&out)[8][8]) {
+  std::memset(out, -1, sizeof out);
+  int sl[4] = {0, 0, 0, 0}, wl[8] = {0, 0, 0, 0, 0, 0, 0, 0}, cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < n; ++i) {
+    int s = 0;
+    for (int k = 1; k < 4; ++k)
+      if (sl[k] < sl[s]) s = k;
+    const int w = nwv == 8 && wl[s + 4] < wl[s] ? s + 4 : s;
+    sl[s] += load[i];
+    wl[w] += load[i];
+    if (cnt[w] == 8) return false;
+    out[w][cnt[w]++] = (int8_t)i;
+  }
+  return true;
+}
+
+// forward: query blocks (heaviest first: the last); backward: key blocks (heaviest first: the first) in
+// query steps of two blocks, then query blocks in steps of two key blocks; costs in MFMA groups
+static bool make_schedule(SliceArgs& p, int hd, int nwv) {
+  const int I = p.I, K = p.K, q_off = I - K, nkb = (I + 15) / 16, nqb = (K + 15) / 16;
+  const int NT = hd / 32, NM = hd / 16;
+  int load[MAXKB];
+  for (int idx = 0; idx < nqb; ++idx) {
+    const int kl = (q_off + std::min(16 * (nqb - 1 - idx) + 15, K - 1)) >> 4;
+    load[idx] = NT * (kl + 1) + NM * (kl / 2 + 1);
+  }
+  if (!lpt(nqb, load, nwv, p.sched[0])) return false;
+  int base = 0;
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int f = tail_qf(kb, q_off, nqb);
+    load[kb] = (nqb - f + 1) >> 1;
+    p.qf[kb] = (int8_t)f;
+    p.bbase[kb] = (int16_t)base;
+    base += nqb - f;
+  }
+  if (!lpt(nkb, load, nwv, p.sched[1])) return false;
+  for (int idx = 0; idx < nqb; ++idx) load[idx] = (((q_off + std::min(16 * (nqb - 1 - idx) + 15, K - 1)) >> 4) + 2) >> 1;
+  return lpt(nqb, load, nwv, p.sched[2]);
 }
 
 static int g_enabled = [] {
@@ -562,13 +696,13 @@ static void raise_lds_limit(F* k) {
 }  // namespace slice
 
 bool attn_slice_fwd_supported(int I, int K, int head_dim) {
-  return slice::g_enabled && (head_dim == 32 || head_dim == 64) && I <= 16 * slice::MAXKB && K > 0 && K <= I &&
+  return slice::g_enabled && (head_dim == 32 || head_dim == 64) && I <= slice::rmax(head_dim) && K > 0 && K <= I &&
          slice::fwd_lds(I, head_dim) <= (size_t)slice::LDS_MAX;
 }
 
 bool attn_slice_bwd_supported(int I, int K, int head_dim, bool selected) {
-  return slice::g_enabled && !selected && (head_dim == 32 || head_dim == 64) && I <= 16 * slice::MAXKB && K > 0 &&
-         K <= I && slice::bwd_lds(I, K, head_dim) <= (size_t)slice::LDS_MAX;
+  return slice::g_enabled && !selected && (head_dim == 32 || head_dim == 64) && I <= slice::rmax(head_dim) &&
+         K > 0 && K <= I && slice::bwd_lds(I, K, head_dim) <= (size_t)slice::LDS_MAX;
 }
 
 int attn_slice_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos, int head_dim,
@@ -576,24 +710,27 @@ int attn_slice_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, con
   using namespace slice;
   static std::once_flag once;
   std::call_once(once, [] {
-    raise_lds_limit(attn_fwd_slice_kernel<32, 8>);
-    raise_lds_limit(attn_fwd_slice_kernel<64, 8>);
-    raise_lds_limit(attn_fwd_slice_kernel<32, 4>);
-    raise_lds_limit(attn_fwd_slice_kernel<64, 4>);
+    for (auto k : {attn_fwd_slice_kernel<32, 8, false, false>, attn_fwd_slice_kernel<32, 8, true, false>,
+                   attn_fwd_slice_kernel<32, 4, false, false>, attn_fwd_slice_kernel<32, 4, true, false>,
+                   attn_fwd_slice_kernel<64, 8, false, true>, attn_fwd_slice_kernel<64, 8, true, true>,
+                   attn_fwd_slice_kernel<64, 4, false, true>, attn_fwd_slice_kernel<64, 4, true, true>})
+      raise_lds_limit(k);
     (void)hipGetLastError();
   });
   SliceArgs p{qkv, ld, H * head_dim, nullptr, nullptr, nullptr, out, lse, nullptr, B, H, I, K,
               1.f / sqrtf((float)head_dim), qpos};
   const size_t lds = fwd_lds(I, head_dim);
   const int nw = g_waves[head_dim == 32 ? 0 : 1] == 4 ? 4 : 8;
-  const dim3 grid((unsigned)((int64_t)B * H)), block(64 * nw);
-  if (head_dim == 32) {
-    if (nw == 4) hipLaunchKernelGGL((attn_fwd_slice_kernel<32, 4>), grid, block, lds, stream, p);
-    else hipLaunchKernelGGL((attn_fwd_slice_kernel<32, 8>), grid, block, lds, stream, p);
-  } else {
-    if (nw == 4) hipLaunchKernelGGL((attn_fwd_slice_kernel<64, 4>), grid, block, lds, stream, p);
-    else hipLaunchKernelGGL((attn_fwd_slice_kernel<64, 8>), grid, block, lds, stream, p);
-  }
+  OT_REQUIRE(make_schedule(p, head_dim, nw), "ot_attn_fwd(slice): schedule");
+  void (*const table[2][2][2])(SliceArgs) = {
+      {{attn_fwd_slice_kernel<32, 4, false, false>, attn_fwd_slice_kernel<32, 4, true, false>},
+       {attn_fwd_slice_kernel<32, 8, false, false>, attn_fwd_slice_kernel<32, 8, true, false>}},
+      {{attn_fwd_slice_kernel<64, 4, false, true>, attn_fwd_slice_kernel<64, 4, true, true>},
+       {attn_fwd_slice_kernel<64, 8, false, true>, attn_fwd_slice_kernel<64, 8, true, true>}}};
+  void (*k)(SliceArgs) = table[head_dim == 64][nw == 8][qpos != nullptr];
+  const unsigned slices = (unsigned)((int64_t)B * H);
+  const dim3 grid(head_dim == 64 ? persistent_grid((const void*)k, 64 * nw, lds, slices) : slices), block(64 * nw);
+  hipLaunchKernelGGL(k, grid, block, lds, stream, p);
   OT_LAUNCH_CHECK("ot_attn_fwd(slice)");
   return OT_OK;
 }
@@ -613,16 +750,20 @@ int attn_slice_bwd(const float* qkv, int64_t ld, const float* out, const float* 
               1.f / sqrtf((float)head_dim), nullptr};
   const size_t lds = bwd_lds(I, K, head_dim);
   const int nw = g_waves[head_dim == 32 ? 2 : 3] == 4 ? 4 : 8;
-  const dim3 grid((unsigned)((int64_t)B * H)), block(64 * nw);
-  if (head_dim == 32) {
-    if (nw == 4) hipLaunchKernelGGL((attn_bwd_slice_kernel<32, 4>), grid, block, lds, stream, p);
-    else hipLaunchKernelGGL((attn_bwd_slice_kernel<32, 8>), grid, block, lds, stream, p);
-  } else {
-    if (nw == 4) hipLaunchKernelGGL((attn_bwd_slice_kernel<64, 4>), grid, block, lds, stream, p);
-    else hipLaunchKernelGGL((attn_bwd_slice_kernel<64, 8>), grid, block, lds, stream, p);
-  }
+  OT_REQUIRE(make_schedule(p, head_dim, nw), "ot_attn_bwd(slice): schedule");
+  void (*k)(SliceArgs) = head_dim == 32 ? (nw == 4 ? attn_bwd_slice_kernel<32, 4> : attn_bwd_slice_kernel<32, 8>)
+                                         : (nw == 4 ? attn_bwd_slice_kernel<64, 4> : attn_bwd_slice_kernel<64, 8>);
+  const dim3 grid(persistent_grid((const void*)k, 64 * nw, lds, (int64_t)B * H)), block(64 * nw);
+  hipLaunchKernelGGL(k, grid, block, lds, stream, p);
   OT_LAUNCH_CHECK("ot_attn_bwd(slice)");
   return OT_OK;
 }
 
 }  // namespace ot
+
+#if OT_SLICE_STAMPS
+extern "C" int ot_slice_stamps_read(unsigned long long* host, size_t bytes) {
+  if (bytes < sizeof(ot::slice::g_slice_stamps)) return -1;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(ot::slice::g_slice_stamps), sizeof(ot::slice::g_slice_stamps)) == hipSuccess ? 0 : -2;
+}
+#endif

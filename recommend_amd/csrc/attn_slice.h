@@ -14,6 +14,11 @@ struct SliceArgs {
   int B, H, I, K;
   float scale;
   const int32_t* qpos;                        // forward only: kept query positions [B*K] or null (tail)
+  // work schedule from the host (attention_slice.hip make_schedule): item of slot s of wave w, -1 = none;
+  // [0] forward query blocks, [1] backward key blocks, [2] backward query blocks (items heaviest first)
+  alignas(8) int8_t sched[3][8][8];            // rows read as one uint64 each (slot s = byte s)
+  int8_t qf[16];                              // backward: first query block that sees key block kb
+  int16_t bbase[16];                          // backward: dS-store block index of (qf[kb], kb)
 };
 
 bool attn_slice_fwd_supported(int I, int K, int head_dim);

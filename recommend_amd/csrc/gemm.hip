@@ -1638,27 +1638,11 @@ __global__ __launch_bounds__(256) void transpose_banks_kernel(const float* __res
   }
 }
 
-// matmul arithmetic of the GEMM family (ot_set_matmul_mode); process-wide, set before launching
-static int g_matmul_mode = OT_MATMUL_SPLIT_BF16;
-// plane GEMM pipeline: 0 = 3 LDS stages at 2 waves / SIMD, 1 = 2 stages at 4 waves / SIMD
-// (tuning switch: environment ONETRANS_PLANE_CFG, read once)
-static int g_plane_cfg = [] {
-  const char* e = getenv("ONETRANS_PLANE_CFG");
-  return e ? atoi(e) : 1;
-}();
 
 }  // namespace ot
 
 using namespace ot;
 
-extern "C" int ot_set_matmul_mode(int mode) {
-  OT_REQUIRE(mode == OT_MATMUL_F32 || mode == OT_MATMUL_SPLIT_BF16 || mode == OT_MATMUL_BF16,
-             "ot_set_matmul_mode: unknown mode %d", mode);
-  g_matmul_mode = mode;
-  return OT_OK;
-}
-
-extern "C" int ot_get_matmul_mode(void) { return g_matmul_mode; }
 
 extern "C" int ot_transpose_banks(const float* src, float* dst, const int64_t* banks_dev, int nbanks,
                                   int64_t total_tiles, void* stream) {
@@ -1681,7 +1665,9 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
                            uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
                            const int32_t* tail_pos,
                            const ot_rms_epilogue* rms, const uint16_t* bimg, int bimg_ntn, int bimg_tn0,
-                           void* stream) {
+                           int prec, void* stream) {
+  OT_REQUIRE(prec == OT_MATMUL_F32 || prec == OT_MATMUL_SPLIT_BF16 || prec == OT_MATMUL_BF16,
+             "ot_mixed_gemm: unknown precision %d", prec);
   OT_REQUIRE(A && W && C, "ot_mixed_gemm: null operand");
   const int rms_flags = epi & (OT_EPI_ROW_RSTD | OT_EPI_RMSNORM_BWD | OT_EPI_ROWDOT);
   OT_REQUIRE(!rms_flags || rms, "ot_mixed_gemm: row-norm epilogue flags need ot_mixed_gemm_rms");
@@ -1700,7 +1686,7 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
   OT_REQUIRE(a_xform != OT_AX_BF16_RMSNORM || (a_rstd && a_gamma),
              "ot_mixed_gemm: OT_AX_BF16_RMSNORM needs rstd / gamma (gamma folded into the B image)");
   OT_REQUIRE((a_xform != OT_AX_BF16 && a_xform != OT_AX_BF16_RMSNORM) ||
-                 (g_matmul_mode == OT_MATMUL_BF16 && bimg && mode == OT_GEMM_NT &&
+                 (prec == OT_MATMUL_BF16 && bimg && mode == OT_GEMM_NT &&
                                        lda % 8 == 0 && ((uintptr_t)A % 16) == 0),
              "ot_mixed_gemm: OT_AX_BF16 (bf16 A) needs the bf16 mode, a B image (plane GEMM), NT mode and 16-B "
              "aligned rows");
@@ -1776,8 +1762,8 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
     p.drop_thr = drop_threshold(drop_rate);
     p.drop_scale = 1.f / (1.f - drop_rate);
   }
-  const bool split = g_matmul_mode != OT_MATMUL_F32 && mode == OT_GEMM_NT;
-  const bool one = g_matmul_mode == OT_MATMUL_BF16;
+  const bool split = prec != OT_MATMUL_F32 && mode == OT_GEMM_NT;
+  const bool one = prec == OT_MATMUL_BF16;
   const size_t shmem = split ? 4 * GT * SRS * sizeof(uint16_t) : 4 * GT * GLD * sizeof(float);
   auto a16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
   const bool vec_ok = ldc % 4 == 0 && a16(C) && (!(epi & OT_EPI_RESIDUAL) || (ldres % 4 == 0 && a16(res))) &&
@@ -1824,7 +1810,7 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
 #define OT_PSPEC(AX_, EP_) \
     if (x == AX_ && e == (EP_)) \
       pk = one ? plane_gemm_kernel<AX_, EP_, PLANE_BF16_NSTG, 4, 1> \
-               : (g_plane_cfg == 0 ? plane_gemm_kernel<AX_, EP_, 3, 2> : plane_gemm_kernel<AX_, EP_, 2, 4>);
+               : plane_gemm_kernel<AX_, EP_, 2, 4>;
     OT_PSPEC(OT_AX_RMSNORM, 0)
     OT_PSPEC(OT_AX_RMSNORM, OT_EPI_BIAS)
     OT_PSPEC(OT_AX_GELU, OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_DROPOUT)
@@ -1896,7 +1882,7 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
   const size_t launch_shmem = !plane ? shmem
                               : one ? std::max((size_t)PLANE_BF16_NSTG * pg_stage_bytes<1>() + xn_lds,
                                                (size_t)(64 * (GT + 4) + 8 * GT) * 4)
-                                    : (size_t)(g_plane_cfg == 0 ? 3 : 2) * PG_STG_BYTES + xn_lds;
+                                    : (size_t)2 * PG_STG_BYTES + xn_lds;
   OT_REQUIRE(kern || !rms_flags, "ot_mixed_gemm_rms: no specialised kernel for epilogue flags %d", epi);
   if (!kern) {   // any other combination: generic instantiation (run-time prologue/epilogue)
     if (mode == OT_GEMM_NT && split && one)
@@ -1943,10 +1929,10 @@ extern "C" int ot_mixed_gemm(int mode, const float* A, int64_t lda, int K, const
                              const float* res, int64_t ldres, int res_tok,
                              const float* aux, int64_t ldaux,
                              uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
-                             const int32_t* tail_pos, void* stream) {
+                             const int32_t* tail_pos, int precision, void* stream) {
   return mixed_gemm_impl(mode, A, lda, K, in_rows, a_xform, a_rstd, a_gamma, W, w_gstride, ldw, N, tile_group,
                          ntiles, bias, bias_gstride, C, ldc, out_rows, epi, res, ldres, res_tok, aux, ldaux, seed,
-                         site, drop_rate, tail_K, tail_I, tail_pos, nullptr, nullptr, 0, 0, stream);
+                         site, drop_rate, tail_K, tail_I, tail_pos, nullptr, nullptr, 0, 0, precision, stream);
 }
 
 extern "C" int ot_mixed_gemm_img(int mode, const float* A, int64_t lda, int K, const int32_t* in_rows,
@@ -1959,10 +1945,10 @@ extern "C" int ot_mixed_gemm_img(int mode, const float* A, int64_t lda, int K, c
                                  const float* aux, int64_t ldaux,
                                  uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
                                  const int32_t* tail_pos, const uint16_t* b_image, int image_ntn, int image_tn0,
-                                 void* stream) {
+                                 int precision, void* stream) {
   return mixed_gemm_impl(mode, A, lda, K, in_rows, a_xform, a_rstd, a_gamma, W, w_gstride, ldw, N, tile_group,
                          ntiles, bias, bias_gstride, C, ldc, out_rows, epi, res, ldres, res_tok, aux, ldaux, seed,
-                         site, drop_rate, tail_K, tail_I, tail_pos, nullptr, b_image, image_ntn, image_tn0, stream);
+                         site, drop_rate, tail_K, tail_I, tail_pos, nullptr, b_image, image_ntn, image_tn0, precision, stream);
 }
 
 extern "C" size_t ot_split_image_elems(int G, int N, int K) {
@@ -1971,11 +1957,13 @@ extern "C" size_t ot_split_image_elems(int G, int N, int K) {
 }
 
 extern "C" int ot_split_images(const float* base, const int64_t* desc_dev, int ndesc, int64_t total_units,
-                               uint16_t* img, void* stream) {
+                               uint16_t* img, int precision, void* stream) {
   OT_REQUIRE(base && desc_dev && img && ndesc > 0 && total_units >= 0, "ot_split_images: bad args");
+  OT_REQUIRE(precision == OT_MATMUL_SPLIT_BF16 || precision == OT_MATMUL_BF16,
+             "ot_split_images: precision %d has no plane images", precision);
   if (total_units == 0) return OT_OK;
   hipLaunchKernelGGL(split_images_kernel, dim3((unsigned)total_units), dim3(256), 0, (hipStream_t)stream, base,
-                     desc_dev, ndesc, img, g_matmul_mode == OT_MATMUL_BF16 ? 1 : 0);
+                     desc_dev, ndesc, img, precision == OT_MATMUL_BF16 ? 1 : 0);
   OT_LAUNCH_CHECK("ot_split_images");
   return OT_OK;
 }
@@ -1994,14 +1982,14 @@ extern "C" int ot_mixed_gemm_rms(int mode, const float* A, int64_t lda, int K, c
                                  const float* res, int64_t ldres, int res_tok,
                                  const float* aux, int64_t ldaux,
                                  uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
-                                 const int32_t* tail_pos, const ot_rms_epilogue* rms, void* stream) {
+                                 const int32_t* tail_pos, const ot_rms_epilogue* rms, int precision, void* stream) {
   OT_REQUIRE(rms, "ot_mixed_gemm_rms: null epilogue operands");
   OT_REQUIRE(rms->struct_size == sizeof(ot_rms_epilogue),
              "ot_mixed_gemm_rms: ot_rms_epilogue.struct_size %zu != %zu (header of another ot_version)",
              rms->struct_size, sizeof(ot_rms_epilogue));
   return mixed_gemm_impl(mode, A, lda, K, in_rows, a_xform, a_rstd, a_gamma, W, w_gstride, ldw, N, tile_group,
                          ntiles, bias, bias_gstride, C, ldc, out_rows, epi, res, ldres, res_tok, aux, ldaux, seed,
-                         site, drop_rate, tail_K, tail_I, tail_pos, rms, nullptr, 0, 0, stream);
+                         site, drop_rate, tail_K, tail_I, tail_pos, rms, nullptr, 0, 0, precision, stream);
 }
 
 extern "C" int ot_mixed_gemm_rms_img(int mode, const float* A, int64_t lda, int K, const int32_t* in_rows,
@@ -2014,20 +2002,16 @@ extern "C" int ot_mixed_gemm_rms_img(int mode, const float* A, int64_t lda, int 
                                      const float* aux, int64_t ldaux,
                                      uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
                                      const int32_t* tail_pos, const ot_rms_epilogue* rms, const uint16_t* b_image,
-                                     int image_ntn, int image_tn0, void* stream) {
+                                     int image_ntn, int image_tn0, int precision, void* stream) {
   OT_REQUIRE(rms, "ot_mixed_gemm_rms: null epilogue operands");
   OT_REQUIRE(rms->struct_size == sizeof(ot_rms_epilogue),
              "ot_mixed_gemm_rms: ot_rms_epilogue.struct_size %zu != %zu (header of another ot_version)",
              rms->struct_size, sizeof(ot_rms_epilogue));
   return mixed_gemm_impl(mode, A, lda, K, in_rows, a_xform, a_rstd, a_gamma, W, w_gstride, ldw, N, tile_group,
                          ntiles, bias, bias_gstride, C, ldc, out_rows, epi, res, ldres, res_tok, aux, ldaux, seed,
-                         site, drop_rate, tail_K, tail_I, tail_pos, rms, b_image, image_ntn, image_tn0, stream);
+                         site, drop_rate, tail_K, tail_I, tail_pos, rms, b_image, image_ntn, image_tn0, precision, stream);
 }
 
-static int g_wgrad_copy = [] {
-  const char* e = std::getenv("ONETRANS_WGRAD_COPY");
-  return e ? std::atoi(e) : 1;
-}();
 
 extern "C" size_t ot_wgrad_workspace_size(int nchunks, int K, int N) {
   return ((size_t)nchunks * K * N + (size_t)nchunks * N) * sizeof(float);
@@ -2038,7 +2022,10 @@ extern "C" int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a
                                    const float* D, int64_t ldd, const int32_t* d_rows, int K, int N,
                                    const int32_t* chunks, int nchunks, const int32_t* gchunk, int ngroups,
                                    float* dW, int64_t dw_gstride, float* db, int64_t db_gstride,
-                                   int accumulate, void* workspace, size_t ws_bytes, void* stream) {
+                                   int accumulate, void* workspace, size_t ws_bytes, int precision,
+                                   void* stream) {
+  OT_REQUIRE(precision == OT_MATMUL_F32 || precision == OT_MATMUL_SPLIT_BF16 || precision == OT_MATMUL_BF16,
+             "ot_mixed_gemm_wgrad: unknown precision %d", precision);
   OT_REQUIRE(A && D && dW && chunks && gchunk && workspace, "ot_mixed_gemm_wgrad: null operand");
   OT_REQUIRE(K % 4 == 0 && N % 4 == 0 && lda % 4 == 0 && ldd % 4 == 0 && dw_gstride % 4 == 0,
              "ot_mixed_gemm_wgrad: K, N, lda, ldd, dw_gstride must be multiples of 4");
@@ -2046,7 +2033,7 @@ extern "C" int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a
   const bool dbf = (a_xform & OT_WG_D_BF16) != 0;
   a_xform &= ~OT_WG_D_BF16;
   OT_REQUIRE(a_xform != OT_AX_RMSNORM || (a_rstd && a_gamma), "ot_mixed_gemm_wgrad: rmsnorm prologue needs rstd/gamma");
-  OT_REQUIRE(!dbf || (g_matmul_mode == OT_MATMUL_BF16 &&
+  OT_REQUIRE(!dbf || (precision == OT_MATMUL_BF16 &&
                       (a_xform == OT_AX_NONE || a_xform == OT_AX_RMSNORM || a_xform == OT_AX_BF16) &&
                       ((uintptr_t)D % 8) == 0),
              "ot_mixed_gemm_wgrad: OT_WG_D_BF16 needs the bf16 mode, A form OT_AX_NONE / OT_AX_RMSNORM and 8-B "
@@ -2058,21 +2045,20 @@ extern "C" int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a
     WgradArgs p{A, lda, a_rows, a_xform, a_rstd, a_gamma, D, ldd, d_rows, K, N, chunks, nchunks, slab, bslab,
                 (int)ceil_div(K, GT), (int)ceil_div(N, GT)};
     const size_t shmem = (OT_WGRAD_DBUF ? 4 : 2) * WBR * WLD * sizeof(float);
-    const bool split = g_matmul_mode != OT_MATMUL_F32;
-    OT_REQUIRE(a_xform != OT_AX_BF16 || (g_matmul_mode != OT_MATMUL_F32 && lda % 4 == 0 && ((uintptr_t)A % 8) == 0),
+    const bool split = precision != OT_MATMUL_F32;
+    OT_REQUIRE(a_xform != OT_AX_BF16 || (precision != OT_MATMUL_F32 && lda % 4 == 0 && ((uintptr_t)A % 8) == 0),
                "ot_mixed_gemm_wgrad: OT_AX_BF16 needs the split / bf16 mode and 8-B aligned rows");
-    // both operands bf16 with whole 16-B column chunks: the copy-staged kernel (ONETRANS_WGRAD_COPY=0: the
-    // register-staged one)
-    const bool copy = dbf && a_xform == OT_AX_BF16 && g_wgrad_copy && K % 8 == 0 && N % 8 == 0 && lda % 8 == 0 &&
+    // both operands bf16 with whole 16-B column chunks: the copy-staged kernel
+    const bool copy = dbf && a_xform == OT_AX_BF16 && K % 8 == 0 && N % 8 == 0 && lda % 8 == 0 &&
                       ldd % 8 == 0 && ((uintptr_t)A % 16) == 0 && ((uintptr_t)D % 16) == 0 && a_rows == d_rows;
     void (*kern)(WgradArgs) =
         copy ? (a_rows ? wgrad_bf16_kernel<true> : wgrad_bf16_kernel<false>)
         : dbf ? (a_xform == OT_AX_NONE      ? wgrad_split_kernel<OT_AX_NONE, 1, true>
                  : a_xform == OT_AX_BF16    ? wgrad_split_kernel<OT_AX_BF16, 1, true>
                                             : wgrad_split_kernel<OT_AX_RMSNORM, 1, true>)
-        : a_xform == OT_AX_BF16 ? (g_matmul_mode == OT_MATMUL_BF16 ? wgrad_split_kernel<OT_AX_BF16, 1>
+        : a_xform == OT_AX_BF16 ? (precision == OT_MATMUL_BF16 ? wgrad_split_kernel<OT_AX_BF16, 1>
                                                                 : wgrad_split_kernel<OT_AX_BF16, SPLIT_TERMS>)
-        : g_matmul_mode == OT_MATMUL_BF16
+        : precision == OT_MATMUL_BF16
             ? (a_xform == OT_AX_NONE      ? wgrad_split_kernel<OT_AX_NONE, 1>
                : a_xform == OT_AX_RMSNORM ? wgrad_split_kernel<OT_AX_RMSNORM, 1>
                : a_xform == OT_AX_GELU    ? wgrad_split_kernel<OT_AX_GELU, 1>

@@ -5,7 +5,11 @@ Pointer arguments accept a tensor, ``(tensor, element_offset)`` or None."""
 
 from __future__ import annotations
 
+import contextlib
 import ctypes
+import functools
+import os
+import threading
 from typing import Optional, Tuple, Union
 
 import torch
@@ -94,18 +98,60 @@ def set_probe(p) -> None:
     _probe = p
 
 
+# Matmul arithmetic is an argument of every GEMM / weight-gradient / plane-image / attention call (the C ABI
+# holds no precision state).  The wrappers below pass the innermost ``precision(...)`` scope of the calling
+# thread (a model enters its own: OneTransModel.matmul, from cfg.compute_dtype), else the process default
+# (``set_matmul_mode``; initially ONETRANS_MATMUL, 'split').
+_default_mode = os.environ.get('ONETRANS_MATMUL', 'split')
+if _default_mode not in _lib.MATMUL_MODES:
+    raise _lib.OneTransHipError(f'ONETRANS_MATMUL={_default_mode!r}: expected one of {sorted(_lib.MATMUL_MODES)}')
+_scope = threading.local()
+
+
 def set_matmul_mode(mode: str) -> str:
-    """GEMM arithmetic: 'split' (exact 3-way bf16 split on bf16 MFMA, f32-accurate) or 'f32'
-    (native f32 MFMA).  Returns the previous mode."""
-    inv = {v: k for k, v in _lib.MATMUL_MODES.items()}
-    old = inv[_lib.load().ot_get_matmul_mode()]
-    call('ot_set_matmul_mode', _lib.MATMUL_MODES[mode])
+    """Process-default GEMM / attention arithmetic for calls outside a ``precision`` scope: 'split' (exact
+    3-way bf16 split on bf16 MFMA, f32-accurate), 'f32' (native f32 MFMA) or 'bf16'.  Returns the previous."""
+    global _default_mode
+    if mode not in _lib.MATMUL_MODES:
+        raise ValueError(f'matmul mode {mode!r}: expected one of {sorted(_lib.MATMUL_MODES)}')
+    old, _default_mode = _default_mode, mode
     return old
 
 
 def matmul_mode() -> str:
-    inv = {v: k for k, v in _lib.MATMUL_MODES.items()}
-    return inv[_lib.load().ot_get_matmul_mode()]
+    """The arithmetic the next call on this thread uses."""
+    st = getattr(_scope, 'stack', None)
+    return st[-1] if st else _default_mode
+
+
+@contextlib.contextmanager
+def precision(mode: str):
+    """Calls on this thread inside the block use ``mode``."""
+    if mode not in _lib.MATMUL_MODES:
+        raise ValueError(f'matmul mode {mode!r}: expected one of {sorted(_lib.MATMUL_MODES)}')
+    st = getattr(_scope, 'stack', None)
+    if st is None:
+        st = _scope.stack = []
+    st.append(mode)
+    try:
+        yield
+    finally:
+        st.pop()
+
+
+def _prec() -> int:
+    return _lib.MATMUL_MODES[matmul_mode()]
+
+
+def in_model_precision(fn):
+    """Run a method of a model (``.matmul``) or of an object holding one (``.m`` / ``.model``) inside that
+    model's ``precision`` scope: every GEMM / attention call it makes carries the model's arithmetic."""
+    @functools.wraps(fn)
+    def wrapped(self, *args, **kw):
+        owner = self if hasattr(self, 'matmul') else getattr(self, 'm', None) or self.model
+        with precision(owner.matmul):
+            return fn(self, *args, **kw)
+    return wrapped
 
 
 def ptr(x: Ptrish):
@@ -156,9 +202,9 @@ def gemm(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish, w_g
             ldw, N, ptr(tile_group), ntiles, ptr(bias), bias_gstride, ptr(C), ldc, ptr(out_rows), epi, ptr(res),
             ldres, res_tok, ptr(aux), ldaux, seed & 0xFFFFFFFF, site, float(drop), tail[0], tail[1], _sel(tail))
     if bimg is not None:
-        call('ot_mixed_gemm_img', *args, ptr(bimg[0]), bimg[1], bimg[2], stream())
+        call('ot_mixed_gemm_img', *args, ptr(bimg[0]), bimg[1], bimg[2], _prec(), stream())
     else:
-        call('ot_mixed_gemm', *args, stream())
+        call('ot_mixed_gemm', *args, _prec(), stream())
     if ev is not None:
         M = m_rows or ntiles * 128
         _probe.end('mixed_gemm', 2.0 * M * K * N, ev, f'gemm mode{mode} ax{a_xform} epi{epi} M{M} K{K} N{N}',
@@ -198,9 +244,9 @@ def gemm_rms(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish,
             ptr(res), ldres, res_tok, ptr(aux), ldaux, seed & 0xFFFFFFFF, site, float(drop), tail[0], tail[1],
             _sel(tail), ctypes.byref(e))
     if bimg is not None:
-        call('ot_mixed_gemm_rms_img', *args, ptr(bimg[0]), bimg[1], bimg[2], stream())
+        call('ot_mixed_gemm_rms_img', *args, ptr(bimg[0]), bimg[1], bimg[2], _prec(), stream())
     else:
-        call('ot_mixed_gemm_rms', *args, stream())
+        call('ot_mixed_gemm_rms', *args, _prec(), stream())
     if ev is not None:
         M = m_rows or ntiles * 128
         extra = (nx is not None) + (dres is not None) + (dx_masked is not None)   # norm-backward operands
@@ -225,7 +271,7 @@ def wgrad(A: Ptrish, lda: int, a_rows: Ptrish, D: Ptrish, ldd: int, d_rows: Ptri
     ev = _probe.begin() if _probe is not None else None
     call('ot_mixed_gemm_wgrad', ptr(A), lda, ptr(a_rows), a_xform, ptr(rstd), ptr(gamma), ptr(D), ldd,
          ptr(d_rows), K, N, ptr(rmap_dev['chunks']), nchunks, ptr(rmap_dev['gchunk']), ngroups, ptr(dW),
-         dw_gstride, ptr(db), db_gstride, int(accumulate), ptr(ws), ws.numel(), stream())
+         dw_gstride, ptr(db), db_gstride, int(accumulate), ptr(ws), ws.numel(), _prec(), stream())
     if ev is not None:
         _probe.end('mixed_gemm', 2.0 * m_rows * K * N, ev, f'wgrad ax{a_xform} M{m_rows} K{K} N{N} ch{nchunks}',
                    (2.0 if (a_xform & ~_lib.OT_WG_D_BF16) == _lib.OT_AX_BF16 else 4.0) * m_rows * K
@@ -242,7 +288,7 @@ def split_image_elems(G: int, N: int, K: int) -> int:
 
 
 def split_images(base, desc_dev, ndesc, total_units, img) -> None:
-    call('ot_split_images', ptr(base), ptr(desc_dev), ndesc, total_units, ptr(img), stream())
+    call('ot_split_images', ptr(base), ptr(desc_dev), ndesc, total_units, ptr(img), _prec(), stream())
 
 
 def attn_fwd(qkv: torch.Tensor, ld: int, B: int, H: int, I: int, K: int, hd: int, out: torch.Tensor,
@@ -267,7 +313,7 @@ def attn_fwd(qkv: torch.Tensor, ld: int, B: int, H: int, I: int, K: int, hd: int
              ws.numel(), (_lib.OT_FP8_DEQUANT if dequant else 0) | (_lib.OT_FP8_TWO_TERM if fp8_terms == 2 else 0),
              stream())
     else:
-        call('ot_attn_fwd', ptr(qkv), ld, B, H, I, K, ptr(qpos), hd, ptr(out), ptr(lse), stream())
+        call('ot_attn_fwd', ptr(qkv), ld, B, H, I, K, ptr(qpos), hd, ptr(out), ptr(lse), _prec(), stream())
     if ev is not None:
         _probe.end('attention', 4.0 * (K * I - K * (K - 1) / 2) * hd * H * B, ev,
                    f'fwd{"_fp8" if fp8 else ""} I{I} K{K} hd{hd}')
@@ -275,12 +321,12 @@ def attn_fwd(qkv: torch.Tensor, ld: int, B: int, H: int, I: int, K: int, hd: int
 
 def attn_bwd_bf16_forms(I, K, hd, qpos=None) -> int:
     """ot_attn_bwd_bf16_forms: the OT_ATTN_*_BF16 flags the backward supports at this shape."""
-    return int(_lib.load().ot_attn_bwd_bf16_forms(I, K, hd, int(qpos is not None)))
+    return int(_lib.load().ot_attn_bwd_bf16_forms(I, K, hd, int(qpos is not None), _prec()))
 
 
 def attn_bwd_bf16_supported(I, K, hd, qpos=None) -> bool:
     """ot_attn_bwd_dqkv_bf16_supported: can the backward emit dqkv in bf16 (key-grouped bf16 kernel)?"""
-    return bool(_lib.load().ot_attn_bwd_dqkv_bf16_supported(I, K, hd, int(qpos is not None)))
+    return bool(_lib.load().ot_attn_bwd_dqkv_bf16_supported(I, K, hd, int(qpos is not None), _prec()))
 
 
 def attn_bwd(qkv, ld, out, dout, lse, B, H, I, K, hd, dqkv, qpos=None, dq_part_bf16: bool = False) -> None:
@@ -290,11 +336,11 @@ def attn_bwd(qkv, ld, out, dout, lse, B, H, I, K, hd, dqkv, qpos=None, dq_part_b
              | (_lib.OT_ATTN_QKV_BF16 if qkv.dtype == torch.int16 else 0)
              | (_lib.OT_ATTN_DQ_PART_BF16 if dq_part_bf16 and dqkv.dtype == torch.int16
                 and attn_bwd_bf16_forms(I, K, hd, qpos) & _lib.OT_ATTN_DQ_PART_BF16 else 0))
-    ws = workspace(size('ot_attn_bwd_flags_workspace_size', B, H, I, K, hd, int(qpos is not None), flags),
+    ws = workspace(size('ot_attn_bwd_flags_workspace_size', B, H, I, K, hd, int(qpos is not None), flags, _prec()),
                    qkv.device)
     ev = _probe.begin() if _probe is not None else None
     call('ot_attn_bwd_flags', ptr(qkv), ld, ptr(out), ptr(dout), ptr(lse), B, H, I, K, ptr(qpos), hd, ptr(dqkv),
-         flags, ptr(ws), ws.numel(), stream())
+         flags, ptr(ws), ws.numel(), _prec(), stream())
     if ev is not None:
         _probe.end('attention', 8.0 * (K * I - K * (K - 1) / 2) * hd * H * B, ev, f'bwd I{I} K{K} hd{hd}')
 

@@ -71,6 +71,12 @@ class _Tokenize(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dx0):
+        # the autograd engine runs this on its own thread: enter the model's precision there
+        with K.precision(ctx.m.matmul):
+            return _Tokenize._backward(ctx, dx0)
+
+    @staticmethod
+    def _backward(ctx, dx0):
         m, plan = ctx.m, ctx.plan
         if plan['gen'] != ctx.gen:
             raise RuntimeError('OneTransModel: a second forward with the same input shapes ran before this '
@@ -326,6 +332,12 @@ class _Block(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dx2, _drstd=None):
+        # the autograd engine runs this on its own thread: enter the model's precision there
+        with K.precision(ctx.m.matmul):
+            return _Block._backward(ctx, dx2, _drstd)
+
+    @staticmethod
+    def _backward(ctx, dx2, _drstd=None):
         m, l, I, Kq, seed, rate = ctx.m, ctx.l, ctx.I, ctx.Kq, ctx.seed, ctx.rate
         pos, inv = ctx.pos, ctx.inv
         if m.recompute:
@@ -509,6 +521,12 @@ class _Head(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dprobs):
+        # the autograd engine runs this on its own thread: enter the model's precision there
+        with K.precision(ctx.m.matmul):
+            return _Head._backward(ctx, dprobs)
+
+    @staticmethod
+    def _backward(ctx, dprobs):
         x, rstd, y, pre1, probs = ctx.saved_tensors
         m = ctx.m
         cfg = m.config
@@ -579,6 +597,9 @@ def keras_bce_loss(labels: torch.Tensor, probs: torch.Tensor, tasks=None) -> tor
 
 
 # =============================================================================== the module
+in_model_precision = K.in_model_precision
+
+
 class OneTransModel(nn.Module):
     """model.py:305-408 on MI355X (see module docstring)."""
 
@@ -593,13 +614,17 @@ class OneTransModel(nn.Module):
         if cfg.hidden_dim % cfg.num_heads or (cfg.hidden_dim // cfg.num_heads) not in (16, 32, 64, 128):
             raise ValueError('head_dim must be 16, 32, 64 or 128')
         check_pyramid_select(cfg)
-        # compute_dtype (build knob): 'fp32' (the reference's arithmetic; GEMM precision is the process-wide
-        # ot_set_matmul_mode / ONETRANS_MATMUL), 'bf16', or 'fp8attn' = BASELINE configs[4]'s attention on
+        # compute_dtype (build knob): 'fp32' (the reference's arithmetic: split or f32 GEMMs, ``matmul`` below),
+        # 'bf16', or 'fp8attn' = BASELINE configs[4]'s attention on
         # block-scaled fp8 MFMA (forward QK^T and PV; the backward recomputes in the GEMM mode's precision from
         # the dequantised fp8 operands the training forward leaves in qkv: the straight-through gradient).
         # ONETRANS_ATTN=fp8 selects the fp8 forward too.
         if getattr(cfg, 'compute_dtype', 'fp32') not in ('fp32', 'bf16', 'fp8attn'):
             raise ValueError(f"compute_dtype {cfg.compute_dtype!r}: expected 'fp32', 'bf16' or 'fp8attn'")
+        # this model's GEMM / attention arithmetic, passed with every kernel call it makes (the C ABI holds no
+        # precision state): 'bf16' for the reduced-precision configs, else the process default at construction
+        # ('split', f32-accurate; kernels.set_matmul_mode / ONETRANS_MATMUL)
+        self.matmul = 'bf16' if getattr(cfg, 'compute_dtype', 'fp32') in ('bf16', 'fp8attn') else K.matmul_mode()
         # activation recompute (config.recompute_blocks / ONETRANS_RECOMPUTE=1): a block keeps only its
         # input for backward and re-runs its forward kernels there (_Block)
         self.recompute = bool(getattr(cfg, 'recompute_blocks', False)) or os.environ.get('ONETRANS_RECOMPUTE') == '1'
@@ -699,7 +724,7 @@ class OneTransModel(nn.Module):
             dist_on = dist.is_available() and dist.is_initialized()
             st = ShardedTable('emb.seq_item', cfg.seq_item_vocab, cfg.seq_feature_dim,
                               dist.get_world_size() if dist_on else 1, dist.get_rank() if dist_on else 0,
-                              self.device, seed=seed + 2, full_init=full)
+                              self.device, seed=seed + 2, full_init=full, route_stream=self.comm_stream())
             self.sharded['emb.seq_item'] = st
             self.tables['emb.seq_item'] = st.table
         self.load_param_dict(params)
@@ -716,6 +741,7 @@ class OneTransModel(nn.Module):
     def pT(self, name):
         return self.layout.tview(self.flatT, name)
 
+    @in_model_precision
     def refresh_shadow(self) -> None:
         """Re-derive the transposed weight banks after any change of the weights (init, load, optimizer)."""
         K.transpose_banks(self.flat.data, self.flatT, self._tdesc, self.layout.transpose_desc.shape[0],
@@ -1029,6 +1055,7 @@ class OneTransModel(nn.Module):
         probs = self.forward_probs(non_seq_features, seq_features, training)
         return {t: probs[i].view(-1, 1) for i, t in enumerate(self.config.tasks)}
 
+    @in_model_precision
     def forward_probs(self, ns, seq, training: bool) -> torch.Tensor:
         """All tasks as one [T, B] tensor (the trainer's fused loss consumes it)."""
         plan = self._plan(ns, seq)
@@ -1059,6 +1086,15 @@ class OneTransModel(nn.Module):
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
             return dist.get_rank() * B
         return 0
+
+    # ---------------------------------------------------------------- streams
+    def comm_stream(self):
+        """The communication stream: the dense gradient all-reduces (OneTransOptimizer) and the row-sharded
+        tables' id routing share it, so a rank drives four hardware queues (GPU_MAX_HW_QUEUES = 4): the main
+        stream, the weight-gradient side stream, this one and RCCL's internal stream."""
+        if getattr(self, '_comm', None) is None:
+            self._comm = torch.cuda.Stream(device=self.device)
+        return self._comm
 
     # ---------------------------------------------------------------- side stream (wgrad overlap)
     def side(self, *tensors):

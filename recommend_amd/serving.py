@@ -122,6 +122,7 @@ class OneTransServer:
 
     # ------------------------------------------------------------------ stage I
     @torch.no_grad()
+    @K.in_model_precision
     def encode_requests(self, seq_features: Dict[str, torch.Tensor]) -> RequestCache:
         """Tokenize the requests' sequences (model.py:256-277) and run the S side of every layer;
         cache each layer's S-side K/V."""
@@ -156,6 +157,7 @@ class OneTransServer:
 
     # ------------------------------------------------------------------ cross-request append
     @torch.no_grad()
+    @K.in_model_precision
     def extend_requests(self, cache: RequestCache, seq_name: str, new_events: torch.Tensor) -> RequestCache:
         """Cross-request KV cache (paper §3.5.1): the requests' newest behaviours ``new_events``
         ([R, dL, 64] features or [R, dL] ids) are appended to sequence ``seq_name`` and only the new
@@ -207,6 +209,7 @@ class OneTransServer:
 
     # ------------------------------------------------------------------ stage II
     @torch.no_grad()
+    @K.in_model_precision
     def score(self, cache: RequestCache, req: torch.Tensor, non_seq_features: Dict[str, torch.Tensor]):
         """Candidates' NS tokens (model.py:239-254) through every layer against their request's cache;
         returns {task: probs [C, 1]} like ``OneTransModel.forward`` (model.py:384-391)."""
@@ -245,6 +248,7 @@ class OneTransServer:
         return {t: probs[i].view(-1, 1) for i, t in enumerate(cfg.tasks)}
 
     @torch.no_grad()
+    @K.in_model_precision
     def predict(self, non_seq_features, seq_features, req: Optional[torch.Tensor] = None):
         """One call: ``seq_features`` hold R requests, ``non_seq_features`` C candidates, ``req`` [C] maps
         candidates to requests (default: candidate i belongs to request i, R == C)."""

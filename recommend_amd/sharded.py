@@ -18,11 +18,14 @@ transformer stays data-parallel; only the table is partitioned:
 
 All bytes move on device; the only host traffic is the ``world`` split sizes the all-to-alls need.  That
 one host wait is taken off the main stream: the ids are staged, routed and their per-owner counts
-exchanged on the table's own route stream (host ids are copied there; device ids wait only for the event
-the caller names as their producer, ``ready``), so the host waits for those few kernels — not for the
-previous step's backward and optimizer still queued on the main stream — and the GPU keeps running them
-while it does.  The gather that follows stays on the main stream (it reads the table the previous step's
-sparse update wrote).
+exchanged on the route stream — the model's communication stream (host ids are copied there; device ids
+wait only for the event the caller names as their producer, ``ready``), so the host waits for those few
+kernels — not for the previous step's backward and optimizer still queued on the main stream — and the GPU
+keeps running them while it does (measured at world 1; at world > 1 the counts' all-to-all also queues
+behind earlier collectives on RCCL's stream, unmeasured on hardware).  The gather that follows stays on the
+main stream (it reads the table the previous step's sparse update wrote).  A fixed-capacity exchange with no
+host sizes was considered: the only sound per-peer bound is the batch's id count n, and the rows coming
+back would then move world x n x E x 4 bytes — ~20x the distinct rows at C4 / N = 8.
 """
 
 from __future__ import annotations
@@ -49,7 +52,7 @@ class _nullctx:
 class ShardedTable:
     def __init__(self, name: str, num_rows: int, E: int, world: int, rank: int, device, seed: int = 0,
                  full_init: Optional[np.ndarray] = None, lo: float = -0.05, hi: float = 0.05,
-                 dedup: Optional[bool] = None):
+                 dedup: Optional[bool] = None, route_stream=None):
         if dedup is None:
             dedup = os.environ.get('ONETRANS_SHARD_DEDUP', '1') != '0'
         self.dedup = bool(dedup)
@@ -69,9 +72,11 @@ class ShardedTable:
         self.last_route = None
         self.sent_rows = 0         # ids (rows) the last lookup sent to their owners
         is_cuda = torch.device(device).type == 'cuda'
-        # ONETRANS_ROUTE_STREAM=0: route on the current stream (the host wait then drains it; A/B switch)
-        side = is_cuda and os.environ.get('ONETRANS_ROUTE_STREAM', '1') != '0'
-        self.route_stream = torch.cuda.Stream(device=device) if side else None
+        # the stream the ids are staged / routed on: the owning model's communication stream (shared with the
+        # dense gradient exchange, so a rank drives main + weight-gradient side + comm + RCCL's internal
+        # stream = GPU_MAX_HW_QUEUES 4 hardware queues), or a stream of its own when used standalone
+        self.route_stream = route_stream if route_stream is not None else (
+            torch.cuda.Stream(device=device) if is_cuda else None)
         self._counts_host = torch.empty(2 * self.world, dtype=torch.int32, pin_memory=is_cuda)
         self.events = None        # diagnostics: a list collects HIP-event pairs around lookup / update
 

@@ -130,7 +130,7 @@ class OneTransOptimizer:
             return
         if not hasattr(self, '_ranges'):
             self._ranges = self.bank_ranges()
-            self._comm = torch.cuda.Stream(device=m.flat.device)
+            self._comm = m.comm_stream()
         self._works = []
         m.grad_ready = self._launch
 

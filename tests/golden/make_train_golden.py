@@ -3,9 +3,11 @@
 steps"), computed by the CPU oracle (oracle/onetrans_ref.py, float64) in the build container:
 
     python tests/golden/make_train_golden.py      # -> tests/golden/train_C2.npz
+    python tests/golden/make_train_golden.py T    # -> tests/golden/train_T.npz (north_star's attention
+                                                  #    shape: d 256, head_dim 64, for the bf16 / fp8attn runs)
 
 The run: the C2 model shape (4L d128 H4 f512, L_NS 12, L0 140, the C2 embedding tables with hash
-values, tests/fullsize_common.py), perturbed Keras init (seed 0), STEPS train steps of B = 512 fresh
+values, tests/fullsize_common.py; T: d 256 f 1024, the same tables), perturbed Keras init (seed 0), STEPS train steps of B = 512 fresh
 Criteo-shape batches (seeds 5000 + i, teacher labels, dropout on with the model's step seeds), the
 parity optimizer settings of setup_config (per-variable clip + RMSprop(momentum), clipped sparse
 Adagrad; train.py:111-138).  Then the held-out batch (4096 samples, seed 6000) in inference mode.
@@ -41,7 +43,8 @@ EVAL_SEED = 6000
 
 def main() -> None:
     t0 = time.time()
-    cfg = setup_config('C2')
+    name = sys.argv[1] if len(sys.argv) > 1 else 'C2'
+    cfg = setup_config(name)
     P = init_params(cfg, cfg.ns_input_width(), seed=MODEL_SEED, perturb=True, with_tables=False)
     batches = [make_batch(B_TRAIN, cfg, seed=TRAIN_SEED0 + i) for i in range(STEPS)]
     batches.append(make_batch(B_EVAL, cfg, seed=EVAL_SEED))
@@ -79,7 +82,7 @@ def main() -> None:
         idx = bank_samples(k, w.size)
         res[f'w_idx.{k}'] = idx
         res[f'w.{k}'] = w[idx]
-    out_path = os.path.join(HERE, 'train_C2.npz')
+    out_path = os.path.join(HERE, f'train_{name}.npz')
     np.savez_compressed(out_path, **res)
     print(f'wrote {out_path} ({os.path.getsize(out_path) / 1e6:.1f} MB, {time.time() - t0:.0f}s)')
 

@@ -45,17 +45,19 @@ def test_library_exports_every_symbol():
 def test_errors_are_reported_not_crashing():
     """Invalid arguments return OT_ERR_INVALID_ARG with a message (no device work)."""
     with pytest.raises(_lib.OneTransHipError, match='null operand'):
-        _lib.call('ot_attn_fwd', None, 96, 1, 1, 4, 4, None, 32, None, None, None)
+        _lib.call('ot_attn_fwd', None, 96, 1, 1, 4, 4, None, 32, None, None, 1, None)
     with pytest.raises(_lib.OneTransHipError, match='multiples of 4'):
         _lib.call('ot_mixed_gemm', 0, 8, 3, 3, None, 0, None, None, 8, 0, 4, 4, None, 1, None, 0, 8, 4, None, 0,
-                  None, 0, 0, None, 0, 0, 0, 0.0, 1, 1, None, None)
+                  None, 0, 0, None, 0, 0, 0, 0.0, 1, 1, None, 1, None)
+    with pytest.raises(_lib.OneTransHipError, match='unknown precision'):
+        _lib.call('ot_attn_fwd', None, 96, 1, 1, 4, 4, None, 32, None, None, 7, None)
     # an ot_rms_epilogue from another header version (struct_size differs) is refused, not read past its end
     import ctypes
     e = _lib.RmsEpilogue()
     e.struct_size = ctypes.sizeof(_lib.RmsEpilogue) - 24
     with pytest.raises(_lib.OneTransHipError, match='struct_size'):
         _lib.call('ot_mixed_gemm_rms', 0, None, 128, 128, None, 0, None, None, None, 0, 128, 128, None, 1, None, 0,
-                  None, 128, None, 0, None, 0, 0, None, 0, 0, 0, 0.0, 1, 1, None, ctypes.byref(e), None)
+                  None, 128, None, 0, None, 0, 0, None, 0, 0, 0, 0.0, 1, 1, None, ctypes.byref(e), 1, None)
     with pytest.raises(_lib.OneTransHipError, match='bad sizes'):
         _lib.call('ot_pyramid_select', None, 1.0, 2, 8, 9, 0, 8, None, None, 0, None)    # K > I
     with pytest.raises(_lib.OneTransHipError, match='bad sizes'):

@@ -41,7 +41,7 @@ def _random_map(rng, n_in, n_out, G, counts):
 
 @pytest.fixture(params=['split', 'f32'])
 def matmul(request, dev):
-    """Run a GEMM test under both matmul modes (ot_set_matmul_mode)."""
+    """Run a GEMM test under both matmul modes (kernels.set_matmul_mode: the precision argument of each call)."""
     old = K.set_matmul_mode(request.param)
     yield request.param
     K.set_matmul_mode(old)
@@ -650,7 +650,7 @@ def test_attn_bwd_key_slices(dev, B, H, I, Kq, hd):
     from recommend_amd import _lib
     old = K.set_matmul_mode('bf16')
     try:
-        S_ws = _lib.load().ot_attn_bwd_ex_workspace_size(B, H, I, Kq, hd, 0)
+        S_ws = _lib.load().ot_attn_bwd_ex_workspace_size(B, H, I, Kq, hd, 0, _lib.OT_MATMUL_BF16)
         assert S_ws > K.size('ot_attn_bwd_workspace_size', B, H, Kq)       # slices are used
         g = torch.Generator().manual_seed(I + Kq)
         d = H * hd
@@ -667,7 +667,7 @@ def test_attn_bwd_key_slices(dev, B, H, I, Kq, hd):
             else:
                 ws = K.workspace(K.size('ot_attn_bwd_workspace_size', B, H, Kq), dev)
                 K.call('ot_attn_bwd', K.ptr(qkv), 3 * d, K.ptr(out), K.ptr(dout), K.ptr(lse), B, H, I, Kq, None,
-                       hd, K.ptr(dqkv), K.ptr(ws), K.stream())
+                       hd, K.ptr(dqkv), K.ptr(ws), _lib.OT_MATMUL_BF16, K.stream())
             torch.cuda.synchronize()
             res.append(dqkv.cpu())
         a, b = res
@@ -818,43 +818,3 @@ def test_attn_bwd_small_bf16_dqkv(dev, K_):
     assert torch.equal(d16, d32.to(torch.bfloat16).view(torch.int16))
 
 
-_FDL_CHILD = r'''
-import sys, torch
-sys.path.insert(0, sys.argv[1])
-from recommend_amd import kernels as K
-B, H, I, Kq, hd = 4, 4, 140, 100, 32
-d = H * hd
-g = torch.Generator().manual_seed(7)
-qkv = torch.randn(B * I, 3 * d, generator=g).cuda()
-dout = torch.randn(B * Kq, d, generator=g).cuda()
-out = torch.empty(B * Kq, d, device='cuda')
-lse = torch.empty(B * H * Kq, device='cuda')
-K.attn_fwd(qkv, 3 * d, B, H, I, Kq, hd, out, lse)
-dqkv = torch.zeros(B * I, 3 * d, device='cuda')
-K.attn_bwd(qkv, 3 * d, out, dout, lse, B, H, I, Kq, hd, dqkv)
-torch.cuda.synchronize()
-torch.save(dqkv.cpu(), sys.argv[2])
-'''
-
-
-def test_attn_bwd_row_stats_in_kernel_matches_prep(dev, tmp_path):
-    """The hd-32 backward's in-kernel row statistics (default) against the prep-kernel form
-    (ONETRANS_ATTN_BWD_FDL=0, read once per process: run in a child process): the same gradient up to the
-    f32 summation order of delta = rowsum(dO * O)."""
-    import os
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    script = tmp_path / 'fdl_child.py'
-    script.write_text(_FDL_CHILD)
-    res = {}
-    for v in ('1', '0'):
-        outp = tmp_path / f'dqkv_{v}.pt'
-        env = dict(os.environ, ONETRANS_ATTN_BWD_FDL=v)
-        r = subprocess.run([sys.executable, str(script), root, str(outp)], env=env, stdout=subprocess.PIPE,
-                           stderr=subprocess.STDOUT, timeout=150)
-        assert r.returncode == 0, r.stdout.decode()[-2000:]
-        res[v] = torch.load(str(outp), weights_only=True)
-    a, b = res['1'].double(), res['0'].double()
-    assert torch.isfinite(a).all()
-    assert (a - b).abs().max().item() <= 1e-5 * max(1.0, b.abs().max().item())

@@ -246,6 +246,39 @@ def test_bf16_mode_forward_and_train(dev, dtype):
         K.set_matmul_mode(old)
 
 
+def test_two_precisions_in_one_process(dev):
+    """Precision is a property of each model (the C ABI takes it per call; no process-wide mode): an f32-
+    accurate model and a bf16 model built in one process, their forwards and backwards interleaved, each
+    within its own bound of the f64 oracle (2e-4 for the split mode, 2e-2 for bf16) — and the f32 model's
+    result is bit-identical to a run with no bf16 model around."""
+    from recommend_amd import kernels as K
+    cfg32 = small_criteo('head', d=128, H=4, f=256, Lns=12, seq_lens=(20, 20, 20))
+    cfg16 = small_criteo('head', d=128, H=4, f=256, Lns=12, seq_lens=(20, 20, 20))
+    cfg16.compute_dtype = 'bf16'
+    assert K.matmul_mode() == 'split'
+    P, m32, batch = setup(cfg32, 37, dev)
+    _, m16, _ = setup(cfg16, 37, dev)
+    assert (m32.matmul, m16.matmul) == ('split', 'bf16')
+    ns, seq, lab = batch
+    ref = oracle_out(P, cfg32, batch)
+    y = stack_labels(lab, cfg32.tasks, dev)
+    alone = None
+    for rnd in range(2):
+        outs = {}
+        for name, m in (('f32', m32), ('bf16', m16)) if rnd == 0 else (('bf16', m16), ('f32', m32)):
+            m.flat.grad.zero_()
+            probs = m.forward_probs(ns_t(ns, dev), ns_t(seq, dev), training=False)
+            keras_bce_loss(y, probs, cfg32.tasks).backward()
+            outs[name] = (probs.double().cpu().numpy(), m.flat.grad.clone())
+        for i, t in enumerate(cfg32.tasks):
+            np.testing.assert_allclose(outs['f32'][0][i], ref['probs'][t].numpy()[:, 0], atol=LOGIT_TOL / 4, rtol=0)
+            np.testing.assert_allclose(outs['bf16'][0][i], ref['probs'][t].numpy()[:, 0], atol=2e-2, rtol=0)
+        assert np.abs(outs['f32'][0] - outs['bf16'][0]).max() > 1e-6         # the bf16 model really ran bf16
+        if alone is None:
+            alone = outs['f32']
+        assert np.array_equal(outs['f32'][0], alone[0]) and torch.equal(outs['f32'][1], alone[1])
+
+
 @pytest.mark.parametrize('d,f', [(128, 320), (256, 320)])
 def test_bf16_mode_ffn_width_without_plane_image(dev, d, f):
     """bf16 mode with an FFN width that is not a multiple of the 128-column tile: W1 has no plane image,

@@ -14,11 +14,19 @@ for r in rows:
     name = name if len(name) < 80 else name[:77] + '...'
     print(f"| `{name}` | {r['Calls']} | {float(r['AverageNs'])/1e3:.1f} | {t/1e6/steps:.3f} | {100*t/tot:.1f} |")
 print(f'| **total** | | | {tot/1e6/steps:.3f} | 100 |')
-# the bench's roofline family (mixed_gemm_kernel / plane_gemm_kernel + wgrad_kernel): average launch, to compare with
-# bench.py's roofline.avg_launch_us
-fam = [r for r in rows if 'mixed_gemm_kernel' in r['Name'] or 'plane_gemm_kernel' in r['Name'] or ('wgrad_kernel<' in r['Name'] or 'wgrad_split_kernel<' in r['Name'])]
+# the bench's roofline family: every kernel a GEMM call of kernels.gemm / gemm_rms / gemm_wgrad launches (the
+# bench brackets each call with HIP events, so the call's small reduce launches are inside its time): the
+# GEMM kernels (mixed / plane, wgrad / wgrad_split / wgrad_bf16) and their helpers (wgrad_reduce_kernel,
+# row_rstd_finish_kernel, the fused-norm dgamma colsum; the row-wise RMSNorm backward's dgamma uses the
+# same colsum kernels, a small overcount).  'main' launches compare with the bench's
+# roofline.launches_per_step (one per call), the time with its kernel_time_ms_per_step.mixed_gemm.
+MAIN = ('mixed_gemm_kernel', 'plane_gemm_kernel', 'wgrad_kernel<', 'wgrad_split_kernel<', 'wgrad_bf16_kernel')
+HELP = ('wgrad_reduce_kernel', 'row_rstd_finish_kernel', 'colsum_reduce_kernel', 'colsum_chunk_kernel')
+fam = [r for r in rows if any(k in r['Name'] for k in MAIN)]
+hlp = [r for r in rows if any(k in r['Name'] for k in HELP)]
 ft, fn = sum(float(r['TotalDurationNs']) for r in fam), sum(int(r['Calls']) for r in fam)
+ht = sum(float(r['TotalDurationNs']) for r in hlp)
 if fn:
-    print(f'\nGEMM family (mixed/plane_gemm_kernel + wgrad[_split]_kernel): {fn / steps:.1f} launches/step, '
-          f'avg {ft / fn / 1e3:.1f} us/launch, {ft / 1e6 / steps:.3f} ms/step')
-
+    print(f'\nGEMM family (mixed/plane_gemm_kernel + wgrad/_split/_bf16_kernel): {fn / steps:.1f} launches/step, '
+          f'avg {ft / fn / 1e3:.1f} us/launch, {ft / 1e6 / steps:.3f} ms/step; with the helper kernels '
+          f'(wgrad_reduce, row_rstd_finish, colsum) {(ft + ht) / 1e6 / steps:.3f} ms/step')

@@ -246,6 +246,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_slice_kernel(SliceArgs p
       const int j = 16 * qb + li;                                    // this lane's query
       const int qpos = qpos_of(j < K ? j : K - 1);
       const int kbl = qpos_of(min(16 * qb + 15, K - 1)) >> 4;        // last visible key block
+      const int kbm = qpos_of(16 * qb) >> 4;                          // key blocks >= kbm may be masked
       u32x4 qp[NT][3];
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
@@ -269,11 +270,11 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_slice_kernel(SliceArgs p
           row_frag<HD>(fk, kimg, PB, 16 * kb + li, t, g);
           acc = mma6(fk, qp[t], acc);                                 // S^T: row = key, col = query
         }
+        if (kb >= kbm) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          acc[i] = (16 * kb + 4 * g + i <= qpos) ? acc[i] : -INFINITY;
-          mx = fmaxf(mx, acc[i]);
+          for (int i = 0; i < 4; ++i) acc[i] = (16 * kb + 4 * g + i <= qpos) ? acc[i] : -INFINITY;
         }
+        mx = fmaxf(mx, fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3])));
         sc[kb] = acc;
       }
       mx = group_max(mx);
@@ -340,7 +341,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_slice_kernel(SliceArgs p
 //   from global — L2-warm — into the Q planes' space).
 // Loads in flight during compute: the next key block's K / V (phase 1), the K image rows (issued by each
 // wave as it leaves phase 1), and the next slice's Q / dO / O rows, lse and first K / V (phase 2).
-template <int HD, int NWV>
+// PFPOS: where the next slice's loads are issued — 0: before phase 2 (overlapping it), 1: after it
+template <int HD, int NWV, int PFPOS>
 __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NT = HD / 32, NM = HD / 16, CPR = HD / 8, NTH = 64 * NWV;
@@ -455,9 +457,37 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
 #pragma unroll
       for (int m = 0; m < NM; ++m) dk[m] = dv[m] = f32x4{0.f, 0.f, 0.f, 0.f};
       const int a0 = tab[kb], blk0 = tab[16 + kb];
+      // S and dP of query step a (blocks a, a + 1; the second zero past the last block)
+      auto sdp = [&](int a, f32x4 (&sc)[2], f32x4 (&dc)[2]) {
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          const int qb = a + half;
+          sc[half] = dc[half] = f32x4{0.f, 0.f, 0.f, 0.f};
+          if (half == 1 && qb >= nqb) continue;
+#pragma unroll
+          for (int t = 0; t < NT; ++t) {
+            u32x4 fa[3], fb[3];
+            row_frag<HD>(fa, qimg, PB, 16 * qb + li, t, g);
+            row_frag<HD>(fb, oimg, PB, 16 * qb + li, t, g);
+            sc[half] = mma6(fa, kp[t], sc[half]);                     // S: row = query, col = key
+            dc[half] = mma6(fb, vp[t], dc[half]);                     // dP
+          }
+        }
+      };
+      // PIPE (one wave per SIMD, 512 registers): step a + 2's S / dP products are issued before step a's
+      // softmax gradient, so the wave's VALU work overlaps its own MFMAs
+      constexpr bool PIPE = NWV == 4;
+      f32x4 sc[2], dc[2];
+      if (PIPE && a0 < nqb) sdp(a0, sc, dc);
 #pragma unroll 1
       for (int a = a0; a < nqb; a += 2) {
         const bool two = a + 1 < nqb;
+        f32x4 sn[2], dn[2];
+        if (PIPE) {
+          if (a + 2 < nqb) sdp(a + 2, sn, dn);
+        } else {
+          sdp(a, sc, dc);
+        }
         float P[8], dS[8];
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
@@ -465,15 +495,6 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
 #pragma unroll
           for (int i = 0; i < 4; ++i) P[4 * half + i] = dS[4 * half + i] = 0.f;
           if (half == 1 && !two) continue;
-          f32x4 sacc = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int t = 0; t < NT; ++t) {
-            u32x4 fa[3], fb[3];
-            row_frag<HD>(fa, qimg, PB, 16 * qb + li, t, g);
-            row_frag<HD>(fb, oimg, PB, 16 * qb + li, t, g);
-            sacc = mma6(fa, kp[t], sacc);                             // S: row = query, col = key
-            dp = mma6(fb, vp[t], dp);                                 // dP
-          }
           const int q0 = 16 * qb + 4 * g;
           const f32x4 L = *reinterpret_cast<const f32x4*>(lse2 + q0);
           const f32x4 D = *reinterpret_cast<const f32x4*>(dlt + q0);
@@ -481,9 +502,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
           char* blk = dss + 1024 * (blk0 + qb - a0);
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float e = __builtin_amdgcn_exp2f(fmaf(sacc[i], c1, -L[i]));
+            const float e = __builtin_amdgcn_exp2f(fmaf(sc[half][i], c1, -L[i]));
             const float pv = krow <= Qp[i] ? e : 0.f;
-            const float ds = pv * (dp[i] - D[i]) * p.scale;
+            const float ds = pv * (dc[half][i] - D[i]) * p.scale;
             P[4 * half + i] = pv;
             dS[4 * half + i] = ds;
             *reinterpret_cast<float*>(blk + poff<32>(4 * g + i, li >> 2) + 4 * (li & 3)) = ds;
@@ -500,6 +521,10 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
           tr_frag<HD>(fb, qimg, PB, 16 * a, rb, m, lane);
           dv[m] = mma6(fa, pp, dv[m]);                                // dV^T += dO^T P
           dk[m] = mma6(fb, sp, dk[m]);                                // dK^T += Q^T dS
+        }
+        if (PIPE) {
+#pragma unroll
+          for (int h2 = 0; h2 < 2; ++h2) { sc[h2] = sn[h2]; dc[h2] = dn[h2]; }
         }
       }
       if (krow < I) {
@@ -535,7 +560,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
     }
     __syncthreads();
     SLICE_STAMP(1, it, 4);
-    if (s + (int)gridDim.x < nslices) prefetch(s + gridDim.x);   // next slice, in flight during phase 2
+    if (PFPOS == 0 && s + (int)gridDim.x < nslices) prefetch(s + gridDim.x);   // next slice, during phase 2
 
     // ---- phase 2: query-block owners, dQ^T = K^T dS^T
 #pragma unroll 1
@@ -585,6 +610,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
       }
     }
     SLICE_STAMP(1, it, 5);
+    if (PFPOS == 1 && s + (int)gridDim.x < nslices) prefetch(s + gridDim.x);
     __syncthreads();                               // LDS is restaged next slice
     SLICE_STAMP(1, it, 6);
   }
@@ -740,10 +766,10 @@ int attn_slice_bwd(const float* qkv, int64_t ld, const float* out, const float* 
   using namespace slice;
   static std::once_flag once;
   std::call_once(once, [] {
-    raise_lds_limit(attn_bwd_slice_kernel<32, 8>);
-    raise_lds_limit(attn_bwd_slice_kernel<64, 8>);
-    raise_lds_limit(attn_bwd_slice_kernel<32, 4>);
-    raise_lds_limit(attn_bwd_slice_kernel<64, 4>);
+    for (auto k : {attn_bwd_slice_kernel<32, 8, 0>, attn_bwd_slice_kernel<64, 8, 0>, attn_bwd_slice_kernel<32, 4, 0>,
+                   attn_bwd_slice_kernel<64, 4, 0>, attn_bwd_slice_kernel<32, 8, 1>, attn_bwd_slice_kernel<64, 8, 1>,
+                   attn_bwd_slice_kernel<32, 4, 1>, attn_bwd_slice_kernel<64, 4, 1>})
+      raise_lds_limit(k);
     (void)hipGetLastError();
   });
   SliceArgs p{qkv, ld, H * head_dim, out, dout, lse, nullptr, nullptr, dqkv, B, H, I, K,
@@ -751,8 +777,16 @@ int attn_slice_bwd(const float* qkv, int64_t ld, const float* out, const float* 
   const size_t lds = bwd_lds(I, K, head_dim);
   const int nw = g_waves[head_dim == 32 ? 2 : 3] == 4 ? 4 : 8;
   OT_REQUIRE(make_schedule(p, head_dim, nw), "ot_attn_bwd(slice): schedule");
-  void (*k)(SliceArgs) = head_dim == 32 ? (nw == 4 ? attn_bwd_slice_kernel<32, 4> : attn_bwd_slice_kernel<32, 8>)
-                                         : (nw == 4 ? attn_bwd_slice_kernel<64, 4> : attn_bwd_slice_kernel<64, 8>);
+  static const int pfpos = [] {
+    const char* e = std::getenv("ONETRANS_ATTN_SLICE_PFPOS");     // A/B timing of the prefetch point
+    return e ? std::atoi(e) : 0;
+  }();
+  void (*const table[2][2][2])(SliceArgs) = {
+      {{attn_bwd_slice_kernel<32, 4, 0>, attn_bwd_slice_kernel<32, 4, 1>},
+       {attn_bwd_slice_kernel<32, 8, 0>, attn_bwd_slice_kernel<32, 8, 1>}},
+      {{attn_bwd_slice_kernel<64, 4, 0>, attn_bwd_slice_kernel<64, 4, 1>},
+       {attn_bwd_slice_kernel<64, 8, 0>, attn_bwd_slice_kernel<64, 8, 1>}}};
+  void (*k)(SliceArgs) = table[head_dim == 64][nw == 8][pfpos == 1];
   const dim3 grid(persistent_grid((const void*)k, 64 * nw, lds, (int64_t)B * H)), block(64 * nw);
   hipLaunchKernelGGL(k, grid, block, lds, stream, p);
   OT_LAUNCH_CHECK("ot_attn_bwd(slice)");

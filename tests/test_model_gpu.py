@@ -269,7 +269,7 @@ def test_two_precisions_in_one_process(dev):
             m.flat.grad.zero_()
             probs = m.forward_probs(ns_t(ns, dev), ns_t(seq, dev), training=False)
             keras_bce_loss(y, probs, cfg32.tasks).backward()
-            outs[name] = (probs.double().cpu().numpy(), m.flat.grad.clone())
+            outs[name] = (probs.detach().double().cpu().numpy(), m.flat.grad.clone())
         for i, t in enumerate(cfg32.tasks):
             np.testing.assert_allclose(outs['f32'][0][i], ref['probs'][t].numpy()[:, 0], atol=LOGIT_TOL / 4, rtol=0)
             np.testing.assert_allclose(outs['bf16'][0][i], ref['probs'][t].numpy()[:, 0], atol=2e-2, rtol=0)

@@ -25,6 +25,7 @@ from recommend_amd.params import init_params
 from recommend_amd.trainer import OneTransTrainer
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden', 'train_C2.npz')
+DW_TOL = 1e-3       # max |d param| over the golden's sampled entries after 20 steps
 
 
 def test_train_20_steps_auc_parity(dev):
@@ -64,3 +65,4 @@ def test_train_20_steps_auc_parity(dev):
     assert dlog < 1e-3, dlog
     for t, (da, dka) in dauc.items():
         assert da < 1e-3 and dka < 1e-3, (t, da, dka)
+    assert dw < DW_TOL, dw

@@ -341,13 +341,17 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_slice_kernel(SliceArgs p
 //   from global — L2-warm — into the Q planes' space).
 // Loads in flight during compute: the next key block's K / V (phase 1), the K image rows (issued by each
 // wave as it leaves phase 1), and the next slice's Q / dO / O rows, lse and first K / V (phase 2).
-// PFPOS: where the next slice's loads are issued — 0: before phase 2 (overlapping it), 1: after it
-template <int HD, int NWV, int PFPOS>
+// The next slice's loads are issued before phase 2 at head_dim 64 (overlapping it) and after it at head_dim
+// 32 (measured: 1,688-1,697 vs 1,710-1,717 us at hd 64, 931-955 vs 943-1,019 us at hd 32; B 4096 H 4, I 140).
+// Software pipelining of phase 1 (step a + 2's S / dP issued before step a's softmax gradient) measured
+// 1-4% slower at hd 64 and within noise at hd 32; not kept.
+template <int HD, int NWV>
 __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NT = HD / 32, NM = HD / 16, CPR = HD / 8, NTH = 64 * NWV;
   constexpr int RM = RMAX<HD>(), PB = RM * HD * 2;
   constexpr int SR = (RM * CPR + NTH - 1) / NTH;
+  constexpr bool LAT = NWV == 4;                    // one wave per SIMD: fragment reads one item ahead, fenced
   const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform
   const int I = p.I, K = p.K, q_off = I - K;
@@ -457,37 +461,36 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
 #pragma unroll
       for (int m = 0; m < NM; ++m) dk[m] = dv[m] = f32x4{0.f, 0.f, 0.f, 0.f};
       const int a0 = tab[kb], blk0 = tab[16 + kb];
-      // S and dP of query step a (blocks a, a + 1; the second zero past the last block)
-      auto sdp = [&](int a, f32x4 (&sc)[2], f32x4 (&dc)[2]) {
+      // S and dP of query step a (blocks a, a + 1; the second zero past the last block).  With one wave per
+      // SIMD nothing else hides LDS latency, so each (half, t) item's fragments are read one item ahead
+      // (sched_barrier keeps the compiler from sinking the reads back to their MFMAs)
+      auto sdp = [&](int a, bool two, f32x4 (&sc)[2], f32x4 (&dc)[2]) {
+        constexpr int NI = 2 * NT;
+        u32x4 fq[2][3], fo[2][3];
+        row_frag<HD>(fq[0], qimg, PB, 16 * a + li, 0, g);
+        row_frag<HD>(fo[0], oimg, PB, 16 * a + li, 0, g);
 #pragma unroll
-        for (int half = 0; half < 2; ++half) {
-          const int qb = a + half;
-          sc[half] = dc[half] = f32x4{0.f, 0.f, 0.f, 0.f};
-          if (half == 1 && qb >= nqb) continue;
+        for (int h = 0; h < 2; ++h) sc[h] = dc[h] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int t = 0; t < NT; ++t) {
-            u32x4 fa[3], fb[3];
-            row_frag<HD>(fa, qimg, PB, 16 * qb + li, t, g);
-            row_frag<HD>(fb, oimg, PB, 16 * qb + li, t, g);
-            sc[half] = mma6(fa, kp[t], sc[half]);                     // S: row = query, col = key
-            dc[half] = mma6(fb, vp[t], dc[half]);                     // dP
+        for (int i = 0; i < NI; ++i) {
+          if (i + 1 < NI) {
+            const int qb1 = two ? a + (i + 1) / NT : a;            // past the last block: a harmless re-read
+            row_frag<HD>(fq[(i + 1) & 1], qimg, PB, 16 * qb1 + li, (i + 1) % NT, g);
+            row_frag<HD>(fo[(i + 1) & 1], oimg, PB, 16 * qb1 + li, (i + 1) % NT, g);
           }
+          const int half = i / NT, t = i % NT;
+          if (half == 0 || two) {
+            sc[half] = mma6(fq[i & 1], kp[t], sc[half]);            // S: row = query, col = key
+            dc[half] = mma6(fo[i & 1], vp[t], dc[half]);            // dP
+          }
+          if (LAT) __builtin_amdgcn_sched_barrier(0);
         }
       };
-      // PIPE (one wave per SIMD, 512 registers): step a + 2's S / dP products are issued before step a's
-      // softmax gradient, so the wave's VALU work overlaps its own MFMAs
-      constexpr bool PIPE = NWV == 4;
-      f32x4 sc[2], dc[2];
-      if (PIPE && a0 < nqb) sdp(a0, sc, dc);
 #pragma unroll 1
       for (int a = a0; a < nqb; a += 2) {
         const bool two = a + 1 < nqb;
-        f32x4 sn[2], dn[2];
-        if (PIPE) {
-          if (a + 2 < nqb) sdp(a + 2, sn, dn);
-        } else {
-          sdp(a, sc, dc);
-        }
+        f32x4 sc[2], dc[2];
+        sdp(a, two, sc, dc);
         float P[8], dS[8];
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
@@ -514,17 +517,18 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
         split8(P, pp);
         split8(dS, sp);
         const int rb = two ? 16 * a + 16 : 16 * a;
+        u32x4 fa[2][3], fb[2][3];
+        tr_frag<HD>(fa[0], oimg, PB, 16 * a, rb, 0, lane);
+        tr_frag<HD>(fb[0], qimg, PB, 16 * a, rb, 0, lane);
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
-          u32x4 fa[3], fb[3];
-          tr_frag<HD>(fa, oimg, PB, 16 * a, rb, m, lane);
-          tr_frag<HD>(fb, qimg, PB, 16 * a, rb, m, lane);
-          dv[m] = mma6(fa, pp, dv[m]);                                // dV^T += dO^T P
-          dk[m] = mma6(fb, sp, dk[m]);                                // dK^T += Q^T dS
-        }
-        if (PIPE) {
-#pragma unroll
-          for (int h2 = 0; h2 < 2; ++h2) { sc[h2] = sn[h2]; dc[h2] = dn[h2]; }
+          if (m + 1 < NM) {                                           // next dim tile's fragments in flight
+            tr_frag<HD>(fa[(m + 1) & 1], oimg, PB, 16 * a, rb, m + 1, lane);
+            tr_frag<HD>(fb[(m + 1) & 1], qimg, PB, 16 * a, rb, m + 1, lane);
+          }
+          dv[m] = mma6(fa[m & 1], pp, dv[m]);                         // dV^T += dO^T P
+          dk[m] = mma6(fb[m & 1], sp, dk[m]);                         // dK^T += Q^T dS
+          if (LAT) __builtin_amdgcn_sched_barrier(0);
         }
       }
       if (krow < I) {
@@ -560,7 +564,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
     }
     __syncthreads();
     SLICE_STAMP(1, it, 4);
-    if (PFPOS == 0 && s + (int)gridDim.x < nslices) prefetch(s + gridDim.x);   // next slice, during phase 2
+    constexpr bool EARLY = HD == 64;
+    if (EARLY && s + (int)gridDim.x < nslices) prefetch(s + gridDim.x);   // next slice, during phase 2
 
     // ---- phase 2: query-block owners, dQ^T = K^T dS^T
 #pragma unroll 1
@@ -584,15 +589,18 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
         f32x4 x1 = {0.f, 0.f, 0.f, 0.f};
         if (two)
           x1 = *reinterpret_cast<const f32x4*>(dss + 1024 * (tab[17 + k2] + qb - tab[k2 + 1]) + poff<32>(li, g));
+        const int rb = two ? 16 * k2 + 16 : 16 * k2;
+        u32x4 fa[2][3];
+        tr_frag<HD>(fa[0], qimg, PB, 16 * k2, rb, 0, lane);            // in flight during the split
 #pragma unroll
         for (int i = 0; i < 4; ++i) { v[i] = x0[i]; v[4 + i] = x1[i]; }
         u32x4 bp[3];
         split8(v, bp);
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
-          u32x4 fa[3];
-          tr_frag<HD>(fa, qimg, PB, 16 * k2, two ? 16 * k2 + 16 : 16 * k2, m, lane);
-          acc[m] = mma6(fa, bp, acc[m]);
+          if (m + 1 < NM) tr_frag<HD>(fa[(m + 1) & 1], qimg, PB, 16 * k2, rb, m + 1, lane);
+          acc[m] = mma6(fa[m & 1], bp, acc[m]);
+          if (LAT) __builtin_amdgcn_sched_barrier(0);
         }
       };
 #pragma unroll 1
@@ -610,7 +618,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
       }
     }
     SLICE_STAMP(1, it, 5);
-    if (PFPOS == 1 && s + (int)gridDim.x < nslices) prefetch(s + gridDim.x);
+    if (!EARLY && s + (int)gridDim.x < nslices) prefetch(s + gridDim.x);
     __syncthreads();                               // LDS is restaged next slice
     SLICE_STAMP(1, it, 6);
   }
@@ -705,9 +713,9 @@ static int g_enabled = [] {
   return e ? std::atoi(e) : 1;
 }();
 
-constexpr int FWD_WAVES = 8, BWD_WAVES = 8;
+constexpr int FWD_WAVES = 8, BWD_WAVES = 8, BWD_WAVES64 = 4;
 // A/B timing of the workgroup size (4 or 8 waves) per head_dim: ONETRANS_ATTN_SLICE_WAVES=fwd32,fwd64,bwd32,bwd64
-static int g_waves[4] = {FWD_WAVES, FWD_WAVES, BWD_WAVES, BWD_WAVES};
+static int g_waves[4] = {FWD_WAVES, FWD_WAVES, BWD_WAVES, BWD_WAVES64};
 static int g_waves_init = [] {
   if (const char* e = std::getenv("ONETRANS_ATTN_SLICE_WAVES"))
     std::sscanf(e, "%d,%d,%d,%d", &g_waves[0], &g_waves[1], &g_waves[2], &g_waves[3]);
@@ -764,29 +772,21 @@ int attn_slice_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, con
 int attn_slice_bwd(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse, int B, int H,
                    int I, int K, int head_dim, float* dqkv, hipStream_t stream) {
   using namespace slice;
+  using KF = void (*)(SliceArgs);
+  static const KF k32 = attn_bwd_slice_kernel<32, 8>, k64_4 = attn_bwd_slice_kernel<64, 4>,
+                  k64_8 = attn_bwd_slice_kernel<64, 8>;
   static std::once_flag once;
   std::call_once(once, [] {
-    for (auto k : {attn_bwd_slice_kernel<32, 8, 0>, attn_bwd_slice_kernel<64, 8, 0>, attn_bwd_slice_kernel<32, 4, 0>,
-                   attn_bwd_slice_kernel<64, 4, 0>, attn_bwd_slice_kernel<32, 8, 1>, attn_bwd_slice_kernel<64, 8, 1>,
-                   attn_bwd_slice_kernel<32, 4, 1>, attn_bwd_slice_kernel<64, 4, 1>})
-      raise_lds_limit(k);
+    for (KF k : {k32, k64_4, k64_8}) raise_lds_limit(k);
     (void)hipGetLastError();
   });
   SliceArgs p{qkv, ld, H * head_dim, out, dout, lse, nullptr, nullptr, dqkv, B, H, I, K,
               1.f / sqrtf((float)head_dim), nullptr};
   const size_t lds = bwd_lds(I, K, head_dim);
-  const int nw = g_waves[head_dim == 32 ? 2 : 3] == 4 ? 4 : 8;
+  // head_dim 32: 8 waves (4 waves measured 1,136-1,160 vs 928-965 us); head_dim 64: 4 waves by default
+  const int nw = head_dim == 32 ? 8 : (g_waves[3] == 8 ? 8 : 4);
   OT_REQUIRE(make_schedule(p, head_dim, nw), "ot_attn_bwd(slice): schedule");
-  static const int pfpos = [] {
-    const char* e = std::getenv("ONETRANS_ATTN_SLICE_PFPOS");     // A/B timing of the prefetch point
-    return e ? std::atoi(e) : 0;
-  }();
-  void (*const table[2][2][2])(SliceArgs) = {
-      {{attn_bwd_slice_kernel<32, 4, 0>, attn_bwd_slice_kernel<32, 4, 1>},
-       {attn_bwd_slice_kernel<32, 8, 0>, attn_bwd_slice_kernel<32, 8, 1>}},
-      {{attn_bwd_slice_kernel<64, 4, 0>, attn_bwd_slice_kernel<64, 4, 1>},
-       {attn_bwd_slice_kernel<64, 8, 0>, attn_bwd_slice_kernel<64, 8, 1>}}};
-  void (*k)(SliceArgs) = table[head_dim == 64][nw == 8][pfpos == 1];
+  const KF k = head_dim == 32 ? k32 : (nw == 4 ? k64_4 : k64_8);
   const dim3 grid(persistent_grid((const void*)k, 64 * nw, lds, (int64_t)B * H)), block(64 * nw);
   hipLaunchKernelGGL(k, grid, block, lds, stream, p);
   OT_LAUNCH_CHECK("ot_attn_bwd(slice)");

@@ -149,7 +149,7 @@ def hbm_traffic(config):
     (tools/hbm_traffic.py: separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes over this bench,
     calibrated on a known 1 GiB copy).  (None, None) when no summary for this config exists."""
     import glob
-    for fn in sorted(glob.glob(os.path.join(ROOT, 'profiles', '*', 'hbm_traffic.json')), reverse=True):
+    for fn in sorted(glob.glob(os.path.join(ROOT, 'profiles', '*', 'hbm_traffic*.json')), reverse=True):
         try:
             d = json.load(open(fn))
         except (OSError, ValueError):

@@ -88,6 +88,43 @@ __device__ __forceinline__ void tr_frag(u32x4 (&f)[3], const char* img, int pb, 
   }
 }
 
+// the same reads from precomputed per-lane offsets: every plane image row block of 16 rows has the same
+// swizzle (the XOR terms of poff depend on row mod 8 / 16 only), so the offset of (block, lane) is
+// block * 16 * row bytes + a per-lane constant, and a loop adds one uniform term per block
+__device__ __forceinline__ void frag_at(u32x4 (&f)[3], const char* p, int pb) {
+#pragma unroll
+  for (int pl = 0; pl < 3; ++pl) f[pl] = *reinterpret_cast<const u32x4*>(p + pl * pb);
+}
+__device__ __forceinline__ void tr_at(u32x4 (&f)[3], const char* p0, const char* p1, int pb) {
+#pragma unroll
+  for (int pl = 0; pl < 3; ++pl) {
+    const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(p0 + pl * pb));
+    const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(p1 + pl * pb));
+    const u32x2 x = __builtin_bit_cast(u32x2, lo), y = __builtin_bit_cast(u32x2, hi);
+    f[pl] = u32x4{x.x, x.y, y.x, y.y};
+  }
+}
+// split8 with the two subtractions of each element pair on packed-f32 adds (v_pk_add_f32); the planes are
+// the high halves of x, r1, r2 (v_perm), so only the residuals need the masked values.  Bit-identical to split8.
+__device__ __forceinline__ void split8p(const float* v, u32x4 (&pl)[3]) {
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  uint32_t a[4], b[4], c[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const f32x2 x = {v[2 * k], v[2 * k + 1]};
+    const f32x2 x0 = {__uint_as_float(__float_as_uint(x.x) & 0xffff0000u), __uint_as_float(__float_as_uint(x.y) & 0xffff0000u)};
+    const f32x2 r1 = x - x0;
+    const f32x2 x1 = {__uint_as_float(__float_as_uint(r1.x) & 0xffff0000u), __uint_as_float(__float_as_uint(r1.y) & 0xffff0000u)};
+    const f32x2 r2 = r1 - x1;
+    a[k] = __builtin_amdgcn_perm(__float_as_uint(x.y), __float_as_uint(x.x), 0x07060302u);
+    b[k] = __builtin_amdgcn_perm(__float_as_uint(r1.y), __float_as_uint(r1.x), 0x07060302u);
+    c[k] = __builtin_amdgcn_perm(__float_as_uint(r2.y), __float_as_uint(r2.x), 0x07060302u);
+  }
+  pl[0] = u32x4{a[0], a[1], a[2], a[3]};
+  pl[1] = u32x4{b[0], b[1], b[2], b[3]};
+  pl[2] = u32x4{c[0], c[1], c[2], c[3]};
+}
+
 // max / sum with the lane 16 and 32 apart (the 4 lane groups of a 16x16 accumulator column) on the VALU
 // lane-swap instructions (no LDS round trip as ds_bpermute): each swap hands every lane its own value and
 // its partner's, in some order — max and + are symmetric, so all four groups get identical results
@@ -211,6 +248,19 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_slice_kernel(SliceArgs p
   };
   const uint64_t srow = sched_row(p, 0, wave);
   const int idx0 = sched_item(srow, 0);
+  // per-lane LDS offsets of the fragment reads (see the backward): held opaque so each key block adds one
+  // uniform term to a register instead of re-deriving image + plane constants per read
+  int kbase[NT], vtbase[NM];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    kbase[t] = poff<HD>(li, 4 * t + g);
+    asm volatile("" : "+v"(kbase[t]));
+  }
+#pragma unroll
+  for (int m = 0; m < NM; ++m) {
+    vtbase[m] = poff<HD>(4 * g + ((lane >> 2) & 3), 2 * m + ((lane & 3) >> 1)) + 8 * (lane & 1) + 3 * PB;
+    asm volatile("" : "+v"(vtbase[m]));
+  }
   int s = blockIdx.x;
   if (s < nslices) {
     load_kv(s);
@@ -252,7 +302,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_slice_kernel(SliceArgs p
       for (int t = 0; t < NT; ++t) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) qr[t][e] *= qscale;
-        split8(qr[t], qp[t]);
+        split8p(qr[t], qp[t]);
       }
       const int idxn = sched_item(srow, slot + 1);
       if (idxn >= 0) load_q(s, idxn);                                // next block's Q, in flight meanwhile
@@ -267,7 +317,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_slice_kernel(SliceArgs p
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           u32x4 fk[3];
-          row_frag<HD>(fk, kimg, PB, 16 * kb + li, t, g);
+          frag_at(fk, smem + 16 * HD * 2 * kb + kbase[t], PB);
           acc = mma6(fk, qp[t], acc);                                 // S^T: row = key, col = query
         }
         if (kb >= kbm) {
@@ -304,11 +354,12 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_slice_kernel(SliceArgs p
           v[4 + i] = two ? sc[kb + 1][i] : 0.f;
         }
         u32x4 pp[3];
-        split8(v, pp);
+        split8p(v, pp);
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
           u32x4 fa[3];
-          tr_frag<HD>(fa, vimg, PB, 16 * kb, two ? 16 * kb + 16 : 16 * kb, m, lane);
+          const int ra = 16 * HD * 2 * kb, rb = two ? ra + 16 * HD * 2 : ra;
+          tr_at(fa, smem + ra + vtbase[m], smem + rb + vtbase[m], PB);
           o[m] = mma6(fa, pp, o[m]);                                  // O^T += V^T P^T
         }
       }
@@ -352,6 +403,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
   constexpr int RM = RMAX<HD>(), PB = RM * HD * 2;
   constexpr int SR = (RM * CPR + NTH - 1) / NTH;
   constexpr bool LAT = NWV == 4;                    // one wave per SIMD: fragment reads one item ahead, fenced
+  constexpr int RBY = HD * 2;                       // bytes per plane image row
   const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform
   const int I = p.I, K = p.K, q_off = I - K;
@@ -370,6 +422,25 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
     tab[16 + threadIdx.x] = p.bbase[threadIdx.x];
   }
   const uint64_t srow1 = sched_row(p, 1, wave), srow2 = sched_row(p, 2, wave);
+  // per-lane LDS offsets, held opaque (asm) so the compiler keeps one register per base and adds each
+  // loop's uniform block offset to it once, instead of re-deriving image + plane constants past the
+  // 16-bit immediate per read
+  int rbase[NT], tbase[NM], orbase[NT], otbase[NM], dsw[4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    rbase[t] = poff<HD>(li, 4 * t + g);
+    orbase[t] = rbase[t] + 3 * PB;
+    asm volatile("" : "+v"(rbase[t]), "+v"(orbase[t]));
+  }
+#pragma unroll
+  for (int m = 0; m < NM; ++m) {
+    tbase[m] = poff<HD>(4 * g + ((lane >> 2) & 3), 2 * m + ((lane & 3) >> 1)) + 8 * (lane & 1);
+    otbase[m] = tbase[m] + 3 * PB;
+    asm volatile("" : "+v"(tbase[m]), "+v"(otbase[m]));
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dsw[i] = poff<32>(4 * g + i, li >> 2) + 4 * (li & 3);
+  const int dsr = poff<32>(li, g);
   auto qkv_of = [&](int s) { return p.qkv + (int64_t)(s / p.H) * I * p.ld + (s % p.H) * HD; };
   auto row_of = [&](int s) { return (int64_t)(s / p.H) * K * p.d + (s % p.H) * HD; };   // O / dO slice
   // rows past K / I read the last valid row (finite) and are zeroed at use, so no load is predicated
@@ -417,11 +488,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
     }
 #pragma unroll
     for (int r = 0; r < SR; ++r) {
+      // query rows past K hold row K - 1 (finite): their P and dS are 0 (lse +inf, qpos -1) and their dQ is
+      // not stored, so they need no zeroing
       const int task = threadIdx.x + r * NTH, j = task / CPR, c = task % CPR;
-      if (j >= K) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) qr[r][e] = yr[r][e] = orr[r][e] = 0.f;
-      }
       float pd = 0.f;
 #pragma unroll
       for (int e = 0; e < 8; ++e) pd = fmaf(yr[r][e], orr[r][e], pd);
@@ -441,16 +510,13 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
 #pragma unroll 1
     for (int slot = 0, kb = kb0; kb >= 0; ++slot) {
       const int krow = 16 * kb + li;               // this lane's key
+      // keys past I hold row I - 1 (finite): their S / dP columns are masked (P = dS = 0, a select) and
+      // their dK / dV rows are not stored, so they need no zeroing
       u32x4 kp[NT][3], vp[NT][3];
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          kr[t][e] = krow < I ? kr[t][e] : 0.f;
-          vr[t][e] = krow < I ? vr[t][e] : 0.f;
-        }
-        split8(kr[t], kp[t]);
-        split8(vr[t], vp[t]);
+        split8p(kr[t], kp[t]);
+        split8p(vr[t], vp[t]);
       }
       const int kbn = sched_item(srow1, slot + 1);
       // next key block's K / V in flight meanwhile (hd 64 at 2 waves / SIMD: loaded at its turn instead —
@@ -467,16 +533,16 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
       auto sdp = [&](int a, bool two, f32x4 (&sc)[2], f32x4 (&dc)[2]) {
         constexpr int NI = 2 * NT;
         u32x4 fq[2][3], fo[2][3];
-        row_frag<HD>(fq[0], qimg, PB, 16 * a + li, 0, g);
-        row_frag<HD>(fo[0], oimg, PB, 16 * a + li, 0, g);
+        frag_at(fq[0], smem + 16 * RBY * a + rbase[0], PB);
+        frag_at(fo[0], smem + 16 * RBY * a + orbase[0], PB);
 #pragma unroll
         for (int h = 0; h < 2; ++h) sc[h] = dc[h] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
           if (i + 1 < NI) {
             const int qb1 = two ? a + (i + 1) / NT : a;            // past the last block: a harmless re-read
-            row_frag<HD>(fq[(i + 1) & 1], qimg, PB, 16 * qb1 + li, (i + 1) % NT, g);
-            row_frag<HD>(fo[(i + 1) & 1], oimg, PB, 16 * qb1 + li, (i + 1) % NT, g);
+            frag_at(fq[(i + 1) & 1], smem + 16 * RBY * qb1 + rbase[(i + 1) % NT], PB);
+            frag_at(fo[(i + 1) & 1], smem + 16 * RBY * qb1 + orbase[(i + 1) % NT], PB);
           }
           const int half = i / NT, t = i % NT;
           if (half == 0 || two) {
@@ -510,21 +576,21 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
             const float ds = pv * (dc[half][i] - D[i]) * p.scale;
             P[4 * half + i] = pv;
             dS[4 * half + i] = ds;
-            *reinterpret_cast<float*>(blk + poff<32>(4 * g + i, li >> 2) + 4 * (li & 3)) = ds;
+            *reinterpret_cast<float*>(blk + dsw[i]) = ds;
           }
         }
         u32x4 pp[3], sp[3];
-        split8(P, pp);
-        split8(dS, sp);
-        const int rb = two ? 16 * a + 16 : 16 * a;
+        split8p(P, pp);
+        split8p(dS, sp);
+        const int ra = 16 * RBY * a, rb = two ? ra + 16 * RBY : ra;
         u32x4 fa[2][3], fb[2][3];
-        tr_frag<HD>(fa[0], oimg, PB, 16 * a, rb, 0, lane);
-        tr_frag<HD>(fb[0], qimg, PB, 16 * a, rb, 0, lane);
+        tr_at(fa[0], smem + ra + otbase[0], smem + rb + otbase[0], PB);
+        tr_at(fb[0], smem + ra + tbase[0], smem + rb + tbase[0], PB);
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
           if (m + 1 < NM) {                                           // next dim tile's fragments in flight
-            tr_frag<HD>(fa[(m + 1) & 1], oimg, PB, 16 * a, rb, m + 1, lane);
-            tr_frag<HD>(fb[(m + 1) & 1], qimg, PB, 16 * a, rb, m + 1, lane);
+            tr_at(fa[(m + 1) & 1], smem + ra + otbase[m + 1], smem + rb + otbase[m + 1], PB);
+            tr_at(fb[(m + 1) & 1], smem + ra + tbase[m + 1], smem + rb + tbase[m + 1], PB);
           }
           dv[m] = mma6(fa[m & 1], pp, dv[m]);                         // dV^T += dO^T P
           dk[m] = mma6(fb[m & 1], sp, dk[m]);                         // dK^T += Q^T dS
@@ -554,13 +620,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
 #pragma unroll
     for (int r = 0; r < SR; ++r) {
       const int task = threadIdx.x + r * NTH, row = task / CPR, c = task % CPR;
-      if (task < IP * CPR) {
-        if (row >= I) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) kk[r][e] = 0.f;
-        }
-        store_planes(qimg, PB, poff<HD>(row, c), kk[r]);
-      }
+      if (task < IP * CPR) store_planes(qimg, PB, poff<HD>(row, c), kk[r]);   // rows past I: row I - 1, times dS = 0
     }
     __syncthreads();
     SLICE_STAMP(1, it, 4);
@@ -585,20 +645,19 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
       auto step = [&](int k2, f32x4 (&acc)[NM]) {
         const bool two = k2 + 1 <= kbl;
         float v[8];
-        const f32x4 x0 = *reinterpret_cast<const f32x4*>(dss + 1024 * (tab[16 + k2] + qb - tab[k2]) + poff<32>(li, g));
+        const f32x4 x0 = *reinterpret_cast<const f32x4*>(dss + 1024 * (tab[16 + k2] + qb - tab[k2]) + dsr);
         f32x4 x1 = {0.f, 0.f, 0.f, 0.f};
-        if (two)
-          x1 = *reinterpret_cast<const f32x4*>(dss + 1024 * (tab[17 + k2] + qb - tab[k2 + 1]) + poff<32>(li, g));
-        const int rb = two ? 16 * k2 + 16 : 16 * k2;
+        if (two) x1 = *reinterpret_cast<const f32x4*>(dss + 1024 * (tab[17 + k2] + qb - tab[k2 + 1]) + dsr);
+        const int ra = 16 * RBY * k2, rb = two ? ra + 16 * RBY : ra;
         u32x4 fa[2][3];
-        tr_frag<HD>(fa[0], qimg, PB, 16 * k2, rb, 0, lane);            // in flight during the split
+        tr_at(fa[0], smem + ra + tbase[0], smem + rb + tbase[0], PB);   // in flight during the split
 #pragma unroll
         for (int i = 0; i < 4; ++i) { v[i] = x0[i]; v[4 + i] = x1[i]; }
         u32x4 bp[3];
-        split8(v, bp);
+        split8p(v, bp);
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
-          if (m + 1 < NM) tr_frag<HD>(fa[(m + 1) & 1], qimg, PB, 16 * k2, rb, m + 1, lane);
+          if (m + 1 < NM) tr_at(fa[(m + 1) & 1], smem + ra + tbase[m + 1], smem + rb + tbase[m + 1], PB);
           acc[m] = mma6(fa[m & 1], bp, acc[m]);
           if (LAT) __builtin_amdgcn_sched_barrier(0);
         }

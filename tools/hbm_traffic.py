@@ -20,7 +20,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-FAMILIES = {'gemm': ('mixed_gemm_kernel', 'plane_gemm_kernel', 'wgrad_kernel', 'wgrad_split_kernel'),
+FAMILIES = {'gemm': ('mixed_gemm_kernel', 'plane_gemm_kernel', 'wgrad_kernel<', 'wgrad_split_kernel', 'wgrad_bf16_kernel'),
             'attention': ('attn_',),
             # the embedding path: NS gather, sequence-id row maps, and the sparse update
             # (key prep, rocPRIM radix sort, de-duplication, segment sums, clip, Adagrad); the sequence

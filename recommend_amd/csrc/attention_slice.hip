@@ -468,13 +468,16 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
       load8(orr[r], Og + (int64_t)j * p.d + 8 * c);
     }
     lsev = p.lse_in[(int64_t)s * K + min((int)threadIdx.x, K - 1)];
-    if (kb0 >= 0) load_kv(s, kb0);
   };
   int s = blockIdx.x;
   if (s < nslices) prefetch(s);
 #pragma unroll 1
   for (int it = 0; s < nslices; s += gridDim.x, ++it) {
     SLICE_STAMP(1, it, 0);
+    // the first key block's K / V: issued here, not with the slice prefetch — loaded during phase 2, the
+    // compiler parked them in AGPRs and drained every load (vmcnt(0)) to copy them out before phase 2.  Here
+    // they stay in flight through the staging (which waits only for the older Q / dO / O loads)
+    if (kb0 >= 0) load_kv(s, kb0);
     float* dQg = p.dqkv + (int64_t)(s / p.H) * I * p.ld + (s % p.H) * HD;
     float* dKg = dQg + p.d;
     float* dVg = dQg + 2 * p.d;
@@ -519,10 +522,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
         split8p(vr[t], vp[t]);
       }
       const int kbn = sched_item(srow1, slot + 1);
-      // next key block's K / V in flight meanwhile (hd 64 at 2 waves / SIMD: loaded at its turn instead —
-      // the 32 registers of the prefetch spill there, and the SIMD's other wave covers the latency)
-      constexpr bool PREFETCH_KV = !(HD == 64 && NWV == 8);
-      if (PREFETCH_KV && kbn >= 0) load_kv(s, kbn);
+      if (kbn >= 0) load_kv(s, kbn);                // next key block's K / V in flight meanwhile
       f32x4 dk[NM], dv[NM];
 #pragma unroll
       for (int m = 0; m < NM; ++m) dk[m] = dv[m] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -605,7 +605,6 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
         }
       }
       kb = kbn;
-      if (!PREFETCH_KV && kb >= 0) load_kv(s, kb);
     }
     // K image for phase 2: the rows re-read (L2-warm) before the barrier, stored into the Q planes' space after it
     float kk[SR][8];
@@ -772,14 +771,10 @@ static int g_enabled = [] {
   return e ? std::atoi(e) : 1;
 }();
 
-constexpr int FWD_WAVES = 8, BWD_WAVES = 8, BWD_WAVES64 = 4;
-// A/B timing of the workgroup size (4 or 8 waves) per head_dim: ONETRANS_ATTN_SLICE_WAVES=fwd32,fwd64,bwd32,bwd64
-static int g_waves[4] = {FWD_WAVES, FWD_WAVES, BWD_WAVES, BWD_WAVES64};
-static int g_waves_init = [] {
-  if (const char* e = std::getenv("ONETRANS_ATTN_SLICE_WAVES"))
-    std::sscanf(e, "%d,%d,%d,%d", &g_waves[0], &g_waves[1], &g_waves[2], &g_waves[3]);
-  return 0;
-}();
+// waves per workgroup (measured, B 4096 H 4 I 140): forward 8 (hd 32: 4 waves / SIMD at 128 VGPRs); backward hd 32
+// 8 (4 waves: 1,136-1,160 vs 928-965 us), hd 64 4 (one wave per SIMD with up to 512 registers; 8 waves spill at
+// the 256-register limit: 1,971-2,095 vs 1,688-1,782 us)
+constexpr int FWD_WAVES = 8, BWD_WAVES32 = 8, BWD_WAVES64 = 4;
 
 template <typename F>
 static void raise_lds_limit(F* k) {
@@ -803,24 +798,20 @@ int attn_slice_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, con
   using namespace slice;
   static std::once_flag once;
   std::call_once(once, [] {
-    for (auto k : {attn_fwd_slice_kernel<32, 8, false, false>, attn_fwd_slice_kernel<32, 8, true, false>,
-                   attn_fwd_slice_kernel<32, 4, false, false>, attn_fwd_slice_kernel<32, 4, true, false>,
-                   attn_fwd_slice_kernel<64, 8, false, true>, attn_fwd_slice_kernel<64, 8, true, true>,
-                   attn_fwd_slice_kernel<64, 4, false, true>, attn_fwd_slice_kernel<64, 4, true, true>})
+    for (auto k : {attn_fwd_slice_kernel<32, FWD_WAVES, false, false>, attn_fwd_slice_kernel<32, FWD_WAVES, true, false>,
+                   attn_fwd_slice_kernel<64, FWD_WAVES, false, true>, attn_fwd_slice_kernel<64, FWD_WAVES, true, true>})
       raise_lds_limit(k);
     (void)hipGetLastError();
   });
   SliceArgs p{qkv, ld, H * head_dim, nullptr, nullptr, nullptr, out, lse, nullptr, B, H, I, K,
               1.f / sqrtf((float)head_dim), qpos};
   const size_t lds = fwd_lds(I, head_dim);
-  const int nw = g_waves[head_dim == 32 ? 0 : 1] == 4 ? 4 : 8;
+  const int nw = FWD_WAVES;
   OT_REQUIRE(make_schedule(p, head_dim, nw), "ot_attn_fwd(slice): schedule");
-  void (*const table[2][2][2])(SliceArgs) = {
-      {{attn_fwd_slice_kernel<32, 4, false, false>, attn_fwd_slice_kernel<32, 4, true, false>},
-       {attn_fwd_slice_kernel<32, 8, false, false>, attn_fwd_slice_kernel<32, 8, true, false>}},
-      {{attn_fwd_slice_kernel<64, 4, false, true>, attn_fwd_slice_kernel<64, 4, true, true>},
-       {attn_fwd_slice_kernel<64, 8, false, true>, attn_fwd_slice_kernel<64, 8, true, true>}}};
-  void (*k)(SliceArgs) = table[head_dim == 64][nw == 8][qpos != nullptr];
+  void (*const table[2][2])(SliceArgs) = {
+      {attn_fwd_slice_kernel<32, FWD_WAVES, false, false>, attn_fwd_slice_kernel<32, FWD_WAVES, true, false>},
+      {attn_fwd_slice_kernel<64, FWD_WAVES, false, true>, attn_fwd_slice_kernel<64, FWD_WAVES, true, true>}};
+  void (*k)(SliceArgs) = table[head_dim == 64][qpos != nullptr];
   const unsigned slices = (unsigned)((int64_t)B * H);
   const dim3 grid(head_dim == 64 ? persistent_grid((const void*)k, 64 * nw, lds, slices) : slices), block(64 * nw);
   hipLaunchKernelGGL(k, grid, block, lds, stream, p);
@@ -832,20 +823,18 @@ int attn_slice_bwd(const float* qkv, int64_t ld, const float* out, const float* 
                    int I, int K, int head_dim, float* dqkv, hipStream_t stream) {
   using namespace slice;
   using KF = void (*)(SliceArgs);
-  static const KF k32 = attn_bwd_slice_kernel<32, 8>, k64_4 = attn_bwd_slice_kernel<64, 4>,
-                  k64_8 = attn_bwd_slice_kernel<64, 8>;
+  static const KF k32 = attn_bwd_slice_kernel<32, BWD_WAVES32>, k64 = attn_bwd_slice_kernel<64, BWD_WAVES64>;
   static std::once_flag once;
   std::call_once(once, [] {
-    for (KF k : {k32, k64_4, k64_8}) raise_lds_limit(k);
+    for (KF k : {k32, k64}) raise_lds_limit(k);
     (void)hipGetLastError();
   });
   SliceArgs p{qkv, ld, H * head_dim, out, dout, lse, nullptr, nullptr, dqkv, B, H, I, K,
               1.f / sqrtf((float)head_dim), nullptr};
   const size_t lds = bwd_lds(I, K, head_dim);
-  // head_dim 32: 8 waves (4 waves measured 1,136-1,160 vs 928-965 us); head_dim 64: 4 waves by default
-  const int nw = head_dim == 32 ? 8 : (g_waves[3] == 8 ? 8 : 4);
+  const int nw = head_dim == 32 ? BWD_WAVES32 : BWD_WAVES64;
   OT_REQUIRE(make_schedule(p, head_dim, nw), "ot_attn_bwd(slice): schedule");
-  const KF k = head_dim == 32 ? k32 : (nw == 4 ? k64_4 : k64_8);
+  const KF k = head_dim == 32 ? k32 : k64;
   const dim3 grid(persistent_grid((const void*)k, 64 * nw, lds, (int64_t)B * H)), block(64 * nw);
   hipLaunchKernelGGL(k, grid, block, lds, stream, p);
   OT_LAUNCH_CHECK("ot_attn_bwd(slice)");

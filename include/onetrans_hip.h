@@ -244,9 +244,13 @@ int ot_attn_fwd_fp8(const float* qkv, int64_t ld, int B, int H, int I, int K, co
                     int head_dim, float* out, float* lse, void* workspace, size_t ws_bytes, void* stream);
 /* flags of ot_attn_fwd_fp8_ex */
 #define OT_FP8_DEQUANT 1 /* training: overwrite qkv's Q (kept query rows), K and V with their dequantised fp8
-                          * values (e4m3 x block scale: exact in bf16), so ot_attn_bwd in the bf16 GEMM mode
-                          * recomputes S from the products the fp8 forward summed (its P matches this lse; the
-                          * straight-through gradient of the forward that ran) */
+                          * values, so ot_attn_bwd in the bf16 GEMM mode recomputes S from (nearly) the operands
+                          * the fp8 forward used.  One term (e4m3 x block scale) is exact in bf16 and the
+                          * backward's P then matches this lse up to summation order.  With OT_FP8_TWO_TERM the
+                          * dequantised value hi + lo has more than bf16's 8 significant bits (the bf16 backward
+                          * rounds it) and the forward dropped the lo.lo product, so the recomputed S differs from
+                          * the forward's by those two terms: the straight-through gradient is approximate
+                          * (tests/test_attn_fp8_gpu.py: 0.5-1% of max|g| from the exact attention gradient) */
 #define OT_FP8_TWO_TERM 2 /* two-term e4m3 operands: every Q / K / V / P element as hi = e4m3(x) plus lo =
                            * e4m3(x - hi), each with its own block scale; QK^T and PV as three fp8 MFMA
                            * products (hi.hi + hi.lo + lo.hi): ~7 significant bits per operand */

@@ -17,12 +17,15 @@
 //     and the row sum l in the same units, so O = sum(P V) / l needs no extra scale.
 //
 // OT_FP8_DEQUANT (training): both launches also write the dequantised operands back into qkv (each
-// Q / K / V element replaced by its e4m3 value times its block scale — exactly representable in bf16),
-// so the backward (ot_attn_bwd in the bf16 GEMM mode) recomputes S from the very products the fp8
-// forward summed: its P matches the forward's log-sum-exp and delta = rowsum(dO o O) is the
-// straight-through gradient of the forward that ran (P's own e4m3 rounding aside).  Without it the
-// backward would recompute S from unquantised operands against the fp8 forward's statistics (rows of
-// P off by up to the fp8 lse error).
+// Q / K / V element replaced by its dequantised value), so the backward (ot_attn_bwd in the bf16 GEMM
+// mode) recomputes S from the operands the fp8 forward used.  One term: the e4m3 value times its block
+// scale is exact in bf16, the recomputed P matches the forward's log-sum-exp up to summation order and
+// delta = rowsum(dO o O) gives the straight-through gradient of the forward that ran (P's own e4m3
+// rounding aside).  Two terms (the default): hi + lo needs more than bf16's 8 significant bits, so the
+// bf16 backward (and ot_attn_fwd_fp8_deq16's copy) round it, and the forward summed hi.hi + hi.lo + lo.hi
+// without lo.lo — the recomputed S is off by those terms and the gradient is approximate (0.5-1% of
+// max|g| from the exact attention gradient, tests/test_attn_fp8_gpu.py).  Without OT_FP8_DEQUANT the
+// backward would recompute S from unquantised operands against the fp8 forward's statistics.
 //
 // Operand layout of the 32x32x64 scaled MFMA, measured on the box (tools/micro/fp8_probe.hip): A lane l
 // holds row l&31, B lane l column l&31; byte j of lane half h meets byte j of the other operand's lane

@@ -227,7 +227,8 @@ def _block_forward(m, l, x, I, Kq, seed, training, rstd_in=None, select=False, n
     # arithmetically (no per-query position loads; C3 attention 20.2 -> 18.3 ms/step); the select map
     # still drives the GEMM row maps and epilogues
     # fp8 training forward: qkv's operands are replaced by their dequantised fp8 values, so the backward
-    # differentiates the forward that ran (OT_FP8_DEQUANT)
+    # differentiates (nearly) the forward that ran (OT_FP8_DEQUANT; exact for one-term operands, approximate
+    # for the default two-term ones: bf16 rounding of hi + lo and the dropped lo.lo product)
     # with the key-grouped bf16 backward, the dequantised operands go to a bf16 copy that replaces qkv as the
     # backward's saved operand (the backward rounds them to bf16 anyway)
     qp_f = _attn_qpos(cfg, pos)

@@ -95,6 +95,12 @@ def device_batches(cfg, B, n, rank, dev):
     return out
 
 
+def log(msg):
+    """Progress to stderr (rank 0): a long bench keeps writing, and the JSON line stays alone on stdout."""
+    if int(os.environ.get('RANK', '0')) == 0:
+        print(f'[bench {time.strftime("%H:%M:%S")}] {msg}', file=sys.stderr, flush=True)
+
+
 def cpu_baseline(cfg_name, seconds):
     """Oracle (torch CPU fp32) fwd+bwd+optimizer steps on the host cores, in both restatements of
     SURVEY §8d: 'literal' (per-token projection/FFN loops like model.py:84-88, 154-161) and
@@ -104,7 +110,17 @@ def cpu_baseline(cfg_name, seconds):
     from recommend_amd.params import init_params, keras_variables
     from oracle import onetrans_ref as R
     cores = len(os.sched_getaffinity(0))          # the node's host cores this process may run on
-    torch.set_num_threads(cores)
+    quota = None                                   # cgroup CPU quota (cores' worth), when the container sets one
+    try:
+        q, per = open('/sys/fs/cgroup/cpu.max').read().split()[:2]
+        quota = None if q == 'max' else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    # one thread per core this process can actually run on: the affinity set, or the cgroup's CPU share when
+    # that is smaller (the GPU box lists the whole machine's CPUs in the affinity mask but grants a 16-CPU
+    # quota; 200+ threads under it throttle each other to a standstill)
+    threads = cores if quota is None else max(1, min(cores, int(quota + 0.999)))
+    torch.set_num_threads(threads)
     cfg = workload_config(cfg_name)
     # the oracle's table gradient is dense: cap table cardinalities (transformer work is unchanged)
     cfg.sparse_features = {k: min(v, 20000) for k, v in cfg.sparse_features.items()}
@@ -128,14 +144,9 @@ def cpu_baseline(cfg_name, seconds):
             if el >= seconds / 2 or n >= 200:
                 break
         rates[variant] = (B * n / el, n, el)
+        log(f'cpu baseline {variant}: {n} steps in {el:.1f}s on {threads} threads')
     best = max(rates, key=lambda v: rates[v][0])
     v, n, el = rates[best]
-    quota = None                                   # cgroup CPU quota (cores' worth), when the container sets one
-    try:
-        q, per = open('/sys/fs/cgroup/cpu.max').read().split()[:2]
-        quota = None if q == 'max' else round(int(q) / int(per), 2)
-    except (OSError, ValueError):
-        pass
     return {'value': round(v, 2), 'unit': 'samples/s', 'cores': torch.get_num_threads(), 'affinity_cores': cores,
             'cgroup_cpu_quota_cores': quota, 'kind': 'port', 'variant': best,
             'variants': {k: round(r[0], 2) for k, r in rates.items()},
@@ -179,7 +190,9 @@ def main():
     if args.no_overlap:
         model.overlap_wgrad = False
     trainer = OneTransTrainer(cfg, model=model)
+    log(f'{args.config}: model built ({precision})')
     batches = device_batches(cfg, B, args.nbatches, rank, dev)
+    log(f'{args.nbatches} resident batches of {B}')
     torch.cuda.synchronize()
     model.inputs_ready = True           # resident, complete batches: a row-sharded lookup routes them at once
 
@@ -217,6 +230,7 @@ def main():
         return max(wall, ev0.elapsed_time(ev1) / 1e3), o
 
     times, exposed = [], []
+    log(f'{args.warmup} warm-up steps done')
     for r in range(max(1, args.repeats)):
         t_r, out = timed_region(args.warmup + r * args.steps)
         times.append(t_r)
@@ -377,6 +391,7 @@ def main():
                            'runs block-scaled fp8, whose dense peak is 2x)' if K.matmul_mode() == 'bf16'
                            else 'attention core on native f32 MFMA (peak 157.3)')}
     if not args.no_cpu_baseline and world == 1:          # rank 0 at N=1 only
+        log('timed region and probe done; CPU baseline')
         res['cpu_baseline'] = cpu_baseline(args.config, args.cpu_seconds)
     print(json.dumps(res), flush=True)
 

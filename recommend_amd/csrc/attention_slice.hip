@@ -167,6 +167,9 @@ __host__ __device__ inline int tail_qf(int kb, int q_off, int nqb) {
 // plus an immediate.  hd 64: 144 rows (the backward's LDS limit at I = 140), hd 32: 192.
 template <int HD>
 constexpr int RMAX() { return HD == 64 ? 144 : 192; }
+// key blocks a backward wave may own (its K planes are kept in registers for the phase-2 K image): hd 64,
+// 4 waves, <= 9 key blocks; hd 32, 8 waves, <= 12
+__host__ __device__ constexpr int keep_slots(int hd) { return hd == 64 ? 3 : 2; }
 
 // the wave's schedule row as one uniform 64-bit value (a scalar load at kernel start: an in-loop vector
 // load of the kernel argument would wait, in-order, for every prefetch load issued before it)
@@ -195,10 +198,12 @@ __device__ unsigned long long g_slice_stamps[2][2048][2][8];
 #define SLICE_STAMP(kind, it, k) do {} while (0)
 #endif
 
-// Both kernels are persistent: a workgroup walks slices s = blockIdx.x, + gridDim.x, ... (grid = the
-// co-resident workgroups), and the next slice's operands are loaded into registers while the current
-// slice computes — with one or two workgroups per CU (LDS), a non-persistent grid left every CU loading
-// or computing in lock-step (MFMA busy 19% in the backward, profiles/r04).
+// The backward and the head_dim-64 forward are persistent: a workgroup walks slices s = blockIdx.x,
+// + gridDim.x, ... (grid = the co-resident workgroups), and the next slice's operands are loaded into
+// registers while the current slice computes — at one workgroup per CU (LDS) a non-persistent grid leaves
+// each CU loading, then computing.  The head_dim-32 forward fits two workgroups per CU at 128 VGPRs and runs
+// one slice per workgroup.  MFMA busy is ~20% in both directions at the T shape
+// (profiles/r04/pmc_attn_slice_T.txt): the issue stream (splits, softmax, addressing) sets the time.
 
 // ------------------------------------------------------------------------------------------
 // Forward.  The slice's K and V planes are staged in LDS ([RMAX][HD] x 3 each); each wave takes whole
@@ -510,6 +515,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
     SLICE_STAMP(1, it, 1);
 
     // ---- phase 1: key-block owners
+    constexpr int KEEP = keep_slots(HD);
+    u32x4 keep[KEEP][NT][3];                       // the owned key blocks' K planes, for the phase-2 K image
 #pragma unroll 1
     for (int slot = 0, kb = kb0; kb >= 0; ++slot) {
       const int krow = 16 * kb + li;               // this lane's key
@@ -521,6 +528,14 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
         split8p(kr[t], kp[t]);
         split8p(vr[t], vp[t]);
       }
+#pragma unroll
+      for (int k2 = 0; k2 < KEEP; ++k2)              // uniform branch, static register index
+        if (slot == k2) {
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) keep[k2][t][pl] = kp[t][pl];
+        }
       const int kbn = sched_item(srow1, slot + 1);
       if (kbn >= 0) load_kv(s, kbn);                // next key block's K / V in flight meanwhile
       f32x4 dk[NM], dv[NM];
@@ -606,20 +621,21 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
       }
       kb = kbn;
     }
-    // K image for phase 2: the rows re-read (L2-warm) before the barrier, stored into the Q planes' space after it
-    float kk[SR][8];
-#pragma unroll
-    for (int r = 0; r < SR; ++r) {
-      const int task = threadIdx.x + r * NTH, row = min(task / CPR, I - 1), c = task % CPR;
-      load8(kk[r], Kg + (int64_t)row * p.ld + 8 * c);
-    }
+    // K image for phase 2, in the Q planes' space: each key-block owner stores the K planes it kept (rows past
+    // I hold row I - 1, times dS = 0) — no re-read or re-split of K
     SLICE_STAMP(1, it, 2);
     __syncthreads();                               // dS store complete, Q planes no longer read
     SLICE_STAMP(1, it, 3);
 #pragma unroll
-    for (int r = 0; r < SR; ++r) {
-      const int task = threadIdx.x + r * NTH, row = task / CPR, c = task % CPR;
-      if (task < IP * CPR) store_planes(qimg, PB, poff<HD>(row, c), kk[r]);   // rows past I: row I - 1, times dS = 0
+    for (int k2 = 0; k2 < KEEP; ++k2) {
+      const int kb = sched_item(srow1, k2);
+      if (kb >= 0) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl)
+            *reinterpret_cast<u32x4*>(qimg + pl * PB + poff<HD>(16 * kb + li, 4 * t + g)) = keep[k2][t][pl];
+      }
     }
     __syncthreads();
     SLICE_STAMP(1, it, 4);
@@ -726,17 +742,20 @@ static unsigned persistent_grid(const void* kernel, int threads, size_t lds, int
 // LPT over the SIMDs: waves w and w + 4 share SIMD w & 3 (a workgroup's waves go to the SIMDs
 // cyclically, MI355X_MICROARCH.md §LDS), so each item (heaviest first) goes to the least-loaded SIMD,
 // then to its less-loaded wave.  Returns false if a wave would get more than 8 items.
-static bool lpt(int n, const int* load, int nwv, int8_t (&out)[8][8]) {
+static bool lpt(int n, const int* load, int nwv, int8_t (&out)[8][8], int cap = 8) {
   std::memset(out, -1, sizeof out);
   int sl[4] = {0, 0, 0, 0}, wl[8] = {0, 0, 0, 0, 0, 0, 0, 0}, cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (int i = 0; i < n; ++i) {
-    int s = 0;
-    for (int k = 1; k < 4; ++k)
-      if (sl[k] < sl[s]) s = k;
-    const int w = nwv == 8 && wl[s + 4] < wl[s] ? s + 4 : s;
-    sl[s] += load[i];
+    int w = -1;
+    for (int k = 0; k < 4; ++k) {                  // least-loaded SIMD with a wave under the cap
+      int c = -1;
+      for (int v = k; v < nwv; v += 4)
+        if (cnt[v] < cap && (c < 0 || wl[v] < wl[c])) c = v;
+      if (c >= 0 && (w < 0 || sl[k] < sl[w & 3])) w = c;
+    }
+    if (w < 0) return false;
+    sl[w & 3] += load[i];
     wl[w] += load[i];
-    if (cnt[w] == 8) return false;
     out[w][cnt[w]++] = (int8_t)i;
   }
   return true;
@@ -761,7 +780,7 @@ static bool make_schedule(SliceArgs& p, int hd, int nwv) {
     p.bbase[kb] = (int16_t)base;
     base += nqb - f;
   }
-  if (!lpt(nkb, load, nwv, p.sched[1])) return false;
+  if (!lpt(nkb, load, nwv, p.sched[1], keep_slots(hd))) return false;   // the backward keeps K planes per slot
   for (int idx = 0; idx < nqb; ++idx) load[idx] = (((q_off + std::min(16 * (nqb - 1 - idx) + 15, K - 1)) >> 4) + 2) >> 1;
   return lpt(nqb, load, nwv, p.sched[2]);
 }

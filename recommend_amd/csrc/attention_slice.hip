@@ -401,13 +401,13 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_slice_kernel(SliceArgs p
 // 32 (measured: 1,688-1,697 vs 1,710-1,717 us at hd 64, 931-955 vs 943-1,019 us at hd 32; B 4096 H 4, I 140).
 // Software pipelining of phase 1 (step a + 2's S / dP issued before step a's softmax gradient) measured
 // 1-4% slower at hd 64 and within noise at hd 32; not kept.
-template <int HD, int NWV>
+template <int HD, int NWV, bool LAT_ = NWV == 4>
 __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NT = HD / 32, NM = HD / 16, CPR = HD / 8, NTH = 64 * NWV;
   constexpr int RM = RMAX<HD>(), PB = RM * HD * 2;
   constexpr int SR = (RM * CPR + NTH - 1) / NTH;
-  constexpr bool LAT = NWV == 4;                    // one wave per SIMD: fragment reads one item ahead, fenced
+  constexpr bool LAT = LAT_;                        // fragment reads one item ahead, fenced (one wave per SIMD)
   constexpr int RBY = HD * 2;                       // bytes per plane image row
   const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform
@@ -842,6 +842,8 @@ int attn_slice_bwd(const float* qkv, int64_t ld, const float* out, const float* 
                    int I, int K, int head_dim, float* dqkv, hipStream_t stream) {
   using namespace slice;
   using KF = void (*)(SliceArgs);
+  // fenced one-item-ahead fragment reads: head_dim 64 (one wave per SIMD); at head_dim 32 (two waves per
+  // SIMD) they measured within noise (914-952 vs 933-938 us) and are off
   static const KF k32 = attn_bwd_slice_kernel<32, BWD_WAVES32>, k64 = attn_bwd_slice_kernel<64, BWD_WAVES64>;
   static std::once_flag once;
   std::call_once(once, [] {

@@ -30,7 +30,9 @@ def attn_ref(qkv, B, H, I, qpos, hd):
 
 SHAPES = [(3, 4, 140, 140, 32), (2, 4, 140, 140, 64), (2, 2, 144, 144, 64), (2, 4, 17, 17, 32),
           (2, 4, 33, 20, 64), (2, 2, 192, 192, 32), (2, 2, 100, 37, 64), (1, 4, 16, 5, 32), (2, 4, 5, 5, 32),
-          (2, 2, 130, 128, 64), (3, 2, 130, 129, 32), (2, 4, 141, 140, 32)]
+          (2, 2, 130, 128, 64), (3, 2, 130, 129, 32), (2, 4, 141, 140, 32),
+          # more slices than co-resident workgroups: the persistent loop's later slices (prefetch, restaging)
+          (300, 4, 140, 140, 64), (600, 4, 140, 140, 32), (257, 3, 100, 60, 64)]
 
 
 def _supported(I, Kq, hd):

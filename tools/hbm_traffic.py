@@ -28,7 +28,7 @@ FAMILIES = {'gemm': ('mixed_gemm_kernel', 'plane_gemm_kernel', 'wgrad_kernel<', 
             'embedding': ('ns_assemble', 'ns_grad_pack', 'seq_rows', 'keys_prep', 'head_flags', 'seg_start',
                           'piece_count', 'piece_sum', 'seg_sum', 'clip_scale', 'adagrad_apply', 'rocprim',
                           'scatter_rows', 'dense_sumsq', 'dense_adagrad', 'sum_parts', 'clip_from_sumsq')}
-PER_KERNEL = ('embedding',)     # families also broken down per kernel name (with kernel-trace durations)
+PER_KERNEL = ('embedding', 'attention')   # families also broken down per kernel name (with kernel-trace durations)
 
 
 def short(name):

@@ -133,30 +133,69 @@ __device__ __forceinline__ int64_t kept_row(int64_t o, int K, int I, const int32
 // erf for the GELU: branch-free rational minimax on [-4, 4] (|error| < 5e-7; erf(±4) rounds to ±1 in
 // fp32).  This is the float erf TensorFlow's CPU kernels evaluate (Eigen's generic fast erf), so it
 // is also the reference's own arithmetic; ~15 VALU ops instead of the two-regime libm erff.
-__device__ __forceinline__ float fast_erf(float a) {
+// Every multiply-add is an explicit fma (no contraction left to the compiler) so the scalar form and the
+// packed-pair form below give identical bits per element; the pair form runs the polynomials on
+// v_pk_fma_f32 / v_pk_mul_f32 (half the VALU issue of four scalar evaluations: the GELU prologues and
+// epilogues of the FFN GEMMs evaluate it once per element of a [rows, f] tensor).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+#define OT_ERF_P(V, T)                                                   \
+  V = __builtin_elementwise_fma(V, x2, (T)(2.77068142495902e-08f));      \
+  V = __builtin_elementwise_fma(V, x2, (T)(-2.10102402082508e-06f));     \
+  V = __builtin_elementwise_fma(V, x2, (T)(-5.69250639462346e-05f));     \
+  V = __builtin_elementwise_fma(V, x2, (T)(-7.34990630326855e-04f));     \
+  V = __builtin_elementwise_fma(V, x2, (T)(-2.95459980854025e-03f));     \
+  V = __builtin_elementwise_fma(V, x2, (T)(-1.60960333262415e-02f));
+#define OT_ERF_Q(V, T)                                                   \
+  V = __builtin_elementwise_fma(V, x2, (T)(-2.13374055278905e-04f));     \
+  V = __builtin_elementwise_fma(V, x2, (T)(-1.68282697438203e-03f));     \
+  V = __builtin_elementwise_fma(V, x2, (T)(-7.37332916720468e-03f));     \
+  V = __builtin_elementwise_fma(V, x2, (T)(-1.42647390514189e-02f));
+// 1 + erf(a)
+__device__ __forceinline__ float one_plus_erf(float a) {
   const float x = fminf(fmaxf(a, -4.f), 4.f);
   const float x2 = x * x;
   float p = -2.72614225801306e-10f;
-  p = fmaf(p, x2, 2.77068142495902e-08f);
-  p = fmaf(p, x2, -2.10102402082508e-06f);
-  p = fmaf(p, x2, -5.69250639462346e-05f);
-  p = fmaf(p, x2, -7.34990630326855e-04f);
-  p = fmaf(p, x2, -2.95459980854025e-03f);
-  p = fmaf(p, x2, -1.60960333262415e-02f);
+  OT_ERF_P(p, float)
   float q = -1.45660718464996e-05f;
-  q = fmaf(q, x2, -2.13374055278905e-04f);
-  q = fmaf(q, x2, -1.68282697438203e-03f);
-  q = fmaf(q, x2, -7.37332916720468e-03f);
-  q = fmaf(q, x2, -1.42647390514189e-02f);
-  return x * p * __builtin_amdgcn_rcpf(q);
+  OT_ERF_Q(q, float)
+  return __builtin_fmaf(x * p, __builtin_amdgcn_rcpf(q), 1.0f);
 }
+__device__ __forceinline__ f32x2 one_plus_erf2(f32x2 a) {
+  const f32x2 x = __builtin_elementwise_min(__builtin_elementwise_max(a, (f32x2)(-4.f)), (f32x2)(4.f));
+  const f32x2 x2 = x * x;
+  f32x2 p = (f32x2)(-2.72614225801306e-10f);
+  OT_ERF_P(p, f32x2)
+  f32x2 q = (f32x2)(-1.45660718464996e-05f);
+  OT_ERF_Q(q, f32x2)
+  const f32x2 r = {__builtin_amdgcn_rcpf(q.x), __builtin_amdgcn_rcpf(q.y)};
+  return __builtin_elementwise_fma(x * p, r, (f32x2)(1.0f));
+}
+#undef OT_ERF_P
+#undef OT_ERF_Q
 __device__ __forceinline__ float gelu_erf(float x) {
-  return 0.5f * x * (1.0f + fast_erf(x * 0.70710678118654752440f));
+  return (0.5f * x) * one_plus_erf(x * 0.70710678118654752440f);
 }
 __device__ __forceinline__ float gelu_erf_grad(float x) {
   // d/dx 0.5 x (1 + erf(x/sqrt2)) = 0.5 (1 + erf(x/sqrt2)) + x * exp(-x^2/2) / sqrt(2 pi)
-  return 0.5f * (1.0f + fast_erf(x * 0.70710678118654752440f)) +
-         x * 0.39894228040143267794f * __builtin_amdgcn_exp2f(-0.72134752044448170368f * x * x);
+  return __builtin_fmaf(x * 0.39894228040143267794f, __builtin_amdgcn_exp2f((-0.72134752044448170368f * x) * x),
+                        0.5f * one_plus_erf(x * 0.70710678118654752440f));
+}
+__device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
+  return (0.5f * x) * one_plus_erf2(x * 0.70710678118654752440f);
+}
+__device__ __forceinline__ f32x2 gelu_erf_grad2(f32x2 x) {
+  const f32x2 t = (-0.72134752044448170368f * x) * x;
+  const f32x2 e = {__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+  return __builtin_elementwise_fma(x * 0.39894228040143267794f, e, 0.5f * one_plus_erf2(x * 0.70710678118654752440f));
+}
+// four elements as two packed pairs (bit-identical to gelu_erf / gelu_erf_grad per element)
+__device__ __forceinline__ f32x4 gelu_erf4(f32x4 v) {
+  const f32x2 a = gelu_erf2(f32x2{v.x, v.y}), b = gelu_erf2(f32x2{v.z, v.w});
+  return f32x4{a.x, a.y, b.x, b.y};
+}
+__device__ __forceinline__ f32x4 gelu_erf_grad4(f32x4 v) {
+  const f32x2 a = gelu_erf_grad2(f32x2{v.x, v.y}), b = gelu_erf_grad2(f32x2{v.z, v.w});
+  return f32x4{a.x, a.y, b.x, b.y};
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -119,7 +119,7 @@ __device__ __forceinline__ f32x4 apply_pro(f32x4 v, int xf, float rs, const floa
   if (xf == OT_AX_RMSNORM) {
     v.x *= rs * gamma[k]; v.y *= rs * gamma[k + 1]; v.z *= rs * gamma[k + 2]; v.w *= rs * gamma[k + 3];
   } else if (xf == OT_AX_GELU) {
-    v.x = gelu_erf(v.x); v.y = gelu_erf(v.y); v.z = gelu_erf(v.z); v.w = gelu_erf(v.w);
+    v = gelu_erf4(v);
   }
   return v;
 }
@@ -249,10 +249,9 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
           if (ROWSCALE) v = v * rsc[i0 + i];
           if (epi & OT_EPI_BIAS) v += bias4;
           if (epi & OT_EPI_GELU_BWD) {
-            v.x *= gelu_erf_grad(aux4[i].x); v.y *= gelu_erf_grad(aux4[i].y);
-            v.z *= gelu_erf_grad(aux4[i].z); v.w *= gelu_erf_grad(aux4[i].w);
+            v *= gelu_erf_grad4(aux4[i]);
             if (p.gelu_out && orr >= 0) {                      // the stored GELU (W2 weight gradient's A)
-              const f32x4 hv = {gelu_erf(aux4[i].x), gelu_erf(aux4[i].y), gelu_erf(aux4[i].z), gelu_erf(aux4[i].w)};
+              const f32x4 hv = gelu_erf4(aux4[i]);
               *reinterpret_cast<u32x2*>(p.gelu_out + (int64_t)orr * p.ldgelu + col) = bf16_rne4(hv);
             }
             if (ROWDOT) {                                      // this tile's part of sum_f dU_f (U_f - b_f)
@@ -262,7 +261,7 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
             }
           }
           if (epi & OT_EPI_GELU) {
-            v.x = gelu_erf(v.x); v.y = gelu_erf(v.y); v.z = gelu_erf(v.z); v.w = gelu_erf(v.w);
+            v = gelu_erf4(v);
           }
           if (RMSBWD) {
             // v = dL/dy of y = x * rstd * gamma:  dx = rstd * (g - x * rstd^2 * <g, x> / N) + dres
@@ -317,7 +316,7 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
             }
           }
           if (GSTORE && p.gelu_out && orr >= 0) {              // FFN1 forward: also gelu(U) in bf16
-            const f32x4 hv = {gelu_erf(v.x), gelu_erf(v.y), gelu_erf(v.z), gelu_erf(v.w)};
+            const f32x4 hv = gelu_erf4(v);
             *reinterpret_cast<u32x2*>(p.gelu_out + (int64_t)orr * p.ldgelu + col) = bf16_rne4(hv);
           }
           if (GS && p.c16_out && orr >= 0)                     // + a bf16 copy of C (the next GEMM's A)
@@ -428,7 +427,7 @@ __global__ __launch_bounds__(256, (NT && SPLT) ? 2 : OT_GEMM_MINWG) void mixed_g
       if (!RMS_EARLY && ax == OT_AX_RMSNORM) {
         v = v * gm * ars[i];
       } else if (ax == OT_AX_GELU) {
-        v.x = gelu_erf(v.x); v.y = gelu_erf(v.y); v.z = gelu_erf(v.z); v.w = gelu_erf(v.w);
+        v = gelu_erf4(v);
       }
       if (!(aok[i] && kin)) v = zero4;
       *reinterpret_cast<f32x4*>(as + (sr + RPP * i) * GLD + 4 * sc) = v;
@@ -487,7 +486,7 @@ __global__ __launch_bounds__(256, (NT && SPLT) ? 2 : OT_GEMM_MINWG) void mixed_g
         if (!RMS_EARLY && ax == OT_AX_RMSNORM) {
           v = v * st.g * ars[i];
         } else if (ax == OT_AX_GELU) {
-          v.x = gelu_erf(v.x); v.y = gelu_erf(v.y); v.z = gelu_erf(v.z); v.w = gelu_erf(v.w);
+          v = gelu_erf4(v);
         }
         if (!(aok[i] && st.kin)) v = zero4;
         const f32x4 w = (bok[i] && st.kin) ? st.b[i] : zero4;
@@ -887,6 +886,8 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
       *reinterpret_cast<u32x4*>(xnp + 16 * kt) = u32x4{b0.x, b0.y, b1.x, b1.y};
     }
     if (AXT == OT_AX_GELU) {
+      // scalar form here (bit-identical per element to gelu_erf4): the packed pairs measured 2-3% slower in this
+      // main loop (register pressure next to the stage copies), while the epilogues and the weight gradient gain
       a0.x = gelu_erf(a0.x); a0.y = gelu_erf(a0.y); a0.z = gelu_erf(a0.z); a0.w = gelu_erf(a0.w);
       a1.x = gelu_erf(a1.x); a1.y = gelu_erf(a1.y); a1.z = gelu_erf(a1.z); a1.w = gelu_erf(a1.w);
     }
@@ -1028,7 +1029,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
       if (ax == OT_AX_RMSNORM) {
         a = a * gv[i] * rsd;
       } else if (ax == OT_AX_GELU) {
-        a.x = gelu_erf(a.x); a.y = gelu_erf(a.y); a.z = gelu_erf(a.z); a.w = gelu_erf(a.w);
+        a = gelu_erf4(a);
       }
       if (!(aok && k0 + kk < p.K)) a = zero4;
       if (!(dok && n0 + kk < p.N)) dv = zero4;
@@ -1219,7 +1220,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(WgradArgs p) {
         if (ax == OT_AX_RMSNORM) {
           a = a * gv[i] * rsd[j];
         } else if (ax == OT_AX_GELU) {
-          a.x = gelu_erf(a.x); a.y = gelu_erf(a.y); a.z = gelu_erf(a.z); a.w = gelu_erf(a.w);
+          a = gelu_erf4(a);
         }
         if (!(inr[j] && k0 + 4 * cc < p.K)) a = zero4;
         if (!(inr[j] && n0 + 4 * cc < p.N)) dv = zero4;

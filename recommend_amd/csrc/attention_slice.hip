@@ -582,16 +582,30 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
           const int q0 = 16 * qb + 4 * g;
           const f32x4 L = *reinterpret_cast<const f32x4*>(lse2 + q0);
           const f32x4 D = *reinterpret_cast<const f32x4*>(dlt + q0);
-          const i32x4 Qp = *reinterpret_cast<const i32x4*>(qps + q0);
           char* blk = dss + 1024 * (blk0 + qb - a0);
+          // the causal mask only on blocks the diagonal crosses (uniform): elsewhere every key of the block
+          // precedes every query (padded queries have lse +inf, so P = 0 without it; the key block holding
+          // keys past I is always on the diagonal)
+          if (16 * kb + 15 > q_off + 16 * qb) {
+            const i32x4 Qp = *reinterpret_cast<const i32x4*>(qps + q0);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float e = __builtin_amdgcn_exp2f(fmaf(sc[half][i], c1, -L[i]));
-            const float pv = krow <= Qp[i] ? e : 0.f;
-            const float ds = pv * (dc[half][i] - D[i]) * p.scale;
-            P[4 * half + i] = pv;
-            dS[4 * half + i] = ds;
-            *reinterpret_cast<float*>(blk + dsw[i]) = ds;
+            for (int i = 0; i < 4; ++i) {
+              const float e = __builtin_amdgcn_exp2f(fmaf(sc[half][i], c1, -L[i]));
+              const float pv = krow <= Qp[i] ? e : 0.f;
+              const float ds = pv * (dc[half][i] - D[i]) * p.scale;
+              P[4 * half + i] = pv;
+              dS[4 * half + i] = ds;
+              *reinterpret_cast<float*>(blk + dsw[i]) = ds;
+            }
+          } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float pv = __builtin_amdgcn_exp2f(fmaf(sc[half][i], c1, -L[i]));
+              const float ds = pv * (dc[half][i] - D[i]) * p.scale;
+              P[4 * half + i] = pv;
+              dS[4 * half + i] = ds;
+              *reinterpret_cast<float*>(blk + dsw[i]) = ds;
+            }
           }
         }
         u32x4 pp[3], sp[3];

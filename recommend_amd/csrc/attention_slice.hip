@@ -167,9 +167,11 @@ __host__ __device__ inline int tail_qf(int kb, int q_off, int nqb) {
 // plus an immediate.  hd 64: 144 rows (the backward's LDS limit at I = 140), hd 32: 192.
 template <int HD>
 constexpr int RMAX() { return HD == 64 ? 144 : 192; }
-// key blocks a backward wave may own (its K planes are kept in registers for the phase-2 K image): hd 64,
-// 4 waves, <= 9 key blocks; hd 32, 8 waves, <= 12
-__host__ __device__ constexpr int keep_slots(int hd) { return hd == 64 ? 3 : 2; }
+// key blocks a backward wave may own (its K planes are kept in registers for the phase-2 K image): at most
+// RMAX / 16 key blocks (9 at hd 64, 12 at hd 32) over the workgroup's waves
+__host__ __device__ constexpr int keep_slots(int hd, int nwv) {
+  return ((hd == 64 ? 144 : 192) / 16 + nwv - 1) / nwv;
+}
 
 // the wave's schedule row as one uniform 64-bit value (a scalar load at kernel start: an in-loop vector
 // load of the kernel argument would wait, in-order, for every prefetch load issued before it)
@@ -515,7 +517,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
     SLICE_STAMP(1, it, 1);
 
     // ---- phase 1: key-block owners
-    constexpr int KEEP = keep_slots(HD);
+    constexpr int KEEP = keep_slots(HD, NWV);
     u32x4 keep[KEEP][NT][3];                       // the owned key blocks' K planes, for the phase-2 K image
 #pragma unroll 1
     for (int slot = 0, kb = kb0; kb >= 0; ++slot) {
@@ -794,7 +796,7 @@ static bool make_schedule(SliceArgs& p, int hd, int nwv) {
     p.bbase[kb] = (int16_t)base;
     base += nqb - f;
   }
-  if (!lpt(nkb, load, nwv, p.sched[1], keep_slots(hd))) return false;   // the backward keeps K planes per slot
+  if (!lpt(nkb, load, nwv, p.sched[1], keep_slots(hd, nwv))) return false;   // the backward keeps K planes per slot
   for (int idx = 0; idx < nqb; ++idx) load[idx] = (((q_off + std::min(16 * (nqb - 1 - idx) + 15, K - 1)) >> 4) + 2) >> 1;
   return lpt(nqb, load, nwv, p.sched[2]);
 }
@@ -805,9 +807,13 @@ static int g_enabled = [] {
 }();
 
 // waves per workgroup (measured, B 4096 H 4 I 140): forward 8 (hd 32: 4 waves / SIMD at 128 VGPRs); backward hd 32
-// 8 (4 waves: 1,136-1,160 vs 928-965 us), hd 64 4 (one wave per SIMD with up to 512 registers; 8 waves spill at
+// 8 (4 waves: 1,136-1,160 vs 928-965 us; again 1,066-1,093 vs 919-948 with the kept K planes and fenced
+// fragment reads), hd 64 4 (one wave per SIMD with up to 512 registers; 8 waves spill at
 // the 256-register limit: 1,971-2,095 vs 1,688-1,782 us)
-constexpr int FWD_WAVES = 8, BWD_WAVES32 = 8, BWD_WAVES64 = 4;
+#ifndef OT_SLICE_BWD32_WAVES
+#define OT_SLICE_BWD32_WAVES 8
+#endif
+constexpr int FWD_WAVES = 8, BWD_WAVES32 = OT_SLICE_BWD32_WAVES, BWD_WAVES64 = 4;
 
 template <typename F>
 static void raise_lds_limit(F* k) {

@@ -132,6 +132,18 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
   return base + (b >> 3);
 }
 
+// Weight-gradient tiles: whole row chunks per XCD.  Block b runs on XCD b % 8 (round-robin dispatch), so XCD x
+// takes chunks x, x + 8, x + 16, ... and each chunk's (k, n) tiles occupy consecutive dispatch slots of that XCD:
+// every tile of a chunk streams the same rows, and they are then read through one L2.  (The contiguous-range
+// remap split chunks across two XCDs whenever a range was not a whole number of chunks: C5's W1 weight gradient
+// fetched 2.3x its algorithmic bytes.)  The grid is padded to whole rounds of 8 chunks; padding blocks return.
+__device__ __forceinline__ bool wgrad_tile(int b, int per_chunk, int nchunks, int& c, int& rem) {
+  const int x = b & 7, j = b >> 3;
+  c = x + 8 * (j / per_chunk);
+  rem = j % per_chunk;
+  return c < nchunks;
+}
+
 // ---- vector epilogue shared by the GEMM kernels (compile-time flags EPIT >= 0, no edge tiles): the
 // accumulator tile goes through LDS (the staging buffers are free: the caller's last barrier ended
 // every main-loop read) in two 64-row halves; each thread then finishes 8 rows x one float4 column
@@ -968,9 +980,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
   const int per_chunk = p.ntk * p.ntn;
   // XCD-aware: the output tiles of one chunk (which share its A or D rows) get consecutive logical
   // ids, and xcd_remap places consecutive ids on one XCD, so the shared rows come from that L2
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int c = wg / per_chunk;
-  const int rem = wg % per_chunk;
+  int c, rem;
+  if (!wgrad_tile(blockIdx.x, per_chunk, p.nchunks, c, rem)) return;
   const int tk = rem / p.ntn, tn = rem % p.ntn;
   const int k0 = tk * GT, n0 = tn * GT;
   const int row_begin = p.chunks[3 * c + 1], row_count = p.chunks[3 * c + 2];
@@ -1136,9 +1147,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(WgradArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem_c[];
   const int ax = AXT >= 0 ? AXT : p.a_xform;
   const int per_chunk = p.ntk * p.ntn;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int c = wg / per_chunk;
-  const int rem = wg % per_chunk;
+  int c, rem;
+  if (!wgrad_tile(blockIdx.x, per_chunk, p.nchunks, c, rem)) return;
   const int tk = rem / p.ntn, tn = rem % p.ntn;
   const int k0 = tk * GT, n0 = tn * GT;
   const int row_begin = p.chunks[3 * c + 1], row_count = p.chunks[3 * c + 2];
@@ -1389,8 +1399,8 @@ template <bool IDL>
 __global__ __launch_bounds__(256, OT_WGRAD_COPY_MINW) void wgrad_bf16_kernel(WgradArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem_c[];
   const int per_chunk = p.ntk * p.ntn;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int c = wg / per_chunk, rem = wg % per_chunk;
+  int c, rem;
+  if (!wgrad_tile(blockIdx.x, per_chunk, p.nchunks, c, rem)) return;
   const int tk = rem / p.ntn, tn = rem % p.ntn;
   const int k0 = tk * GT, n0 = tn * GT;
   const int row_begin = p.chunks[3 * c + 1], row_count = p.chunks[3 * c + 2];
@@ -2089,7 +2099,7 @@ extern "C" int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a
         (void)hipGetLastError();
       });
     }
-    hipLaunchKernelGGL(kern, dim3((unsigned)nchunks * p.ntk * p.ntn), dim3(256),
+    hipLaunchKernelGGL(kern, dim3((unsigned)(ceil_div(nchunks, 8) * 8) * p.ntk * p.ntn), dim3(256),
                        copy ? copy_shmem : split ? split_shmem : shmem, s, p);
     OT_LAUNCH_CHECK("ot_mixed_gemm_wgrad");
   }

@@ -156,6 +156,16 @@ __device__ __forceinline__ void store_out4(float* dst, f32x4 v) {
   if (OT_GEMM_NT_STORE) __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(dst));
   else *reinterpret_cast<f32x4*>(dst) = v;
 }
+// four values rounded to bf16 (8 B), streamed like store_out4: the bf16-mode outputs (C, gelu(U), the bf16
+// residual copies) are the bulk of those GEMMs' traffic, and written through the L2 they evict the A rows the
+// tile's neighbours in N still read
+#ifndef OT_GEMM_NT_STORE16
+#define OT_GEMM_NT_STORE16 1
+#endif
+__device__ __forceinline__ void store_out4_bf16(uint16_t* dst, f32x4 v) {
+  if (OT_GEMM_NT_STORE16) __builtin_nontemporal_store(bf16_rne4(v), reinterpret_cast<u32x2*>(dst));
+  else *reinterpret_cast<u32x2*>(dst) = bf16_rne4(v);
+}
 
 // GS: compile the forward stored-GELU path (bf16-mode plane GEMM only: registers elsewhere)
 template <int EPIT, int LAYOUT, bool ROWSCALE, int RBN = 8, bool GS = false>
@@ -264,7 +274,7 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
             v *= gelu_erf_grad4(aux4[i]);
             if (p.gelu_out && orr >= 0) {                      // the stored GELU (W2 weight gradient's A)
               const f32x4 hv = gelu_erf4(aux4[i]);
-              *reinterpret_cast<u32x2*>(p.gelu_out + (int64_t)orr * p.ldgelu + col) = bf16_rne4(hv);
+              store_out4_bf16(p.gelu_out + (int64_t)orr * p.ldgelu + col, hv);
             }
             if (ROWDOT) {                                      // this tile's part of sum_f dU_f (U_f - b_f)
               const f32x4 ub = aux4[i] - rdb4;
@@ -329,12 +339,12 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
           }
           if (GSTORE && p.gelu_out && orr >= 0) {              // FFN1 forward: also gelu(U) in bf16
             const f32x4 hv = gelu_erf4(v);
-            *reinterpret_cast<u32x2*>(p.gelu_out + (int64_t)orr * p.ldgelu + col) = bf16_rne4(hv);
+            store_out4_bf16(p.gelu_out + (int64_t)orr * p.ldgelu + col, hv);
           }
           if (GS && p.c16_out && orr >= 0)                     // + a bf16 copy of C (the next GEMM's A)
-            *reinterpret_cast<u32x2*>(p.c16_out + (int64_t)orr * p.ldc16 + col) = bf16_rne4(v);
+            store_out4_bf16(p.c16_out + (int64_t)orr * p.ldc16 + col, v);
           if (CBF) {                                           // C in bf16 (the FFN2 dgrad's dU)
-            if (orr >= 0) *reinterpret_cast<u32x2*>(reinterpret_cast<uint16_t*>(p.C) + (int64_t)orr * p.ldc + col) = bf16_rne4(v);
+            if (orr >= 0) store_out4_bf16(reinterpret_cast<uint16_t*>(p.C) + (int64_t)orr * p.ldc + col, v);
           } else if (orr >= 0) {
             store_out4(p.C + (int64_t)orr * p.ldc + col, v);
           }

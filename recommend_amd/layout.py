@@ -30,14 +30,21 @@ IMAGE_UNIT_ELEMS = 3 * TILE * 16      # one (group, column tile, 16-k stage) blo
 # all of C2's) are capped at one round of the split kernel's 512 resident workgroups -- a count just
 # past a multiple of 512 (e.g. 513) leaves a nearly empty extra round; capped, the C2 GEMM family
 # measured 332 -> 316 us/launch standalone.  Weights of >= 8 tiles (d >= 256) take ~3 rounds plus one
-# chunk per weight group (C5 +5-7%, T +2% over 768; a hard cap measured worse there).  Tuning override
-# ONETRANS_WGRAD_SLOTS (both cases); tools/wgrad_probe.py sweeps it.
+# chunk per weight group (C5 +5-7%, T +2% over 768; a hard cap measured worse there).  Weights of >= 32
+# tiles (d = 512: C5's) take 4096 since the kernels place whole chunks per XCD (round 4, gemm.hip
+# wgrad_tile): shorter chunks keep a chunk's tiles closer together in the rows they stream, so more of the
+# shared rows hit the XCD's L2 (C5 1,425 / 1,438 / 1,463 / 1,466 samples/s at 1536 / 3072 / 4096 / 6144 on one
+# box; T, C3, C4 flat or -1% at 3072, so they keep 1536).  Tuning override ONETRANS_WGRAD_SLOTS (every case);
+# tools/wgrad_probe.py sweeps it.
 _SLOTS_ENV = os.environ.get('ONETRANS_WGRAD_SLOTS')
 WGRAD_SLOTS = int(_SLOTS_ENV) if _SLOTS_ENV else 1536
 WGRAD_SLOTS_SMALL = int(_SLOTS_ENV) if _SLOTS_ENV else 512
+WGRAD_SLOTS_LARGE = int(_SLOTS_ENV) if _SLOTS_ENV else 4096
 
 
 def wgrad_slots(tiles_per_chunk: int) -> int:
+    if tiles_per_chunk >= 32:
+        return WGRAD_SLOTS_LARGE
     return WGRAD_SLOTS if tiles_per_chunk >= 8 else WGRAD_SLOTS_SMALL
 
 

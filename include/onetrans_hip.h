@@ -379,7 +379,24 @@ size_t ot_head_bwd_workspace_size(int T, int B, int dh);
 int ot_head_bwd(const float* pre1, const float* w2, const float* probs, const float* dprobs, int T, int B,
                 int dh, float* dpre1, float* dw2, float* db2, int64_t task_stride_w2, int64_t task_stride_b2,
                 int accumulate, void* workspace, size_t ws_bytes, void* stream);
-/* tf.keras.losses.BinaryCrossentropy(from_logits=False) summed over tasks, train.py:78-93/124-128:
+/* ot_head_bwd with the loss gradient given w.r.t. the logits and / or the probabilities (either may be null):
+ * dz = dlogits + dprobs * p (1 - p).  The model's training path passes dlogits (ot_task_loss_logits_bwd). */
+int ot_head_bwd_ex(const float* pre1, const float* w2, const float* probs, const float* dprobs, const float* dlogits,
+                   int T, int B, int dh, float* dpre1, float* dw2, float* db2, int64_t task_stride_w2,
+                   int64_t task_stride_b2, int accumulate, void* workspace, size_t ws_bytes, void* stream);
+/* The task loss of train.py:78-93 as the reference's Keras 2.12 evaluates it on its sigmoid heads (model.py:327-329,
+ * train.py:84-87, 124-128): keras.activations.sigmoid caches its input as the output's _keras_logits and
+ * keras.backend.binary_crossentropy(from_logits=False) then computes tf.nn.sigmoid_cross_entropy_with_logits:
+ *   BCE task t:  mean_b  max(z, 0) - z y + log(1 + exp(-|z|))      (z = logits[t][b]; no clipping)
+ *   MSE task t (bit t of mse_mask, tasks other than 'ctr' / 'cvr'):  mean_b (y - p)^2
+ * loss = sum over the T <= 32 tasks.  Workspace: ot_bce_workspace_size.
+ * bwd: dlogits = gscale[0] * d loss / d z = gscale (p - y) / B (BCE), gscale 2 (p - y) p (1 - p) / B (MSE). */
+int ot_task_loss_logits_fwd(const float* logits, const float* probs, const float* labels, int T, int B,
+                            unsigned mse_mask, float* loss, void* workspace, size_t ws_bytes, void* stream);
+int ot_task_loss_logits_bwd(const float* probs, const float* labels, const float* gscale, int T, int B,
+                            unsigned mse_mask, float* dlogits, void* stream);
+/* The probability form (a caller holding only probabilities: Keras without a cached logit):
+ * tf.keras.losses.BinaryCrossentropy(from_logits=False) summed over tasks,
  * loss = sum_t mean_b -(y log(clip(p)+eps) + (1-y) log(1-clip(p)+eps)). */
 size_t ot_bce_workspace_size(int T, int B);
 int ot_bce_fwd(const float* probs, const float* labels, int T, int B, float* loss, void* workspace,

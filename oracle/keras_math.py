@@ -51,6 +51,12 @@ def keras_bce(y: np.ndarray, p: np.ndarray) -> float:
     return float(np.mean(bce))
 
 
+def keras_bce_logits(y: np.ndarray, z: np.ndarray) -> float:
+    """The same loss on a sigmoid head's output in Keras 2.12 (the cached ``_keras_logits`` path):
+    tf.nn.sigmoid_cross_entropy_with_logits = max(z, 0) - z y + log(1 + exp(-|z|)), SUM_OVER_BATCH_SIZE."""
+    return float(np.mean(np.maximum(z, 0.0) - z * y + np.log1p(np.exp(-np.abs(z)))))
+
+
 def clip_by_norm(g: np.ndarray, clip: float) -> np.ndarray:
     """tf.clip_by_norm (train.py:135): g * clip / max(||g||_2, clip)."""
     l2 = np.sqrt(np.sum(g * g))

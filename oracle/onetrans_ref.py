@@ -278,9 +278,18 @@ def forward(P, cfg, ns, seq, training: bool = False, seed: int = 0,
 
 
 def keras_bce(y: Tensor, p: Tensor) -> Tensor:
+    """BinaryCrossentropy(from_logits=False) on bare probabilities (Keras clips p, eps inside the logs)."""
     eps = km.KERAS_EPSILON
     pc = torch.clamp(p, eps, 1.0 - eps)
     return torch.mean(-(y * torch.log(pc + eps) + (1.0 - y) * torch.log(1.0 - pc + eps)))
+
+
+def keras_bce_logits(y: Tensor, z: Tensor) -> Tensor:
+    """BinaryCrossentropy(from_logits=False) on the output of a sigmoid Dense head (model.py:327-329) in Keras
+    2.12 (third-party, not in /root/reference): keras.activations.sigmoid caches its input as the output's
+    ``_keras_logits``, and keras.backend.binary_crossentropy then evaluates
+    tf.nn.sigmoid_cross_entropy_with_logits(y, z) = max(z, 0) - z y + log(1 + exp(-|z|)) — no clipping."""
+    return torch.mean(torch.relu(z) - z * y + torch.log1p(torch.exp(-torch.abs(z))))
 
 
 def keras_mse(y: Tensor, p: Tensor) -> Tensor:
@@ -288,9 +297,12 @@ def keras_mse(y: Tensor, p: Tensor) -> Tensor:
     return torch.mean((y - p) ** 2)
 
 
-def task_loss(task: str, y: Tensor, p: Tensor) -> Tensor:
-    """train.py:82-91: BCE for 'ctr'/'cvr', MSE for every other task."""
-    return keras_bce(y, p) if task in ('ctr', 'cvr') else keras_mse(y, p)
+def task_loss(task: str, y: Tensor, p: Tensor, z: Tensor = None) -> Tensor:
+    """train.py:82-91: BCE for 'ctr'/'cvr' (from the head's logits z when given, as the reference's Keras
+    does for its sigmoid heads: keras_bce_logits), MSE for every other task."""
+    if task not in ('ctr', 'cvr'):
+        return keras_mse(y, p)
+    return keras_bce_logits(y, z) if z is not None else keras_bce(y, p)
 
 
 def to_torch(arrs: Dict[str, np.ndarray], dtype=torch.float64, requires_grad=False) -> Dict[str, Tensor]:
@@ -312,7 +324,7 @@ def loss_and_grads(P: Dict[str, Tensor], cfg, ns, seq, labels, training=True, se
     out = forward(leaves, cfg, ns, seq, training=training, seed=seed, variant=variant)
     loss = 0.0
     for t in cfg.tasks:
-        loss = loss + task_loss(t, labels[t].to(out['probs'][t].dtype), out['probs'][t])
+        loss = loss + task_loss(t, labels[t].to(out['probs'][t].dtype), out['probs'][t], out['logits'][t])
     loss.backward()
     grads = {k: (v.grad if v.grad is not None else torch.zeros_like(v)) for k, v in leaves.items()}
     return loss.detach(), grads, out

@@ -108,6 +108,9 @@ SIGNATURES = {
     'ot_bce_bwd': (c_int, [P, P, P, c_int, c_int, P, P]),
     'ot_task_loss_fwd': (c_int, [P, P, c_int, c_int, c_uint32, P, P, c_size_t, P]),
     'ot_task_loss_bwd': (c_int, [P, P, P, c_int, c_int, c_uint32, P, P]),
+    'ot_task_loss_logits_fwd': (c_int, [P, P, P, c_int, c_int, c_uint32, P, P, c_size_t, P]),
+    'ot_task_loss_logits_bwd': (c_int, [P, P, P, c_int, c_int, c_uint32, P, P]),
+    'ot_head_bwd_ex': (c_int, [P, P, P, P, P, c_int, c_int, c_int, P, P, P, I64, I64, c_int, P, c_size_t, P]),
     'ot_sparse_adagrad_workspace_size': (c_size_t, [I64, c_int]),
     'ot_sparse_adagrad': (c_int, [P, P, c_int, I64, P, P, I64, c_float, c_float, c_float, P, c_size_t, P]),
     'ot_sparse_grad_dense': (c_int, [c_int, I64, P, P, I64, P, P, c_size_t, P]),

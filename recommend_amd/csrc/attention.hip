@@ -1646,18 +1646,11 @@ extern "C" size_t ot_attn_bwd_workspace_size(int B, int H, int K) {
 // key-grouped bf16 backward (attn_bwd_group_kernel): long tails only — at C2-like lengths (<= 8 key
 // blocks) the per-pair kernel re-reads little and has more parallelism
 // (4 waves per workgroup measured faster than 8 at C5: 7.19 vs 8.66 ms per layer, 18.36 per pair)
-static int g_attn_bwd_group = [] {
-  const char* e = getenv("ONETRANS_ATTN_BWD_GROUP");
-  return e ? atoi(e) : 4;
-}();
-static int g_attn_bwd_group_min_kb = [] {       // key blocks from which the grouped form is used (A/B: lower)
-  const char* e = getenv("ONETRANS_ATTN_BWD_GROUP_MIN_KB");
-  return e ? atoi(e) : 9;
-}();
+constexpr int ATTN_BWD_GROUP = 4, ATTN_BWD_GROUP_MIN_KB = 9;   // waves (key blocks) per group; from 9 key blocks
 static int attn_bwd_kgroup(int I, int K, int head_dim, bool sel, int prec) {
   if (sel || K <= SMALL_K || prec != OT_MATMUL_BF16 || (head_dim != 32 && head_dim != 64)) return 0;
-  if ((I + 31) / 32 < g_attn_bwd_group_min_kb || (g_attn_bwd_group != 4 && g_attn_bwd_group != 8)) return 0;
-  return g_attn_bwd_group;
+  if ((I + 31) / 32 < ATTN_BWD_GROUP_MIN_KB) return 0;
+  return ATTN_BWD_GROUP;
 }
 static int attn_bwd_kslices(int B, int H, int I, int K, int head_dim, bool sel, int prec) {
   const int g = attn_bwd_kgroup(I, K, head_dim, sel, prec);

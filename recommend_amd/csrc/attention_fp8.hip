@@ -592,18 +592,10 @@ static int attn_fwd_fp8_impl(float* qkv, int64_t ld, int B, int H, int I, int K,
   hipLaunchKernelGGL(pk, pg, dim3(256), 0, s, qkv, ld, H, I, f, dq, deq16);
   OT_LAUNCH_CHECK("ot_attn_fwd_fp8(pack)");
   Fp8AttnArgs p{qkv, ld, H * head_dim, out, lse, B, H, I, K, 1.f / sqrtf((float)head_dim), qpos, f, dq, deq16};
-  // waves per (b, h): ONETRANS_FP8_FWD_WAVES (1: one pair per wave; 4 / 8: a workgroup per pair)
-  static const int pw = [] {
-    const char* e = std::getenv("ONETRANS_FP8_FWD_WAVES");
-    const int v = e ? std::atoi(e) : 8;
-    return (v == 1 || v == 4) ? v : 8;
-  }();
-#define OT_FP8K(PW_) (head_dim == 64 ? (two ? attn_fwd_fp8_kernel<64, 2, PW_> : attn_fwd_fp8_kernel<64, 1, PW_>) \
-                                     : (two ? attn_fwd_fp8_kernel<128, 2, PW_> : attn_fwd_fp8_kernel<128, 1, PW_>))
-  auto fk = pw == 1 ? OT_FP8K(1) : pw == 4 ? OT_FP8K(4) : OT_FP8K(8);
-#undef OT_FP8K
-  const unsigned grid = pw == 1 ? (unsigned)ceil_div(BH, 4) : (unsigned)BH;
-  hipLaunchKernelGGL(fk, dim3(grid), dim3(pw == 1 ? 256 : 64 * pw), 0, s, p);
+  // one workgroup of 8 waves per (b, h) (measured faster than one pair per wave or 4 waves: DESIGN.md §5)
+  auto fk = head_dim == 64 ? (two ? attn_fwd_fp8_kernel<64, 2, 8> : attn_fwd_fp8_kernel<64, 1, 8>)
+                           : (two ? attn_fwd_fp8_kernel<128, 2, 8> : attn_fwd_fp8_kernel<128, 1, 8>);
+  hipLaunchKernelGGL(fk, dim3((unsigned)BH), dim3(64 * 8), 0, s, p);
   OT_LAUNCH_CHECK("ot_attn_fwd_fp8");
   return OT_OK;
 }

@@ -154,6 +154,85 @@ __device__ __forceinline__ void store_planes(char* img, int pb, int o, const flo
   for (int k = 0; k < 3; ++k) *reinterpret_cast<u32x4*>(img + k * pb + o) = pl[k];
 }
 
+// ---- two-plane fp16 form (NP = 2).  x s = h + l with h = fp16(x s), l = fp16(x s - h) (round to nearest even,
+// v_cvt_pk_f16_f32): 22 significant bits, and a product is the sum of the three largest plane products
+// (h h' + h l' + l h', v_mfma_f32_16x16x32_f16; the dropped l l' is below 2^-22 |a||b|).  The power-of-two scale s
+// puts the operand's largest magnitude in [2^13, 2^14) so every plane is a normal fp16 (smaller elements keep an
+// absolute error below 2^-25 of that scale).  Emulated against float64 at the C2 / T slice shapes this is as
+// accurate as the three-plane bf16 split with six products (1e-7 - 4e-7 of max|x| on O, dQ, dK, dV), at half the
+// MFMAs, two planes of LDS images instead of three and a cheaper split.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x4 mmh(u32x4 a, u32x4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+template <int NP>
+__device__ __forceinline__ f32x4 mmaN(const u32x4 (&a)[NP], const u32x4 (&b)[NP], f32x4 c) {
+  if constexpr (NP == 3) {
+    return mma6(a, b, c);
+  } else {
+    c = mmh(a[0], b[1], c);
+    c = mmh(a[1], b[0], c);
+    return mmh(a[0], b[0], c);
+  }
+}
+// 8 floats -> NP planes; NP = 2: of v * s (s a power of two); NP = 3: the exact bf16 split (s must be 1)
+template <int NP>
+__device__ __forceinline__ void splitN(const float* v, float s, u32x4 (&pl)[NP]) {
+  if constexpr (NP == 3) {
+    split8p(v, pl);
+  } else {
+    uint32_t a[4], b[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const f32x2 x = f32x2{v[2 * k], v[2 * k + 1]} * s;
+      const f16x2 h = __builtin_convertvector(x, f16x2);
+      const f16x2 l = __builtin_convertvector(x - __builtin_convertvector(h, f32x2), f16x2);
+      a[k] = __builtin_bit_cast(uint32_t, h);
+      b[k] = __builtin_bit_cast(uint32_t, l);
+    }
+    pl[0] = u32x4{a[0], a[1], a[2], a[3]};
+    pl[1] = u32x4{b[0], b[1], b[2], b[3]};
+  }
+}
+template <int NP>
+__device__ __forceinline__ void frag_atN(u32x4 (&f)[NP], const char* p, int pb) {
+#pragma unroll
+  for (int pl = 0; pl < NP; ++pl) f[pl] = *reinterpret_cast<const u32x4*>(p + pl * pb);
+}
+template <int NP>
+__device__ __forceinline__ void tr_atN(u32x4 (&f)[NP], const char* p0, const char* p1, int pb) {
+#pragma unroll
+  for (int pl = 0; pl < NP; ++pl) {
+    const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(p0 + pl * pb));
+    const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(p1 + pl * pb));
+    const u32x2 x = __builtin_bit_cast(u32x2, lo), y = __builtin_bit_cast(u32x2, hi);
+    f[pl] = u32x4{x.x, x.y, y.x, y.y};
+  }
+}
+template <int NP>
+__device__ __forceinline__ void store_planesN(char* img, int pb, int o, const float (&v)[8], float s) {
+  u32x4 pl[NP];
+  if constexpr (NP == 3) split8(v, pl);
+  else splitN<2>(v, s, pl);
+#pragma unroll
+  for (int k = 0; k < NP; ++k) *reinterpret_cast<u32x4*>(img + k * pb + o) = pl[k];
+}
+// power-of-two scale putting a largest magnitude m in [2^13, 2^14) (1 for m = 0; clamped to the normal range)
+__device__ __forceinline__ float pow2scale(float m) {
+  const int e = (int)((__float_as_uint(m) >> 23) & 255u);   // m in [2^(e-127), 2^(e-126))
+  int se = 127 + 13 - (e - 127);
+  se = e == 0 ? 127 : (se < 1 ? 1 : (se > 254 ? 254 : se));
+  return __uint_as_float((uint32_t)se << 23);
+}
+__device__ __forceinline__ float wave_maxf(float v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
 // tail queries: first 16-query block whose last query sees key block kb (query blocks before the last
 // end at 16f + 15 < K, so the first f with q_off + 16f + 15 >= 16 kb, capped at the last block)
 __host__ __device__ inline int tail_qf(int kb, int q_off, int nqb) {
@@ -217,7 +296,9 @@ __device__ unsigned long long g_slice_stamps[2][2048][2][8];
 // rows (all of them), the next query block's Q (the next slice's first one during the last block).
 // PF: persistent with the next slice's K / V prefetched (hd 64: one workgroup per CU by LDS anyway); without
 // it one workgroup per slice and fewer registers, so more waves per SIMD (hd 32: 4 instead of 2, faster).
-template <int HD, int NWV, bool SEL, bool PF>
+// NP planes per operand: 3 = the exact bf16 split (6 products), 2 = the scaled fp16 pair (3 products, splitN): K and V
+// each get a power-of-two scale per slice (the largest magnitude, reduced over the workgroup), Q one per query (lane)
+template <int HD, int NWV, bool SEL, bool PF, int NP>
 __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_slice_kernel(SliceArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NT = HD / 32, NM = HD / 16, CPR = HD / 8, NTH = 64 * NWV;
@@ -229,8 +310,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_slice_kernel(SliceArgs p
   const int nkb = (I + 15) >> 4, nqb = (K + 15) >> 4, IP = nkb * 16;
   const int nslices = p.B * p.H;
   char* kimg = smem;
-  char* vimg = smem + 3 * PB;
-  int* qposl = reinterpret_cast<int*>(smem + 6 * PB);                // SEL: the slice's kept positions
+  char* vimg = smem + NP * PB;
+  int* qposl = reinterpret_cast<int*>(smem + 2 * NP * PB);           // SEL: the slice's kept positions
+  float* red = reinterpret_cast<float*>(qposl + RMAX<HD>());          // NP = 2: per-wave K / V maxima
   const float qscale = p.scale * L2E;
   auto qkv_of = [&](int s) { return p.qkv + (int64_t)(s / p.H) * I * p.ld + (s % p.H) * HD; };
   // query positions: the tail rule, or (SEL) the slice's kept positions staged in LDS with K / V
@@ -265,7 +347,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_slice_kernel(SliceArgs p
   }
 #pragma unroll
   for (int m = 0; m < NM; ++m) {
-    vtbase[m] = poff<HD>(4 * g + ((lane >> 2) & 3), 2 * m + ((lane & 3) >> 1)) + 8 * (lane & 1) + 3 * PB;
+    vtbase[m] = poff<HD>(4 * g + ((lane >> 2) & 3), 2 * m + ((lane & 3) >> 1)) + 8 * (lane & 1) + NP * PB;
     asm volatile("" : "+v"(vtbase[m]));
   }
   int s = blockIdx.x;
@@ -276,6 +358,31 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_slice_kernel(SliceArgs p
 #pragma unroll 1
   for (int it = 0; s < nslices; s += gridDim.x, ++it) {
     SLICE_STAMP(0, it, 0);
+    float sk = 1.f, sv = 1.f;                                        // K / V scales (NP = 2)
+    if constexpr (NP == 2) {
+      float mk = 0.f, mv = 0.f;
+#pragma unroll
+      for (int r = 0; r < SR; ++r)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {                                 // (rows past I hold row I - 1)
+          mk = fmaxf(mk, fabsf(kr[r][e]));
+          mv = fmaxf(mv, fabsf(vr[r][e]));
+        }
+      mk = wave_maxf(mk);
+      mv = wave_maxf(mv);
+      if (lane == 0) {
+        red[2 * wave] = mk;
+        red[2 * wave + 1] = mv;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int w = 0; w < NWV; ++w) {
+        mk = fmaxf(mk, red[2 * w]);
+        mv = fmaxf(mv, red[2 * w + 1]);
+      }
+      sk = pow2scale(mk);
+      sv = pow2scale(mv);
+    }
 #pragma unroll
     for (int r = 0; r < SR; ++r) {
       const int task = threadIdx.x + r * NTH, row = task / CPR, c = task % CPR;
@@ -285,8 +392,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_slice_kernel(SliceArgs p
           for (int e = 0; e < 8; ++e) kr[r][e] = vr[r][e] = 0.f;
         }
         const int o = poff<HD>(row, c);
-        store_planes(kimg, PB, o, kr[r]);
-        store_planes(vimg, PB, o, vr[r]);
+        store_planesN<NP>(kimg, PB, o, kr[r], sk);
+        store_planesN<NP>(vimg, PB, o, vr[r], sv);
       }
     }
     if (SEL)
@@ -304,12 +411,25 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_slice_kernel(SliceArgs p
       const int qpos = qpos_of(j < K ? j : K - 1);
       const int kbl = qpos_of(min(16 * qb + 15, K - 1)) >> 4;        // last visible key block
       const int kbm = qpos_of(16 * qb) >> 4;                          // key blocks >= kbm may be masked
-      u32x4 qp[NT][3];
+      u32x4 qp[NT][NP];
+      float cs = 1.f;                                                 // NP = 2: S^T = acc * cs (this lane's query)
+      if constexpr (NP == 2) {
+        float mq = 0.f;
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
+        for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) qr[t][e] *= qscale;
-        split8p(qr[t], qp[t]);
+          for (int e = 0; e < 8; ++e) mq = fmaxf(mq, fabsf(qr[t][e]));
+        const float sq = pow2scale(group_max(mq) * qscale) * qscale;   // the query row is spread over 4 lane groups
+#pragma unroll
+        for (int t = 0; t < NT; ++t) splitN<2>(qr[t], sq, qp[t]);
+        cs = qscale / (sk * sq);
+      } else {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) qr[t][e] *= qscale;
+          split8p(qr[t], qp[t]);
+        }
       }
       const int idxn = sched_item(srow, slot + 1);
       if (idxn >= 0) load_q(s, idxn);                                // next block's Q, in flight meanwhile
@@ -323,9 +443,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_slice_kernel(SliceArgs p
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
-          u32x4 fk[3];
-          frag_at(fk, smem + 16 * HD * 2 * kb + kbase[t], PB);
-          acc = mma6(fk, qp[t], acc);                                 // S^T: row = key, col = query
+          u32x4 fk[NP];
+          frag_atN<NP>(fk, smem + 16 * HD * 2 * kb + kbase[t], PB);
+          acc = mmaN<NP>(fk, qp[t], acc);                             // S^T: row = key, col = query
         }
         if (kb >= kbm) {
 #pragma unroll
@@ -335,13 +455,15 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_slice_kernel(SliceArgs p
         sc[kb] = acc;
       }
       mx = group_max(mx);
+      // NP = 2: exp2 of the unscaled S^T, times 2^14 (P's scale, in the exponent: P' in [0, 2^14])
+      const float mxc = NP == 2 ? 14.f - mx * cs : -mx;
       float l = 0.f;
 #pragma unroll
       for (int kb = 0; kb < MAXKB; ++kb) {
         if (kb > kbl) continue;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float e = __builtin_amdgcn_exp2f(sc[kb][i] - mx);
+          const float e = __builtin_amdgcn_exp2f(NP == 2 ? fmaf(sc[kb][i], cs, mxc) : sc[kb][i] + mxc);
           sc[kb][i] = e;
           l += e;
         }
@@ -360,22 +482,22 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_slice_kernel(SliceArgs p
           v[i] = sc[kb][i];
           v[4 + i] = two ? sc[kb + 1][i] : 0.f;
         }
-        u32x4 pp[3];
-        split8p(v, pp);
+        u32x4 pp[NP];
+        splitN<NP>(v, 1.f, pp);
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
-          u32x4 fa[3];
+          u32x4 fa[NP];
           const int ra = 16 * HD * 2 * kb, rb = two ? ra + 16 * HD * 2 : ra;
-          tr_at(fa, smem + ra + vtbase[m], smem + rb + vtbase[m], PB);
-          o[m] = mma6(fa, pp, o[m]);                                  // O^T += V^T P^T
+          tr_atN<NP>(fa, smem + ra + vtbase[m], smem + rb + vtbase[m], PB);
+          o[m] = mmaN<NP>(fa, pp, o[m]);                              // O^T += V^T P^T
         }
       }
       if (j < K) {
-        const float inv = 1.f / l;
+        const float inv = 1.f / (NP == 2 ? l * sv : l);               // (NP = 2: l and O^T carry 2^14, O^T sv)
         float* orow = p.out + ((int64_t)b * K + j) * p.d + h * HD + 4 * g;
 #pragma unroll
         for (int m = 0; m < NM; ++m) *reinterpret_cast<f32x4*>(orow + 16 * m) = o[m] * inv;
-        if (g == 0) p.lse[(int64_t)s * K + j] = mx * LN2 + __logf(l);
+        if (g == 0) p.lse[(int64_t)s * K + j] = NP == 2 ? (mx * cs - 14.f) * LN2 + __logf(l) : mx * LN2 + __logf(l);
       }
       idx = idxn;
     }
@@ -403,7 +525,11 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_slice_kernel(SliceArgs p
 // 32 (measured: 1,688-1,697 vs 1,710-1,717 us at hd 64, 931-955 vs 943-1,019 us at hd 32; B 4096 H 4, I 140).
 // Software pipelining of phase 1 (step a + 2's S / dP issued before step a's softmax gradient) measured
 // 1-4% slower at hd 64 and within noise at hd 32; not kept.
-template <int HD, int NWV, bool LAT_ = NWV == 4>
+// NP = 2 (the scaled fp16 pair): Q and dO get a power-of-two scale per slice and K / V per key block (the owner's),
+// P is exp2(... + 14) (P' = P 2^14, in [0, 2^14]), phase 1's dS a per-key-block scale from the bound
+// |dS| <= (hd max|dO| max|V| + max|delta|) / sqrt(hd); phase 2's K image and dS one slice scale each (maxima
+// reduced through LDS at the phase-1 barrier).  Outputs are unscaled at their stores.
+template <int HD, int NWV, int NP, bool LAT_ = NWV == 4>
 __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NT = HD / 32, NM = HD / 16, CPR = HD / 8, NTH = 64 * NWV;
@@ -417,12 +543,13 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
   const int nkb = (I + 15) >> 4, nqb = (K + 15) >> 4, IP = nkb * 16, KP = nqb * 16;
   const int nslices = p.B * p.H;
   char* qimg = smem;
-  char* oimg = smem + 3 * PB;
-  float* lse2 = reinterpret_cast<float*>(smem + 6 * PB);
+  char* oimg = smem + NP * PB;
+  float* lse2 = reinterpret_cast<float*>(smem + 2 * NP * PB);
   float* dlt = lse2 + RM;
   int* qps = reinterpret_cast<int*>(dlt + RM);
   int* tab = qps + RM;                             // [16] first visible query block, [16] dS-store base per key block
-  char* dss = reinterpret_cast<char*>(tab + 32);
+  float* red = reinterpret_cast<float*>(tab + 32);   // NP = 2: per-wave maxima [3][8] (staging), [2][8] (phase 1)
+  char* dss = reinterpret_cast<char*>(red + 32);
   const float c1 = p.scale * L2E;
   if (threadIdx.x < 16) {
     tab[threadIdx.x] = p.qf[threadIdx.x];
@@ -436,13 +563,13 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     rbase[t] = poff<HD>(li, 4 * t + g);
-    orbase[t] = rbase[t] + 3 * PB;
+    orbase[t] = rbase[t] + NP * PB;
     asm volatile("" : "+v"(rbase[t]), "+v"(orbase[t]));
   }
 #pragma unroll
   for (int m = 0; m < NM; ++m) {
     tbase[m] = poff<HD>(4 * g + ((lane >> 2) & 3), 2 * m + ((lane & 3) >> 1)) + 8 * (lane & 1);
-    otbase[m] = tbase[m] + 3 * PB;
+    otbase[m] = tbase[m] + NP * PB;
     asm volatile("" : "+v"(tbase[m]), "+v"(otbase[m]));
   }
 #pragma unroll
@@ -494,8 +621,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
     if ((int)threadIdx.x < KP) {
       const bool v = (int)threadIdx.x < K;
       qps[threadIdx.x] = v ? q_off + threadIdx.x : -1;
-      lse2[threadIdx.x] = v ? lsev * L2E : INFINITY;
+      lse2[threadIdx.x] = v ? lsev * L2E - (NP == 2 ? 14.f : 0.f) : INFINITY;   // (NP = 2: P' = P 2^14)
     }
+    float sq = 1.f, so = 1.f, mo = 0.f, mdl = 0.f;                  // Q / dO scales, max|dO|, max|delta| (NP = 2)
 #pragma unroll
     for (int r = 0; r < SR; ++r) {
       // query rows past K hold row K - 1 (finite): their P and dS are 0 (lse +inf, qpos -1) and their dQ is
@@ -506,11 +634,43 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
       for (int e = 0; e < 8; ++e) pd = fmaf(yr[r][e], orr[r][e], pd);
 #pragma unroll
       for (int off = 1; off < CPR; off <<= 1) pd += __shfl_xor(pd, off, 64);
+      if (task < KP * CPR && c == 0) dlt[j] = pd;
+      if constexpr (NP == 2) mdl = fmaxf(mdl, fabsf(pd));
+    }
+    if constexpr (NP == 2) {
+      float mq = 0.f;
+#pragma unroll
+      for (int r = 0; r < SR; ++r)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          mq = fmaxf(mq, fabsf(qr[r][e]));
+          mo = fmaxf(mo, fabsf(yr[r][e]));
+        }
+      mq = wave_maxf(mq);
+      mo = wave_maxf(mo);
+      mdl = wave_maxf(mdl);
+      if (lane == 0) {
+        red[wave] = mq;
+        red[8 + wave] = mo;
+        red[16 + wave] = mdl;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int w = 0; w < NWV; ++w) {
+        mq = fmaxf(mq, red[w]);
+        mo = fmaxf(mo, red[8 + w]);
+        mdl = fmaxf(mdl, red[16 + w]);
+      }
+      sq = pow2scale(mq);
+      so = pow2scale(mo);
+    }
+#pragma unroll
+    for (int r = 0; r < SR; ++r) {
+      const int task = threadIdx.x + r * NTH, j = task / CPR, c = task % CPR;
       if (task < KP * CPR) {
-        if (c == 0) dlt[j] = pd;
         const int o = poff<HD>(j, c);
-        store_planes(qimg, PB, o, qr[r]);
-        store_planes(oimg, PB, o, yr[r]);
+        store_planesN<NP>(qimg, PB, o, qr[r], sq);
+        store_planesN<NP>(oimg, PB, o, yr[r], so);
       }
     }
     __syncthreads();
@@ -518,25 +678,55 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
 
     // ---- phase 1: key-block owners
     constexpr int KEEP = keep_slots(HD, NWV);
-    u32x4 keep[KEEP][NT][3];                       // the owned key blocks' K planes, for the phase-2 K image
+    // the owned key blocks' K planes (NP = 3) or K rows (NP = 2: split at the slice scale after phase 1), for the
+    // phase-2 K image
+    u32x4 keep[NP == 3 ? KEEP : 1][NT][3];
+    float keepf[NP == 2 ? KEEP : 1][NT][8];
+    float mkw = 0.f, mdsw = 0.f;                   // NP = 2: this wave's max |K| and max |dS| (phase 2's scales)
 #pragma unroll 1
     for (int slot = 0, kb = kb0; kb >= 0; ++slot) {
       const int krow = 16 * kb + li;               // this lane's key
       // keys past I hold row I - 1 (finite): their S / dP columns are masked (P = dS = 0, a select) and
       // their dK / dV rows are not stored, so they need no zeroing
-      u32x4 kp[NT][3], vp[NT][3];
+      u32x4 kp[NT][NP], vp[NT][NP];
+      float sk = 1.f, sv = 1.f, cS = c1, cdp = 1.f, sds = 1.f, dsc = p.scale;
+      if constexpr (NP == 2) {
+        float mk = 0.f, mv = 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            mk = fmaxf(mk, fabsf(kr[t][e]));
+            mv = fmaxf(mv, fabsf(vr[t][e]));
+          }
+        mk = wave_maxf(mk);
+        mv = wave_maxf(mv);
+        mkw = fmaxf(mkw, mk);
+        sk = pow2scale(mk);
+        sv = pow2scale(mv);
+        cS = c1 / (sq * sk);
+        cdp = 1.f / (so * sv);
+        sds = pow2scale(((float)HD * mo * mv + mdl) * p.scale);     // bound on this key block's |dS|
+        dsc = p.scale * (1.f / 16384.f);                            // dS = P' (dP - delta) / sqrt(hd) / 2^14
+      }
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        split8p(kr[t], kp[t]);
-        split8p(vr[t], vp[t]);
+        splitN<NP>(kr[t], sk, kp[t]);
+        splitN<NP>(vr[t], sv, vp[t]);
       }
 #pragma unroll
       for (int k2 = 0; k2 < KEEP; ++k2)              // uniform branch, static register index
         if (slot == k2) {
 #pragma unroll
-          for (int t = 0; t < NT; ++t)
+          for (int t = 0; t < NT; ++t) {
+            if constexpr (NP == 3) {
 #pragma unroll
-            for (int pl = 0; pl < 3; ++pl) keep[k2][t][pl] = kp[t][pl];
+              for (int pl = 0; pl < 3; ++pl) keep[k2][t][pl] = kp[t][pl];
+            } else {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) keepf[k2][t][e] = kr[t][e];
+            }
+          }
         }
       const int kbn = sched_item(srow1, slot + 1);
       if (kbn >= 0) load_kv(s, kbn);                // next key block's K / V in flight meanwhile
@@ -549,22 +739,22 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
       // (sched_barrier keeps the compiler from sinking the reads back to their MFMAs)
       auto sdp = [&](int a, bool two, f32x4 (&sc)[2], f32x4 (&dc)[2]) {
         constexpr int NI = 2 * NT;
-        u32x4 fq[2][3], fo[2][3];
-        frag_at(fq[0], smem + 16 * RBY * a + rbase[0], PB);
-        frag_at(fo[0], smem + 16 * RBY * a + orbase[0], PB);
+        u32x4 fq[2][NP], fo[2][NP];
+        frag_atN<NP>(fq[0], smem + 16 * RBY * a + rbase[0], PB);
+        frag_atN<NP>(fo[0], smem + 16 * RBY * a + orbase[0], PB);
 #pragma unroll
         for (int h = 0; h < 2; ++h) sc[h] = dc[h] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
           if (i + 1 < NI) {
             const int qb1 = two ? a + (i + 1) / NT : a;            // past the last block: a harmless re-read
-            frag_at(fq[(i + 1) & 1], smem + 16 * RBY * qb1 + rbase[(i + 1) % NT], PB);
-            frag_at(fo[(i + 1) & 1], smem + 16 * RBY * qb1 + orbase[(i + 1) % NT], PB);
+            frag_atN<NP>(fq[(i + 1) & 1], smem + 16 * RBY * qb1 + rbase[(i + 1) % NT], PB);
+            frag_atN<NP>(fo[(i + 1) & 1], smem + 16 * RBY * qb1 + orbase[(i + 1) % NT], PB);
           }
           const int half = i / NT, t = i % NT;
           if (half == 0 || two) {
-            sc[half] = mma6(fq[i & 1], kp[t], sc[half]);            // S: row = query, col = key
-            dc[half] = mma6(fo[i & 1], vp[t], dc[half]);            // dP
+            sc[half] = mmaN<NP>(fq[i & 1], kp[t], sc[half]);        // S: row = query, col = key
+            dc[half] = mmaN<NP>(fo[i & 1], vp[t], dc[half]);        // dP
           }
           if (LAT) __builtin_amdgcn_sched_barrier(0);
         }
@@ -592,47 +782,50 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
             const i32x4 Qp = *reinterpret_cast<const i32x4*>(qps + q0);
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-              const float e = __builtin_amdgcn_exp2f(fmaf(sc[half][i], c1, -L[i]));
+              const float e = __builtin_amdgcn_exp2f(fmaf(sc[half][i], cS, -L[i]));
               const float pv = krow <= Qp[i] ? e : 0.f;
-              const float ds = pv * (dc[half][i] - D[i]) * p.scale;
+              const float ds = pv * (NP == 2 ? fmaf(dc[half][i], cdp, -D[i]) : dc[half][i] - D[i]) * dsc;
               P[4 * half + i] = pv;
               dS[4 * half + i] = ds;
               *reinterpret_cast<float*>(blk + dsw[i]) = ds;
+              if constexpr (NP == 2) mdsw = fmaxf(mdsw, fabsf(ds));
             }
           } else {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-              const float pv = __builtin_amdgcn_exp2f(fmaf(sc[half][i], c1, -L[i]));
-              const float ds = pv * (dc[half][i] - D[i]) * p.scale;
+              const float pv = __builtin_amdgcn_exp2f(fmaf(sc[half][i], cS, -L[i]));
+              const float ds = pv * (NP == 2 ? fmaf(dc[half][i], cdp, -D[i]) : dc[half][i] - D[i]) * dsc;
               P[4 * half + i] = pv;
               dS[4 * half + i] = ds;
               *reinterpret_cast<float*>(blk + dsw[i]) = ds;
+              if constexpr (NP == 2) mdsw = fmaxf(mdsw, fabsf(ds));
             }
           }
         }
-        u32x4 pp[3], sp[3];
-        split8p(P, pp);
-        split8p(dS, sp);
+        u32x4 pp[NP], sp[NP];
+        splitN<NP>(P, 1.f, pp);
+        splitN<NP>(dS, sds, sp);
         const int ra = 16 * RBY * a, rb = two ? ra + 16 * RBY : ra;
-        u32x4 fa[2][3], fb[2][3];
-        tr_at(fa[0], smem + ra + otbase[0], smem + rb + otbase[0], PB);
-        tr_at(fb[0], smem + ra + tbase[0], smem + rb + tbase[0], PB);
+        u32x4 fa[2][NP], fb[2][NP];
+        tr_atN<NP>(fa[0], smem + ra + otbase[0], smem + rb + otbase[0], PB);
+        tr_atN<NP>(fb[0], smem + ra + tbase[0], smem + rb + tbase[0], PB);
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
           if (m + 1 < NM) {                                           // next dim tile's fragments in flight
-            tr_at(fa[(m + 1) & 1], smem + ra + otbase[m + 1], smem + rb + otbase[m + 1], PB);
-            tr_at(fb[(m + 1) & 1], smem + ra + tbase[m + 1], smem + rb + tbase[m + 1], PB);
+            tr_atN<NP>(fa[(m + 1) & 1], smem + ra + otbase[m + 1], smem + rb + otbase[m + 1], PB);
+            tr_atN<NP>(fb[(m + 1) & 1], smem + ra + tbase[m + 1], smem + rb + tbase[m + 1], PB);
           }
-          dv[m] = mma6(fa[m & 1], pp, dv[m]);                         // dV^T += dO^T P
-          dk[m] = mma6(fb[m & 1], sp, dk[m]);                         // dK^T += Q^T dS
+          dv[m] = mmaN<NP>(fa[m & 1], pp, dv[m]);                     // dV^T += dO^T P
+          dk[m] = mmaN<NP>(fb[m & 1], sp, dk[m]);                     // dK^T += Q^T dS
           if (LAT) __builtin_amdgcn_sched_barrier(0);
         }
       }
       if (krow < I) {
+        const float uk = NP == 2 ? 1.f / (sq * sds) : 1.f, uv = NP == 2 ? 1.f / (so * 16384.f) : 1.f;
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
-          *reinterpret_cast<f32x4*>(dKg + (int64_t)krow * p.ld + 16 * m + 4 * g) = dk[m];
-          *reinterpret_cast<f32x4*>(dVg + (int64_t)krow * p.ld + 16 * m + 4 * g) = dv[m];
+          *reinterpret_cast<f32x4*>(dKg + (int64_t)krow * p.ld + 16 * m + 4 * g) = dk[m] * uk;
+          *reinterpret_cast<f32x4*>(dVg + (int64_t)krow * p.ld + 16 * m + 4 * g) = dv[m] * uv;
         }
       }
       kb = kbn;
@@ -640,23 +833,53 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
     // K image for phase 2, in the Q planes' space: each key-block owner stores the K planes it kept (rows past
     // I hold row I - 1, times dS = 0) — no re-read or re-split of K
     SLICE_STAMP(1, it, 2);
+    if constexpr (NP == 2) {
+      mdsw = wave_maxf(mdsw);
+      if (lane == 0) {                             // (the staging maxima were read before phase 1)
+        red[wave] = mkw;
+        red[8 + wave] = mdsw;
+      }
+    }
     __syncthreads();                               // dS store complete, Q planes no longer read
     SLICE_STAMP(1, it, 3);
+    float sks = 1.f, sdss = 1.f;                   // NP = 2: phase 2's K image and dS scales (slice-wide)
+    if constexpr (NP == 2) {
+      float mk = 0.f, md = 0.f;
+#pragma unroll
+      for (int w = 0; w < NWV; ++w) {
+        mk = fmaxf(mk, red[w]);
+        md = fmaxf(md, red[8 + w]);
+      }
+      sks = pow2scale(mk);
+      sdss = pow2scale(md);
+    }
 #pragma unroll
     for (int k2 = 0; k2 < KEEP; ++k2) {
       const int kb = sched_item(srow1, k2);
       if (kb >= 0) {
 #pragma unroll
-        for (int t = 0; t < NT; ++t)
+        for (int t = 0; t < NT; ++t) {
+          u32x4 kp[NP];
+          if constexpr (NP == 3) {
 #pragma unroll
-          for (int pl = 0; pl < 3; ++pl)
-            *reinterpret_cast<u32x4*>(qimg + pl * PB + poff<HD>(16 * kb + li, 4 * t + g)) = keep[k2][t][pl];
+            for (int pl = 0; pl < 3; ++pl) kp[pl] = keep[k2][t][pl];
+          } else {
+            splitN<2>(keepf[k2][t], sks, kp);
+          }
+#pragma unroll
+          for (int pl = 0; pl < NP; ++pl)
+            *reinterpret_cast<u32x4*>(qimg + pl * PB + poff<HD>(16 * kb + li, 4 * t + g)) = kp[pl];
+        }
       }
     }
     __syncthreads();
     SLICE_STAMP(1, it, 4);
+    // the next slice's Q / dO / O rows: issued before phase 2 at head_dim 64, after it at 32.  Issuing them (~108
+    // KiB per CU at head_dim 64) stalls the wave for about 7k cycles wherever they go — at the start of phase 1
+    // measured the same, streamed a piece per phase-1 / phase-2 step slower (the waits for the next key block's
+    // K / V then drain them too)
     constexpr bool EARLY = HD == 64;
-    if (EARLY && s + (int)gridDim.x < nslices) prefetch(s + gridDim.x);   // next slice, during phase 2
+    if (EARLY && s + (int)gridDim.x < nslices) prefetch(s + gridDim.x);
 
     // ---- phase 2: query-block owners, dQ^T = K^T dS^T
 #pragma unroll 1
@@ -680,16 +903,16 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
         f32x4 x1 = {0.f, 0.f, 0.f, 0.f};
         if (two) x1 = *reinterpret_cast<const f32x4*>(dss + 1024 * (tab[17 + k2] + qb - tab[k2 + 1]) + dsr);
         const int ra = 16 * RBY * k2, rb = two ? ra + 16 * RBY : ra;
-        u32x4 fa[2][3];
-        tr_at(fa[0], smem + ra + tbase[0], smem + rb + tbase[0], PB);   // in flight during the split
+        u32x4 fa[2][NP];
+        tr_atN<NP>(fa[0], smem + ra + tbase[0], smem + rb + tbase[0], PB);   // in flight during the split
 #pragma unroll
         for (int i = 0; i < 4; ++i) { v[i] = x0[i]; v[4 + i] = x1[i]; }
-        u32x4 bp[3];
-        split8p(v, bp);
+        u32x4 bp[NP];
+        splitN<NP>(v, sdss, bp);
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
-          if (m + 1 < NM) tr_at(fa[(m + 1) & 1], smem + ra + tbase[m + 1], smem + rb + tbase[m + 1], PB);
-          acc[m] = mma6(fa[m & 1], bp, acc[m]);
+          if (m + 1 < NM) tr_atN<NP>(fa[(m + 1) & 1], smem + ra + tbase[m + 1], smem + rb + tbase[m + 1], PB);
+          acc[m] = mmaN<NP>(fa[m & 1], bp, acc[m]);
           if (LAT) __builtin_amdgcn_sched_barrier(0);
         }
       };
@@ -698,8 +921,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
         step(k2, dq);
         if (k2 + 2 <= kbl) step(k2 + 2, dq2);
       }
+      const float uq = NP == 2 ? 1.f / (sks * sdss) : 1.f;
 #pragma unroll
-      for (int m = 0; m < NM; ++m) dq[m] += dq2[m];
+      for (int m = 0; m < NM; ++m) dq[m] = (dq[m] + dq2[m]) * uq;
       const int j = 16 * qb + li;
       if (j < K) {
         float* drow = dQg + (int64_t)(q_off + j) * p.ld + 4 * g;
@@ -715,7 +939,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
 }
 
 static int rmax(int hd) { return hd == 64 ? RMAX<64>() : RMAX<32>(); }
-size_t fwd_lds(int I, int hd) { return (size_t)6 * rmax(hd) * hd * 2 + 4 * (size_t)rmax(hd); }
+size_t fwd_lds(int I, int hd, int np = 3) { return (size_t)4 * np * rmax(hd) * hd + 4 * (size_t)rmax(hd) + 64; }
 
 // causal 16 x 16 block pairs of the tail-query backward
 int bwd_pairs(int I, int K) {
@@ -725,8 +949,8 @@ int bwd_pairs(int I, int K) {
   return n;
 }
 
-size_t bwd_lds(int I, int K, int hd) {
-  return (size_t)6 * rmax(hd) * hd * 2 + 12 * (size_t)rmax(hd) + 128 + 1024 * (size_t)bwd_pairs(I, K);
+size_t bwd_lds(int I, int K, int hd, int np = 3) {
+  return (size_t)4 * np * rmax(hd) * hd + 12 * (size_t)rmax(hd) + 128 + 128 + 1024 * (size_t)bwd_pairs(I, K);
 }
 
 // persistent grid: the workgroups that are co-resident (occupancy query, cached per kernel and LDS size),
@@ -796,15 +1020,17 @@ static bool make_schedule(SliceArgs& p, int hd, int nwv) {
     p.bbase[kb] = (int16_t)base;
     base += nqb - f;
   }
-  if (!lpt(nkb, load, nwv, p.sched[1], keep_slots(hd, nwv))) return false;   // the backward keeps K planes per slot
+  if (!lpt(nkb, load, nwv, p.sched[1], keep_slots(hd, nwv))) return false;   // the backward keeps K per slot
   for (int idx = 0; idx < nqb; ++idx) load[idx] = (((q_off + std::min(16 * (nqb - 1 - idx) + 15, K - 1)) >> 4) + 2) >> 1;
   return lpt(nqb, load, nwv, p.sched[2]);
 }
 
-static int g_enabled = [] {
-  const char* e = std::getenv("ONETRANS_ATTN_SLICE");
-  return e ? std::atoi(e) : 1;
-}();
+// Arithmetic (measured at B 4096 H 4 I 140, round 5): the scaled fp16 pair (NP 2) everywhere except the head_dim-32
+// forward, where the three-plane bf16 split (NP 3) stays faster (286-302 vs 318-330 us: the per-slice K / V scale
+// reduction costs more than the halved MFMAs save in that short, non-persistent kernel).  hd 64: forward 605-617 ->
+// 550-561 us, backward 1,616-1,629 -> 1,515-1,523; hd 32 backward 936-950 -> 871-901.
+constexpr int fwd_planes(int hd) { return hd == 64 ? 2 : 3; }
+constexpr int BWD_PLANES = 2;
 
 // waves per workgroup (measured, B 4096 H 4 I 140): forward 8 (hd 32: 4 waves / SIMD at 128 VGPRs); backward hd 32
 // 8 (4 waves: 1,136-1,160 vs 928-965 us; again 1,066-1,093 vs 919-948 with the kept K planes and fenced
@@ -823,34 +1049,36 @@ static void raise_lds_limit(F* k) {
 }  // namespace slice
 
 bool attn_slice_fwd_supported(int I, int K, int head_dim) {
-  return slice::g_enabled && (head_dim == 32 || head_dim == 64) && I <= slice::rmax(head_dim) && K > 0 && K <= I &&
-         slice::fwd_lds(I, head_dim) <= (size_t)slice::LDS_MAX;
+  return (head_dim == 32 || head_dim == 64) && I <= slice::rmax(head_dim) && K > 0 && K <= I &&
+         slice::fwd_lds(I, head_dim, head_dim == 64 ? slice::fwd_planes(64) : slice::fwd_planes(32)) <=
+             (size_t)slice::LDS_MAX;
 }
 
 bool attn_slice_bwd_supported(int I, int K, int head_dim, bool selected) {
-  return slice::g_enabled && !selected && (head_dim == 32 || head_dim == 64) && I <= slice::rmax(head_dim) &&
-         K > 0 && K <= I && slice::bwd_lds(I, K, head_dim) <= (size_t)slice::LDS_MAX;
+  return !selected && (head_dim == 32 || head_dim == 64) && I <= slice::rmax(head_dim) && K > 0 && K <= I &&
+         slice::bwd_lds(I, K, head_dim, slice::BWD_PLANES) <= (size_t)slice::LDS_MAX;
 }
 
 int attn_slice_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos, int head_dim,
                    float* out, float* lse, hipStream_t stream) {
   using namespace slice;
+  using KF = void (*)(SliceArgs);
+  constexpr int P32 = fwd_planes(32), P64 = fwd_planes(64);
+  static const KF table[2][2] = {
+      {attn_fwd_slice_kernel<32, FWD_WAVES, false, false, P32>, attn_fwd_slice_kernel<32, FWD_WAVES, true, false, P32>},
+      {attn_fwd_slice_kernel<64, FWD_WAVES, false, true, P64>, attn_fwd_slice_kernel<64, FWD_WAVES, true, true, P64>}};
   static std::once_flag once;
   std::call_once(once, [] {
-    for (auto k : {attn_fwd_slice_kernel<32, FWD_WAVES, false, false>, attn_fwd_slice_kernel<32, FWD_WAVES, true, false>,
-                   attn_fwd_slice_kernel<64, FWD_WAVES, false, true>, attn_fwd_slice_kernel<64, FWD_WAVES, true, true>})
-      raise_lds_limit(k);
+    for (int a = 0; a < 2; ++a)
+      for (int b = 0; b < 2; ++b) raise_lds_limit(table[a][b]);
     (void)hipGetLastError();
   });
   SliceArgs p{qkv, ld, H * head_dim, nullptr, nullptr, nullptr, out, lse, nullptr, B, H, I, K,
               1.f / sqrtf((float)head_dim), qpos};
-  const size_t lds = fwd_lds(I, head_dim);
+  const size_t lds = fwd_lds(I, head_dim, head_dim == 64 ? P64 : P32);
   const int nw = FWD_WAVES;
   OT_REQUIRE(make_schedule(p, head_dim, nw), "ot_attn_fwd(slice): schedule");
-  void (*const table[2][2])(SliceArgs) = {
-      {attn_fwd_slice_kernel<32, FWD_WAVES, false, false>, attn_fwd_slice_kernel<32, FWD_WAVES, true, false>},
-      {attn_fwd_slice_kernel<64, FWD_WAVES, false, true>, attn_fwd_slice_kernel<64, FWD_WAVES, true, true>}};
-  void (*k)(SliceArgs) = table[head_dim == 64][qpos != nullptr];
+  const KF k = table[head_dim == 64][qpos != nullptr];
   const unsigned slices = (unsigned)((int64_t)B * H);
   const dim3 grid(head_dim == 64 ? persistent_grid((const void*)k, 64 * nw, lds, slices) : slices), block(64 * nw);
   hipLaunchKernelGGL(k, grid, block, lds, stream, p);
@@ -862,9 +1090,8 @@ int attn_slice_bwd(const float* qkv, int64_t ld, const float* out, const float* 
                    int I, int K, int head_dim, float* dqkv, hipStream_t stream) {
   using namespace slice;
   using KF = void (*)(SliceArgs);
-  // fenced one-item-ahead fragment reads: head_dim 64 (one wave per SIMD); at head_dim 32 (two waves per
-  // SIMD) they measured within noise (914-952 vs 933-938 us) and are off
-  static const KF k32 = attn_bwd_slice_kernel<32, BWD_WAVES32>, k64 = attn_bwd_slice_kernel<64, BWD_WAVES64>;
+  static const KF k32 = attn_bwd_slice_kernel<32, BWD_WAVES32, BWD_PLANES>,
+                  k64 = attn_bwd_slice_kernel<64, BWD_WAVES64, BWD_PLANES>;
   static std::once_flag once;
   std::call_once(once, [] {
     for (KF k : {k32, k64}) raise_lds_limit(k);
@@ -872,7 +1099,7 @@ int attn_slice_bwd(const float* qkv, int64_t ld, const float* out, const float* 
   });
   SliceArgs p{qkv, ld, H * head_dim, out, dout, lse, nullptr, nullptr, dqkv, B, H, I, K,
               1.f / sqrtf((float)head_dim), nullptr};
-  const size_t lds = bwd_lds(I, K, head_dim);
+  const size_t lds = bwd_lds(I, K, head_dim, BWD_PLANES);
   const int nw = head_dim == 32 ? BWD_WAVES32 : BWD_WAVES64;
   OT_REQUIRE(make_schedule(p, head_dim, nw), "ot_attn_bwd(slice): schedule");
   const KF k = head_dim == 32 ? k32 : k64;

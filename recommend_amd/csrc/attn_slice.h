@@ -1,4 +1,5 @@
-// Short-sequence attention: one workgroup per (sample, head) slice on split-bf16 MFMA
+// Short-sequence attention: one workgroup per (sample, head) slice on split MFMA (three bf16 planes or a scaled fp16
+// pair per f32 operand)
 // (attention_slice.hip).  Dispatched from ot_attn_fwd / ot_attn_bwd (attention.hip) in the
 // f32-accurate mode (OT_MATMUL_SPLIT_BF16) when the slice fits LDS.
 #pragma once

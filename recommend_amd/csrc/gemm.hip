@@ -137,7 +137,17 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 // every tile of a chunk streams the same rows, and they are then read through one L2.  (The contiguous-range
 // remap split chunks across two XCDs whenever a range was not a whole number of chunks: C5's W1 weight gradient
 // fetched 2.3x its algorithmic bytes.)  The grid is padded to whole rounds of 8 chunks; padding blocks return.
+// Fewer than 8 chunks (small batches): whole chunks per XCD would leave XCDs idle, so the tiles are dealt in
+// order (block b = chunk b / per_chunk), spread over every XCD; the grid is then nchunks x per_chunk.
+__host__ __device__ inline unsigned wgrad_grid(int nchunks, int per_chunk) {
+  return (unsigned)(nchunks < 8 ? nchunks : (nchunks + 7) / 8 * 8) * per_chunk;
+}
 __device__ __forceinline__ bool wgrad_tile(int b, int per_chunk, int nchunks, int& c, int& rem) {
+  if (nchunks < 8) {
+    c = b / per_chunk;
+    rem = b % per_chunk;
+    return true;
+  }
   const int x = b & 7, j = b >> 3;
   c = x + 8 * (j / per_chunk);
   rem = j % per_chunk;
@@ -2109,7 +2119,7 @@ extern "C" int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a
         (void)hipGetLastError();
       });
     }
-    hipLaunchKernelGGL(kern, dim3((unsigned)(ceil_div(nchunks, 8) * 8) * p.ntk * p.ntn), dim3(256),
+    hipLaunchKernelGGL(kern, dim3(wgrad_grid(nchunks, p.ntk * p.ntn)), dim3(256),
                        copy ? copy_shmem : split ? split_shmem : shmem, s, p);
     OT_LAUNCH_CHECK("ot_mixed_gemm_wgrad");
   }

@@ -76,7 +76,8 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__
 // dw2 (dh values) and db2 (1 value) per block -> part[t][x][dh + 1]
 __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__ pre1, const float* __restrict__ w2,
                                                        const float* __restrict__ probs,
-                                                       const float* __restrict__ dprobs, int B, int dh,
+                                                       const float* __restrict__ dprobs,
+                                                       const float* __restrict__ dlogits, int B, int dh,
                                                        float* dpre1, float* part) {
   extern __shared__ __attribute__((aligned(16))) float red[];   // [4][dh + 1]
   const int t = blockIdx.y, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -86,7 +87,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
   for (int b = blockIdx.x * 4 + wave; b < B; b += NB * 4) {
     const int64_t row = (int64_t)t * B + b;
     const float pr = probs[row];
-    const float dz = dprobs[row] * pr * (1.f - pr);
+    const float dz = (dprobs ? dprobs[row] * pr * (1.f - pr) : 0.f) + (dlogits ? dlogits[row] : 0.f);
     pb += dz;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -122,6 +123,11 @@ __global__ void head_bwd_reduce_kernel(const float* __restrict__ part, int NB, i
   float* dst = j < dh ? dw2 + t * sw2 + j : db2 + t * sb2;
   *dst = accumulate ? *dst + s : s;
 }
+
+// Keras 2.12 on a sigmoid head (model.py:327-329): activations.sigmoid caches its input as the output's
+// _keras_logits and backend.binary_crossentropy then returns tf.nn.sigmoid_cross_entropy_with_logits —
+// max(z, 0) - z y + log(1 + exp(-|z|)), no clipping; d/dz = sigmoid(z) - y
+__device__ __forceinline__ float bce_logits(float y, float z) { return fmaxf(z, 0.f) - z * y + log1pf(expf(-fabsf(z))); }
 
 __device__ __forceinline__ float keras_bce(float y, float p) {
   const float eps = 1e-7f;
@@ -168,6 +174,37 @@ __global__ void bce_bwd_kernel(const float* __restrict__ probs, const float* __r
   if ((mse_mask >> (int)(i / B)) & 1u) g = 2.f * (p - y) * invB;
   else if (p >= eps && p <= 1.f - eps) g = (-y / (p + eps) + (1.f - y) / (1.f - p + eps)) * invB;
   dprobs[i] = g * gscale[0];
+}
+
+// the logits form: BCE tasks from z, MSE tasks (bit t of mse_mask) from p
+__global__ __launch_bounds__(256) void loss_z_fwd_kernel(const float* __restrict__ logits, const float* __restrict__ probs,
+                                                         const float* __restrict__ labels, int64_t n, int B, float invB,
+                                                         unsigned mse_mask, float* part) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float y = labels[i];
+    if ((mse_mask >> (int)(i / B)) & 1u) {
+      const float e = probs[i] - y;
+      s += e * e * invB;
+    } else {
+      s += bce_logits(y, logits[i]) * invB;
+    }
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ void loss_z_bwd_kernel(const float* __restrict__ probs, const float* __restrict__ labels,
+                                  const float* __restrict__ gscale, int64_t n, int B, float invB, unsigned mse_mask,
+                                  float* dlogits) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float p = probs[i], y = labels[i];
+  const float g = ((mse_mask >> (int)(i / B)) & 1u) ? 2.f * (p - y) * p * (1.f - p) : p - y;
+  dlogits[i] = g * invB * gscale[0];
 }
 
 inline int bce_blocks(int64_t n) {
@@ -240,13 +277,23 @@ extern "C" size_t ot_head_bwd_workspace_size(int T, int B, int dh) {
 extern "C" int ot_head_bwd(const float* pre1, const float* w2, const float* probs, const float* dprobs, int T, int B,
                            int dh, float* dpre1, float* dw2, float* db2, int64_t task_stride_w2,
                            int64_t task_stride_b2, int accumulate, void* workspace, size_t ws_bytes, void* stream) {
-  OT_REQUIRE(pre1 && w2 && probs && dprobs && dpre1 && dw2 && db2, "ot_head_bwd: null operand");
+  OT_REQUIRE(dprobs, "ot_head_bwd: null operand");
+  return ot_head_bwd_ex(pre1, w2, probs, dprobs, nullptr, T, B, dh, dpre1, dw2, db2, task_stride_w2, task_stride_b2,
+                        accumulate, workspace, ws_bytes, stream);
+}
+
+extern "C" int ot_head_bwd_ex(const float* pre1, const float* w2, const float* probs, const float* dprobs,
+                              const float* dlogits, int T, int B, int dh, float* dpre1, float* dw2, float* db2,
+                              int64_t task_stride_w2, int64_t task_stride_b2, int accumulate, void* workspace,
+                              size_t ws_bytes, void* stream) {
+  OT_REQUIRE(pre1 && w2 && probs && dpre1 && dw2 && db2, "ot_head_bwd: null operand");
+  OT_REQUIRE(dprobs || dlogits, "ot_head_bwd_ex: neither dprobs nor dlogits");
   OT_REQUIRE(dh <= 256, "ot_head_bwd: dh=%d > 256 unsupported", dh);
   OT_REQUIRE(workspace && ws_bytes >= ot_head_bwd_workspace_size(T, B, dh), "ot_head_bwd: workspace too small");
   if ((int64_t)T * B == 0) return OT_OK;
   const int nb = head_nb(B);
   hipLaunchKernelGGL(head_bwd_kernel, dim3(nb, T), dim3(256), 4 * (dh + 1) * sizeof(float), (hipStream_t)stream,
-                     pre1, w2, probs, dprobs, B, dh, dpre1, (float*)workspace);
+                     pre1, w2, probs, dprobs, dlogits, B, dh, dpre1, (float*)workspace);
   OT_LAUNCH_CHECK("ot_head_bwd");
   hipLaunchKernelGGL(head_bwd_reduce_kernel, dim3(ceil_div(dh + 1, 256), T), dim3(256), 0, (hipStream_t)stream,
                      (const float*)workspace, nb, dh, dw2, db2, task_stride_w2, task_stride_b2, accumulate);
@@ -280,6 +327,33 @@ extern "C" int ot_task_loss_bwd(const float* probs, const float* labels, const f
   hipLaunchKernelGGL(bce_bwd_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream, probs, labels, gscale,
                      n, B, 1.f / B, mse_mask, dprobs);
   OT_LAUNCH_CHECK("ot_task_loss_bwd");
+  return OT_OK;
+}
+
+extern "C" int ot_task_loss_logits_fwd(const float* logits, const float* probs, const float* labels, int T, int B,
+                                       unsigned mse_mask, float* loss, void* workspace, size_t ws_bytes, void* stream) {
+  OT_REQUIRE(logits && probs && labels && loss && workspace, "ot_task_loss_logits_fwd: null operand");
+  OT_REQUIRE(ws_bytes >= ot_bce_workspace_size(T, B), "ot_task_loss_logits_fwd: workspace too small");
+  OT_REQUIRE(B > 0, "ot_task_loss_logits_fwd: empty batch");
+  OT_REQUIRE(T > 0 && T <= 32, "ot_task_loss_logits_fwd: 1..32 tasks");
+  const int64_t n = (int64_t)T * B;
+  const int nb = bce_blocks(n);
+  hipLaunchKernelGGL(loss_z_fwd_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, logits, probs, labels, n, B,
+                     1.f / B, mse_mask, (float*)workspace);
+  OT_LAUNCH_CHECK("ot_task_loss_logits_fwd");
+  hipLaunchKernelGGL(bce_reduce_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (const float*)workspace, nb, loss);
+  OT_LAUNCH_CHECK("ot_task_loss_logits_fwd(reduce)");
+  return OT_OK;
+}
+
+extern "C" int ot_task_loss_logits_bwd(const float* probs, const float* labels, const float* gscale, int T, int B,
+                                       unsigned mse_mask, float* dlogits, void* stream) {
+  OT_REQUIRE(probs && labels && gscale && dlogits && B > 0, "ot_task_loss_logits_bwd: bad args");
+  OT_REQUIRE(T > 0 && T <= 32, "ot_task_loss_logits_bwd: 1..32 tasks");
+  const int64_t n = (int64_t)T * B;
+  hipLaunchKernelGGL(loss_z_bwd_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream, probs, labels,
+                     gscale, n, B, 1.f / B, mse_mask, dlogits);
+  OT_LAUNCH_CHECK("ot_task_loss_logits_bwd");
   return OT_OK;
 }
 

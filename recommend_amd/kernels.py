@@ -110,7 +110,8 @@ _scope = threading.local()
 
 def set_matmul_mode(mode: str) -> str:
     """Process-default GEMM / attention arithmetic for calls outside a ``precision`` scope: 'split' (exact
-    3-way bf16 split on bf16 MFMA, f32-accurate), 'f32' (native f32 MFMA) or 'bf16'.  Returns the previous."""
+    3-way bf16 split on bf16 MFMA, f32-accurate), 'f32' (native f32 MFMA) or 'bf16'.  Returns the previous.
+    A model reads the default once, at construction (OneTransModel.matmul): models that exist keep their mode."""
     global _default_mode
     if mode not in _lib.MATMUL_MODES:
         raise ValueError(f'matmul mode {mode!r}: expected one of {sorted(_lib.MATMUL_MODES)}')
@@ -143,13 +144,27 @@ def _prec() -> int:
     return _lib.MATMUL_MODES[matmul_mode()]
 
 
+def precision_owner(obj):
+    """The model whose arithmetic a method of ``obj`` runs in: ``obj`` itself when it carries a matmul mode
+    (``OneTransModel``), else the object's ``precision_model`` (serving engines, trainers: a property naming
+    the model they drive)."""
+    if isinstance(getattr(obj, 'matmul', None), str):
+        return obj
+    owner = getattr(type(obj), 'precision_model', None)
+    if owner is None:
+        raise TypeError(f'{type(obj).__name__}: in_model_precision needs a .matmul mode or a precision_model property')
+    owner = owner.__get__(obj)
+    if not isinstance(getattr(owner, 'matmul', None), str):
+        raise TypeError(f'{type(obj).__name__}.precision_model has no matmul mode')
+    return owner
+
+
 def in_model_precision(fn):
-    """Run a method of a model (``.matmul``) or of an object holding one (``.m`` / ``.model``) inside that
+    """Run a method of a model (``.matmul``) or of an object driving one (``precision_model``) inside that
     model's ``precision`` scope: every GEMM / attention call it makes carries the model's arithmetic."""
     @functools.wraps(fn)
     def wrapped(self, *args, **kw):
-        owner = self if hasattr(self, 'matmul') else getattr(self, 'm', None) or self.model
-        with precision(owner.matmul):
+        with precision(precision_owner(self).matmul):
             return fn(self, *args, **kw)
     return wrapped
 
@@ -430,11 +445,13 @@ def head_fwd(pre1, w2, b2, T, B, dh, logits, probs) -> None:
         _probe.end('head_loss', 0.0, ev)
 
 
-def head_bwd(pre1, w2, probs, dprobs, T, B, dh, dpre1, dw2, db2, sw2, sb2, accumulate=False, device=None) -> None:
+def head_bwd(pre1, w2, probs, dprobs, T, B, dh, dpre1, dw2, db2, sw2, sb2, accumulate=False, device=None,
+             dlogits=None) -> None:
+    """ot_head_bwd_ex: the loss gradient w.r.t. the probabilities (``dprobs``) and / or the logits."""
     ws = workspace(size('ot_head_bwd_workspace_size', T, B, dh), device)
     ev = _probe.begin() if _probe is not None else None
-    call('ot_head_bwd', ptr(pre1), ptr(w2), ptr(probs), ptr(dprobs), T, B, dh, ptr(dpre1), ptr(dw2), ptr(db2), sw2,
-         sb2, int(accumulate), ptr(ws), ws.numel(), stream())
+    call('ot_head_bwd_ex', ptr(pre1), ptr(w2), ptr(probs), ptr(dprobs), ptr(dlogits), T, B, dh, ptr(dpre1), ptr(dw2),
+         ptr(db2), sw2, sb2, int(accumulate), ptr(ws), ws.numel(), stream())
     if ev is not None:
         _probe.end('head_loss', 0.0, ev)
 
@@ -451,6 +468,24 @@ def bce_fwd(probs, labels, T, B, loss, device=None, mse_mask: int = 0) -> None:
 def bce_bwd(probs, labels, gscale, T, B, dprobs, mse_mask: int = 0) -> None:
     ev = _probe.begin() if _probe is not None else None
     call('ot_task_loss_bwd', ptr(probs), ptr(labels), ptr(gscale), T, B, mse_mask, ptr(dprobs), stream())
+    if ev is not None:
+        _probe.end('head_loss', 0.0, ev)
+
+
+def task_loss_logits_fwd(logits, probs, labels, T, B, loss, device=None, mse_mask: int = 0) -> None:
+    """Σ_task loss (train.py:78-93) as Keras 2.12 computes it on sigmoid heads: BCE from the logits, MSE
+    (bits of ``mse_mask``) from the probabilities."""
+    ws = workspace(size('ot_bce_workspace_size', T, B), device)
+    ev = _probe.begin() if _probe is not None else None
+    call('ot_task_loss_logits_fwd', ptr(logits), ptr(probs), ptr(labels), T, B, mse_mask, ptr(loss), ptr(ws),
+         ws.numel(), stream())
+    if ev is not None:
+        _probe.end('head_loss', 0.0, ev)
+
+
+def task_loss_logits_bwd(probs, labels, gscale, T, B, dlogits, mse_mask: int = 0) -> None:
+    ev = _probe.begin() if _probe is not None else None
+    call('ot_task_loss_logits_bwd', ptr(probs), ptr(labels), ptr(gscale), T, B, mse_mask, ptr(dlogits), stream())
     if ev is not None:
         _probe.end('head_loss', 0.0, ev)
 

@@ -195,7 +195,7 @@ def _block_forward(m, l, x, I, Kq, seed, training, rstd_in=None, select=False, n
     qkv = torch.empty(B * I, 3 * d, device=dev)
     # bf16 mode, training: the QKV / FFN1 GEMMs also store their normalised A rows in bf16 (ot_rms_epilogue
     # .xn_out) for the copy-staged bf16 weight gradients of Wqkv / W1 (operands read once, no norm re-applied)
-    xn_on = (training and m.xn_bf16 and K.matmul_mode() == 'bf16' and d % TILE == 0
+    xn_on = (training and K.matmul_mode() == 'bf16' and d % TILE == 0
              and m.bimg(f'blk.{l}.wqkv') is not None)
     xn1 = torch.empty(B * I, d, dtype=torch.int16, device=dev) if xn_on else None
     x1n = torch.empty(B * Kq, d, dtype=torch.int16, device=dev) if xn_on else None
@@ -233,7 +233,7 @@ def _block_forward(m, l, x, I, Kq, seed, training, rstd_in=None, select=False, n
     # backward's saved operand (the backward rounds them to bf16 anyway)
     qp_f = _attn_qpos(cfg, pos)
     qkv16 = (torch.empty(B * I, 3 * d, dtype=torch.int16, device=dev)
-             if m.attn_fp8 and training and m.qkv_bf16 and K.attn_bwd_bf16_supported(I, Kq, hd, qp_f) else None)
+             if m.attn_fp8 and training and K.attn_bwd_bf16_supported(I, Kq, hd, qp_f) else None)
     K.attn_fwd(qkv, 3 * d, B, H, I, Kq, hd, o, lse, qpos=qp_f, fp8=m.attn_fp8,
                dequant=m.attn_fp8 and training, fp8_terms=m.fp8_terms, deq16=qkv16)
     if qkv16 is not None:
@@ -261,11 +261,11 @@ def _block_forward(m, l, x, I, Kq, seed, training, rstd_in=None, select=False, n
     # once per output column tile), and the W2 weight gradient reuses h
     w2img = m.bimg(f'blk.{l}.w2')
     h = (torch.empty(B * Kq, f, dtype=torch.int16, device=dev)
-         if m.store_gelu_fwd and K.matmul_mode() == 'bf16' and w2img is not None
+         if K.matmul_mode() == 'bf16' and w2img is not None
          and m.bimg(f'blk.{l}.w1') is not None and f % TILE == 0 else None)
     # ... and u itself in bf16 (as a bf16 Keras policy stores it): its one reader is then the FFN2 dgrad's
     # GELU' / row-dot epilogue (OT_EPI_AUX_BF16), which needs the fused norm2 backward's bf16-dU form
-    u_bf = h is not None and m.u_bf16 and m.du_bf16 and m.fuse_bwd2 and not m.fuse_bwd and f % TILE == 0
+    u_bf = h is not None and m.fuse_bwd2 and not m.fuse_bwd and f % TILE == 0
     u = torch.empty(B * Kq, f, device=dev, dtype=torch.int16 if u_bf else torch.float32)
     if h is not None:
         K.gemm_rms(OT_GEMM_NT, x1 if x1_16 is None else x1_16, d, d, mt['rows'][1], w1, d * f, d, f,
@@ -364,11 +364,11 @@ class _Block(torch.autograd.Function):
         dx2 = dx2.contiguous()
         rowdot = None
         fused2 = m.fuse_bwd2 and not m.fuse_bwd and f % TILE == 0
-        du_bf = (fused2 and h is not None and m.du_bf16 and m.bimg(f'blk.{l}.w1', 'dgrad') is not None)
+        du_bf = (fused2 and h is not None and m.bimg(f'blk.{l}.w1', 'dgrad') is not None)
         # FFN branch: dY2 = mask(dx2) — in bf16 with the bf16 dU path (its two readers, the FFN2 dgrad's A and
         # the W2 weight gradient's D, round it to bf16; the latter then runs copy-staged)
         if rate > 0:
-            dy2 = torch.empty(B * Kq, d, device=dev, dtype=torch.int16 if du_bf and m.dy_bf16 else torch.float32)
+            dy2 = torch.empty(B * Kq, d, device=dev, dtype=torch.int16 if du_bf else torch.float32)
             K.dropout_apply(dx2, d, dy2, d, B * Kq, d, seed, 2 * l + 1, rate, tail)
         else:
             dy2 = dx2
@@ -383,7 +383,7 @@ class _Block(torch.autograd.Function):
         # U's 4 and evaluates no erf (it did, once per output column tile: 4x at f = 2048, d = 512)
         # (the forward's FFN1 epilogue stored it already when h is not None)
         hbf = (torch.empty(B * Kq, f, dtype=torch.int16, device=dev)
-               if h is None and fused2 and m.store_gelu and K.matmul_mode() == 'bf16' else None)
+               if h is None and fused2 and K.matmul_mode() == 'bf16' else None)
         if hbf is None:
             with m.side(u if h is None else h, dy2):   # weight gradients overlap the dgrad chain on a second stream
                 K.wgrad(u if h is None else h, f, mt['rows'][1], dy2, d, mt['rows'][1], f, d, mt, nct, G,
@@ -445,13 +445,13 @@ class _Block(torch.autograd.Function):
         # bf16 mode, key-grouped backward (C5): dQKV in bf16 (OT_ATTN_DQKV_BF16) — the QKV dgrad (bf16 A) and
         # the Wqkv weight gradient (OT_WG_D_BF16) round it to bf16 anyway: the same values, half the bytes
         qp = _attn_qpos(cfg, pos)
-        dq_bf = (m.dqkv_bf16 and K.matmul_mode() == 'bf16'
+        dq_bf = (K.matmul_mode() == 'bf16'
                  and K.attn_bwd_bf16_forms(I, Kq, hd, qp) & _lib.OT_ATTN_DQKV_BF16
                  and m.bimg(f'blk.{l}.wqkv', 'dgrad') is not None)
         dqkv = torch.empty(B * I, 3 * d, device=dev, dtype=torch.int16 if dq_bf else torch.float32)
         if Kq < I:
             dqkv[:, :d].zero_()
-        K.attn_bwd(qkv, 3 * d, o, do, lse, B, H, I, Kq, hd, dqkv, qpos=qp, dq_part_bf16=m.dq_part_bf16)
+        K.attn_bwd(qkv, 3 * d, o, do, lse, B, H, I, Kq, hd, dqkv, qpos=qp, dq_part_bf16=True)
         an1 = xn1 is not None and dq_bf
         with m.side(xn1 if an1 else x, dqkv, rstd1):
             K.wgrad(xn1 if an1 else x, d, ma['rows'][0], dqkv, 3 * d, ma['rows'][0], d, 3 * d, ma, nca, G,
@@ -517,17 +517,18 @@ class _Head(torch.autograd.Function):
         K.head_fwd(pre1, m.p('head.w2'), m.p('head.b2'), T, B, dh, logits, probs)
         ctx.save_for_backward(x, rstd, y, pre1, probs)
         ctx.m = m
+        ctx.set_materialize_grads(False)
         m._last_logits = logits
-        return probs
+        return probs, logits
 
     @staticmethod
-    def backward(ctx, dprobs):
+    def backward(ctx, dprobs, dlogits):
         # the autograd engine runs this on its own thread: enter the model's precision there
         with K.precision(ctx.m.matmul):
-            return _Head._backward(ctx, dprobs)
+            return _Head._backward(ctx, dprobs, dlogits)
 
     @staticmethod
-    def _backward(ctx, dprobs):
+    def _backward(ctx, dprobs, dlogits):
         x, rstd, y, pre1, probs = ctx.saved_tensors
         m = ctx.m
         cfg = m.config
@@ -536,10 +537,13 @@ class _Head(torch.autograd.Function):
         B = x.shape[0]
         dev = x.device
         acc = m.accumulate_grads
-        dprobs = dprobs.contiguous()
+        dprobs = dprobs.contiguous() if dprobs is not None else None
+        dlogits = dlogits.contiguous() if dlogits is not None else None
+        if dprobs is None and dlogits is None:
+            return None, None, None
         dpre1 = torch.empty(T * B, dh, device=dev)
         K.head_bwd(pre1, m.p('head.w2'), probs, dprobs, T, B, dh, dpre1, m.g('head.w2'), m.g('head.b2'), dh, 1,
-                   accumulate=acc, device=dev)
+                   accumulate=acc, device=dev, dlogits=dlogits)
         hm = m.head_rows(B)
         hmd = hm.to(dev)
         K.wgrad(y, d, hmd['rows'][0], dpre1, dh, hmd['rows'][1], d, dh, hmd, hm.chunks.shape[0], T, m.g('head.w1'),
@@ -556,6 +560,30 @@ class _Head(torch.autograd.Function):
         if m.grad_ready is not None:
             m.grad_ready('head')                # out_norm + heads are final: the DP exchange may start
         return None, dx, None
+
+
+class _TaskLoss(torch.autograd.Function):
+    """Σ_task loss (train.py:78-93, 124-128) of the model's heads as the reference's Keras 2.12 computes it:
+    the sigmoid heads' cached logits give tf.nn.sigmoid_cross_entropy_with_logits for 'ctr' / 'cvr' (no
+    clipping), MeanSquaredError on the probabilities for any other task; the gradient goes to the logits."""
+
+    @staticmethod
+    def forward(ctx, probs, logits, labels, mse_mask):
+        T, B = probs.shape
+        loss = torch.empty(1, device=probs.device)
+        K.task_loss_logits_fwd(logits, probs, labels, T, B, loss, device=probs.device, mse_mask=mse_mask)
+        ctx.save_for_backward(probs, labels)
+        ctx.mse_mask = mse_mask
+        return loss[0]
+
+    @staticmethod
+    def backward(ctx, gl):
+        probs, labels = ctx.saved_tensors
+        T, B = probs.shape
+        dlogits = torch.empty_like(probs)
+        gl = gl.reshape(1).contiguous().float()
+        K.task_loss_logits_bwd(probs, labels, gl, T, B, dlogits, mse_mask=ctx.mse_mask)
+        return None, dlogits, None, None
 
 
 class _BCE(torch.autograd.Function):
@@ -593,8 +621,15 @@ def task_mse_mask(tasks) -> int:
 
 def keras_bce_loss(labels: torch.Tensor, probs: torch.Tensor, tasks=None) -> torch.Tensor:
     """Sum over tasks of the reference's per-task loss; labels/probs [T, B] device tensors.  ``tasks``
-    (names, in row order) selects MSE for tasks other than 'ctr'/'cvr'; None = BCE for every row."""
-    return _BCE.apply(probs, labels, task_mse_mask(tasks) if tasks is not None else 0)
+    (names, in row order) selects MSE for tasks other than 'ctr'/'cvr'; None = BCE for every row.
+    Probabilities from ``OneTransModel.forward_probs`` carry their heads' logits (``_ot_logits``, as Keras's
+    sigmoid output carries ``_keras_logits``) and the BCE is taken from those; other probabilities use the
+    clipped probability form."""
+    mask = task_mse_mask(tasks) if tasks is not None else 0
+    z = getattr(probs, '_ot_logits', None)
+    if z is not None:
+        return _TaskLoss.apply(probs, z, labels, mask)
+    return _BCE.apply(probs, labels, mask)
 
 
 # =============================================================================== the module
@@ -619,28 +654,29 @@ class OneTransModel(nn.Module):
         # 'bf16', or 'fp8attn' = BASELINE configs[4]'s attention on
         # block-scaled fp8 MFMA (forward QK^T and PV; the backward recomputes in the GEMM mode's precision from
         # the dequantised fp8 operands the training forward leaves in qkv: the straight-through gradient).
-        # ONETRANS_ATTN=fp8 selects the fp8 forward too.
         if getattr(cfg, 'compute_dtype', 'fp32') not in ('fp32', 'bf16', 'fp8attn'):
             raise ValueError(f"compute_dtype {cfg.compute_dtype!r}: expected 'fp32', 'bf16' or 'fp8attn'")
         # this model's GEMM / attention arithmetic, passed with every kernel call it makes (the C ABI holds no
         # precision state): 'bf16' for the reduced-precision configs, else the process default at construction
         # ('split', f32-accurate; kernels.set_matmul_mode / ONETRANS_MATMUL)
-        self.matmul = 'bf16' if getattr(cfg, 'compute_dtype', 'fp32') in ('bf16', 'fp8attn') else K.matmul_mode()
-        # activation recompute (config.recompute_blocks / ONETRANS_RECOMPUTE=1): a block keeps only its
+        if getattr(cfg, 'compute_dtype', 'fp32') in ('bf16', 'fp8attn'):
+            self.matmul = 'bf16'
+        elif K.matmul_mode() == 'bf16':
+            raise ValueError("compute_dtype 'fp32' with the process default matmul 'bf16' (ONETRANS_MATMUL / "
+                             "kernels.set_matmul_mode): set config.compute_dtype = 'bf16' for the bf16 arithmetic")
+        else:
+            self.matmul = K.matmul_mode()
+        # activation recompute (config.recompute_blocks): a block keeps only its
         # input for backward and re-runs its forward kernels there (_Block)
-        self.recompute = bool(getattr(cfg, 'recompute_blocks', False)) or os.environ.get('ONETRANS_RECOMPUTE') == '1'
-        self.attn_fp8 = (getattr(cfg, 'compute_dtype', 'fp32') == 'fp8attn'
-                         or os.environ.get('ONETRANS_ATTN', '') == 'fp8')
+        self.recompute = bool(getattr(cfg, 'recompute_blocks', False))
+        self.attn_fp8 = getattr(cfg, 'compute_dtype', 'fp32') == 'fp8attn'
         if self.attn_fp8 and cfg.hidden_dim // cfg.num_heads not in (64, 128):
             raise ValueError('fp8 attention needs head_dim 64 or 128')
         # e4m3 terms per attention operand: 2 (default; hi + lo, AUC within north_star's 1e-3 at C5) or 1
-        # (plain e4m3); config fp8_terms, env ONETRANS_FP8_TERMS
-        self.fp8_terms = int(os.environ.get('ONETRANS_FP8_TERMS', getattr(cfg, 'fp8_terms', 2)))
+        # (plain e4m3); config fp8_terms
+        self.fp8_terms = int(getattr(cfg, 'fp8_terms', 2))
         if self.fp8_terms not in (1, 2):
             raise ValueError(f'fp8_terms {self.fp8_terms}: 1 or 2')
-        # diagnostics only: ONETRANS_PYRAMID_KERNEL=0 addresses a 'tail' keep arithmetically instead of
-        # through ot_pyramid_select's position map (same kept set; for A/B timing of the map plumbing)
-        self.pyramid_kernel = os.environ.get('ONETRANS_PYRAMID_KERNEL', '1') != '0'
         self.f_ns = cfg.ns_input_width()
         self.layout = FlatLayout(cfg, self.f_ns)
         self.cfg_Lnsd = cfg.num_ns_tokens * cfg.hidden_dim
@@ -648,9 +684,8 @@ class OneTransModel(nn.Module):
         self.flat.grad = torch.zeros_like(self.flat)
         self.flatT = torch.zeros(self.layout.total, device=self.device)     # transposed GEMM weight shadow
         self._tdesc = torch.from_numpy(self.layout.transpose_desc.reshape(-1)).to(self.device)
-        # pre-split bf16 plane images of the GEMM weight banks (the plane GEMM's B operand, split mode);
-        # rebuilt with the transposed shadow after every weight update.  ONETRANS_PLANE_GEMM=0: off
-        self.use_plane = os.environ.get('ONETRANS_PLANE_GEMM', '1') != '0'
+        # pre-split bf16 plane images of the GEMM weight banks (the plane GEMM's B operand, split / bf16 mode);
+        # rebuilt with the transposed shadow after every weight update
         self.img = torch.zeros(max(1, self.layout.image_elems), dtype=torch.int16, device=self.device)
         self._img_valid, self._img_mode = False, None
         self._idesc = (torch.from_numpy(self.layout.image_desc.reshape(-1)).to(self.device)
@@ -668,36 +703,18 @@ class OneTransModel(nn.Module):
         # = rstd2 <gamma2 dy, x1>, the one row reduction the FFN1 dgrad epilogue cannot see.  norm1's
         # backward stays row-wise at d > 128 — a row-complete epilogue (each workgroup looping over the
         # row's column tiles, two passes) measured slower than the row-wise kernel at T
-        self.fuse_norms = (config.hidden_dim % TILE == 0 and os.environ.get('ONETRANS_FUSE_NORMS', '1') != '0')
+        # (tests/test_model_gpu.py::test_fused_norms_match_unfused turns fuse_norms / fuse_bwd2 off for the
+        # row-wise reference path)
+        self.fuse_norms = config.hidden_dim % TILE == 0
         self.fuse_bwd = self.fuse_norms and config.hidden_dim == TILE
-        self.fuse_bwd2 = self.fuse_norms and os.environ.get('ONETRANS_FUSE_NORM2_BWD', '1') != '0'
-        # bf16 mode: the FFN1 forward epilogue stores h = bf16(gelu(U)), which the FFN2 GEMM and the W2 weight
-        # gradient read (ONETRANS_STORE_GELU=bwd: only the FFN2 dgrad epilogue stores it, for the weight
-        # gradient; 0: both GEMMs recompute GELU from f32 U)
-        sg = os.environ.get('ONETRANS_STORE_GELU', '1')
-        self.store_gelu = sg != '0'
-        self.store_gelu_fwd = sg not in ('0', 'bwd')
-        # bf16 mode with the stored GELU: dU in bf16 (ONETRANS_DU_BF16=0: f32)
-        self.du_bf16 = os.environ.get('ONETRANS_DU_BF16', '1') != '0'
-        # bf16 mode, key-grouped attention backward: dQKV in bf16 (ONETRANS_DQKV_BF16=0: f32)
-        self.dqkv_bf16 = os.environ.get('ONETRANS_DQKV_BF16', '1') != '0'
-        # bf16 mode with the stored GELU and bf16 dU: the FFN1 pre-activation U in bf16 (ONETRANS_U_BF16=0: f32)
-        self.u_bf16 = os.environ.get('ONETRANS_U_BF16', '1') != '0'
-        # bf16 mode, training: bf16 normalised QKV / FFN1 inputs for the Wqkv / W1 weight gradients
-        # (ONETRANS_XN_BF16=0: those re-read the f32 inputs and re-apply the norm)
-        self.xn_bf16 = os.environ.get('ONETRANS_XN_BF16', '1') != '0'
-        # ... and the FFN2 dgrad's dY in bf16 (ONETRANS_DY_BF16=0: f32)
-        self.dy_bf16 = os.environ.get('ONETRANS_DY_BF16', '1') != '0'
-        # fp8 attention, training: the dequantised Q / K / V kept in bf16 for the backward (ONETRANS_QKV_BF16=0:
-        # written back into qkv in f32)
-        self.qkv_bf16 = os.environ.get('ONETRANS_QKV_BF16', '1') != '0'
-        # ... and the key slices' dQ partials in bf16 (ONETRANS_DQ_PART_BF16=0: f32; not bit-identical)
-        self.dq_part_bf16 = os.environ.get('ONETRANS_DQ_PART_BF16', '1') != '0'
-        # ... and the residual stream's bf16 copies for the QKV / FFN1 GEMMs' A (ONETRANS_X16=0: f32 A)
-        self.x16 = os.environ.get('ONETRANS_X16', '1') != '0'
+        self.fuse_bwd2 = self.fuse_norms
+        # bf16 mode (C5): every activation whose only readers are GEMM / attention operands rounded to bf16 anyway
+        # is stored in bf16 by its producer: h = gelu(U), U, dU, dY2, dQKV and the key slices'
+        # dQ partials, the normalised QKV / FFN1 inputs for the weight gradients, the fp8 forward's dequantised
+        # Q / K / V, the residual stream's copies for the QKV / FFN1 A operands (take_x16 / put_x16)
         self._x16 = None
         # block weight gradients run on a second stream, overlapping the dgrad chain
-        self.overlap_wgrad = os.environ.get('ONETRANS_OVERLAP_WGRAD', '1') != '0'
+        self.overlap_wgrad = True            # bench.py --no-overlap turns it off for standalone kernel traces
         self._side = None
         self._side_used = False
         self._side_keep: List[torch.Tensor] = []
@@ -771,7 +788,7 @@ class OneTransModel(nn.Module):
 
     def x16_on(self, d: int) -> bool:
         """Store bf16 copies of the residual stream for the next GEMM's A (bf16 mode, plane GEMMs)?"""
-        return self.x16 and d % TILE == 0 and K.matmul_mode() == 'bf16' and self.use_plane
+        return d % TILE == 0 and K.matmul_mode() == 'bf16'
 
     def put_x16(self, layer: int, x: torch.Tensor, x16: Optional[torch.Tensor]) -> None:
         """Block ``layer - 1``'s output x and its bf16 copy, for block ``layer``."""
@@ -789,8 +806,6 @@ class OneTransModel(nn.Module):
         """(image, column tiles per group, first tile) of a weight bank's pre-split B image for the plane
         GEMM: orient 'fwd' = W^T (RMSNorm gamma folded in for wqkv / w1), 'dgrad' = W; None when the
         bank has no image (partial column tiles) or the plane GEMM is off."""
-        if not self.use_plane:
-            return None
         e = self.layout.images.get((name, orient))
         if e is None:
             return None
@@ -1072,10 +1087,11 @@ class OneTransModel(nn.Module):
         for l, s in enumerate(sched):
             Kq = s['keep'] if l < nl - 1 else 1
             select = l < nl - 1 and Kq < s['in_len']         # a pyramid keep (the last layer: DCE, tail)
-            select = select and (self.pyramid_kernel or self.config.pyramid_select != 'tail')
             x, rstd = _Block.apply(self.flat, x, self, l, s['in_len'], Kq, layer_seed(seed, b0, s['in_len'],
                                    self.config.hidden_dim), training, rstd, select)
-        return _Head.apply(self.flat, x, self)
+        probs, logits = _Head.apply(self.flat, x, self)
+        probs._ot_logits = logits            # keras_bce_loss takes the BCE from the logits (Keras _keras_logits)
+        return probs
 
     def batch_offset(self, B: int) -> int:
         """Index of this process's first sample in the global batch (dropout masks are a function of the

@@ -60,6 +60,11 @@ class OneTransServer:
         self._maps = {}
 
     # ------------------------------------------------------------------ schedule
+
+    @property
+    def precision_model(self):
+        """The model whose arithmetic the cached stages run in (kernels.in_model_precision)."""
+        return self.m
     def schedule(self, L_S: int) -> List[Dict]:
         """Per layer: S rows s, N rows n, kept S rows kS, kept N rows kN (kS + kN = the layer's keep)."""
         cfg = self.m.config
@@ -244,7 +249,7 @@ class OneTransServer:
                 return o
 
             x, _ = self._block(l, x, C, n, kN, s, e['I'], attn)
-        probs = _Head.apply(m.flat, x, m)                                  # [T, C]
+        probs, _ = _Head.apply(m.flat, x, m)                               # [T, C]
         return {t: probs[i].view(-1, 1) for i, t in enumerate(cfg.tasks)}
 
     @torch.no_grad()

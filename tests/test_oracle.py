@@ -105,6 +105,17 @@ def test_bce_clip_rmsprop_kat():
     assert abs(km.keras_bce(np.array([1.0]), np.array([0.5])) - (-math.log(0.5 + 1e-7))) < 1e-15
     # p clipped to 1-1e-7 then log(1 - p + eps) = log(2e-7)
     assert abs(km.keras_bce(np.array([0.0]), np.array([1.0])) + math.log(2e-7)) < 1e-9
+    # the sigmoid-head form (Keras 2.12 _keras_logits): sigmoid_cross_entropy_with_logits, no clipping
+    assert abs(km.keras_bce_logits(np.array([1.0]), np.array([0.0])) - math.log(2.0)) < 1e-15
+    assert abs(km.keras_bce_logits(np.array([0.0]), np.array([40.0])) - 40.0) < 1e-12      # unclipped: not -log(2e-7)
+    assert abs(km.keras_bce_logits(np.array([1.0]), np.array([-3.0])) - math.log1p(math.exp(3.0))) < 1e-12
+    z = np.array([-2.0, 0.3, 5.0])
+    y = np.array([0.0, 1.0, 1.0])
+    p = 1.0 / (1.0 + np.exp(-z))
+    assert abs(km.keras_bce_logits(y, z) - km.keras_bce(y, p)) < 1e-6                        # same loss off saturation
+    zt = torch.tensor(z, requires_grad=True)
+    R.keras_bce_logits(torch.tensor(y), zt).backward()
+    np.testing.assert_allclose(zt.grad.numpy(), (p - y) / 3, rtol=1e-12)                    # d/dz = (sigmoid - y) / B
     g = np.array([3.0, 4.0])
     np.testing.assert_allclose(km.clip_by_norm(g, 1.0), [0.6, 0.8])
     np.testing.assert_allclose(km.clip_by_norm(g, 10.0), g)

@@ -66,14 +66,20 @@ def create_sample_batch(batch_size: int, config: OneTransConfig, seq_lens: Optio
 
 
 def criteo_batch(batch_size: int, config: OneTransConfig, seq_lens: Optional[List[int]] = None,
-                 seed: int = 1000) -> Batch:
-    """Criteo-shape batch: dense I* float32 [B,1]; sparse C* int64 [B,1]; seqs int64 [B,L_i]."""
+                 seed: int = 1000, teacher: str = 'ids') -> Batch:
+    """Criteo-shape batch: dense I* float32 [B,1]; sparse C* int64 [B,1]; seqs int64 [B,L_i].
+
+    ``teacher`` picks the label signal: 'ids' (default; every feature, the sparse ids through a hashed
+    per-id effect — learnable only by memorising ids) or 'dense' (the 13 dense features alone, 4x the
+    weight: a signal a few hundred steps of training pick up, for tests that need a model that has
+    learned)."""
     rng = np.random.Generator(np.random.PCG64(seed))
     B = batch_size
     fc = config.feature_config
     ns: Dict[str, np.ndarray] = {}
     trng = np.random.Generator(np.random.PCG64(7))
     signal = np.zeros((B, 2))
+    dense_signal = np.zeros((B, 2))
     for name in config.ns_feature_names():
         if name in config.sparse_features:
             card = config.sparse_features[name]
@@ -84,19 +90,25 @@ def criteo_batch(batch_size: int, config: OneTransConfig, seq_lens: Optional[Lis
         else:
             v = np.log1p(rng.lognormal(0.0, 1.0, size=(B, 1))).astype(np.float32)
             ns[name] = v
-            signal += v * trng.normal(size=(1, 2)) * 0.3
+            w = trng.normal(size=(1, 2)) * 0.3
+            signal += v * w
+            dense_signal += v * w * 4.0
     seq: Dict[str, np.ndarray] = {}
     lens = seq_lens or getattr(config, '_seq_lens', None)
     vocab = config.seq_item_vocab
     for name, L in zip(fc['sequence_features'], lens):
         seq[name] = ((rng.zipf(1.1, size=(B, L)) - 1) % vocab).astype(np.int64)
+    if teacher == 'dense':
+        signal = dense_signal
+    elif teacher != 'ids':
+        raise ValueError(f"teacher {teacher!r}: 'ids' or 'dense'")
     labels = _teacher_labels(seed + 1, B, config.tasks, signal - signal.mean(axis=0))
     return ns, seq, labels
 
 
 def make_batch(batch_size: int, config: OneTransConfig, seed: int = 1000,
-               seq_lens: Optional[List[int]] = None) -> Batch:
-    """Dispatch on the config: Criteo-shape when embedding tables are configured."""
+               seq_lens: Optional[List[int]] = None, teacher: str = 'ids') -> Batch:
+    """Dispatch on the config: Criteo-shape when embedding tables are configured (``teacher``: criteo_batch)."""
     if config.sparse_features or config.seq_item_vocab:
-        return criteo_batch(batch_size, config, seq_lens, seed)
+        return criteo_batch(batch_size, config, seq_lens, seed, teacher)
     return create_sample_batch(batch_size, config, seq_lens, seed)

@@ -137,6 +137,20 @@ def setup_config(name: str):
     return cfg
 
 
+# The reduced-precision training test's trajectory (tests/test_train_lowprec_gpu.py, golden train_T.npz): labels
+# from the dense features (data.criteo_batch teacher='dense') and RMSprop at dense lr 1e-4 with momentum 0.9 (an
+# optimizer_config the reference's trainer accepts, train.py:60-66), on which the T model learns within 20 steps
+# (held-out AUC 0.82 / 0.68, logit std 1.2 / 0.36; tools/lowprec_sweep.py, profiles/r05/lowprec_sweep.log)
+LOWPREC_TEACHER = 'dense'
+LOWPREC_OPT = {'dense_lr': 1e-4, 'momentum': 0.9}
+
+
+def lowprec_config():
+    cfg = setup_config('T')
+    cfg.optimizer_config = dict(cfg.optimizer_config, **LOWPREC_OPT)
+    return cfg
+
+
 BATCH_SEED = 424242
 MODEL_SEED = 0
 

@@ -4,7 +4,9 @@ steps"), computed by the CPU oracle (oracle/onetrans_ref.py, float64) in the bui
 
     python tests/golden/make_train_golden.py      # -> tests/golden/train_C2.npz
     python tests/golden/make_train_golden.py T    # -> tests/golden/train_T.npz (north_star's attention
-                                                  #    shape: d 256, head_dim 64, for the bf16 / fp8attn runs)
+                                                  #    shape: d 256, head_dim 64, for the bf16 / fp8attn runs;
+                                                  #    the learnable trajectory of fullsize_common.lowprec_config:
+                                                  #    dense-feature teacher, dense lr 1e-4, momentum 0.9)
 
 The run: the C2 model shape (4L d128 H4 f512, L_NS 12, L0 140, the C2 embedding tables with hash
 values, tests/fullsize_common.py; T: d 256 f 1024, the same tables), perturbed Keras init (seed 0), STEPS train steps of B = 512 fresh
@@ -28,7 +30,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 
-from fullsize_common import MODEL_SEED, bank_samples, compact_problem_multi, dropout_seed, setup_config  # noqa: E402
+from fullsize_common import (LOWPREC_TEACHER, MODEL_SEED, bank_samples, compact_problem_multi,  # noqa: E402
+                             dropout_seed, lowprec_config, setup_config)
 from oracle import onetrans_ref as R  # noqa: E402
 from recommend_amd.data import make_batch  # noqa: E402
 from recommend_amd.metrics import auc, keras_auc  # noqa: E402
@@ -44,10 +47,11 @@ EVAL_SEED = 6000
 def main() -> None:
     t0 = time.time()
     name = sys.argv[1] if len(sys.argv) > 1 else 'C2'
-    cfg = setup_config(name)
+    cfg = lowprec_config() if name == 'T' else setup_config(name)
+    teacher = LOWPREC_TEACHER if name == 'T' else 'ids'
     P = init_params(cfg, cfg.ns_input_width(), seed=MODEL_SEED, perturb=True, with_tables=False)
-    batches = [make_batch(B_TRAIN, cfg, seed=TRAIN_SEED0 + i) for i in range(STEPS)]
-    batches.append(make_batch(B_EVAL, cfg, seed=EVAL_SEED))
+    batches = [make_batch(B_TRAIN, cfg, seed=TRAIN_SEED0 + i, teacher=teacher) for i in range(STEPS)]
+    batches.append(make_batch(B_EVAL, cfg, seed=EVAL_SEED, teacher=teacher))
     ocfg, ob, tables, _ = compact_problem_multi(cfg, batches)
     Pt = R.to_torch(dict(P, **tables))
     st = R.init_state(Pt, ocfg)

@@ -2,31 +2,29 @@
 train.py:111-155, evaluate.py:45) at the T shape (north_star's attention shape: 4L d256, head_dim 64, L0 140,
 so the block-scaled fp8 attention forward is eligible).
 
-The f32-accurate model is trained (B = 512 fresh batches, dropout on) and its first 20 steps must follow the
+The trajectory is one the f32 model learns on (fullsize_common.lowprec_config: labels from the dense features,
+RMSprop at dense lr 1e-4 with momentum 0.9 — an optimizer_config the reference's trainer accepts).  The
+f32-accurate model is trained (B = 512 fresh batches, dropout on) and its first 20 steps must follow the
 float64 oracle's run (tests/golden/train_T.npz, make_train_golden.py T; AUC within 1e-3, loss within 2e-3).
-It continues to step 400 (held-out AUC 0.50 -> 0.58).  At steps 0, 20, 100, 200 and 400 its weights and
-tables are copied into a bf16 model and an fp8attn model (`compute_dtype`), which at the SAME weights must
+It continues to step 400.  At steps 0, 20, 50, 100, 200 and 400 its weights and tables are copied into a bf16
+model and an fp8attn model (`compute_dtype`), which at the SAME weights must
 
   * score the held-out 4096 samples with logits within the reduced precisions' logit bound of the f32
-    model's (rms 5e-3, max 2.5e-2; tests/test_fullsize_lowprec_gpu.py uses 0.05 at C5),
-  * give each task's exact and Keras AUC within north_star's 1e-3 of the f32 model's wherever the AUC is
-    well-conditioned, and never move it by more than 3x what i.i.d. noise of the measured logit error does,
+    model's (rms 5e-3 of max(1, logit std) — bf16 rounds relative to magnitude, and trained logits reach std
+    1.9 — and max 0.05, tests/test_fullsize_lowprec_gpu.py's C5 bound),
+  * give each task's exact and Keras 200-threshold AUC within north_star's 1e-3 of the f32 model's, at every
+    checkpoint,
   * produce the training gradient of the step's batch (same dropout masks) within GRAD_TOL of the f32
     gradient (relative L2 over all dense banks; the worst single bank is printed).
 
-Well-conditioned: i.i.d. Gaussian noise with the rms of the measured logit error moves the AUC by less
-than 2.5e-4.  This synthetic task trains with its logits compressed (their std falls from 0.26 at init to
-1e-3 - 1e-4 while the AUC climbs), so after step 0 the held-out ranking is decided by logit differences the
-size of bf16's rounding (~1e-3 absolute at every checkpoint): there the AUC measures tie-breaking, not
-the model, and is checked for being noise-like instead.  The test requires step 0 to be well-conditioned
-for every task, so the 1e-3 check is never vacuous.
+The checks are meaningful only on a model that ranks: from step 20 on, every task's held-out AUC must be at
+least 0.65 and its logit std at least 0.1 (at step 0, the initialisation, the logit std; measured
+tools/lowprec_sweep.py: AUC 0.82 / 0.68 at step 20, 0.85 / 0.86 at 400, std 0.36 - 1.9).
 
-Why the reduced precisions are not run free and compared at the end: the optimizer is chaotic in this
-regime.  RMSprop's g / sqrt(v) gives every near-zero gradient entry a full-size step whose sign is the
-rounding noise's, so the f32 model itself, started from weights perturbed by 1e-4 (relative), ends 20
-steps later with AUCs 8e-4 / 1.4e-3 away from the unperturbed run and up to 1.3e-2 away after 400 steps
-(tools/lowprec_chaos.py, profiles/r04/lowprec_chaos.txt) — a trajectory comparison measures the optimizer's
-Lyapunov exponent, not the precision."""
+Why the reduced precisions are not run free and compared at the end: RMSprop's g / sqrt(v) gives every
+near-zero gradient entry a full-size step whose sign is the rounding noise's, so two f32 runs from weights 1e-4
+apart drift apart by more than 1e-3 in AUC (tools/lowprec_chaos.py, profiles/r04/lowprec_chaos.txt) — a
+trajectory comparison measures the optimizer's sensitivity, not the precision."""
 
 import os
 
@@ -36,7 +34,7 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-from fullsize_common import MODEL_SEED, TABLE_SEED, fill_table_device, setup_config
+from fullsize_common import LOWPREC_TEACHER, MODEL_SEED, TABLE_SEED, fill_table_device, lowprec_config
 from recommend_amd.data import make_batch
 from recommend_amd.metrics import auc, keras_auc
 from recommend_amd.model import OneTransModel, keras_bce_loss
@@ -44,10 +42,11 @@ from recommend_amd.params import init_params
 from recommend_amd.trainer import OneTransTrainer, stack_labels
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden', 'train_T.npz')
-CHECKPOINTS = (0, 20, 100, 200, 400)
+CHECKPOINTS = (0, 20, 50, 100, 200, 400)
 GRAD_TOL = {'bf16': 5e-2, 'fp8attn': 1e-1}
-LOGIT_RMS, LOGIT_MAX = 5e-3, 2.5e-2
-WELL_CONDITIONED = 2.5e-4
+LOGIT_RMS, LOGIT_MAX = 5e-3, 5e-2  # rms relative to max(1, the f32 logits' std); max as test_fullsize_lowprec_gpu
+AUC_TOL = 1e-3                      # north_star
+MIN_AUC, MIN_LOGIT_STD = 0.65, 0.1  # the model ranks (from step 20; the std also at step 0)
 
 
 def _tdev(d, dev):
@@ -55,7 +54,7 @@ def _tdev(d, dev):
 
 
 def _model(dtype, P, dev):
-    cfg = setup_config('T')
+    cfg = lowprec_config()
     cfg.compute_dtype = dtype
     m = OneTransModel(cfg, device=dev, seed=MODEL_SEED, init=P)
     for k, t in m.tables.items():
@@ -74,13 +73,6 @@ def _aucs(m, ev, dev, with_logits=False):
     if with_logits:
         return out, m._last_logits.double().cpu().numpy().reshape(len(m.config.tasks), -1)
     return out
-
-
-def _noise_auc_shift(y, z, rms, draws=16):
-    """Mean |AUC change| when i.i.d. Gaussian noise of the given rms is added to the logits z."""
-    r = np.random.default_rng(11)
-    a0 = auc(y, z)
-    return float(np.mean([abs(auc(y, z + rms * r.standard_normal(z.shape)) - a0) for _ in range(draws)]))
 
 
 def _grad(m, batch, step, dev):
@@ -105,7 +97,7 @@ def test_train_lowprec_along_f32_trajectory(dev):
     G = np.load(GOLDEN)
     steps, Bt, Be = int(G['steps']), int(G['B_train']), int(G['B_eval'])
     assert steps == 20
-    cfg = setup_config('T')
+    cfg = lowprec_config()
     P = init_params(cfg, cfg.ns_input_width(), seed=MODEL_SEED, perturb=True, with_tables=False)
     ref = _model('fp32', P, dev)
     probe = _model('fp32', P, dev)                                # f32 gradients without touching ref's state
@@ -113,13 +105,17 @@ def test_train_lowprec_along_f32_trajectory(dev):
     assert ref.matmul == 'split' and all(m.matmul == 'bf16' for m in low.values())
     assert ref.flat.numel() == low['bf16'].flat.numel()
     tr = OneTransTrainer(cfg, model=ref)
-    ev = make_batch(Be, cfg, seed=6000)
+    ev = make_batch(Be, cfg, seed=6000, teacher=LOWPREC_TEACHER)
     report, fails = [], []
     losses = []
     for i in range(CHECKPOINTS[-1] + 1):
-        batch = make_batch(Bt, cfg, seed=5000 + i)
+        batch = make_batch(Bt, cfg, seed=5000 + i, teacher=LOWPREC_TEACHER)
         if i in CHECKPOINTS:
             a32, z32 = _aucs(ref, ev, dev, True)
+            for j, t in enumerate(cfg.tasks):
+                report.append(f'step {i} f32 {t}: AUC {a32[j][0]:.6f} (keras {a32[j][1]:.6f}), logit std {z32[j].std():.3f}')
+                if z32[j].std() < MIN_LOGIT_STD or (i > 0 and a32[j][0] < MIN_AUC):
+                    fails.append((i, 'f32 does not rank', t, a32[j][0], float(z32[j].std())))
             _copy_state(probe, ref)
             g32 = _grad(probe, batch, i + 1, dev)
             for dt, m in low.items():
@@ -129,22 +125,13 @@ def test_train_lowprec_along_f32_trajectory(dev):
                 for j, t in enumerate(cfg.tasks):
                     dz = z[j] - z32[j]
                     rms, mx = float(np.sqrt(np.mean(dz ** 2))), float(np.abs(dz).max())
-                    y = np.asarray(ev[2][t]).reshape(-1)
-                    shift = _noise_auc_shift(y, z32[j], rms)
                     d = (abs(a[j][0] - a32[j][0]), abs(a[j][1] - a32[j][1]))
-                    good = shift < WELL_CONDITIONED
                     report.append(f'step {i} {dt} {t}: AUC {a[j][0]:.6f} vs f32 {a32[j][0]:.6f} (|d| {d[0]:.1e}, keras '
-                                  f'|d| {d[1]:.1e}); logits: f32 std {z32[j].std():.2e}, |d| rms {rms:.2e} max '
-                                  f'{mx:.2e}; AUC shift of iid noise of that rms {shift:.1e} '
-                                  f'({"well-conditioned" if good else "ill-conditioned"})')
-                    if rms >= LOGIT_RMS or mx >= LOGIT_MAX:
+                                  f'|d| {d[1]:.1e}); logits |d| rms {rms:.2e} max {mx:.2e}')
+                    if rms >= LOGIT_RMS * max(1.0, float(z32[j].std())) or mx >= LOGIT_MAX:
                         fails.append((i, dt, t, 'logits', rms, mx))
-                    if good and max(d) >= 1e-3:
+                    if max(d) >= AUC_TOL:
                         fails.append((i, dt, t, 'auc', d))
-                    if max(d) > max(1e-3, 3 * shift):
-                        fails.append((i, dt, t, 'auc beyond noise', d, shift))
-                    if i == 0 and not good:
-                        fails.append((i, dt, t, 'step 0 ill-conditioned', shift))
                 num = sum(float(np.sum((g[k] - g32[k]) ** 2)) for k in g32)
                 den = sum(float(np.sum(g32[k] ** 2)) for k in g32)
                 rel = (num / den) ** 0.5

@@ -170,6 +170,20 @@ def hbm_traffic(config):
     return None, None
 
 
+def attention_pmc(config):
+    """MFMA-busy and VALU-per-MFMA of the attention kernels from the newest committed PMC summary of this
+    config's layer shape (tools/pmc_attn.sh -> profiles/*/pmc_attn_<config>.json), or None."""
+    import glob
+    for fn in sorted(glob.glob(os.path.join(ROOT, 'profiles', '*', f'pmc_attn_{config}.json')), reverse=True):
+        try:
+            d = json.load(open(fn))
+        except (OSError, ValueError):
+            continue
+        d['source'] = os.path.relpath(fn, ROOT)
+        return d
+    return None
+
+
 def main():
     args = parse()
     world, rank, local = init_dist(args)
@@ -271,7 +285,7 @@ def main():
         torch.cuda.synchronize()
         K.set_probe(None)
         model.overlap_wgrad = overlap
-        mm = K.matmul_mode()
+        mm = model.matmul
         gpk = (BF16_MFMA_PEAK_TFLOPS / SPLIT_TERMS if mm == 'split' else
                BF16_MFMA_PEAK_TFLOPS if mm == 'bf16' else FP32_MFMA_PEAK_TFLOPS)
         rep = probe.report(args.probe_steps, gpk, HBM_PEAK_GBS)
@@ -291,7 +305,7 @@ def main():
         'value': round(value, 1), 'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': round(1e3 * t / args.steps, 3), 'higher_is_better': True,
         'scaling': 'weak', 'vs_baseline': None,
-        'dtype': 'bf16' if K.matmul_mode() == 'bf16' else 'f32', 'data': 'synthetic', 'precision': precision,
+        'dtype': 'bf16' if model.matmul == 'bf16' else 'f32', 'data': 'synthetic', 'precision': precision,
         'config': {'workload': f'{args.config}: OneTrans {cfg.num_layers}L d{cfg.hidden_dim} H{cfg.num_heads} f{cfg.ffn_dim} '
                                f'L_NS{cfg.num_ns_tokens} L_S{sum(seq_lens) + 2} (seq 3x{seq_lens[0]}), '
                                f'Criteo-shape 13 dense + 26 ids, '
@@ -323,20 +337,20 @@ def main():
     if rep is not None and 'mixed_gemm' in rep['families']:
         traffic, tsrc = hbm_traffic(args.config)
         dom = rep['families']['mixed_gemm']
-        if K.matmul_mode() == 'split':
+        if model.matmul == 'split':
             # the GEMMs issue SPLIT_TERMS bf16 MFMA products per f32 product: their matrix-core
             # ceiling in f32 flops is the bf16 dense peak / SPLIT_TERMS
             gpeak = round(BF16_MFMA_PEAK_TFLOPS / SPLIT_TERMS, 1)
             gkern = ('plane_gemm_kernel / mixed_gemm_kernel + wgrad_split_kernel (f32 operands split exactly into '
                      f'3 bf16 parts, {SPLIT_TERMS} bf16 MFMA products per f32 product; peak = bf16 dense / {SPLIT_TERMS})')
-        elif K.matmul_mode() == 'bf16':
+        elif model.matmul == 'bf16':
             gpeak = BF16_MFMA_PEAK_TFLOPS
             gkern = ('plane_gemm_kernel / mixed_gemm_kernel + wgrad_split_kernel (operands rounded to bf16, one bf16 '
                      'MFMA product)')
         else:
             gpeak = FP32_MFMA_PEAK_TFLOPS
             gkern = 'mixed_gemm_kernel + wgrad_kernel (native f32 MFMA)'
-        res['matmul'] = K.matmul_mode()
+        res['matmul'] = model.matmul
         # the family's binding roof: each launch is floored by max(flops / MFMA peak, bytes / HBM peak);
         # 'bound' is the roof that holds the larger share of that floor over the family's launches
         # (C2's K = 128 GEMMs sit right of the ridge on HBM; C5's bf16 GEMMs on MFMA)
@@ -366,7 +380,7 @@ def main():
         res['kernel_time_ms_per_step'] = {k: round(v['ms_per_step'], 3) for k, v in rep['families'].items()}
         # north_star "MFMA utilisation on OneTrans attention" (standalone attention at
         # L~140 is memory-heavy, so the block's matrix work is reported beside the core): achieved
-        # fp32-MFMA fraction of (i) the attention core kernels, (ii) the transformer block = every
+        # algorithmic fraction of (i) the attention core kernels, (ii) the transformer block = every
         # MFMA kernel (GEMMs + attention) over all of the block's kernel time (+ row-wise kernels)
         fams = rep['families']
         att = fams.get('attention')
@@ -375,21 +389,32 @@ def main():
             fl = lambda f: fams[f]['tflops'] * fams[f]['ms_per_step'] * 1e9 if f in fams else 0.0
             blk_fl = fl('mixed_gemm') + fl('attention')
             blk_ms = ms('mixed_gemm') + ms('attention') + ms('rowwise')
-            # matrix-core time the block's algorithmic work needs at each kernel's own peak, over the
-            # block's kernel time (GEMMs at the split ceiling, attention at the f32 MFMA peak)
-            busy_ms = fl('mixed_gemm') / (gpeak * 1e9) + fl('attention') / ((
-                BF16_MFMA_PEAK_TFLOPS if K.matmul_mode() == 'bf16' else FP32_MFMA_PEAK_TFLOPS) * 1e9)
-            apeak = BF16_MFMA_PEAK_TFLOPS if K.matmul_mode() == 'bf16' else FP32_MFMA_PEAK_TFLOPS
+            bf16 = model.matmul == 'bf16'
+            # the f32-accurate attention is priced against the native f32 MFMA peak (what an exact-f32 attention
+            # could reach), and beside it against the ceiling of the arithmetic it actually issues: the slice
+            # kernels (I <= 192) run each f32 product as 3 fp16 MFMA products (two scaled fp16 planes; the
+            # head_dim-32 forward as 6 bf16 products of three planes), so that ceiling is bf16 dense / 3
+            apeak = BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_MFMA_PEAK_TFLOPS
+            issued_peak = BF16_MFMA_PEAK_TFLOPS if bf16 else BF16_MFMA_PEAK_TFLOPS / 3
+            busy_ms = fl('mixed_gemm') / (gpk * 1e9) + fl('attention') / (apeak * 1e9)
             res['attention_mfma'] = {
                 'core_tflops': round(att['tflops'], 2),
                 'core_frac': round(att['tflops'] / apeak, 4),
                 'core_peak': apeak,
+                'core_frac_of_issued_ceiling': round(att['tflops'] / issued_peak, 4),
+                'issued_ceiling': round(issued_peak, 1),
                 'block_tflops': round(blk_fl / (blk_ms * 1e-3) / 1e12, 2),
                 'block_frac': round(busy_ms / blk_ms, 4), 'unit': 'TFLOP/s',
                 'note': 'algorithmic flops (tail-only queries, causal pairs) / HIP-event kernel time; '
-                        + ('attention core on bf16 MFMA (peak = bf16 dense 2516.8; with fp8attn the forward '
-                           'runs block-scaled fp8, whose dense peak is 2x)' if K.matmul_mode() == 'bf16'
-                           else 'attention core on native f32 MFMA (peak 157.3)')}
+                        + ('attention on bf16 MFMA (peak = bf16 dense 2516.8; with fp8attn the forward runs '
+                           'block-scaled fp8, whose dense peak is 2x)' if bf16 else
+                           'f32-accurate attention: core_frac against the native f32 MFMA peak 157.3; the kernels '
+                           'issue split MFMA products (slice kernels: 3 fp16 products per f32 product, the hd-32 '
+                           'forward 6 bf16 products; longer sequences: 6 bf16 products or native f32), so '
+                           'core_frac_of_issued_ceiling prices them against bf16 dense / 3')}
+            pmc = attention_pmc(args.config)
+            if pmc is not None:
+                res['attention_mfma']['pmc'] = pmc
     if not args.no_cpu_baseline and world == 1:          # rank 0 at N=1 only
         log('timed region and probe done; CPU baseline')
         res['cpu_baseline'] = cpu_baseline(args.config, args.cpu_seconds)

@@ -46,6 +46,8 @@ def parse():
     ap.add_argument('--no-probe', action='store_true', help='skip the per-kernel HIP-event (roofline) pass')
     ap.add_argument('--probe-steps', type=int, default=10, help='steps of the roofline pass (0: no roofline)')
     ap.add_argument('--repeats', type=int, default=3, help='timed regions of --steps steps; value = median')
+    ap.add_argument('--no-lookahead', action='store_true',
+                    help='row-sharded tables route each step\'s ids when it starts (default: during the step before)')
     ap.add_argument('--no-overlap', action='store_true',
                     help='weight gradients on the main stream for the whole run (rocprofv3 runs: every kernel '
                          'standalone, so its trace durations compare with the roofline pass)')
@@ -212,7 +214,9 @@ def main():
 
     def step(i):
         ns, seq, y = batches[i % len(batches)]
-        return trainer.train_step((ns, seq, y))
+        # the next batch is known (resident ring): a row-sharded table routes its ids during this step
+        nxt = None if args.no_lookahead else batches[(i + 1) % len(batches)]
+        return trainer.train_step((ns, seq, y), next_batch=nxt)
 
     for i in range(args.warmup):
         step(i)
@@ -243,11 +247,14 @@ def main():
         torch.cuda.synchronize()
         return max(wall, ev0.elapsed_time(ev1) / 1e3), o
 
-    times, exposed = [], []
+    times, exposed, route_wait = [], [], []
     log(f'{args.warmup} warm-up steps done')
     for r in range(max(1, args.repeats)):
+        for st_ in model.sharded.values():
+            st_.route_wait_s = 0.0
         t_r, out = timed_region(args.warmup + r * args.steps)
         times.append(t_r)
+        route_wait.append(1e3 * sum(st_.route_wait_s for st_ in model.sharded.values()) / args.steps)
         if exch is not None:
             ms = sum(a.elapsed_time(b) for (a, b) in exch)
             exch.clear()
@@ -257,13 +264,14 @@ def main():
     per_rank = [rank_t]
     if world > 1:
         import torch.distributed as dist
-        tt = torch.tensor([rank_t, float(np.median(exposed)) if exposed else 0.0],
+        tt = torch.tensor([rank_t, float(np.median(exposed)) if exposed else 0.0, float(np.median(route_wait))],
                           device='cpu' if dist.get_backend() == 'gloo' else dev)
         gath = [torch.empty_like(tt) for _ in range(world)]
         dist.all_gather(gath, tt)
         allr = torch.stack(gath).cpu()
         per_rank = allr[:, 0].tolist()
         exposed_ranks = allr[:, 1].tolist()
+        route_wait_ranks = allr[:, 2].tolist()
         t = max(per_rank)                             # max over ranks
     loss = float(out['total_loss'].item())
     trainer.optimizer.exchange_events = None
@@ -327,6 +335,10 @@ def main():
                        'exposed_exchange_ms_per_step_max': round(max(exposed_ranks), 3),
                        'exposed_exchange_ms_per_step_min': round(min(exposed_ranks), 3),
                        'sharded_tables': sorted(model.sharded),
+                       # host time the row-sharded lookups spend routing at the start of a step's forward,
+                       # before their first gather launch (look-ahead routing moves it into the step before)
+                       'route_host_wait_ms_per_step_max': round(max(route_wait_ranks), 3),
+                       'lookahead_routing': not args.no_lookahead,
                        # per row-sharded table: rows this rank sent to their owners in the last lookup
                        # (distinct ids when de-duplicated) and the ids of that lookup
                        'sharded_rows_sent_of_ids': {k: [t.sent_rows, t.last_route[0] if t.last_route else 0]

@@ -732,6 +732,7 @@ class OneTransModel(nn.Module):
         self.inputs_ready = None
         # row-sharded tables (data-parallel runs): 'emb.seq_item' lives partitioned over the ranks
         self.sharded: Dict[str, 'ShardedTable'] = {}
+        self._pending_route = None                    # route_ahead(): the next lookup's routed ids
         shard_seq = self._shard_seq_table()
         params = init if init is not None else init_params(cfg, self.f_ns, seed=seed, with_tables=False)
         if shard_seq:
@@ -954,7 +955,8 @@ class OneTransModel(nn.Module):
                 st = self.sharded['emb.seq_item']
                 ids = [seq[n] if isinstance(seq[n], torch.Tensor) else torch.from_numpy(np.asarray(seq[n]))
                        for (_, n, _) in present]
-                plan['seq_A'] = st.lookup(ids, ready=self.inputs_ready)
+                routed, self._pending_route = self._pending_route, None     # route_ahead() of these ids
+                plan['seq_A'] = st.lookup(ids, ready=self.inputs_ready, routed=routed)
                 plan['seq_ids'] = st.last_ids
                 plan['seq_route'] = st.last_route
             elif id_seq:
@@ -1092,6 +1094,20 @@ class OneTransModel(nn.Module):
         probs, logits = _Head.apply(self.flat, x, self)
         probs._ot_logits = logits            # keras_bce_loss takes the BCE from the logits (Keras _keras_logits)
         return probs
+
+    def route_ahead(self, seq_features: Dict) -> None:
+        """Look-ahead routing of the row-sharded item table (sharded.py ShardedTable.route): issue the routing of
+        the NEXT forward's sequence ids now — the trainer calls it between step i's forward and backward with
+        step i + 1's batch, so the split-size all-to-all and its host copy run beside step i's backward and the
+        next lookup finds them done.  The next forward must be called with the same id tensors."""
+        if 'emb.seq_item' not in self.sharded or not seq_features:
+            return
+        names = [n for n in self.config.feature_config['sequence_features'] if n in seq_features]
+        if not names or torch.is_floating_point(torch.as_tensor(seq_features[names[0]])):
+            return
+        ids = [seq_features[n] if isinstance(seq_features[n], torch.Tensor)
+               else torch.from_numpy(np.asarray(seq_features[n])) for n in names]
+        self._pending_route = self.sharded['emb.seq_item'].route(ids, ready=self.inputs_ready)
 
     def batch_offset(self, B: int) -> int:
         """Index of this process's first sample in the global batch (dropout masks are a function of the

@@ -34,6 +34,8 @@ from typing import Optional
 
 import os
 
+import time
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -77,8 +79,12 @@ class ShardedTable:
         # stream = GPU_MAX_HW_QUEUES 4 hardware queues), or a stream of its own when used standalone
         self.route_stream = route_stream if route_stream is not None else (
             torch.cuda.Stream(device=device) if is_cuda else None)
-        self._counts_host = torch.empty(2 * self.world, dtype=torch.int32, pin_memory=is_cuda)
+        # split sizes land here (pinned); two buffers, so a look-ahead route (route()) of the next batch can be
+        # in flight while this batch's are still being read
+        self._counts_host = [torch.empty(2 * self.world, dtype=torch.int32, pin_memory=is_cuda) for _ in range(2)]
+        self._counts_i = 0
         self.events = None        # diagnostics: a list collects HIP-event pairs around lookup / update
+        self.route_wait_s = 0.0   # diagnostics: host seconds lookup() spent routing before its first gather launch
 
     def _mark(self):
         if self.events is None:
@@ -98,10 +104,21 @@ class ShardedTable:
         else:
             dist.all_to_all_single(out, inp, out_splits, in_splits)
 
+    def route(self, ids, ready=None) -> 'PendingRoute':
+        """Look-ahead routing: stage ``ids`` and issue their routing (sort by owner, the split-size all-to-all,
+        the split sizes' copy to the host) on the route stream now, and return without waiting; ``lookup(ids,
+        routed=<the result>)`` later takes the routed ids (its host wait then finds the sizes already there).
+        The trainer routes step i + 1's ids during step i (OneTransTrainer.train_step(next_batch=...)), so at
+        N > 1 the split-size exchange overlaps step i's backward instead of stalling step i + 1's start."""
+        return PendingRoute(self, ids, *self._issue_route(ids, ready))
+
     def _route(self, ids, ready):
         """Stage ``ids`` (a tensor or a list concatenated in order; host or device) and route them by owner
         on the route stream; returns (ids on the device, route buffers, send splits, recv splits) after the
         host has waited for that stream alone (the split sizes)."""
+        return self._finish_route(*self._issue_route(ids, ready))
+
+    def _issue_route(self, ids, ready):
         dev, rs = self.device, self.route_stream
         parts = list(ids) if isinstance(ids, (list, tuple)) else [ids]
         host = all(t.device.type == 'cpu' for t in parts)
@@ -134,27 +151,40 @@ class ShardedTable:
             recv_counts = torch.empty_like(counts)
             self._a2a(recv_counts, counts, None, None)
             both = torch.cat([counts, recv_counts])
-            self._counts_host.copy_(both, non_blocking=rs is not None)
+            host_counts = self._counts_host[self._counts_i]
+            self._counts_i ^= 1
+            host_counts.copy_(both, non_blocking=rs is not None)
+            done = None
             if rs is not None:
                 done = torch.cuda.Event()
                 done.record(rs)
-        if rs is not None:
+        return ids_d, bufs, host_counts, done
+
+    def _finish_route(self, ids_d, bufs, host_counts, done):
+        if done is not None:
             done.synchronize()                       # the one host wait: this stream's few kernels only
-            main = torch.cuda.current_stream(dev)
-            main.wait_stream(rs)
+            main = torch.cuda.current_stream(self.device)
+            main.wait_stream(self.route_stream)
             for t in (ids_d, *bufs):                 # allocated on the route stream, used on the main one
                 t.record_stream(main)
-        both = self._counts_host.tolist()
+        both = host_counts.tolist()
         return ids_d, bufs, both[:self.world], both[self.world:]
 
-    def lookup(self, ids, ready=None) -> torch.Tensor:
+    def lookup(self, ids, ready=None, routed: 'PendingRoute' = None) -> torch.Tensor:
         """Rows of ``ids`` (int64 [n], or a list of id tensors taken in order; host or device) -> [n, E] fp32
         (zeros for ids outside the table); the staged device ids are kept in ``last_ids``.  ``ready``:
         for device ids, the HIP event after which they are valid (True: already complete, e.g. resident
-        batches; None: wait for the current stream)."""
+        batches; None: wait for the current stream).  ``routed``: these ids' look-ahead ``route()``."""
         ev0 = self._mark()
         E, dev = self.E, self.device
-        ids_d, bufs, send_splits, recv_splits = self._route(ids, ready)
+        t0 = time.perf_counter()
+        if routed is not None:
+            if not routed.matches(self, ids):
+                raise ValueError(f'{self.name}: lookup with a look-ahead route of other ids')
+            ids_d, bufs, send_splits, recv_splits = self._finish_route(*routed.parts)
+        else:
+            ids_d, bufs, send_splits, recv_splits = self._route(ids, ready)
+        self.route_wait_s += time.perf_counter() - t0
         n = ids_d.numel()
         S = sum(send_splits)                  # ids this rank sends: distinct ids (dedup) or n
         R = sum(recv_splits)
@@ -231,3 +261,17 @@ class ShardedTable:
             lr_ = (self.num_rows - r + self.world - 1) // self.world
             out[r::self.world] = parts[r][:lr_]
         return out
+
+
+class PendingRoute:
+    """A look-ahead route (ShardedTable.route): the staged ids' routing issued on the route stream, not yet
+    waited for.  Identified by the id tensors it was made from."""
+
+    def __init__(self, table, ids, *parts):
+        self.table = table
+        self.key = tuple((t.data_ptr(), tuple(t.shape)) for t in (ids if isinstance(ids, (list, tuple)) else [ids]))
+        self.parts = parts
+
+    def matches(self, table, ids) -> bool:
+        key = tuple((t.data_ptr(), tuple(t.shape)) for t in (ids if isinstance(ids, (list, tuple)) else [ids]))
+        return table is self.table and key == self.key

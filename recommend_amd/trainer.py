@@ -238,13 +238,17 @@ class OneTransTrainer:
         self.history = {'train_loss': [], 'val_loss': [], 'train_metrics': {}, 'val_metrics': {}}
 
     # --------------------------------------------------------------- steps
-    def train_step(self, batch_data) -> Dict[str, torch.Tensor]:
-        """train.py:111-155.  Returns {'total_loss': device scalar} (no host sync)."""
+    def train_step(self, batch_data, next_batch=None) -> Dict[str, torch.Tensor]:
+        """train.py:111-155.  Returns {'total_loss': device scalar} (no host sync).  ``next_batch`` (optional, the
+        batch the next call will get, e.g. from a prefetching loader): a row-sharded table routes its ids during
+        this step (OneTransModel.route_ahead)."""
         non_seq, seq, labels = batch_data
         dev = self.device
         y = labels if isinstance(labels, torch.Tensor) else stack_labels(labels, self.config.tasks, dev)
         self.model.train()
         probs = self.model.forward_probs(_to_dev(non_seq, dev), _seq_inputs(self.model, seq, dev), training=True)
+        if next_batch is not None and self.model.sharded:
+            self.model.route_ahead(_seq_inputs(self.model, next_batch[1], dev))
         loss = keras_bce_loss(y, probs, self.config.tasks)
         self.optimizer.begin_backward()
         loss.backward()

@@ -110,7 +110,7 @@ def _ids_of(rank, num_rows, world, rng):
     return np.concatenate([ids, ids[:5], [-1, num_rows + 2]]).astype(np.int64)
 
 
-def _worker(rank, world, port, q, dedup):
+def _worker(rank, world, port, q, dedup, lookahead=False):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
     dist.init_process_group('gloo', rank=rank, world_size=world)
@@ -133,8 +133,19 @@ def _worker(rank, world, port, q, dedup):
         recv = route[5]
         acc = torch.full((st.table.shape[0], E), 0.1)
         lr, eps, clip = 0.05, 1e-7, 1.5
+        nxt = None
+        if lookahead:            # the next batch's ids routed before this step's update (trainer.route_ahead)
+            ids2 = torch.from_numpy(_ids_of(rank, num_rows, world, np.random.default_rng(300 + rank)))
+            nxt = st.route(ids2)
         st.apply_gradient(route, torch.from_numpy(grads_all[rank]), acc, lr, eps, clip)
         new = st.full_table().numpy()
+        err_next = 0.0
+        if lookahead:            # ... looked up after the update: the updated rows, through the look-ahead route
+            got2 = st.lookup(ids2, routed=nxt).numpy()
+            i2 = ids2.numpy()
+            ok2 = (i2 >= 0) & (i2 < num_rows)
+            exp2 = np.where(ok2[:, None], new[np.clip(i2, 0, num_rows - 1)], 0.0)
+            err_next = float(np.abs(got2 - exp2).max()) if len(i2) else 0.0
         g = np.zeros((num_rows, E), np.float64)
         for i, gr in zip(ids_all, grads_all):
             v = (i >= 0) & (i < num_rows)
@@ -143,18 +154,19 @@ def _worker(rank, world, port, q, dedup):
         g = g * clip / max(l2, clip)
         ref = full - lr * g / np.sqrt(0.1 + g * g + eps)
         distinct = len(np.unique(np.where(ok, ids, -1))) if len(ids) else 0
-        q.put((rank, len(ids), recv, err_lookup, float(np.abs(new - ref).max()), st.sent_rows, distinct))
+        q.put((rank, len(ids), recv, max(err_lookup, err_next), float(np.abs(new - ref).max()), st.sent_rows if not
+               lookahead else distinct if dedup else len(ids), distinct))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('dedup', [True, False])
-def test_sharded_exchange_world4_with_empty_peers(dedup):
+@pytest.mark.parametrize('dedup,lookahead', [(True, False), (False, False), (True, True)])
+def test_sharded_exchange_world4_with_empty_peers(dedup, lookahead):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
     world = 4
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, dedup)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, dedup, lookahead)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

@@ -100,11 +100,15 @@ def _worker(rank, world, port, q, sharding='row'):
         st = R.init_state(Pt, cfg)
         kv = keras_variables(cfg, {k: v.shape for k, v in P.items() if not k.startswith('emb.')})
         losses = []
+        sl = slice(rank * B // world, (rank + 1) * B // world)
+        part = lambda d: {k: v[sl] for k, v in d.items()}
+        batches = [make_batch(B, cfg, seed=3000 + step) for step in range(3)]
+        parts = [tuple(part(x) for x in b) for b in batches]
         for step in range(3):
-            ns, seq, lab = make_batch(B, cfg, seed=3000 + step)
-            sl = slice(rank * B // world, (rank + 1) * B // world)
-            part = lambda d: {k: v[sl] for k, v in d.items()}
-            out = tr.train_step((part(ns), part(seq), part(lab)))
+            ns, seq, lab = batches[step]
+            # the row-sharded runs route the next step's ids during this step (look-ahead, trainer.route_ahead)
+            nxt = parts[step + 1] if step + 1 < 3 and sharding == 'row' else None
+            out = tr.train_step(parts[step], next_batch=nxt)
             loss = out['total_loss'].detach().reshape(1).cpu()
             dist.all_reduce(loss)
             losses.append(float(loss) / world)

@@ -292,10 +292,13 @@ int ot_attn_bwd_dqkv_bf16_supported(int I, int K, int head_dim, int selected, in
 /* the OT_ATTN_*_BF16 flags the backward supports at this shape: all three on the key-grouped bf16 backward,
  * OT_ATTN_DQKV_BF16 alone on the short-tail kernel (K <= 4: the last layer after DCE), none otherwise */
 int ot_attn_bwd_bf16_forms(int I, int K, int head_dim, int selected, int precision);
+/* (in the f32-accurate mode it also covers the head_dim-64 slice backward's dS scratch: one causal block pair
+ * store per co-resident workgroup, two per CU; a smaller workspace shrinks that kernel's grid) */
 size_t ot_attn_bwd_flags_workspace_size(int B, int H, int I, int K, int head_dim, int selected, int flags, int precision);
 /* 1 when the f32-accurate mode (OT_MATMUL_SPLIT_BF16) runs this shape's forward and backward as one
- * workgroup per (sample, head) slice on split-bf16 MFMA (attention_slice.hip: head_dim 32 / 64, I <= 192,
- * tail queries for the backward, the slice's planes and dS store within LDS), else 0 */
+ * workgroup per (sample, head) slice on split MFMA (attention_slice.hip: head_dim 32 / 64, I <= 192,
+ * tail queries for the backward, the slice's planes within LDS; the dS store in LDS at head_dim 32, in the
+ * workspace at 64), else 0 */
 int ot_attn_slice_supported(int I, int K, int head_dim, int selected);
 int ot_attn_bwd_flags(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
                       int B, int H, int I, int K, const int32_t* qpos, int head_dim, void* dqkv, int flags,

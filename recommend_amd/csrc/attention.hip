@@ -12,6 +12,7 @@
 // Orientation: S^T = K Q^T puts the query on the MFMA column (lane) and keys in registers, so
 // P^T (registers) is directly the B operand of O^T = V^T P^T (the accumulator-as-operand idiom,
 // cdna_hip_programming.md §3) with the k index of step r = the key held in register r.
+#include <algorithm>
 #include <cstdlib>
 #include <mutex>
 
@@ -1683,7 +1684,12 @@ extern "C" size_t ot_attn_bwd_flags_workspace_size(int B, int H, int I, int K, i
                                                    int precision) {
   const int S = attn_bwd_kslices(B, H, I, K, head_dim, selected != 0, precision);
   const int slots = (flags & OT_ATTN_DQKV_BF16) ? S : S - 1;
-  return ot_attn_bwd_workspace_size(B, H, K) + (size_t)slots * B * K * H * head_dim * sizeof(float);
+  const size_t n = ot_attn_bwd_workspace_size(B, H, K) + (size_t)slots * B * K * H * head_dim * sizeof(float);
+  // the slice backward's dS scratch (two workgroups per CU), when that kernel takes the shape
+  if (precision == OT_MATMUL_SPLIT_BF16 && flags == 0 && K > SMALL_K && !selected &&
+      attn_slice_bwd_supported(I, K, head_dim, false))
+    return std::max(n, attn_slice_bwd_ws_bytes(B, H, I, K, head_dim));
+  return n;
 }
 
 static int attn_bwd_impl(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
@@ -1739,7 +1745,7 @@ static int attn_bwd_impl(const float* qkv, int64_t ld, const float* out, const f
              1.f / sqrtf((float)head_dim), qpos};
   const int mm = prec;
   if (mm == OT_MATMUL_SPLIT_BF16 && flags == 0 && K > SMALL_K && attn_slice_bwd_supported(I, K, head_dim, qpos != nullptr))
-    return attn_slice_bwd(qkv, ld, out, dout, lse, B, H, I, K, head_dim, dqkv, (hipStream_t)stream);
+    return attn_slice_bwd(qkv, ld, out, dout, lse, B, H, I, K, head_dim, dqkv, delta_ws, ws_bytes, (hipStream_t)stream);
   // the f32 head_dim-32 backward over tail queries forms its own row statistics (no prep launch)
   const bool fdl = !qpos && head_dim == 32 && K > SMALL_K && attn_kpad(K) <= FDL_KP &&
                    mm != OT_MATMUL_BF16;

@@ -529,8 +529,13 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_slice_kernel(SliceArgs p
 // P is exp2(... + 14) (P' = P 2^14, in [0, 2^14]), phase 1's dS a per-key-block scale from the bound
 // |dS| <= (hd max|dO| max|V| + max|delta|) / sqrt(hd); phase 2's K image and dS one slice scale each (maxima
 // reduced through LDS at the phase-1 barrier).  Outputs are unscaled at their stores.
-template <int HD, int NWV, int NP, bool LAT_ = NWV == 4>
-__global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p) {
+// G2: two workgroups per CU instead of one — the dS store goes to a per-workgroup global scratch (p.dsws,
+// L2-resident) instead of LDS, so the LDS holds only the planes (75.7 KiB at hd 64); no cross-slice prefetch (its
+// 120 registers do not fit the 256 of two waves per SIMD; the other workgroup's compute covers a slice's loads), the
+// K image re-read from global (issued before the phase-1 barrier) instead of kept in registers, and phase 2's dS
+// reads issued two key-block pairs ahead.
+template <int HD, int NWV, int NP, bool LAT_ = NWV == 4, bool G2 = false>
+__global__ __launch_bounds__(64 * NWV, G2 ? 2 : 1) void attn_bwd_slice_kernel(SliceArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NT = HD / 32, NM = HD / 16, CPR = HD / 8, NTH = 64 * NWV;
   constexpr int RM = RMAX<HD>(), PB = RM * HD * 2;
@@ -549,7 +554,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
   int* qps = reinterpret_cast<int*>(dlt + RM);
   int* tab = qps + RM;                             // [16] first visible query block, [16] dS-store base per key block
   float* red = reinterpret_cast<float*>(tab + 32);   // NP = 2: per-wave maxima [3][8] (staging), [2][8] (phase 1)
-  char* dss = reinterpret_cast<char*>(red + 32);
+  char* dss = G2 ? reinterpret_cast<char*>(p.dsws + (size_t)blockIdx.x * p.ds_floats) : reinterpret_cast<char*>(red + 32);
   const float c1 = p.scale * L2E;
   if (threadIdx.x < 16) {
     tab[threadIdx.x] = p.qf[threadIdx.x];
@@ -604,10 +609,11 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
     lsev = p.lse_in[(int64_t)s * K + min((int)threadIdx.x, K - 1)];
   };
   int s = blockIdx.x;
-  if (s < nslices) prefetch(s);
+  if (!G2 && s < nslices) prefetch(s);
 #pragma unroll 1
   for (int it = 0; s < nslices; s += gridDim.x, ++it) {
     SLICE_STAMP(1, it, 0);
+    if (G2) prefetch(s);                           // (G2: this slice's Q / dO / O rows, no cross-slice prefetch)
     // the first key block's K / V: issued here, not with the slice prefetch — loaded during phase 2, the
     // compiler parked them in AGPRs and drained every load (vmcnt(0)) to copy them out before phase 2.  Here
     // they stay in flight through the staging (which waits only for the older Q / dO / O loads)
@@ -680,8 +686,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
     constexpr int KEEP = keep_slots(HD, NWV);
     // the owned key blocks' K planes (NP = 3) or K rows (NP = 2: split at the slice scale after phase 1), for the
     // phase-2 K image
-    u32x4 keep[NP == 3 ? KEEP : 1][NT][3];
-    float keepf[NP == 2 ? KEEP : 1][NT][8];
+    u32x4 keep[NP == 3 && !G2 ? KEEP : 1][NT][3];
+    float keepf[NP == 2 && !G2 ? KEEP : 1][NT][8];      // (G2: the K image is re-read from global, L2-warm)
     float mkw = 0.f, mdsw = 0.f;                   // NP = 2: this wave's max |K| and max |dS| (phase 2's scales)
 #pragma unroll 1
     for (int slot = 0, kb = kb0; kb >= 0; ++slot) {
@@ -715,7 +721,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
         splitN<NP>(vr[t], sv, vp[t]);
       }
 #pragma unroll
-      for (int k2 = 0; k2 < KEEP; ++k2)              // uniform branch, static register index
+      for (int k2 = 0; k2 < (G2 ? 0 : KEEP); ++k2)   // uniform branch, static register index
         if (slot == k2) {
 #pragma unroll
           for (int t = 0; t < NT; ++t) {
@@ -833,6 +839,16 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
     // K image for phase 2, in the Q planes' space: each key-block owner stores the K planes it kept (rows past
     // I hold row I - 1, times dS = 0) — no re-read or re-split of K
     SLICE_STAMP(1, it, 2);
+    // G2: the K rows for the phase-2 image, issued before the barrier (in flight while the other waves finish)
+    constexpr int SRK = (RM * CPR + NTH - 1) / NTH;
+    float kim[G2 ? SRK : 1][8];
+    if constexpr (G2) {
+#pragma unroll
+      for (int r = 0; r < SRK; ++r) {
+        const int task = threadIdx.x + r * NTH, j = min(task / CPR, I - 1), c = task % CPR;
+        load8(kim[r], Kg + (int64_t)j * p.ld + 8 * c);
+      }
+    }
     if constexpr (NP == 2) {
       mdsw = wave_maxf(mdsw);
       if (lane == 0) {                             // (the staging maxima were read before phase 1)
@@ -853,8 +869,15 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
       sks = pow2scale(mk);
       sdss = pow2scale(md);
     }
+    if constexpr (G2) {                            // the whole workgroup: K rows -> the image at the slice scale
 #pragma unroll
-    for (int k2 = 0; k2 < KEEP; ++k2) {
+      for (int r = 0; r < SRK; ++r) {
+        const int task = threadIdx.x + r * NTH, j = task / CPR, c = task % CPR;
+        if (task < IP * CPR) store_planesN<NP>(qimg, PB, poff<HD>(j, c), kim[r], sks);
+      }
+    }
+#pragma unroll
+    for (int k2 = 0; k2 < (G2 ? 0 : KEEP); ++k2) {
       const int kb = sched_item(srow1, k2);
       if (kb >= 0) {
 #pragma unroll
@@ -879,7 +902,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
     // measured the same, streamed a piece per phase-1 / phase-2 step slower (the waits for the next key block's
     // K / V then drain them too)
     constexpr bool EARLY = HD == 64;
-    if (EARLY && s + (int)gridDim.x < nslices) prefetch(s + gridDim.x);
+    if (!G2 && EARLY && s + (int)gridDim.x < nslices) prefetch(s + gridDim.x);
 
     // ---- phase 2: query-block owners, dQ^T = K^T dS^T
 #pragma unroll 1
@@ -896,12 +919,14 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
       f32x4 dq2[NM];
 #pragma unroll
       for (int m = 0; m < NM; ++m) dq2[m] = f32x4{0.f, 0.f, 0.f, 0.f};
-      auto step = [&](int k2, f32x4 (&acc)[NM]) {
+      auto ldds = [&](int k2, f32x4& x0, f32x4& x1) {
+        x0 = *reinterpret_cast<const f32x4*>(dss + 1024 * (tab[16 + k2] + qb - tab[k2]) + dsr);
+        x1 = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (k2 + 1 <= kbl) x1 = *reinterpret_cast<const f32x4*>(dss + 1024 * (tab[17 + k2] + qb - tab[k2 + 1]) + dsr);
+      };
+      auto stepx = [&](int k2, f32x4 x0, f32x4 x1, f32x4 (&acc)[NM]) {
         const bool two = k2 + 1 <= kbl;
         float v[8];
-        const f32x4 x0 = *reinterpret_cast<const f32x4*>(dss + 1024 * (tab[16 + k2] + qb - tab[k2]) + dsr);
-        f32x4 x1 = {0.f, 0.f, 0.f, 0.f};
-        if (two) x1 = *reinterpret_cast<const f32x4*>(dss + 1024 * (tab[17 + k2] + qb - tab[k2 + 1]) + dsr);
         const int ra = 16 * RBY * k2, rb = two ? ra + 16 * RBY : ra;
         u32x4 fa[2][NP];
         tr_atN<NP>(fa[0], smem + ra + tbase[0], smem + rb + tbase[0], PB);   // in flight during the split
@@ -916,10 +941,32 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
           if (LAT) __builtin_amdgcn_sched_barrier(0);
         }
       };
+      if constexpr (G2) {                          // global dS: each pair's reads issued two pairs ahead
+        f32x4 xa0, xa1, xb0, xb1;
+        ldds(0, xa0, xa1);
+        if (2 <= kbl) ldds(2, xb0, xb1);
 #pragma unroll 1
-      for (int k2 = 0; k2 <= kbl; k2 += 4) {
-        step(k2, dq);
-        if (k2 + 2 <= kbl) step(k2 + 2, dq2);
+        for (int k2 = 0; k2 <= kbl; k2 += 4) {
+          const f32x4 c0 = xa0, c1 = xa1;
+          if (k2 + 4 <= kbl) ldds(k2 + 4, xa0, xa1);
+          stepx(k2, c0, c1, dq);
+          if (k2 + 2 <= kbl) {
+            const f32x4 d0 = xb0, d1 = xb1;
+            if (k2 + 6 <= kbl) ldds(k2 + 6, xb0, xb1);
+            stepx(k2 + 2, d0, d1, dq2);
+          }
+        }
+      } else {
+#pragma unroll 1
+        for (int k2 = 0; k2 <= kbl; k2 += 4) {
+          f32x4 x0, x1;
+          ldds(k2, x0, x1);
+          stepx(k2, x0, x1, dq);
+          if (k2 + 2 <= kbl) {
+            ldds(k2 + 2, x0, x1);
+            stepx(k2 + 2, x0, x1, dq2);
+          }
+        }
       }
       const float uq = NP == 2 ? 1.f / (sks * sdss) : 1.f;
 #pragma unroll
@@ -932,7 +979,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bwd_slice_kernel(SliceArgs p
       }
     }
     SLICE_STAMP(1, it, 5);
-    if (!EARLY && s + (int)gridDim.x < nslices) prefetch(s + gridDim.x);
+    if (!G2 && !EARLY && s + (int)gridDim.x < nslices) prefetch(s + gridDim.x);
     __syncthreads();                               // LDS is restaged next slice
     SLICE_STAMP(1, it, 6);
   }
@@ -949,8 +996,22 @@ int bwd_pairs(int I, int K) {
   return n;
 }
 
-size_t bwd_lds(int I, int K, int hd, int np = 3) {
-  return (size_t)4 * np * rmax(hd) * hd + 12 * (size_t)rmax(hd) + 128 + 128 + 1024 * (size_t)bwd_pairs(I, K);
+size_t bwd_lds(int I, int K, int hd, int np = 3, bool g2 = false) {
+  return (size_t)4 * np * rmax(hd) * hd + 12 * (size_t)rmax(hd) + 128 + 128 + (g2 ? 0 : 1024 * (size_t)bwd_pairs(I, K));
+}
+
+static int device_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        n > 0)
+      cus = n;
+    else
+      cus = 256;
+    (void)hipGetLastError();
+  }
+  return cus;
 }
 
 // persistent grid: the workgroups that are co-resident (occupancy query, cached per kernel and LDS size),
@@ -1086,24 +1147,46 @@ int attn_slice_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, con
   return OT_OK;
 }
 
+// two workgroups per CU (global dS scratch) at head_dim 64.  Measured at B 4096 H 4 I 140 (round 5): hd 64 1,523 ->
+// 1,385 us (with the K image's loads issued before the phase-1 barrier; the fenced one-item-ahead fragment reads
+// (LAT) cost 40-60 us at two waves per SIMD; half a slice of start skew between the two workgroups changed nothing);
+// hd 32 as two workgroups of 4 waves 868-879 us against 816-821 for one of 8 (kept)
+constexpr bool bwd_g2(int hd) { return hd == 64; }
+
+size_t attn_slice_bwd_ws_bytes(int B, int H, int I, int K, int head_dim) {
+  using namespace slice;
+  if (!bwd_g2(head_dim)) return 0;
+  const int64_t grid = std::min<int64_t>((int64_t)B * H, 2 * (int64_t)device_cus());
+  return (size_t)grid * 1024 * bwd_pairs(I, K);
+}
+
 int attn_slice_bwd(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse, int B, int H,
-                   int I, int K, int head_dim, float* dqkv, hipStream_t stream) {
+                   int I, int K, int head_dim, float* dqkv, float* ws, size_t ws_bytes, hipStream_t stream) {
   using namespace slice;
   using KF = void (*)(SliceArgs);
   static const KF k32 = attn_bwd_slice_kernel<32, BWD_WAVES32, BWD_PLANES>,
-                  k64 = attn_bwd_slice_kernel<64, BWD_WAVES64, BWD_PLANES>;
+                  k64 = attn_bwd_slice_kernel<64, BWD_WAVES64, BWD_PLANES>,
+                  k64g = attn_bwd_slice_kernel<64, BWD_WAVES64, BWD_PLANES, false, true>;
   static std::once_flag once;
   std::call_once(once, [] {
-    for (KF k : {k32, k64}) raise_lds_limit(k);
+    for (KF k : {k32, k64, k64g}) raise_lds_limit(k);
     (void)hipGetLastError();
   });
   SliceArgs p{qkv, ld, H * head_dim, out, dout, lse, nullptr, nullptr, dqkv, B, H, I, K,
               1.f / sqrtf((float)head_dim), nullptr};
-  const size_t lds = bwd_lds(I, K, head_dim, BWD_PLANES);
+  const size_t per_wg = (size_t)1024 * bwd_pairs(I, K);
+  const bool g2 = bwd_g2(head_dim) && ws && ws_bytes >= per_wg;
   const int nw = head_dim == 32 ? BWD_WAVES32 : BWD_WAVES64;
   OT_REQUIRE(make_schedule(p, head_dim, nw), "ot_attn_bwd(slice): schedule");
-  const KF k = head_dim == 32 ? k32 : k64;
-  const dim3 grid(persistent_grid((const void*)k, 64 * nw, lds, (int64_t)B * H)), block(64 * nw);
+  const KF k = head_dim == 32 ? k32 : g2 ? k64g : k64;
+  const size_t lds = bwd_lds(I, K, head_dim, BWD_PLANES, g2);
+  unsigned g = persistent_grid((const void*)k, 64 * nw, lds, (int64_t)B * H);
+  if (g2) {
+    g = (unsigned)std::min<size_t>(g, ws_bytes / per_wg);      // each workgroup owns per_wg bytes of scratch
+    p.dsws = ws;
+    p.ds_floats = (int)(per_wg / sizeof(float));
+  }
+  const dim3 grid(g), block(64 * nw);
   hipLaunchKernelGGL(k, grid, block, lds, stream, p);
   OT_LAUNCH_CHECK("ot_attn_bwd(slice)");
   return OT_OK;

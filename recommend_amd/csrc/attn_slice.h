@@ -20,13 +20,17 @@ struct SliceArgs {
   alignas(8) int8_t sched[3][8][8];            // rows read as one uint64 each (slot s = byte s)
   int8_t qf[16];                              // backward: first query block that sees key block kb
   int16_t bbase[16];                          // backward: dS-store block index of (qf[kb], kb)
+  float* dsws; int ds_floats;                 // backward, two workgroups per CU: per-workgroup dS scratch
 };
 
 bool attn_slice_fwd_supported(int I, int K, int head_dim);
 bool attn_slice_bwd_supported(int I, int K, int head_dim, bool selected);
 int attn_slice_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos, int head_dim,
                    float* out, float* lse, hipStream_t stream);
+// ws / ws_bytes: scratch for the two-workgroups-per-CU backward (attn_slice_bwd_ws_bytes for the full grid; less
+// shrinks its grid; below one workgroup's share the one-workgroup-per-CU kernel runs)
 int attn_slice_bwd(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse, int B, int H,
-                   int I, int K, int head_dim, float* dqkv, hipStream_t stream);
+                   int I, int K, int head_dim, float* dqkv, float* ws, size_t ws_bytes, hipStream_t stream);
+size_t attn_slice_bwd_ws_bytes(int B, int H, int I, int K, int head_dim);
 
 }  // namespace ot

@@ -152,8 +152,10 @@ def test_mixed_gemm_prologue_epilogue(dev, matmul):
     torch.testing.assert_close(C2.double().cpu(), ref2, rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize('shared', [False, True])
 @pytest.mark.parametrize('xf', [OT_AX_NONE, OT_AX_RMSNORM, OT_AX_GELU])
-def test_wgrad(dev, matmul, xf):
+def test_wgrad(dev, matmul, xf, shared):
+    """shared: one row map for A and D (the model's calls) or two maps with the same rows"""
     rng = np.random.default_rng(2)
     G, M, K_, N = 3, 1500, 128, 192
     counts = [1000, 300, 200]
@@ -171,7 +173,7 @@ def test_wgrad(dev, matmul, xf):
     dd = rm.to(dev)
     dW = torch.full((G, K_, N), float('nan'), device=dev)
     db = torch.full((G, N), float('nan'), device=dev)
-    K.wgrad(A.float().to(dev), K_, dd['rows'][0], D.float().to(dev), N, dd['rows'][1], K_, N, dd,
+    K.wgrad(A.float().to(dev), K_, dd['rows'][0], D.float().to(dev), N, dd['rows'][0 if shared else 1], K_, N, dd,
             rm.chunks.shape[0], G, dW, K_ * N, db, N, a_xform=xf, rstd=rstd.float().to(dev),
             gamma=gamma.float().to(dev), device=dev)
     Ax = A * rstd[:, None] * gamma if xf == OT_AX_RMSNORM else (gelu64(A) if xf == OT_AX_GELU else A)

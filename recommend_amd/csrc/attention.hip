@@ -1431,6 +1431,87 @@ __global__ __launch_bounds__(256) void attn_bwd_small_kernel(AttnArgs p) {
   }
 }
 
+// Forward for a short query tail (K <= SMALL_K: the last layer's single query after DCE), the f32-accurate modes.
+// HBM-bound (each K / V row read once; 2 K hd flops per row), so plain f32 FMAs on the VALU: the slice kernel's
+// MFMA tiles would be 1/16 occupied and it would split all I K / V rows into planes for one query (as slow as a
+// full layer).  One wave per (sample, head); HD/4 lanes per key (one float4 of dims each), 64/(HD/4) key slots
+// per pass, each slot with its own online softmax (running max m, sum l, output o; scores in log2 units) over the
+// keys it sees; the slots' states are merged at the end with xor shuffles (max, then rescaled sums).  Exact f32
+// products — no split.
+template <int HD>
+__global__ __launch_bounds__(256) void attn_fwd_small_kernel(AttnArgs p) {
+  constexpr int LPK = HD / 4, KPW = 64 / LPK;
+  const int lane = threadIdx.x & 63, sub = lane % LPK, slot = lane / LPK;
+  const int pair = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (pair >= p.B * p.H) return;
+  const int b = pair / p.H, h = pair % p.H;
+  const int I = p.I, K = p.K, q_off = I - K;
+  const int64_t tok0 = (int64_t)b * I;
+  const float* Q = p.qkv + tok0 * p.ld + h * HD + 4 * sub;
+  const float* Kp = Q + p.d;
+  const float* V = Q + 2 * p.d;
+  const int32_t* qp = p.qpos ? p.qpos + (int64_t)b * K : nullptr;
+  const float c = p.scale * 1.4426950408889634f;      // scores in log2 units
+  f32x4 q[SMALL_K], o[SMALL_K];
+  float m[SMALL_K], l[SMALL_K];
+  int qpos[SMALL_K];
+#pragma unroll
+  for (int j = 0; j < SMALL_K; ++j) {
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    q[j] = z; o[j] = z; m[j] = -INFINITY; l[j] = 0.f; qpos[j] = -1;
+    if (j < K) {
+      qpos[j] = query_pos(qp, q_off, j);
+      q[j] = *reinterpret_cast<const f32x4*>(Q + (int64_t)qpos[j] * p.ld) * c;
+    }
+  }
+  int last = 0;                                        // keys past every query's position are never visible
+#pragma unroll
+  for (int j = 0; j < SMALL_K; ++j)
+    if (j < K) last = max(last, qpos[j]);
+  for (int key0 = 0; key0 <= last; key0 += KPW) {
+    const int key = key0 + slot;
+    const bool live = key <= last;
+    const int64_t ro = (int64_t)(live ? key : 0) * p.ld;
+    const f32x4 kv = *reinterpret_cast<const f32x4*>(Kp + ro);
+    const f32x4 vv = *reinterpret_cast<const f32x4*>(V + ro);
+#pragma unroll
+    for (int j = 0; j < SMALL_K; ++j) {
+      if (j >= K) break;
+      float s = q[j].x * kv.x + q[j].y * kv.y + q[j].z * kv.z + q[j].w * kv.w;
+#pragma unroll
+      for (int off = 1; off < LPK; off <<= 1) s += __shfl_xor(s, off, 64);
+      if (live && key <= qpos[j]) {                   // (uniform over the key's lanes)
+        const float mn = fmaxf(m[j], s);
+        const float corr = __builtin_amdgcn_exp2f(m[j] - mn), e = __builtin_amdgcn_exp2f(s - mn);
+        l[j] = l[j] * corr + e;
+        o[j] = o[j] * corr + e * vv;
+        m[j] = mn;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < SMALL_K; ++j) {
+    if (j >= K) break;
+    // merge the key slots (lanes sub + LPK * slot): max of m, then the rescaled l and o summed
+    float mx = m[j];
+#pragma unroll
+    for (int off = LPK; off < 64; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+    const float corr = m[j] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m[j] - mx);
+    float lt = l[j] * corr;
+    f32x4 v = o[j] * corr;
+#pragma unroll
+    for (int off = LPK; off < 64; off <<= 1) {
+      lt += __shfl_xor(lt, off, 64);
+      v.x += __shfl_xor(v.x, off, 64); v.y += __shfl_xor(v.y, off, 64);
+      v.z += __shfl_xor(v.z, off, 64); v.w += __shfl_xor(v.w, off, 64);
+    }
+    if (slot == 0) {
+      *reinterpret_cast<f32x4*>(p.out + ((int64_t)b * K + j) * p.d + h * HD + 4 * sub) = v * (1.f / lt);
+      if (sub == 0) p.lse[(int64_t)pair * K + j] = mx * 0.6931471805599453f + __logf(lt);
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // Serving (paper §3.5.1 two-stage KV cache; the reference's broken cache path model.py:94-98,
 // 359-381): candidate c of request req[c] attends with its last Kq N-side queries over the request's
@@ -1600,6 +1681,13 @@ extern "C" int ot_attn_fwd(const float* qkv, int64_t ld, int B, int H, int I, in
   const size_t kv_bytes = 2 * (size_t)((I + 31) / 32 * 32) * (head_dim + 4) * sizeof(float);
   const bool kv_fits = head_dim <= 64 && kv_bytes <= OT_ATTN_KV_LDS_MAX && (K + 31) / 32 >= 3;
   const int mm = precision;
+  if (mm != OT_MATMUL_BF16 && K <= SMALL_K && (head_dim == 32 || head_dim == 64 || head_dim == 128)) {
+    // a short query tail (the last layer's one query): f32 VALU, HBM-bound
+    OT_ATTN_DISPATCH(attn_fwd_small_kernel, head_dim, dim3(ceil_div((int64_t)B * H, 4)), dim3(256), 0,
+                     (hipStream_t)stream, p);
+    OT_LAUNCH_CHECK("ot_attn_fwd(small)");
+    return OT_OK;
+  }
   if (mm == OT_MATMUL_SPLIT_BF16 && attn_slice_fwd_supported(I, K, head_dim)) {
     // short sequence, f32-accurate: one workgroup per (sample, head) slice on split-bf16 MFMA
     return attn_slice_fwd(qkv, ld, B, H, I, K, qpos, head_dim, out, lse, (hipStream_t)stream);

@@ -1377,12 +1377,19 @@ __global__ __launch_bounds__(256) void attn_bwd_small_kernel(AttnArgs p) {
       delta[j] = p.delta[((int64_t)p.B * p.H + pair) * attn_kpad(K) + j];
     }
   }
+  // each pass's K / V rows are loaded one pass ahead (two loads per lane in flight during a pass's math)
+  f32x4 kvn = *reinterpret_cast<const f32x4*>(Kp + (int64_t)min(slot, I - 1) * p.ld);
+  f32x4 vvn = *reinterpret_cast<const f32x4*>(V + (int64_t)min(slot, I - 1) * p.ld);
   for (int key0 = 0; key0 < I; key0 += KPW) {
     const int key = key0 + slot;
     const bool live = key < I;
     const int64_t ro = (int64_t)(live ? key : 0) * p.ld;
-    const f32x4 kv = *reinterpret_cast<const f32x4*>(Kp + ro);
-    const f32x4 vv = *reinterpret_cast<const f32x4*>(V + ro);
+    const f32x4 kv = kvn, vv = vvn;
+    if (key0 + KPW < I) {
+      const int64_t rn = (int64_t)min(key + KPW, I - 1) * p.ld;
+      kvn = *reinterpret_cast<const f32x4*>(Kp + rn);
+      vvn = *reinterpret_cast<const f32x4*>(V + rn);
+    }
     f32x4 dk = {0.f, 0.f, 0.f, 0.f}, dv = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < SMALL_K; ++j) {
@@ -1468,12 +1475,17 @@ __global__ __launch_bounds__(256) void attn_fwd_small_kernel(AttnArgs p) {
 #pragma unroll
   for (int j = 0; j < SMALL_K; ++j)
     if (j < K) last = max(last, qpos[j]);
+  f32x4 kvn = *reinterpret_cast<const f32x4*>(Kp + (int64_t)min(slot, last) * p.ld);   // one pass ahead
+  f32x4 vvn = *reinterpret_cast<const f32x4*>(V + (int64_t)min(slot, last) * p.ld);
   for (int key0 = 0; key0 <= last; key0 += KPW) {
     const int key = key0 + slot;
     const bool live = key <= last;
-    const int64_t ro = (int64_t)(live ? key : 0) * p.ld;
-    const f32x4 kv = *reinterpret_cast<const f32x4*>(Kp + ro);
-    const f32x4 vv = *reinterpret_cast<const f32x4*>(V + ro);
+    const f32x4 kv = kvn, vv = vvn;
+    if (key0 + KPW <= last) {
+      const int64_t rn = (int64_t)min(key + KPW, last) * p.ld;
+      kvn = *reinterpret_cast<const f32x4*>(Kp + rn);
+      vvn = *reinterpret_cast<const f32x4*>(V + rn);
+    }
 #pragma unroll
     for (int j = 0; j < SMALL_K; ++j) {
       if (j >= K) break;

@@ -279,12 +279,12 @@ __device__ unsigned long long g_slice_stamps[2][2048][2][8];
 #define SLICE_STAMP(kind, it, k) do {} while (0)
 #endif
 
-// The backward and the head_dim-64 forward are persistent: a workgroup walks slices s = blockIdx.x,
-// + gridDim.x, ... (grid = the co-resident workgroups), and the next slice's operands are loaded into
-// registers while the current slice computes — at one workgroup per CU (LDS) a non-persistent grid leaves
-// each CU loading, then computing.  The head_dim-32 forward fits two workgroups per CU at 128 VGPRs and runs
-// one slice per workgroup.  MFMA busy is ~20% in both directions at the T shape
-// (profiles/r04/pmc_attn_slice_T.txt): the issue stream (splits, softmax, addressing) sets the time.
+// The backward is persistent: a workgroup walks slices s = blockIdx.x, + gridDim.x, ... (grid = the co-resident
+// workgroups); at head_dim 32 (one workgroup per CU by LDS) the next slice's operands are loaded into registers
+// while the current slice computes, at head_dim 64 two workgroups per CU cover each other's loads.  The forward
+// runs one slice per workgroup, two workgroups of 8 waves per CU (<= 128 VGPRs, <= 74 KiB of LDS): the other
+// workgroup covers a slice's K / V loads.  (Round 5: the head_dim-64 forward as a persistent workgroup per CU
+// with the next slice's K / V prefetched, 243 VGPRs, measured 574-631 us against 497-507 at B 4096 H 4 I 140.)
 
 // ------------------------------------------------------------------------------------------
 // Forward.  The slice's K and V planes are staged in LDS ([RMAX][HD] x 3 each); each wave takes whole
@@ -292,14 +292,11 @@ __device__ unsigned long long g_slice_stamps[2][2048][2][8];
 // (pre-scaled by log2(e)/sqrt(hd), split) as the B operand of S^T = K Q^T (query on the lane) and
 // computes S^T for every visible key block at once (<= 12 x 4 registers), so the softmax is exact in one
 // pass (row max and sum over the 4 lane groups by shuffles, no rescaling); O^T = V^T P^T takes P^T from
-// the S^T registers and V^T by transposed reads.  Loads in flight during compute: the next slice's K / V
-// rows (all of them), the next query block's Q (the next slice's first one during the last block).
-// PF: persistent with the next slice's K / V prefetched (hd 64: one workgroup per CU by LDS anyway); without
-// it one workgroup per slice and fewer registers, so more waves per SIMD (hd 32: 4 instead of 2, faster).
+// the S^T registers and V^T by transposed reads.  Loads in flight during compute: the next query block's Q.
 // NP planes per operand: 3 = the exact bf16 split (6 products), 2 = the scaled fp16 pair (3 products, splitN): K and V
 // each get a power-of-two scale per slice (the largest magnitude, reduced over the workgroup), Q one per query (lane)
-template <int HD, int NWV, bool SEL, bool PF, int NP>
-__global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_slice_kernel(SliceArgs p) {
+template <int HD, int NWV, bool SEL, int NP>
+__global__ __launch_bounds__(64 * NWV, 2) void attn_fwd_slice_kernel(SliceArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NT = HD / 32, NM = HD / 16, CPR = HD / 8, NTH = 64 * NWV;
   constexpr int PB = RMAX<HD>() * HD * 2;
@@ -350,13 +347,12 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_slice_kernel(SliceArgs p
     vtbase[m] = poff<HD>(4 * g + ((lane >> 2) & 3), 2 * m + ((lane & 3) >> 1)) + 8 * (lane & 1) + NP * PB;
     asm volatile("" : "+v"(vtbase[m]));
   }
-  int s = blockIdx.x;
-  if (s < nslices) {
-    load_kv(s);
-    if (!SEL && idx0 >= 0) load_q(s, idx0);
-  }
-#pragma unroll 1
-  for (int it = 0; s < nslices; s += gridDim.x, ++it) {
+  const int s = blockIdx.x;
+  if (s >= nslices) return;
+  load_kv(s);
+  if (!SEL && idx0 >= 0) load_q(s, idx0);
+  {
+    constexpr int it = 0;
     SLICE_STAMP(0, it, 0);
     float sk = 1.f, sv = 1.f;                                        // K / V scales (NP = 2)
     if constexpr (NP == 2) {
@@ -400,9 +396,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_slice_kernel(SliceArgs p
       for (int j = threadIdx.x; j < K; j += NTH) qposl[j] = p.qpos[(int64_t)(s / p.H) * K + j];
     __syncthreads();
     SLICE_STAMP(0, it, 1);
-    if (SEL && idx0 >= 0) load_q(s, idx0);                           // (positions of the next slice unknown yet)
-    const int sn = s + gridDim.x;
-    if (PF && sn < nslices) load_kv(sn);                             // next slice's K / V, in flight meanwhile
+    if (SEL && idx0 >= 0) load_q(s, idx0);
     const int b = s / p.H, h = s % p.H;
 #pragma unroll 1
     for (int slot = 0, idx = idx0; idx >= 0; ++slot) {
@@ -433,7 +427,6 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_slice_kernel(SliceArgs p
       }
       const int idxn = sched_item(srow, slot + 1);
       if (idxn >= 0) load_q(s, idxn);                                // next block's Q, in flight meanwhile
-      else if (PF && !SEL && sn < nslices && idx0 >= 0) load_q(sn, idx0);
       f32x4 sc[MAXKB];
       float mx = -INFINITY;
 #pragma unroll
@@ -502,9 +495,6 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_slice_kernel(SliceArgs p
       idx = idxn;
     }
     SLICE_STAMP(0, it, 2);
-    if constexpr (!PF) break;                                        // one slice per workgroup
-    __syncthreads();                                                 // the planes are rewritten next slice
-    SLICE_STAMP(0, it, 3);
   }
 }
 
@@ -1126,8 +1116,8 @@ int attn_slice_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, con
   using KF = void (*)(SliceArgs);
   constexpr int P32 = fwd_planes(32), P64 = fwd_planes(64);
   static const KF table[2][2] = {
-      {attn_fwd_slice_kernel<32, FWD_WAVES, false, false, P32>, attn_fwd_slice_kernel<32, FWD_WAVES, true, false, P32>},
-      {attn_fwd_slice_kernel<64, FWD_WAVES, false, true, P64>, attn_fwd_slice_kernel<64, FWD_WAVES, true, true, P64>}};
+      {attn_fwd_slice_kernel<32, FWD_WAVES, false, P32>, attn_fwd_slice_kernel<32, FWD_WAVES, true, P32>},
+      {attn_fwd_slice_kernel<64, FWD_WAVES, false, P64>, attn_fwd_slice_kernel<64, FWD_WAVES, true, P64>}};
   static std::once_flag once;
   std::call_once(once, [] {
     for (int a = 0; a < 2; ++a)
@@ -1141,7 +1131,7 @@ int attn_slice_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, con
   OT_REQUIRE(make_schedule(p, head_dim, nw), "ot_attn_fwd(slice): schedule");
   const KF k = table[head_dim == 64][qpos != nullptr];
   const unsigned slices = (unsigned)((int64_t)B * H);
-  const dim3 grid(head_dim == 64 ? persistent_grid((const void*)k, 64 * nw, lds, slices) : slices), block(64 * nw);
+  const dim3 grid(slices), block(64 * nw);
   hipLaunchKernelGGL(k, grid, block, lds, stream, p);
   OT_LAUNCH_CHECK("ot_attn_fwd(slice)");
   return OT_OK;

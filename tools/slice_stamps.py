@@ -18,7 +18,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from recommend_amd import _lib, kernels as K
 
-FWD = ['stage K/V planes + barrier', 'query blocks (wave 0)', 'end barrier']
+FWD = ['stage K/V planes + barrier', 'query blocks (wave 0)']
 BWD = ['stage Q/dO planes + barrier', 'phase 1 (wave 0)', 'phase-1 barrier', 'K image + barrier', 'phase 2 (wave 0)',
        'end barrier']
 
@@ -46,7 +46,7 @@ def main():
         for kind, names in ((0, FWD), (1, BWD)):
             a = st[kind].astype(np.float64)
             used = a[:, 0, 0] > 0
-            for it in (0, 1):
+            for it in ((0,) if kind == 0 else (0, 1)):      # the forward runs one slice per workgroup
                 x = a[used, it, :len(names) + 1]
                 ok = np.all(x > 0, axis=1)
                 dx = np.diff(x[ok], axis=1)

@@ -21,16 +21,21 @@ namespace ot {
 // f32x4 -> three planes of 4 bf16 (each packed into 2 dwords, element 0 in the low half):
 // x = x0 + x1 + x2 exactly (x0 the top 8 significant bits, x1 the next 8, x2 the rest; truncation
 // keeps every step exact)
+// The subtractions run on packed-f32 adds (v_pk_add_f32, two elements each) and the planes are the high halves
+// of x, r1, r2 (v_perm): the masked values are needed only as the subtrahends.
 __device__ __forceinline__ void split3(f32x4 v, u32x2& p0, u32x2& p1, u32x2& p2) {
+  typedef float f32x2_ __attribute__((ext_vector_type(2)));
   uint32_t a[4], b[4], c[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float x = v[j];
-    const uint32_t u0 = __float_as_uint(x) & 0xffff0000u;
-    const float r1 = x - __uint_as_float(u0);
-    const uint32_t u1 = __float_as_uint(r1) & 0xffff0000u;
-    const float r2 = r1 - __uint_as_float(u1);
-    a[j] = u0; b[j] = u1; c[j] = __float_as_uint(r2);
+  for (int k = 0; k < 2; ++k) {
+    const f32x2_ x = {v[2 * k], v[2 * k + 1]};
+    const f32x2_ x0 = {__uint_as_float(__float_as_uint(x.x) & 0xffff0000u), __uint_as_float(__float_as_uint(x.y) & 0xffff0000u)};
+    const f32x2_ r1 = x - x0;
+    const f32x2_ x1 = {__uint_as_float(__float_as_uint(r1.x) & 0xffff0000u), __uint_as_float(__float_as_uint(r1.y) & 0xffff0000u)};
+    const f32x2_ r2 = r1 - x1;
+    a[2 * k] = __float_as_uint(x.x); a[2 * k + 1] = __float_as_uint(x.y);
+    b[2 * k] = __float_as_uint(r1.x); b[2 * k + 1] = __float_as_uint(r1.y);
+    c[2 * k] = __float_as_uint(r2.x); c[2 * k + 1] = __float_as_uint(r2.y);
   }
   p0 = u32x2{__builtin_amdgcn_perm(a[1], a[0], 0x07060302u), __builtin_amdgcn_perm(a[3], a[2], 0x07060302u)};
   p1 = u32x2{__builtin_amdgcn_perm(b[1], b[0], 0x07060302u), __builtin_amdgcn_perm(b[3], b[2], 0x07060302u)};

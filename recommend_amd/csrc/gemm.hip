@@ -1252,8 +1252,9 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(WgradArgs p) {
         } else if (ax == OT_AX_GELU) {
           a = gelu_erf4(a);
         }
-        if (!(inr[j] && k0 + 4 * cc < p.K)) a = zero4;
-        if (!(inr[j] && n0 + 4 * cc < p.N)) dv = zero4;
+        // only D is zeroed, for rows past the chunk or with a negative id: their A (row 0 of the map, clamped
+        // columns) is finite, so its products are 0; columns past K / N feed outputs that are never stored
+        if (!inr[j]) dv = zero4;
         if (do_bias) bsum[i] += dv;
         const int off = wsw_off(sr + WBR * j, cc >> 1) + 8 * (cc & 1);
         if constexpr (TERMS == 1) {

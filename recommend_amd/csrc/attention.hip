@@ -1347,7 +1347,9 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(AttnArgs p) {
 // reduced over the wave's key slots at the end.
 constexpr int SMALL_K = 4;
 
-template <int HD>
+// KQ: the largest K the instance takes (1: the last layer's one query — a quarter of the registers, so more waves
+// per SIMD keep more K / V rows in flight)
+template <int HD, int KQ = SMALL_K>
 __global__ __launch_bounds__(256) void attn_bwd_small_kernel(AttnArgs p) {
   constexpr int LPK = HD / 4, KPW = 64 / LPK;
   const int lane = threadIdx.x & 63, sub = lane % LPK, slot = lane / LPK;
@@ -1362,11 +1364,11 @@ __global__ __launch_bounds__(256) void attn_bwd_small_kernel(AttnArgs p) {
   float* dK = p.dqkv + tok0 * p.ld + p.d + h * HD + 4 * sub;
   float* dV = dK + p.d;
   const int32_t* qp = p.qpos ? p.qpos + (int64_t)b * K : nullptr;
-  f32x4 q[SMALL_K], o[SMALL_K], dq[SMALL_K];
-  float lse[SMALL_K], delta[SMALL_K];
-  int qpos[SMALL_K];
+  f32x4 q[KQ], o[KQ], dq[KQ];
+  float lse[KQ], delta[KQ];
+  int qpos[KQ];
 #pragma unroll
-  for (int j = 0; j < SMALL_K; ++j) {
+  for (int j = 0; j < KQ; ++j) {
     const f32x4 z = {0.f, 0.f, 0.f, 0.f};
     q[j] = z; o[j] = z; dq[j] = z; lse[j] = 0.f; delta[j] = 0.f; qpos[j] = -1;
     if (j < K) {
@@ -1392,7 +1394,7 @@ __global__ __launch_bounds__(256) void attn_bwd_small_kernel(AttnArgs p) {
     }
     f32x4 dk = {0.f, 0.f, 0.f, 0.f}, dv = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int j = 0; j < SMALL_K; ++j) {
+    for (int j = 0; j < KQ; ++j) {
       if (j >= K) break;
       float sdot = q[j].x * kv.x + q[j].y * kv.y + q[j].z * kv.z + q[j].w * kv.w;
       float pdot = o[j].x * vv.x + o[j].y * vv.y + o[j].z * vv.z + o[j].w * vv.w;
@@ -1420,7 +1422,7 @@ __global__ __launch_bounds__(256) void attn_bwd_small_kernel(AttnArgs p) {
     }
   }
 #pragma unroll
-  for (int j = 0; j < SMALL_K; ++j) {
+  for (int j = 0; j < KQ; ++j) {
     if (j >= K) break;
     f32x4 v = dq[j];
 #pragma unroll
@@ -1445,7 +1447,7 @@ __global__ __launch_bounds__(256) void attn_bwd_small_kernel(AttnArgs p) {
 // per pass, each slot with its own online softmax (running max m, sum l, output o; scores in log2 units) over the
 // keys it sees; the slots' states are merged at the end with xor shuffles (max, then rescaled sums).  Exact f32
 // products — no split.
-template <int HD>
+template <int HD, int KQ = SMALL_K>
 __global__ __launch_bounds__(256) void attn_fwd_small_kernel(AttnArgs p) {
   constexpr int LPK = HD / 4, KPW = 64 / LPK;
   const int lane = threadIdx.x & 63, sub = lane % LPK, slot = lane / LPK;
@@ -1459,11 +1461,11 @@ __global__ __launch_bounds__(256) void attn_fwd_small_kernel(AttnArgs p) {
   const float* V = Q + 2 * p.d;
   const int32_t* qp = p.qpos ? p.qpos + (int64_t)b * K : nullptr;
   const float c = p.scale * 1.4426950408889634f;      // scores in log2 units
-  f32x4 q[SMALL_K], o[SMALL_K];
-  float m[SMALL_K], l[SMALL_K];
-  int qpos[SMALL_K];
+  f32x4 q[KQ], o[KQ];
+  float m[KQ], l[KQ];
+  int qpos[KQ];
 #pragma unroll
-  for (int j = 0; j < SMALL_K; ++j) {
+  for (int j = 0; j < KQ; ++j) {
     const f32x4 z = {0.f, 0.f, 0.f, 0.f};
     q[j] = z; o[j] = z; m[j] = -INFINITY; l[j] = 0.f; qpos[j] = -1;
     if (j < K) {
@@ -1473,7 +1475,7 @@ __global__ __launch_bounds__(256) void attn_fwd_small_kernel(AttnArgs p) {
   }
   int last = 0;                                        // keys past every query's position are never visible
 #pragma unroll
-  for (int j = 0; j < SMALL_K; ++j)
+  for (int j = 0; j < KQ; ++j)
     if (j < K) last = max(last, qpos[j]);
   f32x4 kvn = *reinterpret_cast<const f32x4*>(Kp + (int64_t)min(slot, last) * p.ld);   // one pass ahead
   f32x4 vvn = *reinterpret_cast<const f32x4*>(V + (int64_t)min(slot, last) * p.ld);
@@ -1487,7 +1489,7 @@ __global__ __launch_bounds__(256) void attn_fwd_small_kernel(AttnArgs p) {
       vvn = *reinterpret_cast<const f32x4*>(V + rn);
     }
 #pragma unroll
-    for (int j = 0; j < SMALL_K; ++j) {
+    for (int j = 0; j < KQ; ++j) {
       if (j >= K) break;
       float s = q[j].x * kv.x + q[j].y * kv.y + q[j].z * kv.z + q[j].w * kv.w;
 #pragma unroll
@@ -1502,7 +1504,7 @@ __global__ __launch_bounds__(256) void attn_fwd_small_kernel(AttnArgs p) {
     }
   }
 #pragma unroll
-  for (int j = 0; j < SMALL_K; ++j) {
+  for (int j = 0; j < KQ; ++j) {
     if (j >= K) break;
     // merge the key slots (lanes sub + LPK * slot): max of m, then the rescaled l and o summed
     float mx = m[j];
@@ -1652,6 +1654,15 @@ __global__ __launch_bounds__(256) void attn_fwd_cached_kernel(AttnCachedArgs p) 
 
 using namespace ot;
 
+// (KERNEL<HD, 1>: the one-query instance of a short-tail kernel)
+#define OT_ATTN_DISPATCH_K1(KERNEL, HD_, ...)                                                \
+  switch (HD_) {                                                                             \
+    case 16: hipLaunchKernelGGL((KERNEL<16, 1>), __VA_ARGS__); break;                        \
+    case 32: hipLaunchKernelGGL((KERNEL<32, 1>), __VA_ARGS__); break;                        \
+    case 64: hipLaunchKernelGGL((KERNEL<64, 1>), __VA_ARGS__); break;                        \
+    case 128: hipLaunchKernelGGL((KERNEL<128, 1>), __VA_ARGS__); break;                      \
+    default: return fail(OT_ERR_UNSUPPORTED, "attention: head_dim %d unsupported", HD_);     \
+  }
 #define OT_ATTN_DISPATCH(KERNEL, HD_, ...)                                                   \
   switch (HD_) {                                                                             \
     case 16: hipLaunchKernelGGL(KERNEL<16>, __VA_ARGS__); break;                             \
@@ -1695,8 +1706,13 @@ extern "C" int ot_attn_fwd(const float* qkv, int64_t ld, int B, int H, int I, in
   const int mm = precision;
   if (mm != OT_MATMUL_BF16 && K <= SMALL_K && (head_dim == 32 || head_dim == 64 || head_dim == 128)) {
     // a short query tail (the last layer's one query): f32 VALU, HBM-bound
-    OT_ATTN_DISPATCH(attn_fwd_small_kernel, head_dim, dim3(ceil_div((int64_t)B * H, 4)), dim3(256), 0,
-                     (hipStream_t)stream, p);
+    if (K == 1) {
+      OT_ATTN_DISPATCH_K1(attn_fwd_small_kernel, head_dim, dim3(ceil_div((int64_t)B * H, 4)), dim3(256), 0,
+                       (hipStream_t)stream, p);
+    } else {
+      OT_ATTN_DISPATCH(attn_fwd_small_kernel, head_dim, dim3(ceil_div((int64_t)B * H, 4)), dim3(256), 0,
+                       (hipStream_t)stream, p);
+    }
     OT_LAUNCH_CHECK("ot_attn_fwd(small)");
     return OT_OK;
   }
@@ -1862,7 +1878,10 @@ static int attn_bwd_impl(const float* qkv, int64_t ld, const float* out, const f
                      (hipStream_t)stream, out, dout, lse, delta_ws, B, H, K, head_dim, main_blocks, pad_blocks, qpos);
   OT_LAUNCH_CHECK("ot_attn_bwd(prep)");
   p.dq_bf16 = (flags & OT_ATTN_DQKV_BF16) ? 1 : 0;
-  if (K <= SMALL_K) {
+  if (K == 1) {
+    OT_ATTN_DISPATCH_K1(attn_bwd_small_kernel, head_dim, dim3(ceil_div((int64_t)B * H, 4)), dim3(256), 0,
+                     (hipStream_t)stream, p);
+  } else if (K <= SMALL_K) {
     OT_ATTN_DISPATCH(attn_bwd_small_kernel, head_dim, dim3(ceil_div((int64_t)B * H, 4)), dim3(256), 0,
                      (hipStream_t)stream, p);
   } else if (mm == OT_MATMUL_BF16 && (head_dim == 32 || head_dim == 64) &&

@@ -567,9 +567,13 @@ __global__ __launch_bounds__(64 * NWV, G2 ? 2 : 1) void attn_bwd_slice_kernel(Sl
     otbase[m] = tbase[m] + NP * PB;
     asm volatile("" : "+v"(tbase[m]), "+v"(otbase[m]));
   }
+  // dS block rows permuted within each group of four (row r at 4 (r / 4) + (r + r / 4) % 4): the phase-1 stores
+  // of rows 4g + i (g = 0..3, one per 16-lane group) then fall in four different bank quarters (2 extra cycles
+  // per store instruction otherwise); the phase-2 row reads stay conflict-free (tools/lds_conflicts.py)
+  auto dsrow = [](int r) { return (r & ~3) | ((r + (r >> 2)) & 3); };
 #pragma unroll
-  for (int i = 0; i < 4; ++i) dsw[i] = poff<32>(4 * g + i, li >> 2) + 4 * (li & 3);
-  const int dsr = poff<32>(li, g);
+  for (int i = 0; i < 4; ++i) dsw[i] = poff<32>(dsrow(4 * g + i), li >> 2) + 4 * (li & 3);
+  const int dsr = poff<32>(dsrow(li), g);
   auto qkv_of = [&](int s) { return p.qkv + (int64_t)(s / p.H) * I * p.ld + (s % p.H) * HD; };
   auto row_of = [&](int s) { return (int64_t)(s / p.H) * K * p.d + (s % p.H) * HD; };   // O / dO slice
   // rows past K / I read the last valid row (finite) and are zeroed at use, so no load is predicated

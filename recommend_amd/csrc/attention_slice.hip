@@ -531,6 +531,7 @@ __global__ __launch_bounds__(64 * NWV, G2 ? 2 : 1) void attn_bwd_slice_kernel(Sl
   constexpr int RM = RMAX<HD>(), PB = RM * HD * 2;
   constexpr int SR = (RM * CPR + NTH - 1) / NTH;
   constexpr bool LAT = LAT_;                        // fragment reads one item ahead, fenced (one wave per SIMD)
+  static_assert(NTH >= RM, "attn_bwd_slice_kernel: the staging gives each padded query row one thread");
   constexpr int RBY = HD * 2;                       // bytes per plane image row
   const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform

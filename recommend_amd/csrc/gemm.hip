@@ -1254,8 +1254,10 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(WgradArgs p) {
         }
         // only D is zeroed, for rows past the chunk or with a negative id: their A (row 0 of the map, clamped
         // columns) is finite, so its products are 0; columns past K / N feed outputs that are never stored
-        if (!inr[j]) dv = zero4;
-        if (do_bias) bsum[i] += dv;
+        // (a 0 / 1 row factor: two packed multiplies instead of four selects; the row is finite)
+        dv = dv * (inr[j] ? 1.f : 0.f);
+        bsum[i] += dv;                                  // (unconditional: cheaper than the if-converted select;
+                                                        // stored only when do_bias)
         const int off = wsw_off(sr + WBR * j, cc >> 1) + 8 * (cc & 1);
         if constexpr (TERMS == 1) {
           *reinterpret_cast<u32x2*>(As + off) = bf16_rne4(a);

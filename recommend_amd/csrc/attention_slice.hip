@@ -524,11 +524,15 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_fwd_slice_kernel(SliceArgs p
 // 120 registers do not fit the 256 of two waves per SIMD; the other workgroup's compute covers a slice's loads), the
 // K image re-read from global (issued before the phase-1 barrier) instead of kept in registers, and phase 2's dS
 // reads issued two key-block pairs ahead.
-template <int HD, int NWV, int NP, bool LAT_ = NWV == 4, bool G2 = false>
+template <int HD, int NWV, int NP, bool LAT_ = NWV == 4, bool G2 = false, int RQ = RMAX<HD>(), int KR = RQ>
 __global__ __launch_bounds__(64 * NWV, G2 ? 2 : 1) void attn_bwd_slice_kernel(SliceArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NT = HD / 32, NM = HD / 16, CPR = HD / 8, NTH = 64 * NWV;
-  constexpr int RM = RMAX<HD>(), PB = RM * HD * 2;
+  constexpr int RM = RQ, PB = RM * HD * 2;
+  // phase 2's K image: KR rows; past RQ (the long forms) its planes take twice the Q planes' stride, the second
+  // plane over the dO planes (free after phase 1)
+  static_assert(KR == RQ || (G2 && NP == 2 && KR <= 2 * RQ), "attn_bwd_slice_kernel: K image rows");
+  constexpr int KPB = KR > RQ ? 2 * PB : PB;
   constexpr int SR = (RM * CPR + NTH - 1) / NTH;
   constexpr bool LAT = LAT_;                        // fragment reads one item ahead, fenced (one wave per SIMD)
   static_assert(NTH >= RM, "attn_bwd_slice_kernel: the staging gives each padded query row one thread");
@@ -543,13 +547,13 @@ __global__ __launch_bounds__(64 * NWV, G2 ? 2 : 1) void attn_bwd_slice_kernel(Sl
   float* lse2 = reinterpret_cast<float*>(smem + 2 * NP * PB);
   float* dlt = lse2 + RM;
   int* qps = reinterpret_cast<int*>(dlt + RM);
-  int* tab = qps + RM;                             // [16] first visible query block, [16] dS-store base per key block
-  float* red = reinterpret_cast<float*>(tab + 32);   // NP = 2: per-wave maxima [3][8] (staging), [2][8] (phase 1)
+  int* tab = qps + RM;                     // [TABN] first visible query block, [TABN] dS-store base per key block
+  float* red = reinterpret_cast<float*>(tab + 2 * SLICE_TABN);   // NP = 2: per-wave maxima [3][8], [2][8]
   char* dss = G2 ? reinterpret_cast<char*>(p.dsws + (size_t)blockIdx.x * p.ds_floats) : reinterpret_cast<char*>(red + 32);
   const float c1 = p.scale * L2E;
-  if (threadIdx.x < 16) {
+  if (threadIdx.x < SLICE_TABN) {
     tab[threadIdx.x] = p.qf[threadIdx.x];
-    tab[16 + threadIdx.x] = p.bbase[threadIdx.x];
+    tab[SLICE_TABN + threadIdx.x] = p.bbase[threadIdx.x];
   }
   const uint64_t srow1 = sched_row(p, 1, wave), srow2 = sched_row(p, 2, wave);
   // per-lane LDS offsets, held opaque (asm) so the compiler keeps one register per base and adds each
@@ -734,7 +738,7 @@ __global__ __launch_bounds__(64 * NWV, G2 ? 2 : 1) void attn_bwd_slice_kernel(Sl
       f32x4 dk[NM], dv[NM];
 #pragma unroll
       for (int m = 0; m < NM; ++m) dk[m] = dv[m] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const int a0 = tab[kb], blk0 = tab[16 + kb];
+      const int a0 = tab[kb], blk0 = tab[SLICE_TABN + kb];
       // S and dP of query step a (blocks a, a + 1; the second zero past the last block).  With one wave per
       // SIMD nothing else hides LDS latency, so each (half, t) item's fragments are read one item ahead
       // (sched_barrier keeps the compiler from sinking the reads back to their MFMAs)
@@ -835,7 +839,7 @@ __global__ __launch_bounds__(64 * NWV, G2 ? 2 : 1) void attn_bwd_slice_kernel(Sl
     // I hold row I - 1, times dS = 0) — no re-read or re-split of K
     SLICE_STAMP(1, it, 2);
     // G2: the K rows for the phase-2 image, issued before the barrier (in flight while the other waves finish)
-    constexpr int SRK = (RM * CPR + NTH - 1) / NTH;
+    constexpr int SRK = (KR * CPR + NTH - 1) / NTH;
     float kim[G2 ? SRK : 1][8];
     if constexpr (G2) {
 #pragma unroll
@@ -868,7 +872,7 @@ __global__ __launch_bounds__(64 * NWV, G2 ? 2 : 1) void attn_bwd_slice_kernel(Sl
 #pragma unroll
       for (int r = 0; r < SRK; ++r) {
         const int task = threadIdx.x + r * NTH, j = task / CPR, c = task % CPR;
-        if (task < IP * CPR) store_planesN<NP>(qimg, PB, poff<HD>(j, c), kim[r], sks);
+        if (task < IP * CPR) store_planesN<NP>(qimg, KPB, poff<HD>(j, c), kim[r], sks);
       }
     }
 #pragma unroll
@@ -886,7 +890,7 @@ __global__ __launch_bounds__(64 * NWV, G2 ? 2 : 1) void attn_bwd_slice_kernel(Sl
           }
 #pragma unroll
           for (int pl = 0; pl < NP; ++pl)
-            *reinterpret_cast<u32x4*>(qimg + pl * PB + poff<HD>(16 * kb + li, 4 * t + g)) = kp[pl];
+            *reinterpret_cast<u32x4*>(qimg + pl * KPB + poff<HD>(16 * kb + li, 4 * t + g)) = kp[pl];
         }
       }
     }
@@ -915,23 +919,24 @@ __global__ __launch_bounds__(64 * NWV, G2 ? 2 : 1) void attn_bwd_slice_kernel(Sl
 #pragma unroll
       for (int m = 0; m < NM; ++m) dq2[m] = f32x4{0.f, 0.f, 0.f, 0.f};
       auto ldds = [&](int k2, f32x4& x0, f32x4& x1) {
-        x0 = *reinterpret_cast<const f32x4*>(dss + 1024 * (tab[16 + k2] + qb - tab[k2]) + dsr);
+        x0 = *reinterpret_cast<const f32x4*>(dss + 1024 * (tab[SLICE_TABN + k2] + qb - tab[k2]) + dsr);
         x1 = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (k2 + 1 <= kbl) x1 = *reinterpret_cast<const f32x4*>(dss + 1024 * (tab[17 + k2] + qb - tab[k2 + 1]) + dsr);
+        if (k2 + 1 <= kbl)
+          x1 = *reinterpret_cast<const f32x4*>(dss + 1024 * (tab[SLICE_TABN + 1 + k2] + qb - tab[k2 + 1]) + dsr);
       };
       auto stepx = [&](int k2, f32x4 x0, f32x4 x1, f32x4 (&acc)[NM]) {
         const bool two = k2 + 1 <= kbl;
         float v[8];
         const int ra = 16 * RBY * k2, rb = two ? ra + 16 * RBY : ra;
         u32x4 fa[2][NP];
-        tr_atN<NP>(fa[0], smem + ra + tbase[0], smem + rb + tbase[0], PB);   // in flight during the split
+        tr_atN<NP>(fa[0], smem + ra + tbase[0], smem + rb + tbase[0], KPB);   // in flight during the split
 #pragma unroll
         for (int i = 0; i < 4; ++i) { v[i] = x0[i]; v[4 + i] = x1[i]; }
         u32x4 bp[NP];
         splitN<NP>(v, sdss, bp);
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
-          if (m + 1 < NM) tr_atN<NP>(fa[(m + 1) & 1], smem + ra + tbase[m + 1], smem + rb + tbase[m + 1], PB);
+          if (m + 1 < NM) tr_atN<NP>(fa[(m + 1) & 1], smem + ra + tbase[m + 1], smem + rb + tbase[m + 1], KPB);
           acc[m] = mmaN<NP>(fa[m & 1], bp, acc[m]);
           if (LAT) __builtin_amdgcn_sched_barrier(0);
         }
@@ -991,8 +996,9 @@ int bwd_pairs(int I, int K) {
   return n;
 }
 
-size_t bwd_lds(int I, int K, int hd, int np = 3, bool g2 = false) {
-  return (size_t)4 * np * rmax(hd) * hd + 12 * (size_t)rmax(hd) + 128 + 128 + (g2 ? 0 : 1024 * (size_t)bwd_pairs(I, K));
+size_t bwd_lds(int I, int K, int hd, int np = 3, bool g2 = false, int rq = 0) {
+  const size_t r = rq ? rq : rmax(hd);
+  return (size_t)4 * np * r * hd + 12 * r + 8 * SLICE_TABN + 128 + (g2 ? 0 : 1024 * (size_t)bwd_pairs(I, K));
 }
 
 static int device_cus() {
@@ -1059,10 +1065,11 @@ static bool lpt(int n, const int* load, int nwv, int8_t (&out)[8][8], int cap = 
 
 // forward: query blocks (heaviest first: the last); backward: key blocks (heaviest first: the first) in
 // query steps of two blocks, then query blocks in steps of two key blocks; costs in MFMA groups
-static bool make_schedule(SliceArgs& p, int hd, int nwv) {
+static bool make_schedule(SliceArgs& p, int hd, int nwv, int kcap) {
   const int I = p.I, K = p.K, q_off = I - K, nkb = (I + 15) / 16, nqb = (K + 15) / 16;
   const int NT = hd / 32, NM = hd / 16;
-  int load[MAXKB];
+  if (nkb > SLICE_TABN) return false;
+  int load[SLICE_TABN];
   for (int idx = 0; idx < nqb; ++idx) {
     const int kl = (q_off + std::min(16 * (nqb - 1 - idx) + 15, K - 1)) >> 4;
     load[idx] = NT * (kl + 1) + NM * (kl / 2 + 1);
@@ -1076,7 +1083,7 @@ static bool make_schedule(SliceArgs& p, int hd, int nwv) {
     p.bbase[kb] = (int16_t)base;
     base += nqb - f;
   }
-  if (!lpt(nkb, load, nwv, p.sched[1], keep_slots(hd, nwv))) return false;   // the backward keeps K per slot
+  if (!lpt(nkb, load, nwv, p.sched[1], kcap)) return false;   // (one workgroup per CU: the backward keeps K per slot)
   for (int idx = 0; idx < nqb; ++idx) load[idx] = (((q_off + std::min(16 * (nqb - 1 - idx) + 15, K - 1)) >> 4) + 2) >> 1;
   return lpt(nqb, load, nwv, p.sched[2]);
 }
@@ -1102,6 +1109,23 @@ static void raise_lds_limit(F* k) {
   (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
 }
 
+// Backward forms.  Past I = 144 at head_dim 64 (C3's first two layers: I 524 / K 262, I 262 / K 131) the key
+// side outgrows the Q planes' rows: the K / V blocks come from global per key block anyway, so only phase 2's K
+// image needs room — it takes the Q and dO planes' space together (KR = 2 RQ rows), and dS goes to the workspace.
+//   MID:  K <= 144, I <= 288 — the two-workgroup kernel (4 waves, 75.9 KiB of LDS) with a 288-row K image;
+//   LONG: K <= 272, I <= 544 — one workgroup of 8 waves per CU (Q / dO planes of 272 rows: 139.6 KiB).
+enum BwdForm { BWD_NONE, BWD_32, BWD_64, BWD_MID, BWD_LONG };
+constexpr int RQ_LONG = 272, BWD_WAVES_LONG = 8;
+static BwdForm bwd_form(int I, int K, int hd) {
+  if (K <= 0 || K > I) return BWD_NONE;
+  if (hd == 32) return I <= RMAX<32>() && bwd_lds(I, K, 32, BWD_PLANES) <= (size_t)LDS_MAX ? BWD_32 : BWD_NONE;
+  if (hd != 64) return BWD_NONE;
+  if (I <= RMAX<64>()) return bwd_lds(I, K, 64, BWD_PLANES) <= (size_t)LDS_MAX ? BWD_64 : BWD_NONE;
+  if (K <= RMAX<64>() && I <= 2 * RMAX<64>()) return BWD_MID;
+  if (K <= RQ_LONG && I <= 2 * RQ_LONG && (I + 15) / 16 <= SLICE_TABN) return BWD_LONG;
+  return BWD_NONE;
+}
+
 }  // namespace slice
 
 bool attn_slice_fwd_supported(int I, int K, int head_dim) {
@@ -1111,8 +1135,7 @@ bool attn_slice_fwd_supported(int I, int K, int head_dim) {
 }
 
 bool attn_slice_bwd_supported(int I, int K, int head_dim, bool selected) {
-  return !selected && (head_dim == 32 || head_dim == 64) && I <= slice::rmax(head_dim) && K > 0 && K <= I &&
-         slice::bwd_lds(I, K, head_dim, slice::BWD_PLANES) <= (size_t)slice::LDS_MAX;
+  return !selected && slice::bwd_form(I, K, head_dim) != slice::BWD_NONE;
 }
 
 int attn_slice_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos, int head_dim,
@@ -1133,7 +1156,7 @@ int attn_slice_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, con
               1.f / sqrtf((float)head_dim), qpos};
   const size_t lds = fwd_lds(I, head_dim, head_dim == 64 ? P64 : P32);
   const int nw = FWD_WAVES;
-  OT_REQUIRE(make_schedule(p, head_dim, nw), "ot_attn_fwd(slice): schedule");
+  OT_REQUIRE(make_schedule(p, head_dim, nw, 8), "ot_attn_fwd(slice): schedule");
   const KF k = table[head_dim == 64][qpos != nullptr];
   const unsigned slices = (unsigned)((int64_t)B * H);
   const dim3 grid(slices), block(64 * nw);
@@ -1148,11 +1171,23 @@ int attn_slice_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, con
 // hd 32 as two workgroups of 4 waves 868-879 us against 816-821 for one of 8 (kept)
 constexpr bool bwd_g2(int hd) { return hd == 64; }
 
+// workgroups per CU of the workspace-dS forms (0: dS in LDS only)
+static int bwd_ws_wpc(slice::BwdForm f) {
+  return f == slice::BWD_64 || f == slice::BWD_MID ? 2 : f == slice::BWD_LONG ? 1 : 0;
+}
+
 size_t attn_slice_bwd_ws_bytes(int B, int H, int I, int K, int head_dim) {
   using namespace slice;
-  if (!bwd_g2(head_dim)) return 0;
-  const int64_t grid = std::min<int64_t>((int64_t)B * H, 2 * (int64_t)device_cus());
+  const int wpc = bwd_ws_wpc(bwd_form(I, K, head_dim));
+  if (!wpc) return 0;
+  const int64_t grid = std::min<int64_t>((int64_t)B * H, wpc * (int64_t)device_cus());
   return (size_t)grid * 1024 * bwd_pairs(I, K);
+}
+
+size_t attn_slice_bwd_min_ws(int I, int K, int head_dim) {
+  using namespace slice;
+  const BwdForm f = bwd_form(I, K, head_dim);
+  return f == BWD_MID || f == BWD_LONG ? (size_t)1024 * bwd_pairs(I, K) : 0;
 }
 
 int attn_slice_bwd(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse, int B, int H,
@@ -1161,20 +1196,26 @@ int attn_slice_bwd(const float* qkv, int64_t ld, const float* out, const float* 
   using KF = void (*)(SliceArgs);
   static const KF k32 = attn_bwd_slice_kernel<32, BWD_WAVES32, BWD_PLANES>,
                   k64 = attn_bwd_slice_kernel<64, BWD_WAVES64, BWD_PLANES>,
-                  k64g = attn_bwd_slice_kernel<64, BWD_WAVES64, BWD_PLANES, false, true>;
+                  k64g = attn_bwd_slice_kernel<64, BWD_WAVES64, BWD_PLANES, false, true>,
+                  kmid = attn_bwd_slice_kernel<64, BWD_WAVES64, BWD_PLANES, false, true, RMAX<64>(), 2 * RMAX<64>()>,
+                  klong = attn_bwd_slice_kernel<64, BWD_WAVES_LONG, BWD_PLANES, false, true, RQ_LONG, 2 * RQ_LONG>;
   static std::once_flag once;
   std::call_once(once, [] {
-    for (KF k : {k32, k64, k64g}) raise_lds_limit(k);
+    for (KF k : {k32, k64, k64g, kmid, klong}) raise_lds_limit(k);
     (void)hipGetLastError();
   });
+  const BwdForm form = bwd_form(I, K, head_dim);
+  OT_REQUIRE(form != BWD_NONE, "ot_attn_bwd(slice): I %d K %d head_dim %d unsupported", I, K, head_dim);
   SliceArgs p{qkv, ld, H * head_dim, out, dout, lse, nullptr, nullptr, dqkv, B, H, I, K,
               1.f / sqrtf((float)head_dim), nullptr};
   const size_t per_wg = (size_t)1024 * bwd_pairs(I, K);
-  const bool g2 = bwd_g2(head_dim) && ws && ws_bytes >= per_wg;
-  const int nw = head_dim == 32 ? BWD_WAVES32 : BWD_WAVES64;
-  OT_REQUIRE(make_schedule(p, head_dim, nw), "ot_attn_bwd(slice): schedule");
-  const KF k = head_dim == 32 ? k32 : g2 ? k64g : k64;
-  const size_t lds = bwd_lds(I, K, head_dim, BWD_PLANES, g2);
+  const bool wsok = ws && ws_bytes >= per_wg;
+  const bool g2 = form == BWD_MID || form == BWD_LONG || (form == BWD_64 && bwd_g2(64) && wsok);
+  OT_REQUIRE(!g2 || wsok, "ot_attn_bwd(slice): I %d K %d needs %zu bytes of workspace", I, K, per_wg);
+  const int nw = form == BWD_32 ? BWD_WAVES32 : form == BWD_LONG ? BWD_WAVES_LONG : BWD_WAVES64;
+  OT_REQUIRE(make_schedule(p, head_dim, nw, g2 ? 8 : keep_slots(head_dim, nw)), "ot_attn_bwd(slice): schedule");
+  const KF k = form == BWD_32 ? k32 : form == BWD_MID ? kmid : form == BWD_LONG ? klong : g2 ? k64g : k64;
+  const size_t lds = bwd_lds(I, K, head_dim, BWD_PLANES, g2, form == BWD_LONG ? RQ_LONG : 0);
   unsigned g = persistent_grid((const void*)k, 64 * nw, lds, (int64_t)B * H);
   if (g2) {
     g = (unsigned)std::min<size_t>(g, ws_bytes / per_wg);      // each workgroup owns per_wg bytes of scratch

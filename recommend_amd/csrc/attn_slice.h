@@ -7,6 +7,8 @@
 
 namespace ot {
 
+constexpr int SLICE_TABN = 36;                // backward key blocks per slice (I <= 544 at head_dim 64)
+
 struct SliceArgs {
   const float* qkv; int64_t ld; int d;        // qkv [B*I, ld]: q at col 0, k at d, v at 2d; head h at +h*hd
   const float* o; const float* dout; const float* lse_in;   // backward inputs: O, dO [B*K, d], lse [B*H*K]
@@ -18,8 +20,8 @@ struct SliceArgs {
   // work schedule from the host (attention_slice.hip make_schedule): item of slot s of wave w, -1 = none;
   // [0] forward query blocks, [1] backward key blocks, [2] backward query blocks (items heaviest first)
   alignas(8) int8_t sched[3][8][8];            // rows read as one uint64 each (slot s = byte s)
-  int8_t qf[16];                              // backward: first query block that sees key block kb
-  int16_t bbase[16];                          // backward: dS-store block index of (qf[kb], kb)
+  int8_t qf[SLICE_TABN];                      // backward: first query block that sees key block kb
+  int16_t bbase[SLICE_TABN];                  // backward: dS-store block index of (qf[kb], kb)
   float* dsws; int ds_floats;                 // backward, two workgroups per CU: per-workgroup dS scratch
 };
 
@@ -32,5 +34,7 @@ int attn_slice_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, con
 int attn_slice_bwd(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse, int B, int H,
                    int I, int K, int head_dim, float* dqkv, float* ws, size_t ws_bytes, hipStream_t stream);
 size_t attn_slice_bwd_ws_bytes(int B, int H, int I, int K, int head_dim);
+// the workspace the backward cannot run without (the long forms keep dS only there; 0 otherwise)
+size_t attn_slice_bwd_min_ws(int I, int K, int head_dim);
 
 }  // namespace ot

@@ -422,7 +422,8 @@ def main():
                            'block-scaled fp8, whose dense peak is 2x)' if bf16 else
                            'f32-accurate attention: core_frac against the native f32 MFMA peak 157.3; the kernels '
                            'issue split MFMA products (slice kernels: 3 fp16 products per f32 product, the hd-32 '
-                           'forward 6 bf16 products; longer sequences: 6 bf16 products or native f32), so '
+                           'forward 6 bf16 products; the head_dim-64 backward up to I 544 also on the slice '
+                           'kernels; longer forwards: 6 bf16 products, other shapes native f32), so '
                            'core_frac_of_issued_ceiling prices them against bf16 dense / 3')}
             pmc = attention_pmc(args.config)
             if pmc is not None:

@@ -1114,6 +1114,7 @@ static void raise_lds_limit(F* k) {
 // image needs room — it takes the Q and dO planes' space together (KR = 2 RQ rows), and dS goes to the workspace.
 //   MID:  K <= 144, I <= 288 — the two-workgroup kernel (4 waves, 75.9 KiB of LDS) with a 288-row K image;
 //   LONG: K <= 272, I <= 544 — one workgroup of 8 waves per CU (Q / dO planes of 272 rows: 139.6 KiB).
+// (The MID shapes on the LONG form measured 7-8% slower: I 262 / K 131, B 2048 H 4 1,620-1,628 vs 1,503-1,552 us.)
 enum BwdForm { BWD_NONE, BWD_32, BWD_64, BWD_MID, BWD_LONG };
 constexpr int RQ_LONG = 272, BWD_WAVES_LONG = 8;
 static BwdForm bwd_form(int I, int K, int hd) {

@@ -1861,7 +1861,7 @@ static int attn_bwd_impl(const float* qkv, int64_t ld, const float* out, const f
              1.f / sqrtf((float)head_dim), qpos};
   const int mm = prec;
   if (mm == OT_MATMUL_SPLIT_BF16 && flags == 0 && K > SMALL_K && attn_slice_bwd_supported(I, K, head_dim, qpos != nullptr) &&
-      ws_bytes >= attn_slice_bwd_min_ws(I, K, head_dim))
+      ws_bytes >= attn_slice_bwd_min_ws(B, H, I, K, head_dim))
     return attn_slice_bwd(qkv, ld, out, dout, lse, B, H, I, K, head_dim, dqkv, delta_ws, ws_bytes, (hipStream_t)stream);
   // the f32 head_dim-32 backward over tail queries forms its own row statistics (no prep launch)
   const bool fdl = !qpos && head_dim == 32 && K > SMALL_K && attn_kpad(K) <= FDL_KP &&

@@ -1185,10 +1185,13 @@ size_t attn_slice_bwd_ws_bytes(int B, int H, int I, int K, int head_dim) {
   return (size_t)grid * 1024 * bwd_pairs(I, K);
 }
 
-size_t attn_slice_bwd_min_ws(int I, int K, int head_dim) {
+// the long forms keep dS only in the workspace: below one workgroup's share per CU (e.g. ot_attn_bwd's lse / delta
+// workspace) the caller takes the per-pair f32 kernels instead of a starved grid
+size_t attn_slice_bwd_min_ws(int B, int H, int I, int K, int head_dim) {
   using namespace slice;
   const BwdForm f = bwd_form(I, K, head_dim);
-  return f == BWD_MID || f == BWD_LONG ? (size_t)1024 * bwd_pairs(I, K) : 0;
+  if (f != BWD_MID && f != BWD_LONG) return 0;
+  return (size_t)1024 * bwd_pairs(I, K) * (size_t)std::min<int64_t>((int64_t)B * H, device_cus());
 }
 
 int attn_slice_bwd(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse, int B, int H,

@@ -34,7 +34,7 @@ int attn_slice_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, con
 int attn_slice_bwd(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse, int B, int H,
                    int I, int K, int head_dim, float* dqkv, float* ws, size_t ws_bytes, hipStream_t stream);
 size_t attn_slice_bwd_ws_bytes(int B, int H, int I, int K, int head_dim);
-// the workspace the backward cannot run without (the long forms keep dS only there; 0 otherwise)
-size_t attn_slice_bwd_min_ws(int I, int K, int head_dim);
+// the workspace below which the backward's long forms are not taken (they keep dS only there; 0 otherwise)
+size_t attn_slice_bwd_min_ws(int B, int H, int I, int K, int head_dim);
 
 }  // namespace ot

@@ -130,6 +130,15 @@ def test_slice_attention_long_backward(dev, B, H, I, Kq, hd):
     dq2[:, :d].zero_()
     K.attn_bwd(qkv_d, 3 * d, out, dout.float().to(dev), lse, B, H, I, Kq, hd, dq2)
     assert torch.equal(dq2, dqkv)
+    if B <= 3:
+        # ot_attn_bwd's own workspace (lse / delta only) is below the long forms' dS share: the per-pair f32
+        # backward runs instead, to the same bound
+        ws = K.workspace(K.size('ot_attn_bwd_workspace_size', B, H, Kq), dev)
+        dq3 = torch.zeros_like(dqkv)
+        dout_d = dout.float().to(dev)
+        K.call('ot_attn_bwd', K.ptr(qkv_d), 3 * d, K.ptr(out), K.ptr(dout_d), K.ptr(lse), B, H, I, Kq,
+               None, hd, K.ptr(dq3), K.ptr(ws), _lib.OT_MATMUL_SPLIT_BF16, K.stream())
+        torch.testing.assert_close(dq3.double().cpu(), qkv_r.grad, rtol=2e-5, atol=2e-5)
 
 
 def test_slice_limits():

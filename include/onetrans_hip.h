@@ -293,12 +293,16 @@ int ot_attn_bwd_dqkv_bf16_supported(int I, int K, int head_dim, int selected, in
  * OT_ATTN_DQKV_BF16 alone on the short-tail kernel (K <= 4: the last layer after DCE), none otherwise */
 int ot_attn_bwd_bf16_forms(int I, int K, int head_dim, int selected, int precision);
 /* (in the f32-accurate mode it also covers the head_dim-64 slice backward's dS scratch: one causal block pair
- * store per co-resident workgroup, two per CU; a smaller workspace shrinks that kernel's grid) */
+ * store per co-resident workgroup, two per CU — one per CU for the long form, K <= 272 / I <= 544; a smaller
+ * workspace shrinks that kernel's grid, and below one workgroup's share per CU the long forms (I > 144) are not
+ * taken: the per-pair f32 backward runs instead) */
 size_t ot_attn_bwd_flags_workspace_size(int B, int H, int I, int K, int head_dim, int selected, int flags, int precision);
 /* 1 when the f32-accurate mode (OT_MATMUL_SPLIT_BF16) runs this shape's forward and backward as one
  * workgroup per (sample, head) slice on split MFMA (attention_slice.hip: head_dim 32 / 64, I <= 192,
  * tail queries for the backward, the slice's planes within LDS; the dS store in LDS at head_dim 32, in the
- * workspace at 64), else 0 */
+ * workspace at 64), else 0.  (The backward alone also takes head_dim 64 up to I 544 / K 272 on the slice
+ * kernels, with a forward from attn_fwd_split_kernel: ot_attn_bwd_flags_workspace_size then exceeds
+ * ot_attn_bwd_workspace_size by its dS scratch.) */
 int ot_attn_slice_supported(int I, int K, int head_dim, int selected);
 int ot_attn_bwd_flags(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
                       int B, int H, int I, int K, const int32_t* qpos, int head_dim, void* dqkv, int flags,

@@ -1,6 +1,7 @@
 // Short-sequence causal attention (I <= 192 keys) on split-bf16 MFMA, one workgroup per (sample, head)
 // slice.  Replaces model.py:100-114 (QK^T / sqrt(hd), band_part causal mask, softmax, PV) and its
-// gradient for the f32-accurate mode (OT_MATMUL_SPLIT_BF16) at head_dim 32 / 64.
+// gradient for the f32-accurate mode (OT_MATMUL_SPLIT_BF16) at head_dim 32 / 64; the backward also in two long
+// forms at head_dim 64 (I <= 544, K <= 272: the query side in LDS, the key side from global; see bwd_form).
 //
 // Why a new kernel family: the per-(sample, head)-wave kernels of attention.hip
 // walk (key block, query block) pairs and re-read the Q / dO block and read-modify-write the running

@@ -354,7 +354,9 @@ def main():
             # ceiling in f32 flops is the bf16 dense peak / SPLIT_TERMS
             gpeak = round(BF16_MFMA_PEAK_TFLOPS / SPLIT_TERMS, 1)
             gkern = ('plane_gemm_kernel / mixed_gemm_kernel + wgrad_split_kernel (f32 operands split exactly into '
-                     f'3 bf16 parts, {SPLIT_TERMS} bf16 MFMA products per f32 product; peak = bf16 dense / {SPLIT_TERMS})')
+                     f'3 bf16 parts, {SPLIT_TERMS} bf16 MFMA products per f32 product; peak = bf16 dense / {SPLIT_TERMS}; '
+                     'the RMSNorm-prologue plane GEMMs (QKV / FFN1 forward) issue 3 fp16 products of a scaled fp16 '
+                     'pair, so the family can exceed that ceiling by up to their share)')
         elif model.matmul == 'bf16':
             gpeak = BF16_MFMA_PEAK_TFLOPS
             gkern = ('plane_gemm_kernel / mixed_gemm_kernel + wgrad_split_kernel (operands rounded to bf16, one bf16 '

@@ -190,7 +190,10 @@ int ot_transpose_banks(const float* src, float* dst, const int64_t* banks_dev, i
  * B[g][n][k] = src[g*gstride + n*sn + k*sk] (* kscale[k] when kscale_off >= 0: an RMSNorm gamma folded
  * into the weights, x*rstd*gamma @ W = rstd * (x @ (gamma W))) is written once per weight update as
  * its three exact bf16 planes, one 12-KiB block per (g, 128-column tile, 16-k stage) in the LDS image
- * the GEMM reads.  desc_dev: [ndesc][10] int64 {src_off, sn, sk, gstride, kscale_off, dst_off
+ * the GEMM reads — except a gamma-folded bank (the RMSNorm-prologue GEMMs'), written as the scaled fp16
+ * pair of B[g][n][k] s_n (s_n a power of two per column n putting its largest magnitude in [2^13, 2^14),
+ * stored as 128 floats in the third plane of the tile's first block), which those GEMMs multiply with three
+ * f16 products (A scaled per row from the bound |x| <= sqrt(K) / rstd).  desc_dev: [ndesc][10] int64 {src_off, sn, sk, gstride, kscale_off, dst_off
  * (elements of img), first_unit, G, N, K} (offsets into base; K % 16 == 0); a bank owns
  * G*ceil(N/128)*(K/16) consecutive units of the launch; ot_split_image_elems gives its size. */
 size_t ot_split_image_elems(int G, int N, int K);

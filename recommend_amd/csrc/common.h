@@ -90,6 +90,42 @@ __device__ __forceinline__ f32x16 mfma_terms(const u32x4 (&a)[3], const u32x4 (&
   else return mfma_split6(a, b, c);
 }
 
+// ---- scaled fp16 pair (the plane GEMM's split mode; attention_slice.hip has the 16x16 form) -----------------
+// x s = h + l, h = fp16(x s), l = fp16(x s - h) (round to nearest even): 22 significant bits when the power-of-two
+// scale s puts the operand's largest magnitude in [2^13, 2^14); a product is h h' + h l' + l h' (the dropped l l'
+// is below 2^-22 |a||b|)
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float pow2_scale14(float m) {
+  const int e = (int)((__float_as_uint(m) >> 23) & 255u);   // m in [2^(e-127), 2^(e-126))
+  int se = 127 + 13 - (e - 127);
+  se = e == 0 ? 127 : (se < 1 ? 1 : (se > 254 ? 254 : se));
+  return __uint_as_float((uint32_t)se << 23);
+}
+__device__ __forceinline__ void pair8(const float* v, float s, u32x4 (&pl)[3]) {
+  uint32_t a[4], b[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const f32x2_t x = f32x2_t{v[2 * k], v[2 * k + 1]} * s;
+    const f16x2_t h = __builtin_convertvector(x, f16x2_t);
+    const f16x2_t l = __builtin_convertvector(x - __builtin_convertvector(h, f32x2_t), f16x2_t);
+    a[k] = __builtin_bit_cast(uint32_t, h);
+    b[k] = __builtin_bit_cast(uint32_t, l);
+  }
+  pl[0] = u32x4{a[0], a[1], a[2], a[3]};
+  pl[1] = u32x4{b[0], b[1], b[2], b[3]};
+}
+__device__ __forceinline__ f32x16 mfma_f16(u32x4 a, u32x4 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c, 0, 0,
+                                                 0);
+}
+__device__ __forceinline__ f32x16 mfma_pair(const u32x4 (&a)[3], const u32x4 (&b)[3], f32x16 c) {
+  c = mfma_f16(a[0], b[1], c);
+  c = mfma_f16(a[1], b[0], c);
+  return mfma_f16(a[0], b[0], c);
+}
+
 // ---- error reporting (per host thread) ---------------------------------------------
 void set_error(const char* fmt, ...);
 int fail(int code, const char* fmt, ...);

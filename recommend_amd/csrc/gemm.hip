@@ -760,10 +760,15 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 template <int TERMS>
 constexpr int pg_stage_bytes() { return PG_A_BYTES + (TERMS == 1 ? GT * 16 * 2 : PG_B_BYTES); }
 
+// TERMS = 2 (split mode with the RMSNorm prologue): the scaled fp16 pair, three f16 products.  B's image is the pair
+// of B[k][n] s_n (ot_split_images: every gamma-folded image, s_n from the column max); A = x gets one power-of-two
+// scale per row from the bound |x_k| <= sqrt(K) / rstd (sum_k x_k^2 = K (1 / rstd^2 - eps)) — no pass over the row;
+// the accumulator is unscaled per row and column before the epilogue.  Precision: 22 bits relative to the bound
+// (a row whose largest |x| is 2^-b of it keeps 22 - b bits there).
 template <int AXT, int EPIT, int NSTG, int MINW, int TERMS = 6>
 __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
   static_assert(NSTG >= 2 && NSTG <= 4, "plane GEMM stages");
-  static_assert(TERMS == 6 || TERMS == 1, "plane GEMM terms");
+  static_assert(TERMS == 6 || TERMS == 1 || (TERMS == 2 && AXT == OT_AX_RMSNORM), "plane GEMM terms");
   // OT_AX_BF16: A holds bf16 values (the FFN1 epilogue's stored gelu(U)): 32 B per row and stage, the
   // lane's fragment is one 16-B LDS read, no conversion (bf16 mode only)
   // OT_AX_BF16_RMSNORM: bf16 x with the RMSNorm applied as the RMSNorm prologue does on this kernel (gamma
@@ -810,7 +815,8 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
   // weight shared by every group, w_gstride 0 like Wo, has one group's image)
   const int gb = p.w_gstride ? g : 0;
   const char* bimg0 = reinterpret_cast<const char*>(p.bimg) + ((int64_t)gb * p.bimg_ntn + p.bimg_tn0 + tn) * nk * PG_B_BYTES;
-  const char* bsrc = bimg0 + (3 * wave) * 1024 + 16 * lane;
+  constexpr int BPL = TERMS == 2 ? 2 : 3;              // B planes copied per stage (split modes)
+  const char* bsrc = bimg0 + (BPL * wave) * 1024 + 16 * lane;
   const char* bsrc1 = bimg0 + wave * 1024 + 16 * lane;
 
   auto issue = [&](int ks, int buf) {
@@ -828,9 +834,9 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
                                        (lds_void_t*)(sb + PG_A_BYTES + wave * 1024), 16, 0, 0);
     } else {
 #pragma unroll
-      for (int i = 0; i < 3; ++i)
+      for (int i = 0; i < BPL; ++i)
         __builtin_amdgcn_global_load_lds((const void*)(bsrc + (int64_t)ks * PG_B_BYTES + i * 1024),
-                                         (lds_void_t*)(sb + PG_A_BYTES + (3 * wave + i) * 1024), 16, 0, 0);
+                                         (lds_void_t*)(sb + PG_A_BYTES + (BPL * wave + i) * 1024), 16, 0, 0);
     }
   };
 
@@ -866,14 +872,28 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
     }
   }
 
+  // TERMS 2: this lane's A row scale from the RMSNorm bound sqrt(K) / rstd (the row's rstd, as the epilogue reads
+  // it; loaded ahead of the stage copies, so waiting for it does not drain them)
+  float arstd = 1.f;
+  if constexpr (TERMS == 2) {
+    const int64_t gr = (int64_t)tm * GT + ra;
+    int ir = p.in_rows ? p.in_rows[gr] : (int)gr;
+    ir = ir < 0 ? 0 : ir;
+    arstd = p.a_rstd[ir];
+  }
   issue(0, 0);
   if (NSTG >= 3 && nk > 1) issue(1, 1);
   if (NSTG >= 4 && nk > 2) issue(2, 2);
+  float asc = 1.f, ainv = 1.f;
+  if constexpr (TERMS == 2) {
+    asc = pow2_scale14(sqrtf((float)p.K) / arstd);
+    ainv = 1.f / asc;
+  }
   for (int kt = 0; kt < nk; ++kt) {
     // this wave's copies of stage kt are done (with 3 stages the 5 (TERMS 1: 3) of stage kt+1 may
     // still fly), every wave's after the barrier; the barrier also retires every read of the buffer
     // that the copies of stage kt+NSTG-1 then overwrite (last read in iteration kt-1)
-    constexpr int OPS = ABF ? 2 : (TERMS == 1 ? 3 : 5);    // copies per wave and stage
+    constexpr int OPS = ABF ? 2 : (TERMS == 1 ? 3 : 2 + BPL);    // copies per wave and stage
     const int ahead = (NSTG - 2 < nk - 1 - kt) ? NSTG - 2 : nk - 1 - kt;   // later stages that may still fly
     if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * OPS) : "memory");
     else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(OPS) : "memory");
@@ -887,7 +907,7 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb)
 #pragma unroll
-      for (int q = 0; q < (TERMS == 1 ? 1 : 3); ++q)
+      for (int q = 0; q < (TERMS == 1 ? 1 : BPL); ++q)
         fb[nb][q] = *reinterpret_cast<const u32x4*>(sb + boff + q * 4096 + nb * 1024);
     if constexpr (ABF) {
       u32x4 fa[3];
@@ -925,9 +945,29 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
     }
     const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
     u32x4 fa[3];
-    split8t<TERMS == 1 ? 1 : 6>(av, fa);
+    if constexpr (TERMS == 2) {
+      pair8(av, asc, fa);
 #pragma unroll
-    for (int nb = 0; nb < 4; ++nb) acc[nb] = mfma_terms<TERMS == 1 ? 1 : 6>(fa, fb[nb], acc[nb]);
+      for (int nb = 0; nb < 4; ++nb) acc[nb] = mfma_pair(fa, fb[nb], acc[nb]);
+    } else {
+      split8t<TERMS == 1 ? 1 : 6>(av, fa);
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) acc[nb] = mfma_terms<TERMS == 1 ? 1 : 6>(fa, fb[nb], acc[nb]);
+    }
+  }
+  if constexpr (TERMS == 2) {
+    // unscale: row factor 1 / s_a (held by the lane whose A row it is: lane = row within the wave), column
+    // factor 1 / s_b (ot_split_images' column scales, plane 2 of the tile's first unit); exact powers of two
+    const float* csc = reinterpret_cast<const float*>(bimg0 + 2 * GT * 16 * 2);
+    float cinv[4];
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) cinv[nb] = 1.f / csc[32 * nb + li];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float ri = __shfl(ainv, (r & 3) + 8 * (r >> 2) + 4 * h, 64);
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) acc[nb][r] *= ri * cinv[nb];
+    }
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();                                    // the epilogue reuses the stage buffers
@@ -936,21 +976,59 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
 
 // Pre-split B images (ot_split_images).  desc [nd][10] int64: {src_off, sn, sk, gstride, kscale_off
 // (-1: none), dst_off (ushorts), first_unit, G, N, K}; B[g][n][k] = src[g*gstride + n*sn + k*sk]
-// (* kscale[k]); one unit = one (g, n tile, 16-k stage) block of 3 x 128 x 16 bf16, one thread per
-// (row n, 8-k half): split8 of the 8 values, each plane's 16 B at its swizzled half.
-__global__ __launch_bounds__(256) void split_images_kernel(const float* __restrict__ base, const int64_t* __restrict__ desc,
-                                                           int nd, uint16_t* img, int one) {
-  const int64_t unit = blockIdx.x;
+// (* kscale[k]); one unit = one (g, n tile, 16-k stage) block of 3 x 128 x 16 16-bit planes, one thread per
+// (row n, 8-k half), each plane's 16 B at its swizzled half.  Split mode: the exact three-plane bf16 split (split8),
+// except for gamma-folded images (kscale_off >= 0: the RMSNorm-prologue GEMMs, plane_gemm_kernel TERMS 2): the
+// scaled fp16 pair (planes 0, 1) of B[g][n][k] s_n, s_n a power of two per column n (image_colscale_kernel, stored
+// as 128 floats in plane 2 of the tile's first unit); bf16 mode: plane 0 = the value rounded to nearest.
+__device__ __forceinline__ const int64_t* image_unit(const int64_t* desc, int nd, int64_t unit, int64_t& g, int64_t& tn,
+                                                     int64_t& ks) {
   int b = 0;
   while (b + 1 < nd && desc[10 * (b + 1) + 6] <= unit) ++b;
   const int64_t* d = desc + 10 * b;
   const int64_t G = d[7], N = d[8], K = d[9];
   const int64_t ntn = (N + GT - 1) / GT, nks = K / 16;
   int64_t u = unit - d[6];
-  if (u >= G * ntn * nks) return;
-  const int64_t g = u / (ntn * nks);
+  if (u >= G * ntn * nks) return nullptr;
+  g = u / (ntn * nks);
   u %= ntn * nks;
-  const int64_t tn = u / nks, ks = u % nks;
+  tn = u / nks;
+  ks = u % nks;
+  return d;
+}
+
+// per column n of each (group, n tile): the power-of-two scale putting max_k |B[g][n][k]| in [2^13, 2^14) (one
+// block per image unit; the tile's first-unit blocks work, two threads per column)
+__global__ __launch_bounds__(256) void image_colscale_kernel(const float* __restrict__ base, const int64_t* __restrict__ desc,
+                                                             int nd, uint16_t* img) {
+  int64_t g, tn, ks;
+  const int64_t* d = image_unit(desc, nd, blockIdx.x, g, tn, ks);
+  if (!d || ks != 0 || d[4] < 0) return;
+  const int64_t N = d[8], K = d[9];
+  const int n = threadIdx.x >> 1, hh = threadIdx.x & 1;
+  const int64_t gn = tn * GT + n;
+  float m = 0.f;
+  if (gn < N) {
+    const float* src = base + d[0] + g * d[3] + gn * d[1];
+#pragma unroll 8
+    for (int64_t k = hh; k < K; k += 2) {
+      float x = src[k * d[2]];
+      if (d[4] >= 0) x *= base[d[4] + k];
+      m = fmaxf(m, fabsf(x));
+    }
+  }
+  m = fmaxf(m, __shfl_xor(m, 1, 64));
+  if (hh == 0)
+    reinterpret_cast<float*>(img + d[5] + ((int64_t)blockIdx.x - d[6]) * (PG_B_BYTES / 2) + 2 * GT * 16)[n] = pow2_scale14(m);
+}
+
+__global__ __launch_bounds__(256) void split_images_kernel(const float* __restrict__ base, const int64_t* __restrict__ desc,
+                                                           int nd, uint16_t* img, int one) {
+  const int64_t unit = blockIdx.x;
+  int64_t g, tn, ks;
+  const int64_t* d = image_unit(desc, nd, unit, g, tn, ks);
+  if (!d) return;
+  const int64_t N = d[8];
   const int n = threadIdx.x >> 1, hh = threadIdx.x & 1;
   const int64_t gn = tn * GT + n;
   const float* src = base + d[0] + g * d[3] + gn * d[1];
@@ -962,13 +1040,21 @@ __global__ __launch_bounds__(256) void split_images_kernel(const float* __restri
     if (d[4] >= 0) x *= base[d[4] + k];
     v[j] = x;
   }
-  u32x4 pl[3];
-  if (one) split8t<1>(v, pl);                         // OT_MATMUL_BF16: plane 0 = round to nearest
-  else split8(v, pl);
   uint16_t* dst = img + d[5] + (unit - d[6]) * (PG_B_BYTES / 2);
+  u32x4 pl[3];
+  const bool pair = !one && d[4] >= 0;
+  if (one) {
+    split8t<1>(v, pl);                                // OT_MATMUL_BF16: plane 0 = round to nearest
+  } else if (pair) {
+    const float sn = reinterpret_cast<const float*>(dst - ks * (PG_B_BYTES / 2) + 2 * GT * 16)[n];
+    pair8(v, sn, pl);
+  } else {
+    split8(v, pl);
+  }
+  const int npl = one ? 1 : pair ? 2 : 3;            // (pair: plane 2 of the first unit holds the column scales)
 #pragma unroll
   for (int q = 0; q < 3; ++q)
-    if (q == 0 || !one) *reinterpret_cast<u32x4*>(dst + q * GT * 16 + n * 16 + 8 * (hh ^ ((n >> 3) & 1))) = pl[q];
+    if (q < npl) *reinterpret_cast<u32x4*>(dst + q * GT * 16 + n * 16 + 8 * (hh ^ ((n >> 3) & 1))) = pl[q];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1844,7 +1930,7 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
 #define OT_PSPEC(AX_, EP_) \
     if (x == AX_ && e == (EP_)) \
       pk = one ? plane_gemm_kernel<AX_, EP_, PLANE_BF16_NSTG, 4, 1> \
-               : plane_gemm_kernel<AX_, EP_, 2, 4>;
+               : plane_gemm_kernel<AX_, EP_, 2, 4, (AX_) == OT_AX_RMSNORM ? 2 : 6>;
     OT_PSPEC(OT_AX_RMSNORM, 0)
     OT_PSPEC(OT_AX_RMSNORM, OT_EPI_BIAS)
     OT_PSPEC(OT_AX_GELU, OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_DROPOUT)
@@ -1996,6 +2082,11 @@ extern "C" int ot_split_images(const float* base, const int64_t* desc_dev, int n
   OT_REQUIRE(precision == OT_MATMUL_SPLIT_BF16 || precision == OT_MATMUL_BF16,
              "ot_split_images: precision %d has no plane images", precision);
   if (total_units == 0) return OT_OK;
+  if (precision == OT_MATMUL_SPLIT_BF16) {
+    hipLaunchKernelGGL(image_colscale_kernel, dim3((unsigned)total_units), dim3(256), 0, (hipStream_t)stream, base,
+                       desc_dev, ndesc, img);
+    OT_LAUNCH_CHECK("ot_split_images(column scales)");
+  }
   hipLaunchKernelGGL(split_images_kernel, dim3((unsigned)total_units), dim3(256), 0, (hipStream_t)stream, base,
                      desc_dev, ndesc, img, precision == OT_MATMUL_BF16 ? 1 : 0);
   OT_LAUNCH_CHECK("ot_split_images");

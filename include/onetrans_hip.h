@@ -155,6 +155,16 @@ typedef struct ot_rms_epilogue {
   uint16_t* c16_out; int64_t ldc16;                    /* optional, bf16-mode plane GEMM (not with the norm-backward
                                                           or bf16-C epilogues): also C rounded to bf16 — the next
                                                           GEMM's OT_AX_BF16_RMSNORM operand */
+  float* rowmax_out; int rowmax_n;                     /* optional, split-mode plane GEMM: each 128-column tile's
+                                                          largest C value after the bias (signed) at
+                                                          [out_row][tile] (rowmax_n = N / 128): the FFN1 forward's
+                                                          row maxima of U for the FFN2 GEMM's a_rowmax */
+  const float* a_rowmax; int a_rowmax_n;               /* optional, split-mode plane GEMM with the GELU prologue:
+                                                          the A rows' partial maxima [in_row][a_rowmax_n] (as
+                                                          rowmax_out wrote them); the GEMM then multiplies on the
+                                                          scaled fp16 pair, the row scale from max(max_j a_rowmax,
+                                                          0.17) >= max |gelu(a)|, and b_image must be a pair image
+                                                          (desc kscale_off -2, ot_split_images) */
 } ot_rms_epilogue;
 size_t ot_mixed_gemm_rms_workspace_size(int ntiles, int N);
 int ot_mixed_gemm_rms(int mode, const float* A, int64_t lda, int K, const int32_t* in_rows,
@@ -194,7 +204,8 @@ int ot_transpose_banks(const float* src, float* dst, const int64_t* banks_dev, i
  * pair of B[g][n][k] s_n (s_n a power of two per column n putting its largest magnitude in [2^13, 2^14),
  * stored as 128 floats in the third plane of the tile's first block), which those GEMMs multiply with three
  * f16 products (A scaled per row from the bound |x| <= sqrt(K) / rstd).  desc_dev: [ndesc][10] int64 {src_off, sn, sk, gstride, kscale_off, dst_off
- * (elements of img), first_unit, G, N, K} (offsets into base; K % 16 == 0); a bank owns
+ * (elements of img), first_unit, G, N, K} (offsets into base; K % 16 == 0; kscale_off -1: none, -2: none
+ * and the pair form — the FFN2 forward's W2 image, read with ot_rms_epilogue.a_rowmax); a bank owns
  * G*ceil(N/128)*(K/16) consecutive units of the launch; ot_split_image_elems gives its size. */
 size_t ot_split_image_elems(int G, int N, int K);
 int ot_split_images(const float* base, const int64_t* desc_dev, int ndesc, int64_t total_units, uint16_t* img,

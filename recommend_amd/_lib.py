@@ -43,7 +43,9 @@ class RmsEpilogue(ctypes.Structure):
                 ('rowdot', c_void_p), ('rowdot_n', c_int),
                 ('gelu_out', c_void_p), ('ldgelu', c_int64),
                 ('xn_out', c_void_p), ('ldxn', c_int64),
-                ('c16_out', c_void_p), ('ldc16', c_int64)]
+                ('c16_out', c_void_p), ('ldc16', c_int64),
+                ('rowmax_out', c_void_p), ('rowmax_n', c_int),
+                ('a_rowmax', c_void_p), ('a_rowmax_n', c_int)]
 
 P = c_void_p
 I64 = c_int64

@@ -105,6 +105,8 @@ struct GemmArgs {
   // of their A rows (the bf16 weight gradient's normalised A operand)
   uint16_t* xn_out; int64_t ldxn;
   uint16_t* c16_out; int64_t ldc16;             // bf16-mode plane GEMM: also C rounded to bf16 (optional)
+  float* rowmax_out; int rowmax_n;              // split plane GEMM: per (out row, column tile) max of C after bias
+  const float* a_rowmax; int a_rowmax_n;        // split plane GEMM, GELU prologue: A's row maxima (pair arithmetic)
 };
 
 // sum over the 32 lanes that hold one output row in the vector epilogue (same order as the
@@ -280,6 +282,12 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
           f32x4 v = *reinterpret_cast<const f32x4*>(ct + (rb + 8 * (i0 + i)) * CLD + 4 * c4);
           if (ROWSCALE) v = v * rsc[i0 + i];
           if (epi & OT_EPI_BIAS) v += bias4;
+          if (p.rowmax_out) {                                  // this tile's largest C of the row (signed)
+            float mx = fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w));
+#pragma unroll
+            for (int o = 16; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+            if (orr >= 0 && c4 == 0) p.rowmax_out[(int64_t)orr * p.rowmax_n + n0 / GT] = mx;
+          }
           if (epi & OT_EPI_GELU_BWD) {
             v *= gelu_erf_grad4(aux4[i]);
             if (p.gelu_out && orr >= 0) {                      // the stored GELU (W2 weight gradient's A)
@@ -768,7 +776,8 @@ constexpr int pg_stage_bytes() { return PG_A_BYTES + (TERMS == 1 ? GT * 16 * 2 :
 template <int AXT, int EPIT, int NSTG, int MINW, int TERMS = 6>
 __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
   static_assert(NSTG >= 2 && NSTG <= 4, "plane GEMM stages");
-  static_assert(TERMS == 6 || TERMS == 1 || (TERMS == 2 && AXT == OT_AX_RMSNORM), "plane GEMM terms");
+  static_assert(TERMS == 6 || TERMS == 1 || (TERMS == 2 && (AXT == OT_AX_RMSNORM || AXT == OT_AX_GELU)),
+                "plane GEMM terms");
   // OT_AX_BF16: A holds bf16 values (the FFN1 epilogue's stored gelu(U)): 32 B per row and stage, the
   // lane's fragment is one 16-B LDS read, no conversion (bf16 mode only)
   // OT_AX_BF16_RMSNORM: bf16 x with the RMSNorm applied as the RMSNorm prologue does on this kernel (gamma
@@ -874,19 +883,25 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
 
   // TERMS 2: this lane's A row scale from the RMSNorm bound sqrt(K) / rstd (the row's rstd, as the epilogue reads
   // it; loaded ahead of the stage copies, so waiting for it does not drain them)
-  float arstd = 1.f;
+  // (GELU prologue: the row's bound max(max_j a_rowmax, 0.17) >= max |gelu(a)|, from the producer's partial maxima)
+  float abound = 1.f;
   if constexpr (TERMS == 2) {
     const int64_t gr = (int64_t)tm * GT + ra;
     int ir = p.in_rows ? p.in_rows[gr] : (int)gr;
     ir = ir < 0 ? 0 : ir;
-    arstd = p.a_rstd[ir];
+    if constexpr (AXT == OT_AX_RMSNORM) {
+      abound = p.a_rstd[ir];
+    } else {
+      abound = 0.17f;
+      for (int j = 0; j < p.a_rowmax_n; ++j) abound = fmaxf(abound, p.a_rowmax[(int64_t)ir * p.a_rowmax_n + j]);
+    }
   }
   issue(0, 0);
   if (NSTG >= 3 && nk > 1) issue(1, 1);
   if (NSTG >= 4 && nk > 2) issue(2, 2);
   float asc = 1.f, ainv = 1.f;
   if constexpr (TERMS == 2) {
-    asc = pow2_scale14(sqrtf((float)p.K) / arstd);
+    asc = pow2_scale14(AXT == OT_AX_RMSNORM ? sqrtf((float)p.K) / abound : abound);
     ainv = 1.f / asc;
   }
   for (int kt = 0; kt < nk; ++kt) {
@@ -1003,7 +1018,7 @@ __global__ __launch_bounds__(256) void image_colscale_kernel(const float* __rest
                                                              int nd, uint16_t* img) {
   int64_t g, tn, ks;
   const int64_t* d = image_unit(desc, nd, blockIdx.x, g, tn, ks);
-  if (!d || ks != 0 || d[4] < 0) return;
+  if (!d || ks != 0 || d[4] == -1) return;
   const int64_t N = d[8], K = d[9];
   const int n = threadIdx.x >> 1, hh = threadIdx.x & 1;
   const int64_t gn = tn * GT + n;
@@ -1042,7 +1057,7 @@ __global__ __launch_bounds__(256) void split_images_kernel(const float* __restri
   }
   uint16_t* dst = img + d[5] + (unit - d[6]) * (PG_B_BYTES / 2);
   u32x4 pl[3];
-  const bool pair = !one && d[4] >= 0;
+  const bool pair = !one && d[4] != -1;                 // gamma-folded (>= 0) or the -2 pair form
   if (one) {
     split8t<1>(v, pl);                                // OT_MATMUL_BF16: plane 0 = round to nearest
   } else if (pair) {
@@ -1855,6 +1870,14 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
     p.c16_out = rms->c16_out;
     p.ldc16 = rms->ldc16;
   }
+  if (rms && rms->rowmax_out) {
+    p.rowmax_out = rms->rowmax_out;
+    p.rowmax_n = rms->rowmax_n;
+  }
+  if (rms && rms->a_rowmax && a_xform == OT_AX_GELU) {
+    p.a_rowmax = rms->a_rowmax;
+    p.a_rowmax_n = rms->a_rowmax_n;
+  }
   if (rms && ((epi & OT_EPI_GELU_BWD) || (epi & ~OT_EPI_C_BF16) == OT_EPI_BIAS)) {   // the stored GELU (optional)
     p.gelu_out = rms->gelu_out;
     p.ldgelu = rms->ldgelu;
@@ -1930,7 +1953,8 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
 #define OT_PSPEC(AX_, EP_) \
     if (x == AX_ && e == (EP_)) \
       pk = one ? plane_gemm_kernel<AX_, EP_, PLANE_BF16_NSTG, 4, 1> \
-               : plane_gemm_kernel<AX_, EP_, 2, 4, (AX_) == OT_AX_RMSNORM ? 2 : 6>;
+         : (p.a_rowmax ? plane_gemm_kernel<AX_, EP_, 2, 4, ((AX_) == OT_AX_RMSNORM || (AX_) == OT_AX_GELU) ? 2 : 6> \
+                       : plane_gemm_kernel<AX_, EP_, 2, 4, (AX_) == OT_AX_RMSNORM ? 2 : 6>);
     OT_PSPEC(OT_AX_RMSNORM, 0)
     OT_PSPEC(OT_AX_RMSNORM, OT_EPI_BIAS)
     OT_PSPEC(OT_AX_GELU, OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_DROPOUT)

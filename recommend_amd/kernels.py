@@ -237,7 +237,8 @@ def gemm_rms(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish,
              dgamma: Ptrish = None, accumulate_dgamma: bool = False, device=None, bimg=None,
              aux: Ptrish = None, ldaux: int = 0, rowdot: Ptrish = None, rowdot_n: int = 0,
              gelu_out: Ptrish = None, ldgelu: int = 0, xn_out: Ptrish = None, ldxn: int = 0,
-             c16_out: Ptrish = None, ldc16: int = 0) -> None:
+             c16_out: Ptrish = None, ldc16: int = 0, rowmax_out: Ptrish = None, rowmax_n: int = 0,
+             a_rowmax: Ptrish = None, a_rowmax_n: int = 0) -> None:
     """ot_mixed_gemm_rms: the GEMM with a row-norm epilogue (OT_EPI_ROW_RSTD: emit the next RMSNorm's
     rstd; OT_EPI_RMSNORM_BWD: apply the RMSNorm backward to the product, + dres, dgamma, taking
     <gamma dy, x> from ``rowdot`` when N > 128; OT_EPI_GELU_BWD | OT_EPI_ROWDOT: also write each 128-column
@@ -245,14 +246,17 @@ def gemm_rms(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish,
     receives gelu(aux) (with OT_EPI_GELU_BWD) or gelu(C) (epi == OT_EPI_BIAS: the FFN1 forward) rounded to
     bf16 — the OT_AX_BF16 operand of the FFN2 GEMM and the W2 weight gradient.  ``xn_out`` (bf16 bits,
     [in rows][ldxn]; RMSNorm prologue, plane GEMM) receives bf16((A * gamma) * rstd): the normalised A
-    operand of the bf16 weight gradient."""
+    operand of the bf16 weight gradient.  ``rowmax_out`` ([out rows][N / 128], split-mode plane GEMM) receives
+    each column tile's largest C after the bias (the FFN1 forward's U); ``a_rowmax`` hands such maxima of A to a
+    GELU-prologue plane GEMM, which then multiplies on the scaled fp16 pair (its image in the pair form)."""
     need_ws = dgamma is not None or (rstd_out is not None and N > 128)     # dgamma / row-sum partials
     ws = workspace(size('ot_mixed_gemm_rms_workspace_size', ntiles, N) if need_ws else 16,
                    device if device is not None else (C[0] if isinstance(C, tuple) else C).device)
     e = _lib.RmsEpilogue(ctypes.sizeof(_lib.RmsEpilogue), ptr(rstd_out), float(eps), ptr(nx), ldnx, ptr(ngamma), ptr(nrstd), ptr(dres), lddres,
                          dres_tail[0], dres_tail[1], _sel(dres_tail), ptr(dx_masked), lddxm, ptr(dgamma),
                          int(accumulate_dgamma), ptr(ws), ws.numel(), ptr(rowdot), int(rowdot_n),
-                         ptr(gelu_out), int(ldgelu), ptr(xn_out), int(ldxn), ptr(c16_out), int(ldc16))
+                         ptr(gelu_out), int(ldgelu), ptr(xn_out), int(ldxn), ptr(c16_out), int(ldc16),
+                         ptr(rowmax_out), int(rowmax_n), ptr(a_rowmax), int(a_rowmax_n))
     ev = _probe.begin() if _probe is not None else None
     args = (mode, ptr(A), lda, K, ptr(in_rows), a_xform, ptr(rstd), ptr(gamma), ptr(W),
             w_gstride, ldw, N, ptr(tile_group), ntiles, ptr(bias), bias_gstride, ptr(C), ldc, ptr(out_rows), epi,

@@ -104,7 +104,10 @@ class FlatLayout:
                 if Nb % TILE or Kb % 16:
                     continue
                 nu = G * (Nb // TILE) * (Kb // 16)
-                kscale = gamma if (orient == 'fwd' and gamma is not None) else -1
+                # -2: the FFN2 forward's W2 image in the scaled-fp16-pair form (split mode: the GEMM reads U's row
+                # maxima from the FFN1 epilogue, ot_rms_epilogue.a_rowmax); gamma-folded images are pairs too
+                pair_w2 = orient == 'fwd' and name.endswith('.w2') and name.startswith('blk.')
+                kscale = gamma if (orient == 'fwd' and gamma is not None) else (-2 if pair_w2 else -1)
                 irecs.append((o, sn, sk, K * N, kscale, ioff, units, G, Nb, Kb))
                 self.images[(name, orient)] = (ioff, G, Nb, Kb)
                 units += nu

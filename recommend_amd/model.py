@@ -267,6 +267,10 @@ def _block_forward(m, l, x, I, Kq, seed, training, rstd_in=None, select=False, n
     # GELU' / row-dot epilogue (OT_EPI_AUX_BF16), which needs the fused norm2 backward's bf16-dU form
     u_bf = h is not None and m.fuse_bwd2 and not m.fuse_bwd and f % TILE == 0
     u = torch.empty(B * Kq, f, device=dev, dtype=torch.int16 if u_bf else torch.float32)
+    # split mode: the FFN1 epilogue also writes each column tile's row maximum of u, from which the FFN2 plane GEMM
+    # takes its rows' fp16-pair scales (its W2 image is in the pair form, layout kscale -2)
+    umax = (torch.empty(B * Kq, (f + TILE - 1) // TILE, device=dev)
+            if h is None and K.matmul_mode() == 'split' and w2img is not None else None)
     if h is not None:
         K.gemm_rms(OT_GEMM_NT, x1 if x1_16 is None else x1_16, d, d, mt['rows'][1], w1, d * f, d, f,
                    mt['tile_group'], nt, u, f, mt['rows'][1],
@@ -275,6 +279,11 @@ def _block_forward(m, l, x, I, Kq, seed, training, rstd_in=None, select=False, n
                    epi=OT_EPI_BIAS | (OT_EPI_C_BF16 if u_bf else 0),
                    m_rows=maps['tail'].nrows, bimg=m.bimg(f'blk.{l}.w1'), gelu_out=h, ldgelu=f,
                    xn_out=x1n, ldxn=d)
+    elif umax is not None:
+        K.gemm_rms(OT_GEMM_NT, x1 if x1_16 is None else x1_16, d, d, mt['rows'][1], w1, d * f, d, f, mt['tile_group'],
+                   nt, u, f, mt['rows'][1], a_xform=OT_AX_RMSNORM if x1_16 is None else OT_AX_BF16_RMSNORM,
+                   rstd=rstd2, gamma=g2, bias=b1, bias_gstride=f, epi=OT_EPI_BIAS, m_rows=maps['tail'].nrows,
+                   bimg=m.bimg(f'blk.{l}.w1'), rowmax_out=umax, rowmax_n=umax.shape[1])
     else:
         K.gemm(OT_GEMM_NT, x1 if x1_16 is None else x1_16, d, d, mt['rows'][1], w1, d * f, d, f, mt['tile_group'],
                nt, u, f, mt['rows'][1], a_xform=OT_AX_RMSNORM if x1_16 is None else OT_AX_BF16_RMSNORM, rstd=rstd2,
@@ -296,8 +305,14 @@ def _block_forward(m, l, x, I, Kq, seed, training, rstd_in=None, select=False, n
                    mt['rows'][1], a_xform=ax2, bias=b2, bias_gstride=d,
                    epi=OT_EPI_BIAS | OT_EPI_RESIDUAL | dflag | OT_EPI_ROW_RSTD, res=x1, ldres=d, res_tok=0,
                    seed=seed, site=2 * l + 1, drop=rate, tail=tail, m_rows=maps['tail'].nrows,
-                   rstd_out=rstd_out, eps=RMS_EPS, bimg=w2img, c16_out=x2_16, ldc16=d)
+                   rstd_out=rstd_out, eps=RMS_EPS, bimg=w2img, c16_out=x2_16, ldc16=d,
+                   a_rowmax=umax, a_rowmax_n=umax.shape[1] if umax is not None else 0)
         m.put_x16(l + 1, x2, x2_16)
+    elif umax is not None:
+        K.gemm_rms(OT_GEMM_NT, a2, f, f, mt['rows'][1], w2, f * d, f, d, mt['tile_group'], nt, x2, d, mt['rows'][1],
+                   a_xform=ax2, bias=b2, bias_gstride=d, epi=OT_EPI_BIAS | OT_EPI_RESIDUAL | dflag, res=x1,
+                   ldres=d, res_tok=0, seed=seed, site=2 * l + 1, drop=rate, tail=tail,
+                   m_rows=maps['tail'].nrows, bimg=w2img, a_rowmax=umax, a_rowmax_n=umax.shape[1])
     else:
         K.gemm(OT_GEMM_NT, a2, f, f, mt['rows'][1], w2, f * d, f, d, mt['tile_group'], nt, x2, d, mt['rows'][1],
                a_xform=ax2, bias=b2, bias_gstride=d, epi=OT_EPI_BIAS | OT_EPI_RESIDUAL | dflag, res=x1,

@@ -31,6 +31,10 @@ FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: Peak FP32 (matrix), de
 BF16_MFMA_PEAK_TFLOPS = 16 * FP32_MFMA_PEAK_TFLOPS   # "1/16 of BF16" (same table): 2516.8 dense
 SPLIT_TERMS = 6                    # bf16 MFMA products per f32 product in OT_MATMUL_SPLIT_BF16
 HBM_PEAK_GBS = 8000.0
+# dense RMSprop settings of the default bench trajectory: config.py's dense_lr 0.005 with momentum 0.99999 drives the
+# weights to inf within ~100 steps; at these (an optimizer_config train.py:60-66 accepts) the model trains and every
+# timed step runs on finite operands (the kernels' work is the same either way)
+TRAINABLE_OPT = {'dense_lr': 1e-4, 'momentum': 0.9}
 
 
 def parse():
@@ -42,7 +46,16 @@ def parse():
     ap.add_argument('--batch', type=int, default=0, help='per-GPU batch (default: the config\'s)')
     ap.add_argument('--nbatches', type=int, default=4, help='distinct resident batches cycled')
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--cpu-seconds', type=float, default=15.0)
+    ap.add_argument('--cpu-batch', type=int, default=0,
+                    help="samples per CPU-baseline step (default: the config's per-GPU batch)")
+    ap.add_argument('--cpu-steps', type=int, default=2, help='timed CPU-baseline steps (after one warm-up step)')
+    ap.add_argument('--optimizer', default='trainable', choices=['trainable', 'reference'],
+                    help="dense RMSprop settings.  trainable (default): dense_lr 1e-4, momentum 0.9 (an optimizer_config "
+                         "the reference trainer accepts, train.py:60-66), on which the f32 model trains and the loss stays "
+                         "finite; reference: config.py's dense_lr 0.005 / momentum 0.99999, under which the weights blow "
+                         "up within ~100 steps (identical kernel work, but NaN-state operands change kernel timing)")
+    ap.add_argument('--allow-nonfinite', action='store_true',
+                    help='report instead of failing when a repeat ends on a non-finite loss (diagnostics only)')
     ap.add_argument('--no-probe', action='store_true', help='skip the per-kernel HIP-event (roofline) pass')
     ap.add_argument('--probe-steps', type=int, default=10, help='steps of the roofline pass (0: no roofline)')
     ap.add_argument('--repeats', type=int, default=3, help='timed regions of --steps steps; value = median')
@@ -103,10 +116,10 @@ def log(msg):
         print(f'[bench {time.strftime("%H:%M:%S")}] {msg}', file=sys.stderr, flush=True)
 
 
-def cpu_baseline(cfg_name, seconds):
-    """Oracle (torch CPU fp32) fwd+bwd+optimizer steps on the host cores, in both restatements of
-    SURVEY §8d: 'literal' (per-token projection/FFN loops like model.py:84-88, 154-161) and
-    'vectorized'; each gets half of ``seconds``, and the faster one is the baseline."""
+def cpu_baseline(cfg_name, batch, steps, optimizer_config):
+    """Oracle (torch CPU fp32, the vectorized restatement of model.py / train.py) train steps on the host
+    cores at the configured batch: one warm-up step, then ``steps`` timed steps (forward + backward +
+    clip + RMSprop + Adagrad, the GPU step's work)."""
     from recommend_amd.config import workload_config
     from recommend_amd.data import make_batch
     from recommend_amd.params import init_params, keras_variables
@@ -124,37 +137,31 @@ def cpu_baseline(cfg_name, seconds):
     threads = cores if quota is None else max(1, min(cores, int(quota + 0.999)))
     torch.set_num_threads(threads)
     cfg = workload_config(cfg_name)
-    # the oracle's table gradient is dense: cap table cardinalities (transformer work is unchanged)
+    cfg.optimizer_config = dict(optimizer_config)
+    # the oracle's table gradient is dense (a [rows, E] tensor per table): cap the table cardinalities so it
+    # stays small; ids are drawn mod the cap, the transformer work is unchanged
     cfg.sparse_features = {k: min(v, 20000) for k, v in cfg.sparse_features.items()}
     cfg.seq_item_vocab = min(cfg.seq_item_vocab, 50000)
-    B = 64
+    B = batch
     P = init_params(cfg, cfg.ns_input_width(), seed=0)
     kv = keras_variables(cfg, {k: v.shape for k, v in P.items() if not k.startswith('emb.')})
-    batches = [make_batch(B, cfg, seed=7000 + i) for i in range(2)]
-    tb = [tuple(R.to_torch(x, dtype=torch.float32) for x in b) for b in batches]
-    rates = {}
-    for variant in ('vectorized', 'literal'):
-        Pt = R.to_torch(P, dtype=torch.float32)
-        st = R.init_state(Pt, cfg)
-        Pt, st, _, _ = R.train_step(Pt, st, cfg, kv, *tb[0], seed=1, variant=variant)          # warm-up
-        n = 0
-        t0 = time.perf_counter()
-        while True:
-            Pt, st, _, _ = R.train_step(Pt, st, cfg, kv, *tb[n % 2], seed=2 + n, variant=variant)
-            n += 1
-            el = time.perf_counter() - t0
-            if el >= seconds / 2 or n >= 200:
-                break
-        rates[variant] = (B * n / el, n, el)
-        log(f'cpu baseline {variant}: {n} steps in {el:.1f}s on {threads} threads')
-    best = max(rates, key=lambda v: rates[v][0])
-    v, n, el = rates[best]
-    return {'value': round(v, 2), 'unit': 'samples/s', 'cores': torch.get_num_threads(), 'affinity_cores': cores,
-            'cgroup_cpu_quota_cores': quota, 'kind': 'port', 'variant': best,
-            'variants': {k: round(r[0], 2) for k, r in rates.items()},
-            'sample': f'{n} train steps x B={B} of {cfg_name} (full model shape, fp32, {best} oracle '
-                      f'restatement of model.py/train.py, the faster of literal/vectorized; tables capped '
-                      f'at 2e4/5e4 rows), {el:.1f}s'}
+    tb = [tuple(R.to_torch(x, dtype=torch.float32) for x in make_batch(B, cfg, seed=7000 + i)) for i in range(2)]
+    Pt = R.to_torch(P, dtype=torch.float32)
+    st = R.init_state(Pt, cfg)
+    t0 = time.perf_counter()
+    Pt, st, _, _ = R.train_step(Pt, st, cfg, kv, *tb[0], seed=1, variant='vectorized')          # warm-up
+    log(f'cpu baseline: warm-up step (B={B}) {time.perf_counter() - t0:.1f}s on {threads} threads')
+    t0 = time.perf_counter()
+    for n in range(steps):
+        Pt, st, loss, _ = R.train_step(Pt, st, cfg, kv, *tb[(n + 1) % 2], seed=2 + n, variant='vectorized')
+    el = time.perf_counter() - t0
+    log(f'cpu baseline: {steps} steps in {el:.1f}s')
+    return {'value': round(B * steps / el, 2), 'unit': 'samples/s', 'cores': torch.get_num_threads(),
+            'affinity_cores': cores, 'cgroup_cpu_quota_cores': quota, 'kind': 'port', 'variant': 'vectorized',
+            'final_loss': round(float(loss), 5),
+            'sample': f'{steps} train steps x B={B} of {cfg_name} after 1 warm-up step (full model shape, fp32, '
+                      f'the vectorized oracle restatement of model.py / train.py; embedding tables capped at '
+                      f'2e4 / 5e4 rows because the oracle\'s table gradient is dense), {el:.1f}s'}
 
 
 def hbm_traffic(config):
@@ -201,6 +208,8 @@ def main():
         precision = 'fp8attn' if args.config == 'C5' else os.environ.get('ONETRANS_MATMUL', 'split')
     K.set_matmul_mode('bf16' if precision in ('bf16', 'fp8attn') else precision)
     cfg.compute_dtype = {'fp8attn': 'fp8attn', 'bf16': 'bf16'}.get(precision, 'fp32')
+    if args.optimizer == 'trainable':
+        cfg.optimizer_config = dict(cfg.optimizer_config, **TRAINABLE_OPT)
     B = args.batch or cfg._batch
     model = OneTransModel(cfg, device=dev, seed=0)
     if args.no_overlap:
@@ -247,13 +256,18 @@ def main():
         torch.cuda.synchronize()
         return max(wall, ev0.elapsed_time(ev1) / 1e3), o
 
-    times, exposed, route_wait = [], [], []
+    times, exposed, route_wait, losses = [], [], [], []
     log(f'{args.warmup} warm-up steps done')
     for r in range(max(1, args.repeats)):
         for st_ in model.sharded.values():
             st_.route_wait_s = 0.0
         t_r, out = timed_region(args.warmup + r * args.steps)
         times.append(t_r)
+        losses.append(float(out['total_loss'].item()))        # after the region's closing synchronize
+        if not np.isfinite(losses[-1]) and not args.allow_nonfinite:
+            raise SystemExit(f'bench: repeat {r} ended on a non-finite loss ({losses[-1]}); the timed steps ran on '
+                             f'degenerate operands (--allow-nonfinite to report anyway)')
+        log(f'repeat {r}: {1e3 * t_r / args.steps:.3f} ms/step, loss {losses[-1]:.5f}')
         route_wait.append(1e3 * sum(st_.route_wait_s for st_ in model.sharded.values()) / args.steps)
         if exch is not None:
             ms = sum(a.elapsed_time(b) for (a, b) in exch)
@@ -313,7 +327,14 @@ def main():
         'value': round(value, 1), 'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': round(1e3 * t / args.steps, 3), 'higher_is_better': True,
         'scaling': 'weak', 'vs_baseline': None,
-        'dtype': 'bf16' if model.matmul == 'bf16' else 'f32', 'data': 'synthetic', 'precision': precision,
+        # the f32-accurate mode emulates f32 products on 16-bit MFMA: split-bf16 (three planes, six products) and,
+        # for the QKV / FFN1 / FFN2 forward GEMMs and the slice attention, a scaled fp16 pair (22 significant bits
+        # relative to a row / column bound); bf16 is C5's stated reduced precision
+        'dtype': ('bf16' if model.matmul == 'bf16' else
+                  'f32-emulated (fp16-pair / split-bf16)' if model.matmul == 'split' else 'f32'),
+        'data': 'synthetic', 'precision': precision,
+        'optimizer': {'kind': args.optimizer, 'dense_lr': trainer.optimizer.lr,
+                      'momentum': trainer.optimizer.momentum, 'sparse_lr': trainer.optimizer.sparse_lr},
         'config': {'workload': f'{args.config}: OneTrans {cfg.num_layers}L d{cfg.hidden_dim} H{cfg.num_heads} f{cfg.ffn_dim} '
                                f'L_NS{cfg.num_ns_tokens} L_S{sum(seq_lens) + 2} (seq 3x{seq_lens[0]}), '
                                f'Criteo-shape 13 dense + 26 ids, '
@@ -322,7 +343,7 @@ def main():
                    'global_batch': B * world, 'per_gpu_batch': B, 'seq_len': sum(seq_lens) + 2,
                    'parallelism': f'dp{world}'},
         'model_tflops': round(fl['fwd_bwd'] * value / 1e12, 2),
-        'final_loss': round(loss, 5),
+        'final_loss': round(loss, 5), 'loss_repeats': [round(x, 5) for x in losses],
         'repeats': len(times), 'ms_per_step_repeats': [round(1e3 * x / args.steps, 3) for x in times],
         'peak_hbm_gb': round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2),
         'recompute': bool(model.recompute),
@@ -432,7 +453,8 @@ def main():
                 res['attention_mfma']['pmc'] = pmc
     if not args.no_cpu_baseline and world == 1:          # rank 0 at N=1 only
         log('timed region and probe done; CPU baseline')
-        res['cpu_baseline'] = cpu_baseline(args.config, args.cpu_seconds)
+        res['cpu_baseline'] = cpu_baseline(args.config, args.cpu_batch or B, args.cpu_steps,
+                                           cfg.optimizer_config)
     print(json.dumps(res), flush=True)
 
 

@@ -324,7 +324,13 @@ def loss_and_grads(P: Dict[str, Tensor], cfg, ns, seq, labels, training=True, se
     out = forward(leaves, cfg, ns, seq, training=training, seed=seed, variant=variant)
     loss = 0.0
     for t in cfg.tasks:
-        loss = loss + task_loss(t, labels[t].to(out['probs'][t].dtype), out['probs'][t], out['logits'][t])
+        y = labels[t].to(out['probs'][t].dtype)
+        # Keras 2.12 LossFunctionWrapper squeezes y_pred [B,1] to [B] when the labels are [B] (the batched scalar
+        # labels of data_loader.py:215-218's get_tf_dataset); the squeezed tensor has lost the sigmoid's
+        # _keras_logits and is no Sigmoid op, so the clipped probability form applies.  [B,1] labels
+        # (create_sample_batch, data_loader.py:327) keep the logits form.  (Parity unpinned: Keras is absent.)
+        z = out['logits'][t] if y.dim() >= 2 else None
+        loss = loss + task_loss(t, y.reshape(-1), out['probs'][t].reshape(-1), None if z is None else z.reshape(-1))
     loss.backward()
     grads = {k: (v.grad if v.grad is not None else torch.zeros_like(v)) for k, v in leaves.items()}
     return loss.detach(), grads, out

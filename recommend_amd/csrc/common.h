@@ -103,11 +103,14 @@ __device__ __forceinline__ float pow2_scale14(float m) {
   se = e == 0 ? 127 : (se < 1 ? 1 : (se > 254 ? 254 : se));
   return __uint_as_float((uint32_t)se << 23);
 }
+// x s is saturated to the fp16 range first (v_med3_f32): a row bound that under-estimates the operand (a stale or
+// wrong a_rowmax) then gives a deterministic, finite, clipped product instead of an inf plane and inf - inf = NaN
 __device__ __forceinline__ void pair8(const float* v, float s, u32x4 (&pl)[3]) {
   uint32_t a[4], b[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const f32x2_t x = f32x2_t{v[2 * k], v[2 * k + 1]} * s;
+    const f32x2_t x = f32x2_t{__builtin_amdgcn_fmed3f(v[2 * k] * s, -65504.f, 65504.f),
+                              __builtin_amdgcn_fmed3f(v[2 * k + 1] * s, -65504.f, 65504.f)};
     const f16x2_t h = __builtin_convertvector(x, f16x2_t);
     const f16x2_t l = __builtin_convertvector(x - __builtin_convertvector(h, f32x2_t), f16x2_t);
     a[k] = __builtin_bit_cast(uint32_t, h);

@@ -768,6 +768,13 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 template <int TERMS>
 constexpr int pg_stage_bytes() { return PG_A_BYTES + (TERMS == 1 ? GT * 16 * 2 : PG_B_BYTES); }
 
+// Pair-form images carry a tag behind their 128 column scales (plane 2 of the tile's first unit, float 128): the
+// TERMS-2 plane GEMM refuses (all-NaN output) an image without it, and the tag's bytes are two bf16 quiet NaNs, so a
+// six-product kernel handed a pair image multiplies NaN into its outputs (plane 2 at n = 16, k = 0, 1) instead of
+// silently reading the scales as a third bf16 plane.  (The C ABI cannot see an image's form: the host layer pairs
+// the images with a_rowmax, recommend_amd/model.py; this makes a mismatch loud.)
+constexpr uint32_t PAIR_IMAGE_TAG = 0x7FC17FC1u;
+
 // TERMS = 2 (split mode with the RMSNorm prologue): the scaled fp16 pair, three f16 products.  B's image is the pair
 // of B[k][n] s_n (ot_split_images: every gamma-folded image, s_n from the column max); A = x gets one power-of-two
 // scale per row from the bound |x_k| <= sqrt(K) / rstd (sum_k x_k^2 = K (1 / rstd^2 - eps)) — no pass over the row;
@@ -974,9 +981,10 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
     // unscale: row factor 1 / s_a (held by the lane whose A row it is: lane = row within the wave), column
     // factor 1 / s_b (ot_split_images' column scales, plane 2 of the tile's first unit); exact powers of two
     const float* csc = reinterpret_cast<const float*>(bimg0 + 2 * GT * 16 * 2);
+    const float bad = reinterpret_cast<const uint32_t*>(csc)[GT] == PAIR_IMAGE_TAG ? 1.f : __builtin_nanf("");
     float cinv[4];
 #pragma unroll
-    for (int nb = 0; nb < 4; ++nb) cinv[nb] = 1.f / csc[32 * nb + li];
+    for (int nb = 0; nb < 4; ++nb) cinv[nb] = bad / csc[32 * nb + li];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float ri = __shfl(ainv, (r & 3) + 8 * (r >> 2) + 4 * h, 64);
@@ -1033,8 +1041,9 @@ __global__ __launch_bounds__(256) void image_colscale_kernel(const float* __rest
     }
   }
   m = fmaxf(m, __shfl_xor(m, 1, 64));
-  if (hh == 0)
-    reinterpret_cast<float*>(img + d[5] + ((int64_t)blockIdx.x - d[6]) * (PG_B_BYTES / 2) + 2 * GT * 16)[n] = pow2_scale14(m);
+  float* csc = reinterpret_cast<float*>(img + d[5] + ((int64_t)blockIdx.x - d[6]) * (PG_B_BYTES / 2) + 2 * GT * 16);
+  if (hh == 0) csc[n] = pow2_scale14(m);
+  if (threadIdx.x == 0) reinterpret_cast<uint32_t*>(csc)[GT] = PAIR_IMAGE_TAG;   // the form tag (see PAIR_IMAGE_TAG)
 }
 
 __global__ __launch_bounds__(256) void split_images_kernel(const float* __restrict__ base, const int64_t* __restrict__ desc,
@@ -1355,7 +1364,10 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(WgradArgs p) {
         }
         // only D is zeroed, for rows past the chunk or with a negative id: their A (row 0 of the map, clamped
         // columns) is finite, so its products are 0; columns past K / N feed outputs that are never stored
-        // (a 0 / 1 row factor: two packed multiplies instead of four selects; the row is finite)
+        // (a 0 / 1 row factor: two packed multiplies instead of four selects).  Finiteness assumption: row 0 of A
+        // and D must be finite — a non-finite value there (a diverged step) turns the padding rows' 0 * inf into
+        // NaN in every dW tile and bias sum of a chunk with padding, where selects would have kept it to the rows
+        // that hold it.  A diverged step's gradients are NaN anyway; bench.py refuses to time non-finite steps.
         dv = dv * (inr[j] ? 1.f : 0.f);
         bsum[i] += dv;                                  // (unconditional: cheaper than the if-converted select;
                                                         // stored only when do_bias)
@@ -2021,6 +2033,12 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
              "alignment");
   OT_REQUIRE(!p.rowpart || plane, "ot_mixed_gemm_rms: OT_EPI_ROW_RSTD with N = %d > %d needs the plane GEMM "
              "(split mode, a pre-split B image, 16-B aligned A)", N, GT);
+  // the row maxima are written by the split-mode plane GEMM's vector epilogue only (the edge kernels' scalar
+  // epilogue has no row reduction): refuse a call that would leave them unwritten
+  OT_REQUIRE(!p.rowmax_out || (plane && !one && p.rowmax_n == (int)ceil_div(N, GT)),
+             "ot_mixed_gemm_rms: rowmax_out needs the split-mode plane GEMM (pre-split B image, whole tiles, 16-B "
+             "aligned A) and rowmax_n == ceil(N / %d) = %d (got %d)", GT, (int)ceil_div(N, GT), p.rowmax_n);
+  OT_REQUIRE(!p.a_rowmax || p.a_rowmax_n >= 1, "ot_mixed_gemm_rms: a_rowmax needs a_rowmax_n >= 1");
   // (+ K floats of gamma behind the stage buffers for the xn_out side output)
   const size_t xn_lds = p.xn_out ? (size_t)K * 4 : 0;
   const size_t launch_shmem = !plane ? shmem

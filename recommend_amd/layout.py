@@ -93,6 +93,9 @@ class FlatLayout:
         # and 'dgrad' (B = W); only where the GEMM has whole 128-column tiles and 16-k stages
         self.images: Dict[Tuple[str, str], Tuple[int, int, int, int]] = {}   # -> (offset, G, N, K)
         irecs, units, ioff = [], 0, 0
+        # images written in the scaled-fp16-pair form in split mode (gamma-folded, kscale >= 0, and the FFN2 W2
+        # forward image, kscale -2): the plane GEMM reads them with three f16 products only
+        self.pair_images = set()
         for name, (G, K, N) in self.gemm_banks.items():
             o = self.offsets[name]
             gamma = None
@@ -106,10 +109,15 @@ class FlatLayout:
                 nu = G * (Nb // TILE) * (Kb // 16)
                 # -2: the FFN2 forward's W2 image in the scaled-fp16-pair form (split mode: the GEMM reads U's row
                 # maxima from the FFN1 epilogue, ot_rms_epilogue.a_rowmax); gamma-folded images are pairs too
-                pair_w2 = orient == 'fwd' and name.endswith('.w2') and name.startswith('blk.')
+                # (only when W1's forward image exists too, f % 128 == 0 and d % 16 == 0: the FFN1 forward then runs on
+                # the plane GEMM, whose epilogue writes those maxima — OneTransModel allocates them under pair_form())
+                pair_w2 = (orient == 'fwd' and name.endswith('.w2') and name.startswith('blk.')
+                           and K % TILE == 0 and N % 16 == 0)
                 kscale = gamma if (orient == 'fwd' and gamma is not None) else (-2 if pair_w2 else -1)
                 irecs.append((o, sn, sk, K * N, kscale, ioff, units, G, Nb, Kb))
                 self.images[(name, orient)] = (ioff, G, Nb, Kb)
+                if kscale != -1:
+                    self.pair_images.add((name, orient))
                 units += nu
                 ioff += nu * IMAGE_UNIT_ELEMS
         self.image_desc = np.array(irecs, dtype=np.int64).reshape(-1, 10)

@@ -269,8 +269,13 @@ def _block_forward(m, l, x, I, Kq, seed, training, rstd_in=None, select=False, n
     u = torch.empty(B * Kq, f, device=dev, dtype=torch.int16 if u_bf else torch.float32)
     # split mode: the FFN1 epilogue also writes each column tile's row maximum of u, from which the FFN2 plane GEMM
     # takes its rows' fp16-pair scales (its W2 image is in the pair form, layout kscale -2)
-    umax = (torch.empty(B * Kq, (f + TILE - 1) // TILE, device=dev)
-            if h is None and K.matmul_mode() == 'split' and w2img is not None else None)
+    # (exactly when W2's forward image is in the pair form, layout.pair_images: then W1's forward image exists, f % 128
+    # == 0, and the FFN1 plane GEMM below writes every row's maxima; the library refuses rowmax_out anywhere else and a
+    # pair image read without them multiplies NaN into the output)
+    pair_w2 = K.matmul_mode() == 'split' and w2img is not None and (f'blk.{l}.w2', 'fwd') in m.layout.pair_images
+    assert not pair_w2 or (h is None and m.bimg(f'blk.{l}.w1') is not None and f % TILE == 0), \
+        'the pair-form W2 image needs the FFN1 plane GEMM to write the row maxima of u'
+    umax = torch.empty(B * Kq, f // TILE, device=dev) if pair_w2 else None
     if h is not None:
         K.gemm_rms(OT_GEMM_NT, x1 if x1_16 is None else x1_16, d, d, mt['rows'][1], w1, d * f, d, f,
                    mt['tile_group'], nt, u, f, mt['rows'][1],
@@ -634,14 +639,16 @@ def task_mse_mask(tasks) -> int:
     return sum(1 << i for i, t in enumerate(tasks) if t not in BINARY_TASKS)
 
 
-def keras_bce_loss(labels: torch.Tensor, probs: torch.Tensor, tasks=None) -> torch.Tensor:
+def keras_bce_loss(labels: torch.Tensor, probs: torch.Tensor, tasks=None, label_rank: int = 2) -> torch.Tensor:
     """Sum over tasks of the reference's per-task loss; labels/probs [T, B] device tensors.  ``tasks``
     (names, in row order) selects MSE for tasks other than 'ctr'/'cvr'; None = BCE for every row.
     Probabilities from ``OneTransModel.forward_probs`` carry their heads' logits (``_ot_logits``, as Keras's
-    sigmoid output carries ``_keras_logits``) and the BCE is taken from those; other probabilities use the
-    clipped probability form."""
+    sigmoid output carries ``_keras_logits``) and the BCE is taken from those when the caller's labels were
+    [B, 1] (``label_rank`` 2: create_sample_batch, data_loader.py:327).  Keras 2.12 squeezes the [B, 1]
+    prediction to [B] for [B] labels (get_tf_dataset's batched scalars, data_loader.py:215-218), which drops
+    the cached logits: ``label_rank`` 1 and probabilities without logits use the clipped probability form."""
     mask = task_mse_mask(tasks) if tasks is not None else 0
-    z = getattr(probs, '_ot_logits', None)
+    z = getattr(probs, '_ot_logits', None) if label_rank >= 2 else None
     if z is not None:
         return _TaskLoss.apply(probs, z, labels, mask)
     return _BCE.apply(probs, labels, mask)
@@ -938,7 +945,7 @@ class OneTransModel(nn.Module):
         return self._aux_maps[key]
 
     # ---------------------------------------------------------------- input plan
-    def _plan(self, ns: Dict[str, torch.Tensor], seq: Dict[str, torch.Tensor]):
+    def _plan(self, ns: Dict[str, torch.Tensor], seq: Dict[str, torch.Tensor], training: bool = False):
         cfg = self.config
         d = cfg.hidden_dim
         dev = self.device
@@ -946,7 +953,7 @@ class OneTransModel(nn.Module):
         seq_names = cfg.feature_config['sequence_features']
         present = [(i, n, int(seq[n].shape[1])) for i, n in enumerate(seq_names) if n in seq]
         ns_present = tuple(n for n in cfg.ns_feature_names() if n in ns)
-        id_seq = bool(cfg.seq_item_vocab) and bool(present) and not torch.is_floating_point(seq[present[0][1]])
+        id_seq = bool(cfg.seq_item_vocab) and bool(present) and not torch.is_floating_point(torch.as_tensor(seq[present[0][1]]))
         key = (B, tuple(present), ns_present, id_seq)
         plan = self._plans.get(key)
         if plan is None:
@@ -968,10 +975,15 @@ class OneTransModel(nn.Module):
                 # and routed on the table's route stream (host ids copied there, device ids after
                 # ``inputs_ready``), so its one host wait does not drain the main stream
                 st = self.sharded['emb.seq_item']
-                ids = [seq[n] if isinstance(seq[n], torch.Tensor) else torch.from_numpy(np.asarray(seq[n]))
-                       for (_, n, _) in present]
-                routed, self._pending_route = self._pending_route, None     # route_ahead() of these ids
-                plan['seq_A'] = st.lookup(ids, ready=self.inputs_ready, routed=routed)
+                srcs = [seq[n] for (_, n, _) in present]
+                ids = [s_ if isinstance(s_, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(s_)) for s_ in srcs]
+                # route_ahead() routed the next TRAINING forward's ids: only a training forward consumes it (an
+                # evaluation forward in between routes its own ids), and it must be handed the very id objects
+                # that were routed (PendingRoute.matches)
+                routed = None
+                if training and self._pending_route is not None:
+                    routed, self._pending_route = self._pending_route, None
+                plan['seq_A'] = st.lookup(ids, ready=self.inputs_ready, routed=routed, srcs=srcs)
                 plan['seq_ids'] = st.last_ids
                 plan['seq_route'] = st.last_route
             elif id_seq:
@@ -1091,7 +1103,7 @@ class OneTransModel(nn.Module):
     @in_model_precision
     def forward_probs(self, ns, seq, training: bool) -> torch.Tensor:
         """All tasks as one [T, B] tensor (the trainer's fused loss consumes it)."""
-        plan = self._plan(ns, seq)
+        plan = self._plan(ns, seq, training)
         seed = 0
         if training:
             self._step += 1
@@ -1120,9 +1132,9 @@ class OneTransModel(nn.Module):
         names = [n for n in self.config.feature_config['sequence_features'] if n in seq_features]
         if not names or torch.is_floating_point(torch.as_tensor(seq_features[names[0]])):
             return
-        ids = [seq_features[n] if isinstance(seq_features[n], torch.Tensor)
-               else torch.from_numpy(np.asarray(seq_features[n])) for n in names]
-        self._pending_route = self.sharded['emb.seq_item'].route(ids, ready=self.inputs_ready)
+        srcs = [seq_features[n] for n in names]
+        ids = [s_ if isinstance(s_, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(s_)) for s_ in srcs]
+        self._pending_route = self.sharded['emb.seq_item'].route(ids, ready=self.inputs_ready, srcs=srcs)
 
     def batch_offset(self, B: int) -> int:
         """Index of this process's first sample in the global batch (dropout masks are a function of the

@@ -104,13 +104,13 @@ class ShardedTable:
         else:
             dist.all_to_all_single(out, inp, out_splits, in_splits)
 
-    def route(self, ids, ready=None) -> 'PendingRoute':
+    def route(self, ids, ready=None, srcs=None) -> 'PendingRoute':
         """Look-ahead routing: stage ``ids`` and issue their routing (sort by owner, the split-size all-to-all,
         the split sizes' copy to the host) on the route stream now, and return without waiting; ``lookup(ids,
         routed=<the result>)`` later takes the routed ids (its host wait then finds the sizes already there).
         The trainer routes step i + 1's ids during step i (OneTransTrainer.train_step(next_batch=...)), so at
         N > 1 the split-size exchange overlaps step i's backward instead of stalling step i + 1's start."""
-        return PendingRoute(self, ids, *self._issue_route(ids, ready))
+        return PendingRoute(self, ids if srcs is None else srcs, *self._issue_route(ids, ready))
 
     def _route(self, ids, ready):
         """Stage ``ids`` (a tensor or a list concatenated in order; host or device) and route them by owner
@@ -170,16 +170,17 @@ class ShardedTable:
         both = host_counts.tolist()
         return ids_d, bufs, both[:self.world], both[self.world:]
 
-    def lookup(self, ids, ready=None, routed: 'PendingRoute' = None) -> torch.Tensor:
+    def lookup(self, ids, ready=None, routed: 'PendingRoute' = None, srcs=None) -> torch.Tensor:
         """Rows of ``ids`` (int64 [n], or a list of id tensors taken in order; host or device) -> [n, E] fp32
         (zeros for ids outside the table); the staged device ids are kept in ``last_ids``.  ``ready``:
         for device ids, the HIP event after which they are valid (True: already complete, e.g. resident
-        batches; None: wait for the current stream).  ``routed``: these ids' look-ahead ``route()``."""
+        batches; None: wait for the current stream).  ``routed``: these ids' look-ahead ``route()``, made from
+        ``srcs`` (the caller's id objects, when ``ids`` are tensors made from them; default ``ids``)."""
         ev0 = self._mark()
         E, dev = self.E, self.device
         t0 = time.perf_counter()
         if routed is not None:
-            if not routed.matches(self, ids):
+            if not routed.matches(self, ids if srcs is None else srcs):
                 raise ValueError(f'{self.name}: lookup with a look-ahead route of other ids')
             ids_d, bufs, send_splits, recv_splits = self._finish_route(*routed.parts)
         else:
@@ -265,13 +266,20 @@ class ShardedTable:
 
 class PendingRoute:
     """A look-ahead route (ShardedTable.route): the staged ids' routing issued on the route stream, not yet
-    waited for.  Identified by the id tensors it was made from."""
+    waited for.  Identified by the id objects it was made from (tensors or host arrays), which it keeps alive:
+    ``matches`` requires the very same objects, and for tensors an unchanged version counter, so a loader that
+    reuses a buffer's address for new ids (a new tensor) or writes new ids into it through torch is refused.
+    (Writes that bypass torch — into a numpy array that was routed — cannot be seen: a loader must not refill a
+    batch it has passed as ``next_batch``.)"""
 
-    def __init__(self, table, ids, *parts):
+    def __init__(self, table, srcs, *parts):
         self.table = table
-        self.key = tuple((t.data_ptr(), tuple(t.shape)) for t in (ids if isinstance(ids, (list, tuple)) else [ids]))
+        self.srcs = list(srcs) if isinstance(srcs, (list, tuple)) else [srcs]
+        self.versions = [t._version if isinstance(t, torch.Tensor) else None for t in self.srcs]
         self.parts = parts
 
-    def matches(self, table, ids) -> bool:
-        key = tuple((t.data_ptr(), tuple(t.shape)) for t in (ids if isinstance(ids, (list, tuple)) else [ids]))
-        return table is self.table and key == self.key
+    def matches(self, table, srcs) -> bool:
+        srcs = list(srcs) if isinstance(srcs, (list, tuple)) else [srcs]
+        return (table is self.table and len(srcs) == len(self.srcs)
+                and all(a is b for a, b in zip(srcs, self.srcs))
+                and all(v is None or b._version == v for b, v in zip(self.srcs, self.versions)))

@@ -36,12 +36,21 @@ def _to_dev(d: Dict, dev) -> Dict[str, torch.Tensor]:
     return out
 
 
-def _seq_inputs(model, seq: Dict, dev) -> Dict[str, torch.Tensor]:
-    """Sequence features for forward_probs: with a row-sharded item table the id sequences stay host
-    tensors — the lookup copies them on the table's route stream, off the main stream (sharded.py)."""
+def _seq_inputs(model, seq: Dict, dev) -> Dict:
+    """Sequence features for forward_probs: with a row-sharded item table the id sequences stay as the caller
+    gave them (host arrays or tensors) — the lookup copies them on the table's route stream, off the main stream
+    (sharded.py), and a look-ahead route (route_ahead) is matched against these very objects."""
     if not getattr(model, 'sharded', None):
         return _to_dev(seq, dev)
-    return {k: v if isinstance(v, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(v)) for k, v in seq.items()}
+    return dict(seq)
+
+
+def label_rank(labels) -> int:
+    """Rank of the caller's per-task labels: 1 for [B] (get_tf_dataset's batched scalars), 2 for [B, 1]
+    (create_sample_batch) and for an already stacked [T, B] tensor.  It picks the BCE form (keras_bce_loss)."""
+    if isinstance(labels, torch.Tensor):
+        return 2
+    return min(2, max(np.ndim(v) for v in labels.values()))
 
 
 def stack_labels(labels: Dict, tasks, dev) -> torch.Tensor:
@@ -249,7 +258,7 @@ class OneTransTrainer:
         probs = self.model.forward_probs(_to_dev(non_seq, dev), _seq_inputs(self.model, seq, dev), training=True)
         if next_batch is not None and self.model.sharded:
             self.model.route_ahead(_seq_inputs(self.model, next_batch[1], dev))
-        loss = keras_bce_loss(y, probs, self.config.tasks)
+        loss = keras_bce_loss(y, probs, self.config.tasks, label_rank(labels))
         self.optimizer.begin_backward()
         loss.backward()
         self.optimizer.step()
@@ -262,7 +271,7 @@ class OneTransTrainer:
         dev = self.device
         y = labels if isinstance(labels, torch.Tensor) else stack_labels(labels, self.config.tasks, dev)
         probs = self.model.forward_probs(_to_dev(non_seq, dev), _seq_inputs(self.model, seq, dev), training=False)
-        loss = keras_bce_loss(y, probs, self.config.tasks)
+        loss = keras_bce_loss(y, probs, self.config.tasks, label_rank(labels))
         return {'total_loss': loss, 'probs': probs}
 
     def evaluate(self, batches) -> Dict[str, float]:

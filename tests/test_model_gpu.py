@@ -107,6 +107,35 @@ def test_gradient_parity(dev, case, training):
     check_grads(cfg, 37 if case.startswith('criteo') else 64, dev, training)
 
 
+@pytest.mark.parametrize('rank', [1, 2])
+def test_loss_form_follows_label_rank(dev, rank):
+    """The trainer's BCE form follows the labels' rank as Keras 2.12's squeeze rule does: [B] labels ->
+    clipped probabilities, [B, 1] -> the sigmoid head's logits.  Saturated heads (b2 + 40) against all-zero labels
+    separate the forms; loss and every gradient vs the oracle given the same labels."""
+    cfg = CASES['criteo_head']()
+    cfg.dropout_rate = 0.0
+    P = init_params(cfg, cfg.ns_input_width(), seed=0, perturb=True)
+    P['head.b2'] = P['head.b2'] + 40.0
+    model = OneTransModel(cfg, device=dev, init=P)
+    tr = OneTransTrainer(cfg, model=model)
+    ns, seq, lab = make_batch(37, cfg, seed=1000)
+    lab = {t: np.zeros((37, 1) if rank == 2 else (37,), np.float32) for t in cfg.tasks}
+    model.flat.grad.fill_(float('nan'))
+    out = tr.val_step((ns, seq, lab))
+    # (the oracle in float32, as Keras computes: at p = sigmoid(40) the clipped form reads 1 - (1 - 1e-7) + 1e-7,
+    # whose f32 value is 2.19e-7 against float64's 2e-7 — the f32 rounding of the clip bound, not a kernel error)
+    f32 = lambda x: R.to_torch(x, dtype=torch.float32)
+    rl, rg, _ = R.loss_and_grads(f32(P), cfg, f32(ns), f32(seq), f32(lab), training=False)
+    assert abs(out['total_loss'].item() - rl.item()) < 1e-4 * max(1.0, abs(rl.item()))
+    from recommend_amd.trainer import label_rank
+    probs = model.forward_probs(ns_t(ns, dev), ns_t(seq, dev), training=False)
+    keras_bce_loss(stack_labels(lab, cfg.tasks, dev), probs, cfg.tasks, label_rank(lab)).backward()
+    for name in ('head.w2', 'head.b2', 'blk.0.w1'):
+        r = rg[name].double()
+        g = model.g(name).double().cpu().reshape(r.shape)
+        assert (g - r).abs().max().item() <= 2e-4 * max(1e-3, r.abs().max().item()), name
+
+
 @pytest.mark.parametrize('case', ['criteo_d128_pyramid', 'criteo_norm_pyramid'])
 @pytest.mark.parametrize('B', [1, 2, 129])
 def test_edge_batches(dev, case, B):

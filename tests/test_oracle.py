@@ -126,6 +126,31 @@ def test_bce_clip_rmsprop_kat():
     np.testing.assert_allclose(w, 1.0 - m)
 
 
+def test_loss_form_follows_label_rank():
+    """Keras 2.12's squeeze rule: [B, 1] labels keep the sigmoid head's logits form, [B] labels
+    (get_tf_dataset's batched scalars, data_loader.py:215-218) the clipped probability form.  Saturated heads
+    (|z| = 40) tell the two apart by orders of magnitude."""
+    from recommend_amd.config import workload_config
+    from recommend_amd.data import make_batch
+    from recommend_amd.params import init_params
+    cfg = workload_config('C1')
+    cfg.num_layers, cfg.dropout_rate = 1, 0.0
+    P = R.to_torch(init_params(cfg, cfg.ns_input_width(), seed=3))
+    P['head.b2'] = P['head.b2'] + 40.0                    # saturated heads: z ~ 40
+    ns, seq, lab = make_batch(8, cfg, seed=5)
+    for t in cfg.tasks:
+        lab[t][:] = 0.0                                      # every sample wrong-sided against the saturated head
+    out = R.forward(P, cfg, R.to_torch(ns), R.to_torch(seq), training=False)
+    l2, _, _ = R.loss_and_grads(P, cfg, R.to_torch(ns), R.to_torch(seq), R.to_torch(lab), training=False)
+    l1, _, _ = R.loss_and_grads(P, cfg, R.to_torch(ns), R.to_torch(seq),
+                                R.to_torch({t: v.reshape(-1) for t, v in lab.items()}), training=False)
+    y = {t: torch.tensor(lab[t].reshape(-1), dtype=torch.float64) for t in cfg.tasks}
+    want2 = sum(R.keras_bce_logits(y[t], out['logits'][t].reshape(-1)) for t in cfg.tasks)
+    want1 = sum(R.keras_bce(y[t], out['probs'][t].reshape(-1)) for t in cfg.tasks)
+    assert abs(l2.item() - want2.item()) < 1e-10 and abs(l1.item() - want1.item()) < 1e-10
+    assert l2.item() != pytest.approx(l1.item(), rel=0.1)
+
+
 def test_auc_kat():
     y = np.array([0, 0, 1, 1])
     s = np.array([0.1, 0.4, 0.35, 0.8])

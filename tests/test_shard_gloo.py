@@ -184,3 +184,21 @@ def test_sharded_exchange_world4_with_empty_peers(dedup, lookahead):
     for r, (n, recv, el, ea) in res.items():
         assert el == 0.0, (r, el)
         assert ea < 1e-6, (r, ea)
+
+
+def test_pending_route_identity():
+    """A look-ahead route matches only the very id objects it was made from, unchanged: not a copy,
+    not a tensor written in place since, not another table."""
+    from recommend_amd.sharded import PendingRoute
+    table = object()
+    ids = torch.arange(10)
+    pr = PendingRoute(table, [ids], None)
+    assert pr.matches(table, [ids]) and pr.matches(table, ids)
+    assert not pr.matches(table, [ids.clone()])
+    assert not pr.matches(object(), [ids])
+    assert not pr.matches(table, [ids, ids])
+    ids.add_(1)                                   # same address, new contents
+    assert not pr.matches(table, [ids])
+    arr = np.arange(5)
+    pr2 = PendingRoute(table, [arr], None)
+    assert pr2.matches(table, [arr]) and not pr2.matches(table, [arr.copy()])

@@ -159,12 +159,24 @@ typedef struct ot_rms_epilogue {
                                                           largest C value after the bias (signed) at
                                                           [out_row][tile] (rowmax_n = N / 128): the FFN1 forward's
                                                           row maxima of U for the FFN2 GEMM's a_rowmax */
-  const float* a_rowmax; int a_rowmax_n;               /* optional, split-mode plane GEMM with the GELU prologue:
+  const float* a_rowmax; int a_rowmax_n;               /* optional, split-mode plane GEMM with the GELU prologue
+                                                          (or none: then the parts are max |a|, e.g. rowabs_out /
+                                                          ot_dropout_apply_ex / ot_rows_absmax of A's producer):
                                                           the A rows' partial maxima [in_row][a_rowmax_n] (as
                                                           rowmax_out wrote them); the GEMM then multiplies on the
                                                           scaled fp16 pair, the row scale from max(max_j a_rowmax,
                                                           0.17) >= max |gelu(a)|, and b_image must be a pair image
                                                           (desc kscale_off -2, ot_split_images) */
+  float* amax_out;                                     /* optional, whole-tile kernels: *amax_out = max(*amax_out,
+                                                          max |v|) over the values v the epilogue stores for the next
+                                                          consumer (dx_masked when written, else C), by one atomic
+                                                          per wave (order-independent, deterministic); the caller
+                                                          zeroes it first.  The |D| / |A| bound of the fp16-pair
+                                                          weight gradient (ot_mixed_gemm_wgrad_ex) */
+  float* rowabs_out; int rowabs_n;                     /* optional, whole-tile kernels: each 128-column tile's max
+                                                          |v| of every output row (v as for amax_out) at
+                                                          [out_row][tile], rowabs_n = ceil(N / 128): the row bounds
+                                                          (a_rowmax) of an fp16-pair consumer GEMM whose A this is */
 } ot_rms_epilogue;
 size_t ot_mixed_gemm_rms_workspace_size(int ntiles, int N);
 int ot_mixed_gemm_rms(int mode, const float* A, int64_t lda, int K, const int32_t* in_rows,
@@ -189,6 +201,22 @@ int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a_rows, int 
                         const int32_t* chunks, int nchunks, const int32_t* gchunk, int ngroups,
                         float* dW, int64_t dw_gstride, float* db, int64_t db_gstride,
                         int accumulate, void* workspace, size_t ws_bytes, int precision, void* stream);
+
+/* ot_mixed_gemm_wgrad on the scaled fp16 pair (OT_MATMUL_SPLIT_BF16, f32 operands, a_xform OT_AX_NONE /
+ * OT_AX_RMSNORM / OT_AX_GELU): A column k and D are scaled by powers of two from magnitude bounds and split into an
+ * fp16 pair (x s = h + l, 22 significant bits of each element down to 2^-16 of its bound), three f16 products per
+ * f32 product instead of the six bf16 ones.  d_bound: one float >= max |D| over the rows used; a_bound: one float
+ * >= max |A'| of the transformed A (GELU: >= max |A|, since |gelu(u)| <= |u|), not needed with OT_AX_RMSNORM
+ * (|x_k rstd gamma_k| <= sqrt(K) |gamma_k|).  The bounds are device pointers, typically the amax outputs of the
+ * operands' producers (ot_rms_epilogue.amax_out, ot_dropout_apply_ex, ot_attn_fwd_amax, ot_attn_bwd_amax).
+ * With d_bound NULL (or a_bound NULL where needed, or another mode / form) the call is ot_mixed_gemm_wgrad. */
+int ot_mixed_gemm_wgrad_ex(const float* A, int64_t lda, const int32_t* a_rows, int a_xform,
+                           const float* a_rstd, const float* a_gamma,
+                           const float* D, int64_t ldd, const int32_t* d_rows, int K, int N,
+                           const int32_t* chunks, int nchunks, const int32_t* gchunk, int ngroups,
+                           float* dW, int64_t dw_gstride, float* db, int64_t db_gstride,
+                           int accumulate, void* workspace, size_t ws_bytes, const float* a_bound,
+                           const float* d_bound, int precision, void* stream);
 
 /* Transposed weight shadow for the forward GEMMs (NT staging reads k-contiguous rows):
  * dst[g][n][k] = src[g][k][n] per bank; banks_dev: [nbanks][6] int64 {src_off, dst_off, G, K, N,
@@ -321,6 +349,17 @@ int ot_attn_slice_supported(int I, int K, int head_dim, int selected);
 int ot_attn_bwd_flags(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
                       int B, int H, int I, int K, const int32_t* qpos, int head_dim, void* dqkv, int flags,
                       void* workspace, size_t ws_bytes, int precision, void* stream);
+/* Output bounds for the fp16-pair weight gradients (ot_mixed_gemm_wgrad_ex): ot_attn_fwd / ot_attn_bwd_ex that also
+ * fold max |O| (forward) or max |dQKV| (backward) into *amax (one float the caller zeroes; atomic max, deterministic).
+ * Only where the slice kernels run the shape — ot_attn_amax_supported: bit 1 the forward (OT_MATMUL_SPLIT_BF16, K > 4,
+ * the slice forward's shapes), bit 2 the backward (also qpos NULL, the slice backward's shapes; it needs
+ * ot_attn_bwd_flags_workspace_size bytes) — elsewhere the call is refused. */
+int ot_attn_amax_supported(int I, int K, int head_dim, int selected, int precision);
+int ot_attn_fwd_amax(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos,
+                     int head_dim, float* out, float* lse, float* amax, int precision, void* stream);
+int ot_attn_bwd_amax(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
+                     int B, int H, int I, int K, const int32_t* qpos, int head_dim, float* dqkv,
+                     void* workspace, size_t ws_bytes, float* amax, int precision, void* stream);
 
 /* Two-stage cached serving (paper §3.5.1; replaces the reference's defective cache path
  * model.py:94-98, 359-381, D6): candidate c (request req[c]) attends with the last Kq of its n
@@ -359,6 +398,15 @@ int ot_rmsnorm_bwd(const float* dy, int64_t lddy, const float* x, int64_t ldx, c
 int ot_dropout_apply(const float* src, int64_t lds, float* dst, int64_t ldd, int64_t rows, int d,
                      uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
                      const int32_t* tail_pos, void* stream);
+/* ot_dropout_apply that also reports the output's magnitude for fp16-pair consumers: amax (optional, one float the
+ * caller zeroes) = max(*amax, max |out|) (atomic, order-independent); rowmax (optional, [rows][rowmax_n], rowmax_n =
+ * ceil(d / 256), d / 4 a power of two or a multiple of 64) = max |out| of each row's 256-column parts */
+int ot_dropout_apply_ex(const float* src, int64_t lds, float* dst, int64_t ldd, int64_t rows, int d,
+                        uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
+                        const int32_t* tail_pos, float* amax, float* rowmax, int rowmax_n, void* stream);
+/* out[r][j] = max |x[r][c]| over c in [256 j, 256 j + 256) (parts = ceil(d / 256)): the row bounds (a_rowmax) of an
+ * fp16-pair GEMM whose A has no producer that reports them */
+int ot_rows_absmax(const float* x, int64_t ldx, int64_t rows, int d, float* out, int parts, void* stream);
 /* ot_dropout_apply with the masked rows stored rounded to bf16 (uint16 bits, ldd in elements): the bf16
  * mode's dY of the FFN2 GEMM, whose consumers (the FFN2 dgrad's A operand, the W2 weight gradient's D)
  * round it to bf16 anyway */

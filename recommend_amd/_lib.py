@@ -45,7 +45,8 @@ class RmsEpilogue(ctypes.Structure):
                 ('xn_out', c_void_p), ('ldxn', c_int64),
                 ('c16_out', c_void_p), ('ldc16', c_int64),
                 ('rowmax_out', c_void_p), ('rowmax_n', c_int),
-                ('a_rowmax', c_void_p), ('a_rowmax_n', c_int)]
+                ('a_rowmax', c_void_p), ('a_rowmax_n', c_int),
+                ('amax_out', c_void_p), ('rowabs_out', c_void_p), ('rowabs_n', c_int)]
 
 P = c_void_p
 I64 = c_int64
@@ -65,6 +66,8 @@ SIGNATURES = {
     'ot_wgrad_workspace_size': (c_size_t, [c_int, c_int, c_int]),
     'ot_mixed_gemm_wgrad': (c_int, [P, I64, P, c_int, P, P, P, I64, P, c_int, c_int, P, c_int, P, c_int, P,
                                     I64, P, I64, c_int, P, c_size_t, c_int, P]),
+    'ot_mixed_gemm_wgrad_ex': (c_int, [P, I64, P, c_int, P, P, P, I64, P, c_int, c_int, P, c_int, P, c_int, P,
+                                       I64, P, I64, c_int, P, c_size_t, P, P, c_int, P]),
     'ot_transpose_banks': (c_int, [P, P, P, c_int, I64, P]),
     'ot_mixed_gemm_img': (c_int, [c_int, P, I64, c_int, P, c_int, P, P, P, I64, I64, c_int, P, c_int, P, I64,
                                   P, I64, P, c_int, P, I64, c_int, P, I64, c_uint32, c_uint32, c_float, c_int,
@@ -89,6 +92,9 @@ SIGNATURES = {
     'ot_attn_bwd_flags_workspace_size': (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int]),
     'ot_attn_bwd_flags': (c_int, [P, I64, P, P, P, c_int, c_int, c_int, c_int, P, c_int, P, c_int, P, c_size_t, c_int, P]),
     'ot_attn_fwd_cached': (c_int, [P, I64, P, I64, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
+    'ot_attn_amax_supported': (c_int, [c_int, c_int, c_int, c_int, c_int]),
+    'ot_attn_fwd_amax': (c_int, [P, I64, c_int, c_int, c_int, c_int, P, c_int, P, P, P, c_int, P]),
+    'ot_attn_bwd_amax': (c_int, [P, I64, P, P, P, c_int, c_int, c_int, c_int, P, c_int, P, P, c_size_t, P, c_int, P]),
     'ot_pyramid_select': (c_int, [P, c_float, c_int, c_int, c_int, c_int, P, P, P, c_int, P]),
     'ot_rmsnorm_fwd': (c_int, [P, I64, P, P, I64, P, I64, c_int, c_float, P]),
     'ot_rmsnorm_bwd_workspace_size': (c_size_t, [I64, c_int]),
@@ -96,6 +102,9 @@ SIGNATURES = {
                                c_uint32, c_float, c_int, c_int, P, P, c_int, I64, c_int, P, c_size_t, P]),
     'ot_dropout_apply': (c_int, [P, I64, P, I64, I64, c_int, c_uint32, c_uint32, c_float, c_int, c_int, P, P]),
     'ot_dropout_apply_bf16': (c_int, [P, I64, P, I64, I64, c_int, c_uint32, c_uint32, c_float, c_int, c_int, P, P]),
+    'ot_rows_absmax': (c_int, [P, I64, I64, c_int, P, c_int, P]),
+    'ot_dropout_apply_ex': (c_int, [P, I64, P, I64, I64, c_int, c_uint32, c_uint32, c_float, c_int, c_int, P, P, P,
+                                    c_int, P]),
     'ot_rows_colsum_workspace_size': (c_size_t, [I64, c_int]),
     'ot_rows_colsum': (c_int, [P, I64, P, I64, c_int, P, c_int, P, c_size_t, P]),
     'ot_ns_assemble': (c_int, [P, c_int, P, c_int, P, I64, P]),

@@ -1691,8 +1691,32 @@ extern "C" int ot_attn_fwd_cached(const float* qkv, int64_t ld, const float* kv_
 }
 
 
+static int attn_fwd_impl(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos,
+                         int head_dim, float* out, float* lse, int precision, void* stream, float* amax);
+
 extern "C" int ot_attn_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos,
                            int head_dim, float* out, float* lse, int precision, void* stream) {
+  return attn_fwd_impl(qkv, ld, B, H, I, K, qpos, head_dim, out, lse, precision, stream, nullptr);
+}
+
+extern "C" int ot_attn_amax_supported(int I, int K, int head_dim, int selected, int precision) {
+  // the slice kernels fold max |output| in as they store: bit 1 the forward (O), bit 2 the backward (dQKV, tail
+  // queries; its long forms reach I 544 at head_dim 64)
+  if (precision != OT_MATMUL_SPLIT_BF16 || K <= SMALL_K) return 0;
+  return (attn_slice_fwd_supported(I, K, head_dim) ? 1 : 0) |
+         (!selected && attn_slice_bwd_supported(I, K, head_dim, false) ? 2 : 0);
+}
+
+extern "C" int ot_attn_fwd_amax(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos,
+                                int head_dim, float* out, float* lse, float* amax, int precision, void* stream) {
+  OT_REQUIRE(amax && (ot_attn_amax_supported(I, K, head_dim, qpos != nullptr, precision) & 1),
+             "ot_attn_fwd_amax: the output bound needs the slice forward (split mode, I %d K %d head_dim %d: see "
+             "ot_attn_amax_supported)", I, K, head_dim);
+  return attn_fwd_impl(qkv, ld, B, H, I, K, qpos, head_dim, out, lse, precision, stream, amax);
+}
+
+static int attn_fwd_impl(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos,
+                         int head_dim, float* out, float* lse, int precision, void* stream, float* amax) {
   OT_REQUIRE(precision == OT_MATMUL_F32 || precision == OT_MATMUL_SPLIT_BF16 || precision == OT_MATMUL_BF16,
              "ot_attn_fwd: unknown precision %d", precision);
   OT_REQUIRE(qkv && out && lse, "ot_attn_fwd: null operand");
@@ -1718,7 +1742,7 @@ extern "C" int ot_attn_fwd(const float* qkv, int64_t ld, int B, int H, int I, in
   }
   if (mm == OT_MATMUL_SPLIT_BF16 && attn_slice_fwd_supported(I, K, head_dim)) {
     // short sequence, f32-accurate: one workgroup per (sample, head) slice on split-bf16 MFMA
-    return attn_slice_fwd(qkv, ld, B, H, I, K, qpos, head_dim, out, lse, (hipStream_t)stream);
+    return attn_slice_fwd(qkv, ld, B, H, I, K, qpos, head_dim, out, lse, (hipStream_t)stream, amax);
   }
   if (head_dim >= 32 && (mm == OT_MATMUL_BF16 || (mm == OT_MATMUL_SPLIT_BF16 && !kv_fits && I > 256))) {
     // split-bf16: long sequences (I > 256), with the next key block prefetched (short ones stay on
@@ -1810,7 +1834,20 @@ extern "C" size_t ot_attn_bwd_flags_workspace_size(int B, int H, int I, int K, i
 
 static int attn_bwd_impl(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
                          int B, int H, int I, int K, const int32_t* qpos, int head_dim, float* dqkv,
-                         float* delta_ws, size_t ws_bytes, int prec, void* stream, int flags = 0);
+                         float* delta_ws, size_t ws_bytes, int prec, void* stream, int flags = 0,
+                         float* amax = nullptr);
+
+extern "C" int ot_attn_bwd_amax(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
+                                int B, int H, int I, int K, const int32_t* qpos, int head_dim, float* dqkv,
+                                void* workspace, size_t ws_bytes, float* amax, int precision, void* stream) {
+  OT_REQUIRE(amax && !qpos && precision == OT_MATMUL_SPLIT_BF16 && K > SMALL_K &&
+                 attn_slice_bwd_supported(I, K, head_dim, false) &&
+                 ws_bytes >= ot_attn_bwd_flags_workspace_size(B, H, I, K, head_dim, 0, 0, precision),
+             "ot_attn_bwd_amax: the dQKV bound needs the slice backward (split mode, tail queries, I %d K %d head_dim "
+             "%d, ot_attn_bwd_flags_workspace_size bytes)", I, K, head_dim);
+  return attn_bwd_impl(qkv, ld, out, dout, lse, B, H, I, K, qpos, head_dim, dqkv, (float*)workspace, ws_bytes,
+                       precision, stream, 0, amax);
+}
 
 extern "C" int ot_attn_bwd(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
                            int B, int H, int I, int K, const int32_t* qpos, int head_dim, float* dqkv,
@@ -1850,7 +1887,7 @@ extern "C" int ot_attn_bwd_flags(const float* qkv, int64_t ld, const float* out,
 
 static int attn_bwd_impl(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
                          int B, int H, int I, int K, const int32_t* qpos, int head_dim, float* dqkv,
-                         float* delta_ws, size_t ws_bytes, int prec, void* stream, int flags) {
+                         float* delta_ws, size_t ws_bytes, int prec, void* stream, int flags, float* amax) {
   OT_REQUIRE(prec == OT_MATMUL_F32 || prec == OT_MATMUL_SPLIT_BF16 || prec == OT_MATMUL_BF16,
              "ot_attn_bwd: unknown precision %d", prec);
   OT_REQUIRE(qkv && out && dout && lse && dqkv && delta_ws, "ot_attn_bwd: null operand");
@@ -1862,7 +1899,9 @@ static int attn_bwd_impl(const float* qkv, int64_t ld, const float* out, const f
   const int mm = prec;
   if (mm == OT_MATMUL_SPLIT_BF16 && flags == 0 && K > SMALL_K && attn_slice_bwd_supported(I, K, head_dim, qpos != nullptr) &&
       ws_bytes >= attn_slice_bwd_min_ws(B, H, I, K, head_dim))
-    return attn_slice_bwd(qkv, ld, out, dout, lse, B, H, I, K, head_dim, dqkv, delta_ws, ws_bytes, (hipStream_t)stream);
+    return attn_slice_bwd(qkv, ld, out, dout, lse, B, H, I, K, head_dim, dqkv, delta_ws, ws_bytes, (hipStream_t)stream,
+                          amax);
+  OT_REQUIRE(!amax, "ot_attn_bwd_amax: shape not on the slice backward");
   // the f32 head_dim-32 backward over tail queries forms its own row statistics (no prep launch)
   const bool fdl = !qpos && head_dim == 32 && K > SMALL_K && attn_kpad(K) <= FDL_KP &&
                    mm != OT_MATMUL_BF16;

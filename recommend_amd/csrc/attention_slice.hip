@@ -299,6 +299,7 @@ __device__ unsigned long long g_slice_stamps[2][2048][2][8];
 template <int HD, int NWV, bool SEL, int NP>
 __global__ __launch_bounds__(64 * NWV, 2) void attn_fwd_slice_kernel(SliceArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  float am = 0.f;                                   // max |stored O| (p.amax)
   constexpr int NT = HD / 32, NM = HD / 16, CPR = HD / 8, NTH = 64 * NWV;
   constexpr int PB = RMAX<HD>() * HD * 2;
   constexpr int SR = (RMAX<HD>() * CPR + NTH - 1) / NTH;          // staging rounds
@@ -490,13 +491,17 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_fwd_slice_kernel(SliceArgs p
         const float inv = 1.f / (NP == 2 ? l * sv : l);               // (NP = 2: l and O^T carry 2^14, O^T sv)
         float* orow = p.out + ((int64_t)b * K + j) * p.d + h * HD + 4 * g;
 #pragma unroll
-        for (int m = 0; m < NM; ++m) *reinterpret_cast<f32x4*>(orow + 16 * m) = o[m] * inv;
+        for (int m = 0; m < NM; ++m) {
+          *reinterpret_cast<f32x4*>(orow + 16 * m) = o[m] * inv;
+          am = amax4(am, o[m] * inv);
+        }
         if (g == 0) p.lse[(int64_t)s * K + j] = NP == 2 ? (mx * cs - 14.f) * LN2 + __logf(l) : mx * LN2 + __logf(l);
       }
       idx = idxn;
     }
     SLICE_STAMP(0, it, 2);
   }
+  if (p.amax) amax_flush(p.amax, am);               // |O| bound of the Wo weight gradient (fp16 pair)
 }
 
 // ------------------------------------------------------------------------------------------
@@ -528,6 +533,7 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_fwd_slice_kernel(SliceArgs p
 template <int HD, int NWV, int NP, bool LAT_ = NWV == 4, bool G2 = false, int RQ = RMAX<HD>(), int KR = RQ>
 __global__ __launch_bounds__(64 * NWV, G2 ? 2 : 1) void attn_bwd_slice_kernel(SliceArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  float am = 0.f;                                   // max |stored dQ / dK / dV| (p.amax)
   constexpr int NT = HD / 32, NM = HD / 16, CPR = HD / 8, NTH = 64 * NWV;
   constexpr int RM = RQ, PB = RM * HD * 2;
   // phase 2's K image: KR rows; past RQ (the long forms) its planes take twice the Q planes' stride, the second
@@ -832,6 +838,7 @@ __global__ __launch_bounds__(64 * NWV, G2 ? 2 : 1) void attn_bwd_slice_kernel(Sl
         for (int m = 0; m < NM; ++m) {
           *reinterpret_cast<f32x4*>(dKg + (int64_t)krow * p.ld + 16 * m + 4 * g) = dk[m] * uk;
           *reinterpret_cast<f32x4*>(dVg + (int64_t)krow * p.ld + 16 * m + 4 * g) = dv[m] * uv;
+          am = amax4(amax4(am, dk[m] * uk), dv[m] * uv);
         }
       }
       kb = kbn;
@@ -976,7 +983,10 @@ __global__ __launch_bounds__(64 * NWV, G2 ? 2 : 1) void attn_bwd_slice_kernel(Sl
       if (j < K) {
         float* drow = dQg + (int64_t)(q_off + j) * p.ld + 4 * g;
 #pragma unroll
-        for (int m = 0; m < NM; ++m) *reinterpret_cast<f32x4*>(drow + 16 * m) = dq[m];
+        for (int m = 0; m < NM; ++m) {
+          *reinterpret_cast<f32x4*>(drow + 16 * m) = dq[m];
+          am = amax4(am, dq[m]);
+        }
       }
     }
     SLICE_STAMP(1, it, 5);
@@ -984,6 +994,7 @@ __global__ __launch_bounds__(64 * NWV, G2 ? 2 : 1) void attn_bwd_slice_kernel(Sl
     __syncthreads();                               // LDS is restaged next slice
     SLICE_STAMP(1, it, 6);
   }
+  if (p.amax) amax_flush(p.amax, am);               // |dQKV| bound of the Wqkv weight gradient (fp16 pair)
 }
 
 static int rmax(int hd) { return hd == 64 ? RMAX<64>() : RMAX<32>(); }
@@ -1141,7 +1152,7 @@ bool attn_slice_bwd_supported(int I, int K, int head_dim, bool selected) {
 }
 
 int attn_slice_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos, int head_dim,
-                   float* out, float* lse, hipStream_t stream) {
+                   float* out, float* lse, hipStream_t stream, float* amax) {
   using namespace slice;
   using KF = void (*)(SliceArgs);
   constexpr int P32 = fwd_planes(32), P64 = fwd_planes(64);
@@ -1156,6 +1167,7 @@ int attn_slice_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, con
   });
   SliceArgs p{qkv, ld, H * head_dim, nullptr, nullptr, nullptr, out, lse, nullptr, B, H, I, K,
               1.f / sqrtf((float)head_dim), qpos};
+  p.amax = amax;
   const size_t lds = fwd_lds(I, head_dim, head_dim == 64 ? P64 : P32);
   const int nw = FWD_WAVES;
   OT_REQUIRE(make_schedule(p, head_dim, nw, 8), "ot_attn_fwd(slice): schedule");
@@ -1196,7 +1208,8 @@ size_t attn_slice_bwd_min_ws(int B, int H, int I, int K, int head_dim) {
 }
 
 int attn_slice_bwd(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse, int B, int H,
-                   int I, int K, int head_dim, float* dqkv, float* ws, size_t ws_bytes, hipStream_t stream) {
+                   int I, int K, int head_dim, float* dqkv, float* ws, size_t ws_bytes, hipStream_t stream,
+                   float* amax) {
   using namespace slice;
   using KF = void (*)(SliceArgs);
   static const KF k32 = attn_bwd_slice_kernel<32, BWD_WAVES32, BWD_PLANES>,
@@ -1213,6 +1226,7 @@ int attn_slice_bwd(const float* qkv, int64_t ld, const float* out, const float* 
   OT_REQUIRE(form != BWD_NONE, "ot_attn_bwd(slice): I %d K %d head_dim %d unsupported", I, K, head_dim);
   SliceArgs p{qkv, ld, H * head_dim, out, dout, lse, nullptr, nullptr, dqkv, B, H, I, K,
               1.f / sqrtf((float)head_dim), nullptr};
+  p.amax = amax;
   const size_t per_wg = (size_t)1024 * bwd_pairs(I, K);
   const bool wsok = ws && ws_bytes >= per_wg;
   const bool g2 = form == BWD_MID || form == BWD_LONG || (form == BWD_64 && bwd_g2(64) && wsok);

@@ -101,7 +101,33 @@ __device__ __forceinline__ float pow2_scale14(float m) {
   const int e = (int)((__float_as_uint(m) >> 23) & 255u);   // m in [2^(e-127), 2^(e-126))
   int se = 127 + 13 - (e - 127);
   se = e == 0 ? 127 : (se < 1 ? 1 : (se > 254 ? 254 : se));
-  return __uint_as_float((uint32_t)se << 23);
+  // an inf / NaN bound (a diverged producer) gives a NaN scale: the product turns NaN instead of silently 0
+  return e == 255 ? __builtin_nanf("") : __uint_as_float((uint32_t)se << 23);
+}
+// 4 floats (already scaled) -> the fp16 pair's planes, 8 B each
+__device__ __forceinline__ void pair4(f32x4 v, u32x2& hi, u32x2& lo) {
+  const f32x2_t x0 = f32x2_t{v.x, v.y}, x1 = f32x2_t{v.z, v.w};
+  const f16x2_t h0 = __builtin_convertvector(x0, f16x2_t), h1 = __builtin_convertvector(x1, f16x2_t);
+  const f16x2_t l0 = __builtin_convertvector(x0 - __builtin_convertvector(h0, f32x2_t), f16x2_t);
+  const f16x2_t l1 = __builtin_convertvector(x1 - __builtin_convertvector(h1, f32x2_t), f16x2_t);
+  hi = u32x2{__builtin_bit_cast(uint32_t, h0), __builtin_bit_cast(uint32_t, h1)};
+  lo = u32x2{__builtin_bit_cast(uint32_t, l0), __builtin_bit_cast(uint32_t, l1)};
+}
+// per-tensor magnitude bounds for the fp16-pair weight gradient: a producer max-reduces |value| over what it stores
+// and folds it into *amax (zeroed by the caller) with one atomic per wave — max is order-independent, so the bound
+// is deterministic.  Non-negative floats order like their bit patterns; NaNs are skipped by fmaxf.
+__device__ __forceinline__ float amax4(float m, f32x4 v) {
+  return fmaxf(fmaxf(m, fmaxf(fabsf(v.x), fabsf(v.y))), fmaxf(fabsf(v.z), fabsf(v.w)));
+}
+// One address takes every wave's max: the atomic is issued only when the wave's max exceeds the value the wave reads
+// there (a plain, possibly stale load: stale is smaller, so at worst an atomic too many) — after the first waves the
+// maximum is in and the rest skip it (a million unconditional atomics per launch serialised at one L2 channel:
+// measured 9 ms per C2 step in the row-wise kernels and 4 in the attention forward)
+__device__ __forceinline__ void amax_flush(float* amax, float m) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if (amax && (threadIdx.x & 63) == 0 && __float_as_uint(m) > *reinterpret_cast<volatile unsigned int*>(amax))
+    atomicMax(reinterpret_cast<unsigned int*>(amax), __float_as_uint(m));
 }
 // x s is saturated to the fp16 range first (v_med3_f32): a row bound that under-estimates the operand (a stale or
 // wrong a_rowmax) then gives a deterministic, finite, clipped product instead of an inf plane and inf - inf = NaN

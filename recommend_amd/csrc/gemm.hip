@@ -107,6 +107,8 @@ struct GemmArgs {
   uint16_t* c16_out; int64_t ldc16;             // bf16-mode plane GEMM: also C rounded to bf16 (optional)
   float* rowmax_out; int rowmax_n;              // split plane GEMM: per (out row, column tile) max of C after bias
   const float* a_rowmax; int a_rowmax_n;        // split plane GEMM, GELU prologue: A's row maxima (pair arithmetic)
+  float* amax_out;                              // vector epilogue: atomic max of |stored output| (pair wgrad bound)
+  float* rowabs_out; int rowabs_n;              // vector epilogue: per (out row, column tile) max |stored output|
 };
 
 // sum over the 32 lanes that hold one output row in the vector epilogue (same order as the
@@ -217,6 +219,7 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
       *reinterpret_cast<f32x4*>(dgs + rb * GT + 4 * c4) = f32x4{0.f, 0.f, 0.f, 0.f};
     }
     constexpr int RB = RMSBWD ? RBN / 2 : RBN;          // rows per operand-load batch (register budget)
+    float am = 0.f;                                     // amax_out: |the output the next consumer reads|
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
       // this half's output rows (the loads stay in flight across the accumulator write below)
@@ -323,6 +326,8 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
             }
             v = gv * r - x4[i] * coef + dr4[i];
             if (orr >= 0) store_out4(p.C + (int64_t)orr * p.ldc + col, v);
+            if (!(epi & OT_EPI_DROPOUT) && orr >= 0) am = amax4(am, v);
+            f32x4 cv = v;                                      // what the next consumer reads (mask(dx) or dx)
             if ((epi & OT_EPI_DROPOUT) && orr >= 0) {          // mask(dx) for the dropout site upstream
               const uint32_t idx = (uint32_t)(tok[i] * p.drop_width + col);
               f32x4 mv;
@@ -331,6 +336,14 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
               mv.z = drop_keep(p.seed, p.site, idx + 2, p.drop_thr) ? v.z * p.drop_scale : 0.f;
               mv.w = drop_keep(p.seed, p.site, idx + 3, p.drop_thr) ? v.w * p.drop_scale : 0.f;
               store_out4(p.dxm + (int64_t)orr * p.lddxm + col, mv);
+              am = amax4(am, mv);
+              cv = mv;
+            }
+            if (p.rowabs_out) {                                // the consumer's row bound (dx_masked, else dx)
+              float mx = amax4(0.f, cv);
+#pragma unroll
+              for (int o = 16; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+              if (orr >= 0 && c4 == 0) p.rowabs_out[(int64_t)orr * p.rowabs_n + n0 / GT] = mx;
             }
             continue;
           }
@@ -366,6 +379,13 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
           } else if (orr >= 0) {
             store_out4(p.C + (int64_t)orr * p.ldc + col, v);
           }
+          if (orr >= 0) am = amax4(am, v);
+          if (p.rowabs_out) {                                  // this tile's max |C| of the row (fp16-pair consumer)
+            float mx = amax4(0.f, v);
+#pragma unroll
+            for (int o = 16; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+            if (orr >= 0 && c4 == 0) p.rowabs_out[(int64_t)orr * p.rowabs_n + n0 / GT] = mx;
+          }
         }
       }
       __syncthreads();                                  // ct is rewritten by the next half
@@ -376,6 +396,7 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
       for (int k = 0; k < 8; ++k) a += dgs[k * GT + t];
       p.dgpart[(int64_t)tm * p.N + n0 + t] = a;
     }
+    if (p.amax_out) amax_flush(p.amax_out, am);          // (uniform: every wave reaches it)
 }
 
 // AXT / EPIT: compile-time prologue / epilogue (-1 = read p.a_xform / p.epi at run time).
@@ -783,7 +804,7 @@ constexpr uint32_t PAIR_IMAGE_TAG = 0x7FC17FC1u;
 template <int AXT, int EPIT, int NSTG, int MINW, int TERMS = 6>
 __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
   static_assert(NSTG >= 2 && NSTG <= 4, "plane GEMM stages");
-  static_assert(TERMS == 6 || TERMS == 1 || (TERMS == 2 && (AXT == OT_AX_RMSNORM || AXT == OT_AX_GELU)),
+  static_assert(TERMS == 6 || TERMS == 1 || (TERMS == 2 && (AXT == OT_AX_RMSNORM || AXT == OT_AX_GELU || AXT == OT_AX_NONE)),
                 "plane GEMM terms");
   // OT_AX_BF16: A holds bf16 values (the FFN1 epilogue's stored gelu(U)): 32 B per row and stage, the
   // lane's fragment is one 16-B LDS read, no conversion (bf16 mode only)
@@ -899,7 +920,8 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
     if constexpr (AXT == OT_AX_RMSNORM) {
       abound = p.a_rstd[ir];
     } else {
-      abound = 0.17f;
+      // GELU prologue: signed maxima of u, floored at 0.17 >= |gelu| of negative u; plain A: the rows' max |a| parts
+      abound = AXT == OT_AX_GELU ? 0.17f : 0.f;
       for (int j = 0; j < p.a_rowmax_n; ++j) abound = fmaxf(abound, p.a_rowmax[(int64_t)ir * p.a_rowmax_n + j]);
     }
   }
@@ -1100,6 +1122,9 @@ struct WgradArgs {
   float* slab;               // [nchunks][K][N]
   float* bslab;              // [nchunks][N] or null
   int ntk, ntn;
+  // TERMS 2 (the scaled fp16 pair): bounds of |A| (null with the RMSNorm prologue: sqrt(K) |gamma_k| per column)
+  // and |D|, one float each (ot_mixed_gemm_wgrad_ex)
+  const float* a_bound; const float* d_bound;
 };
 
 template <int AXT>
@@ -1268,12 +1293,20 @@ template <int TERMS>
 constexpr int wgrad_rs() { return WGRAD_BF16_RS > 0 && TERMS == 1 ? WGRAD_BF16_RS : 1; }
 
 // DBF: D holds bf16 values (OT_WG_D_BF16: the FFN2 dgrad's bf16 dU)
+// TERMS 2: the scaled fp16 pair (two planes, three f16 products instead of six bf16): A column k scaled by s_k and D
+// by t, powers of two from per-tensor bounds (p.a_bound / p.d_bound, written by the operands' producers; the
+// RMSNorm prologue's A needs none: |x_k rstd gamma_k| <= sqrt(K) |gamma_k|), the accumulator unscaled by
+// 1 / (s_k t) at the store.  Every element keeps 22 significant bits of itself down to 2^-16 of its bound (below,
+// an absolute error under 2^-38 of the bound).
 template <int AXT, int TERMS, bool DBF = false>
 __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(WgradArgs p) {
   constexpr int RS = wgrad_rs<TERMS>();
   static_assert(RS * WSPLANE <= WSOP && (TERMS == 1 || RS == 1), "wgrad stage LDS");
+  static_assert(TERMS != 2 || (!DBF && (AXT == OT_AX_NONE || AXT == OT_AX_RMSNORM || AXT == OT_AX_GELU)),
+                "pair wgrad forms");
+  constexpr bool PAIR = TERMS == 2;
   constexpr int BR = WBR * RS;                   // rows per stage
-  constexpr int NPL = TERMS == 1 ? 1 : 3;
+  constexpr int NPL = TERMS == 1 ? 1 : PAIR ? 2 : 3;
   extern __shared__ __attribute__((aligned(16))) char smem_c[];
   const int ax = AXT >= 0 ? AXT : p.a_xform;
   const int per_chunk = p.ntk * p.ntn;
@@ -1306,6 +1339,20 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(WgradArgs p) {
       const int k = k0 + 4 * (sc + 8 * i);
       gv[i] = *reinterpret_cast<const f32x4*>(p.a_gamma + (k < p.K ? k : 0));
     }
+  }
+  // TERMS 2: this thread's column scales of A (k columns 4 (sc + 8 i) ..) and D's scale
+  f32x4 sa[4];
+  float sdv = 1.f;
+  if constexpr (PAIR) {
+    sdv = pow2_scale14(p.d_bound[0]);
+    const float sqk = sqrtf((float)p.K);
+    const float s1 = AXT == OT_AX_RMSNORM ? 1.f : pow2_scale14(p.a_bound[0]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      sa[i] = AXT == OT_AX_RMSNORM
+                  ? f32x4{pow2_scale14(sqk * fabsf(gv[i].x)), pow2_scale14(sqk * fabsf(gv[i].y)),
+                          pow2_scale14(sqk * fabsf(gv[i].z)), pow2_scale14(sqk * fabsf(gv[i].w))}
+                  : f32x4{s1, s1, s1, s1};
   }
 
   auto rows_of = [&](int rs, int (&ar)[RS], int (&dr)[RS]) {
@@ -1377,6 +1424,16 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(WgradArgs p) {
           *reinterpret_cast<u32x2*>(Ds + off) = bf16_rne4(dv);
           continue;
         }
+        if constexpr (PAIR) {
+          u32x2 h0, l0;
+          pair4(a * sa[i], h0, l0);
+          *reinterpret_cast<u32x2*>(As + off) = h0;
+          *reinterpret_cast<u32x2*>(As + WSPLANE + off) = l0;
+          pair4(dv * sdv, h0, l0);
+          *reinterpret_cast<u32x2*>(Ds + off) = h0;
+          *reinterpret_cast<u32x2*>(Ds + WSPLANE + off) = l0;
+          continue;
+        }
         u32x2 q0, q1, q2;
         split3(a, q0, q1, q2);
         *reinterpret_cast<u32x2*>(As + off) = q0;
@@ -1438,6 +1495,12 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(WgradArgs p) {
             acc[m][n] = mfma_bf16(fa[m][0], fb[n][0], acc[m][n]);
             continue;
           }
+          if constexpr (PAIR) {
+            acc[m][n] = mfma_f16(fa[m][0], fb[n][1], acc[m][n]);
+            acc[m][n] = mfma_f16(fa[m][1], fb[n][0], acc[m][n]);
+            acc[m][n] = mfma_f16(fa[m][0], fb[n][0], acc[m][n]);
+            continue;
+          }
           if (SPLIT_TERMS >= 9) {
             acc[m][n] = mfma_bf16(fa[m][2], fb[n][2], acc[m][n]);
             acc[m][n] = mfma_bf16(fa[m][1], fb[n][2], acc[m][n]);
@@ -1460,16 +1523,20 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(WgradArgs p) {
     for (int j = 0; j < RS; ++j) { ar2[j] = ar3[j]; dr2[j] = dr3[j]; }
   }
   float* slab = p.slab + (int64_t)c * p.K * p.N;
+  float ainv1 = 1.f;                                  // TERMS 2: 1 / (s_k t), exact powers of two
+  if constexpr (PAIR) ainv1 = 1.f / ((AXT == OT_AX_RMSNORM ? 1.f : pow2_scale14(p.a_bound[0])) * sdv);
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int k = k0 + wm + 32 * m + (r & 3) + 8 * (r >> 2) + 4 * h;
       if (k >= p.K) continue;
+      float un = ainv1;
+      if (PAIR && AXT == OT_AX_RMSNORM) un = 1.f / (pow2_scale14(sqrtf((float)p.K) * fabsf(p.a_gamma[k])) * sdv);
 #pragma unroll
       for (int n = 0; n < 2; ++n) {
         const int col = n0 + wn + 32 * n + li;
-        if (col < p.N) slab[(int64_t)k * p.N + col] = acc[m][n][r];
+        if (col < p.N) slab[(int64_t)k * p.N + col] = PAIR ? acc[m][n][r] * un : acc[m][n][r];
       }
     }
   if (do_bias) {
@@ -1886,7 +1953,12 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
     p.rowmax_out = rms->rowmax_out;
     p.rowmax_n = rms->rowmax_n;
   }
-  if (rms && rms->a_rowmax && a_xform == OT_AX_GELU) {
+  if (rms) {
+    p.amax_out = rms->amax_out;
+    p.rowabs_out = rms->rowabs_out;
+    p.rowabs_n = rms->rowabs_n;
+  }
+  if (rms && rms->a_rowmax && (a_xform == OT_AX_GELU || a_xform == OT_AX_NONE)) {
     p.a_rowmax = rms->a_rowmax;
     p.a_rowmax_n = rms->a_rowmax_n;
   }
@@ -1965,7 +2037,7 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
 #define OT_PSPEC(AX_, EP_) \
     if (x == AX_ && e == (EP_)) \
       pk = one ? plane_gemm_kernel<AX_, EP_, PLANE_BF16_NSTG, 4, 1> \
-         : (p.a_rowmax ? plane_gemm_kernel<AX_, EP_, 2, 4, ((AX_) == OT_AX_RMSNORM || (AX_) == OT_AX_GELU) ? 2 : 6> \
+         : (p.a_rowmax ? plane_gemm_kernel<AX_, EP_, 2, 4, ((AX_) == OT_AX_RMSNORM || (AX_) == OT_AX_GELU || (AX_) == OT_AX_NONE) ? 2 : 6> \
                        : plane_gemm_kernel<AX_, EP_, 2, 4, (AX_) == OT_AX_RMSNORM ? 2 : 6>);
     OT_PSPEC(OT_AX_RMSNORM, 0)
     OT_PSPEC(OT_AX_RMSNORM, OT_EPI_BIAS)
@@ -2039,6 +2111,12 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
              "ot_mixed_gemm_rms: rowmax_out needs the split-mode plane GEMM (pre-split B image, whole tiles, 16-B "
              "aligned A) and rowmax_n == ceil(N / %d) = %d (got %d)", GT, (int)ceil_div(N, GT), p.rowmax_n);
   OT_REQUIRE(!p.a_rowmax || p.a_rowmax_n >= 1, "ot_mixed_gemm_rms: a_rowmax needs a_rowmax_n >= 1");
+  // the output bound is taken in the vector epilogue (whole tiles; the edge kernels' scalar epilogue has none)
+  OT_REQUIRE(!p.rowabs_out || (!edge && kern != nullptr && p.rowabs_n == (int)ceil_div(N, GT)),
+             "ot_mixed_gemm_rms: rowabs_out needs a specialised whole-tile kernel and rowabs_n == ceil(N / %d)", GT);
+  OT_REQUIRE(!p.amax_out || (!edge && kern != nullptr),
+             "ot_mixed_gemm_rms: amax_out needs a specialised whole-tile kernel (K %% 16 == 0, N %% 128 == 0, 16-B "
+             "aligned operands)");
   // (+ K floats of gamma behind the stage buffers for the xn_out side output)
   const size_t xn_lds = p.xn_out ? (size_t)K * 4 : 0;
   const size_t launch_shmem = !plane ? shmem
@@ -2184,13 +2262,13 @@ extern "C" size_t ot_wgrad_workspace_size(int nchunks, int K, int N) {
   return ((size_t)nchunks * K * N + (size_t)nchunks * N) * sizeof(float);
 }
 
-extern "C" int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a_rows, int a_xform,
-                                   const float* a_rstd, const float* a_gamma,
-                                   const float* D, int64_t ldd, const int32_t* d_rows, int K, int N,
-                                   const int32_t* chunks, int nchunks, const int32_t* gchunk, int ngroups,
-                                   float* dW, int64_t dw_gstride, float* db, int64_t db_gstride,
-                                   int accumulate, void* workspace, size_t ws_bytes, int precision,
-                                   void* stream) {
+static int wgrad_impl(const float* A, int64_t lda, const int32_t* a_rows, int a_xform,
+                      const float* a_rstd, const float* a_gamma,
+                      const float* D, int64_t ldd, const int32_t* d_rows, int K, int N,
+                      const int32_t* chunks, int nchunks, const int32_t* gchunk, int ngroups,
+                      float* dW, int64_t dw_gstride, float* db, int64_t db_gstride,
+                      int accumulate, void* workspace, size_t ws_bytes, const float* a_bound, const float* d_bound,
+                      int precision, void* stream) {
   OT_REQUIRE(precision == OT_MATMUL_F32 || precision == OT_MATMUL_SPLIT_BF16 || precision == OT_MATMUL_BF16,
              "ot_mixed_gemm_wgrad: unknown precision %d", precision);
   OT_REQUIRE(A && D && dW && chunks && gchunk && workspace, "ot_mixed_gemm_wgrad: null operand");
@@ -2210,7 +2288,10 @@ extern "C" int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a
   float* bslab = db ? slab + (size_t)nchunks * K * N : nullptr;
   if (nchunks > 0) {
     WgradArgs p{A, lda, a_rows, a_xform, a_rstd, a_gamma, D, ldd, d_rows, K, N, chunks, nchunks, slab, bslab,
-                (int)ceil_div(K, GT), (int)ceil_div(N, GT)};
+                (int)ceil_div(K, GT), (int)ceil_div(N, GT), a_bound, d_bound};
+    // the scaled fp16 pair: split mode, f32 operands, D's bound given, and A's (or the RMSNorm prologue's own)
+    const bool pair = precision == OT_MATMUL_SPLIT_BF16 && !dbf && d_bound &&
+                      ((a_xform == OT_AX_RMSNORM) || ((a_xform == OT_AX_NONE || a_xform == OT_AX_GELU) && a_bound));
     const size_t shmem = (OT_WGRAD_DBUF ? 4 : 2) * WBR * WLD * sizeof(float);
     const bool split = precision != OT_MATMUL_F32;
     OT_REQUIRE(a_xform != OT_AX_BF16 || (precision != OT_MATMUL_F32 && lda % 4 == 0 && ((uintptr_t)A % 8) == 0),
@@ -2219,7 +2300,10 @@ extern "C" int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a
     const bool copy = dbf && a_xform == OT_AX_BF16 && K % 8 == 0 && N % 8 == 0 && lda % 8 == 0 &&
                       ldd % 8 == 0 && ((uintptr_t)A % 16) == 0 && ((uintptr_t)D % 16) == 0 && a_rows == d_rows;
     void (*kern)(WgradArgs) =
-        copy ? (a_rows ? wgrad_bf16_kernel<true> : wgrad_bf16_kernel<false>)
+        pair ? (a_xform == OT_AX_NONE      ? wgrad_split_kernel<OT_AX_NONE, 2>
+                : a_xform == OT_AX_RMSNORM ? wgrad_split_kernel<OT_AX_RMSNORM, 2>
+                                           : wgrad_split_kernel<OT_AX_GELU, 2>)
+        : copy ? (a_rows ? wgrad_bf16_kernel<true> : wgrad_bf16_kernel<false>)
         : dbf ? (a_xform == OT_AX_NONE      ? wgrad_split_kernel<OT_AX_NONE, 1, true>
                  : a_xform == OT_AX_BF16    ? wgrad_split_kernel<OT_AX_BF16, 1, true>
                                             : wgrad_split_kernel<OT_AX_RMSNORM, 1, true>)
@@ -2266,4 +2350,28 @@ extern "C" int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a
                      db_gstride, accumulate, wblocks);
   OT_LAUNCH_CHECK("ot_mixed_gemm_wgrad(reduce)");
   return OT_OK;
+}
+
+extern "C" int ot_mixed_gemm_wgrad(const float* A, int64_t lda, const int32_t* a_rows, int a_xform,
+                                   const float* a_rstd, const float* a_gamma,
+                                   const float* D, int64_t ldd, const int32_t* d_rows, int K, int N,
+                                   const int32_t* chunks, int nchunks, const int32_t* gchunk, int ngroups,
+                                   float* dW, int64_t dw_gstride, float* db, int64_t db_gstride,
+                                   int accumulate, void* workspace, size_t ws_bytes, int precision,
+                                   void* stream) {
+  return wgrad_impl(A, lda, a_rows, a_xform, a_rstd, a_gamma, D, ldd, d_rows, K, N, chunks, nchunks, gchunk, ngroups,
+                    dW, dw_gstride, db, db_gstride, accumulate, workspace, ws_bytes, nullptr, nullptr, precision,
+                    stream);
+}
+
+extern "C" int ot_mixed_gemm_wgrad_ex(const float* A, int64_t lda, const int32_t* a_rows, int a_xform,
+                                      const float* a_rstd, const float* a_gamma,
+                                      const float* D, int64_t ldd, const int32_t* d_rows, int K, int N,
+                                      const int32_t* chunks, int nchunks, const int32_t* gchunk, int ngroups,
+                                      float* dW, int64_t dw_gstride, float* db, int64_t db_gstride,
+                                      int accumulate, void* workspace, size_t ws_bytes, const float* a_bound,
+                                      const float* d_bound, int precision, void* stream) {
+  return wgrad_impl(A, lda, a_rows, a_xform, a_rstd, a_gamma, D, ldd, d_rows, K, N, chunks, nchunks, gchunk, ngroups,
+                    dW, dw_gstride, db, db_gstride, accumulate, workspace, ws_bytes, a_bound, d_bound, precision,
+                    stream);
 }

@@ -173,23 +173,60 @@ __global__ void rows_colsum_kernel(const float* __restrict__ src, int64_t ld, co
 
 // OUT: float (f32 rows) or uint16_t (bf16 rows, rounded to nearest even: the bf16 mode's FFN2 dgrad A operand
 // and W2 weight-gradient D operand, which round it so anyway)
+constexpr int DROPOUT_PASSES = 4;
 template <typename OUT>
 __global__ void dropout_apply_kernel(const float* __restrict__ src, int64_t lds, OUT* dst, int64_t ldd,
                                      int64_t rows, int d, uint32_t seed, uint32_t site, uint32_t thr, float scale,
-                                     int tail_K, int tail_I, const int32_t* tail_pos) {
-  const int64_t i4 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-  if (i4 >= rows * d) return;
-  const int64_t r = i4 / d;
-  const int c = (int)(i4 % d);
-  const int64_t tok = tail_token(r, tail_K, tail_I, tail_pos);
-  f32x4 v = *reinterpret_cast<const f32x4*>(src + r * lds + c);
-  uint32_t base = (uint32_t)(tok * d + c);
-  v.x = drop_keep(seed, site, base + 0, thr) ? v.x * scale : 0.f;
-  v.y = drop_keep(seed, site, base + 1, thr) ? v.y * scale : 0.f;
-  v.z = drop_keep(seed, site, base + 2, thr) ? v.z * scale : 0.f;
-  v.w = drop_keep(seed, site, base + 3, thr) ? v.w * scale : 0.f;
-  if constexpr (sizeof(OUT) == 2) *reinterpret_cast<u32x2*>(dst + r * ldd + c) = bf16_rne4(v);
-  else *reinterpret_cast<f32x4*>(dst + r * ldd + c) = v;
+                                     int tail_K, int tail_I, const int32_t* tail_pos, float* amax, float* rowmax,
+                                     int rowmax_n) {
+  // PASSES float4s per thread, grid-strided (each pass coalesced): the magnitude outputs cost one wave reduction per
+  // PASSES float4s instead of per one
+  const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
+  float am = 0.f;
+#pragma unroll
+  for (int ps = 0; ps < DROPOUT_PASSES; ++ps) {
+    const int64_t i4 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x + ps * nthreads) * 4;
+    const bool in = i4 < rows * d;
+    const int64_t r = in ? i4 / d : 0;
+    const int c = (int)(i4 % d);
+    float pm = 0.f;
+    if (in) {
+      const int64_t tok = tail_token(r, tail_K, tail_I, tail_pos);
+      f32x4 v = *reinterpret_cast<const f32x4*>(src + r * lds + c);
+      uint32_t base = (uint32_t)(tok * d + c);
+      v.x = drop_keep(seed, site, base + 0, thr) ? v.x * scale : 0.f;
+      v.y = drop_keep(seed, site, base + 1, thr) ? v.y * scale : 0.f;
+      v.z = drop_keep(seed, site, base + 2, thr) ? v.z * scale : 0.f;
+      v.w = drop_keep(seed, site, base + 3, thr) ? v.w * scale : 0.f;
+      if constexpr (sizeof(OUT) == 2) *reinterpret_cast<u32x2*>(dst + r * ldd + c) = bf16_rne4(v);
+      else *reinterpret_cast<f32x4*>(dst + r * ldd + c) = v;
+      pm = amax4(0.f, v);
+    }
+    am = fmaxf(am, pm);
+    // each row's max |v| per 256-column part (a row is d / 4 consecutive lanes: groups of min(d / 4, 64) lanes; the
+    // host checks the shape)
+    if (rowmax) {
+      const int gl = d / 4 < 64 ? d / 4 : 64;
+      for (int o = gl / 2; o > 0; o >>= 1) pm = fmaxf(pm, __shfl_xor(pm, o, 64));
+      if (in && (c % 256) == 0) rowmax[r * rowmax_n + c / 256] = pm;
+    }
+  }
+  if (amax) amax_flush(amax, am);
+}
+
+// out[r][j] = max |x[r][256 j .. 256 j + 255]|: one wave per (row, part), a float4 per lane
+__global__ __launch_bounds__(256) void rows_absmax_kernel(const float* __restrict__ x, int64_t ldx, int64_t rows, int d,
+                                                          float* out, int parts) {
+  const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  const int64_t r = w / parts;
+  const int j = (int)(w % parts);
+  const int c = 256 * j + 4 * lane;
+  float m = 0.f;
+  if (r < rows && c < d) m = amax4(0.f, *reinterpret_cast<const f32x4*>(x + r * ldx + c));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if (r < rows && lane == 0) out[r * parts + j] = m;
 }
 
 inline int tpr_for(int d) {
@@ -281,10 +318,37 @@ extern "C" int ot_dropout_apply(const float* src, int64_t lds, float* dst, int64
   OT_REQUIRE(src && dst && d % 4 == 0 && lds % 4 == 0 && ldd % 4 == 0, "ot_dropout_apply: bad args");
   OT_REQUIRE(tail_K > 0 && tail_I >= tail_K, "ot_dropout_apply: bad tail map");
   if (rows == 0) return OT_OK;
-  hipLaunchKernelGGL(dropout_apply_kernel<float>, dim3(ceil_div(rows * d / 4, 256)), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(dropout_apply_kernel<float>, dim3(ceil_div(ceil_div(rows * d / 4, DROPOUT_PASSES), 256)), dim3(256), 0, (hipStream_t)stream,
                      src, lds, dst, ldd, rows, d, seed, site, drop_threshold(drop_rate),
-                     drop_rate < 1.f ? 1.f / (1.f - drop_rate) : 0.f, tail_K, tail_I, tail_pos);
+                     drop_rate < 1.f ? 1.f / (1.f - drop_rate) : 0.f, tail_K, tail_I, tail_pos, nullptr, nullptr, 0);
   OT_LAUNCH_CHECK("ot_dropout_apply");
+  return OT_OK;
+}
+
+extern "C" int ot_dropout_apply_ex(const float* src, int64_t lds, float* dst, int64_t ldd, int64_t rows, int d,
+                                   uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
+                                   const int32_t* tail_pos, float* amax, float* rowmax, int rowmax_n, void* stream) {
+  OT_REQUIRE(src && dst && d % 4 == 0 && lds % 4 == 0 && ldd % 4 == 0, "ot_dropout_apply_ex: bad args");
+  OT_REQUIRE(tail_K > 0 && tail_I >= tail_K, "ot_dropout_apply_ex: bad tail map");
+  const int q = d / 4;
+  OT_REQUIRE(!rowmax || (rowmax_n == (d + 255) / 256 && (q % 64 == 0 || (q & (q - 1)) == 0)),
+             "ot_dropout_apply_ex: rowmax needs rowmax_n == ceil(d / 256) and d / 4 a power of two or a multiple of 64");
+  if (rows == 0) return OT_OK;
+  hipLaunchKernelGGL(dropout_apply_kernel<float>, dim3(ceil_div(ceil_div(rows * d / 4, DROPOUT_PASSES), 256)), dim3(256), 0, (hipStream_t)stream,
+                     src, lds, dst, ldd, rows, d, seed, site, drop_threshold(drop_rate),
+                     drop_rate < 1.f ? 1.f / (1.f - drop_rate) : 0.f, tail_K, tail_I, tail_pos, amax, rowmax, rowmax_n);
+  OT_LAUNCH_CHECK("ot_dropout_apply_ex");
+  return OT_OK;
+}
+
+extern "C" int ot_rows_absmax(const float* x, int64_t ldx, int64_t rows, int d, float* out, int parts,
+                              void* stream) {
+  OT_REQUIRE(x && out && d % 4 == 0 && ldx % 4 == 0 && parts == (d + 255) / 256,
+             "ot_rows_absmax: bad args (d %% 4 == 0, parts == ceil(d / 256))");
+  if (rows == 0) return OT_OK;
+  hipLaunchKernelGGL(rows_absmax_kernel, dim3(ceil_div(rows * parts, 4)), dim3(256), 0, (hipStream_t)stream, x, ldx,
+                     rows, d, out, parts);
+  OT_LAUNCH_CHECK("ot_rows_absmax");
   return OT_OK;
 }
 
@@ -295,9 +359,9 @@ extern "C" int ot_dropout_apply_bf16(const float* src, int64_t lds, uint16_t* ds
              "ot_dropout_apply_bf16: bad args");
   OT_REQUIRE(tail_K > 0 && tail_I >= tail_K, "ot_dropout_apply_bf16: bad tail map");
   if (rows == 0) return OT_OK;
-  hipLaunchKernelGGL(dropout_apply_kernel<uint16_t>, dim3(ceil_div(rows * d / 4, 256)), dim3(256), 0,
+  hipLaunchKernelGGL(dropout_apply_kernel<uint16_t>, dim3(ceil_div(ceil_div(rows * d / 4, DROPOUT_PASSES), 256)), dim3(256), 0,
                      (hipStream_t)stream, src, lds, dst, ldd, rows, d, seed, site, drop_threshold(drop_rate),
-                     drop_rate < 1.f ? 1.f / (1.f - drop_rate) : 0.f, tail_K, tail_I, tail_pos);
+                     drop_rate < 1.f ? 1.f / (1.f - drop_rate) : 0.f, tail_K, tail_I, tail_pos, nullptr, nullptr, 0);
   OT_LAUNCH_CHECK("ot_dropout_apply_bf16");
   return OT_OK;
 }

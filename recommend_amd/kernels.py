@@ -238,7 +238,8 @@ def gemm_rms(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish,
              aux: Ptrish = None, ldaux: int = 0, rowdot: Ptrish = None, rowdot_n: int = 0,
              gelu_out: Ptrish = None, ldgelu: int = 0, xn_out: Ptrish = None, ldxn: int = 0,
              c16_out: Ptrish = None, ldc16: int = 0, rowmax_out: Ptrish = None, rowmax_n: int = 0,
-             a_rowmax: Ptrish = None, a_rowmax_n: int = 0) -> None:
+             a_rowmax: Ptrish = None, a_rowmax_n: int = 0, amax_out: Ptrish = None, rowabs_out: Ptrish = None,
+             rowabs_n: int = 0) -> None:
     """ot_mixed_gemm_rms: the GEMM with a row-norm epilogue (OT_EPI_ROW_RSTD: emit the next RMSNorm's
     rstd; OT_EPI_RMSNORM_BWD: apply the RMSNorm backward to the product, + dres, dgamma, taking
     <gamma dy, x> from ``rowdot`` when N > 128; OT_EPI_GELU_BWD | OT_EPI_ROWDOT: also write each 128-column
@@ -256,7 +257,8 @@ def gemm_rms(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish,
                          dres_tail[0], dres_tail[1], _sel(dres_tail), ptr(dx_masked), lddxm, ptr(dgamma),
                          int(accumulate_dgamma), ptr(ws), ws.numel(), ptr(rowdot), int(rowdot_n),
                          ptr(gelu_out), int(ldgelu), ptr(xn_out), int(ldxn), ptr(c16_out), int(ldc16),
-                         ptr(rowmax_out), int(rowmax_n), ptr(a_rowmax), int(a_rowmax_n))
+                         ptr(rowmax_out), int(rowmax_n), ptr(a_rowmax), int(a_rowmax_n), ptr(amax_out),
+                         ptr(rowabs_out), int(rowabs_n))
     ev = _probe.begin() if _probe is not None else None
     args = (mode, ptr(A), lda, K, ptr(in_rows), a_xform, ptr(rstd), ptr(gamma), ptr(W),
             w_gstride, ldw, N, ptr(tile_group), ntiles, ptr(bias), bias_gstride, ptr(C), ldc, ptr(out_rows), epi,
@@ -278,9 +280,11 @@ def gemm_rms(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish,
 def wgrad(A: Ptrish, lda: int, a_rows: Ptrish, D: Ptrish, ldd: int, d_rows: Ptrish, K: int, N: int, rmap_dev,
           nchunks: int, ngroups: int, dW: Ptrish, dw_gstride: int, db: Ptrish = None, db_gstride: int = 0, *,
           a_xform: int = 0, rstd: Ptrish = None, gamma: Ptrish = None, accumulate: bool = False,
-          device=None, m_rows: int = 0, rowmap=None) -> None:
+          device=None, m_rows: int = 0, rowmap=None, a_bound: Ptrish = None, d_bound: Ptrish = None) -> None:
     """rmap_dev: dict with 'chunks'/'gchunk' device tensors; when ``rowmap`` (a layout.RowMap) is given
-    its chunking is re-balanced for this call's output tile count (layout.wgrad_slots)."""
+    its chunking is re-balanced for this call's output tile count (layout.wgrad_slots).  ``d_bound`` / ``a_bound``
+    (one float each on the device, from the operands' producers): the split mode runs the fp16-pair kernel
+    (ot_mixed_gemm_wgrad_ex; the RMSNorm prologue's A needs no bound)."""
     if rowmap is not None and rowmap.group_rows:
         tiles = ((K + 127) // 128) * ((N + 127) // 128)
         ch, gc, nchunks = rowmap.chunks_for(tiles, device)
@@ -288,9 +292,10 @@ def wgrad(A: Ptrish, lda: int, a_rows: Ptrish, D: Ptrish, ldd: int, d_rows: Ptri
     nbytes = size('ot_wgrad_workspace_size', nchunks, K, N)
     ws = workspace(nbytes, device)
     ev = _probe.begin() if _probe is not None else None
-    call('ot_mixed_gemm_wgrad', ptr(A), lda, ptr(a_rows), a_xform, ptr(rstd), ptr(gamma), ptr(D), ldd,
+    call('ot_mixed_gemm_wgrad_ex', ptr(A), lda, ptr(a_rows), a_xform, ptr(rstd), ptr(gamma), ptr(D), ldd,
          ptr(d_rows), K, N, ptr(rmap_dev['chunks']), nchunks, ptr(rmap_dev['gchunk']), ngroups, ptr(dW),
-         dw_gstride, ptr(db), db_gstride, int(accumulate), ptr(ws), ws.numel(), _prec(), stream())
+         dw_gstride, ptr(db), db_gstride, int(accumulate), ptr(ws), ws.numel(), ptr(a_bound), ptr(d_bound), _prec(),
+         stream())
     if ev is not None:
         _probe.end('mixed_gemm', 2.0 * m_rows * K * N, ev, f'wgrad ax{a_xform} M{m_rows} K{K} N{N} ch{nchunks}',
                    (2.0 if (a_xform & ~_lib.OT_WG_D_BF16) == _lib.OT_AX_BF16 else 4.0) * m_rows * K
@@ -312,7 +317,8 @@ def split_images(base, desc_dev, ndesc, total_units, img) -> None:
 
 def attn_fwd(qkv: torch.Tensor, ld: int, B: int, H: int, I: int, K: int, hd: int, out: torch.Tensor,
              lse: torch.Tensor, qpos: Optional[torch.Tensor] = None, fp8: bool = False,
-             dequant: bool = False, fp8_terms: int = 1, deq16: Optional[torch.Tensor] = None) -> None:
+             dequant: bool = False, fp8_terms: int = 1, deq16: Optional[torch.Tensor] = None,
+             amax: Optional[torch.Tensor] = None) -> None:
     """ot_attn_fwd, or with ``fp8`` (head_dim 64/128) ot_attn_fwd_fp8_ex: QK^T and PV on block-scaled fp8
     MFMA, operands as one e4m3 term or two (``fp8_terms`` 2: hi + lo, OT_FP8_TWO_TERM); ``dequant``
     (training) also overwrites qkv's operands with their dequantised fp8 values (OT_FP8_DEQUANT) for the
@@ -331,6 +337,9 @@ def attn_fwd(qkv: torch.Tensor, ld: int, B: int, H: int, I: int, K: int, hd: int
         call('ot_attn_fwd_fp8_ex', ptr(qkv), ld, B, H, I, K, ptr(qpos), hd, ptr(out), ptr(lse), ptr(ws),
              ws.numel(), (_lib.OT_FP8_DEQUANT if dequant else 0) | (_lib.OT_FP8_TWO_TERM if fp8_terms == 2 else 0),
              stream())
+    elif amax is not None:      # + max |O| folded into amax (attn_amax_supported shapes only)
+        call('ot_attn_fwd_amax', ptr(qkv), ld, B, H, I, K, ptr(qpos), hd, ptr(out), ptr(lse), ptr(amax), _prec(),
+             stream())
     else:
         call('ot_attn_fwd', ptr(qkv), ld, B, H, I, K, ptr(qpos), hd, ptr(out), ptr(lse), _prec(), stream())
     if ev is not None:
@@ -348,7 +357,14 @@ def attn_bwd_bf16_supported(I, K, hd, qpos=None) -> bool:
     return bool(_lib.load().ot_attn_bwd_dqkv_bf16_supported(I, K, hd, int(qpos is not None), _prec()))
 
 
-def attn_bwd(qkv, ld, out, dout, lse, B, H, I, K, hd, dqkv, qpos=None, dq_part_bf16: bool = False) -> None:
+def attn_amax_supported(I, K, hd, qpos=None, backward: bool = False) -> bool:
+    """ot_attn_amax_supported: does the attention forward (or ``backward``) report max |O| (max |dQKV|) at this shape
+    (the slice kernels)?"""
+    return bool(_lib.load().ot_attn_amax_supported(I, K, hd, int(qpos is not None), _prec()) & (2 if backward else 1))
+
+
+def attn_bwd(qkv, ld, out, dout, lse, B, H, I, K, hd, dqkv, qpos=None, dq_part_bf16: bool = False,
+             amax=None) -> None:
     """dqkv float32, or int16 (bf16 bits: OT_ATTN_DQKV_BF16, see attn_bwd_bf16_supported); qkv likewise
     (int16: OT_ATTN_QKV_BF16, the fp8 forward's bf16 dequantised operands)."""
     flags = ((_lib.OT_ATTN_DQKV_BF16 if dqkv.dtype == torch.int16 else 0)
@@ -358,8 +374,12 @@ def attn_bwd(qkv, ld, out, dout, lse, B, H, I, K, hd, dqkv, qpos=None, dq_part_b
     ws = workspace(size('ot_attn_bwd_flags_workspace_size', B, H, I, K, hd, int(qpos is not None), flags, _prec()),
                    qkv.device)
     ev = _probe.begin() if _probe is not None else None
-    call('ot_attn_bwd_flags', ptr(qkv), ld, ptr(out), ptr(dout), ptr(lse), B, H, I, K, ptr(qpos), hd, ptr(dqkv),
-         flags, ptr(ws), ws.numel(), _prec(), stream())
+    if amax is not None:        # + max |dQKV| folded into amax (slice backward shapes only)
+        call('ot_attn_bwd_amax', ptr(qkv), ld, ptr(out), ptr(dout), ptr(lse), B, H, I, K, ptr(qpos), hd, ptr(dqkv),
+             ptr(ws), ws.numel(), ptr(amax), _prec(), stream())
+    else:
+        call('ot_attn_bwd_flags', ptr(qkv), ld, ptr(out), ptr(dout), ptr(lse), B, H, I, K, ptr(qpos), hd,
+             ptr(dqkv), flags, ptr(ws), ws.numel(), _prec(), stream())
     if ev is not None:
         _probe.end('attention', 8.0 * (K * I - K * (K - 1) / 2) * hd * H * B, ev, f'bwd I{I} K{K} hd{hd}')
 
@@ -395,12 +415,26 @@ def rmsnorm_bwd(dy: Ptrish, lddy: int, x: Ptrish, ldx: int, gamma: Ptrish, rstd:
         _probe.end('rowwise', 0.0, ev)
 
 
-def dropout_apply(src, lds, dst, ldd, rows, d, seed, site, drop, tail) -> None:
-    """dst float32, or int16 (bf16 bits: ot_dropout_apply_bf16)."""
+def dropout_apply(src, lds, dst, ldd, rows, d, seed, site, drop, tail, amax=None, rowmax=None) -> None:
+    """dst float32, or int16 (bf16 bits: ot_dropout_apply_bf16).  ``amax`` (one float, zeroed) / ``rowmax`` ([rows][ceil(d /
+    256)]): the output's magnitude for fp16-pair consumers (ot_dropout_apply_ex, float32 dst)."""
     ev = _probe.begin() if _probe is not None else None
-    fn = 'ot_dropout_apply_bf16' if getattr(dst, 'dtype', None) == torch.int16 else 'ot_dropout_apply'
-    call(fn, ptr(src), lds, ptr(dst), ldd, rows, d, seed & 0xFFFFFFFF, site, float(drop), tail[0],
-         tail[1], _sel(tail), stream())
+    if amax is not None or rowmax is not None:
+        call('ot_dropout_apply_ex', ptr(src), lds, ptr(dst), ldd, rows, d, seed & 0xFFFFFFFF, site, float(drop),
+             tail[0], tail[1], _sel(tail), ptr(amax), ptr(rowmax), (d + 255) // 256 if rowmax is not None else 0,
+             stream())
+    else:
+        fn = 'ot_dropout_apply_bf16' if getattr(dst, 'dtype', None) == torch.int16 else 'ot_dropout_apply'
+        call(fn, ptr(src), lds, ptr(dst), ldd, rows, d, seed & 0xFFFFFFFF, site, float(drop), tail[0],
+             tail[1], _sel(tail), stream())
+    if ev is not None:
+        _probe.end('rowwise', 0.0, ev)
+
+
+def rows_absmax(x, ldx, rows, d, out) -> None:
+    """ot_rows_absmax: out [rows][ceil(d / 256)] = each row's 256-column parts' max |x| (an fp16-pair GEMM's a_rowmax)."""
+    ev = _probe.begin() if _probe is not None else None
+    call('ot_rows_absmax', ptr(x), ldx, rows, d, ptr(out), (d + 255) // 256, stream())
     if ev is not None:
         _probe.end('rowwise', 0.0, ev)
 

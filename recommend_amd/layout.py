@@ -55,7 +55,7 @@ def round_up(x: int, m: int) -> int:
 class FlatLayout:
     """Offsets of every dense bank inside the flat parameter buffer."""
 
-    def __init__(self, cfg: OneTransConfig, f_ns: int):
+    def __init__(self, cfg: OneTransConfig, f_ns: int, pair_dgrad: bool = False):
         self.f_ns = f_ns
         self.f_pad = max(4, round_up(f_ns, 4))
         self.shapes = dense_param_shapes(cfg, self.f_pad)
@@ -113,7 +113,11 @@ class FlatLayout:
                 # the plane GEMM, whose epilogue writes those maxima — OneTransModel allocates them under pair_form())
                 pair_w2 = (orient == 'fwd' and name.endswith('.w2') and name.startswith('blk.')
                            and K % TILE == 0 and N % 16 == 0)
-                kscale = gamma if (orient == 'fwd' and gamma is not None) else (-2 if pair_w2 else -1)
+                # pair_dgrad: the FFN2 / FFN1 / Wo dgrad images too (their A operands' row maxima come from the
+                # producers: ot_dropout_apply_ex / rowabs_out, or ot_rows_absmax)
+                pair_dg = (pair_dgrad and orient == 'dgrad' and name.startswith('blk.')
+                           and name.endswith(('.w1', '.w2', '.wo')))
+                kscale = gamma if (orient == 'fwd' and gamma is not None) else (-2 if (pair_w2 or pair_dg) else -1)
                 irecs.append((o, sn, sk, K * N, kscale, ioff, units, G, Nb, Kb))
                 self.images[(name, orient)] = (ioff, G, Nb, Kb)
                 if kscale != -1:

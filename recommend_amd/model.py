@@ -234,8 +234,9 @@ def _block_forward(m, l, x, I, Kq, seed, training, rstd_in=None, select=False, n
     qp_f = _attn_qpos(cfg, pos)
     qkv16 = (torch.empty(B * I, 3 * d, dtype=torch.int16, device=dev)
              if m.attn_fp8 and training and K.attn_bwd_bf16_supported(I, Kq, hd, qp_f) else None)
+    am_o = (m.amax_slot(l, 0) if training and not m.attn_fp8 and K.attn_amax_supported(I, Kq, hd, qp_f) else None)
     K.attn_fwd(qkv, 3 * d, B, H, I, Kq, hd, o, lse, qpos=qp_f, fp8=m.attn_fp8,
-               dequant=m.attn_fp8 and training, fp8_terms=m.fp8_terms, deq16=qkv16)
+               dequant=m.attn_fp8 and training, fp8_terms=m.fp8_terms, deq16=qkv16, amax=am_o)
     if qkv16 is not None:
         qkv = qkv16
     # x1 = x[tail] + drop(o @ Wo)      (model.py:117, 193)
@@ -288,7 +289,8 @@ def _block_forward(m, l, x, I, Kq, seed, training, rstd_in=None, select=False, n
         K.gemm_rms(OT_GEMM_NT, x1 if x1_16 is None else x1_16, d, d, mt['rows'][1], w1, d * f, d, f, mt['tile_group'],
                    nt, u, f, mt['rows'][1], a_xform=OT_AX_RMSNORM if x1_16 is None else OT_AX_BF16_RMSNORM,
                    rstd=rstd2, gamma=g2, bias=b1, bias_gstride=f, epi=OT_EPI_BIAS, m_rows=maps['tail'].nrows,
-                   bimg=m.bimg(f'blk.{l}.w1'), rowmax_out=umax, rowmax_n=umax.shape[1])
+                   bimg=m.bimg(f'blk.{l}.w1'), rowmax_out=umax, rowmax_n=umax.shape[1],
+                   amax_out=m.amax_slot(l, 1) if training else None)   # |U| >= |gelu(U)|: the W2 wgrad's A bound
     else:
         K.gemm(OT_GEMM_NT, x1 if x1_16 is None else x1_16, d, d, mt['rows'][1], w1, d * f, d, f, mt['tile_group'],
                nt, u, f, mt['rows'][1], a_xform=OT_AX_RMSNORM if x1_16 is None else OT_AX_BF16_RMSNORM, rstd=rstd2,
@@ -387,11 +389,28 @@ class _Block(torch.autograd.Function):
         du_bf = (fused2 and h is not None and m.bimg(f'blk.{l}.w1', 'dgrad') is not None)
         # FFN branch: dY2 = mask(dx2) — in bf16 with the bf16 dU path (its two readers, the FFN2 dgrad's A and
         # the W2 weight gradient's D, round it to bf16; the latter then runs copy-staged)
+        # fp16-pair weight gradients (split mode): magnitude bounds of their operands, folded in by the producers
+        # (amax_slot; None = no bound, the exact split runs).  |U| from the FFN1 forward (its plane-GEMM epilogue, the
+        # pair-form W2 path), |O| from the slice attention forward
+        am = lambda i: m.amax_slot(l, i)
+        qp_b = _attn_qpos(cfg, pos)
+        b_u = am(1) if m.u_bound_ok(l) else None
+        b_o = am(0) if (am(0) is not None and not m.attn_fp8 and K.attn_amax_supported(I, Kq, hd, qp_b)) else None
+        b_dy2 = b_du = b_dyo = b_dq = None
+        # fp16-pair dgrads (pair-form dgrad images): the A rows' maxima, from the producers where they report them
+        pw2, pw1, pwo = (m.dgrad_pair(f'blk.{l}.{w}') for w in ('w2', 'w1', 'wo'))
+        rm_dy2 = torch.empty(B * Kq, (d + 255) // 256, device=dev) if pw2 else None
         if rate > 0:
             dy2 = torch.empty(B * Kq, d, device=dev, dtype=torch.int16 if du_bf else torch.float32)
-            K.dropout_apply(dx2, d, dy2, d, B * Kq, d, seed, 2 * l + 1, rate, tail)
+            b_dy2 = am(2) if not du_bf else None
+            K.dropout_apply(dx2, d, dy2, d, B * Kq, d, seed, 2 * l + 1, rate, tail, amax=b_dy2,
+                            rowmax=rm_dy2 if not du_bf else None)
         else:
             dy2 = dx2
+            if rm_dy2 is not None:
+                K.rows_absmax(dy2, d, B * Kq, d, rm_dy2)
+        pa2 = dict(a_rowmax=rm_dy2, a_rowmax_n=rm_dy2.shape[1]) if pw2 else {}
+        rm_du = torch.empty(B * Kq, (f + TILE - 1) // TILE, device=dev) if pw1 else None
         dy_bf = dy2.dtype == torch.int16
         # bf16 mode (C5): dU is stored in bf16 by the FFN2 dgrad epilogue (OT_EPI_C_BF16); its two consumers,
         # the FFN1 dgrad (bf16 A, plane GEMM) and the W1 weight gradient (OT_WG_D_BF16), rounded it to bf16 at
@@ -410,7 +429,9 @@ class _Block(torch.autograd.Function):
                         m.g(f'blk.{l}.w2'), f * d, m.g(f'blk.{l}.b2'), d,
                         a_xform=(OT_AX_GELU if h is None else OT_AX_BF16) | (OT_WG_D_BF16 if dy_bf else 0),
                         accumulate=acc, device=dev,
-                        m_rows=maps['tail'].nrows, rowmap=maps['tail'])
+                        m_rows=maps['tail'].nrows, rowmap=maps['tail'],
+                        a_bound=b_u if h is None else None, d_bound=b_dy2)
+        b_du = am(3) if not du_bf else None
         if fused2:
             # d > 128: the FFN2 dgrad also emits rowdot[row][f-tile] = sum dU (U - b1) for the norm2 backward
             rowdot = torch.empty(B * Kq, f // TILE, device=dev)
@@ -419,27 +440,41 @@ class _Block(torch.autograd.Function):
                        epi=OT_EPI_GELU_BWD | OT_EPI_ROWDOT | cbf | (OT_EPI_AUX_BF16 if u.dtype == torch.int16 else 0),
                        bias=m.p(f'blk.{l}.b1'), bias_gstride=f, rowdot=rowdot, rowdot_n=f // TILE,
                        m_rows=maps['tail'].nrows, device=dev, bimg=m.bimg(f'blk.{l}.w2', 'dgrad'),
-                       gelu_out=hbf, ldgelu=f)
+                       gelu_out=hbf, ldgelu=f, amax_out=b_du, rowabs_out=rm_du,
+                       rowabs_n=rm_du.shape[1] if rm_du is not None else 0, **pa2)
             if hbf is not None:
                 with m.side(hbf, dy2):
                     K.wgrad(hbf, f, mt['rows'][1], dy2, d, mt['rows'][1], f, d, mt, nct, G, m.g(f'blk.{l}.w2'),
                             f * d, m.g(f'blk.{l}.b2'), d, a_xform=OT_AX_BF16, accumulate=acc, device=dev,
                             m_rows=maps['tail'].nrows, rowmap=maps['tail'])
+        elif (b_du is not None or pw2 or pw1) and f % TILE == 0:   # (bounds need the whole-tile vector epilogue)
+            K.gemm_rms(OT_GEMM_NT, dy2, d, d, mt['rows'][1], m.p(f'blk.{l}.w2'), f * d, d, f, mt['tile_group'], nt, du,
+                       f, mt['rows'][1], epi=OT_EPI_GELU_BWD, aux=u, ldaux=f, m_rows=maps['tail'].nrows, device=dev,
+                       bimg=m.bimg(f'blk.{l}.w2', 'dgrad'), amax_out=b_du, rowabs_out=rm_du,
+                       rowabs_n=rm_du.shape[1] if rm_du is not None else 0, **pa2)
         else:
-            K.gemm(OT_GEMM_NT, dy2, d, d, mt['rows'][1], m.p(f'blk.{l}.w2'), f * d, d, f, mt['tile_group'], nt, du,
-                   f, mt['rows'][1], epi=OT_EPI_GELU_BWD, aux=u, ldaux=f, m_rows=maps['tail'].nrows,
-                   bimg=m.bimg(f'blk.{l}.w2', 'dgrad'))
+            b_du = None
+            K.gemm_rms(OT_GEMM_NT, dy2, d, d, mt['rows'][1], m.p(f'blk.{l}.w2'), f * d, d, f, mt['tile_group'], nt, du,
+                       f, mt['rows'][1], epi=OT_EPI_GELU_BWD, aux=u, ldaux=f, m_rows=maps['tail'].nrows, device=dev,
+                       bimg=m.bimg(f'blk.{l}.w2', 'dgrad'), **pa2)
+            if rm_du is not None:
+                K.rows_absmax(du, f, B * Kq, f, rm_du := torch.empty(B * Kq, (f + 255) // 256, device=dev))
+        pa1 = dict(a_rowmax=rm_du, a_rowmax_n=rm_du.shape[1]) if pw1 else {}
+        rm_dyo = torch.empty(B * Kq, (d + TILE - 1) // TILE, device=dev) if pwo else None
         a1n = x1n is not None and du_bf               # both operands bf16: the copy-staged weight gradient
         with m.side(x1n if a1n else x1, du, rstd2):
             K.wgrad(x1n if a1n else x1, d, mt['rows'][1], du, f, mt['rows'][1], d, f, mt, nct, G, m.g(f'blk.{l}.w1'),
                     d * f, m.g(f'blk.{l}.b1'), f,
                     a_xform=(OT_AX_BF16 if a1n else OT_AX_RMSNORM) | (OT_WG_D_BF16 if du_bf else 0), rstd=rstd2,
                     gamma=m.p(f'blk.{l}.norm2'),
-                    accumulate=acc, device=dev, m_rows=maps['tail'].nrows, rowmap=maps['tail'])
+                    accumulate=acc, device=dev, m_rows=maps['tail'].nrows, rowmap=maps['tail'], d_bound=b_du)
         # FFN1 dgrad -> norm2 backward + residual; emit mask(dx1) for the attention branch
         dx1 = torch.empty(B * Kq, d, device=dev)
         dyo = torch.empty(B * Kq, d, device=dev) if rate > 0 else dx1
+        dyo_rows = False                       # did the FFN1 dgrad's epilogue write dyo's row maxima (rm_dyo)?
         if m.fuse_bwd or rowdot is not None:   # FFN1 dgrad -> norm2 backward in the epilogue
+            b_dyo = am(4)
+            dyo_rows = rm_dyo is not None
             K.gemm_rms(OT_GEMM_NT, du, f, f, mt['rows'][1], m.p(f'blk.{l}.w1'), d * f, f, d, mt['tile_group'], nt,
                        dx1, d, mt['rows'][1], epi=OT_EPI_RMSNORM_BWD | (OT_EPI_DROPOUT if rate > 0 else 0),
                        a_xform=OT_AX_BF16 if du_bf else 0,
@@ -447,20 +482,26 @@ class _Block(torch.autograd.Function):
                        ngamma=m.p(f'blk.{l}.norm2'), nrstd=rstd2, dres=dx2, lddres=d,
                        dx_masked=dyo if rate > 0 else None, lddxm=d, dgamma=m.g(f'blk.{l}.norm2'),
                        accumulate_dgamma=acc, device=dev, bimg=m.bimg(f'blk.{l}.w1', 'dgrad'),
-                       rowdot=rowdot, rowdot_n=f // TILE if rowdot is not None else 0)
+                       rowdot=rowdot, rowdot_n=f // TILE if rowdot is not None else 0, amax_out=b_dyo,
+                       rowabs_out=rm_dyo, rowabs_n=rm_dyo.shape[1] if rm_dyo is not None else 0, **pa1)
         else:
             dxn2 = torch.empty(B * Kq, d, device=dev)
-            K.gemm(OT_GEMM_NT, du, f, f, mt['rows'][1], m.p(f'blk.{l}.w1'), d * f, f, d, mt['tile_group'], nt, dxn2,
-                   d, mt['rows'][1], m_rows=maps['tail'].nrows, bimg=m.bimg(f'blk.{l}.w1', 'dgrad'))
+            K.gemm_rms(OT_GEMM_NT, du, f, f, mt['rows'][1], m.p(f'blk.{l}.w1'), d * f, f, d, mt['tile_group'], nt,
+                       dxn2, d, mt['rows'][1], epi=0, m_rows=maps['tail'].nrows, device=dev,
+                       bimg=m.bimg(f'blk.{l}.w1', 'dgrad'), **pa1)
             K.rmsnorm_bwd(dxn2, d, x1, d, m.p(f'blk.{l}.norm2'), rstd2, dx1, d, B * Kq, d, dres=dx2, lddres=d,
                           dx_masked=dyo if rate > 0 else None, lddxm=d, seed=seed, site=2 * l, drop=rate,
                           tail=tail, dgamma=m.g(f'blk.{l}.norm2'), accumulate=acc, device=dev)
         # Wo
         with m.side(o, dyo):
-            _wgrad_single(m, o, dyo, d, d, mt, m.g(f'blk.{l}.wo'), acc, dev, maps['tail'].nrows, maps['tail'])
+            _wgrad_single(m, o, dyo, d, d, mt, m.g(f'blk.{l}.wo'), acc, dev, maps['tail'].nrows, maps['tail'],
+                          a_bound=b_o, d_bound=b_dyo)
         do = torch.empty(B * Kq, d, device=dev)
-        K.gemm(OT_GEMM_NT, dyo, d, d, mt['rows'][1], m.p(f'blk.{l}.wo'), 0, d, d, mt['tile_group'], nt, do, d,
-               mt['rows'][1], m_rows=maps['tail'].nrows, bimg=m.bimg(f'blk.{l}.wo', 'dgrad'))
+        if pwo and not dyo_rows:                     # dX1 came from the row-wise norm backward: its maxima here
+            K.rows_absmax(dyo, d, B * Kq, d, rm_dyo := torch.empty(B * Kq, (d + 255) // 256, device=dev))
+        K.gemm_rms(OT_GEMM_NT, dyo, d, d, mt['rows'][1], m.p(f'blk.{l}.wo'), 0, d, d, mt['tile_group'], nt, do, d,
+                   mt['rows'][1], epi=0, m_rows=maps['tail'].nrows, device=dev, bimg=m.bimg(f'blk.{l}.wo', 'dgrad'),
+                   **(dict(a_rowmax=rm_dyo, a_rowmax_n=rm_dyo.shape[1]) if pwo else {}))
         # attention
         # bf16 mode, key-grouped backward (C5): dQKV in bf16 (OT_ATTN_DQKV_BF16) — the QKV dgrad (bf16 A) and
         # the Wqkv weight gradient (OT_WG_D_BF16) round it to bf16 anyway: the same values, half the bytes
@@ -471,14 +512,16 @@ class _Block(torch.autograd.Function):
         dqkv = torch.empty(B * I, 3 * d, device=dev, dtype=torch.int16 if dq_bf else torch.float32)
         if Kq < I:
             dqkv[:, :d].zero_()
-        K.attn_bwd(qkv, 3 * d, o, do, lse, B, H, I, Kq, hd, dqkv, qpos=qp, dq_part_bf16=True)
+        b_dq = am(5) if (am(5) is not None and not dq_bf and K.attn_amax_supported(I, Kq, hd, qp, backward=True)) \
+            else None
+        K.attn_bwd(qkv, 3 * d, o, do, lse, B, H, I, Kq, hd, dqkv, qpos=qp, dq_part_bf16=True, amax=b_dq)
         an1 = xn1 is not None and dq_bf
         with m.side(xn1 if an1 else x, dqkv, rstd1):
             K.wgrad(xn1 if an1 else x, d, ma['rows'][0], dqkv, 3 * d, ma['rows'][0], d, 3 * d, ma, nca, G,
                     m.g(f'blk.{l}.wqkv'), 3 * d * d, None, 0,
                     a_xform=(OT_AX_BF16 if an1 else OT_AX_RMSNORM) | (OT_WG_D_BF16 if dq_bf else 0), rstd=rstd1,
                     gamma=m.p(f'blk.{l}.norm1'), accumulate=acc, device=dev, m_rows=maps['all'].nrows,
-                    rowmap=maps['all'])
+                    rowmap=maps['all'], d_bound=b_dq)
         ax_dq = OT_AX_BF16 if dq_bf else 0
         dx = torch.empty(B * I, d, device=dev)
         if m.fuse_bwd:         # QKV dgrad -> norm1 backward + residual (dx1 on the kept tail rows)
@@ -502,7 +545,7 @@ class _Block(torch.autograd.Function):
         return None, dx, None, None, None, None, None, None, None, None
 
 
-def _wgrad_single(m, A, D, K_, N, mt, dW, acc, dev, mrows=0, rowmap=None):
+def _wgrad_single(m, A, D, K_, N, mt, dW, acc, dev, mrows=0, rowmap=None, a_bound=None, d_bound=None):
     """Wo gradient: one weight shared by every group -> wgrad with every chunk mapped to group 0
     (chunked by layout.wgrad_slots for its single output tile when the row map is given)."""
     if rowmap is not None and rowmap.group_rows:
@@ -511,7 +554,7 @@ def _wgrad_single(m, A, D, K_, N, mt, dW, acc, dev, mrows=0, rowmap=None):
     else:
         mp = m.single_group_chunks(mt)
     K.wgrad(A, K_, mt['rows'][1], D, N, mt['rows'][1], K_, N, mp, mp['chunks'].shape[0], 1, dW, 0, None, 0,
-            accumulate=acc, device=dev, m_rows=mrows)
+            accumulate=acc, device=dev, m_rows=mrows, a_bound=a_bound, d_bound=d_bound)
 
 
 class _Head(torch.autograd.Function):
@@ -700,7 +743,10 @@ class OneTransModel(nn.Module):
         if self.fp8_terms not in (1, 2):
             raise ValueError(f'fp8_terms {self.fp8_terms}: 1 or 2')
         self.f_ns = cfg.ns_input_width()
-        self.layout = FlatLayout(cfg, self.f_ns)
+        # split mode: the FFN2 / FFN1 / Wo dgrad GEMMs on the scaled fp16 pair (pair-form dgrad images, the A rows'
+        # maxima from their producers; ONETRANS_PAIR_DGRAD=0: the six-product split)
+        self.pair_dgrad = os.environ.get('ONETRANS_PAIR_DGRAD', '1') != '0'
+        self.layout = FlatLayout(cfg, self.f_ns, pair_dgrad=self.pair_dgrad)
         self.cfg_Lnsd = cfg.num_ns_tokens * cfg.hidden_dim
         self.flat = nn.Parameter(torch.zeros(self.layout.total, device=self.device))
         self.flat.grad = torch.zeros_like(self.flat)
@@ -737,6 +783,12 @@ class OneTransModel(nn.Module):
         self._x16 = None
         # block weight gradients run on a second stream, overlapping the dgrad chain
         self.overlap_wgrad = True            # bench.py --no-overlap turns it off for standalone kernel traces
+        # split mode: weight gradients on the scaled fp16 pair (ot_mixed_gemm_wgrad_ex) wherever the operands'
+        # producers report a magnitude bound: per layer [|O|, |U|, |dY2|, |dU|, |dX1 masked|, |dQKV|] (amax_slot),
+        # zeroed at every forward, folded in atomically by the producing kernels (ONETRANS_PAIR_WGRAD=0: the exact
+        # six-product split everywhere)
+        self.pair_wgrad = os.environ.get('ONETRANS_PAIR_WGRAD', '1') != '0'
+        self._amax = None
         self._side = None
         self._side_used = False
         self._side_keep: List[torch.Tensor] = []
@@ -808,6 +860,27 @@ class OneTransModel(nn.Module):
         if self.config.hidden_dim == TILE:
             return True
         return all(self.bimg(n, o) is not None for (n, o) in images)
+
+    def dgrad_pair(self, name: str) -> bool:
+        """Is ``name``'s dgrad image in the scaled-fp16-pair form (split mode, ONETRANS_PAIR_DGRAD), so its dgrad GEMM
+        must get its A rows' maxima (a_rowmax)?"""
+        return (K.matmul_mode() == 'split' and (name, 'dgrad') in self.layout.pair_images
+                and self.bimg(name, 'dgrad') is not None)
+
+    def u_bound_ok(self, l: int) -> bool:
+        """Did block l's FFN1 forward report |U| (amax slot 1)?  It does on the pair-form W2 path (the plane GEMM with
+        row maxima, _block_forward's ``pair_w2``)."""
+        return (self.amax_slot(l, 1) is not None and self.bimg(f'blk.{l}.w2') is not None
+                and (f'blk.{l}.w2', 'fwd') in self.layout.pair_images)
+
+    def amax_slot(self, l: int, i: int) -> Optional[torch.Tensor]:
+        """One float of layer l's magnitude bounds (slots: 0 |O|, 1 |U|, 2 |dY2|, 3 |dU|, 4 |dX1 masked|, 5 |dQKV|),
+        or None outside the split mode / with ONETRANS_PAIR_WGRAD=0."""
+        if not self.pair_wgrad or K.matmul_mode() != 'split':
+            return None
+        if self._amax is None:
+            self._amax = torch.zeros(self.config.num_layers, 8, device=self.device)
+        return self._amax[l, i:i + 1]
 
     def x16_on(self, d: int) -> bool:
         """Store bf16 copies of the residual stream for the next GEMM's A (bf16 mode, plane GEMMs)?"""
@@ -1104,6 +1177,8 @@ class OneTransModel(nn.Module):
     def forward_probs(self, ns, seq, training: bool) -> torch.Tensor:
         """All tasks as one [T, B] tensor (the trainer's fused loss consumes it)."""
         plan = self._plan(ns, seq, training)
+        if self._amax is not None:
+            self._amax.zero_()                   # the producers of this step fold their output maxima in
         seed = 0
         if training:
             self._step += 1

@@ -259,3 +259,124 @@ def test_pair_slice_attention(dev, B, H, I, Kq, hd, case):
                 ref.abs().max().item())
     check_ratio(f'attn bwd B{B} I{I} K{Kq} hd{hd} {case}', errs(gp, qr.grad), errs(gf, qr.grad),
                 qr.grad.abs().max().item())
+
+
+@pytest.mark.parametrize('K_,N', [(128, 384), (128, 512), (512, 128), (256, 1024)])
+@pytest.mark.parametrize('ax', ['rmsnorm', 'gelu', 'none'])
+@pytest.mark.parametrize('case', ['normal', 'outlier', 'row_range'])
+def test_pair_wgrad(dev, K_, N, ax, case):
+    """Weight gradient dW[g] = sum_r pro(A[r])^T D[r] on the fp16 pair (ot_mixed_gemm_wgrad_ex): per-tensor bounds
+    of |A| / |D| (the RMSNorm prologue's A bounded by sqrt(K) |gamma_k| itself), against float64 and beside native
+    f32 on the same operands.  'row_range': D rows spanning 1e-6 .. 1 (per-sample gradients), A outliers 1e4x."""
+    from recommend_amd._lib import OT_AX_NONE
+    gen = torch.Generator().manual_seed(K_ + N + len(ax) * 7 + len(case))
+    G, M = 3, 1500
+    rm, d = group_map(M, G, dev)
+    A = rows('outlier' if case != 'normal' else 'normal', M, K_, gen).float()
+    D = torch.randn(M, N, generator=gen, dtype=torch.float64)
+    if case == 'row_range':
+        D *= 10.0 ** (-6 * torch.rand(M, 1, generator=gen, dtype=torch.float64))
+    elif case == 'outlier':
+        D[torch.arange(M), torch.randint(0, N, (M,), generator=gen)] *= 1e3
+    D = D.float()
+    gamma = (1 + 0.3 * torch.randn(K_, generator=gen)).float()
+    rstd = (1.0 / torch.sqrt((A.double() ** 2).mean(1) + EPS)).float()
+    xf = {'rmsnorm': OT_AX_RMSNORM, 'gelu': OT_AX_GELU, 'none': OT_AX_NONE}[ax]
+    Ap = (A.double() * rstd.double()[:, None] * gamma.double() if ax == 'rmsnorm'
+          else gelu64(A.double()) if ax == 'gelu' else A.double())
+    g = torch.arange(M) % G
+    ref = torch.zeros(G, K_, N, dtype=torch.float64)
+    refb = torch.zeros(G, N, dtype=torch.float64)
+    for gi in range(G):
+        ref[gi] = Ap[g == gi].T @ D.double()[g == gi]
+        refb[gi] = D.double()[g == gi].sum(0)
+    a_bound = torch.tensor([A.abs().max().item()], device=dev)          # |gelu(u)| <= |u|
+    d_bound = torch.tensor([D.abs().max().item()], device=dev)
+    Ad, Dd = A.to(dev), D.to(dev)
+
+    def go(mode, pair=True):
+        dW = torch.full((G, K_, N), float('nan'), device=dev)
+        db = torch.full((G, N), float('nan'), device=dev)
+        K.wgrad(Ad, K_, d['rows'][0], Dd, N, d['rows'][1], K_, N, d, rm.chunks.shape[0], G, dW, K_ * N, db, N,
+                a_xform=xf, rstd=rstd.to(dev), gamma=gamma.to(dev), device=dev,
+                a_bound=a_bound if (pair and mode == 'split' and ax != 'rmsnorm') else None,
+                d_bound=d_bound if (pair and mode == 'split') else None)
+        return dW, db
+    (Wp, bp), (Wf, bf) = run_both(go)
+    assert torch.isfinite(Wp).all()
+    scale = ref.abs().max().item()
+    check_ratio(f'wgrad {ax} K{K_} N{N} {case}', errs(Wp, ref), errs(Wf, ref), scale)
+    torch.testing.assert_close(bp.double().cpu(), refb, rtol=1e-5, atol=1e-5 * refb.abs().max().item())
+    old = K.set_matmul_mode('split')
+    try:
+        W2, _ = go('split')
+    finally:
+        K.set_matmul_mode(old)
+    torch.cuda.synchronize()
+    assert torch.equal(W2, Wp), 'pair wgrad not deterministic'
+
+
+@pytest.mark.parametrize('K_,N', [(128, 512), (512, 128), (128, 128), (256, 1024)])
+@pytest.mark.parametrize('case', ['normal', 'outlier', 'row_range', 'underestimated'])
+@pytest.mark.parametrize('epi', ['none', 'gelu_bwd'])
+def test_pair_dgrad(dev, K_, N, case, epi):
+    """The dgrad GEMMs on the fp16 pair (pair-form dgrad image, A rows scaled from their producers' maxima
+    a_rowmax = max |a| parts): FFN2 dgrad (GELU' epilogue), FFN1 / Wo dgrads (plain), against float64 beside native
+    f32.  'row_range': rows spanning 1e-6 .. 1 (per-sample gradients: each row keeps its own 22 bits);
+    'underestimated': maxima 1e-4 of the truth — finite, saturated, deterministic."""
+    from recommend_amd._lib import OT_AX_NONE, OT_EPI_GELU_BWD
+    gen = torch.Generator().manual_seed(K_ * 3 + N + len(case) + len(epi))
+    G, M = 3, 1000
+    rm, d = group_map(M, G, dev)
+    A = torch.randn(M, K_, generator=gen, dtype=torch.float64)
+    if case == 'outlier':
+        A[torch.arange(M), torch.randint(0, K_, (M,), generator=gen)] *= 1e4
+    elif case == 'row_range':
+        A *= 10.0 ** (-6 * torch.rand(M, 1, generator=gen, dtype=torch.float64))
+    A = A.float()
+    W = (torch.randn(G, N, K_, generator=gen, dtype=torch.float64) / math.sqrt(K_)).float()
+    aux = torch.randn(M, N, generator=gen).float()
+    parts = (K_ + 255) // 256
+    rmax = torch.stack([A[:, 256 * j:256 * (j + 1)].abs().max(1).values for j in range(parts)], 1).contiguous()
+    if case == 'underestimated':
+        rmax = rmax * 1e-4
+    g = torch.arange(M) % G
+    ref = torch.einsum('mk,mnk->mn', A.double(), W.double()[g])
+    ge = epi == 'gelu_bwd'
+    if ge:
+        u = aux.double()
+        ref = ref * (0.5 * (1 + torch.erf(u / math.sqrt(2))) + u * torch.exp(-0.5 * u * u) / math.sqrt(2 * math.pi))
+    img, ntn = pair_image(W, dev)
+    kw = dict(epi=OT_EPI_GELU_BWD if ge else 0, aux=aux.to(dev) if ge else None, ldaux=N if ge else 0, device=dev)
+
+    def go(mode):
+        C = torch.full((M, N), float('nan'), device=dev)
+        if mode == 'split':
+            K.gemm_rms(OT_GEMM_NT, A.to(dev), K_, K_, d['rows'][0], W.to(dev), N * K_, K_, N, d['tile_group'],
+                       rm.ntiles, C, N, d['rows'][1], a_xform=OT_AX_NONE, bimg=(img, ntn, 0), a_rowmax=rmax.to(dev),
+                       a_rowmax_n=parts, **kw)
+        else:
+            K.gemm_rms(OT_GEMM_NT, A.to(dev), K_, K_, d['rows'][0], W.to(dev), N * K_, K_, N, d['tile_group'],
+                       rm.ntiles, C, N, d['rows'][1], a_xform=OT_AX_NONE, **kw)
+        return C
+    Cp, Cf = run_both(go)
+    assert torch.isfinite(Cp).all()
+    if case == 'underestimated':
+        old = K.set_matmul_mode('split')
+        try:
+            C2 = go('split')
+        finally:
+            K.set_matmul_mode(old)
+        torch.cuda.synchronize()
+        assert torch.equal(C2, Cp)
+        return
+    if case == 'row_range':          # per row: each row's error against that row's f32 error
+        ep = (Cp.double().cpu() - ref).abs().max(1).values
+        ef = (Cf.double().cpu() - ref).abs().max(1).values
+        floor = 8 * 2.0 ** -24 * ref.abs().max(1).values
+        worst = ((ep - PAIR_VS_F32 * ef - floor) / ref.abs().max(1).values).max().item()
+        print(f'dgrad {epi} K{K_} N{N} row_range: worst per-row excess {worst:.3e}, '
+              f'median ratio {(ep / ef.clamp_min(1e-300)).median().item():.2f}')
+        assert worst <= 0
+        return
+    check_ratio(f'dgrad {epi} K{K_} N{N} {case}', errs(Cp, ref), errs(Cf, ref), ref.abs().max().item())

@@ -310,7 +310,10 @@ def main():
         mm = model.matmul
         gpk = (BF16_MFMA_PEAK_TFLOPS / SPLIT_TERMS if mm == 'split' else
                BF16_MFMA_PEAK_TFLOPS if mm == 'bf16' else FP32_MFMA_PEAK_TFLOPS)
-        rep = probe.report(args.probe_steps, gpk, HBM_PEAK_GBS)
+        # each launch is floored against the ceiling of the arithmetic it issues: bf16 dense / 6 for the split-bf16
+        # kernels, / 3 for the fp16-pair ones (f16 dense = bf16 dense), bf16 dense for the bf16 mode
+        rep = probe.report(args.probe_steps, gpk, HBM_PEAK_GBS,
+                           terms_peak=lambda t: BF16_MFMA_PEAK_TFLOPS / t if t in (1, 3, 6) else FP32_MFMA_PEAK_TFLOPS)
 
     if rank != 0:
         if world > 1:
@@ -371,13 +374,14 @@ def main():
         traffic, tsrc = hbm_traffic(args.config)
         dom = rep['families']['mixed_gemm']
         if model.matmul == 'split':
-            # the GEMMs issue SPLIT_TERMS bf16 MFMA products per f32 product: their matrix-core
-            # ceiling in f32 flops is the bf16 dense peak / SPLIT_TERMS
-            gpeak = round(BF16_MFMA_PEAK_TFLOPS / SPLIT_TERMS, 1)
-            gkern = ('plane_gemm_kernel / mixed_gemm_kernel + wgrad_split_kernel (f32 operands split exactly into '
-                     f'3 bf16 parts, {SPLIT_TERMS} bf16 MFMA products per f32 product; peak = bf16 dense / {SPLIT_TERMS}; '
-                     'the RMSNorm-prologue plane GEMMs (QKV / FFN1 forward) issue 3 fp16 products of a scaled fp16 '
-                     'pair, so the family can exceed that ceiling by up to their share)')
+            # the GEMMs issue either 6 bf16 products per f32 product (the exact three-plane split) or 3 f16 products
+            # (the scaled fp16 pair): the family's ceiling is that of the mix it issued (mfma_peak_eff: its flops
+            # over sum flops_i / (bf16 dense / terms_i))
+            gpeak = round(dom['mfma_peak_eff'], 1)
+            gkern = ('plane_gemm_kernel / mixed_gemm_kernel + wgrad_split_kernel: f32 operands as a scaled fp16 pair '
+                     '(3 f16 MFMA products per f32 product; ceiling bf16 dense / 3 = 838.9) or split exactly into 3 bf16 '
+                     f'parts (6 products; / 6 = 419.5); peak = the issued mix\'s ceiling '
+                     f'({dom["pair_launches_per_step"]:.0f} of {dom["launches_per_step"]:.0f} launches per step on the pair)')
         elif model.matmul == 'bf16':
             gpeak = BF16_MFMA_PEAK_TFLOPS
             gkern = ('plane_gemm_kernel / mixed_gemm_kernel + wgrad_split_kernel (operands rounded to bf16, one bf16 '
@@ -431,7 +435,8 @@ def main():
             # head_dim-32 forward as 6 bf16 products of three planes), so that ceiling is bf16 dense / 3
             apeak = BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_MFMA_PEAK_TFLOPS
             issued_peak = BF16_MFMA_PEAK_TFLOPS if bf16 else BF16_MFMA_PEAK_TFLOPS / 3
-            busy_ms = fl('mixed_gemm') / (gpk * 1e9) + fl('attention') / (apeak * 1e9)
+            gpe = fams['mixed_gemm'].get('mfma_peak_eff') or gpk if 'mixed_gemm' in fams else gpk
+            busy_ms = fl('mixed_gemm') / (gpe * 1e9) + fl('attention') / (apeak * 1e9)
             res['attention_mfma'] = {
                 'core_tflops': round(att['tflops'], 2),
                 'core_frac': round(att['tflops'] / apeak, 4),

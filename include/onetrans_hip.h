@@ -355,11 +355,14 @@ int ot_attn_bwd_flags(const float* qkv, int64_t ld, const float* out, const floa
  * the slice forward's shapes), bit 2 the backward (also qpos NULL, the slice backward's shapes; it needs
  * ot_attn_bwd_flags_workspace_size bytes) — elsewhere the call is refused. */
 int ot_attn_amax_supported(int I, int K, int head_dim, int selected, int precision);
+/* rowmax (optional, either may be NULL): per-row maxima of |output| for an fp16-pair dgrad consumer's a_rowmax —
+ * forward [B*K][H] (row b*K + j, head h: max |O| over the head's columns), backward [B*I][3][H] (row b*I + p: the dQ,
+ * dK, dV parts per head; with K < I the dQ part of the rows without a query is not written: zero the array first) */
 int ot_attn_fwd_amax(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos,
-                     int head_dim, float* out, float* lse, float* amax, int precision, void* stream);
+                     int head_dim, float* out, float* lse, float* amax, float* rowmax, int precision, void* stream);
 int ot_attn_bwd_amax(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
                      int B, int H, int I, int K, const int32_t* qpos, int head_dim, float* dqkv,
-                     void* workspace, size_t ws_bytes, float* amax, int precision, void* stream);
+                     void* workspace, size_t ws_bytes, float* amax, float* rowmax, int precision, void* stream);
 
 /* Two-stage cached serving (paper §3.5.1; replaces the reference's defective cache path
  * model.py:94-98, 359-381, D6): candidate c (request req[c]) attends with the last Kq of its n

@@ -93,8 +93,9 @@ SIGNATURES = {
     'ot_attn_bwd_flags': (c_int, [P, I64, P, P, P, c_int, c_int, c_int, c_int, P, c_int, P, c_int, P, c_size_t, c_int, P]),
     'ot_attn_fwd_cached': (c_int, [P, I64, P, I64, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
     'ot_attn_amax_supported': (c_int, [c_int, c_int, c_int, c_int, c_int]),
-    'ot_attn_fwd_amax': (c_int, [P, I64, c_int, c_int, c_int, c_int, P, c_int, P, P, P, c_int, P]),
-    'ot_attn_bwd_amax': (c_int, [P, I64, P, P, P, c_int, c_int, c_int, c_int, P, c_int, P, P, c_size_t, P, c_int, P]),
+    'ot_attn_fwd_amax': (c_int, [P, I64, c_int, c_int, c_int, c_int, P, c_int, P, P, P, P, c_int, P]),
+    'ot_attn_bwd_amax': (c_int, [P, I64, P, P, P, c_int, c_int, c_int, c_int, P, c_int, P, P, c_size_t, P, P, c_int,
+                                 P]),
     'ot_pyramid_select': (c_int, [P, c_float, c_int, c_int, c_int, c_int, P, P, P, c_int, P]),
     'ot_rmsnorm_fwd': (c_int, [P, I64, P, P, I64, P, I64, c_int, c_float, P]),
     'ot_rmsnorm_bwd_workspace_size': (c_size_t, [I64, c_int]),

@@ -59,6 +59,9 @@ struct AttnArgs {
   // OT_ATTN_DQ_PART_BF16 (with OT_ATTN_DQKV_BF16): the slices' dQ partials are stored rounded to bf16 (half the
   // partial traffic; summed in f32 by attn_dq_reduce_kernel, then rounded once more)
   int dq_part16;
+  // short-tail backward, f32 dqkv (fp16-pair consumers' bounds): max |dQKV| folded in (one float, zeroed by the
+  // caller) and the per-row maxima [B*I][3][H] (dQ / dK / dV part per head; the caller zeroes the array)
+  float* amax; float* rowmax;
 };
 
 // position of kept query j (< K) of the sample whose qpos slice is qp (null: the tail rule)
@@ -1364,6 +1367,7 @@ __global__ __launch_bounds__(256) void attn_bwd_small_kernel(AttnArgs p) {
   float* dK = p.dqkv + tok0 * p.ld + p.d + h * HD + 4 * sub;
   float* dV = dK + p.d;
   const int32_t* qp = p.qpos ? p.qpos + (int64_t)b * K : nullptr;
+  float am = 0.f;                                      // max |stored dK / dV / dQ| (p.amax)
   f32x4 q[KQ], o[KQ], dq[KQ];
   float lse[KQ], delta[KQ];
   int qpos[KQ];
@@ -1420,6 +1424,20 @@ __global__ __launch_bounds__(256) void attn_bwd_small_kernel(AttnArgs p) {
         *reinterpret_cast<f32x4*>(dV + ro) = dv;
       }
     }
+    if (p.rowmax || p.amax) {                          // (uniform) magnitude bounds of the stored rows
+      float rk = live ? amax4(0.f, dk) : 0.f, rv = live ? amax4(0.f, dv) : 0.f;
+#pragma unroll
+      for (int off = 1; off < LPK; off <<= 1) {
+        rk = fmaxf(rk, __shfl_xor(rk, off, 64));
+        rv = fmaxf(rv, __shfl_xor(rv, off, 64));
+      }
+      am = fmaxf(am, fmaxf(rk, rv));
+      if (p.rowmax && live && sub == 0) {
+        float* rr = p.rowmax + (tok0 + key) * 3 * p.H + h;
+        rr[p.H] = rk;
+        rr[2 * p.H] = rv;
+      }
+    }
   }
 #pragma unroll
   for (int j = 0; j < KQ; ++j) {
@@ -1437,7 +1455,15 @@ __global__ __launch_bounds__(256) void attn_bwd_small_kernel(AttnArgs p) {
       else
         *reinterpret_cast<f32x4*>(p.dqkv + (tok0 + qpos[j]) * p.ld + h * HD + 4 * sub) = v;
     }
+    if (p.rowmax || p.amax) {                          // (uniform) the dQ row's bound
+      float rq = amax4(0.f, v);
+#pragma unroll
+      for (int off = 1; off < LPK; off <<= 1) rq = fmaxf(rq, __shfl_xor(rq, off, 64));
+      am = fmaxf(am, rq);
+      if (p.rowmax && slot == 0 && sub == 0) p.rowmax[(tok0 + qpos[j]) * 3 * p.H + h] = rq;
+    }
   }
+  if (p.amax) amax_flush(p.amax, am);
 }
 
 // Forward for a short query tail (K <= SMALL_K: the last layer's single query after DCE), the f32-accurate modes.
@@ -1692,7 +1718,8 @@ extern "C" int ot_attn_fwd_cached(const float* qkv, int64_t ld, const float* kv_
 
 
 static int attn_fwd_impl(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos,
-                         int head_dim, float* out, float* lse, int precision, void* stream, float* amax);
+                         int head_dim, float* out, float* lse, int precision, void* stream, float* amax,
+                         float* rowmax = nullptr);
 
 extern "C" int ot_attn_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos,
                            int head_dim, float* out, float* lse, int precision, void* stream) {
@@ -1702,21 +1729,24 @@ extern "C" int ot_attn_fwd(const float* qkv, int64_t ld, int B, int H, int I, in
 extern "C" int ot_attn_amax_supported(int I, int K, int head_dim, int selected, int precision) {
   // the slice kernels fold max |output| in as they store: bit 1 the forward (O), bit 2 the backward (dQKV, tail
   // queries; its long forms reach I 544 at head_dim 64)
-  if (precision != OT_MATMUL_SPLIT_BF16 || K <= SMALL_K) return 0;
+  if (precision != OT_MATMUL_SPLIT_BF16) return 0;
+  if (K <= SMALL_K) return (head_dim == 32 || head_dim == 64 || head_dim == 128) ? 2 : 0;   // the short-tail backward
   return (attn_slice_fwd_supported(I, K, head_dim) ? 1 : 0) |
          (!selected && attn_slice_bwd_supported(I, K, head_dim, false) ? 2 : 0);
 }
 
 extern "C" int ot_attn_fwd_amax(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos,
-                                int head_dim, float* out, float* lse, float* amax, int precision, void* stream) {
-  OT_REQUIRE(amax && (ot_attn_amax_supported(I, K, head_dim, qpos != nullptr, precision) & 1),
+                                int head_dim, float* out, float* lse, float* amax, float* rowmax, int precision,
+                                void* stream) {
+  OT_REQUIRE((amax || rowmax) && (ot_attn_amax_supported(I, K, head_dim, qpos != nullptr, precision) & 1),
              "ot_attn_fwd_amax: the output bound needs the slice forward (split mode, I %d K %d head_dim %d: see "
              "ot_attn_amax_supported)", I, K, head_dim);
-  return attn_fwd_impl(qkv, ld, B, H, I, K, qpos, head_dim, out, lse, precision, stream, amax);
+  return attn_fwd_impl(qkv, ld, B, H, I, K, qpos, head_dim, out, lse, precision, stream, amax, rowmax);
 }
 
 static int attn_fwd_impl(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos,
-                         int head_dim, float* out, float* lse, int precision, void* stream, float* amax) {
+                         int head_dim, float* out, float* lse, int precision, void* stream, float* amax,
+                         float* rowmax) {
   OT_REQUIRE(precision == OT_MATMUL_F32 || precision == OT_MATMUL_SPLIT_BF16 || precision == OT_MATMUL_BF16,
              "ot_attn_fwd: unknown precision %d", precision);
   OT_REQUIRE(qkv && out && lse, "ot_attn_fwd: null operand");
@@ -1742,7 +1772,7 @@ static int attn_fwd_impl(const float* qkv, int64_t ld, int B, int H, int I, int 
   }
   if (mm == OT_MATMUL_SPLIT_BF16 && attn_slice_fwd_supported(I, K, head_dim)) {
     // short sequence, f32-accurate: one workgroup per (sample, head) slice on split-bf16 MFMA
-    return attn_slice_fwd(qkv, ld, B, H, I, K, qpos, head_dim, out, lse, (hipStream_t)stream, amax);
+    return attn_slice_fwd(qkv, ld, B, H, I, K, qpos, head_dim, out, lse, (hipStream_t)stream, amax, rowmax);
   }
   if (head_dim >= 32 && (mm == OT_MATMUL_BF16 || (mm == OT_MATMUL_SPLIT_BF16 && !kv_fits && I > 256))) {
     // split-bf16: long sequences (I > 256), with the next key block prefetched (short ones stay on
@@ -1835,18 +1865,18 @@ extern "C" size_t ot_attn_bwd_flags_workspace_size(int B, int H, int I, int K, i
 static int attn_bwd_impl(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
                          int B, int H, int I, int K, const int32_t* qpos, int head_dim, float* dqkv,
                          float* delta_ws, size_t ws_bytes, int prec, void* stream, int flags = 0,
-                         float* amax = nullptr);
+                         float* amax = nullptr, float* rowmax = nullptr);
 
 extern "C" int ot_attn_bwd_amax(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
                                 int B, int H, int I, int K, const int32_t* qpos, int head_dim, float* dqkv,
-                                void* workspace, size_t ws_bytes, float* amax, int precision, void* stream) {
-  OT_REQUIRE(amax && !qpos && precision == OT_MATMUL_SPLIT_BF16 && K > SMALL_K &&
-                 attn_slice_bwd_supported(I, K, head_dim, false) &&
-                 ws_bytes >= ot_attn_bwd_flags_workspace_size(B, H, I, K, head_dim, 0, 0, precision),
+                                void* workspace, size_t ws_bytes, float* amax, float* rowmax, int precision,
+                                void* stream) {
+  OT_REQUIRE((amax || rowmax) && (ot_attn_amax_supported(I, K, head_dim, qpos != nullptr, precision) & 2) &&
+                 ws_bytes >= ot_attn_bwd_flags_workspace_size(B, H, I, K, head_dim, qpos != nullptr, 0, precision),
              "ot_attn_bwd_amax: the dQKV bound needs the slice backward (split mode, tail queries, I %d K %d head_dim "
              "%d, ot_attn_bwd_flags_workspace_size bytes)", I, K, head_dim);
   return attn_bwd_impl(qkv, ld, out, dout, lse, B, H, I, K, qpos, head_dim, dqkv, (float*)workspace, ws_bytes,
-                       precision, stream, 0, amax);
+                       precision, stream, 0, amax, rowmax);
 }
 
 extern "C" int ot_attn_bwd(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
@@ -1887,7 +1917,8 @@ extern "C" int ot_attn_bwd_flags(const float* qkv, int64_t ld, const float* out,
 
 static int attn_bwd_impl(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse,
                          int B, int H, int I, int K, const int32_t* qpos, int head_dim, float* dqkv,
-                         float* delta_ws, size_t ws_bytes, int prec, void* stream, int flags, float* amax) {
+                         float* delta_ws, size_t ws_bytes, int prec, void* stream, int flags, float* amax,
+                         float* rowmax) {
   OT_REQUIRE(prec == OT_MATMUL_F32 || prec == OT_MATMUL_SPLIT_BF16 || prec == OT_MATMUL_BF16,
              "ot_attn_bwd: unknown precision %d", prec);
   OT_REQUIRE(qkv && out && dout && lse && dqkv && delta_ws, "ot_attn_bwd: null operand");
@@ -1900,8 +1931,10 @@ static int attn_bwd_impl(const float* qkv, int64_t ld, const float* out, const f
   if (mm == OT_MATMUL_SPLIT_BF16 && flags == 0 && K > SMALL_K && attn_slice_bwd_supported(I, K, head_dim, qpos != nullptr) &&
       ws_bytes >= attn_slice_bwd_min_ws(B, H, I, K, head_dim))
     return attn_slice_bwd(qkv, ld, out, dout, lse, B, H, I, K, head_dim, dqkv, delta_ws, ws_bytes, (hipStream_t)stream,
-                          amax);
-  OT_REQUIRE(!amax, "ot_attn_bwd_amax: shape not on the slice backward");
+                          amax, rowmax);
+  OT_REQUIRE((!amax && !rowmax) || K <= SMALL_K, "ot_attn_bwd_amax: shape not on the slice / short-tail backward");
+  p.amax = amax;
+  p.rowmax = rowmax;
   // the f32 head_dim-32 backward over tail queries forms its own row statistics (no prep launch)
   const bool fdl = !qpos && head_dim == 32 && K > SMALL_K && attn_kpad(K) <= FDL_KP &&
                    mm != OT_MATMUL_BF16;

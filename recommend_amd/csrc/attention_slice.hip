@@ -487,15 +487,21 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_fwd_slice_kernel(SliceArgs p
           o[m] = mmaN<NP>(fa, pp, o[m]);                              // O^T += V^T P^T
         }
       }
+      float rm = 0.f;                                                 // this lane's max |O| (rowmax)
       if (j < K) {
         const float inv = 1.f / (NP == 2 ? l * sv : l);               // (NP = 2: l and O^T carry 2^14, O^T sv)
         float* orow = p.out + ((int64_t)b * K + j) * p.d + h * HD + 4 * g;
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
           *reinterpret_cast<f32x4*>(orow + 16 * m) = o[m] * inv;
-          am = amax4(am, o[m] * inv);
+          rm = amax4(rm, o[m] * inv);
         }
+        am = fmaxf(am, rm);
         if (g == 0) p.lse[(int64_t)s * K + j] = NP == 2 ? (mx * cs - 14.f) * LN2 + __logf(l) : mx * LN2 + __logf(l);
+      }
+      if (p.rowmax) {                                                 // (uniform) the row's max |O| over its head
+        rm = group_max(rm);
+        if (j < K && g == 0) p.rowmax[((int64_t)b * K + j) * p.H + h] = rm;
       }
       idx = idxn;
     }
@@ -832,13 +838,25 @@ __global__ __launch_bounds__(64 * NWV, G2 ? 2 : 1) void attn_bwd_slice_kernel(Sl
           if (LAT) __builtin_amdgcn_sched_barrier(0);
         }
       }
+      float rk = 0.f, rv = 0.f;                                      // this lane's max |dK|, |dV| (rowmax)
       if (krow < I) {
         const float uk = NP == 2 ? 1.f / (sq * sds) : 1.f, uv = NP == 2 ? 1.f / (so * 16384.f) : 1.f;
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
           *reinterpret_cast<f32x4*>(dKg + (int64_t)krow * p.ld + 16 * m + 4 * g) = dk[m] * uk;
           *reinterpret_cast<f32x4*>(dVg + (int64_t)krow * p.ld + 16 * m + 4 * g) = dv[m] * uv;
-          am = amax4(amax4(am, dk[m] * uk), dv[m] * uv);
+          rk = amax4(rk, dk[m] * uk);
+          rv = amax4(rv, dv[m] * uv);
+        }
+        am = fmaxf(am, fmaxf(rk, rv));
+      }
+      if (p.rowmax) {                                // (uniform) [row][q / k / v part][head] maxima of dQKV rows
+        rk = group_max(rk);
+        rv = group_max(rv);
+        if (krow < I && g == 0) {
+          float* rr = p.rowmax + ((int64_t)(s / p.H) * I + krow) * 3 * p.H + (s % p.H);
+          rr[p.H] = rk;
+          rr[2 * p.H] = rv;
         }
       }
       kb = kbn;
@@ -980,13 +998,19 @@ __global__ __launch_bounds__(64 * NWV, G2 ? 2 : 1) void attn_bwd_slice_kernel(Sl
 #pragma unroll
       for (int m = 0; m < NM; ++m) dq[m] = (dq[m] + dq2[m]) * uq;
       const int j = 16 * qb + li;
+      float rq = 0.f;
       if (j < K) {
         float* drow = dQg + (int64_t)(q_off + j) * p.ld + 4 * g;
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
           *reinterpret_cast<f32x4*>(drow + 16 * m) = dq[m];
-          am = amax4(am, dq[m]);
+          rq = amax4(rq, dq[m]);
         }
+        am = fmaxf(am, rq);
+      }
+      if (p.rowmax) {                                // (uniform) the dQ part of the row's maxima
+        rq = group_max(rq);
+        if (j < K && g == 0) p.rowmax[((int64_t)(s / p.H) * I + q_off + j) * 3 * p.H + (s % p.H)] = rq;
       }
     }
     SLICE_STAMP(1, it, 5);
@@ -1152,7 +1176,7 @@ bool attn_slice_bwd_supported(int I, int K, int head_dim, bool selected) {
 }
 
 int attn_slice_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos, int head_dim,
-                   float* out, float* lse, hipStream_t stream, float* amax) {
+                   float* out, float* lse, hipStream_t stream, float* amax, float* rowmax) {
   using namespace slice;
   using KF = void (*)(SliceArgs);
   constexpr int P32 = fwd_planes(32), P64 = fwd_planes(64);
@@ -1168,6 +1192,7 @@ int attn_slice_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, con
   SliceArgs p{qkv, ld, H * head_dim, nullptr, nullptr, nullptr, out, lse, nullptr, B, H, I, K,
               1.f / sqrtf((float)head_dim), qpos};
   p.amax = amax;
+  p.rowmax = rowmax;
   const size_t lds = fwd_lds(I, head_dim, head_dim == 64 ? P64 : P32);
   const int nw = FWD_WAVES;
   OT_REQUIRE(make_schedule(p, head_dim, nw, 8), "ot_attn_fwd(slice): schedule");
@@ -1209,7 +1234,7 @@ size_t attn_slice_bwd_min_ws(int B, int H, int I, int K, int head_dim) {
 
 int attn_slice_bwd(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse, int B, int H,
                    int I, int K, int head_dim, float* dqkv, float* ws, size_t ws_bytes, hipStream_t stream,
-                   float* amax) {
+                   float* amax, float* rowmax) {
   using namespace slice;
   using KF = void (*)(SliceArgs);
   static const KF k32 = attn_bwd_slice_kernel<32, BWD_WAVES32, BWD_PLANES>,
@@ -1227,6 +1252,7 @@ int attn_slice_bwd(const float* qkv, int64_t ld, const float* out, const float* 
   SliceArgs p{qkv, ld, H * head_dim, out, dout, lse, nullptr, nullptr, dqkv, B, H, I, K,
               1.f / sqrtf((float)head_dim), nullptr};
   p.amax = amax;
+  p.rowmax = rowmax;
   const size_t per_wg = (size_t)1024 * bwd_pairs(I, K);
   const bool wsok = ws && ws_bytes >= per_wg;
   const bool g2 = form == BWD_MID || form == BWD_LONG || (form == BWD_64 && bwd_g2(64) && wsok);

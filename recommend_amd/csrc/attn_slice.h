@@ -24,18 +24,20 @@ struct SliceArgs {
   int16_t bbase[SLICE_TABN];                  // backward: dS-store block index of (qf[kb], kb)
   float* dsws; int ds_floats;                 // backward, two workgroups per CU: per-workgroup dS scratch
   float* amax;                                // optional: max |output| folded in atomically (fp16-pair bounds)
+  float* rowmax;                              // optional: per-row max |output| parts: forward [B*K][H] (O, per
+                                              // head), backward [B*I][3][H] (dQ / dK / dV, per head)
 };
 
 bool attn_slice_fwd_supported(int I, int K, int head_dim);
 bool attn_slice_bwd_supported(int I, int K, int head_dim, bool selected);
 // amax (optional): max |output| folded in atomically (the caller zeroes it; fp16-pair weight-gradient bounds)
 int attn_slice_fwd(const float* qkv, int64_t ld, int B, int H, int I, int K, const int32_t* qpos, int head_dim,
-                   float* out, float* lse, hipStream_t stream, float* amax = nullptr);
+                   float* out, float* lse, hipStream_t stream, float* amax = nullptr, float* rowmax = nullptr);
 // ws / ws_bytes: scratch for the two-workgroups-per-CU backward (attn_slice_bwd_ws_bytes for the full grid; less
 // shrinks its grid; below one workgroup's share the one-workgroup-per-CU kernel runs)
 int attn_slice_bwd(const float* qkv, int64_t ld, const float* out, const float* dout, const float* lse, int B, int H,
                    int I, int K, int head_dim, float* dqkv, float* ws, size_t ws_bytes, hipStream_t stream,
-                   float* amax = nullptr);
+                   float* amax = nullptr, float* rowmax = nullptr);
 size_t attn_slice_bwd_ws_bytes(int B, int H, int I, int K, int head_dim);
 // the workspace below which the backward's long forms are not taken (they keep dS only there; 0 otherwise)
 size_t attn_slice_bwd_min_ws(int B, int H, int I, int K, int head_dim);

@@ -175,32 +175,42 @@ __global__ void rows_colsum_kernel(const float* __restrict__ src, int64_t ld, co
 // and W2 weight-gradient D operand, which round it so anyway)
 constexpr int DROPOUT_PASSES = 4;
 template <typename OUT>
-__global__ void dropout_apply_kernel(const float* __restrict__ src, int64_t lds, OUT* dst, int64_t ldd,
+__global__ void dropout_apply_kernel(const float* __restrict__ src, int64_t lds, OUT* __restrict__ dst, int64_t ldd,
                                      int64_t rows, int d, uint32_t seed, uint32_t site, uint32_t thr, float scale,
                                      int tail_K, int tail_I, const int32_t* tail_pos, float* amax, float* rowmax,
                                      int rowmax_n) {
-  // PASSES float4s per thread, grid-strided (each pass coalesced): the magnitude outputs cost one wave reduction per
-  // PASSES float4s instead of per one
-  const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
+  // DROPOUT_PASSES float4s per thread, grid-strided (each pass coalesced; every load issued before the first
+  // store): the magnitude outputs cost one wave reduction per DROPOUT_PASSES float4s instead of per one
+  const int64_t nthreads = (int64_t)gridDim.x * blockDim.x, n4 = rows * d;
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  f32x4 v[DROPOUT_PASSES];
+  int64_t rr[DROPOUT_PASSES];
+  int cc[DROPOUT_PASSES];
+#pragma unroll
+  for (int ps = 0; ps < DROPOUT_PASSES; ++ps) {
+    const int64_t i4 = (t0 + ps * nthreads) * 4;
+    const bool in = i4 < n4;
+    rr[ps] = in ? (n4 < (1ll << 31) ? (int64_t)((uint32_t)i4 / (uint32_t)d) : i4 / d) : -1;   // (32-bit divide)
+    cc[ps] = (int)(i4 - (in ? rr[ps] : 0) * d);
+    v[ps] = in ? *reinterpret_cast<const f32x4*>(src + rr[ps] * lds + cc[ps]) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   float am = 0.f;
 #pragma unroll
   for (int ps = 0; ps < DROPOUT_PASSES; ++ps) {
-    const int64_t i4 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x + ps * nthreads) * 4;
-    const bool in = i4 < rows * d;
-    const int64_t r = in ? i4 / d : 0;
-    const int c = (int)(i4 % d);
+    const int64_t r = rr[ps];
+    const int c = cc[ps];
     float pm = 0.f;
-    if (in) {
+    if (r >= 0) {
       const int64_t tok = tail_token(r, tail_K, tail_I, tail_pos);
-      f32x4 v = *reinterpret_cast<const f32x4*>(src + r * lds + c);
-      uint32_t base = (uint32_t)(tok * d + c);
-      v.x = drop_keep(seed, site, base + 0, thr) ? v.x * scale : 0.f;
-      v.y = drop_keep(seed, site, base + 1, thr) ? v.y * scale : 0.f;
-      v.z = drop_keep(seed, site, base + 2, thr) ? v.z * scale : 0.f;
-      v.w = drop_keep(seed, site, base + 3, thr) ? v.w * scale : 0.f;
-      if constexpr (sizeof(OUT) == 2) *reinterpret_cast<u32x2*>(dst + r * ldd + c) = bf16_rne4(v);
-      else *reinterpret_cast<f32x4*>(dst + r * ldd + c) = v;
-      pm = amax4(0.f, v);
+      const uint32_t base = (uint32_t)(tok * d + c);
+      f32x4 w = v[ps];
+      w.x = drop_keep(seed, site, base + 0, thr) ? w.x * scale : 0.f;
+      w.y = drop_keep(seed, site, base + 1, thr) ? w.y * scale : 0.f;
+      w.z = drop_keep(seed, site, base + 2, thr) ? w.z * scale : 0.f;
+      w.w = drop_keep(seed, site, base + 3, thr) ? w.w * scale : 0.f;
+      if constexpr (sizeof(OUT) == 2) *reinterpret_cast<u32x2*>(dst + r * ldd + c) = bf16_rne4(w);
+      else *reinterpret_cast<f32x4*>(dst + r * ldd + c) = w;
+      pm = amax4(0.f, w);
     }
     am = fmaxf(am, pm);
     // each row's max |v| per 256-column part (a row is d / 4 consecutive lanes: groups of min(d / 4, 64) lanes; the
@@ -208,7 +218,7 @@ __global__ void dropout_apply_kernel(const float* __restrict__ src, int64_t lds,
     if (rowmax) {
       const int gl = d / 4 < 64 ? d / 4 : 64;
       for (int o = gl / 2; o > 0; o >>= 1) pm = fmaxf(pm, __shfl_xor(pm, o, 64));
-      if (in && (c % 256) == 0) rowmax[r * rowmax_n + c / 256] = pm;
+      if (r >= 0 && (c % 256) == 0) rowmax[r * rowmax_n + c / 256] = pm;
     }
   }
   if (amax) amax_flush(amax, am);

@@ -32,16 +32,18 @@ class Probe:
         ev.record()
         return ev
 
-    def end(self, family: str, flops: float, ev0, label: str = '', nbytes: float = 0.0) -> None:
+    def end(self, family: str, flops: float, ev0, label: str = '', nbytes: float = 0.0, terms: int = 0) -> None:
+        """``terms``: 16-bit MFMA products per f32 product the launch issues (6 split-bf16, 3 fp16 pair, 1 bf16; 0 =
+        the family's default peak) — its launch is floored against that arithmetic's ceiling."""
         ev1 = torch.cuda.Event(enable_timing=True)
         ev1.record()
-        self.recs.append((family, flops, ev0, ev1, label, nbytes))
+        self.recs.append((family, flops, ev0, ev1, label, nbytes, terms))
 
     def by_label(self, steps: int):
         """Per-launch-shape breakdown: {label: (launches/step, avg us, TF/s)} (tools/gemm_shapes.py)."""
         torch.cuda.synchronize()
         agg = {}
-        for (f, fl, a, b, lab, _) in self.recs:
+        for (f, fl, a, b, lab, _, _t) in self.recs:
             d = agg.setdefault(f'{f} {lab}', [0, 0.0, 0.0])
             d[0] += 1
             d[1] += a.elapsed_time(b)
@@ -49,22 +51,27 @@ class Probe:
         return {k: (n / steps, 1e3 * ms / n, fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0)
                 for k, (n, ms, fl) in agg.items()}
 
-    def report(self, steps: int, mfma_peak_tflops: float = 0.0, hbm_peak_gbs: float = 0.0):
+    def report(self, steps: int, mfma_peak_tflops: float = 0.0, hbm_peak_gbs: float = 0.0, terms_peak=None):
         """Per family: time, launches, algorithmic FLOPs and bytes per launch; with the peaks given, also
-        the family's roofline floor sum_i max(flops_i / mfma peak, bytes_i / HBM peak) over its launches
-        (each launch bound by whichever roof it meets first) and the MFMA / HBM parts of it."""
+        the family's roofline floor sum_i max(flops_i / mfma peak_i, bytes_i / HBM peak) over its launches
+        (each launch bound by whichever roof it meets first) and the MFMA / HBM parts of it.  ``terms_peak(t)``: the
+        MFMA ceiling (f32 TF/s) of a launch issuing t products per f32 product (its recorded ``terms``); the family's
+        ``mfma_peak_eff`` = its flops over the sum of flops_i / peak_i (the ceiling of the arithmetic it issued)."""
         if torch.cuda.is_available():
             torch.cuda.synchronize()
         fam = {}
-        for (f, fl, a, b, _, nb) in self.recs:
+        for (f, fl, a, b, _, nb, terms) in self.recs:
             d = fam.setdefault(f, {'ms': 0.0, 'flops': 0.0, 'bytes': 0.0, 'n': 0, 'floor': 0.0, 'fl_mfma': 0.0,
-                                   'fl_hbm': 0.0})
+                                   'fl_hbm': 0.0, 'mfma_ms': 0.0, 'pair': 0})
             d['ms'] += a.elapsed_time(b)
             d['flops'] += fl
             d['bytes'] += nb
             d['n'] += 1
+            d['pair'] += terms == 3
             if mfma_peak_tflops > 0 and hbm_peak_gbs > 0:
-                tm, th = fl / (mfma_peak_tflops * 1e9), nb / (hbm_peak_gbs * 1e6)     # ms
+                pk = terms_peak(terms) if (terms_peak is not None and terms) else mfma_peak_tflops
+                tm, th = fl / (pk * 1e9), nb / (hbm_peak_gbs * 1e6)     # ms
+                d['mfma_ms'] += tm
                 d['floor'] += max(tm, th)
                 d['fl_mfma' if tm >= th else 'fl_hbm'] += max(tm, th)
         out = {}
@@ -75,11 +82,24 @@ class Probe:
                       'tflops': d['flops'] / (d['ms'] * 1e-3) / 1e12 if d['ms'] > 0 else 0.0,
                       'gbs': d['bytes'] / (d['ms'] * 1e-3) / 1e9 if d['ms'] > 0 else 0.0,
                       'floor_ms_per_step': d['floor'] / steps, 'floor_mfma_ms_per_step': d['fl_mfma'] / steps,
-                      'floor_hbm_ms_per_step': d['fl_hbm'] / steps}
+                      'floor_hbm_ms_per_step': d['fl_hbm'] / steps,
+                      'mfma_peak_eff': d['flops'] / (d['mfma_ms'] * 1e9) if d['mfma_ms'] > 0 else 0.0,
+                      'pair_launches_per_step': d['pair'] / steps}
         return {'families': out}
 
 
 _probe = None
+
+
+def _terms(bimg, a_xform: int, a_rowmax, N: int) -> int:
+    """MFMA products per f32 product a forward / dgrad launch issues (the probe's ceiling): bf16 mode 1, f32 mode 0
+    (native), split mode 3 on the plane GEMM's fp16 pair (RMSNorm prologue, or A row maxima given), else 6."""
+    mm = matmul_mode()
+    if mm != 'split':
+        return 1 if mm == 'bf16' else 0
+    pair = bimg is not None and N % 128 == 0 and (
+        a_xform == _lib.OT_AX_RMSNORM or (a_rowmax is not None and a_xform in (_lib.OT_AX_NONE, _lib.OT_AX_GELU)))
+    return 3 if pair else 6
 
 
 def gemm_bytes(M: int, K: int, N: int, a_xform: int, epi: int) -> float:
@@ -223,7 +243,7 @@ def gemm(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish, w_g
     if ev is not None:
         M = m_rows or ntiles * 128
         _probe.end('mixed_gemm', 2.0 * M * K * N, ev, f'gemm mode{mode} ax{a_xform} epi{epi} M{M} K{K} N{N}',
-                   gemm_bytes(M, K, N, a_xform, epi))
+                   gemm_bytes(M, K, N, a_xform, epi), _terms(bimg, a_xform, None, N))
 
 
 def gemm_rms(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish, w_gstride: int, ldw: int,
@@ -274,7 +294,7 @@ def gemm_rms(mode: int, A: Ptrish, lda: int, K: int, in_rows: Ptrish, W: Ptrish,
         _probe.end('mixed_gemm', 2.0 * M * K * N, ev, f'gemm_rms mode{mode} ax{a_xform} epi{epi} M{M} K{K} N{N}',
                    gemm_bytes(M, K, N, a_xform, epi) + 4.0 * M * N * extra + 2.0 * M * N * (gelu_out is not None)
                    + 2.0 * M * K * (xn_out is not None)
-                   + 4.0 * M * ((rstd_out is not None) + (nrstd is not None)))
+                   + 4.0 * M * ((rstd_out is not None) + (nrstd is not None)), _terms(bimg, a_xform, a_rowmax, N))
 
 
 def wgrad(A: Ptrish, lda: int, a_rows: Ptrish, D: Ptrish, ldd: int, d_rows: Ptrish, K: int, N: int, rmap_dev,
@@ -297,10 +317,16 @@ def wgrad(A: Ptrish, lda: int, a_rows: Ptrish, D: Ptrish, ldd: int, d_rows: Ptri
          dw_gstride, ptr(db), db_gstride, int(accumulate), ptr(ws), ws.numel(), ptr(a_bound), ptr(d_bound), _prec(),
          stream())
     if ev is not None:
+        ax = a_xform & ~_lib.OT_WG_D_BF16
+        wterms = {'bf16': 1, 'f32': 0}.get(matmul_mode(), 3 if (
+            d_bound is not None and not (a_xform & _lib.OT_WG_D_BF16)
+            and (ax == _lib.OT_AX_RMSNORM or (a_bound is not None and ax in (_lib.OT_AX_NONE, _lib.OT_AX_GELU))))
+            else 6)
         _probe.end('mixed_gemm', 2.0 * m_rows * K * N, ev, f'wgrad ax{a_xform} M{m_rows} K{K} N{N} ch{nchunks}',
                    (2.0 if (a_xform & ~_lib.OT_WG_D_BF16) == _lib.OT_AX_BF16 else 4.0) * m_rows * K
                    + (2.0 if a_xform & _lib.OT_WG_D_BF16 else 4.0) * m_rows * N
-                   + 4.0 * m_rows * ((a_xform & ~_lib.OT_WG_D_BF16) == _lib.OT_AX_RMSNORM) + 4.0 * ngroups * K * N)
+                   + 4.0 * m_rows * ((a_xform & ~_lib.OT_WG_D_BF16) == _lib.OT_AX_RMSNORM) + 4.0 * ngroups * K * N,
+                   wterms)
 
 
 def transpose_banks(src, dst, banks_dev, nbanks, total_tiles) -> None:
@@ -318,7 +344,7 @@ def split_images(base, desc_dev, ndesc, total_units, img) -> None:
 def attn_fwd(qkv: torch.Tensor, ld: int, B: int, H: int, I: int, K: int, hd: int, out: torch.Tensor,
              lse: torch.Tensor, qpos: Optional[torch.Tensor] = None, fp8: bool = False,
              dequant: bool = False, fp8_terms: int = 1, deq16: Optional[torch.Tensor] = None,
-             amax: Optional[torch.Tensor] = None) -> None:
+             amax: Optional[torch.Tensor] = None, rowmax: Optional[torch.Tensor] = None) -> None:
     """ot_attn_fwd, or with ``fp8`` (head_dim 64/128) ot_attn_fwd_fp8_ex: QK^T and PV on block-scaled fp8
     MFMA, operands as one e4m3 term or two (``fp8_terms`` 2: hi + lo, OT_FP8_TWO_TERM); ``dequant``
     (training) also overwrites qkv's operands with their dequantised fp8 values (OT_FP8_DEQUANT) for the
@@ -337,9 +363,9 @@ def attn_fwd(qkv: torch.Tensor, ld: int, B: int, H: int, I: int, K: int, hd: int
         call('ot_attn_fwd_fp8_ex', ptr(qkv), ld, B, H, I, K, ptr(qpos), hd, ptr(out), ptr(lse), ptr(ws),
              ws.numel(), (_lib.OT_FP8_DEQUANT if dequant else 0) | (_lib.OT_FP8_TWO_TERM if fp8_terms == 2 else 0),
              stream())
-    elif amax is not None:      # + max |O| folded into amax (attn_amax_supported shapes only)
-        call('ot_attn_fwd_amax', ptr(qkv), ld, B, H, I, K, ptr(qpos), hd, ptr(out), ptr(lse), ptr(amax), _prec(),
-             stream())
+    elif amax is not None or rowmax is not None:   # + max |O| (amax) / per (row, head) (rowmax [B*K][H])
+        call('ot_attn_fwd_amax', ptr(qkv), ld, B, H, I, K, ptr(qpos), hd, ptr(out), ptr(lse), ptr(amax), ptr(rowmax),
+             _prec(), stream())
     else:
         call('ot_attn_fwd', ptr(qkv), ld, B, H, I, K, ptr(qpos), hd, ptr(out), ptr(lse), _prec(), stream())
     if ev is not None:
@@ -364,7 +390,7 @@ def attn_amax_supported(I, K, hd, qpos=None, backward: bool = False) -> bool:
 
 
 def attn_bwd(qkv, ld, out, dout, lse, B, H, I, K, hd, dqkv, qpos=None, dq_part_bf16: bool = False,
-             amax=None) -> None:
+             amax=None, rowmax=None) -> None:
     """dqkv float32, or int16 (bf16 bits: OT_ATTN_DQKV_BF16, see attn_bwd_bf16_supported); qkv likewise
     (int16: OT_ATTN_QKV_BF16, the fp8 forward's bf16 dequantised operands)."""
     flags = ((_lib.OT_ATTN_DQKV_BF16 if dqkv.dtype == torch.int16 else 0)
@@ -374,9 +400,9 @@ def attn_bwd(qkv, ld, out, dout, lse, B, H, I, K, hd, dqkv, qpos=None, dq_part_b
     ws = workspace(size('ot_attn_bwd_flags_workspace_size', B, H, I, K, hd, int(qpos is not None), flags, _prec()),
                    qkv.device)
     ev = _probe.begin() if _probe is not None else None
-    if amax is not None:        # + max |dQKV| folded into amax (slice backward shapes only)
+    if amax is not None or rowmax is not None:   # + max |dQKV| (amax) / per (row, part, head) (rowmax [B*I][3][H])
         call('ot_attn_bwd_amax', ptr(qkv), ld, ptr(out), ptr(dout), ptr(lse), B, H, I, K, ptr(qpos), hd, ptr(dqkv),
-             ptr(ws), ws.numel(), ptr(amax), _prec(), stream())
+             ptr(ws), ws.numel(), ptr(amax), ptr(rowmax), _prec(), stream())
     else:
         call('ot_attn_bwd_flags', ptr(qkv), ld, ptr(out), ptr(dout), ptr(lse), B, H, I, K, ptr(qpos), hd,
              ptr(dqkv), flags, ptr(ws), ws.numel(), _prec(), stream())

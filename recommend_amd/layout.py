@@ -115,8 +115,10 @@ class FlatLayout:
                            and K % TILE == 0 and N % 16 == 0)
                 # pair_dgrad: the FFN2 / FFN1 / Wo dgrad images too (their A operands' row maxima come from the
                 # producers: ot_dropout_apply_ex / rowabs_out, or ot_rows_absmax)
-                pair_dg = (pair_dgrad and orient == 'dgrad' and name.startswith('blk.')
-                           and name.endswith(('.w1', '.w2', '.wo')))
+                # (and the Wo forward image: its A, the attention output, gets row maxima from the attention forward)
+                pair_dg = pair_dgrad and name.startswith('blk.') and (
+                    (orient == 'dgrad' and name.endswith(('.w1', '.w2', '.wo', '.wqkv')))
+                    or (orient == 'fwd' and name.endswith('.wo')))
                 kscale = gamma if (orient == 'fwd' and gamma is not None) else (-2 if (pair_w2 or pair_dg) else -1)
                 irecs.append((o, sn, sk, K * N, kscale, ioff, units, G, Nb, Kb))
                 self.images[(name, orient)] = (ioff, G, Nb, Kb)

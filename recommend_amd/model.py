@@ -235,8 +235,16 @@ def _block_forward(m, l, x, I, Kq, seed, training, rstd_in=None, select=False, n
     qkv16 = (torch.empty(B * I, 3 * d, dtype=torch.int16, device=dev)
              if m.attn_fp8 and training and K.attn_bwd_bf16_supported(I, Kq, hd, qp_f) else None)
     am_o = (m.amax_slot(l, 0) if training and not m.attn_fp8 and K.attn_amax_supported(I, Kq, hd, qp_f) else None)
+    # the Wo forward on the fp16 pair (pair-form Wo image): O's row maxima, per head, from the slice forward (else
+    # the row-absmax pass)
+    pwo_f = m.gemm_pair(f'blk.{l}.wo', 'fwd')
+    o_fast = pwo_f and not m.attn_fp8 and K.attn_amax_supported(I, Kq, hd, qp_f)
+    rm_o = torch.empty(B * Kq, H, device=dev) if o_fast else None
     K.attn_fwd(qkv, 3 * d, B, H, I, Kq, hd, o, lse, qpos=qp_f, fp8=m.attn_fp8,
-               dequant=m.attn_fp8 and training, fp8_terms=m.fp8_terms, deq16=qkv16, amax=am_o)
+               dequant=m.attn_fp8 and training, fp8_terms=m.fp8_terms, deq16=qkv16, amax=am_o, rowmax=rm_o)
+    if pwo_f and rm_o is None:
+        K.rows_absmax(o, d, B * Kq, d, rm_o := torch.empty(B * Kq, (d + 255) // 256, device=dev))
+    pa_o = dict(a_rowmax=rm_o, a_rowmax_n=rm_o.shape[1]) if pwo_f else {}
     if qkv16 is not None:
         qkv = qkv16
     # x1 = x[tail] + drop(o @ Wo)      (model.py:117, 193)
@@ -250,11 +258,11 @@ def _block_forward(m, l, x, I, Kq, seed, training, rstd_in=None, select=False, n
         K.gemm_rms(OT_GEMM_NT, o, d, d, mt['rows'][1], wo, 0, d, d, mt['tile_group'], nt, x1, d, mt['rows'][1],
                    epi=OT_EPI_RESIDUAL | dflag | OT_EPI_ROW_RSTD, res=x, ldres=d, res_tok=1, seed=seed,
                    site=2 * l, drop=rate, tail=tail, m_rows=maps['tail'].nrows, rstd_out=rstd2, eps=RMS_EPS,
-                   bimg=m.bimg(f'blk.{l}.wo'), c16_out=x1_16, ldc16=d)
+                   bimg=m.bimg(f'blk.{l}.wo'), c16_out=x1_16, ldc16=d, device=dev, **pa_o)
     else:
-        K.gemm(OT_GEMM_NT, o, d, d, mt['rows'][1], wo, 0, d, d, mt['tile_group'], nt, x1, d, mt['rows'][1],
-               epi=OT_EPI_RESIDUAL | dflag, res=x, ldres=d, res_tok=1, seed=seed, site=2 * l, drop=rate,
-               tail=tail, m_rows=maps['tail'].nrows, bimg=m.bimg(f'blk.{l}.wo'))
+        K.gemm_rms(OT_GEMM_NT, o, d, d, mt['rows'][1], wo, 0, d, d, mt['tile_group'], nt, x1, d, mt['rows'][1],
+                   epi=OT_EPI_RESIDUAL | dflag, res=x, ldres=d, res_tok=1, seed=seed, site=2 * l, drop=rate,
+                   tail=tail, m_rows=maps['tail'].nrows, bimg=m.bimg(f'blk.{l}.wo'), device=dev, **pa_o)
         K.rmsnorm_fwd(x1, d, B * Kq, d, rstd2, eps=RMS_EPS)
     # u = norm2(x1) @ W1[g] + b1[g]  (pre-activation; GELU applied by its consumers)
     # bf16 mode: the FFN1 epilogue also stores h = gelu(u) rounded to bf16 — exactly the operand the bf16
@@ -512,9 +520,17 @@ class _Block(torch.autograd.Function):
         dqkv = torch.empty(B * I, 3 * d, device=dev, dtype=torch.int16 if dq_bf else torch.float32)
         if Kq < I:
             dqkv[:, :d].zero_()
-        b_dq = am(5) if (am(5) is not None and not dq_bf and K.attn_amax_supported(I, Kq, hd, qp, backward=True)) \
-            else None
-        K.attn_bwd(qkv, 3 * d, o, do, lse, B, H, I, Kq, hd, dqkv, qpos=qp, dq_part_bf16=True, amax=b_dq)
+        bwd_b = not dq_bf and K.attn_amax_supported(I, Kq, hd, qp, backward=True)
+        b_dq = am(5) if (am(5) is not None and bwd_b) else None
+        # the QKV dgrad on the fp16 pair: dQKV's row maxima [row][q / k / v][head] from the attention backward (the
+        # dQ part of rows without a query stays 0), else the row-absmax pass
+        pqkv = m.dgrad_pair(f'blk.{l}.wqkv')
+        rm_dq = torch.zeros(B * I, 3 * H, device=dev) if pqkv and bwd_b else None
+        K.attn_bwd(qkv, 3 * d, o, do, lse, B, H, I, Kq, hd, dqkv, qpos=qp, dq_part_bf16=True, amax=b_dq,
+                   rowmax=rm_dq)
+        if pqkv and rm_dq is None:
+            K.rows_absmax(dqkv, 3 * d, B * I, 3 * d, rm_dq := torch.empty(B * I, (3 * d + 255) // 256, device=dev))
+        pa_q = dict(a_rowmax=rm_dq, a_rowmax_n=rm_dq.shape[1]) if pqkv else {}
         an1 = xn1 is not None and dq_bf
         with m.side(xn1 if an1 else x, dqkv, rstd1):
             K.wgrad(xn1 if an1 else x, d, ma['rows'][0], dqkv, 3 * d, ma['rows'][0], d, 3 * d, ma, nca, G,
@@ -530,12 +546,12 @@ class _Block(torch.autograd.Function):
                        m_rows=maps['all'].nrows, nx=x, ldnx=d, ngamma=m.p(f'blk.{l}.norm1'), nrstd=rstd1,
                        dres=dx1, lddres=d, dres_tail=(Kq, I, inv) if Kq < I else (0, 0),
                        dgamma=m.g(f'blk.{l}.norm1'), accumulate_dgamma=acc, device=dev,
-                       bimg=m.bimg(f'blk.{l}.wqkv', 'dgrad'))
+                       bimg=m.bimg(f'blk.{l}.wqkv', 'dgrad'), **pa_q)
         else:
             dxn1 = torch.empty(B * I, d, device=dev)
-            K.gemm(OT_GEMM_NT, dqkv, 3 * d, 3 * d, ma['rows'][0], m.p(f'blk.{l}.wqkv'), 3 * d * d, 3 * d, d,
-                   ma['tile_group'], na, dxn1, d, ma['rows'][0], m_rows=maps['all'].nrows, a_xform=ax_dq,
-                   bimg=m.bimg(f'blk.{l}.wqkv', 'dgrad'))
+            K.gemm_rms(OT_GEMM_NT, dqkv, 3 * d, 3 * d, ma['rows'][0], m.p(f'blk.{l}.wqkv'), 3 * d * d, 3 * d, d,
+                       ma['tile_group'], na, dxn1, d, ma['rows'][0], epi=0, m_rows=maps['all'].nrows, a_xform=ax_dq,
+                       bimg=m.bimg(f'blk.{l}.wqkv', 'dgrad'), device=dev, **pa_q)
             K.rmsnorm_bwd(dxn1, d, x, d, m.p(f'blk.{l}.norm1'), rstd1, dx, d, B * I, d, dres=dx1, lddres=d,
                           dres_tail=(Kq, I, inv) if Kq < I else (0, 0), dgamma=m.g(f'blk.{l}.norm1'), accumulate=acc,
                           device=dev)
@@ -807,6 +823,7 @@ class OneTransModel(nn.Module):
         # row-sharded tables (data-parallel runs): 'emb.seq_item' lives partitioned over the ranks
         self.sharded: Dict[str, 'ShardedTable'] = {}
         self._pending_route = None                    # route_ahead(): the next lookup's routed ids
+        self.last_table_ids: Dict[str, torch.Tensor] = {}   # the forward's ids per replicated table (DP mask)
         shard_seq = self._shard_seq_table()
         params = init if init is not None else init_params(cfg, self.f_ns, seed=seed, with_tables=False)
         if shard_seq:
@@ -861,11 +878,16 @@ class OneTransModel(nn.Module):
             return True
         return all(self.bimg(n, o) is not None for (n, o) in images)
 
+    def gemm_pair(self, name: str, orient: str) -> bool:
+        """Is ``name``'s ``orient`` image one of the scaled-fp16-pair forms that need the A rows' maxima (a_rowmax: the
+        dgrad images and the Wo forward image under ONETRANS_PAIR_DGRAD, split mode)?"""
+        return (K.matmul_mode() == 'split' and self.pair_dgrad and (name, orient) in self.layout.pair_images
+                and self.bimg(name, orient) is not None and not (orient == 'fwd' and not name.endswith('.wo')))
+
     def dgrad_pair(self, name: str) -> bool:
         """Is ``name``'s dgrad image in the scaled-fp16-pair form (split mode, ONETRANS_PAIR_DGRAD), so its dgrad GEMM
         must get its A rows' maxima (a_rowmax)?"""
-        return (K.matmul_mode() == 'split' and (name, 'dgrad') in self.layout.pair_images
-                and self.bimg(name, 'dgrad') is not None)
+        return self.gemm_pair(name, 'dgrad')
 
     def u_bound_ok(self, l: int) -> bool:
         """Did block l's FFN1 forward report |U| (amax slot 1)?  It does on the pair-form W2 path (the plane GEMM with
@@ -1064,6 +1086,8 @@ class OneTransModel(nn.Module):
                 for (i, n, L), t, off in zip(present, ids, plan['seq_seg_off']):
                     K.seq_rows(t, L, B, L, cfg.seq_item_vocab, (plan['seq_in'], off))
                 plan['seq_ids'] = torch.cat([t.reshape(-1) for t in ids])
+                # (a replicated table's ids: the optimizer builds the DP exchange's touched-row mask from them)
+                self.last_table_ids = {'emb.seq_item': plan['seq_ids']}
                 plan['seq_A'] = self.tables['emb.seq_item']
             else:
                 buf = plan['seq_buf']

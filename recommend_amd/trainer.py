@@ -90,6 +90,10 @@ class OneTransOptimizer:
         # max all-reduce) when it is under 60% of a >= 128 MB table ('auto'), always ('1') or never ('0')
         self.compact_exchange = os.environ.get('ONETRANS_COMPACT_EXCHANGE', 'auto')
         self._dense_grad: Dict[str, torch.Tensor] = {}
+        self._mask_buf: Dict[str, torch.Tensor] = {}
+        self._masks: Dict = {}
+        self._mask_stream = None
+        self._mask_count: Dict[str, torch.Tensor] = {}
         # diagnostics (bench.py, N > 1): when a list, every step appends HIP-event pairs bracketing the
         # main stream's waits for the gradient exchange, i.e. the exchange time NOT hidden by backward
         self.exchange_events = None
@@ -150,9 +154,59 @@ class OneTransOptimizer:
         if m._side is not None:
             self._comm.wait_stream(m._side)              # this block's wgrads run on the side stream
         with torch.cuda.stream(self._comm):
-            self._works.append(otdist.allreduce_sum_async(m.flat.grad[lo:hi]))
+            for s0 in range(lo, hi, otdist.BUCKET_ELEMS):          # 32 MiB buckets (one for a C2 block)
+                self._works.append(otdist.allreduce_sum_async(m.flat.grad[s0:min(hi, s0 + otdist.BUCKET_ELEMS)]))
 
-    def _start_table_exchange(self, g: torch.Tensor, keys: torch.Tensor):
+    def _compact(self, table: torch.Tensor) -> bool:
+        """Exchange this replicated table's gradient as the union of touched rows (ONETRANS_COMPACT_EXCHANGE: '1'
+        always, 'auto' for tables of >= 128 MB — each compaction costs a mask all-reduce and a host sync)?"""
+        return self.compact_exchange == '1' or (self.compact_exchange == 'auto' and table.numel() * 4 >= 2 ** 27)
+
+    def prepare_table_exchange(self) -> None:
+        """Between the forward and the backward (OneTransTrainer.train_step): for each replicated table exchanged
+        as the union of touched rows, build this rank's touched-row mask from the forward's ids, MAX-all-reduce it
+        and count the union, all on a stream of its own that depends on the forward only; the count goes to pinned
+        host memory.  step() then waits for that stream's event — long complete by the time the host has issued the
+        backward — and takes the union's rows with ``torch.nonzero_static`` (no device sync), so the optimizer
+        step has no host gap (the mask used to be built, reduced and ``torch.nonzero``-ed in step(), a sync on the
+        whole queued backward)."""
+        m = self.model
+        self._masks = {}
+        if otdist.world() == 1:
+            return
+        import torch.distributed as dist
+        for name, ids in getattr(m, 'last_table_ids', {}).items():
+            table = m.tables.get(name)
+            if (ids is None or table is None or name in m.sharded or table.numel() * 4 > self.dense_exchange_bytes
+                    or not self._compact(table)):
+                continue
+            rows = table.shape[0]
+            mask = self._mask_buf.get(name)
+            if mask is None:
+                mask = self._mask_buf[name] = torch.zeros(rows, dtype=torch.uint8, device=table.device)
+            if self._mask_stream is None:
+                self._mask_stream = torch.cuda.Stream(device=table.device)
+            cnt = self._mask_count.get(name)
+            if cnt is None:
+                cnt = self._mask_count[name] = torch.zeros(1, dtype=torch.int64, pin_memory=True)
+            ms = self._mask_stream
+            ms.wait_stream(torch.cuda.current_stream(table.device))      # the forward staged the ids
+            with torch.cuda.stream(ms):
+                mask.zero_()
+                k = ids.reshape(-1)
+                mask[k[(k >= 0) & (k < rows)]] = 1
+                work = dist.all_reduce(mask, op=dist.ReduceOp.MAX, async_op=True)
+                if dist.get_backend() == 'gloo':
+                    # (the CPU rehearsal: gloo's wait blocks the host, so it and the count wait for step())
+                    self._masks[name] = (mask, work, None)
+                    continue
+                work.wait()                              # RCCL: a stream dependency, no host wait
+                cnt.copy_(torch.count_nonzero(mask).reshape(1), non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(ms)
+            self._masks[name] = (mask, None, ev)
+
+    def _start_table_exchange(self, g: torch.Tensor, keys: torch.Tensor, name: str = None):
         """Start the sum over ranks of a replicated table's dense gradient ``g``.  C2's 1M-row item table
         is 256 MB, but a rank's batch touches ~1/6 of its rows: the ranks first agree on the union of
         touched rows (uint8 mask, max all-reduce, 1 B per row) and all-reduce only those rows
@@ -160,13 +214,24 @@ class OneTransOptimizer:
         is the dense all-reduce's.  Returns (g, work, union rows or None, compact rows or None)."""
         import torch.distributed as dist
         rows = g.shape[0]
-        # (auto: tables of >= 128 MB only — each compaction costs a mask all-reduce and a host sync)
-        if self.compact_exchange == '1' or (self.compact_exchange == 'auto' and g.numel() * 4 >= 2 ** 27):
-            mask = torch.zeros(rows, dtype=torch.uint8, device=g.device)
-            k = keys.reshape(-1)
-            mask[k[(k >= 0) & (k < rows)]] = 1
-            dist.all_reduce(mask, op=dist.ReduceOp.MAX)
-            idx = torch.nonzero(mask).reshape(-1)        # host sync: the union's size
+        if self._compact(g):
+            pending = self._masks.pop(name, None) if name is not None else None
+            if pending is not None:                      # built from the forward's ids, reduced during the backward
+                mask, work, ev = pending
+                if work is not None:                     # gloo: wait and count here
+                    work.wait()
+                    torch.cuda.current_stream(g.device).wait_stream(self._mask_stream)
+                    idx = torch.nonzero(mask).reshape(-1)
+                else:
+                    ev.synchronize()                     # (the mask stream's work, not the queued backward)
+                    torch.cuda.current_stream(g.device).wait_event(ev)
+                    idx = torch.nonzero_static(mask, size=int(self._mask_count[name].item())).reshape(-1)
+            else:
+                mask = torch.zeros(rows, dtype=torch.uint8, device=g.device)
+                k = keys.reshape(-1)
+                mask[k[(k >= 0) & (k < rows)]] = 1
+                dist.all_reduce(mask, op=dist.ReduceOp.MAX)
+                idx = torch.nonzero(mask).reshape(-1)    # host sync: the union's size
             if self.compact_exchange == '1' or idx.numel() < 0.6 * rows:
                 cg = g.index_select(0, idx)
                 return g, otdist.allreduce_sum_async(cg), idx, cg
@@ -190,7 +255,7 @@ class OneTransOptimizer:
                 else:
                     g.zero_()
                 K.sparse_grad_dense(E, rows, keys, grads, keys.numel(), g, device=table.device)
-                early[name] = self._start_table_exchange(g, keys)
+                early[name] = self._start_table_exchange(g, keys, name)
         if m.grad_ready is not None:
             for w in self._works:                        # the current stream waits for each exchange
                 w.wait()
@@ -259,6 +324,7 @@ class OneTransTrainer:
         if next_batch is not None and self.model.sharded:
             self.model.route_ahead(_seq_inputs(self.model, next_batch[1], dev))
         loss = keras_bce_loss(y, probs, self.config.tasks, label_rank(labels))
+        self.optimizer.prepare_table_exchange()
         self.optimizer.begin_backward()
         loss.backward()
         self.optimizer.step()

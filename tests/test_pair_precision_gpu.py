@@ -380,3 +380,36 @@ def test_pair_dgrad(dev, K_, N, case, epi):
         assert worst <= 0
         return
     check_ratio(f'dgrad {epi} K{K_} N{N} {case}', errs(Cp, ref), errs(Cf, ref), ref.abs().max().item())
+
+
+@pytest.mark.parametrize('B,H,I,Kq,hd', [(6, 4, 140, 140, 64), (6, 4, 140, 140, 32), (3, 4, 524, 262, 64),
+                                          (5, 4, 140, 1, 64), (5, 4, 140, 1, 32)])
+def test_attention_reports_bounds(dev, B, H, I, Kq, hd):
+    """The attention kernels' magnitude outputs (the fp16-pair consumers' bounds) equal the maxima of what they
+    stored: forward max |O| and per (row, head); backward max |dQKV| and per (row, q / k / v part, head)."""
+    torch.manual_seed(I + Kq + hd)
+    old = K.set_matmul_mode('split')
+    try:
+        d = H * hd
+        qkv = torch.randn(B * I, 3 * d, device=dev)
+        out = torch.empty(B * Kq, d, device=dev)
+        lse = torch.empty(B * H * Kq, device=dev)
+        fwd = K.attn_amax_supported(I, Kq, hd)
+        am = torch.zeros(1, device=dev)
+        rm = torch.full((B * Kq, H), -1.0, device=dev)
+        K.attn_fwd(qkv, 3 * d, B, H, I, Kq, hd, out, lse, amax=am if fwd else None, rowmax=rm if fwd else None)
+        if fwd:
+            torch.cuda.synchronize()
+            assert am.item() == out.abs().max().item()
+            assert torch.equal(rm, out.abs().reshape(B * Kq, H, hd).max(-1).values)
+        assert K.attn_amax_supported(I, Kq, hd, backward=True)
+        dout = torch.randn(B * Kq, d, device=dev)
+        dqkv = torch.zeros(B * I, 3 * d, device=dev)
+        am = torch.zeros(1, device=dev)
+        rm = torch.zeros(B * I, 3 * H, device=dev)
+        K.attn_bwd(qkv, 3 * d, out, dout, lse, B, H, I, Kq, hd, dqkv, amax=am, rowmax=rm)
+        torch.cuda.synchronize()
+        assert am.item() == dqkv.abs().max().item()
+        assert torch.equal(rm, dqkv.abs().reshape(B * I, 3 * H, hd).max(-1).values)
+    finally:
+        K.set_matmul_mode(old)

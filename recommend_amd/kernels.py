@@ -43,7 +43,8 @@ class Probe:
         """Per-launch-shape breakdown: {label: (launches/step, avg us, TF/s)} (tools/gemm_shapes.py)."""
         torch.cuda.synchronize()
         agg = {}
-        for (f, fl, a, b, lab, _, _t) in self.recs:
+        for rec in self.recs:
+            f, fl, a, b, lab = rec[:5]
             d = agg.setdefault(f'{f} {lab}', [0, 0.0, 0.0])
             d[0] += 1
             d[1] += a.elapsed_time(b)
@@ -60,7 +61,9 @@ class Probe:
         if torch.cuda.is_available():
             torch.cuda.synchronize()
         fam = {}
-        for (f, fl, a, b, _, nb, terms) in self.recs:
+        for rec in self.recs:
+            f, fl, a, b, _, nb = rec[:6]
+            terms = rec[6] if len(rec) > 6 else 0
             d = fam.setdefault(f, {'ms': 0.0, 'flops': 0.0, 'bytes': 0.0, 'n': 0, 'floor': 0.0, 'fl_mfma': 0.0,
                                    'fl_hbm': 0.0, 'mfma_ms': 0.0, 'pair': 0})
             d['ms'] += a.elapsed_time(b)

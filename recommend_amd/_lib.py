@@ -76,6 +76,8 @@ SIGNATURES = {
                                       P, I64, P, c_int, P, I64, c_int, P, I64, c_uint32, c_uint32, c_float, c_int,
                                       c_int, P, P, P, c_int, c_int, c_int, P]),
     'ot_split_image_elems': (c_size_t, [c_int, c_int, c_int]),
+    'ot_plane_wide': (c_int, [c_int]),
+    'ot_wgrad_wide': (c_int, [c_int]),
     'ot_split_images': (c_int, [P, P, c_int, I64, P, c_int, P]),
     'ot_attn_fwd': (c_int, [P, I64, c_int, c_int, c_int, c_int, P, c_int, P, P, c_int, P]),
     'ot_attn_fwd_fp8_workspace_size': (c_size_t, [c_int, c_int, c_int, c_int]),

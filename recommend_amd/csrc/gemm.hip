@@ -15,6 +15,7 @@
 // k = 16h + s at step s) so each lane reads 4 consecutive k with one ds_read_b128.
 #include <algorithm>
 #include <cstdlib>
+#include <atomic>
 #include <mutex>
 
 #include "common.h"
@@ -164,7 +165,10 @@ __device__ __forceinline__ bool wgrad_tile(int b, int per_chunk, int nchunks, in
 // chunk, so every global access is a 16-B piece of a 512-B row run and each row index is loaded once
 // per row instead of once per element.  Operand loads of a batch of rows are issued together.
 // LAYOUT 0: 2x2 waves, acc[2m + n] = rows 64 (wave >> 1) + 32 m, cols 64 (wave & 1) + 32 n;
-// LAYOUT 1: 4x1 waves, acc[nb] = rows 32 wave, cols 32 nb.  ROWSCALE: multiply row r by
+// LAYOUT 1: 4x1 waves, acc[nb] = rows 32 wave, cols 32 nb; LAYOUT 2 (a 128-column half `sub` of a 256-column
+// tile held by 2x2 waves): wave 2 r + sub holds rows 64 r + 32 m, cols 32 nb in acc[4 m + nb]; LAYOUT 3 (128-column
+// quarter `sub` of a 512-column tile): wave `sub` holds all 128 rows, rows 32 m / cols 32 nb in acc[4 m + nb].
+// ROWSCALE: multiply row r by
 // a_rstd[in_rows[r]] first (the plane GEMM's RMSNorm prologue, folded into the weights).
 __device__ __forceinline__ void store_out4(float* dst, f32x4 v) {
   if (OT_GEMM_NT_STORE) __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(dst));
@@ -183,8 +187,8 @@ __device__ __forceinline__ void store_out4_bf16(uint16_t* dst, f32x4 v) {
 
 // GS: compile the forward stored-GELU path (bf16-mode plane GEMM only: registers elsewhere)
 template <int EPIT, int LAYOUT, bool ROWSCALE, int RBN = 8, bool GS = false>
-__device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x16 (&acc)[4], float* smem, int tm,
-                                                  int n0, int g) {
+__device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x16* acc, float* smem, int tm,
+                                                  int n0, int g, int sub = 0) {
   const int epi = EPIT;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int h = lane >> 5, li = lane & 31;
@@ -241,12 +245,32 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
 #pragma unroll
           for (int r = 0; r < 16; ++r)
             ct[((wave >> 1) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * CLD + (wave & 1) * 64 + 32 * n + li] = acc[2 * hf + n][r];
-      } else if ((wave >> 1) == hf) {
+      } else if (LAYOUT == 1) {
+        if ((wave >> 1) == hf) {
 #pragma unroll
-        for (int nb = 0; nb < 4; ++nb)
+          for (int nb = 0; nb < 4; ++nb)
 #pragma unroll
-          for (int r = 0; r < 16; ++r)
-            ct[((wave & 1) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * CLD + 32 * nb + li] = acc[nb][r];
+            for (int r = 0; r < 16; ++r)
+              ct[((wave & 1) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * CLD + 32 * nb + li] = acc[nb][r];
+        }
+      } else if (LAYOUT == 3) {                         // LAYOUT 3: sub-tile `sub` is wave `sub`'s 16 blocks
+        if (wave == sub) {
+#pragma unroll
+          for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+              for (int r = 0; r < 16; ++r)
+                ct[(32 * m + (r & 3) + 8 * (r >> 2) + 4 * h) * CLD + 32 * nb + li] = acc[4 * (2 * hf + m) + nb][r];
+        }
+      } else if ((wave >> 1) == hf && (wave & 1) == sub) {   // LAYOUT 2: this half's rows are one wave's 64
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+          for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              ct[(32 * m + (r & 3) + 8 * (r >> 2) + 4 * h) * CLD + 32 * nb + li] = acc[4 * m + nb][r];
       }
       __syncthreads();
 #pragma unroll
@@ -1019,6 +1043,411 @@ __global__ __launch_bounds__(256, MINW) void plane_gemm_kernel(GemmArgs p) {
   gemm_vec_epilogue<EPIT, 1, RSC, MINW >= 4 ? OT_PLANE_EPI_RBN : 8, TERMS == 1>(p, acc, smem, tm, n0, g);
 }
 
+// Wide plane GEMM (OT_MATMUL_BF16, N % 256 == 0, K % 32 == 0): the plane GEMM's bf16 form on tiles of 128 rows x
+// 256 columns with 32 k per stage.  A 128 x 128 tile moves 512 B through L2 -> LDS per 32x32x16 MFMA and 4 MFMAs per
+// wave sit between two barriers; at C5's sizes (M = 530k rows, K 512-2048) that tile ran at 12-26% of the bf16 MFMA
+// rate with its L2 -> CU stream far below what L2 serves.  Here one A fragment feeds 8 MFMAs (each wave: rows 32 w,
+// all 256 columns), a stage is 384 B per MFMA and 16 MFMAs per wave sit between barriers.  A stage is two 16-k
+// sub-stages in the plane GEMM's own LDS images (A as there; B = plane 0 of the two 128-column image blocks), copied
+// by global_load_lds; three stages for bf16 A (72 KiB, two workgroups per CU), two for f32 A.  The epilogue is the
+// plane GEMM's, once per 128-column half (same outputs, bit for bit: one MFMA chain per output in the same k order).
+#ifndef OT_PLANE_WIDE
+#define OT_PLANE_WIDE 1
+#endif
+#ifndef OT_PLANE_WIDE_WL
+#define OT_PLANE_WIDE_WL 2
+#endif
+constexpr int PW_COLS = 2 * GT;
+template <int AXT>
+constexpr bool pw_abf() { return AXT == OT_AX_BF16 || AXT == OT_AX_BF16_RMSNORM; }
+template <int AXT>
+constexpr int pw_abytes() { return pw_abf<AXT>() ? GT * 32 : GT * 64; }      // one 16-k A image
+template <int AXT>
+constexpr int pw_sub() { return pw_abytes<AXT>() + 2 * GT * 32; }            // + B plane 0 of two column blocks
+template <int AXT>
+constexpr int pw_nstg() { return pw_abf<AXT>() ? 3 : 2; }
+template <int AXT>
+constexpr int pw_stage_lds() { return pw_nstg<AXT>() * 2 * pw_sub<AXT>(); }
+
+template <int AXT, int EPIT, int WL = OT_PLANE_WIDE_WL>
+__global__ __launch_bounds__(256, 2) void plane_wide_kernel(GemmArgs p) {
+  static_assert(AXT == OT_AX_NONE || pw_abf<AXT>(), "wide plane GEMM: A in f32 (rounded) or bf16");
+  constexpr bool ABF = pw_abf<AXT>();
+  constexpr bool RSC = AXT == OT_AX_BF16_RMSNORM;
+  constexpr int NSTG = pw_nstg<AXT>();
+  constexpr int ABYTES = pw_abytes<AXT>();
+  constexpr int SUB = pw_sub<AXT>();
+  constexpr int STG = 2 * SUB;
+  constexpr int OPS = 2 * ((ABF ? 1 : 2) + 2);        // copies per wave and stage
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  char* lds = reinterpret_cast<char*>(smem);
+  const int ntw = p.N / PW_COLS;
+  const int nwg = p.ntm * ntw;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int tm = wg / ntw, tw = wg % ntw;
+  const int g = p.tile_group ? p.tile_group[tm] : 0;
+  const int n0 = tw * PW_COLS;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int h = lane >> 5, li = lane & 31;
+  const int nk = p.K >> 4, ns = nk >> 1;
+
+  // A copy sources as in plane_gemm_kernel (rows of the tile past the row map read row 0: never stored)
+  const float* asrc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = (2 * wave + i) * 16 + (lane >> 2);
+    const int64_t gr = (int64_t)tm * GT + r;
+    int ir = p.in_rows ? p.in_rows[gr] : (int)gr;
+    ir = ir < 0 ? 0 : ir;
+    asrc[i] = p.A + (int64_t)ir * p.lda + 4 * ((lane & 3) ^ ((r >> 2) & 3));
+  }
+  const char* asrcb;
+  {
+    const int r = 32 * wave + (lane >> 1);
+    const int64_t gr = (int64_t)tm * GT + r;
+    int ir = p.in_rows ? p.in_rows[gr] : (int)gr;
+    ir = ir < 0 ? 0 : ir;
+    asrcb = reinterpret_cast<const char*>(p.A) + ((int64_t)ir * p.lda + 8 * ((lane & 1) ^ ((r >> 3) & 1))) * 2;
+  }
+  const int gb = p.w_gstride ? g : 0;
+  const char* bsrc[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+    bsrc[c] = reinterpret_cast<const char*>(p.bimg) +
+              ((int64_t)gb * p.bimg_ntn + p.bimg_tn0 + 2 * tw + c) * nk * PG_B_BYTES + wave * 1024 + 16 * lane;
+
+  auto issue = [&](int s, int buf) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ks = 2 * s + j;
+      char* sb = lds + buf * STG + j * SUB;
+      if (ABF) {
+        __builtin_amdgcn_global_load_lds((const void*)(asrcb + 32 * ks), (lds_void_t*)(sb + wave * 1024), 16, 0, 0);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + 16 * ks), (lds_void_t*)(sb + (2 * wave + i) * 1024),
+                                           16, 0, 0);
+      }
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+        __builtin_amdgcn_global_load_lds((const void*)(bsrc[c] + (int64_t)ks * PG_B_BYTES),
+                                         (lds_void_t*)(sb + ABYTES + c * 4096 + wave * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x16 acc[8];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[a][r] = 0.f;
+
+  // WL 1: wave w = rows 32 w, all 256 columns (acc[c * 4 + nb]); WL 2: wave 2 r + c = rows 64 r + 32 m, columns
+  // 128 c + 32 nb (acc[4 m + nb]): 6 fragment reads per 8 MFMAs instead of 9
+  constexpr int NA = WL == 2 ? 2 : 1;                 // A fragments per 16-k step
+  const int wr = WL == 2 ? wave >> 1 : wave, wc = WL == 2 ? wave & 1 : 0;
+  int aoff0[NA], aoff1[NA], aoffb[NA];
+#pragma unroll
+  for (int m = 0; m < NA; ++m) {
+    const int ra = (WL == 2 ? 64 : 32) * wr + 32 * m + li;
+    aoff0[m] = ra * 64 + 16 * ((2 * h) ^ ((li >> 2) & 3));
+    aoff1[m] = ra * 64 + 16 * ((2 * h + 1) ^ ((li >> 2) & 3));
+    aoffb[m] = ra * 32 + 16 * (h ^ ((li >> 3) & 1));
+  }
+  const int boff = ABYTES + li * 32 + 16 * (h ^ ((li >> 3) & 1)) + wc * 4096;
+
+  // normalised-A side output (OT_AX_BF16_RMSNORM, first column tile), as in plane_gemm_kernel (WL 2: the c = 0 waves)
+  bool xnw[NA] = {};
+  float xrs[NA] = {};
+  uint16_t* xnp[NA] = {};
+  float* gsm = reinterpret_cast<float*>(lds + NSTG * STG);
+  if (RSC && p.xn_out && tw == 0) {
+    for (int k = 4 * t; k < p.K; k += 4 * 256)
+      *reinterpret_cast<f32x4*>(gsm + k) = *reinterpret_cast<const f32x4*>(p.a_gamma + k);
+#pragma unroll
+    for (int m = 0; m < NA; ++m) {
+      const int64_t xgr = (int64_t)tm * GT + (WL == 2 ? 64 : 32) * wr + 32 * m + li;
+      const int xir = p.in_rows ? p.in_rows[xgr] : (int)xgr;
+      xnw[m] = xir >= 0 && wc == 0;
+      if (xnw[m]) {
+        xrs[m] = p.a_rstd[xir];
+        xnp[m] = p.xn_out + (int64_t)xir * p.ldxn + 8 * h;
+      }
+    }
+  }
+
+  issue(0, 0);
+  if (NSTG >= 3 && ns > 1) issue(1, 1);
+  for (int s = 0; s < ns; ++s) {
+    // this wave's copies of stage s are done (with three stages those of stage s + 1 may still fly), every
+    // wave's after the barrier, which also retires the reads of the buffer the next issue overwrites
+    if (NSTG >= 3 && s + 1 < ns) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(OPS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (s + NSTG - 1 < ns) issue(s + NSTG - 1, (s + NSTG - 1) % NSTG);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ks = 2 * s + j;
+      const char* sb = lds + (s % NSTG) * STG + j * SUB;
+      constexpr int NB = WL == 2 ? 4 : 8;
+      u32x4 fb[NB];
+#pragma unroll
+      for (int n = 0; n < NB; ++n) fb[n] = *reinterpret_cast<const u32x4*>(sb + boff + (n >> 2) * 4096 + (n & 3) * 1024);
+      u32x4 fa[NA];
+#pragma unroll
+      for (int m = 0; m < NA; ++m) {
+        if constexpr (ABF) {
+          fa[m] = *reinterpret_cast<const u32x4*>(sb + aoffb[m]);
+          if (RSC && xnw[m]) {                          // (x * gamma) * rstd from the bf16 x, rounded
+            const float* gp = gsm + 16 * ks + 8 * h;
+            const u32x4 w = fa[m];
+            const f32x4 a0 = {__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u),
+                              __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u)};
+            const f32x4 a1 = {__uint_as_float(w.z << 16), __uint_as_float(w.z & 0xffff0000u),
+                              __uint_as_float(w.w << 16), __uint_as_float(w.w & 0xffff0000u)};
+            const u32x2 b0 = bf16_rne4(a0 * *reinterpret_cast<const f32x4*>(gp) * xrs[m]);
+            const u32x2 b1 = bf16_rne4(a1 * *reinterpret_cast<const f32x4*>(gp + 4) * xrs[m]);
+            *reinterpret_cast<u32x4*>(xnp[m] + 16 * ks) = u32x4{b0.x, b0.y, b1.x, b1.y};
+          }
+        } else {
+          const f32x4 a0 = *reinterpret_cast<const f32x4*>(sb + aoff0[m]);
+          const f32x4 a1 = *reinterpret_cast<const f32x4*>(sb + aoff1[m]);
+          const u32x2 b0 = bf16_rne4(a0), b1 = bf16_rne4(a1);
+          fa[m] = u32x4{b0.x, b0.y, b1.x, b1.y};
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < NA; ++m)
+#pragma unroll
+        for (int n = 0; n < NB; ++n) acc[m * NB + n] = mfma_bf16(fa[m], fb[n], acc[m * NB + n]);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();                                    // the epilogue reuses the stage buffers
+  if constexpr (WL == 2) {
+    gemm_vec_epilogue<EPIT, 2, RSC, OT_PLANE_EPI_RBN, true>(p, acc, smem, tm, n0, g, 0);
+    __syncthreads();                                  // (the first half's dgamma / row reads of its LDS are done)
+    gemm_vec_epilogue<EPIT, 2, RSC, OT_PLANE_EPI_RBN, true>(p, acc, smem, tm, n0 + GT, g, 1);
+  } else {
+    gemm_vec_epilogue<EPIT, 1, RSC, OT_PLANE_EPI_RBN, true>(p, acc, smem, tm, n0, g);
+    __syncthreads();
+    gemm_vec_epilogue<EPIT, 1, RSC, OT_PLANE_EPI_RBN, true>(p, acc + 4, smem, tm, n0 + GT, g);
+  }
+}
+// Big plane GEMM (OT_MATMUL_BF16, N % 512 == 0, K % 32 == 0): tiles of 128 rows x 512 columns, one workgroup of
+// four waves per CU, each wave one 128 x 128 quarter (16 accumulator blocks: one A fragment feeds 4 MFMAs and one B
+// fragment 4, 0.5 LDS reads per MFMA), 32 k per stage, three stages in flight (bf16 A: 120 KiB of LDS).  The
+// epilogue is the plane GEMM's, once per quarter (the quarter's wave stages it through LDS).
+constexpr int PB_COLS = 4 * GT;
+constexpr int PB_NSTG = 3;
+template <int AXT>
+constexpr int pb_sub() { return pw_abytes<AXT>() + 4 * GT * 32; }            // A + B plane 0 of four column blocks
+template <int AXT>
+constexpr int pb_stage_lds() { return PB_NSTG * 2 * pb_sub<AXT>(); }
+
+template <int AXT, int EPIT>
+__global__ __launch_bounds__(256, 1) void plane_big_kernel(GemmArgs p) {
+  static_assert(AXT == OT_AX_NONE || pw_abf<AXT>(), "big plane GEMM: A in f32 (rounded) or bf16");
+  constexpr bool ABF = pw_abf<AXT>();
+  constexpr bool RSC = AXT == OT_AX_BF16_RMSNORM;
+  constexpr int NSTG = PB_NSTG;
+  constexpr int ABYTES = pw_abytes<AXT>();
+  constexpr int SUB = pb_sub<AXT>();
+  constexpr int STG = 2 * SUB;
+  constexpr int OPS = 2 * ((ABF ? 1 : 2) + 4);        // copies per wave and stage
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  char* lds = reinterpret_cast<char*>(smem);
+  const int ntw = p.N / PB_COLS;
+  const int nwg = p.ntm * ntw;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int tm = wg / ntw, tw = wg % ntw;
+  const int g = p.tile_group ? p.tile_group[tm] : 0;
+  const int n0 = tw * PB_COLS;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int h = lane >> 5, li = lane & 31;
+  const int nk = p.K >> 4, ns = nk >> 1;
+
+  const float* asrc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = (2 * wave + i) * 16 + (lane >> 2);
+    const int64_t gr = (int64_t)tm * GT + r;
+    int ir = p.in_rows ? p.in_rows[gr] : (int)gr;
+    ir = ir < 0 ? 0 : ir;
+    asrc[i] = p.A + (int64_t)ir * p.lda + 4 * ((lane & 3) ^ ((r >> 2) & 3));
+  }
+  const char* asrcb;
+  {
+    const int r = 32 * wave + (lane >> 1);
+    const int64_t gr = (int64_t)tm * GT + r;
+    int ir = p.in_rows ? p.in_rows[gr] : (int)gr;
+    ir = ir < 0 ? 0 : ir;
+    asrcb = reinterpret_cast<const char*>(p.A) + ((int64_t)ir * p.lda + 8 * ((lane & 1) ^ ((r >> 3) & 1))) * 2;
+  }
+  const int gb = p.w_gstride ? g : 0;
+  const char* bsrc = reinterpret_cast<const char*>(p.bimg) +
+                     ((int64_t)gb * p.bimg_ntn + p.bimg_tn0 + 4 * tw) * nk * PG_B_BYTES + wave * 1024 + 16 * lane;
+  const int64_t bstride = (int64_t)nk * PG_B_BYTES;   // next 128-column image block
+
+  auto issue = [&](int s, int buf) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ks = 2 * s + j;
+      char* sb = lds + buf * STG + j * SUB;
+      if (ABF) {
+        __builtin_amdgcn_global_load_lds((const void*)(asrcb + 32 * ks), (lds_void_t*)(sb + wave * 1024), 16, 0, 0);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + 16 * ks), (lds_void_t*)(sb + (2 * wave + i) * 1024),
+                                           16, 0, 0);
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        __builtin_amdgcn_global_load_lds((const void*)(bsrc + c * bstride + (int64_t)ks * PG_B_BYTES),
+                                         (lds_void_t*)(sb + ABYTES + c * 4096 + wave * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x16 acc[16];
+#pragma unroll
+  for (int a = 0; a < 16; ++a)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[a][r] = 0.f;
+
+  int aoff0[4], aoff1[4], aoffb[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int ra = 32 * m + li;
+    aoff0[m] = ra * 64 + 16 * ((2 * h) ^ ((li >> 2) & 3));
+    aoff1[m] = ra * 64 + 16 * ((2 * h + 1) ^ ((li >> 2) & 3));
+    aoffb[m] = ra * 32 + 16 * (h ^ ((li >> 3) & 1));
+  }
+  const int boff = ABYTES + wave * 4096 + li * 32 + 16 * (h ^ ((li >> 3) & 1));
+
+  // normalised-A side output (OT_AX_BF16_RMSNORM, first column tile): wave 0 writes every row
+  bool xnw[4] = {};
+  float xrs[4] = {};
+  uint16_t* xnp[4] = {};
+  float* gsm = reinterpret_cast<float*>(lds + NSTG * STG);
+  if (RSC && p.xn_out && tw == 0) {
+    for (int k = 4 * t; k < p.K; k += 4 * 256)
+      *reinterpret_cast<f32x4*>(gsm + k) = *reinterpret_cast<const f32x4*>(p.a_gamma + k);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int64_t xgr = (int64_t)tm * GT + 32 * m + li;
+      const int xir = p.in_rows ? p.in_rows[xgr] : (int)xgr;
+      xnw[m] = xir >= 0 && wave == 0;
+      if (xnw[m]) {
+        xrs[m] = p.a_rstd[xir];
+        xnp[m] = p.xn_out + (int64_t)xir * p.ldxn + 8 * h;
+      }
+    }
+  }
+
+  issue(0, 0);
+  if (ns > 1) issue(1, 1);
+  for (int s = 0; s < ns; ++s) {
+    if (s + 1 < ns) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(OPS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (s + NSTG - 1 < ns) issue(s + NSTG - 1, (s + NSTG - 1) % NSTG);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ks = 2 * s + j;
+      const char* sb = lds + (s % NSTG) * STG + j * SUB;
+      u32x4 fb[4], fa[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) fb[n] = *reinterpret_cast<const u32x4*>(sb + boff + n * 1024);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        if constexpr (ABF) {
+          fa[m] = *reinterpret_cast<const u32x4*>(sb + aoffb[m]);
+          if (RSC && xnw[m]) {
+            const float* gp = gsm + 16 * ks + 8 * h;
+            const u32x4 w = fa[m];
+            const f32x4 a0 = {__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u),
+                              __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u)};
+            const f32x4 a1 = {__uint_as_float(w.z << 16), __uint_as_float(w.z & 0xffff0000u),
+                              __uint_as_float(w.w << 16), __uint_as_float(w.w & 0xffff0000u)};
+            const u32x2 b0 = bf16_rne4(a0 * *reinterpret_cast<const f32x4*>(gp) * xrs[m]);
+            const u32x2 b1 = bf16_rne4(a1 * *reinterpret_cast<const f32x4*>(gp + 4) * xrs[m]);
+            *reinterpret_cast<u32x4*>(xnp[m] + 16 * ks) = u32x4{b0.x, b0.y, b1.x, b1.y};
+          }
+        } else {
+          const f32x4 a0 = *reinterpret_cast<const f32x4*>(sb + aoff0[m]);
+          const f32x4 a1 = *reinterpret_cast<const f32x4*>(sb + aoff1[m]);
+          const u32x2 b0 = bf16_rne4(a0), b1 = bf16_rne4(a1);
+          fa[m] = u32x4{b0.x, b0.y, b1.x, b1.y};
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[4 * m + n] = mfma_bf16(fa[m], fb[n], acc[4 * m + n]);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();                                    // the epilogue reuses the stage buffers
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (q) __syncthreads();
+    gemm_vec_epilogue<EPIT, 3, RSC, OT_PLANE_EPI_RBN, true>(p, acc, smem, tm, n0 + GT * q, g, q);
+  }
+}
+#define OT_WIDE_LIST(X)                                                                        \
+  X(OT_AX_NONE, 0)                                                                             \
+  X(OT_AX_NONE, OT_EPI_RESIDUAL | OT_EPI_DROPOUT | OT_EPI_ROW_RSTD)                           \
+  X(OT_AX_NONE, OT_EPI_RESIDUAL | OT_EPI_ROW_RSTD)                                            \
+  X(OT_AX_BF16_RMSNORM, 0)                                                                     \
+  X(OT_AX_BF16_RMSNORM, OT_EPI_BIAS)                                                           \
+  X(OT_AX_BF16_RMSNORM, OT_EPI_BIAS | OT_EPI_C_BF16)                                           \
+  X(OT_AX_BF16, 0)                                                                             \
+  X(OT_AX_BF16, OT_EPI_BIAS | OT_EPI_RESIDUAL)                                                 \
+  X(OT_AX_BF16, OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_DROPOUT)                                \
+  X(OT_AX_BF16, OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_DROPOUT | OT_EPI_ROW_RSTD)              \
+  X(OT_AX_BF16, OT_EPI_BIAS | OT_EPI_RESIDUAL | OT_EPI_ROW_RSTD)                               \
+  X(OT_AX_BF16, OT_EPI_GELU_BWD | OT_EPI_ROWDOT | OT_EPI_C_BF16 | OT_EPI_AUX_BF16)             \
+  X(OT_AX_BF16, OT_EPI_GELU_BWD | OT_EPI_ROWDOT | OT_EPI_C_BF16)                               \
+  X(OT_AX_BF16, OT_EPI_RMSNORM_BWD | OT_EPI_DROPOUT)                                           \
+  X(OT_AX_BF16, OT_EPI_RMSNORM_BWD)
+
+// process-wide switch of the wide tile (ot_plane_wide: A/B timing and the bit-identity tests)
+static std::atomic<int> g_plane_wide{OT_PLANE_WIDE};
+extern "C" int ot_plane_wide(int on) {
+  const int prev = g_plane_wide.load();
+  if (on >= 0) g_plane_wide.store(on > 2 ? 2 : on);
+  return prev;
+}
+
+// the wide kernel for (a_xform, epi), or null; its stage LDS bytes in *stage_lds (opted in above 64 KiB once)
+static void (*plane_wide_for(int x, int e, bool big, int* stage_lds))(GemmArgs) {
+  void (*k)(GemmArgs) = nullptr;
+#define OT_WIDE_PICK(AX_, EP_)                                                      \
+  if (x == (AX_) && e == (EP_)) {                                                   \
+    k = big ? plane_big_kernel<AX_, EP_> : plane_wide_kernel<AX_, EP_>;             \
+    *stage_lds = big ? pb_stage_lds<AX_>() : pw_stage_lds<AX_>();                   \
+  }
+  OT_WIDE_LIST(OT_WIDE_PICK)
+#undef OT_WIDE_PICK
+  static std::once_flag once;
+  std::call_once(once, [] {
+#define OT_WIDE_ATTR(AX_, EP_)                                                                               \
+  (void)hipFuncSetAttribute((const void*)plane_wide_kernel<AX_, EP_>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                            pw_stage_lds<AX_>() + 4096);                                                         \
+  (void)hipFuncSetAttribute((const void*)plane_big_kernel<AX_, EP_>, hipFuncAttributeMaxDynamicSharedMemorySize,  \
+                            pb_stage_lds<AX_>() + 4096);
+    OT_WIDE_LIST(OT_WIDE_ATTR)
+#undef OT_WIDE_ATTR
+    (void)hipGetLastError();
+  });
+  return k;
+}
+
 // Pre-split B images (ot_split_images).  desc [nd][10] int64: {src_off, sn, sk, gstride, kscale_off
 // (-1: none), dst_off (ushorts), first_unit, G, N, K}; B[g][n][k] = src[g*gstride + n*sn + k*sk]
 // (* kscale[k]); one unit = one (g, n tile, 16-k stage) block of 3 x 128 x 16 16-bit planes, one thread per
@@ -1769,6 +2198,183 @@ __global__ __launch_bounds__(256, OT_WGRAD_COPY_MINW) void wgrad_bf16_kernel(Wgr
   }
 }
 
+// The copy-staged bf16 weight gradient on 128 (k) x 256 (n) output tiles (N % 256 == 0): a stage is the A image
+// and two 128-column D images (24 KiB at 32 rows, three stages: two workgroups per CU), each wave 64 k x 128 n
+// (one D image, 8 MFMAs per 16 rows against 4), 384 B of L2 -> LDS traffic per MFMA against 512.  Same
+// products in the same row order as wgrad_bf16_kernel: the slabs are bit-identical.
+#ifndef OT_WGRAD_WIDE
+#define OT_WGRAD_WIDE 1
+#endif
+constexpr int WW_NST = 3;
+constexpr int WW_STB = 3 * WG_IMG;
+constexpr int WW_LDS = WW_NST * WW_STB + 2 * WG_IDR * 4;
+template <bool IDL>
+__global__ __launch_bounds__(256, 2) void wgrad_bf16_wide_kernel(WgradArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem_c[];
+  const int ntw = p.N / (2 * GT);
+  const int per_chunk = p.ntk * ntw;
+  int c, rem;
+  if (!wgrad_tile(blockIdx.x, per_chunk, p.nchunks, c, rem)) return;
+  const int tk = rem / ntw, tw = rem % ntw;
+  const int k0 = tk * GT, n0 = tw * 2 * GT;
+  const int row_begin = p.chunks[3 * c + 1], row_count = p.chunks[3 * c + 2];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int h = lane >> 5, li = lane & 31;
+  const int wm = (wave >> 1) * 64, wh = wave & 1;
+  const uint16_t* A16 = reinterpret_cast<const uint16_t*>(p.A);
+  const uint16_t* D16 = reinterpret_cast<const uint16_t*>(p.D);
+  int lrow[WG_NI], acol[WG_NI], dcol[WG_NI];
+#pragma unroll
+  for (int i = 0; i < WG_NI; ++i) {
+    const int r = 4 * (WG_NI * wave + i) + (lane >> 4);
+    const int lc = (lane & 15) ^ (((r & 3) << 2) | ((r >> 2) & 3));
+    lrow[i] = r;
+    acol[i] = k0 + 8 * lc < p.K ? k0 + 8 * lc : 0;
+    dcol[i] = n0 + 8 * lc;                              // (+ 128 for the second image; N % 256 == 0)
+  }
+  const int nst = (row_count + WG_SR - 1) / WG_SR;
+  auto row_id = [&](int st, int i) -> int {
+    const int r = st * WG_SR + lrow[i];
+    const int64_t mi = (int64_t)row_begin + (r < row_count ? r : 0);
+    return IDL ? p.a_rows[mi] : (int)mi;
+  };
+  int* idbuf = reinterpret_cast<int*>(smem_c + WW_NST * WW_STB);   // [2][WG_IDR]
+  int pre[WG_IDR / 256];
+  auto prefetch_block = [&](int b) {
+#pragma unroll
+    for (int j = 0; j < WG_IDR / 256; ++j) {
+      const int r = (WG_IDB * b + WW_NST - 1) * WG_SR + t + 256 * j;
+      const int64_t mi = (int64_t)row_begin + (r < row_count ? r : 0);
+      pre[j] = p.a_rows[mi];
+    }
+  };
+  auto issue = [&](int st, const int (&ids)[WG_NI]) {
+    char* sb = smem_c + (st % WW_NST) * WW_STB;
+#pragma unroll
+    for (int i = 0; i < WG_NI; ++i) {
+      const bool ok = st * WG_SR + lrow[i] < row_count && ids[i] >= 0;
+      const uint16_t* sa = A16 + (int64_t)(ok ? ids[i] : 0) * p.lda + acol[i];
+      const uint16_t* sd = ok ? D16 + (int64_t)ids[i] * p.ldd + dcol[i] : g_zero_row + 8 * (lane & 15);
+      const int o = (WG_NI * wave + i) * 1024;
+      __builtin_amdgcn_global_load_lds((const void*)sa, (lds_void_t*)(sb + o), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)sd, (lds_void_t*)(sb + WG_IMG + o), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(ok ? sd + GT : sd), (lds_void_t*)(sb + 2 * WG_IMG + o), 16, 0, 0);
+    }
+  };
+  const int gi = lane & 15, q = gi >> 2, pp = gi & 3, g1 = (lane >> 4) & 1;
+  int aoff[2][2], doff[4][2];
+#pragma unroll
+  for (int rd = 0; rd < 2; ++rd) {
+    const int r = 8 * h + 4 * rd + q;
+#pragma unroll
+    for (int m = 0; m < 2; ++m) aoff[m][rd] = wsw_off(r, (wm + 32 * m + 16 * g1) / 8 + (pp >> 1)) + 8 * (pp & 1);
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) doff[nb][rd] = wsw_off(r, (32 * nb + 16 * g1) / 8 + (pp >> 1)) + 8 * (pp & 1);
+  }
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  // bias (tk == 0): thread t sums columns 4 (t & 63) .. + 3 (image (t & 63) >> 5) over rows (SR / 4) (t >> 6) ..
+  const bool do_bias = p.bslab && tk == 0;
+  const int bcp = t & 63, brs = t >> 6;
+  float bs[4] = {0.f, 0.f, 0.f, 0.f};
+
+  for (int s0 = 0; s0 < WW_NST - 1; ++s0)
+    if (s0 < nst) {
+      int ids[WG_NI];
+#pragma unroll
+      for (int i = 0; i < WG_NI; ++i) ids[i] = row_id(s0, i);
+      issue(s0, ids);
+    }
+  if (IDL) prefetch_block(0);
+  for (int st = 0; st < nst; ++st) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (st + WW_NST - 1 <= nst) {
+      asm volatile("s_waitcnt vmcnt(%0)" :: "n"((WW_NST - 2) * 3 * WG_NI) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const bool blk = IDL && (st % WG_IDB) == 0;
+    if (blk) {
+      int* ib = idbuf + ((st / WG_IDB) & 1) * WG_IDR;
+#pragma unroll
+      for (int j = 0; j < WG_IDR / 256; ++j) ib[t + 256 * j] = pre[j];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (blk) prefetch_block(st / WG_IDB + 1);
+    if (st + WW_NST - 1 < nst) {
+      int ids[WG_NI];
+      const int* ib = idbuf + ((st / WG_IDB) & 1) * WG_IDR + (st % WG_IDB) * WG_SR;
+#pragma unroll
+      for (int i = 0; i < WG_NI; ++i) ids[i] = IDL ? ib[lrow[i]] : row_id(st + WW_NST - 1, i);
+      issue(st + WW_NST - 1, ids);
+    }
+    const char* As = smem_c + (st % WW_NST) * WW_STB;
+    const char* Ds = As + WG_IMG * (1 + wh);
+    if (do_bias) {
+      const char* Db = As + WG_IMG * (1 + (bcp >> 5));
+      const int bc = 4 * (bcp & 31);
+#pragma unroll
+      for (int r8 = 0; r8 < WG_SR / 4; ++r8) {
+        const int r = (WG_SR / 4) * brs + r8;
+        const u32x2 w = *reinterpret_cast<const u32x2*>(Db + wsw_off(r, bc >> 3) + 2 * (bc & 7));
+        bs[0] += __uint_as_float(w.x << 16);
+        bs[1] += __uint_as_float(w.x & 0xffff0000u);
+        bs[2] += __uint_as_float(w.y << 16);
+        bs[3] += __uint_as_float(w.y & 0xffff0000u);
+      }
+    }
+#pragma unroll
+    for (int t2 = 0; t2 < WG_SR / 16; ++t2) {
+      const int po = t2 * 16 * 256;
+      u32x4 fa[2], fb[4];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        v4i16 a0 = ds_tr16_nowait(As + po, aoff[m][0]), a1 = ds_tr16_nowait(As + po, aoff[m][1]);
+        v4i16 d0 = ds_tr16_nowait(Ds + po, doff[2 * m][0]), d1 = ds_tr16_nowait(Ds + po, doff[2 * m][1]);
+        v4i16 e0 = ds_tr16_nowait(Ds + po, doff[2 * m + 1][0]), e1 = ds_tr16_nowait(Ds + po, doff[2 * m + 1][1]);
+        tr16_wait(a0, a1, d0, d1);
+        asm volatile("" : "+v"(e0), "+v"(e1) :: "memory");   // (complete: the wait above is lgkmcnt(0))
+        const u32x2 a0u = __builtin_bit_cast(u32x2, a0), a1u = __builtin_bit_cast(u32x2, a1);
+        const u32x2 d0u = __builtin_bit_cast(u32x2, d0), d1u = __builtin_bit_cast(u32x2, d1);
+        const u32x2 e0u = __builtin_bit_cast(u32x2, e0), e1u = __builtin_bit_cast(u32x2, e1);
+        fa[m] = u32x4{a0u.x, a0u.y, a1u.x, a1u.y};
+        fb[2 * m] = u32x4{d0u.x, d0u.y, d1u.x, d1u.y};
+        fb[2 * m + 1] = u32x4{e0u.x, e0u.y, e1u.x, e1u.y};
+      }
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[m][n] = mfma_bf16(fa[m], fb[n], acc[m][n]);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float* slab = p.slab + (int64_t)c * p.K * p.N;
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int k = k0 + wm + 32 * m + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (k >= p.K) continue;
+#pragma unroll
+      for (int n = 0; n < 4; ++n) slab[(int64_t)k * p.N + n0 + GT * wh + 32 * n + li] = acc[m][n][r];
+    }
+  if (do_bias) {                                      // fixed-order sum of the 4 row sets per column
+    __syncthreads();
+    float* bl = reinterpret_cast<float*>(smem_c);     // [4][256]
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bl[brs * 2 * GT + 4 * bcp + j] = bs[j];
+    __syncthreads();
+    p.bslab[(int64_t)c * p.N + n0 + t] = ((bl[t] + bl[2 * GT + t]) + bl[4 * GT + t]) + bl[6 * GT + t];
+  }
+}
+
 // Sum the slabs of each group's chunks (chunks of one group are contiguous) into dW[g] (and db).
 // Block = 16 float4 columns x 16 chunk lanes; chunk lane c sums chunks c, c+16, ... and the 16
 // partials are combined in a fixed order through LDS (deterministic).
@@ -2002,6 +2608,8 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
   hipStream_t s = (hipStream_t)stream;
   void (*kern)(GemmArgs) = nullptr;
   bool plane = false;
+  int wide_lds = 0;                     // > 0: the wide / big plane GEMM (its stage LDS bytes, its tile columns)
+  int wide_cols = 0;
   const int e = epi, x = a_xform;
 #define OT_SPEC(NT_, AX_, EP_)                                                                  \
   if (mode == (NT_ ? OT_GEMM_NT : OT_GEMM_NN) && x == AX_ && e == (EP_))                         \
@@ -2086,6 +2694,18 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
     OT_PSPEC_BR(OT_EPI_BIAS | OT_EPI_C_BF16)
 #undef OT_PSPEC_BR
     if (pk) { kern = pk; plane = true; }
+    // bf16 mode, whole 256-column tiles and 32-k stages: the wide tile (same outputs)
+    const int wmode = g_plane_wide.load(std::memory_order_relaxed);
+    if (pk && one && wmode && N % PW_COLS == 0 && K % 32 == 0 && !(p.xn_out && K > 1024)) {
+      const bool big = wmode == 2 && N % PB_COLS == 0;
+      int stage_lds = 0;
+      void (*wk)(GemmArgs) = plane_wide_for(x, e, big, &stage_lds);
+      if (wk) {
+        kern = wk;
+        wide_lds = stage_lds;
+        wide_cols = big ? PB_COLS : PW_COLS;
+      }
+    }
   }
   OT_REQUIRE((x != OT_AX_BF16 && x != OT_AX_BF16_RMSNORM) || plane,
              "ot_mixed_gemm: no plane GEMM for a_xform %d with epilogue %d (or edge tiles)", x, epi);
@@ -2145,7 +2765,12 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
       (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     (void)hipGetLastError();
   });
-  hipLaunchKernelGGL(kern, dim3(nwg), dim3(256), launch_shmem, s, p);
+  if (wide_lds > 0) {
+    const size_t wshm = std::max((size_t)wide_lds + xn_lds, (size_t)(64 * (GT + 4) + 8 * GT) * 4);
+    hipLaunchKernelGGL(kern, dim3((unsigned)ntiles * (unsigned)(N / wide_cols)), dim3(256), wshm, s, p);
+  } else {
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(256), launch_shmem, s, p);
+  }
   OT_LAUNCH_CHECK("ot_mixed_gemm");
   if (dgpart) {
     launch_colsum_reduce(dgpart, ntiles, N, rms->dgamma, rms->accumulate_dgamma, s, dgpart + (int64_t)ntiles * N);
@@ -2258,6 +2883,14 @@ extern "C" int ot_mixed_gemm_rms_img(int mode, const float* A, int64_t lda, int 
 }
 
 
+// process-wide switch of the 128 x 256 bf16 weight-gradient tile (ot_wgrad_wide)
+static std::atomic<int> g_wgrad_wide{OT_WGRAD_WIDE};
+extern "C" int ot_wgrad_wide(int on) {
+  const int prev = g_wgrad_wide.load();
+  if (on >= 0) g_wgrad_wide.store(on ? 1 : 0);
+  return prev;
+}
+
 extern "C" size_t ot_wgrad_workspace_size(int nchunks, int K, int N) {
   return ((size_t)nchunks * K * N + (size_t)nchunks * N) * sizeof(float);
 }
@@ -2339,8 +2972,19 @@ static int wgrad_impl(const float* A, int64_t lda, const int32_t* a_rows, int a_
         (void)hipGetLastError();
       });
     }
-    hipLaunchKernelGGL(kern, dim3(wgrad_grid(nchunks, p.ntk * p.ntn)), dim3(256),
-                       copy ? copy_shmem : split ? split_shmem : shmem, s, p);
+    if (copy && N % (2 * GT) == 0 && g_wgrad_wide.load(std::memory_order_relaxed)) {
+      static std::once_flag wide_once;
+      std::call_once(wide_once, [] {
+        for (void (*k)(WgradArgs) : {wgrad_bf16_wide_kernel<true>, wgrad_bf16_wide_kernel<false>})
+          (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, WW_LDS);
+        (void)hipGetLastError();
+      });
+      hipLaunchKernelGGL(a_rows ? wgrad_bf16_wide_kernel<true> : wgrad_bf16_wide_kernel<false>,
+                         dim3(wgrad_grid(nchunks, p.ntk * (N / (2 * GT)))), dim3(256), (size_t)WW_LDS, s, p);
+    } else {
+      hipLaunchKernelGGL(kern, dim3(wgrad_grid(nchunks, p.ntk * p.ntn)), dim3(256),
+                         copy ? copy_shmem : split ? split_shmem : shmem, s, p);
+    }
     OT_LAUNCH_CHECK("ot_mixed_gemm_wgrad");
   }
   const int wblocks = (int)ceil_div((int64_t)K * N / 4, 16);

@@ -340,6 +340,18 @@ def split_image_elems(G: int, N: int, K: int) -> int:
     return int(_lib.load().ot_split_image_elems(G, N, K))
 
 
+def plane_wide(on: int = -1) -> int:
+    """ot_plane_wide: switch the bf16-mode plane GEMM's 128 x 256 tile on (1) / off (0) process-wide, or query
+    (-1); returns the previous setting (a tuning / test knob: both tiles give bit-identical outputs)."""
+    return _lib.size('ot_plane_wide', int(on))
+
+
+def wgrad_wide(on: int = -1) -> int:
+    """ot_wgrad_wide: the bf16 weight gradient's 128 x 256 tile on (1) / off (0) / query (-1); returns the previous
+    setting (bit-identical slabs either way)."""
+    return _lib.size('ot_wgrad_wide', int(on))
+
+
 def split_images(base, desc_dev, ndesc, total_units, img) -> None:
     call('ot_split_images', ptr(base), ptr(desc_dev), ndesc, total_units, ptr(img), _prec(), stream())
 

@@ -275,6 +275,42 @@ def test_bf16_mode_forward_and_train(dev, dtype):
         K.set_matmul_mode(old)
 
 
+@pytest.mark.parametrize('dtype', ['bf16', 'fp8attn'])
+def test_bf16_plane_wide_tile_bit_identical(dev, dtype):
+    """The bf16-mode plane GEMM's 128 x 256 and 128 x 512 tiles and the bf16 weight gradient's 128 x 256 tile
+    (ot_plane_wide 1 / 2, ot_wgrad_wide; every C5-width GEMM: N % 256 == 0) against the 128 x 128 tiles on one d = 512 model (C5's width, FFN 1024, pyramid tail maps, NS-token weight groups): the
+    training forward's probabilities and every parameter gradient bit-identical — each output is the same MFMA
+    chain in the same k order and the same epilogue."""
+    from recommend_amd import kernels as K
+    cfg = small_criteo('tail', pyramid=True, layers=2, d=512, H=8, f=1024, Lns=4, seq_lens=(12, 9, 7))
+    cfg.compute_dtype = dtype
+    old = K.set_matmul_mode('bf16')
+    prev = (K.plane_wide(-1), K.wgrad_wide(-1))
+    try:
+        P, model, batch = setup(cfg, 37, dev)
+        ns, seq, lab = batch
+        y = stack_labels(lab, cfg.tasks, dev)
+        res = {}
+        for wide in (2, 1, 0, 2):
+            K.plane_wide(wide); K.wgrad_wide(min(wide, 1))
+            model._step = 0                      # the same dropout masks every run
+            model.flat.grad.zero_()
+            probs = model.forward_probs(ns_t(ns, dev), ns_t(seq, dev), training=True)
+            keras_bce_loss(y, probs, cfg.tasks).backward()
+            torch.cuda.synchronize()
+            r = (probs.detach().clone(), model.flat.grad.clone())
+            if wide in res:
+                assert torch.equal(res[wide][0], r[0]) and torch.equal(res[wide][1], r[1])   # run to run
+            res[wide] = r
+        assert torch.isfinite(res[0][1]).all()
+        for wide in (1, 2):
+            assert torch.equal(res[wide][0], res[0][0])
+            assert torch.equal(res[wide][1], res[0][1])
+    finally:
+        K.plane_wide(prev[0]); K.wgrad_wide(prev[1])
+        K.set_matmul_mode(old)
+
+
 def test_two_precisions_in_one_process(dev):
     """Precision is a property of each model (the C ABI takes it per call; no process-wide mode): an f32-
     accurate model and a bf16 model built in one process, their forwards and backwards interleaved, each

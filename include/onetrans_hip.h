@@ -254,12 +254,14 @@ int ot_mixed_gemm_img(int mode, const float* A, int64_t lda, int K, const int32_
                       uint32_t seed, uint32_t site, float drop_rate, int tail_K, int tail_I,
                       const int32_t* tail_pos, const uint16_t* b_image, int image_ntn, int image_tn0,
                       int precision, void* stream);
-/* The bf16-mode plane GEMM's wide tile (128 rows x 256 columns, 32 k per stage; N % 256 == 0, K % 32 == 0): the
- * same outputs bit for bit as the 128 x 128 tile, fewer L2 -> LDS bytes per MFMA.  on = 1 / 0 switches it process-
- * wide (default 1), on = -1 only queries; returns the previous setting.  A tuning and test knob. */
+/* The bf16-mode plane GEMM's tile for N % 256 == 0, K % 32 == 0: 0 = 128 x 128, 1 = auto (default: 128 x 256 when
+ * N <= K, else 128 x 128), 2 / 3 / 4 = 128 x 256 / 128 x 512 / 256 x 256 where the shape allows; every tile gives
+ * the same outputs bit for bit (fewer L2 -> LDS bytes per MFMA on the larger ones).  Process-wide; on = -1 only
+ * queries; returns the previous setting.  A tuning and test knob. */
 int ot_plane_wide(int on);
-/* The bf16 weight gradient's (OT_WG_D_BF16 with OT_AX_BF16 A) wide tile, 128 x 256 outputs (N % 256 == 0): the same
- * slabs bit for bit as the 128 x 128 tile.  Same switch semantics as ot_plane_wide. */
+/* The bf16 weight gradient's (OT_WG_D_BF16 with OT_AX_BF16 A) tile: 0 = 128 x 128, 1 = auto (default: 256 x 256
+ * where K % 256 == N % 256 == 0, else 128 x 256 where N % 256 == 0), 2 = 128 x 256, 3 = 256 x 256; the same slabs
+ * bit for bit.  Same switch semantics as ot_plane_wide. */
 int ot_wgrad_wide(int on);
 int ot_mixed_gemm_rms_img(int mode, const float* A, int64_t lda, int K, const int32_t* in_rows,
                           int a_xform, const float* a_rstd, const float* a_gamma,

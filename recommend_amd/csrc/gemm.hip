@@ -167,7 +167,9 @@ __device__ __forceinline__ bool wgrad_tile(int b, int per_chunk, int nchunks, in
 // LAYOUT 0: 2x2 waves, acc[2m + n] = rows 64 (wave >> 1) + 32 m, cols 64 (wave & 1) + 32 n;
 // LAYOUT 1: 4x1 waves, acc[nb] = rows 32 wave, cols 32 nb; LAYOUT 2 (a 128-column half `sub` of a 256-column
 // tile held by 2x2 waves): wave 2 r + sub holds rows 64 r + 32 m, cols 32 nb in acc[4 m + nb]; LAYOUT 3 (128-column
-// quarter `sub` of a 512-column tile): wave `sub` holds all 128 rows, rows 32 m / cols 32 nb in acc[4 m + nb].
+// quarter `sub` of a 512-column tile): wave `sub` holds all 128 rows, rows 32 m / cols 32 nb in acc[4 m + nb];
+// LAYOUT 4 (128-column half `sub` of a 256 x 256 tile's row half, the epilogue run by that row half's four waves
+// with thread ids `tid` 0..255): wave 2 sub + j holds all 128 rows x columns 64 j + 32 nb in acc[2 m + nb].
 // ROWSCALE: multiply row r by
 // a_rstd[in_rows[r]] first (the plane GEMM's RMSNorm prologue, folded into the weights).
 __device__ __forceinline__ void store_out4(float* dst, f32x4 v) {
@@ -188,9 +190,9 @@ __device__ __forceinline__ void store_out4_bf16(uint16_t* dst, f32x4 v) {
 // GS: compile the forward stored-GELU path (bf16-mode plane GEMM only: registers elsewhere)
 template <int EPIT, int LAYOUT, bool ROWSCALE, int RBN = 8, bool GS = false>
 __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x16* acc, float* smem, int tm,
-                                                  int n0, int g, int sub = 0) {
+                                                  int n0, int g, int sub = 0, int tid = -1) {
   const int epi = EPIT;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = tid >= 0 ? tid : (int)threadIdx.x, lane = t & 63, wave = t >> 6;
   const int h = lane >> 5, li = lane & 31;
     // ---- vector epilogue: the accumulator tile goes through LDS (the staging buffers are free: the
     // last main-loop barrier ended every read) in two 64-row halves; each thread then finishes 8
@@ -252,6 +254,17 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
 #pragma unroll
             for (int r = 0; r < 16; ++r)
               ct[((wave & 1) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * CLD + 32 * nb + li] = acc[nb][r];
+        }
+      } else if (LAYOUT == 4) {                         // LAYOUT 4: waves 2 sub, 2 sub + 1 (64 columns each)
+        if ((wave >> 1) == sub) {
+#pragma unroll
+          for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+              for (int r = 0; r < 16; ++r)
+                ct[(32 * m + (r & 3) + 8 * (r >> 2) + 4 * h) * CLD + 64 * (wave & 1) + 32 * nb + li] =
+                    acc[2 * (2 * hf + m) + nb][r];
         }
       } else if (LAYOUT == 3) {                         // LAYOUT 3: sub-tile `sub` is wave `sub`'s 16 blocks
         if (wave == sub) {
@@ -1399,6 +1412,186 @@ __global__ __launch_bounds__(256, 1) void plane_big_kernel(GemmArgs p) {
     gemm_vec_epilogue<EPIT, 3, RSC, OT_PLANE_EPI_RBN, true>(p, acc, smem, tm, n0 + GT * q, g, q);
   }
 }
+// Square plane GEMM (OT_MATMUL_BF16, N % 256 == 0, K % 32 == 0, an even number of row tiles): 256 x 256 tiles, one
+// workgroup of 8 waves per CU (2 per SIMD), wave (rh, cq) = rows 128 rh .. + 127 x columns 64 cq .. + 63 (8 blocks:
+// 6 fragment reads per 8 MFMAs), 256 B of L2 -> LDS per MFMA (the 128 x 256 tile: 384; at C5's sizes that stream,
+// not the MFMA, set the pace).  The tile's two 128-row halves may belong to different weight groups (tile_group):
+// then each half's B image is copied into its own LDS region (uniform tiles copy one).  Epilogue: the plane GEMM's,
+// each row half's four waves finishing its two 128-column quarters, both halves at once in separate LDS.
+template <int AXT>
+constexpr int ps_abytes() { return pw_abf<AXT>() ? 2 * GT * 32 : 2 * GT * 64; }   // one 16-k A image, 256 rows
+template <int AXT>
+constexpr int ps_sub() { return ps_abytes<AXT>() + 2 * (2 * GT * 32); }           // + two 256-column B planes
+template <int AXT>
+constexpr int ps_nstg() { return pw_abf<AXT>() ? 3 : 2; }
+template <int AXT>
+constexpr int ps_stage_lds() { return ps_nstg<AXT>() * 2 * ps_sub<AXT>(); }
+
+template <int AXT, int EPIT>
+__global__ __launch_bounds__(512, 1) void plane_sq_kernel(GemmArgs p) {
+  static_assert(AXT == OT_AX_NONE || pw_abf<AXT>(), "square plane GEMM: A in f32 (rounded) or bf16");
+  constexpr bool ABF = pw_abf<AXT>();
+  constexpr bool RSC = AXT == OT_AX_BF16_RMSNORM;
+  constexpr int NSTG = ps_nstg<AXT>();
+  constexpr int ABYTES = ps_abytes<AXT>();
+  constexpr int SUB = ps_sub<AXT>();
+  constexpr int STG = 2 * SUB;
+  constexpr int AOPS = ABF ? 1 : 2;                   // A copies per wave and sub-stage
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  char* lds = reinterpret_cast<char*>(smem);
+  const int ntw = p.N / PW_COLS;
+  const int ntp = p.ntm >> 1;                          // row-tile pairs
+  const int wg = xcd_remap(blockIdx.x, ntp * ntw);
+  const int tp = wg / ntw, tw = wg % ntw;
+  const int gA = p.tile_group ? p.tile_group[2 * tp] : 0, gB = p.tile_group ? p.tile_group[2 * tp + 1] : 0;
+  const bool uni = gA == gB || p.w_gstride == 0;
+  const int n0 = tw * PW_COLS;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int h = lane >> 5, li = lane & 31;
+  const int rh = wave >> 2, cq = wave & 3;
+  const int nk = p.K >> 4, ns = nk >> 1;
+
+  // A copies: bf16 A, wave w = rows 32 w .. + 31 of the 256; f32 A, instruction i of wave w = rows 16 (2 w + i) ..
+  const float* asrc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = (2 * wave + i) * 16 + (lane >> 2);
+    const int64_t gr = (int64_t)tp * 2 * GT + r;
+    int ir = p.in_rows ? p.in_rows[gr] : (int)gr;
+    ir = ir < 0 ? 0 : ir;
+    asrc[i] = p.A + (int64_t)ir * p.lda + 4 * ((lane & 3) ^ ((r >> 2) & 3));
+  }
+  const char* asrcb;
+  {
+    const int r = 32 * wave + (lane >> 1);
+    const int64_t gr = (int64_t)tp * 2 * GT + r;
+    int ir = p.in_rows ? p.in_rows[gr] : (int)gr;
+    ir = ir < 0 ? 0 : ir;
+    asrcb = reinterpret_cast<const char*>(p.A) + ((int64_t)ir * p.lda + 8 * ((lane & 1) ^ ((r >> 3) & 1))) * 2;
+  }
+  // B copies: wave w = KiB (w & 3) of column block (w >> 2) of the half's group image (region 1: group gB)
+  const char* bsrc[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int gq = p.w_gstride ? (q ? gB : gA) : 0;
+    bsrc[q] = reinterpret_cast<const char*>(p.bimg) +
+              ((int64_t)gq * p.bimg_ntn + p.bimg_tn0 + 2 * tw + (wave >> 2)) * nk * PG_B_BYTES + (wave & 3) * 1024 +
+              16 * lane;
+  }
+  auto issue = [&](int s, int buf) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ks = 2 * s + j;
+      char* sb = lds + buf * STG + j * SUB;
+      if (ABF) {
+        __builtin_amdgcn_global_load_lds((const void*)(asrcb + 32 * ks), (lds_void_t*)(sb + wave * 1024), 16, 0, 0);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + 16 * ks), (lds_void_t*)(sb + (2 * wave + i) * 1024),
+                                           16, 0, 0);
+      }
+      __builtin_amdgcn_global_load_lds((const void*)(bsrc[0] + (int64_t)ks * PG_B_BYTES),
+                                       (lds_void_t*)(sb + ABYTES + wave * 1024), 16, 0, 0);
+      if (!uni)
+        __builtin_amdgcn_global_load_lds((const void*)(bsrc[1] + (int64_t)ks * PG_B_BYTES),
+                                         (lds_void_t*)(sb + ABYTES + 8192 + wave * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x16 acc[8];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[a][r] = 0.f;
+
+  int aoff0[4], aoff1[4], aoffb[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int ra = 128 * rh + 32 * m + li;
+    aoff0[m] = ra * 64 + 16 * ((2 * h) ^ ((li >> 2) & 3));
+    aoff1[m] = ra * 64 + 16 * ((2 * h + 1) ^ ((li >> 2) & 3));
+    aoffb[m] = ra * 32 + 16 * (h ^ ((li >> 3) & 1));
+  }
+  const int boff = ABYTES + (uni ? 0 : rh * 8192) + (cq >> 1) * 4096 + 2048 * (cq & 1) + li * 32 + 16 * (h ^ ((li >> 3) & 1));
+
+  bool xnw[4] = {};
+  float xrs[4] = {};
+  uint16_t* xnp[4] = {};
+  float* gsm = reinterpret_cast<float*>(lds + NSTG * STG);
+  if (RSC && p.xn_out && tw == 0) {
+    for (int k = 4 * t; k < p.K; k += 4 * 512)
+      *reinterpret_cast<f32x4*>(gsm + k) = *reinterpret_cast<const f32x4*>(p.a_gamma + k);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int64_t xgr = (int64_t)tp * 2 * GT + 128 * rh + 32 * m + li;
+      const int xir = p.in_rows ? p.in_rows[xgr] : (int)xgr;
+      xnw[m] = xir >= 0 && cq == 0;
+      if (xnw[m]) {
+        xrs[m] = p.a_rstd[xir];
+        xnp[m] = p.xn_out + (int64_t)xir * p.ldxn + 8 * h;
+      }
+    }
+  }
+
+  issue(0, 0);
+  if (NSTG >= 3 && ns > 1) issue(1, 1);
+  for (int s = 0; s < ns; ++s) {
+    if (NSTG >= 3 && s + 1 < ns) {
+      if (uni) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * (AOPS + 1)) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * (AOPS + 2)) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (s + NSTG - 1 < ns) issue(s + NSTG - 1, (s + NSTG - 1) % NSTG);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ks = 2 * s + j;
+      const char* sb = lds + (s % NSTG) * STG + j * SUB;
+      u32x4 fb[2], fa[4];
+#pragma unroll
+      for (int n = 0; n < 2; ++n) fb[n] = *reinterpret_cast<const u32x4*>(sb + boff + n * 1024);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        if constexpr (ABF) {
+          fa[m] = *reinterpret_cast<const u32x4*>(sb + aoffb[m]);
+          if (RSC && xnw[m]) {
+            const float* gp = gsm + 16 * ks + 8 * h;
+            const u32x4 w = fa[m];
+            const f32x4 a0 = {__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u),
+                              __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u)};
+            const f32x4 a1 = {__uint_as_float(w.z << 16), __uint_as_float(w.z & 0xffff0000u),
+                              __uint_as_float(w.w << 16), __uint_as_float(w.w & 0xffff0000u)};
+            const u32x2 b0 = bf16_rne4(a0 * *reinterpret_cast<const f32x4*>(gp) * xrs[m]);
+            const u32x2 b1 = bf16_rne4(a1 * *reinterpret_cast<const f32x4*>(gp + 4) * xrs[m]);
+            *reinterpret_cast<u32x4*>(xnp[m] + 16 * ks) = u32x4{b0.x, b0.y, b1.x, b1.y};
+          }
+        } else {
+          const f32x4 a0 = *reinterpret_cast<const f32x4*>(sb + aoff0[m]);
+          const f32x4 a1 = *reinterpret_cast<const f32x4*>(sb + aoff1[m]);
+          const u32x2 b0 = bf16_rne4(a0), b1 = bf16_rne4(a1);
+          fa[m] = u32x4{b0.x, b0.y, b1.x, b1.y};
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) acc[2 * m + n] = mfma_bf16(fa[m], fb[n], acc[2 * m + n]);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();                                    // the epilogue reuses the stage buffers
+  // each row half's four waves finish its two quarters in its own LDS (both halves in step: same barriers)
+  float* esm = smem + rh * (64 * (GT + 4) + 8 * GT);
+  const int tm = 2 * tp + rh;
+  const int g = rh ? gB : gA;
+  gemm_vec_epilogue<EPIT, 4, RSC, OT_PLANE_EPI_RBN, true>(p, acc, esm, tm, n0, g, 0, t & 255);
+  __syncthreads();
+  gemm_vec_epilogue<EPIT, 4, RSC, OT_PLANE_EPI_RBN, true>(p, acc, esm, tm, n0 + GT, g, 1, t & 255);
+}
 #define OT_WIDE_LIST(X)                                                                        \
   X(OT_AX_NONE, 0)                                                                             \
   X(OT_AX_NONE, OT_EPI_RESIDUAL | OT_EPI_DROPOUT | OT_EPI_ROW_RSTD)                           \
@@ -1416,21 +1609,32 @@ __global__ __launch_bounds__(256, 1) void plane_big_kernel(GemmArgs p) {
   X(OT_AX_BF16, OT_EPI_RMSNORM_BWD | OT_EPI_DROPOUT)                                           \
   X(OT_AX_BF16, OT_EPI_RMSNORM_BWD)
 
+// the tile for a bf16-mode plane GEMM of N % 256 == 0 columns (K % 32 == 0): measured at C5's shapes
+// (tools/c5_gemm_bench.py, profiles/r06/c5_gemm_tiles.txt)
+// (K >= N: 128 x 256 ~20% faster than 128 x 128 — C5's FFN2 / Wo forwards and input-gradient GEMMs; output-heavy
+// shapes (N > K: FFN1 / QKV forwards, FFN2 dgrad) stay on 128 x 128, the 256-column tiles' epilogues serialise there;
+// 256 x 256 and 128 x 512 measured slower at every C5 shape)
+static int plane_tile_auto(int K, int N, int ntiles) {
+  (void)ntiles;
+  return N <= K ? 1 : 0;
+}
+
 // process-wide switch of the wide tile (ot_plane_wide: A/B timing and the bit-identity tests)
 static std::atomic<int> g_plane_wide{OT_PLANE_WIDE};
 extern "C" int ot_plane_wide(int on) {
   const int prev = g_plane_wide.load();
-  if (on >= 0) g_plane_wide.store(on > 2 ? 2 : on);
+  if (on >= 0) g_plane_wide.store(on > 4 ? 4 : on);
   return prev;
 }
 
 // the wide kernel for (a_xform, epi), or null; its stage LDS bytes in *stage_lds (opted in above 64 KiB once)
-static void (*plane_wide_for(int x, int e, bool big, int* stage_lds))(GemmArgs) {
+// kind 1: 128 x 256 (plane_wide_kernel), 2: 128 x 512 (plane_big_kernel), 3: 256 x 256 (plane_sq_kernel)
+static void (*plane_wide_for(int x, int e, int kind, int* stage_lds))(GemmArgs) {
   void (*k)(GemmArgs) = nullptr;
-#define OT_WIDE_PICK(AX_, EP_)                                                      \
-  if (x == (AX_) && e == (EP_)) {                                                   \
-    k = big ? plane_big_kernel<AX_, EP_> : plane_wide_kernel<AX_, EP_>;             \
-    *stage_lds = big ? pb_stage_lds<AX_>() : pw_stage_lds<AX_>();                   \
+#define OT_WIDE_PICK(AX_, EP_)                                                                        \
+  if (x == (AX_) && e == (EP_)) {                                                                     \
+    k = kind == 3 ? plane_sq_kernel<AX_, EP_> : kind == 2 ? plane_big_kernel<AX_, EP_> : plane_wide_kernel<AX_, EP_>; \
+    *stage_lds = kind == 3 ? ps_stage_lds<AX_>() : kind == 2 ? pb_stage_lds<AX_>() : pw_stage_lds<AX_>();  \
   }
   OT_WIDE_LIST(OT_WIDE_PICK)
 #undef OT_WIDE_PICK
@@ -1440,7 +1644,9 @@ static void (*plane_wide_for(int x, int e, bool big, int* stage_lds))(GemmArgs) 
   (void)hipFuncSetAttribute((const void*)plane_wide_kernel<AX_, EP_>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                             pw_stage_lds<AX_>() + 4096);                                                         \
   (void)hipFuncSetAttribute((const void*)plane_big_kernel<AX_, EP_>, hipFuncAttributeMaxDynamicSharedMemorySize,  \
-                            pb_stage_lds<AX_>() + 4096);
+                            pb_stage_lds<AX_>() + 4096);                                                        \
+  (void)hipFuncSetAttribute((const void*)plane_sq_kernel<AX_, EP_>, hipFuncAttributeMaxDynamicSharedMemorySize,   \
+                            ps_stage_lds<AX_>() + 4096);
     OT_WIDE_LIST(OT_WIDE_ATTR)
 #undef OT_WIDE_ATTR
     (void)hipGetLastError();
@@ -2203,7 +2409,7 @@ __global__ __launch_bounds__(256, OT_WGRAD_COPY_MINW) void wgrad_bf16_kernel(Wgr
 // (one D image, 8 MFMAs per 16 rows against 4), 384 B of L2 -> LDS traffic per MFMA against 512.  Same
 // products in the same row order as wgrad_bf16_kernel: the slabs are bit-identical.
 #ifndef OT_WGRAD_WIDE
-#define OT_WGRAD_WIDE 1
+#define OT_WGRAD_WIDE 1                                 // auto: 256 x 256 where K and N allow, else 128 x 256
 #endif
 constexpr int WW_NST = 3;
 constexpr int WW_STB = 3 * WG_IMG;
@@ -2372,6 +2578,164 @@ __global__ __launch_bounds__(256, 2) void wgrad_bf16_wide_kernel(WgradArgs p) {
     for (int j = 0; j < 4; ++j) bl[brs * 2 * GT + 4 * bcp + j] = bs[j];
     __syncthreads();
     p.bslab[(int64_t)c * p.N + n0 + t] = ((bl[t] + bl[2 * GT + t]) + bl[4 * GT + t]) + bl[6 * GT + t];
+  }
+}
+
+// The copy-staged bf16 weight gradient on 256 x 256 output tiles (K % 256 == 0, N % 256 == 0): 8 waves, wave
+// (wk, wn) = k rows 64 wk .. + 63 x n columns 128 wn .. + 127; a 32-row stage is four 128-column images (A 0 / 1,
+// D 0 / 1; 32 KiB), four stages (three in flight); 256 B of L2 -> LDS per MFMA.  Same products in the same row order
+// as wgrad_bf16_kernel (bias: the first 256 threads, as wgrad_bf16_wide_kernel): the slabs are bit-identical.
+constexpr int WS_NST = 4;
+constexpr int WS_STB = 4 * WG_IMG;
+constexpr int WS_IDR = WG_IDB * WG_SR;                 // ids per block: one per thread (512)
+constexpr int WS_LDS = WS_NST * WS_STB + 2 * WS_IDR * 4;
+static_assert(WG_SR == 32 && WS_IDR == 512, "square wgrad: 32-row stages");
+template <bool IDL>
+__global__ __launch_bounds__(512, 1) void wgrad_bf16_sq_kernel(WgradArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem_c[];
+  const int ntw = p.N / (2 * GT), ntk = p.K / (2 * GT);
+  const int per_chunk = ntk * ntw;
+  int c, rem;
+  if (!wgrad_tile(blockIdx.x, per_chunk, p.nchunks, c, rem)) return;
+  const int tk = rem / ntw, tw = rem % ntw;
+  const int k0 = tk * 2 * GT, n0 = tw * 2 * GT;
+  const int row_begin = p.chunks[3 * c + 1], row_count = p.chunks[3 * c + 2];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int h = lane >> 5, li = lane & 31;
+  const int wk = wave >> 1, wn = wave & 1;
+  const uint16_t* A16 = reinterpret_cast<const uint16_t*>(p.A);
+  const uint16_t* D16 = reinterpret_cast<const uint16_t*>(p.D);
+  // copy lanes: wave w fills KiB w of each image = rows 4 w + lane / 16, physical chunk lane % 16
+  const int lrow = 4 * wave + (lane >> 4);
+  const int lc = (lane & 15) ^ (((lrow & 3) << 2) | ((lrow >> 2) & 3));
+  const int acol = k0 + 8 * lc, dcol = n0 + 8 * lc;
+  const int nst = (row_count + WG_SR - 1) / WG_SR;
+  auto row_id = [&](int st) -> int {
+    const int r = st * WG_SR + lrow;
+    const int64_t mi = (int64_t)row_begin + (r < row_count ? r : 0);
+    return IDL ? p.a_rows[mi] : (int)mi;
+  };
+  int* idbuf = reinterpret_cast<int*>(smem_c + WS_NST * WS_STB);   // [2][WS_IDR]
+  int pre = 0;
+  auto prefetch_block = [&](int b) {
+    const int r = (WG_IDB * b + WS_NST - 1) * WG_SR + t;
+    const int64_t mi = (int64_t)row_begin + (r < row_count ? r : 0);
+    pre = p.a_rows[mi];
+  };
+  auto issue = [&](int st, int id) {
+    char* sb = smem_c + (st % WS_NST) * WS_STB;
+    const bool ok = st * WG_SR + lrow < row_count && id >= 0;
+    const uint16_t* sa = A16 + (int64_t)(ok ? id : 0) * p.lda + acol;
+    const uint16_t* sd = ok ? D16 + (int64_t)id * p.ldd + dcol : g_zero_row + 8 * (lane & 15);
+    const int o = wave * 1024;
+    __builtin_amdgcn_global_load_lds((const void*)sa, (lds_void_t*)(sb + o), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(sa + GT), (lds_void_t*)(sb + WG_IMG + o), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)sd, (lds_void_t*)(sb + 2 * WG_IMG + o), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(ok ? sd + GT : sd), (lds_void_t*)(sb + 3 * WG_IMG + o), 16, 0, 0);
+  };
+  const int gi = lane & 15, q = gi >> 2, pp = gi & 3, g1 = (lane >> 4) & 1;
+  int aoff[2][2], doff[4][2];
+#pragma unroll
+  for (int rd = 0; rd < 2; ++rd) {
+    const int r = 8 * h + 4 * rd + q;
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+      aoff[m][rd] = wsw_off(r, (64 * (wk & 1) + 32 * m + 16 * g1) / 8 + (pp >> 1)) + 8 * (pp & 1);
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) doff[nb][rd] = wsw_off(r, (32 * nb + 16 * g1) / 8 + (pp >> 1)) + 8 * (pp & 1);
+  }
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  const bool do_bias = p.bslab && tk == 0 && t < 256;
+  const int bcp = t & 63, brs = (t >> 6) & 3;
+  float bs[4] = {0.f, 0.f, 0.f, 0.f};
+
+  for (int s0 = 0; s0 < WS_NST - 1; ++s0)
+    if (s0 < nst) issue(s0, row_id(s0));
+  if (IDL) prefetch_block(0);
+  for (int st = 0; st < nst; ++st) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (st + WS_NST - 1 <= nst) {
+      asm volatile("s_waitcnt vmcnt(%0)" :: "n"((WS_NST - 2) * 4) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const bool blk = IDL && (st % WG_IDB) == 0;
+    if (blk) {
+      idbuf[((st / WG_IDB) & 1) * WS_IDR + t] = pre;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (blk) prefetch_block(st / WG_IDB + 1);
+    if (st + WS_NST - 1 < nst) {
+      const int id = IDL ? idbuf[((st / WG_IDB) & 1) * WS_IDR + (st % WG_IDB) * WG_SR + lrow] : row_id(st + WS_NST - 1);
+      issue(st + WS_NST - 1, id);
+    }
+    const char* Sb = smem_c + (st % WS_NST) * WS_STB;
+    const char* As = Sb + WG_IMG * (wk >> 1);
+    const char* Ds = Sb + WG_IMG * (2 + wn);
+    if (do_bias) {
+      const char* Db = Sb + WG_IMG * (2 + (bcp >> 5));
+      const int bc = 4 * (bcp & 31);
+#pragma unroll
+      for (int r8 = 0; r8 < WG_SR / 4; ++r8) {
+        const int r = (WG_SR / 4) * brs + r8;
+        const u32x2 w = *reinterpret_cast<const u32x2*>(Db + wsw_off(r, bc >> 3) + 2 * (bc & 7));
+        bs[0] += __uint_as_float(w.x << 16);
+        bs[1] += __uint_as_float(w.x & 0xffff0000u);
+        bs[2] += __uint_as_float(w.y << 16);
+        bs[3] += __uint_as_float(w.y & 0xffff0000u);
+      }
+    }
+#pragma unroll
+    for (int t2 = 0; t2 < WG_SR / 16; ++t2) {
+      const int po = t2 * 16 * 256;
+      u32x4 fa[2], fb[4];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        v4i16 a0 = ds_tr16_nowait(As + po, aoff[m][0]), a1 = ds_tr16_nowait(As + po, aoff[m][1]);
+        v4i16 d0 = ds_tr16_nowait(Ds + po, doff[2 * m][0]), d1 = ds_tr16_nowait(Ds + po, doff[2 * m][1]);
+        v4i16 e0 = ds_tr16_nowait(Ds + po, doff[2 * m + 1][0]), e1 = ds_tr16_nowait(Ds + po, doff[2 * m + 1][1]);
+        tr16_wait(a0, a1, d0, d1);
+        asm volatile("" : "+v"(e0), "+v"(e1) :: "memory");
+        const u32x2 a0u = __builtin_bit_cast(u32x2, a0), a1u = __builtin_bit_cast(u32x2, a1);
+        const u32x2 d0u = __builtin_bit_cast(u32x2, d0), d1u = __builtin_bit_cast(u32x2, d1);
+        const u32x2 e0u = __builtin_bit_cast(u32x2, e0), e1u = __builtin_bit_cast(u32x2, e1);
+        fa[m] = u32x4{a0u.x, a0u.y, a1u.x, a1u.y};
+        fb[2 * m] = u32x4{d0u.x, d0u.y, d1u.x, d1u.y};
+        fb[2 * m + 1] = u32x4{e0u.x, e0u.y, e1u.x, e1u.y};
+      }
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[m][n] = mfma_bf16(fa[m], fb[n], acc[m][n]);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float* slab = p.slab + (int64_t)c * p.K * p.N;
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int k = k0 + 64 * wk + 32 * m + (r & 3) + 8 * (r >> 2) + 4 * h;
+#pragma unroll
+      for (int n = 0; n < 4; ++n) slab[(int64_t)k * p.N + n0 + GT * wn + 32 * n + li] = acc[m][n][r];
+    }
+  if (p.bslab && tk == 0) {                           // fixed-order sum of the 4 row sets per column
+    __syncthreads();
+    float* bl = reinterpret_cast<float*>(smem_c);     // [4][256]
+    if (t < 256) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bl[brs * 2 * GT + 4 * bcp + j] = bs[j];
+    }
+    __syncthreads();
+    if (t < 256) p.bslab[(int64_t)c * p.N + n0 + t] = ((bl[t] + bl[2 * GT + t]) + bl[4 * GT + t]) + bl[6 * GT + t];
   }
 }
 
@@ -2608,8 +2972,8 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
   hipStream_t s = (hipStream_t)stream;
   void (*kern)(GemmArgs) = nullptr;
   bool plane = false;
-  int wide_lds = 0;                     // > 0: the wide / big plane GEMM (its stage LDS bytes, its tile columns)
-  int wide_cols = 0;
+  int wide_lds = 0;                     // > 0: the wide / big / square plane GEMM (its stage LDS bytes, its kind)
+  int wide_kind = 0;
   const int e = epi, x = a_xform;
 #define OT_SPEC(NT_, AX_, EP_)                                                                  \
   if (mode == (NT_ ? OT_GEMM_NT : OT_GEMM_NN) && x == AX_ && e == (EP_))                         \
@@ -2695,15 +3059,18 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
 #undef OT_PSPEC_BR
     if (pk) { kern = pk; plane = true; }
     // bf16 mode, whole 256-column tiles and 32-k stages: the wide tile (same outputs)
+    // tile: 1 auto, 2 / 3 / 4 force 128 x 256 / 128 x 512 / 256 x 256 (where the shape allows it)
     const int wmode = g_plane_wide.load(std::memory_order_relaxed);
     if (pk && one && wmode && N % PW_COLS == 0 && K % 32 == 0 && !(p.xn_out && K > 1024)) {
-      const bool big = wmode == 2 && N % PB_COLS == 0;
+      int kind = wmode == 1 ? plane_tile_auto(K, N, ntiles) : wmode - 1;
+      if (kind == 2 && N % PB_COLS != 0) kind = 1;
+      if (kind == 3 && ntiles % 2 != 0) kind = 1;
       int stage_lds = 0;
-      void (*wk)(GemmArgs) = plane_wide_for(x, e, big, &stage_lds);
+      void (*wk)(GemmArgs) = kind ? plane_wide_for(x, e, kind, &stage_lds) : nullptr;
       if (wk) {
         kern = wk;
         wide_lds = stage_lds;
-        wide_cols = big ? PB_COLS : PW_COLS;
+        wide_kind = kind;
       }
     }
   }
@@ -2767,7 +3134,9 @@ static int mixed_gemm_impl(int mode, const float* A, int64_t lda, int K, const i
   });
   if (wide_lds > 0) {
     const size_t wshm = std::max((size_t)wide_lds + xn_lds, (size_t)(64 * (GT + 4) + 8 * GT) * 4);
-    hipLaunchKernelGGL(kern, dim3((unsigned)ntiles * (unsigned)(N / wide_cols)), dim3(256), wshm, s, p);
+    const unsigned wg = wide_kind == 3 ? (unsigned)(ntiles / 2) * (unsigned)(N / PW_COLS)
+                                       : (unsigned)ntiles * (unsigned)(N / (wide_kind == 2 ? PB_COLS : PW_COLS));
+    hipLaunchKernelGGL(kern, dim3(wg), dim3(wide_kind == 3 ? 512 : 256), wshm, s, p);
   } else {
     hipLaunchKernelGGL(kern, dim3(nwg), dim3(256), launch_shmem, s, p);
   }
@@ -2883,11 +3252,12 @@ extern "C" int ot_mixed_gemm_rms_img(int mode, const float* A, int64_t lda, int 
 }
 
 
-// process-wide switch of the 128 x 256 bf16 weight-gradient tile (ot_wgrad_wide)
+// process-wide choice of the bf16 weight-gradient tile (ot_wgrad_wide): 0 128 x 128, 1 auto (256 x 256 where K and N
+// allow, else 128 x 256), 2 128 x 256, 3 256 x 256
 static std::atomic<int> g_wgrad_wide{OT_WGRAD_WIDE};
 extern "C" int ot_wgrad_wide(int on) {
   const int prev = g_wgrad_wide.load();
-  if (on >= 0) g_wgrad_wide.store(on ? 1 : 0);
+  if (on >= 0) g_wgrad_wide.store(on > 3 ? 3 : on);
   return prev;
 }
 
@@ -2972,7 +3342,17 @@ static int wgrad_impl(const float* A, int64_t lda, const int32_t* a_rows, int a_
         (void)hipGetLastError();
       });
     }
-    if (copy && N % (2 * GT) == 0 && g_wgrad_wide.load(std::memory_order_relaxed)) {
+    const int wgw = g_wgrad_wide.load(std::memory_order_relaxed);
+    if (copy && N % (2 * GT) == 0 && K % (2 * GT) == 0 && (wgw == 1 || wgw == 3)) {   // 256 x 256
+      static std::once_flag sq_once;
+      std::call_once(sq_once, [] {
+        for (void (*k)(WgradArgs) : {wgrad_bf16_sq_kernel<true>, wgrad_bf16_sq_kernel<false>})
+          (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, WS_LDS);
+        (void)hipGetLastError();
+      });
+      hipLaunchKernelGGL(a_rows ? wgrad_bf16_sq_kernel<true> : wgrad_bf16_sq_kernel<false>,
+                         dim3(wgrad_grid(nchunks, (K / (2 * GT)) * (N / (2 * GT)))), dim3(512), (size_t)WS_LDS, s, p);
+    } else if (copy && N % (2 * GT) == 0 && wgw) {
       static std::once_flag wide_once;
       std::call_once(wide_once, [] {
         for (void (*k)(WgradArgs) : {wgrad_bf16_wide_kernel<true>, wgrad_bf16_wide_kernel<false>})

@@ -341,14 +341,15 @@ def split_image_elems(G: int, N: int, K: int) -> int:
 
 
 def plane_wide(on: int = -1) -> int:
-    """ot_plane_wide: switch the bf16-mode plane GEMM's 128 x 256 tile on (1) / off (0) process-wide, or query
-    (-1); returns the previous setting (a tuning / test knob: both tiles give bit-identical outputs)."""
+    """ot_plane_wide: the bf16-mode plane GEMM's tile process-wide — 0: 128 x 128, 1: auto (default), 2 / 3 / 4:
+    128 x 256 / 128 x 512 / 256 x 256 where the shape allows — or query (-1); returns the previous setting (a tuning
+    / test knob: every tile gives bit-identical outputs)."""
     return _lib.size('ot_plane_wide', int(on))
 
 
 def wgrad_wide(on: int = -1) -> int:
-    """ot_wgrad_wide: the bf16 weight gradient's 128 x 256 tile on (1) / off (0) / query (-1); returns the previous
-    setting (bit-identical slabs either way)."""
+    """ot_wgrad_wide: the bf16 weight gradient's tile — 0: 128 x 128, 1: auto (default), 2: 128 x 256, 3: 256 x 256
+    where K and N allow — or query (-1); returns the previous setting (bit-identical slabs either way)."""
     return _lib.size('ot_wgrad_wide', int(on))
 
 

@@ -277,8 +277,9 @@ def test_bf16_mode_forward_and_train(dev, dtype):
 
 @pytest.mark.parametrize('dtype', ['bf16', 'fp8attn'])
 def test_bf16_plane_wide_tile_bit_identical(dev, dtype):
-    """The bf16-mode plane GEMM's 128 x 256 and 128 x 512 tiles and the bf16 weight gradient's 128 x 256 tile
-    (ot_plane_wide 1 / 2, ot_wgrad_wide; every C5-width GEMM: N % 256 == 0) against the 128 x 128 tiles on one d = 512 model (C5's width, FFN 1024, pyramid tail maps, NS-token weight groups): the
+    """The bf16-mode plane GEMM's 128 x 256, 128 x 512 and 256 x 256 tiles and the bf16 weight gradient's 128 x 256
+    and 256 x 256 tiles (ot_plane_wide, ot_wgrad_wide, each with its auto choice; every C5-width GEMM: N % 256 == 0; the
+    256 x 256 tile's row halves in different weight groups at the NS tokens) against the 128 x 128 tiles on one d = 512 model (C5's width, FFN 1024, pyramid tail maps, NS-token weight groups): the
     training forward's probabilities and every parameter gradient bit-identical — each output is the same MFMA
     chain in the same k order and the same epilogue."""
     from recommend_amd import kernels as K
@@ -291,8 +292,9 @@ def test_bf16_plane_wide_tile_bit_identical(dev, dtype):
         ns, seq, lab = batch
         y = stack_labels(lab, cfg.tasks, dev)
         res = {}
-        for wide in (2, 1, 0, 2):
-            K.plane_wide(wide); K.wgrad_wide(min(wide, 1))
+        # plane 256x256 / 128x512 / 128x256 / auto / 128x128 with wgrad 256x256 / 128x256 / 128x256 / auto / 128x128
+        for wide in (4, 3, 2, 1, 0, 4):
+            K.plane_wide(wide); K.wgrad_wide({4: 3, 3: 2}.get(wide, wide))
             model._step = 0                      # the same dropout masks every run
             model.flat.grad.zero_()
             probs = model.forward_probs(ns_t(ns, dev), ns_t(seq, dev), training=True)
@@ -303,7 +305,7 @@ def test_bf16_plane_wide_tile_bit_identical(dev, dtype):
                 assert torch.equal(res[wide][0], r[0]) and torch.equal(res[wide][1], r[1])   # run to run
             res[wide] = r
         assert torch.isfinite(res[0][1]).all()
-        for wide in (1, 2):
+        for wide in (1, 2, 3, 4):
             assert torch.equal(res[wide][0], res[0][0])
             assert torch.equal(res[wide][1], res[0][1])
     finally:

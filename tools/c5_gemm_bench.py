@@ -49,12 +49,13 @@ cases.update({
                                               a_xform=WG, device=dev), 2.0 * M * d * 3 * d),
 })
 def switch(on):
-    K.plane_wide(on); K.wgrad_wide(min(on, 1))
+    # plane: 0 128x128 / 2 128x256 / 3 128x512 / 4 256x256; wgrad: 0 128x128 / 2 128x256 / 3 256x256
+    K.plane_wide(on); K.wgrad_wide({4: 3, 3: 2}.get(on, on))
 sel = [k for k in cases if not sys.argv[1:] or any(s in k for s in sys.argv[1:])]
 timed = {}
-NAMES = {2: '128x512', 1: 'wide 128x256', 0: '128x128'}
+NAMES = {4: '256x256', 3: '128x512', 2: '128x256', 0: '128x128'}
 for k in sel:
-    for wide in ((1, 0) if 'wgrad' in k else (2, 1, 0)):
+    for wide in (4, 2, 0):
         timed[f'{k} [{NAMES[wide]}]'] = (wide, cases[k][0], cases[k][1])
 xb = torch.randn(M, d, device=dev, dtype=torch.bfloat16); w1b = torch.randn(d, f, device=dev, dtype=torch.bfloat16)
 ub = torch.empty(M, f, device=dev, dtype=torch.bfloat16)
@@ -69,11 +70,11 @@ timed.update({
 # the two tiles' outputs agree bit for bit
 for k in sel:
     outs = []
-    for wide in (2, 1, 0):
+    for wide in (4, 3, 2, 0):
         switch(wide); cases[k][0](); torch.cuda.synchronize()
         outs.append((u16.clone(), y.clone(), dW.clone(), db.clone()))
-    same = [all(torch.equal(a, b) for a, b in zip(o, outs[2])) for o in outs[:2]]
-    print(f'{k}: 128x512 / 128x256 == 128x128: {same}', flush=True)
+    same = [all(torch.equal(a, b) for a, b in zip(o, outs[3])) for o in outs[:3]]
+    print(f'{k}: 256x256 / 128x512 / 128x256 == 128x128: {same}', flush=True)
 for _ in range(2):
     for k, (w, fn, fl) in timed.items():
         if w is not None: switch(w)

@@ -384,8 +384,9 @@ def main():
                      f'({dom["pair_launches_per_step"]:.0f} of {dom["launches_per_step"]:.0f} launches per step on the pair)')
         elif model.matmul == 'bf16':
             gpeak = BF16_MFMA_PEAK_TFLOPS
-            gkern = ('plane_gemm_kernel / mixed_gemm_kernel + wgrad_split_kernel (operands rounded to bf16, one bf16 '
-                     'MFMA product)')
+            gkern = ('plane_gemm_kernel (128x128; plane_wide_kernel 128x256 where K >= N) / mixed_gemm_kernel + '
+                     'wgrad_bf16_sq_kernel (256x256) / wgrad_split_kernel (operands rounded to bf16, one bf16 MFMA '
+                     'product)')
         else:
             gpeak = FP32_MFMA_PEAK_TFLOPS
             gkern = 'mixed_gemm_kernel + wgrad_kernel (native f32 MFMA)'

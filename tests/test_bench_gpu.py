@@ -2,6 +2,7 @@
 key by key — metric / value / unit / timing fields, the roofline block (bound, achieved, peak, frac,
 traffic, both roofs beside it) and the CPU-baseline block."""
 import json
+import math
 import os
 import subprocess
 import sys
@@ -37,3 +38,24 @@ def test_bench_json_contract():
     for k in ('value', 'unit', 'cores', 'kind', 'sample'):
         assert k in cb, k
     assert cb['value'] > 0 and cb['cores'] >= 1 and cb['kind'] == 'port'
+    # the timed steps ran on a finite trajectory (bench.py fails a repeat that ends on a non-finite loss): the
+    # trainable optimizer by default, every repeat's loss finite
+    assert d['optimizer']['kind'] == 'trainable'
+    assert math.isfinite(d['final_loss']) and len(d['loss_repeats']) == d['repeats'] == 1
+    assert all(math.isfinite(x) for x in d['loss_repeats'])
+
+
+@pytest.mark.gpu
+def test_bench_refuses_nonfinite_trajectory():
+    """The reference optimizer constants (config.py's dense lr 0.005, momentum 0.99999) drive the C1 weights to
+    non-finite values within a few steps; bench.py then exits non-zero instead of timing degenerate operands
+    (--allow-nonfinite reports such a run for diagnostics)."""
+    cmd = [sys.executable, os.path.join(ROOT, 'bench.py'), '--config', 'C1', '--steps', '20', '--warmup', '20',
+           '--repeats', '1', '--no-probe', '--no-cpu-baseline', '--optimizer', 'reference']
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    lines = [l for l in r.stdout.splitlines() if l.startswith('{')]
+    if r.returncode == 0:                     # the trajectory stayed finite for these steps: the line says so
+        d = json.loads(lines[0])
+        assert all(math.isfinite(x) for x in d['loss_repeats'])
+    else:
+        assert 'non-finite loss' in r.stderr and not lines

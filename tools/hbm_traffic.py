@@ -20,7 +20,9 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-FAMILIES = {'gemm': ('mixed_gemm_kernel', 'plane_gemm_kernel', 'wgrad_kernel<', 'wgrad_split_kernel', 'wgrad_bf16_kernel'),
+FAMILIES = {'gemm': ('mixed_gemm_kernel', 'plane_gemm_kernel', 'plane_wide_kernel', 'plane_big_kernel', 'plane_sq_kernel',
+                     'wgrad_kernel<', 'wgrad_split_kernel', 'wgrad_bf16_kernel', 'wgrad_bf16_wide_kernel',
+                     'wgrad_bf16_sq_kernel'),
             'attention': ('attn_',),
             # the embedding path: NS gather, sequence-id row maps, and the sparse update
             # (key prep, rocPRIM radix sort, de-duplication, segment sums, clip, Adagrad); the sequence

@@ -20,7 +20,8 @@ print(f'| **total** | | | {tot/1e6/steps:.3f} | 100 |')
 # row_rstd_finish_kernel, the fused-norm dgamma colsum; the row-wise RMSNorm backward's dgamma uses the
 # same colsum kernels, a small overcount).  'main' launches compare with the bench's
 # roofline.launches_per_step (one per call), the time with its kernel_time_ms_per_step.mixed_gemm.
-MAIN = ('mixed_gemm_kernel', 'plane_gemm_kernel', 'wgrad_kernel<', 'wgrad_split_kernel<', 'wgrad_bf16_kernel')
+MAIN = ('mixed_gemm_kernel', 'plane_gemm_kernel', 'plane_wide_kernel', 'plane_big_kernel', 'plane_sq_kernel', 'wgrad_kernel<',
+        'wgrad_split_kernel<', 'wgrad_bf16_kernel', 'wgrad_bf16_wide_kernel', 'wgrad_bf16_sq_kernel')
 HELP = ('wgrad_reduce_kernel', 'row_rstd_finish_kernel', 'colsum_reduce_kernel', 'colsum_chunk_kernel')
 fam = [r for r in rows if any(k in r['Name'] for k in MAIN)]
 hlp = [r for r in rows if any(k in r['Name'] for k in HELP)]

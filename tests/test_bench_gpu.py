@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 @pytest.mark.gpu
 def test_bench_json_contract():
     cmd = [sys.executable, os.path.join(ROOT, 'bench.py'), '--config', 'C1', '--steps', '2', '--warmup', '1',
-           '--repeats', '1', '--probe-steps', '1', '--cpu-seconds', '1']
+           '--repeats', '1', '--probe-steps', '1', '--cpu-batch', '64', '--cpu-steps', '1']
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith('{')]

@@ -1076,6 +1076,30 @@ __global__ __launch_bounds__(64 * WAVES, TERMS == 1 ? 2 : 1) void attn_bwd_split
 template <int HD, int NW>
 constexpr int BWDG_LDS() { return 2 * 32 * HD * 2 + NW * (2 * 32 * HD * 2 + 32 * 32 * 2) + NW * 32 * HD * 4; }
 
+// XOR-swizzled byte offset in a bf16 image of RB-byte rows (the key-grouped backward's [32][HD] and [32][32]
+// images): row r's 16-B chunk index is XORed with (r / (256 / RB)) mod (RB / 16), so the rows that share LDS banks
+// (256 B apart) spread over the chunks — the row-major fragment reads (one row per lane) and the transposed reads
+// were 2- to 8-way bank-conflicted on the plain layout (C5: conflict cycles 68% of the LDS-active cycles).
+#ifndef OT_BWDG_SWIZZLE
+#define OT_BWDG_SWIZZLE 1
+#endif
+template <int RB>
+__device__ __forceinline__ int gswz(int r, int b) {
+  constexpr int P = 256 / RB, C = RB / 16;
+  return OT_BWDG_SWIZZLE ? r * RB + (b ^ (((r / P) & (C - 1)) << 4)) : r * RB + b;
+}
+template <int RB>
+__device__ __forceinline__ u32x4 tr16_frag_sw(const char* img, int ra, int rb, int colbase, int lane) {
+  typedef short v4i16 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+  const int gi = lane & 15, q = gi >> 2, pp = gi & 3;
+  const int c = colbase + 16 * ((lane >> 4) & 1) + 4 * pp;
+  const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(img + gswz<RB>(ra + q, c * 2)));
+  const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(img + gswz<RB>(rb + q, c * 2)));
+  const u32x2 a = __builtin_bit_cast(u32x2, lo), b = __builtin_bit_cast(u32x2, hi);
+  return u32x4{a.x, a.y, b.x, b.y};
+}
+
 template <int HD, int NW, bool QB = false>
 __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kernel(AttnArgs p) {
   static_assert(HD == 64 || HD == 32, "grouped backward: HD 32 or 64");
@@ -1092,7 +1116,7 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kerne
   char* kimg = oimg + IMG + w * (2 * IMG + SIMG);      // this wave's key block
   char* vimg = kimg + IMG;
   char* simg = vimg + IMG;                             // this wave's dS^T [key][query]
-  float* dqbuf = reinterpret_cast<float*>(lds_g + 2 * IMG + NW * (2 * IMG + SIMG));   // [NW][NB][16][64]
+  float* dqbuf = reinterpret_cast<float*>(lds_g + 2 * IMG + NW * (2 * IMG + SIMG));   // [NW][NB][4][64 lanes][4]
   const int S = p.kslices;
   const int pair = blockIdx.x / S, slice = blockIdx.x - pair * S;
   const int b = pair / p.H, h = pair % p.H;
@@ -1111,6 +1135,8 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kerne
   const int key0 = 32 * kb;
   const int kpos = key0 + li;
   const uint16_t* Q16 = reinterpret_cast<const uint16_t*>(p.qkv) + tok0 * p.ld + h * HD;
+  // this lane's K / V fragments (row li, dims (HD / 2) hh + 8 st ..) for every query block: held in registers
+  u32x4 kF[NS], vF[NS];
   if constexpr (QB) {                                  // bf16 operands: the images are copies
     const u32x4 z = {0u, 0u, 0u, 0u};
 #pragma unroll
@@ -1118,8 +1144,10 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kerne
       const int64_t o = (int64_t)kpos * p.ld + (HD / 2) * hh + 8 * st;
       const u32x4 kB = kpos < I ? *reinterpret_cast<const u32x4*>(Q16 + p.d + o) : z;
       const u32x4 vB = kpos < I ? *reinterpret_cast<const u32x4*>(Q16 + 2 * p.d + o) : z;
-      *reinterpret_cast<u32x4*>(kimg + (li * HD + (HD / 2) * hh + 8 * st) * 2) = kB;
-      *reinterpret_cast<u32x4*>(vimg + (li * HD + (HD / 2) * hh + 8 * st) * 2) = vB;
+      *reinterpret_cast<u32x4*>(kimg + gswz<HD * 2>(li, ((HD / 2) * hh + 8 * st) * 2)) = kB;
+      *reinterpret_cast<u32x4*>(vimg + gswz<HD * 2>(li, ((HD / 2) * hh + 8 * st) * 2)) = vB;
+      kF[st] = kB;
+      vF[st] = vB;
     }
   } else {
     float kf[HD / 2], vf[HD / 2];
@@ -1130,8 +1158,10 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kerne
       u32x4 kB[3], vB[3];
       split8t<1>(kf + 8 * st, kB);
       split8t<1>(vf + 8 * st, vB);
-      *reinterpret_cast<u32x4*>(kimg + (li * HD + (HD / 2) * hh + 8 * st) * 2) = kB[0];
-      *reinterpret_cast<u32x4*>(vimg + (li * HD + (HD / 2) * hh + 8 * st) * 2) = vB[0];
+      *reinterpret_cast<u32x4*>(kimg + gswz<HD * 2>(li, ((HD / 2) * hh + 8 * st) * 2)) = kB[0];
+      *reinterpret_cast<u32x4*>(vimg + gswz<HD * 2>(li, ((HD / 2) * hh + 8 * st) * 2)) = vB[0];
+      kF[st] = kB[0];
+      vF[st] = vB[0];
     }
   }
   f32x16 dk[NB(HD)], dv[NB(HD)];
@@ -1144,7 +1174,11 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kerne
   // cooperative Q / dO block loads: thread t takes float4 e = t + NT i of the [32][HD] block
   f32x4 pq[PT], po[PT];
   u32x2 pq16[PT];
+  // the block's lse (lanes 0-31) and delta (lanes 32-63), one float per lane, loaded with the Q / dO rows and
+  // parked in the wave's dS^T image until the softmax reads them (that image is rewritten only after it)
+  float plsd = 0.f;
   auto load_q = [&](int qb) {
+    plsd = lane < 32 ? lsep[32 * qb + lane] : dltp[32 * qb + lane - 32];
 #pragma unroll
     for (int i = 0; i < PT; ++i) {
       const int e = t + NT * i;
@@ -1159,13 +1193,15 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kerne
     }
   };
   auto store_q = [&]() {
+    reinterpret_cast<float*>(simg)[lane] = plsd;
 #pragma unroll
     for (int i = 0; i < PT; ++i) {
       const int e = t + NT * i;
       if (e < F4) {
-        if constexpr (QB) *reinterpret_cast<u32x2*>(qimg + e * 8) = pq16[i];
-        else *reinterpret_cast<u32x2*>(qimg + e * 8) = bf16_rne4(pq[i]);
-        *reinterpret_cast<u32x2*>(oimg + e * 8) = bf16_rne4(po[i]);
+        const int io = gswz<HD * 2>(e / (HD / 4), (e % (HD / 4)) * 8);
+        if constexpr (QB) *reinterpret_cast<u32x2*>(qimg + io) = pq16[i];
+        else *reinterpret_cast<u32x2*>(qimg + io) = bf16_rne4(pq[i]);
+        *reinterpret_cast<u32x2*>(oimg + io) = bf16_rne4(po[i]);
       }
     }
   };
@@ -1180,13 +1216,14 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kerne
 #pragma unroll
       for (int c = 0; c < NB(HD); ++c)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) dqbuf[((w * NB(HD) + c) * 16 + r) * 64 + lane] = 0.f;
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<f32x4*>(dqbuf + (((w * NB(HD) + c) * 4 + g) * 64 + lane) * 4) = f32x4{0.f, 0.f, 0.f, 0.f};
     } else {
     u32x4 qA[NS][3], oA[NS][3];
 #pragma unroll
     for (int st = 0; st < NS; ++st) {
-      qA[st][0] = *reinterpret_cast<const u32x4*>(qimg + (li * HD + (HD / 2) * hh + 8 * st) * 2);
-      oA[st][0] = *reinterpret_cast<const u32x4*>(oimg + (li * HD + (HD / 2) * hh + 8 * st) * 2);
+      qA[st][0] = *reinterpret_cast<const u32x4*>(qimg + gswz<HD * 2>(li, ((HD / 2) * hh + 8 * st) * 2));
+      oA[st][0] = *reinterpret_cast<const u32x4*>(oimg + gswz<HD * 2>(li, ((HD / 2) * hh + 8 * st) * 2));
     }
     f32x16 s, dp;
 #pragma unroll
@@ -1194,15 +1231,15 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kerne
 #pragma unroll
     for (int st = 0; st < NS; ++st) {
       u32x4 kB[3], vB[3];
-      kB[0] = *reinterpret_cast<const u32x4*>(kimg + (li * HD + (HD / 2) * hh + 8 * st) * 2);
-      vB[0] = *reinterpret_cast<const u32x4*>(vimg + (li * HD + (HD / 2) * hh + 8 * st) * 2);
+      kB[0] = kF[st];
+      vB[0] = vF[st];
       s = mfma_terms<1>(qA[st], kB, s);                // S: row = query, col = key
       dp = mfma_terms<1>(oA[st], vB, dp);              // dP
     }
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      const f32x4 l4 = *reinterpret_cast<const f32x4*>(lsep + q0 + 8 * g + 4 * hh);
-      const f32x4 d4 = *reinterpret_cast<const f32x4*>(dltp + q0 + 8 * g + 4 * hh);
+      const f32x4 l4 = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(simg) + 8 * g + 4 * hh);
+      const f32x4 d4 = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(simg) + 32 + 8 * g + 4 * hh);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int r = 4 * g + e, j = q0 + 8 * g + 4 * hh + e;
@@ -1223,7 +1260,7 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kerne
       for (int g = 0; g < 4; ++g) {
         const u32x4 wv = sB[g >> 1][0];
         const u32x2 two = (g & 1) ? u32x2{wv.z, wv.w} : u32x2{wv.x, wv.y};
-        *reinterpret_cast<u32x2*>(simg + (li * 32 + 8 * g + 4 * hh) * 2) = two;
+        *reinterpret_cast<u32x2*>(simg + gswz<64>(li, (8 * g + 4 * hh) * 2)) = two;
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -1232,8 +1269,8 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kerne
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
         u32x4 oT[3], qT[3];
-        oT[0] = tr16_frag(oimg, HD * 2, 16 * st + 4 * hh, 16 * st + 8 + 4 * hh, 32 * c, lane);
-        qT[0] = tr16_frag(qimg, HD * 2, 16 * st + 4 * hh, 16 * st + 8 + 4 * hh, 32 * c, lane);
+        oT[0] = tr16_frag_sw<HD * 2>(oimg, 16 * st + 4 * hh, 16 * st + 8 + 4 * hh, 32 * c, lane);
+        qT[0] = tr16_frag_sw<HD * 2>(qimg, 16 * st + 4 * hh, 16 * st + 8 + 4 * hh, 32 * c, lane);
         dv[c] = mfma_terms<1>(oT, pB[st], dv[c]);      // dV^T += dO^T P
         dk[c] = mfma_terms<1>(qT, sB[st], dk[c]);      // dK^T += Q^T dS
       }
@@ -1245,18 +1282,20 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kerne
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
       u32x4 sT[3];
-      sT[0] = tr16_frag(simg, 64, 16 * st + 8 * hh, 16 * st + 8 * hh + 4, 0, lane);
+      sT[0] = tr16_frag_sw<64>(simg, 16 * st + 8 * hh, 16 * st + 8 * hh + 4, 0, lane);
 #pragma unroll
       for (int c = 0; c < NB(HD); ++c) {
         u32x4 kT[3];
-        kT[0] = tr16_frag(kimg, HD * 2, 16 * st + 8 * hh, 16 * st + 8 * hh + 4, 32 * c, lane);
+        kT[0] = tr16_frag_sw<HD * 2>(kimg, 16 * st + 8 * hh, 16 * st + 8 * hh + 4, 32 * c, lane);
         dq[c] = mfma_terms<1>(kT, sT, dq[c]);           // dQ^T += K^T dS^T
       }
     }
 #pragma unroll
     for (int c = 0; c < NB(HD); ++c)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) dqbuf[((w * NB(HD) + c) * 16 + r) * 64 + lane] = dq[c][r];
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<f32x4*>(dqbuf + (((w * NB(HD) + c) * 4 + g) * 64 + lane) * 4) =
+            f32x4{dq[c][4 * g], dq[c][4 * g + 1], dq[c][4 * g + 2], dq[c][4 * g + 3]};
     }
     __syncthreads();                                   // every wave's dQ contribution is in LDS
     // fixed-order sum over the NW waves: float4 u = (lane, c, g) -> query q0 + (lane & 31), dims
@@ -1264,10 +1303,7 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kerne
     for (int u = t; u < NB(HD) * 4 * 64; u += NT) {
       const int ln = u & 63, cg = u >> 6, c = cg >> 2, g = cg & 3;
       f32x4 a = {0.f, 0.f, 0.f, 0.f};
-      for (int v = 0; v < NW; ++v) {
-        const float* bb = dqbuf + ((v * NB(HD) + c) * 16 + 4 * g) * 64 + ln;
-        a += f32x4{bb[0], bb[64], bb[128], bb[192]};
-      }
+      for (int v = 0; v < NW; ++v) a += *reinterpret_cast<const f32x4*>(dqbuf + (((v * NB(HD) + c) * 4 + g) * 64 + ln) * 4);
       const int jq = q0 + (ln & 31);
       const int dd = 32 * c + 8 * g + 4 * (ln >> 5);
       if (jq < K && dd < HD) {

@@ -51,14 +51,14 @@ __device__ __forceinline__ void split8(const float* v, u32x4 (&pl)[3]) {
   pl[2] = u32x4{a2.x, a2.y, b2.x, b2.y};
 }
 // f32x4 -> 4 bf16 rounded to nearest even (OT_MATMUL_BF16: the one-plane form), packed like split3
+// (v_cvt_pk_bf16_f32: one instruction per pair, round to nearest even — the integer form u + 0x7fff + lsb took
+// about four per element and is the same for every finite value)
+typedef __bf16 bf16x2_cvt_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_cvt_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ u32x2 bf16_rne4(f32x4 v) {
-  uint32_t r[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint32_t u = __float_as_uint(v[j]);
-    r[j] = u + 0x7fffu + ((u >> 16) & 1u);               // finite inputs (activations / weights)
-  }
-  return u32x2{__builtin_amdgcn_perm(r[1], r[0], 0x07060302u), __builtin_amdgcn_perm(r[3], r[2], 0x07060302u)};
+  const bf16x2_cvt_t a = __builtin_convertvector(f32x2_cvt_t{v[0], v[1]}, bf16x2_cvt_t);
+  const bf16x2_cvt_t b = __builtin_convertvector(f32x2_cvt_t{v[2], v[3]}, bf16x2_cvt_t);
+  return u32x2{__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b)};
 }
 // TERMS = 6: split8; TERMS = 1: plane 0 = the rounded bf16 (planes 1, 2 unused)
 template <int TERMS>

@@ -1853,7 +1853,10 @@ extern "C" size_t ot_attn_bwd_workspace_size(int B, int H, int K) {
 // key-grouped bf16 backward (attn_bwd_group_kernel): long tails only — at C2-like lengths (<= 8 key
 // blocks) the per-pair kernel re-reads little and has more parallelism
 // (4 waves per workgroup measured faster than 8 at C5: 7.19 vs 8.66 ms per layer, 18.36 per pair)
-constexpr int ATTN_BWD_GROUP = 4, ATTN_BWD_GROUP_MIN_KB = 9;   // waves (key blocks) per group; from 9 key blocks
+#ifndef OT_BWDG_NW
+#define OT_BWDG_NW 4
+#endif
+constexpr int ATTN_BWD_GROUP = OT_BWDG_NW, ATTN_BWD_GROUP_MIN_KB = 9;   // waves (key blocks) per group; from 9 key blocks
 static int attn_bwd_kgroup(int I, int K, int head_dim, bool sel, int prec) {
   if (sel || K <= SMALL_K || prec != OT_MATMUL_BF16 || (head_dim != 32 && head_dim != 64)) return 0;
   if ((I + 31) / 32 < ATTN_BWD_GROUP_MIN_KB) return 0;

@@ -114,6 +114,17 @@ struct GemmArgs {
 
 // sum over the 32 lanes that hold one output row in the vector epilogue (same order as the
 // row-wise kernels' group_sum with 32 threads per row)
+// max over the 32 lanes that hold one output row (the vector epilogue's row maxima): within each 16-lane row by
+// DPP (quad swaps, half-row and row mirrors), then across the two rows by v_permlane16_swap — VALU only, where
+// five __shfl_xor steps were five ds_bpermute LDS round trips per row (max is order-free: the same result)
+__device__ __forceinline__ float row32_max(float v) {
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false)));   // quad [1,0,3,2]
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false)));   // quad [2,3,0,1]
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false)));  // row_half_mirror
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false)));  // row_mirror
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+}
 __device__ __forceinline__ float row32_sum(float v) {
 #pragma unroll
   for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -324,8 +335,7 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
           if (epi & OT_EPI_BIAS) v += bias4;
           if (p.rowmax_out) {                                  // this tile's largest C of the row (signed)
             float mx = fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w));
-#pragma unroll
-            for (int o = 16; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+            mx = row32_max(mx);
             if (orr >= 0 && c4 == 0) p.rowmax_out[(int64_t)orr * p.rowmax_n + n0 / GT] = mx;
           }
           if (epi & OT_EPI_GELU_BWD) {
@@ -378,8 +388,7 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
             }
             if (p.rowabs_out) {                                // the consumer's row bound (dx_masked, else dx)
               float mx = amax4(0.f, cv);
-#pragma unroll
-              for (int o = 16; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+              mx = row32_max(mx);
               if (orr >= 0 && c4 == 0) p.rowabs_out[(int64_t)orr * p.rowabs_n + n0 / GT] = mx;
             }
             continue;
@@ -419,8 +428,7 @@ __device__ __forceinline__ void gemm_vec_epilogue(const GemmArgs& p, const f32x1
           if (orr >= 0) am = amax4(am, v);
           if (p.rowabs_out) {                                  // this tile's max |C| of the row (fp16-pair consumer)
             float mx = amax4(0.f, v);
-#pragma unroll
-            for (int o = 16; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+            mx = row32_max(mx);
             if (orr >= 0 && c4 == 0) p.rowabs_out[(int64_t)orr * p.rowabs_n + n0 / GT] = mx;
           }
         }

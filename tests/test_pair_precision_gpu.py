@@ -213,6 +213,35 @@ def test_rowmax_out_refused_off_the_plane_gemm(dev):
                    bias_gstride=N, rowmax_out=rmax, rowmax_n=N // 128)
 
 
+@pytest.mark.parametrize('N', [128, 512])
+def test_row_maxima_outputs_exact(dev, N):
+    """The vector epilogue's per-tile row maxima (rowmax_out: signed max of C; rowabs_out: max |C|; the FFN2 pair's
+    row bound and the dgrads') equal the max over each 128-column tile of the C the same launch stored — exactly
+    (their 32-lane reduction is order-free).  FFN1 forward form: RMSNorm prologue, bias epilogue, a weight group per
+    row residue, rows with signs mixed so signed and absolute maxima differ."""
+    gen = torch.Generator().manual_seed(11)
+    M, K_, G = 600, 128, 3
+    rm, d = group_map(M, G, dev)
+    A = torch.randn(M, K_, generator=gen).to(dev)
+    W = torch.randn(G, N, K_, generator=gen) * 0.1
+    gamma = torch.rand(K_, generator=gen) + 0.5
+    img, ntn = pair_image(W, dev, gamma)
+    rstd = (torch.rand(M, generator=gen) + 0.5).to(dev)
+    bias = (torch.randn(G, N, generator=gen) - 1.0).to(dev)
+    C = torch.empty(M, N, device=dev)
+    rmax = torch.full((M, N // 128), float('nan'), device=dev)
+    rabs = torch.full((M, N // 128), float('nan'), device=dev)
+    K.gemm_rms(OT_GEMM_NT, A, K_, K_, d['rows'][0], W.to(dev), N * K_, K_, N, d['tile_group'], rm.ntiles, C, N,
+               d['rows'][1], a_xform=OT_AX_RMSNORM, rstd=rstd, gamma=gamma.to(dev), epi=OT_EPI_BIAS, bias=bias,
+               bias_gstride=N, rowmax_out=rmax, rowmax_n=N // 128, rowabs_out=rabs, rowabs_n=N // 128,
+               bimg=(img, ntn, 0), device=dev)
+    torch.cuda.synchronize()
+    t = C.reshape(M, N // 128, 128)
+    assert torch.equal(rmax, t.max(-1).values)
+    assert torch.equal(rabs, t.abs().max(-1).values)
+    assert (rmax < rabs).any()                          # the signed and the absolute maxima differ somewhere
+
+
 def attn_ref(qkv, B, H, I, Kq, hd):
     d = H * hd
     qpos = torch.arange(I - Kq, I)

@@ -360,6 +360,30 @@ __global__ __launch_bounds__(256) void attn_fwd_kv_kernel(AttnArgs p) {
 }
 
 // ------------------------------------------------------------------------------------------
+// XOR-swizzled byte offset in a bf16 image of RB-byte rows (the split forward's V planes, the key-grouped
+// backward's [32][HD] and [32][32] images): row r's 16-B chunk index is XORed with (r / (256 / RB)) mod (RB / 16), so the rows that share LDS banks
+// (256 B apart) spread over the chunks — the row-major fragment reads (one row per lane) and the transposed reads
+// were 2- to 8-way bank-conflicted on the plain layout (C5: conflict cycles 68% of the LDS-active cycles).
+#ifndef OT_BWDG_SWIZZLE
+#define OT_BWDG_SWIZZLE 1
+#endif
+template <int RB>
+__device__ __forceinline__ int gswz(int r, int b) {
+  constexpr int P = 256 / RB, C = RB / 16;
+  return OT_BWDG_SWIZZLE ? r * RB + (b ^ (((r / P) & (C - 1)) << 4)) : r * RB + b;
+}
+template <int RB>
+__device__ __forceinline__ u32x4 tr16_frag_sw(const char* img, int ra, int rb, int colbase, int lane) {
+  typedef short v4i16 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+  const int gi = lane & 15, q = gi >> 2, pp = gi & 3;
+  const int c = colbase + 16 * ((lane >> 4) & 1) + 4 * pp;
+  const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(img + gswz<RB>(ra + q, c * 2)));
+  const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(img + gswz<RB>(rb + q, c * 2)));
+  const u32x2 a = __builtin_bit_cast(u32x2, lo), b = __builtin_bit_cast(u32x2, hi);
+  return u32x4{a.x, a.y, b.x, b.y};
+}
+
 // Split-bf16 forward (OT_MATMUL_SPLIT_BF16; HD >= 32): the same online softmax as attn_fwd_kernel,
 // the two products on v_mfma_f32_32x32x16_bf16 with every f32 operand split exactly into three bf16
 // planes and the six largest plane products summed (mfma_split6: f32-accurate, 2.7x fewer MFMA
@@ -377,8 +401,8 @@ __device__ __forceinline__ u32x4 vt_frag(const char* plane, int s, int c, int la
   const int hh = lane >> 5, gi = lane & 15, q = gi >> 2, pp = gi & 3;
   const int c0 = 32 * c + 16 * ((lane >> 4) & 1) + 4 * pp;
   const int r0 = 16 * s + 4 * hh + q;
-  const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(plane + (r0 * HD + c0) * 2));
-  const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(plane + ((r0 + 8) * HD + c0) * 2));
+  const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(plane + gswz<HD * 2>(r0, c0 * 2)));
+  const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(plane + gswz<HD * 2>(r0 + 8, c0 * 2)));
   const u32x2 a = __builtin_bit_cast(u32x2, lo), b = __builtin_bit_cast(u32x2, hi);
   return u32x4{a.x, a.y, b.x, b.y};
 }
@@ -443,7 +467,7 @@ __global__ __launch_bounds__(256) void attn_fwd_split_kernel(AttnArgs p) {
           split8t<TERMS>(vf + 8 * t, vp);
 #pragma unroll
           for (int pl = 0; pl < (TERMS == 1 ? 1 : 3); ++pl)
-            *reinterpret_cast<u32x4*>(vimg + pl * PLANE + (li * HD + (HD / 2) * hh + 8 * t) * 2) = vp[pl];
+            *reinterpret_cast<u32x4*>(vimg + pl * PLANE + gswz<HD * 2>(li, ((HD / 2) * hh + 8 * t) * 2)) = vp[pl];
         }
 #pragma unroll
         for (int t = 0; t < NS; ++t) {
@@ -1075,30 +1099,6 @@ __global__ __launch_bounds__(64 * WAVES, TERMS == 1 ? 2 : 1) void attn_bwd_split
 // Tail queries only (no selection map), TERMS = 1 (OT_MATMUL_BF16).
 template <int HD, int NW>
 constexpr int BWDG_LDS() { return 2 * 32 * HD * 2 + NW * (2 * 32 * HD * 2 + 32 * 32 * 2) + NW * 32 * HD * 4; }
-
-// XOR-swizzled byte offset in a bf16 image of RB-byte rows (the key-grouped backward's [32][HD] and [32][32]
-// images): row r's 16-B chunk index is XORed with (r / (256 / RB)) mod (RB / 16), so the rows that share LDS banks
-// (256 B apart) spread over the chunks — the row-major fragment reads (one row per lane) and the transposed reads
-// were 2- to 8-way bank-conflicted on the plain layout (C5: conflict cycles 68% of the LDS-active cycles).
-#ifndef OT_BWDG_SWIZZLE
-#define OT_BWDG_SWIZZLE 1
-#endif
-template <int RB>
-__device__ __forceinline__ int gswz(int r, int b) {
-  constexpr int P = 256 / RB, C = RB / 16;
-  return OT_BWDG_SWIZZLE ? r * RB + (b ^ (((r / P) & (C - 1)) << 4)) : r * RB + b;
-}
-template <int RB>
-__device__ __forceinline__ u32x4 tr16_frag_sw(const char* img, int ra, int rb, int colbase, int lane) {
-  typedef short v4i16 __attribute__((ext_vector_type(4)));
-  typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
-  const int gi = lane & 15, q = gi >> 2, pp = gi & 3;
-  const int c = colbase + 16 * ((lane >> 4) & 1) + 4 * pp;
-  const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(img + gswz<RB>(ra + q, c * 2)));
-  const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(img + gswz<RB>(rb + q, c * 2)));
-  const u32x2 a = __builtin_bit_cast(u32x2, lo), b = __builtin_bit_cast(u32x2, hi);
-  return u32x4{a.x, a.y, b.x, b.y};
-}
 
 template <int HD, int NW, bool QB = false>
 __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kernel(AttnArgs p) {

@@ -1097,8 +1097,20 @@ __global__ __launch_bounds__(64 * WAVES, TERMS == 1 ? 2 : 1) void attn_bwd_split
 // the NW dQ contributions are summed through LDS in a fixed order and stored once per (slice, query
 // block) — slice 0 into dqkv, slice s > 0 into dqpart[s - 1] (attn_dq_reduce_kernel adds them).
 // Tail queries only (no selection map), TERMS = 1 (OT_MATMUL_BF16).
+// XCD-aware slice placement: measured 4,523 us per C5 layer against 4,489 us without (within noise; the
+// slices' Q / dO re-reads are not the bound) — kept as an option, off
+#ifndef OT_BWDG_XCD
+#define OT_BWDG_XCD 0
+#endif
+// Descending query blocks: every slice of a (sample, head) then streams the same query block at once (with
+// OT_BWDG_XCD the slices share one L2; the kernel re-reads Q / dO once per slice, ~12 GB per C5 layer): 4,330 us
+// against 4,387-4,489 us ascending (runs/r6ab.sh) — not kept: dK / dV would no longer sum the query blocks in the
+// one-wave-per-pair backward's order (bit-identity, test_attn_bwd_key_slices) for ~0.3% of a C5 step
+#ifndef OT_BWDG_DESC
+#define OT_BWDG_DESC 0
+#endif
 template <int HD, int NW>
-constexpr int BWDG_LDS() { return 2 * 32 * HD * 2 + NW * (2 * 32 * HD * 2 + 32 * 32 * 2) + NW * 32 * HD * 4; }
+constexpr int BWDG_LDS() { return 2 * 32 * HD * 2 + NW * (32 * HD * 2 + 32 * 32 * 2) + NW * 32 * HD * 4; }
 
 template <int HD, int NW, bool QB = false>
 __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kernel(AttnArgs p) {
@@ -1110,15 +1122,17 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kerne
   constexpr int F4 = 32 * HD / 4;                      // float4 per [32][HD] block
   constexpr int PT = (F4 + NT - 1) / NT;               // float4 per thread per operand
   extern __shared__ __attribute__((aligned(16))) char lds_g[];
-  const int t = threadIdx.x, lane = t & 63, li = lane & 31, hh = lane >> 5, w = t >> 6;
+  // the wave index in a scalar register: the key-block conditions below are wave-uniform branches
+  const int t = threadIdx.x, lane = t & 63, li = lane & 31, hh = lane >> 5, w = __builtin_amdgcn_readfirstlane(t >> 6);
   char* qimg = lds_g;                                  // shared [query][dim] images of the query block
   char* oimg = qimg + IMG;
-  char* kimg = oimg + IMG + w * (2 * IMG + SIMG);      // this wave's key block
-  char* vimg = kimg + IMG;
-  char* simg = vimg + IMG;                             // this wave's dS^T [key][query]
-  float* dqbuf = reinterpret_cast<float*>(lds_g + 2 * IMG + NW * (2 * IMG + SIMG));   // [NW][NB][4][64 lanes][4]
+  char* kimg = oimg + IMG + w * (IMG + SIMG);          // this wave's key block (its V fragments stay in registers)
+  char* simg = kimg + IMG;                             // this wave's dS^T [key][query]
+  float* dqbuf = reinterpret_cast<float*>(lds_g + 2 * IMG + NW * (IMG + SIMG));   // [NW][NB][4][64 lanes][4]
   const int S = p.kslices;
-  const int pair = blockIdx.x / S, slice = blockIdx.x - pair * S;
+  // the S slices of one (sample, head) read the same query / dO blocks: consecutive logical ids on one XCD
+  const int wg = OT_BWDG_XCD ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int pair = wg / S, slice = wg - pair * S;
   const int b = pair / p.H, h = pair % p.H;
   const int I = p.I, K = p.K, q_off = I - K, KP = attn_kpad(K);
   const int64_t tok0 = (int64_t)b * I;
@@ -1145,7 +1159,6 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kerne
       const u32x4 kB = kpos < I ? *reinterpret_cast<const u32x4*>(Q16 + p.d + o) : z;
       const u32x4 vB = kpos < I ? *reinterpret_cast<const u32x4*>(Q16 + 2 * p.d + o) : z;
       *reinterpret_cast<u32x4*>(kimg + gswz<HD * 2>(li, ((HD / 2) * hh + 8 * st) * 2)) = kB;
-      *reinterpret_cast<u32x4*>(vimg + gswz<HD * 2>(li, ((HD / 2) * hh + 8 * st) * 2)) = vB;
       kF[st] = kB;
       vF[st] = vB;
     }
@@ -1159,7 +1172,6 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kerne
       split8t<1>(kf + 8 * st, kB);
       split8t<1>(vf + 8 * st, vB);
       *reinterpret_cast<u32x4*>(kimg + gswz<HD * 2>(li, ((HD / 2) * hh + 8 * st) * 2)) = kB[0];
-      *reinterpret_cast<u32x4*>(vimg + gswz<HD * 2>(li, ((HD / 2) * hh + 8 * st) * 2)) = vB[0];
       kF[st] = kB[0];
       vF[st] = vB[0];
     }
@@ -1205,12 +1217,14 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kerne
       }
     }
   };
-  load_q(qbs);
-  for (int qb = qbs; qb < nqb; ++qb) {
+  const int nit = nqb - qbs;
+  load_q(OT_BWDG_DESC ? nqb - 1 : qbs);
+  for (int it = 0; it < nit; ++it) {
+    const int qb = OT_BWDG_DESC ? nqb - 1 - it : qbs + it;
     const int q0 = 32 * qb;
     store_q();
     __syncthreads();                                   // images of block qb (and the previous reduce done)
-    if (qb + 1 < nqb) load_q(qb + 1);                  // in flight during this block's MFMAs
+    if (it + 1 < nit) load_q(OT_BWDG_DESC ? qb - 1 : qb + 1);   // in flight during this block's MFMAs
     // a wave whose key block lies wholly after this query block (or past the end) contributes zeros
     if (key0 > q_off + q0 + 31 || key0 >= I) {
 #pragma unroll
@@ -1236,17 +1250,34 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kerne
       s = mfma_terms<1>(qA[st], kB, s);                // S: row = query, col = key
       dp = mfma_terms<1>(oA[st], vB, dp);              // dP
     }
+    // the causal mask only where the block pair straddles the diagonal (or holds keys past I): a wholly visible
+    // pair skips the per-element compare / select (padded queries have lse = +inf: P = 0 either way)
+    if (key0 + 31 <= q_off + q0) {
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const f32x4 l4 = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(simg) + 8 * g + 4 * hh);
-      const f32x4 d4 = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(simg) + 32 + 8 * g + 4 * hh);
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 l4 = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(simg) + 8 * g + 4 * hh);
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(simg) + 32 + 8 * g + 4 * hh);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int r = 4 * g + e, j = q0 + 8 * g + 4 * hh + e;
-        const float ex = __expf(s[r] * p.scale - l4[e]);
-        const float P = kpos <= q_off + j ? ex : 0.f;
-        s[r] = P;
-        dp[r] = P * (dp[r] - d4[e]) * p.scale;          // dS, pre-scaled by 1/sqrt(hd)
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * g + e;
+          const float P = __expf(s[r] * p.scale - l4[e]);
+          s[r] = P;
+          dp[r] = P * (dp[r] - d4[e]) * p.scale;        // dS, pre-scaled by 1/sqrt(hd)
+        }
+      }
+    } else {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 l4 = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(simg) + 8 * g + 4 * hh);
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(simg) + 32 + 8 * g + 4 * hh);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * g + e, j = q0 + 8 * g + 4 * hh + e;
+          const float ex = __expf(s[r] * p.scale - l4[e]);
+          const float P = kpos <= q_off + j ? ex : 0.f;
+          s[r] = P;
+          dp[r] = P * (dp[r] - d4[e]) * p.scale;        // dS, pre-scaled by 1/sqrt(hd)
+        }
       }
     }
     u32x4 pB[2][3], sB[2][3];

@@ -70,6 +70,14 @@ __device__ __forceinline__ void split8t(const float* v, u32x4 (&pl)[3]) {
     split8(v, pl);
   }
 }
+// XCD-aware bijective remap (cdna_hip_programming.md T1): blocks b and b+8 share an XCD, so give
+// each XCD a contiguous range of logical ids (tiles / slices that share operands then share that XCD's L2).
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+  int xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+  int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (b >> 3);
+}
+
 __device__ __forceinline__ f32x16 mfma_bf16(u32x4 a, u32x4 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0,
                                                   0);

@@ -140,13 +140,6 @@ __device__ __forceinline__ f32x4 apply_pro(f32x4 v, int xf, float rs, const floa
   return v;
 }
 
-// XCD-aware bijective remap (cdna_hip_programming.md T1): blocks b and b+8 share an XCD, so give
-// each XCD a contiguous range of tiles (the N tiles of one M tile then share that XCD's L2).
-__device__ __forceinline__ int xcd_remap(int b, int nwg) {
-  int xcd = b & 7, q = nwg >> 3, r = nwg & 7;
-  int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-  return base + (b >> 3);
-}
 
 // Weight-gradient tiles: whole row chunks per XCD.  Block b runs on XCD b % 8 (round-robin dispatch), so XCD x
 // takes chunks x, x + 8, x + 16, ... and each chunk's (k, n) tiles occupy consecutive dispatch slots of that XCD:

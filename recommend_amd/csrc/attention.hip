@@ -1109,11 +1109,28 @@ __global__ __launch_bounds__(64 * WAVES, TERMS == 1 ? 2 : 1) void attn_bwd_split
 #ifndef OT_BWDG_DESC
 #define OT_BWDG_DESC 0
 #endif
+// Cross-wave dQ (head_dim 64, 4 waves): after a barrier that publishes every wave's dS^T image, wave w forms dQ^T
+// tile w & 1 over key blocks 2 (w >> 1) and 2 (w >> 1) + 1 of the group, and waves 2 / 3 hand theirs to waves 0 / 1
+// through an 8 KiB buffer (a third barrier) — the [NW][2][4][64][4] f32 buffer (32 KiB) and its reduce pass go, LDS
+// 64 -> 40 KiB per workgroup.  C5 layer (tools/attn_c5_bench.py, runs/r6ad.sh): 4,228-4,240 us against 4,405-4,435;
+// dQ sums its four key blocks as (kb0 + kb1) + (kb2 + kb3) instead of one fixed-order pass (dK / dV unchanged, bit for
+// bit).  Three workgroups per CU (OT_BWDG_MINWG 3, 168 VGPRs) spill 344 B per lane: 13.5 ms — two kept.
+#ifndef OT_BWDG_DQX
+#define OT_BWDG_DQX 1
+#endif
+#ifndef OT_BWDG_MINWG
+#define OT_BWDG_MINWG 2
+#endif
 template <int HD, int NW>
-constexpr int BWDG_LDS() { return 2 * 32 * HD * 2 + NW * (32 * HD * 2 + 32 * 32 * 2) + NW * 32 * HD * 4; }
+constexpr bool bwdg_dqx() { return OT_BWDG_DQX && HD == 64 && NW == 4; }
+template <int HD, int NW>
+constexpr int BWDG_LDS() {
+  return 2 * 32 * HD * 2 + NW * (32 * HD * 2 + 32 * 32 * 2) + (bwdg_dqx<HD, NW>() ? 2 * 64 * 16 * 4 : NW * 32 * HD * 4);
+}
 
 template <int HD, int NW, bool QB = false>
-__global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kernel(AttnArgs p) {
+__global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : (bwdg_dqx<HD, NW>() ? OT_BWDG_MINWG : 2)) void attn_bwd_group_kernel(AttnArgs p) {
+  constexpr bool DQX = bwdg_dqx<HD, NW>();
   static_assert(HD == 64 || HD == 32, "grouped backward: HD 32 or 64");
   constexpr int NS = HD / 16;                          // k-steps over the head dim
   constexpr int IMG = 32 * HD * 2;                     // one [32][HD] bf16 image
@@ -1227,11 +1244,13 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kerne
     if (it + 1 < nit) load_q(OT_BWDG_DESC ? qb - 1 : qb + 1);   // in flight during this block's MFMAs
     // a wave whose key block lies wholly after this query block (or past the end) contributes zeros
     if (key0 > q_off + q0 + 31 || key0 >= I) {
+      if constexpr (!DQX) {
 #pragma unroll
-      for (int c = 0; c < NB(HD); ++c)
+        for (int c = 0; c < NB(HD); ++c)
 #pragma unroll
-        for (int g = 0; g < 4; ++g)
-          *reinterpret_cast<f32x4*>(dqbuf + (((w * NB(HD) + c) * 4 + g) * 64 + lane) * 4) = f32x4{0.f, 0.f, 0.f, 0.f};
+          for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<f32x4*>(dqbuf + (((w * NB(HD) + c) * 4 + g) * 64 + lane) * 4) = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
     } else {
     u32x4 qA[NS][3], oA[NS][3];
 #pragma unroll
@@ -1305,6 +1324,7 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kerne
         dv[c] = mfma_terms<1>(oT, pB[st], dv[c]);      // dV^T += dO^T P
         dk[c] = mfma_terms<1>(qT, sB[st], dk[c]);      // dK^T += Q^T dS
       }
+    if constexpr (!DQX) {
     f32x16 dq[NB(HD)];
 #pragma unroll
     for (int c = 0; c < NB(HD); ++c)
@@ -1328,15 +1348,9 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kerne
         *reinterpret_cast<f32x4*>(dqbuf + (((w * NB(HD) + c) * 4 + g) * 64 + lane) * 4) =
             f32x4{dq[c][4 * g], dq[c][4 * g + 1], dq[c][4 * g + 2], dq[c][4 * g + 3]};
     }
-    __syncthreads();                                   // every wave's dQ contribution is in LDS
-    // fixed-order sum over the NW waves: float4 u = (lane, c, g) -> query q0 + (lane & 31), dims
-    // 32c + 8g + 4 (lane >> 5) + 0..3; stored once per (slice, query block)
-    for (int u = t; u < NB(HD) * 4 * 64; u += NT) {
-      const int ln = u & 63, cg = u >> 6, c = cg >> 2, g = cg & 3;
-      f32x4 a = {0.f, 0.f, 0.f, 0.f};
-      for (int v = 0; v < NW; ++v) a += *reinterpret_cast<const f32x4*>(dqbuf + (((v * NB(HD) + c) * 4 + g) * 64 + ln) * 4);
-      const int jq = q0 + (ln & 31);
-      const int dd = 32 * c + 8 * g + 4 * (ln >> 5);
+    }
+    // the dQ store of (slice, query block): float4 a = query jq, dims dd .. dd + 3
+    auto store_dq = [&](const f32x4& a, int jq, int dd) {
       if (jq < K && dd < HD) {
         const int ps = p.dq_bf16 ? slice : slice - 1;  // dqpart slot (bf16 output: slice 0 too)
         const int64_t pe = ((int64_t)ps * p.B * K + (int64_t)b * K + jq) * p.d + h * HD + dd;
@@ -1346,6 +1360,54 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_bwd_group_kerne
           float* dst = ps < 0 ? p.dqkv + (tok0 + q_off + jq) * p.ld + h * HD + dd : p.dqpart + pe;
           *reinterpret_cast<f32x4*>(dst) = a;
         }
+      }
+    };
+    if constexpr (DQX) {
+      __syncthreads();                                 // every wave's dS^T image is in LDS
+      const int c = w & 1;
+      f32x16 dq;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dq[r] = 0.f;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int v = 2 * (w >> 1) + j;                // key block v of the group (uniform)
+        const int kv0 = 32 * (slice * NW + v);
+        if (kv0 > q_off + q0 + 31 || kv0 >= I) continue;   // its dS is zero (no image written)
+        const char* kimg_v = lds_g + 2 * IMG + v * (IMG + SIMG);
+        const char* simg_v = kimg_v + IMG;
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          u32x4 sT[3], kT[3];
+          sT[0] = tr16_frag_sw<64>(simg_v, 16 * st + 8 * hh, 16 * st + 8 * hh + 4, 0, lane);
+          kT[0] = tr16_frag_sw<HD * 2>(kimg_v, 16 * st + 8 * hh, 16 * st + 8 * hh + 4, 32 * c, lane);
+          dq = mfma_terms<1>(kT, sT, dq);              // dQ^T (dims 32c ..) += K_v^T dS_v^T
+        }
+      }
+      float* xb = dqbuf;                               // [2][4][64 lanes][4]: waves 2 / 3 -> waves 0 / 1
+      if (w >= 2) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<f32x4*>(xb + (((w - 2) * 4 + g) * 64 + lane) * 4) =
+              f32x4{dq[4 * g], dq[4 * g + 1], dq[4 * g + 2], dq[4 * g + 3]};
+      }
+      __syncthreads();
+      if (w < 2) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 a = f32x4{dq[4 * g], dq[4 * g + 1], dq[4 * g + 2], dq[4 * g + 3]} +
+                          *reinterpret_cast<const f32x4*>(xb + ((w * 4 + g) * 64 + lane) * 4);
+          store_dq(a, q0 + li, 32 * c + 8 * g + 4 * hh);
+        }
+      }
+    } else {
+      __syncthreads();                                 // every wave's dQ contribution is in LDS
+      // fixed-order sum over the NW waves: float4 u = (lane, c, g) -> query q0 + (lane & 31), dims
+      // 32c + 8g + 4 (lane >> 5) + 0..3; stored once per (slice, query block)
+      for (int u = t; u < NB(HD) * 4 * 64; u += NT) {
+        const int ln = u & 63, cg = u >> 6, c = cg >> 2, g = cg & 3;
+        f32x4 a = {0.f, 0.f, 0.f, 0.f};
+        for (int v = 0; v < NW; ++v) a += *reinterpret_cast<const f32x4*>(dqbuf + (((v * NB(HD) + c) * 4 + g) * 64 + ln) * 4);
+        store_dq(a, q0 + (ln & 31), 32 * c + 8 * g + 4 * (ln >> 5));
       }
     }
   }

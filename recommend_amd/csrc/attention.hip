@@ -1122,10 +1122,10 @@ __global__ __launch_bounds__(64 * WAVES, TERMS == 1 ? 2 : 1) void attn_bwd_split
 #define OT_BWDG_MINWG 2
 #endif
 template <int HD, int NW>
-constexpr bool bwdg_dqx() { return OT_BWDG_DQX && HD == 64 && NW == 4; }
+constexpr bool bwdg_dqx() { return OT_BWDG_DQX && HD == 64 && (NW == 4 || NW == 8); }
 template <int HD, int NW>
 constexpr int BWDG_LDS() {
-  return 2 * 32 * HD * 2 + NW * (32 * HD * 2 + 32 * 32 * 2) + (bwdg_dqx<HD, NW>() ? 2 * 64 * 16 * 4 : NW * 32 * HD * 4);
+  return 2 * 32 * HD * 2 + NW * (32 * HD * 2 + 32 * 32 * 2) + (bwdg_dqx<HD, NW>() ? (NW - 2) * 64 * 16 * 4 : NW * 32 * HD * 4);
 }
 
 template <int HD, int NW, bool QB = false>
@@ -1383,7 +1383,7 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : (bwdg_dqx<HD, NW>() ? OT_BWD
           dq = mfma_terms<1>(kT, sT, dq);              // dQ^T (dims 32c ..) += K_v^T dS_v^T
         }
       }
-      float* xb = dqbuf;                               // [2][4][64 lanes][4]: waves 2 / 3 -> waves 0 / 1
+      float* xb = dqbuf;                               // [NW - 2][4][64 lanes][4]: waves w >= 2 -> wave w & 1
       if (w >= 2) {
 #pragma unroll
         for (int g = 0; g < 4; ++g)
@@ -1394,8 +1394,10 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : (bwdg_dqx<HD, NW>() ? OT_BWD
       if (w < 2) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const f32x4 a = f32x4{dq[4 * g], dq[4 * g + 1], dq[4 * g + 2], dq[4 * g + 3]} +
-                          *reinterpret_cast<const f32x4*>(xb + ((w * 4 + g) * 64 + lane) * 4);
+          f32x4 a = f32x4{dq[4 * g], dq[4 * g + 1], dq[4 * g + 2], dq[4 * g + 3]};
+#pragma unroll
+          for (int k = 0; k < NW / 2 - 1; ++k)         // fixed order: key-block pairs 1, 2, ...
+            a += *reinterpret_cast<const f32x4*>(xb + (((w + 2 * k) * 4 + g) * 64 + lane) * 4);
           store_dq(a, q0 + li, 32 * c + 8 * g + 4 * hh);
         }
       }
